@@ -1,0 +1,208 @@
+#!/usr/bin/env python3
+"""Headline benchmark: Mray/s (primary+shadow) and ms/frame, horse_and_mug
+1920x1080, MaxRecursionDepth 6 (BASELINE.json configs[2] = SURVEY.md §8d C3),
+on N GPUs of one node.
+
+One "step" = one frame: every rank renders its round-robin row stripes of the
+frame into an HBM slab (one HIP megakernel launch), then for N>1 the slabs are
+gathered to rank 0 with one RCCL collective over xGMI and un-interleaved by a
+rank-0 kernel.  Inputs (scene + BVH) are resident in HBM before
+timing; the frame stays in HBM (no D2H, no write_ppm) — see DESIGN.md for the
+PCIe-inclusive figure.  Scaling is strong (the frame is fixed, split over N).
+
+  python bench.py [--gpus N] [--steps K] [--warmup W] [--aa F] [--config C3]
+  torchrun --nproc-per-node N bench.py --gpus N ...
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import subprocess
+import sys
+import tempfile
+import time
+from pathlib import Path
+
+ROOT = Path(__file__).resolve().parent
+sys.path.insert(0, str(ROOT))
+
+import __graft_entry__ as graft  # noqa: E402
+
+HBM_PEAK_GBPS = 8000.0     # MI355X spec (MI355X_MICROARCH.md; 6.29 TB/s measured float4 copy)
+# Algorithmic bytes per unit of work
+B_NODE, B_TRI, B_SPH, B_PIX = 32, 36, 16, 3
+
+CONFIGS = {
+    "C3": ("C3_hm_1080p_d6", "horse_and_mug.xml 1920x1080, MaxRecursionDepth 6, full BVH + mirror recursion"),
+    "C2": ("C2_cornellbox_800_d0", "cornellbox.xml camera 2 800x800, primary+shadow only (depth 0)"),
+    "C5": ("C5_hm_8k_d6", "horse_and_mug.xml 7680x4320, depth 6, 16x SSAA (factor 4)"),
+}
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=50)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--config", default="C3", choices=sorted(CONFIGS))
+    ap.add_argument("--aa", type=int, default=None, help="SSAA factor (default 1; C5: 4)")
+    ap.add_argument("--stripe-rows", type=int, default=8)
+    ap.add_argument("--cpu-seconds", type=float, default=10.0, help="CPU baseline budget (rank 0, N=1)")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    return ap.parse_args()
+
+
+def cpu_baseline(xml: str, aa: int, rays_ps_per_frame: int, budget_s: float) -> dict:
+    """Reference CPU renderer timed on this host (rank 0 only).  Prefers the
+    unmodified reference compiled from its sources (oracle/_ref/ref_harness,
+    kind "reference"); falls back to the C restatement (kind "port")."""
+    try:
+        cores = len(os.sched_getaffinity(0))
+    except AttributeError:
+        cores = os.cpu_count() or 1
+    threads = max(1, min(16, cores))
+    harness = ROOT / "oracle" / "_ref" / "ref_harness"
+    if harness.exists():
+        def run(reps):
+            out = subprocess.run([str(harness), xml, "--aa", str(aa), "--threads", str(threads), "--reps", str(reps)],
+                                 check=True, capture_output=True, text=True, cwd=tempfile.gettempdir()).stdout
+            ev = [json.loads(l) for l in out.splitlines() if '"render"' in l][0]
+            return ev["median_s"]
+        first = run(1)
+        reps = int(max(1, min(50, budget_s / max(first, 1e-3))))
+        med = run(reps) if reps > 1 else first
+        kind = "reference"
+    else:
+        orc = graft.import_oracle()
+        sc = orc.OracleScene(xml)
+        t0 = time.perf_counter()
+        sc.render(0, aa=aa, threads=threads)
+        first = time.perf_counter() - t0
+        reps = int(max(1, min(50, budget_s / max(first, 1e-3))))
+        ts = [first]
+        for _ in range(reps - 1):
+            t0 = time.perf_counter()
+            sc.render(0, aa=aa, threads=threads)
+            ts.append(time.perf_counter() - t0)
+        med = sorted(ts)[len(ts) // 2]
+        kind = "port"
+    return {"value": round(rays_ps_per_frame / med / 1e6, 3), "unit": "Mray/s", "cores": threads, "kind": kind,
+            "ms_per_frame": round(med * 1e3, 3),
+            "sample": f"{reps} full frames of the same workload (median), render only, {threads} threads"}
+
+
+def main() -> int:
+    a = parse()
+    import torch
+    import torch.distributed as dist
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != a.gpus:
+        if world == 1 and a.gpus > 1:
+            print(f"--gpus {a.gpus} needs torchrun --nproc-per-node {a.gpus}", file=sys.stderr)
+            return 2
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    if world > 1:
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        dist.init_process_group("nccl", device_id=dev)
+
+    pkg = graft.import_pkg()
+    config, desc = CONFIGS[a.config]
+    aa = a.aa if a.aa is not None else (4 if a.config == "C5" else 1)
+    tmpdir = tempfile.mkdtemp(prefix=f"rtbench{rank}_")
+    xml = pkg.scenes.write_config(config, tmpdir)
+
+    t0 = time.perf_counter()
+    scene = pkg.Scene.from_xml(xml, device=local)
+    load_s = time.perf_counter() - t0
+    cam = scene.camera(0)
+    W, H, S = cam.image_width, cam.image_height, a.stripe_rows
+    rows = pkg.slab_rows(H, S, world)
+    slab = torch.empty((rows, W, 3), dtype=torch.uint8, device=dev)
+    stream = torch.cuda.current_stream(dev)
+    sp = stream.cuda_stream
+    if world > 1:
+        gathered = [torch.empty_like(slab) for _ in range(world)] if rank == 0 else None
+        gbuf = torch.empty((world, rows, W, 3), dtype=torch.uint8, device=dev) if rank == 0 else None
+        image = torch.empty((H, W, 3), dtype=torch.uint8, device=dev) if rank == 0 else None
+
+    # Counting pass (not timed): exact per-rank work for the byte model.
+    scene.counters_reset(sp)
+    scene.render_device(cam, aa, slab.data_ptr(), sp, S, rank, world, count=True)
+    cnt = scene.counters_read()
+    alg_bytes = (cnt["node_visits"] * B_NODE + cnt["tri_tests"] * B_TRI + cnt["sphere_tests"] * B_SPH
+                 + rows * W * aa * aa * B_PIX)
+    ps_local = cnt["primary_rays"] + cnt["shadow_rays"]
+    tot = torch.tensor([ps_local, cnt["primary_rays"], cnt["shadow_rays"], cnt["reflection_rays"]],
+                       dtype=torch.float64, device=dev)
+    if world > 1:
+        dist.all_reduce(tot)
+    ps_frame, prim_frame, shadow_frame, refl_frame = (int(x) for x in tot.tolist())
+
+    def step(ev_pair=None):
+        if ev_pair is not None:
+            ev_pair[0].record(stream)
+        scene.render_device(cam, aa, slab.data_ptr(), sp, S, rank, world)
+        if ev_pair is not None:
+            ev_pair[1].record(stream)
+        if world > 1:
+            dist.gather(slab, gather_list=[gbuf[i] for i in range(world)] if rank == 0 else None, dst=0)
+            if rank == 0:
+                pkg.unshuffle_stripes(gbuf.data_ptr(), image.data_ptr(), W, H, S, world, sp)
+
+    for _ in range(a.warmup):
+        step()
+    evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(a.steps)]
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    for i in range(a.steps):
+        step(evs[i])
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    kern_ms = sum(e0.elapsed_time(e1) for e0, e1 in evs) / a.steps
+    tmax = torch.tensor([elapsed, kern_ms], dtype=torch.float64, device=dev)
+    if world > 1:
+        dist.all_reduce(tmax, op=dist.ReduceOp.MAX)
+    elapsed, kern_ms_max = tmax.tolist()
+
+    if rank == 0:
+        ms = elapsed / a.steps * 1e3
+        value = ps_frame * a.steps / elapsed / 1e6
+        achieved = alg_bytes / (kern_ms / 1e3) / 1e9
+        line = {
+            "metric": "Mray/s (primary+shadow), horse_and_mug 1920x1080 depth 6" if a.config == "C3"
+                      else f"Mray/s (primary+shadow), {desc}",
+            "value": round(value, 3), "unit": "Mray/s", "n_gpus": world, "steps": a.steps, "warmup": a.warmup,
+            "ms_per_step": round(ms, 4), "higher_is_better": True, "scaling": "strong",
+            "vs_baseline": None, "dtype": "f32", "data": "synthetic (reference scene file, derived per SURVEY §8d)",
+            "config": {"workload": config, "description": desc, "width": W, "height": H, "aa": aa,
+                       "max_recursion_depth": 6 if config != "C2_cornellbox_800_d0" else 0,
+                       "parallelism": f"stripes{S}x{world}" + ("+rccl_gather" if world > 1 else ""),
+                       "primary_rays": prim_frame, "shadow_rays": shadow_frame, "reflection_rays": refl_frame,
+                       "mray_s_all": round((ps_frame + refl_frame) * a.steps / elapsed / 1e6, 3),
+                       "scene_load_s": round(load_s, 4)},
+            "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
+                         "frac": round(achieved / HBM_PEAK_GBPS, 4), "traffic": None,
+                         "kernel": "k_render", "kernel_ms": round(kern_ms, 4),
+                         "alg_bytes_per_launch": int(alg_bytes),
+                         "counts_per_launch": {k: cnt[k] for k in ("node_visits", "tri_tests", "sphere_tests")}},
+        }
+        if world == 1 and not a.no_cpu_baseline:
+            line["cpu_baseline"] = cpu_baseline(xml, aa, ps_frame, a.cpu_seconds)
+        print(json.dumps(line), flush=True)
+    scene.close()
+    if world > 1:
+        dist.destroy_process_group()
+    return 0
+
+
+if __name__ == "__main__":
+    sys.exit(main())

@@ -1,0 +1,181 @@
+/*
+ * rt.h — C-ABI of the MI355X-native renderer (librt_hip.so).
+ *
+ * Drop-in boundary for the reference's hot path.  The reference has no FFI;
+ * its operator boundary is the C++ class pair used by main()
+ * (raytracer.cpp:487-525):
+ *
+ *   RayTracer::RayTracer(parser::Scene&)            raytracer.cpp:335-350
+ *        -> rt_scene_create / rt_scene_load_xml     (flatten + BVH build + upload)
+ *   Image RayTracer::render(Camera&)                raytracer.cpp:362-383
+ *        -> rt_render (host buffer, synchronous) / rt_render_device (HBM, async)
+ *   static Image ImageProcessor::downSample(...)    raytracer.cpp:459-484
+ *        -> folded into rt_render* via aa_factor (and rt_downsample_host)
+ *   void write_ppm(const char*, unsigned char*, int, int)   ppm.h:4, ppm.cpp:4-39
+ *        -> rt_write_ppm (byte-identical P3)
+ *   Scene::loadFromXml(const std::string&)          parser.cpp:6-218
+ *        -> rt_scene_load_xml
+ *
+ * Conventions: plain pointers and sizes only; every function returns 0 on
+ * success or a negative rt_status, with a message in rt_last_error()
+ * (thread-local).  No exceptions cross this ABI (the reference throws
+ * std::runtime_error from parser.cpp:14,20 and ppm.cpp:10 instead).
+ * The library owns device copies of the scene until rt_scene_destroy; the
+ * caller owns every host buffer.  One in-flight render per rt_scene.
+ */
+#ifndef RT_RT_H
+#define RT_RT_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define RT_ABI_VERSION 1
+
+typedef enum rt_status {
+    RT_OK = 0,
+    RT_ERR_ARG = -1,        /* bad argument / shape                         */
+    RT_ERR_IO = -2,         /* file cannot be read or written               */
+    RT_ERR_PARSE = -3,      /* XML malformed / missing element              */
+    RT_ERR_HIP = -4,        /* HIP runtime error (message has the HIP name) */
+    RT_ERR_NO_DEVICE = -5,  /* no gfx950 device visible                     */
+    RT_ERR_LIMIT = -6       /* scene exceeds an encoding limit               */
+} rt_status;
+
+/* ---- scene model: field names and meaning follow parser.h:170-251 ---- */
+typedef struct rt_vec3f { float x, y, z; } rt_vec3f;
+
+typedef struct rt_camera {          /* parser::Camera (parser.h:170-178)     */
+    rt_vec3f position, gaze, up;
+    float near_plane[4];            /* left right bottom top (Vec4f x y z w) */
+    float near_distance;
+    int image_width, image_height;  /* OUTPUT resolution (before SSAA)       */
+} rt_camera;
+
+typedef struct rt_point_light { rt_vec3f position, intensity; } rt_point_light;  /* parser.h:180-183 */
+
+typedef struct rt_material {        /* parser::Material (parser.h:185-192)   */
+    int is_mirror;
+    rt_vec3f ambient, diffuse, specular, mirror;
+    float phong_exponent;
+} rt_material;
+
+typedef struct rt_triangle { int material_id, v0_id, v1_id, v2_id; } rt_triangle;  /* 1-based ids */
+typedef struct rt_sphere { int material_id, center_vertex_id; float radius; } rt_sphere;
+
+/* Borrowed host arrays, read during rt_scene_create only.  `triangles` is the
+ * reference's flattened order (raytracer.cpp:336-341): the scene's standalone
+ * <Triangle>s, then each <Mesh>'s faces in file order with the mesh's
+ * material id. */
+typedef struct rt_scene_desc {
+    int background_color[3];
+    float shadow_ray_epsilon;
+    int max_recursion_depth;
+    rt_vec3f ambient_light;
+    const rt_point_light* lights;   int num_lights;
+    const rt_material* materials;   int num_materials;
+    const rt_vec3f* vertices;       int num_vertices;
+    const rt_triangle* triangles;   int num_triangles;
+    const rt_sphere* spheres;       int num_spheres;
+} rt_scene_desc;
+
+#define RT_OPT_HOST_ONLY 1   /* load + BVH build only, no device upload (no GPU needed) */
+
+typedef struct rt_options {
+    int device;       /* HIP device ordinal; -1 = current device            */
+    int flags;        /* RT_OPT_* bits                                       */
+} rt_options;
+
+typedef struct rt_stats {
+    uint64_t primary_rays;      /* eye rays (W*H*F^2)                        */
+    uint64_t shadow_rays;       /* any-hit queries (one per hit per light)   */
+    uint64_t reflection_rays;   /* closest-hit traversals at depth >= 1      */
+    uint64_t node_visits;       /* BVH box tests (stack pops), both walks    */
+    uint64_t tri_tests;         /* Cramer triangle tests                     */
+    uint64_t sphere_tests;      /* analytic sphere tests                     */
+    double   kernel_ms;         /* device time of the render kernel(s)       */
+    double   wall_ms;           /* host wall time of the call                */
+} rt_stats;
+
+typedef struct rt_bvh_info {
+    int nodes, leaves, max_leaf_prims, max_depth, max_stack;
+    int triangles, spheres;
+    double build_ms;
+} rt_bvh_info;
+
+/* ---- errors / devices ---- */
+const char* rt_last_error(void);
+int rt_abi_version(void);
+int rt_device_count(int* count);
+
+/* ---- scene lifetime ---- */
+typedef struct rt_scene rt_scene;
+
+/* RayTracer ctor (raytracer.cpp:335-350): per-triangle normal/centre, BVH
+ * build bit-identical to bvh.h:48-163, SoA/AoS flatten and upload to HBM. */
+int rt_scene_create(const rt_scene_desc* desc, const rt_options* opts, rt_scene** out);
+/* Scene::loadFromXml (parser.cpp:6-218) + rt_scene_create. */
+int rt_scene_load_xml(const char* path, const rt_options* opts, rt_scene** out);
+void rt_scene_destroy(rt_scene* scene);
+
+int rt_scene_num_cameras(const rt_scene* scene);
+/* Camera i of an XML-loaded scene; name may be NULL. */
+int rt_scene_get_camera(const rt_scene* scene, int index, rt_camera* cam, char* name, int name_len);
+int rt_scene_bvh_info(const rt_scene* scene, rt_bvh_info* info);
+/* Override MaxRecursionDepth (parser.cpp:48-57) for subsequent renders. */
+int rt_scene_set_max_depth(rt_scene* scene, int max_recursion_depth);
+/* Copy of the flattened BVH in device layout (32-byte nodes, pre-order, left
+ * child = i+1; see csrc/device_layout.hpp).  Returns the node count; copies
+ * min(count, capacity) nodes when out != NULL. */
+int rt_scene_export_nodes(const rt_scene* scene, void* out, int capacity);
+
+/* ---- rendering ---- */
+/* RayTracer::render + ImageProcessor::downSample: renders `cam` at internal
+ * resolution (W*aa) x (H*aa), quantises each sample (toPixel, parser.h:88-93),
+ * box-filters with integer floor division.  out_rgb: caller-allocated
+ * W*H*3 bytes, row-major, top row first.  Synchronous.  stats may be NULL;
+ * when non-NULL the work counters are collected (slower counting kernel). */
+int rt_render(rt_scene* scene, const rt_camera* cam, int aa_factor,
+              uint8_t* out_rgb, rt_stats* stats);
+
+#define RT_RENDER_COUNT 1   /* flags: accumulate work counters on device */
+
+/* Asynchronous render into device memory on `stream` (a hipStream_t; NULL =
+ * the null stream).  Output rows are split into stripes of `stripe_rows`
+ * rows dealt round-robin over `nranks` ranks (the reference's row interleave,
+ * raytracer.cpp:353, at stripe granularity); this call renders rank `rank`'s
+ * stripes packed contiguously into out_dev, which must hold
+ * rt_slab_rows(H, stripe_rows, nranks) * W * 3 bytes.  nranks = 1 renders the
+ * full frame in row order.  With RT_RENDER_COUNT the counters accumulate
+ * into the scene's device counter block (rt_counters_reset / _read). */
+int rt_render_device(rt_scene* scene, const rt_camera* cam, int aa_factor,
+                     int stripe_rows, int rank, int nranks,
+                     void* out_dev, void* stream, int flags);
+/* Rows in one rank's slab (max over ranks, so all slabs have equal size). */
+int rt_slab_rows(int height, int stripe_rows, int nranks);
+/* Rank-0 reassembly: slabs[nranks][slab_rows][W][3] (gathered) -> image[H][W][3]. */
+int rt_unshuffle_stripes(const void* slabs_dev, void* image_dev, int width, int height,
+                         int stripe_rows, int nranks, void* stream);
+int rt_counters_reset(rt_scene* scene, void* stream);
+int rt_counters_read(rt_scene* scene, rt_stats* stats);   /* synchronises the device */
+
+/* Primary closest-hit per internal pixel ((W*aa) x (H*aa)): t (tSmall, -1 on
+ * miss) and material id (0 on miss) into caller-allocated host arrays
+ * (either may be NULL).  Debug / parity surface for Ray::getFirstIntersection
+ * (raytracer.cpp:177-225). */
+int rt_primary_hits(rt_scene* scene, const rt_camera* cam, int aa_factor,
+                    float* t_out, int32_t* material_out);
+
+/* ---- host utilities ---- */
+/* ImageProcessor::downSample (raytracer.cpp:459-484) on host buffers. */
+int rt_downsample_host(const uint8_t* in, int width, int height, int factor, uint8_t* out);
+/* write_ppm (ppm.cpp:4-39), byte-identical P3 output. */
+int rt_write_ppm(const char* path, const uint8_t* rgb, int width, int height);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* RT_RT_H */

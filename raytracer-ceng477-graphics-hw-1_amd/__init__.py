@@ -1,0 +1,246 @@
+"""Python view of librt_hip.so (the MI355X-native renderer) through its C-ABI.
+
+The product is the C-ABI library (include/rt/rt.h) and the drop-in C++ CLI
+(`raytracer scene.xml`, raytracer.cpp:487-525 semantics).  This module is the
+thin ctypes layer the tests and bench.py use: scene load, render into host or
+device (HBM) buffers, stripe helpers for the multi-GPU path, write_ppm.
+
+There is no CPU fallback: if librt_hip.so is missing this module raises on
+import of the library, and rendering requires a visible gfx950 device.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+from pathlib import Path
+from typing import Optional
+
+import numpy as np
+
+from . import scenes  # noqa: F401  (re-export: scene fixtures / derived configs)
+from . import stripes  # noqa: F401
+
+PKG_DIR = Path(__file__).resolve().parent
+LIB_PATH = PKG_DIR / "librt_hip.so"
+CLI_PATH = PKG_DIR / "raytracer"
+
+RT_OPT_HOST_ONLY = 1
+RT_RENDER_COUNT = 1
+
+
+class RtError(RuntimeError):
+    def __init__(self, code: int, msg: str):
+        super().__init__(f"rt error {code}: {msg}")
+        self.code = code
+
+
+class Vec3f(ctypes.Structure):
+    _fields_ = [("x", ctypes.c_float), ("y", ctypes.c_float), ("z", ctypes.c_float)]
+
+
+class Camera(ctypes.Structure):
+    """rt_camera == parser::Camera (parser.h:170-178) minus image_name."""
+    _fields_ = [("position", Vec3f), ("gaze", Vec3f), ("up", Vec3f),
+                ("near_plane", ctypes.c_float * 4), ("near_distance", ctypes.c_float),
+                ("image_width", ctypes.c_int), ("image_height", ctypes.c_int)]
+
+
+class Options(ctypes.Structure):
+    _fields_ = [("device", ctypes.c_int), ("flags", ctypes.c_int)]
+
+
+class Stats(ctypes.Structure):
+    _fields_ = [("primary_rays", ctypes.c_uint64), ("shadow_rays", ctypes.c_uint64),
+                ("reflection_rays", ctypes.c_uint64), ("node_visits", ctypes.c_uint64),
+                ("tri_tests", ctypes.c_uint64), ("sphere_tests", ctypes.c_uint64),
+                ("kernel_ms", ctypes.c_double), ("wall_ms", ctypes.c_double)]
+
+    def as_dict(self) -> dict:
+        return {k: getattr(self, k) for k, _ in self._fields_}
+
+
+class BvhInfo(ctypes.Structure):
+    _fields_ = [("nodes", ctypes.c_int), ("leaves", ctypes.c_int), ("max_leaf_prims", ctypes.c_int),
+                ("max_depth", ctypes.c_int), ("max_stack", ctypes.c_int), ("triangles", ctypes.c_int),
+                ("spheres", ctypes.c_int), ("build_ms", ctypes.c_double)]
+
+    def as_dict(self) -> dict:
+        return {k: getattr(self, k) for k, _ in self._fields_}
+
+
+# device_layout.hpp dl::Node (32 B)
+NODE_DTYPE = np.dtype([("minx", "<f4"), ("miny", "<f4"), ("minz", "<f4"), ("a", "<i4"),
+                       ("maxx", "<f4"), ("maxy", "<f4"), ("maxz", "<f4"), ("b", "<i4")])
+
+# (name, restype, argtypes) for every function declared in include/rt/rt.h
+_P = ctypes.c_void_p
+_SIGS = [
+    ("rt_last_error", ctypes.c_char_p, []),
+    ("rt_abi_version", ctypes.c_int, []),
+    ("rt_device_count", ctypes.c_int, [ctypes.POINTER(ctypes.c_int)]),
+    ("rt_scene_create", ctypes.c_int, [_P, ctypes.POINTER(Options), ctypes.POINTER(_P)]),
+    ("rt_scene_load_xml", ctypes.c_int, [ctypes.c_char_p, ctypes.POINTER(Options), ctypes.POINTER(_P)]),
+    ("rt_scene_destroy", None, [_P]),
+    ("rt_scene_num_cameras", ctypes.c_int, [_P]),
+    ("rt_scene_get_camera", ctypes.c_int, [_P, ctypes.c_int, ctypes.POINTER(Camera), ctypes.c_char_p, ctypes.c_int]),
+    ("rt_scene_bvh_info", ctypes.c_int, [_P, ctypes.POINTER(BvhInfo)]),
+    ("rt_scene_set_max_depth", ctypes.c_int, [_P, ctypes.c_int]),
+    ("rt_scene_export_nodes", ctypes.c_int, [_P, _P, ctypes.c_int]),
+    ("rt_render", ctypes.c_int, [_P, ctypes.POINTER(Camera), ctypes.c_int, _P, ctypes.POINTER(Stats)]),
+    ("rt_render_device", ctypes.c_int, [_P, ctypes.POINTER(Camera), ctypes.c_int, ctypes.c_int, ctypes.c_int,
+                                        ctypes.c_int, _P, _P, ctypes.c_int]),
+    ("rt_slab_rows", ctypes.c_int, [ctypes.c_int, ctypes.c_int, ctypes.c_int]),
+    ("rt_unshuffle_stripes", ctypes.c_int, [_P, _P, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int, _P]),
+    ("rt_counters_reset", ctypes.c_int, [_P, _P]),
+    ("rt_counters_read", ctypes.c_int, [_P, ctypes.POINTER(Stats)]),
+    ("rt_primary_hits", ctypes.c_int, [_P, ctypes.POINTER(Camera), ctypes.c_int, _P, _P]),
+    ("rt_downsample_host", ctypes.c_int, [_P, ctypes.c_int, ctypes.c_int, ctypes.c_int, _P]),
+    ("rt_write_ppm", ctypes.c_int, [ctypes.c_char_p, _P, ctypes.c_int, ctypes.c_int]),
+]
+
+_lib: Optional[ctypes.CDLL] = None
+
+
+def lib() -> ctypes.CDLL:
+    """Load librt_hip.so (built in-tree by __graft_entry__.build())."""
+    global _lib
+    if _lib is None:
+        if not LIB_PATH.exists():
+            raise RtError(-5, f"{LIB_PATH} not built (run __graft_entry__.build())")
+        L = ctypes.CDLL(str(LIB_PATH))
+        for name, res, args in _SIGS:
+            fn = getattr(L, name)
+            fn.restype = res
+            fn.argtypes = args
+        _lib = L
+    return _lib
+
+
+def _check(rc: int) -> None:
+    if rc != 0:
+        raise RtError(rc, lib().rt_last_error().decode())
+
+
+def device_count() -> int:
+    n = ctypes.c_int(0)
+    _check(lib().rt_device_count(ctypes.byref(n)))
+    return n.value
+
+
+def slab_rows(height: int, stripe_rows: int, nranks: int) -> int:
+    return lib().rt_slab_rows(height, stripe_rows, nranks)
+
+
+class Scene:
+    """An rt_scene: host scene + bit-exact BVH + device copies (one GPU)."""
+
+    def __init__(self, handle: int):
+        self._h = ctypes.c_void_p(handle)
+
+    @classmethod
+    def from_xml(cls, path: str | os.PathLike, device: int = -1, host_only: bool = False) -> "Scene":
+        h = ctypes.c_void_p()
+        opts = Options(device, RT_OPT_HOST_ONLY if host_only else 0)
+        _check(lib().rt_scene_load_xml(str(path).encode(), ctypes.byref(opts), ctypes.byref(h)))
+        return cls(h.value)
+
+    def close(self) -> None:
+        if self._h and self._h.value:
+            lib().rt_scene_destroy(self._h)
+            self._h = ctypes.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
+
+    @property
+    def handle(self) -> ctypes.c_void_p:
+        return self._h
+
+    def cameras(self) -> list[tuple[Camera, str]]:
+        out = []
+        for i in range(lib().rt_scene_num_cameras(self._h)):
+            cam = Camera()
+            name = ctypes.create_string_buffer(1024)
+            _check(lib().rt_scene_get_camera(self._h, i, ctypes.byref(cam), name, 1024))
+            out.append((cam, name.value.decode()))
+        return out
+
+    def camera(self, index: int = 0) -> Camera:
+        return self.cameras()[index][0]
+
+    def bvh_info(self) -> dict:
+        info = BvhInfo()
+        _check(lib().rt_scene_bvh_info(self._h, ctypes.byref(info)))
+        return info.as_dict()
+
+    def export_nodes(self) -> np.ndarray:
+        n = lib().rt_scene_export_nodes(self._h, None, 0)
+        if n < 0:
+            _check(n)
+        arr = np.zeros(n, dtype=NODE_DTYPE)
+        lib().rt_scene_export_nodes(self._h, arr.ctypes.data_as(ctypes.c_void_p), n)
+        return arr
+
+    def set_max_depth(self, depth: int) -> None:
+        _check(lib().rt_scene_set_max_depth(self._h, depth))
+
+    def render(self, cam: Camera, aa: int = 1, stats: bool = False) -> tuple[np.ndarray, Optional[dict]]:
+        """Synchronous render to a host (H, W, 3) uint8 array (rt_render)."""
+        img = np.empty((cam.image_height, cam.image_width, 3), dtype=np.uint8)
+        st = Stats() if stats else None
+        _check(lib().rt_render(self._h, ctypes.byref(cam), aa, img.ctypes.data_as(ctypes.c_void_p),
+                               ctypes.byref(st) if st is not None else None))
+        return img, (st.as_dict() if st is not None else None)
+
+    def render_device(self, cam: Camera, aa: int, out_ptr: int, stream: int = 0, stripe_rows: int | None = None,
+                      rank: int = 0, nranks: int = 1, count: bool = False) -> None:
+        """Asynchronous render of this rank's stripes into device memory (rt_render_device)."""
+        sr = stripe_rows if stripe_rows is not None else cam.image_height
+        _check(lib().rt_render_device(self._h, ctypes.byref(cam), aa, sr, rank, nranks, ctypes.c_void_p(out_ptr),
+                                      ctypes.c_void_p(stream), RT_RENDER_COUNT if count else 0))
+
+    def counters_reset(self, stream: int = 0) -> None:
+        _check(lib().rt_counters_reset(self._h, ctypes.c_void_p(stream)))
+
+    def counters_read(self) -> dict:
+        st = Stats()
+        _check(lib().rt_counters_read(self._h, ctypes.byref(st)))
+        return st.as_dict()
+
+    def primary_hits(self, cam: Camera, aa: int = 1) -> tuple[np.ndarray, np.ndarray]:
+        H, W = cam.image_height * aa, cam.image_width * aa
+        t = np.empty((H, W), dtype=np.float32)
+        m = np.empty((H, W), dtype=np.int32)
+        _check(lib().rt_primary_hits(self._h, ctypes.byref(cam), aa, t.ctypes.data_as(ctypes.c_void_p),
+                                     m.ctypes.data_as(ctypes.c_void_p)))
+        return t, m
+
+
+def unshuffle_stripes(slabs_ptr: int, image_ptr: int, width: int, height: int, stripe_rows: int, nranks: int,
+                      stream: int = 0) -> None:
+    _check(lib().rt_unshuffle_stripes(ctypes.c_void_p(slabs_ptr), ctypes.c_void_p(image_ptr), width, height,
+                                      stripe_rows, nranks, ctypes.c_void_p(stream)))
+
+
+def write_ppm(path: str | os.PathLike, img: np.ndarray) -> None:
+    img = np.ascontiguousarray(img, dtype=np.uint8)
+    h, w = img.shape[:2]
+    _check(lib().rt_write_ppm(str(path).encode(), img.ctypes.data_as(ctypes.c_void_p), w, h))
+
+
+def downsample_host(img: np.ndarray, factor: int) -> np.ndarray:
+    img = np.ascontiguousarray(img, dtype=np.uint8)
+    h, w = img.shape[:2]
+    out = np.empty((h // factor, w // factor, 3), dtype=np.uint8)
+    _check(lib().rt_downsample_host(img.ctypes.data_as(ctypes.c_void_p), w, h, factor,
+                                    out.ctypes.data_as(ctypes.c_void_p)))
+    return out

@@ -1,0 +1,57 @@
+// Device (HBM) layout of a scene — shared by host flattener and HIP kernels.
+//
+//   Node  32 B  (one 32-B sector, two dwordx4 loads)   — 50 079 nodes for horse_and_mug = 1.6 MB
+//     interior: {bmin.xyz, right child index} {bmax.xyz, axis}
+//     leaf:     {bmin.xyz, first prim}        {bmax.xyz, LEAF | nsph<<20 | ntri}
+//     left child of node i is i+1 (pre-order, bvh.h:81-105)
+//   Prim  48 B  leaf-contiguous primitive copies (bvh.h:43-44 leaves own copies),
+//               triangles first then spheres, in the reference's leaf order
+//     triangle: {a.xyz, tri id} {a-b .xyz, 0} {a-c .xyz, 0}
+//               (a-b, a-c are exactly the float differences Cramer's rule
+//                forms at raytracer.cpp:135-160, so precomputing them is exact)
+//     sphere:   {c.xyz, sphere id} {r, r*r, 0, 0} {0, 0, 0, material id}
+//   TriShade 16 B per triangle id: {normal.xyz, material id}  (winner only)
+//   Material 64 B: {ka*Ia .xyz, phong} {kd.xyz, is_mirror} {ks.xyz, 0} {km.xyz, 0}
+//   Light    32 B: {pos.xyz, 0} {intensity.xyz, 0}
+#pragma once
+#include <cstdint>
+
+namespace dl {
+
+constexpr int32_t kLeafBit = (int32_t)0x80000000u;
+constexpr int kNtriBits = 20;
+constexpr int32_t kNtriMask = (1 << kNtriBits) - 1;
+constexpr int kMaxLeafSpheres = (1 << 11) - 1;
+constexpr int kMaxStack = 64;   // traversal stack entries (BVH depth cap 19 -> <= 20 used)
+
+struct alignas(16) Node {
+    float minx, miny, minz; int32_t a;
+    float maxx, maxy, maxz; int32_t b;
+};
+
+struct alignas(16) Prim {
+    float p0x, p0y, p0z; int32_t id;
+    float p1x, p1y, p1z; float p1w;
+    float p2x, p2y, p2z; int32_t p2w;
+};
+
+struct alignas(16) TriShade { float nx, ny, nz; int32_t material; };
+
+struct alignas(16) Material {
+    float kax, kay, kaz, phong;     // ambient reflectance * ambient light (raytracer.cpp:394)
+    float kdx, kdy, kdz; int32_t is_mirror;
+    float ksx, ksy, ksz, pad0;
+    float kmx, kmy, kmz, pad1;
+};
+
+struct alignas(16) Light {
+    float px, py, pz, pad0;
+    float ix, iy, iz, pad1;
+};
+
+static_assert(sizeof(Node) == 32, "node size");
+static_assert(sizeof(Prim) == 48, "prim size");
+static_assert(sizeof(Material) == 64, "material size");
+static_assert(sizeof(Light) == 32, "light size");
+
+}  // namespace dl

@@ -1,0 +1,467 @@
+// XML scene loader, triangle preparation and bit-exact BVH builder (host).
+#include "host_scene.hpp"
+
+#include <cfloat>
+#include <chrono>
+#include <cmath>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <fstream>
+#include <sstream>
+
+namespace rtx {
+
+// ---------------------------------------------------------------------------
+// XML: a small DOM (elements, attributes, first text run).  tinyxml2 4.0.1 is
+// used by the reference only to hand element text to a std::stringstream
+// (parser.cpp:9-217); numbers therefore follow istream >> float / >> int,
+// i.e. strtof / strtol on whitespace-separated tokens.
+// ---------------------------------------------------------------------------
+namespace {
+
+struct Elem {
+    std::string name;
+    std::string attrs;
+    std::string text;
+    std::vector<int> kids;
+};
+
+class Dom {
+  public:
+    std::vector<Elem> el;
+
+    bool parse(const std::string& s, std::string& err) {
+        el.clear();
+        el.push_back(Elem{"#document", "", "", {}});
+        std::vector<int> open{0};
+        size_t i = 0, n = s.size();
+        while (i < n) {
+            if (s[i] != '<') {
+                size_t j = s.find('<', i);
+                if (j == std::string::npos) j = n;
+                Elem& cur = el[open.back()];
+                if (cur.kids.empty() && cur.text.empty()) cur.text.assign(s, i, j - i);
+                i = j;
+                continue;
+            }
+            if (s.compare(i, 4, "<!--") == 0) {
+                size_t j = s.find("-->", i + 4);
+                if (j == std::string::npos) { err = "unterminated comment"; return false; }
+                i = j + 3;
+                continue;
+            }
+            if (i + 1 < n && (s[i + 1] == '?' || s[i + 1] == '!')) {
+                size_t j = s.find('>', i);
+                if (j == std::string::npos) { err = "unterminated declaration"; return false; }
+                i = j + 1;
+                continue;
+            }
+            if (i + 1 < n && s[i + 1] == '/') {
+                size_t j = s.find('>', i);
+                if (j == std::string::npos || open.size() <= 1) { err = "unbalanced closing tag"; return false; }
+                open.pop_back();
+                i = j + 1;
+                continue;
+            }
+            size_t j = i + 1;
+            while (j < n && !std::isspace((unsigned char)s[j]) && s[j] != '>' && s[j] != '/') ++j;
+            Elem e;
+            e.name.assign(s, i + 1, j - i - 1);
+            size_t k = j;
+            while (k < n && s[k] != '>') {
+                if (s[k] == '"') {
+                    k = s.find('"', k + 1);
+                    if (k == std::string::npos) { err = "unterminated attribute"; return false; }
+                }
+                ++k;
+            }
+            if (k >= n) { err = "unterminated tag"; return false; }
+            bool self_close = s[k - 1] == '/';
+            e.attrs.assign(s, j, k - j);
+            int id = (int)el.size();
+            el.push_back(std::move(e));
+            el[open.back()].kids.push_back(id);
+            if (!self_close) open.push_back(id);
+            i = k + 1;
+        }
+        return true;
+    }
+
+    int child(int parent, const char* name) const {
+        if (parent < 0) return -1;
+        for (int k : el[parent].kids)
+            if (el[k].name == name) return k;
+        return -1;
+    }
+    std::vector<int> children(int parent, const char* name) const {
+        std::vector<int> out;
+        if (parent < 0) return out;
+        for (int k : el[parent].kids)
+            if (el[k].name == name) out.push_back(k);
+        return out;
+    }
+};
+
+// Token reader over one element's text.
+class Tok {
+  public:
+    explicit Tok(const std::string& t) : s_(t), p_(s_.c_str()) {}
+    bool f(float& v) {
+        char* e;
+        float x = std::strtof(p_, &e);
+        if (e == p_) return false;
+        v = x; p_ = e; return true;
+    }
+    bool i(int& v) {
+        char* e;
+        long x = std::strtol(p_, &e, 10);
+        if (e == p_) return false;
+        v = (int)x; p_ = e; return true;
+    }
+    bool v3(V3& v) { return f(v.x) && f(v.y) && f(v.z); }
+    bool word(std::string& w) {
+        while (*p_ && std::isspace((unsigned char)*p_)) ++p_;
+        const char* b = p_;
+        while (*p_ && !std::isspace((unsigned char)*p_)) ++p_;
+        w.assign(b, p_ - b);
+        return !w.empty();
+    }
+
+  private:
+    std::string s_;
+    const char* p_;
+};
+
+struct Need {
+    const Dom& d;
+    std::string& err;
+    int get(int parent, const char* name) {
+        int k = d.child(parent, name);
+        if (k < 0 && err.empty()) err = std::string("Error: missing element <") + name + ">";
+        return k;
+    }
+    const std::string& text(int parent, const char* name) {
+        static const std::string empty;
+        int k = get(parent, name);
+        return k < 0 ? empty : d.el[k].text;
+    }
+};
+
+}  // namespace
+
+std::string load_xml(const char* path, HostScene& sc) {
+    std::ifstream in(path, std::ios::binary);
+    if (!in) return "Error: The xml file cannot be loaded.";          // parser.cpp:14
+    std::stringstream buf;
+    buf << in.rdbuf();
+    Dom d;
+    std::string err;
+    if (!d.parse(buf.str(), err)) return "Error: The xml file cannot be loaded. (" + err + ")";
+    if (d.el[0].kids.empty()) return "Error: Root is not found.";   // parser.cpp:20
+    int root = d.el[0].kids.front();
+    Need need{d, err};
+    sc = HostScene();
+
+    if (int e = d.child(root, "BackgroundColor"); e >= 0) {          // parser.cpp:24-33
+        Tok t(d.el[e].text);
+        t.i(sc.bg[0]); t.i(sc.bg[1]); t.i(sc.bg[2]);
+    }
+    if (int e = d.child(root, "ShadowRayEpsilon"); e >= 0) {         // :36-45 (default 0.001)
+        Tok t(d.el[e].text);
+        t.f(sc.eps);
+    }
+    if (int e = d.child(root, "MaxRecursionDepth"); e >= 0) {        // :48-57 (default 0)
+        Tok t(d.el[e].text);
+        t.i(sc.max_depth);
+    }
+    int cams = need.get(root, "Cameras");                            // :60-90
+    for (int c : d.children(cams, "Camera")) {
+        CameraRec cam{};
+        Tok(need.text(c, "Position")).v3(cam.position);
+        Tok(need.text(c, "Gaze")).v3(cam.gaze);
+        Tok(need.text(c, "Up")).v3(cam.up);
+        Tok np(need.text(c, "NearPlane"));
+        for (float& v : cam.near_plane) np.f(v);
+        Tok(need.text(c, "NearDistance")).f(cam.near_distance);
+        Tok res(need.text(c, "ImageResolution"));
+        res.i(cam.width); res.i(cam.height);
+        Tok(need.text(c, "ImageName")).word(cam.name);
+        sc.cameras.push_back(cam);
+    }
+    int lights = need.get(root, "Lights");                           // :93-111
+    Tok(need.text(lights, "AmbientLight")).v3(sc.ambient);
+    for (int l : d.children(lights, "PointLight")) {
+        LightRec L{};
+        Tok(need.text(l, "Position")).v3(L.position);
+        Tok(need.text(l, "Intensity")).v3(L.intensity);
+        sc.lights.push_back(L);
+    }
+    int mats = need.get(root, "Materials");                          // :114-140
+    for (int m : d.children(mats, "Material")) {
+        MaterialRec M{};
+        M.is_mirror = d.el[m].attrs.find("type=\"mirror\"") != std::string::npos;  // :119
+        Tok(need.text(m, "AmbientReflectance")).v3(M.ambient);
+        Tok(need.text(m, "DiffuseReflectance")).v3(M.diffuse);
+        Tok(need.text(m, "SpecularReflectance")).v3(M.specular);
+        Tok(need.text(m, "MirrorReflectance")).v3(M.mirror);
+        Tok(need.text(m, "PhongExponent")).f(M.phong);
+        sc.materials.push_back(M);
+    }
+    {                                                                // :143-151
+        Tok t(need.text(root, "VertexData"));
+        V3 v;
+        while (t.v3(v)) sc.verts.push_back(v);
+    }
+    int objs = need.get(root, "Objects");
+    // raytracer.cpp:336-341: standalone triangles first, then mesh faces.
+    for (int tr : d.children(objs, "Triangle")) {                    // :180-195
+        TriRec T{};
+        Tok(need.text(tr, "Material")).i(T.material_id);
+        Tok ix(need.text(tr, "Indices"));
+        ix.i(T.v0); ix.i(T.v1); ix.i(T.v2);
+        sc.tris.push_back(T);
+    }
+    for (int me : d.children(objs, "Mesh")) {                        // :154-177
+        int mat = 0;
+        Tok(need.text(me, "Material")).i(mat);
+        Tok f(need.text(me, "Faces"));
+        int a, b, c;
+        while (f.i(a) && f.i(b) && f.i(c)) sc.tris.push_back(TriRec{mat, a, b, c, {0, 0, 0}, {0, 0, 0}});
+    }
+    for (int sp : d.children(objs, "Sphere")) {                      // :198-217
+        SphereRec S{};
+        Tok(need.text(sp, "Material")).i(S.material_id);
+        Tok(need.text(sp, "Center")).i(S.center_id);
+        Tok(need.text(sp, "Radius")).f(S.radius);
+        sc.spheres.push_back(S);
+    }
+    if (!err.empty()) return err;
+    // Validate ids (the reference would read out of bounds instead).
+    const int nv = (int)sc.verts.size(), nm = (int)sc.materials.size();
+    for (const TriRec& t : sc.tris)
+        if (t.v0 < 1 || t.v1 < 1 || t.v2 < 1 || t.v0 > nv || t.v1 > nv || t.v2 > nv || t.material_id < 1 || t.material_id > nm)
+            return "Error: triangle references a missing vertex or material";
+    for (const SphereRec& s : sc.spheres)
+        if (s.center_id < 1 || s.center_id > nv || s.material_id < 1 || s.material_id > nm)
+            return "Error: sphere references a missing vertex or material";
+    return "";
+}
+
+// ---------------------------------------------------------------------------
+// raytracer.cpp:342-348
+// ---------------------------------------------------------------------------
+void prepare_triangles(HostScene& s) {
+    for (TriRec& t : s.tris) {
+        const V3 a = s.verts[t.v0 - 1], b = s.verts[t.v1 - 1], c = s.verts[t.v2 - 1];
+        const V3 ba{b.x - a.x, b.y - a.y, b.z - a.z}, ca{c.x - a.x, c.y - a.y, c.z - a.z};
+        V3 n{ba.y * ca.z - ba.z * ca.y, ba.z * ca.x - ba.x * ca.z, ba.x * ca.y - ba.y * ca.x};
+        const float len = std::sqrt(n.x * n.x + n.y * n.y + n.z * n.z);
+        t.normal = V3{n.x / len, n.y / len, n.z / len};
+        const V3 sum{(a.x + b.x) + c.x, (a.y + b.y) + c.y, (a.z + b.z) + c.z};
+        t.center = V3{sum.x / 3, sum.y / 3, sum.z / 3};
+    }
+}
+
+// ---------------------------------------------------------------------------
+// BVH (bvh.h:48-163).  Build recursion is the reference's; the output is the
+// pre-order device layout.
+// ---------------------------------------------------------------------------
+namespace {
+
+constexpr int kMaxDepth = 19;    // bvh.h:18
+constexpr int kMaxTries = 19;    // bvh.h:117
+
+struct BNode {
+    V3 lo, hi;
+    int axis = 0, depth = 0;
+    int left = -1, right = -1;
+    std::vector<int> tris, sph;
+};
+
+class Builder {
+  public:
+    explicit Builder(const HostScene& s) : s_(s) {}
+    std::vector<BNode> nodes;
+
+    int build(std::vector<int> tris, std::vector<int> sph, int depth) {       // bvh.h:48-79
+        if (tris.empty() && sph.empty()) return -1;
+        int id = (int)nodes.size();
+        nodes.emplace_back();
+        nodes[id].depth = depth;
+        bounds(tris, sph, nodes[id].lo, nodes[id].hi);
+        if (tris.size() + sph.size() <= 1 || depth >= kMaxDepth) {
+            nodes[id].tris = std::move(tris);
+            nodes[id].sph = std::move(sph);
+            return id;
+        }
+        const int axis = widest(nodes[id].lo, nodes[id].hi);
+        nodes[id].axis = axis;
+        std::vector<int> lt, ls, rt, rs;
+        if (!split(axis, nodes[id].lo, nodes[id].hi, tris, sph, lt, ls, rt, rs)) {
+            nodes[id].tris = std::move(tris);
+            nodes[id].sph = std::move(sph);
+            return id;
+        }
+        tris.clear(); tris.shrink_to_fit();
+        sph.clear(); sph.shrink_to_fit();
+        int r = build(std::move(rt), std::move(rs), depth + 1);     // right first (bvh.h:69-70)
+        int l = build(std::move(lt), std::move(ls), depth + 1);
+        nodes[id].right = r;
+        nodes[id].left = l;
+        return id;
+    }
+
+  private:
+    const HostScene& s_;
+
+    // Scene::getBoundingBox + extendBoundingBox (parser.h:272-317)
+    void bounds(const std::vector<int>& tris, const std::vector<int>& sph, V3& lo, V3& hi) const {
+        lo = V3{FLT_MAX, FLT_MAX, FLT_MAX};
+        hi = V3{-FLT_MAX, -FLT_MAX, -FLT_MAX};
+        for (int t : tris) {
+            const TriRec& tr = s_.tris[t];
+            for (int vid : {tr.v0, tr.v1, tr.v2}) {
+                const V3& v = s_.verts[vid - 1];
+                if (v.x < lo.x) lo.x = v.x;
+                if (v.y < lo.y) lo.y = v.y;
+                if (v.z < lo.z) lo.z = v.z;
+                if (v.x > hi.x) hi.x = v.x;
+                if (v.y > hi.y) hi.y = v.y;
+                if (v.z > hi.z) hi.z = v.z;
+            }
+        }
+        float* plo = &lo.x;
+        float* phi = &hi.x;
+        for (int k : sph) {
+            const SphereRec& sp = s_.spheres[k];
+            const V3& c = s_.verts[sp.center_id - 1];
+            const float cc[3] = {c.x, c.y, c.z};
+            for (int ax = 0; ax < 3; ++ax) {
+                if (cc[ax] - sp.radius < plo[ax]) plo[ax] = cc[ax] - sp.radius;
+                if (cc[ax] + sp.radius > phi[ax]) phi[ax] = cc[ax] + sp.radius;
+            }
+        }
+    }
+
+    static int widest(const V3& lo, const V3& hi) {                           // parser.h:227-235
+        int w = 0;
+        for (int ax = 1; ax < 3; ++ax)
+            if (vget(hi, ax) - vget(lo, ax) > vget(hi, w) - vget(lo, w)) w = ax;
+        return w;
+    }
+
+    float key_tri(int t, int axis) const { return vget(s_.tris[t].center, axis); }
+    float key_sph(int k, int axis) const { return vget(s_.verts[s_.spheres[k].center_id - 1], axis); }
+
+    // BVHNode::partition (bvh.h:111-163): spatial midpoint of the widest axis,
+    // moved toward the populated side up to 19 times; stable order.
+    bool split(int axis, const V3& lo, const V3& hi, const std::vector<int>& tris, const std::vector<int>& sph,
+               std::vector<int>& lt, std::vector<int>& ls, std::vector<int>& rt, std::vector<int>& rs) const {
+        float start = vget(lo, axis), end = vget(hi, axis);
+        float mid = (start + end) / 2;
+        for (int attempt = 0; attempt < kMaxTries; ++attempt) {
+            size_t left = 0;
+            for (int t : tris) left += key_tri(t, axis) < mid;
+            for (int k : sph) left += key_sph(k, axis) < mid;
+            const size_t right = tris.size() + sph.size() - left;
+            if (left == 0) {
+                start = mid;
+                mid = (start + end) / 2;
+            } else if (right == 0) {
+                end = mid;
+                mid = (start + end) / 2;
+            } else {
+                for (int t : tris) (key_tri(t, axis) < mid ? lt : rt).push_back(t);
+                for (int k : sph) (key_sph(k, axis) < mid ? ls : rs).push_back(k);
+                return true;
+            }
+        }
+        return false;
+    }
+};
+
+inline int32_t fbits(float f) { int32_t i; std::memcpy(&i, &f, 4); return i; }
+inline float ibits(int32_t i) { float f; std::memcpy(&f, &i, 4); return f; }
+
+}  // namespace
+
+std::string build_bvh(const HostScene& s, FlatBVH& out) {
+    auto t0 = std::chrono::steady_clock::now();
+    out = FlatBVH();
+    Builder b(s);
+    std::vector<int> tris(s.tris.size()), sph(s.spheres.size());
+    for (size_t i = 0; i < tris.size(); ++i) tris[i] = (int)i;
+    for (size_t i = 0; i < sph.size(); ++i) sph[i] = (int)i;
+    b.nodes.reserve(2 * (tris.size() + sph.size()) + 1);
+    const int root = b.build(std::move(tris), std::move(sph), 0);
+
+    out.tri_shade.resize(s.tris.size());
+    for (size_t i = 0; i < s.tris.size(); ++i) {
+        const TriRec& t = s.tris[i];
+        out.tri_shade[i] = dl::TriShade{t.normal.x, t.normal.y, t.normal.z, t.material_id};
+    }
+    if (root < 0) return "";
+
+    // Pre-order flatten (bvh.h:81-105): node, left subtree, right subtree.
+    out.nodes.resize(b.nodes.size());
+    std::vector<int> flat_of(b.nodes.size(), -1);
+    std::vector<int> order;
+    order.reserve(b.nodes.size());
+    {
+        std::vector<int> st{root};
+        while (!st.empty()) {
+            int n = st.back();
+            st.pop_back();
+            flat_of[n] = (int)order.size();
+            order.push_back(n);
+            if (b.nodes[n].right >= 0) st.push_back(b.nodes[n].right);
+            if (b.nodes[n].left >= 0) st.push_back(b.nodes[n].left);
+        }
+    }
+    for (size_t f = 0; f < order.size(); ++f) {
+        const BNode& n = b.nodes[order[f]];
+        dl::Node& o = out.nodes[f];
+        o.minx = n.lo.x; o.miny = n.lo.y; o.minz = n.lo.z;
+        o.maxx = n.hi.x; o.maxy = n.hi.y; o.maxz = n.hi.z;
+        out.max_depth = std::max(out.max_depth, n.depth);
+        const bool leaf = n.left < 0 && n.right < 0;                 // bvh.h:107-109
+        if (!leaf) {
+            o.a = flat_of[n.right];
+            o.b = n.axis;
+            continue;
+        }
+        if ((int)n.tris.size() > dl::kNtriMask || (int)n.sph.size() > dl::kMaxLeafSpheres)
+            return "Error: BVH leaf exceeds the device encoding limits";
+        out.leaves++;
+        out.max_leaf = std::max(out.max_leaf, (int)(n.tris.size() + n.sph.size()));
+        o.a = (int32_t)out.prims.size();
+        o.b = dl::kLeafBit | ((int32_t)n.sph.size() << dl::kNtriBits) | (int32_t)n.tris.size();
+        for (int t : n.tris) {
+            const TriRec& tr = s.tris[t];
+            const V3 a = s.verts[tr.v0 - 1], bb = s.verts[tr.v1 - 1], c = s.verts[tr.v2 - 1];
+            dl::Prim p{};
+            p.p0x = a.x; p.p0y = a.y; p.p0z = a.z; p.id = t;
+            p.p1x = a.x - bb.x; p.p1y = a.y - bb.y; p.p1z = a.z - bb.z; p.p1w = 0;
+            p.p2x = a.x - c.x; p.p2y = a.y - c.y; p.p2z = a.z - c.z; p.p2w = 0;
+            out.prims.push_back(p);
+        }
+        for (int k : n.sph) {
+            const SphereRec& sp = s.spheres[k];
+            const V3 c = s.verts[sp.center_id - 1];
+            dl::Prim p{};
+            p.p0x = c.x; p.p0y = c.y; p.p0z = c.z; p.id = ~k;   // negative id marks a sphere
+            p.p1x = sp.radius; p.p1y = sp.radius * sp.radius; p.p1z = 0; p.p1w = 0;
+            p.p2x = 0; p.p2y = 0; p.p2z = 0; p.p2w = sp.material_id;
+            out.prims.push_back(p);
+        }
+    }
+    (void)ibits; (void)fbits;
+    // Ordered DFS pushes two children per interior pop: stack <= depth + 2.
+    out.max_stack = out.max_depth + 2;
+    if (out.max_stack > dl::kMaxStack) return "Error: BVH deeper than the device stack";
+    out.build_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+    return "";
+}
+
+}  // namespace rtx

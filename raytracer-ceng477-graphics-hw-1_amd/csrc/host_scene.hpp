@@ -1,0 +1,66 @@
+// Host-side scene model, XML loader and BVH builder of librt_hip.
+//
+// The BVH must be *bit-identical* to the reference's (bvh.h:48-163): same
+// boxes, same split rule/retries/depth cap, same pre-order flatten and the
+// same per-leaf primitive order — closest-hit tie-breaking and t-pruning
+// depend on it.  The flattened form here is the GPU
+// layout (device_layout.hpp), not the reference's 104-byte AoS BVHNode.
+#pragma once
+
+#include <cstdint>
+#include <string>
+#include <vector>
+
+#include "device_layout.hpp"
+
+namespace rtx {
+
+struct V3 { float x, y, z; };
+
+inline float vget(const V3& v, int i) { return i == 1 ? v.y : (i == 2 ? v.z : v.x); }
+
+struct CameraRec {
+    V3 position, gaze, up;
+    float near_plane[4];
+    float near_distance;
+    int width, height;
+    std::string name;
+};
+
+struct LightRec { V3 position, intensity; };
+struct MaterialRec { int is_mirror; V3 ambient, diffuse, specular, mirror; float phong; };
+struct TriRec { int material_id, v0, v1, v2; V3 normal, center; };
+struct SphereRec { int material_id, center_id; float radius; };
+
+struct HostScene {
+    int bg[3] = {0, 0, 0};
+    float eps = 0.001f;
+    int max_depth = 0;
+    V3 ambient{0, 0, 0};
+    std::vector<CameraRec> cameras;
+    std::vector<LightRec> lights;
+    std::vector<MaterialRec> materials;
+    std::vector<V3> verts;
+    std::vector<TriRec> tris;      // reference flattening order (raytracer.cpp:336-341)
+    std::vector<SphereRec> spheres;
+};
+
+// Flattened BVH in device layout.
+struct FlatBVH {
+    std::vector<dl::Node> nodes;        // pre-order, left child = i + 1
+    std::vector<dl::Prim> prims;        // leaf primitive copies, leaf-contiguous
+    std::vector<dl::TriShade> tri_shade;  // per triangle id: normal + material
+    int leaves = 0, max_leaf = 0, max_depth = 0, max_stack = 0;
+    double build_ms = 0;
+};
+
+// parser.cpp:6-218 semantics.  Returns empty string on success, else message.
+std::string load_xml(const char* path, HostScene& out);
+
+// raytracer.cpp:342-348: per-triangle normal and centre.
+void prepare_triangles(HostScene& s);
+
+// bvh.h:48-163 + the GPU flatten. Returns empty string or an error message.
+std::string build_bvh(const HostScene& s, FlatBVH& out);
+
+}  // namespace rtx

@@ -1,0 +1,56 @@
+// Kernel-launch interface between the C-ABI layer (rt_api.cpp) and the HIP
+// kernels (render_kernels.hip).  Plain structs passed by value as kernel args.
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <cstddef>
+#include <cstdint>
+
+#include "device_layout.hpp"
+
+namespace rtk {
+
+struct DevScene {
+    const dl::Node* nodes;
+    const dl::Prim* prims;
+    const dl::TriShade* tri_shade;
+    const dl::Material* mats;
+    const dl::Light* lights;
+    int nnodes;
+    int nlights;
+    int max_depth;        // MaxRecursionDepth
+    int stack_entries;    // LDS traversal-stack entries per thread
+    float eps;            // ShadowRayEpsilon
+    float bgx, bgy, bgz;  // BackgroundColor as float (raytracer.cpp:446-447)
+    float cos_thr;        // smallest float c with (float)(acos(c)*180/3.1415) <= 90.01
+
+    // Sphere prims carry ~sphere_index in p0.w (negative), triangles their id.
+    __device__ __forceinline__ bool prim_is_sphere(int, const float4 p0) const {
+        return __float_as_int(p0.w) < 0;
+    }
+};
+
+// EyeRayGenerator state (raytracer.cpp:287-288), computed on host in fp32.
+struct Eye {
+    float qx, qy, qz, ux, uy, uz, vx, vy, vz, ex, ey, ez;
+    float su, sv;   // suMultiplier, svMultiplier for the INTERNAL resolution
+};
+
+struct FrameParams {
+    int width, height;    // OUTPUT image
+    int aa;               // SSAA factor F (internal = F*W x F*H)
+    int stripe_rows;      // output rows per stripe
+    int rank, nranks;     // stripe round-robin
+    int slab_rows;        // rows in this rank's slab
+    uint8_t* out;         // slab_rows * width * 3
+    unsigned long long* counters;  // 6 x u64 (RT_RENDER_COUNT)
+};
+
+size_t render_lds_bytes(const DevScene& s);
+hipError_t launch_render(const DevScene& s, const Eye& e, const FrameParams& p, bool count, hipStream_t stream);
+hipError_t launch_primary_hits(const DevScene& s, const Eye& e, int W, int H, float* t, int* m, hipStream_t stream);
+hipError_t launch_unshuffle(const uint8_t* slabs, uint8_t* img, int width, int height, int stripe_rows, int nranks,
+                            int slab_rows, hipStream_t stream);
+
+}  // namespace rtk

@@ -1,0 +1,459 @@
+// C-ABI implementation (include/rt/rt.h): scene lifetime, upload, render
+// entry points, host utilities.  No exceptions cross the ABI.
+#include "rt/rt.h"
+
+#include <hip/hip_runtime.h>
+
+#include <chrono>
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <new>
+#include <string>
+#include <vector>
+
+#include "host_scene.hpp"
+#include "render_kernels.hpp"
+#include "rt_internal.hpp"
+
+namespace {
+
+thread_local std::string g_err;
+
+int fail(int code, const std::string& msg) {
+    g_err = msg;
+    return code;
+}
+
+#define HIP_TRY(expr)                                                                          \
+    do {                                                                                       \
+        hipError_t e_ = (expr);                                                                \
+        if (e_ != hipSuccess)                                                                  \
+            return fail(RT_ERR_HIP, std::string(#expr) + ": " + hipGetErrorName(e_) + " (" + \
+                                        hipGetErrorString(e_) + ")");                         \
+    } while (0)
+
+// theta = (float)(acos(c) * 180 / 3.1415); specular iff theta <= 90.01
+// (raytracer.cpp:411-412).  Each step is monotone in c, so the predicate is
+// exactly "c >= threshold" on [-1, 1] (NaN outside).  The threshold is found
+// with glibc's correctly rounded acos, making the device test bit-exact with
+// the reference without a device acos.
+bool theta_ok(float c) {
+    const float theta = (float)(std::acos((double)c) * 180 / 3.1415);
+    return theta <= 90.01;
+}
+
+int32_t ordered(float f) {
+    int32_t i;
+    std::memcpy(&i, &f, 4);
+    return i < 0 ? (int32_t)(0x80000000u - (uint32_t)i) : i;   // -0 and +0 -> 0
+}
+
+float from_ordered(int32_t o) {
+    int32_t i = o < 0 ? (int32_t)(0x80000000u - (uint32_t)o) : o;
+    float f;
+    std::memcpy(&f, &i, 4);
+    return f;
+}
+
+float cos_threshold() {
+    int32_t lo = ordered(-1.0f), hi = ordered(1.0f);   // theta_ok(lo) false, theta_ok(hi) true
+    while (hi - lo > 1) {
+        const int32_t mid = lo + (hi - lo) / 2;
+        if (theta_ok(from_ordered(mid))) hi = mid; else lo = mid;
+    }
+    return from_ordered(hi);
+}
+
+template <typename T>
+int upload(T** dst, const std::vector<T>& src) {
+    *dst = nullptr;
+    const size_t bytes = std::max<size_t>(sizeof(T), src.size() * sizeof(T));
+    HIP_TRY(hipMalloc(reinterpret_cast<void**>(dst), bytes));
+    if (!src.empty()) HIP_TRY(hipMemcpy(*dst, src.data(), src.size() * sizeof(T), hipMemcpyHostToDevice));
+    return RT_OK;
+}
+
+}  // namespace
+
+int rt_internal_set_error(int code, const char* msg) { return fail(code, msg); }
+
+struct rt_scene {
+    rtx::HostScene host;
+    rtx::FlatBVH bvh;
+    int device = 0;
+    bool host_only = false;
+    rtk::DevScene dev{};
+    dl::Node* d_nodes = nullptr;
+    dl::Prim* d_prims = nullptr;
+    dl::TriShade* d_tri = nullptr;
+    dl::Material* d_mats = nullptr;
+    dl::Light* d_lights = nullptr;
+    unsigned long long* d_counters = nullptr;
+    uint8_t* d_out = nullptr;
+    size_t out_cap = 0;
+    hipEvent_t ev0 = nullptr, ev1 = nullptr;
+
+    ~rt_scene() {
+        (void)hipFree(d_nodes); (void)hipFree(d_prims); (void)hipFree(d_tri); (void)hipFree(d_mats); (void)hipFree(d_lights);
+        (void)hipFree(d_counters); (void)hipFree(d_out);
+        if (ev0) (void)hipEventDestroy(ev0);
+        if (ev1) (void)hipEventDestroy(ev1);
+    }
+};
+
+namespace {
+
+int select_device(const rt_options* opts, int* dev) {
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess || n == 0) return fail(RT_ERR_NO_DEVICE, "no HIP device visible");
+    if (opts && opts->device >= 0) {
+        if (opts->device >= n) return fail(RT_ERR_ARG, "device ordinal out of range");
+        HIP_TRY(hipSetDevice(opts->device));
+    }
+    HIP_TRY(hipGetDevice(dev));
+    return RT_OK;
+}
+
+int finish_scene(rt_scene* s, const rt_options* opts) {
+    rtx::prepare_triangles(s->host);
+    std::string err = rtx::build_bvh(s->host, s->bvh);
+    if (!err.empty()) return fail(RT_ERR_LIMIT, err);
+    s->host_only = opts && (opts->flags & RT_OPT_HOST_ONLY);
+    if (s->host_only) return RT_OK;
+    int rc = select_device(opts, &s->device);
+    if (rc) return rc;
+
+    std::vector<dl::Material> mats(s->host.materials.size());
+    for (size_t i = 0; i < mats.size(); ++i) {
+        const rtx::MaterialRec& m = s->host.materials[i];
+        const rtx::V3& ia = s->host.ambient;
+        dl::Material& o = mats[i];
+        o.kax = m.ambient.x * ia.x; o.kay = m.ambient.y * ia.y; o.kaz = m.ambient.z * ia.z;  // :394
+        o.phong = m.phong;
+        o.kdx = m.diffuse.x; o.kdy = m.diffuse.y; o.kdz = m.diffuse.z; o.is_mirror = m.is_mirror ? 1 : 0;
+        o.ksx = m.specular.x; o.ksy = m.specular.y; o.ksz = m.specular.z; o.pad0 = 0;
+        o.kmx = m.mirror.x; o.kmy = m.mirror.y; o.kmz = m.mirror.z; o.pad1 = 0;
+    }
+    std::vector<dl::Light> lights(s->host.lights.size());
+    for (size_t i = 0; i < lights.size(); ++i) {
+        const rtx::LightRec& l = s->host.lights[i];
+        lights[i] = dl::Light{l.position.x, l.position.y, l.position.z, 0, l.intensity.x, l.intensity.y,
+                              l.intensity.z, 0};
+    }
+    if ((rc = upload(&s->d_nodes, s->bvh.nodes))) return rc;
+    if ((rc = upload(&s->d_prims, s->bvh.prims))) return rc;
+    if ((rc = upload(&s->d_tri, s->bvh.tri_shade))) return rc;
+    if ((rc = upload(&s->d_mats, mats))) return rc;
+    if ((rc = upload(&s->d_lights, lights))) return rc;
+    HIP_TRY(hipMalloc(reinterpret_cast<void**>(&s->d_counters), 8 * sizeof(unsigned long long)));
+    HIP_TRY(hipMemset(s->d_counters, 0, 8 * sizeof(unsigned long long)));
+    HIP_TRY(hipEventCreate(&s->ev0));
+    HIP_TRY(hipEventCreate(&s->ev1));
+
+    rtk::DevScene& d = s->dev;
+    d.nodes = s->d_nodes; d.prims = s->d_prims; d.tri_shade = s->d_tri; d.mats = s->d_mats; d.lights = s->d_lights;
+    d.nnodes = (int)s->bvh.nodes.size();
+    d.nlights = (int)lights.size();
+    d.max_depth = s->host.max_depth;
+    d.stack_entries = std::max(2, s->bvh.max_stack);
+    d.eps = s->host.eps;
+    d.bgx = (float)s->host.bg[0]; d.bgy = (float)s->host.bg[1]; d.bgz = (float)s->host.bg[2];
+    d.cos_thr = cos_threshold();
+    return RT_OK;
+}
+
+// EyeRayGenerator::init (raytracer.cpp:292-314) for the internal resolution.
+rtk::Eye make_eye(const rt_camera& c, int nx, int ny) {
+    using rtx::V3;
+    const V3 e{c.position.x, c.position.y, c.position.z};
+    const V3 w{-c.gaze.x, -c.gaze.y, -c.gaze.z};
+    const float dist = c.near_distance;
+    const float l = c.near_plane[0], r = c.near_plane[1], b = c.near_plane[2], t = c.near_plane[3];
+    const V3 v{c.up.x, c.up.y, c.up.z};
+    const V3 u{v.y * w.z - v.z * w.y, v.z * w.x - v.x * w.z, v.x * w.y - v.y * w.x};   // v x w
+    const V3 mw{-w.x, -w.y, -w.z};
+    const V3 m{e.x + mw.x * dist, e.y + mw.y * dist, e.z + mw.z * dist};
+    const V3 q1{m.x + u.x * l, m.y + u.y * l, m.z + u.z * l};
+    const V3 q{q1.x + v.x * t, q1.y + v.y * t, q1.z + v.z * t};
+    rtk::Eye g;
+    g.qx = q.x; g.qy = q.y; g.qz = q.z;
+    g.ux = u.x; g.uy = u.y; g.uz = u.z;
+    g.vx = v.x; g.vy = v.y; g.vz = v.z;
+    g.ex = e.x; g.ey = e.y; g.ez = e.z;
+    g.su = (r - l) / (float)nx;
+    g.sv = (t - b) / (float)ny;
+    return g;
+}
+
+int check_camera(const rt_camera* cam, int aa) {
+    if (!cam) return fail(RT_ERR_ARG, "camera is NULL");
+    if (aa < 1 || aa > 64) return fail(RT_ERR_ARG, "aa_factor must be in [1, 64]");
+    if (cam->image_width < 1 || cam->image_height < 1) return fail(RT_ERR_ARG, "empty image");
+    const long long iw = (long long)cam->image_width * aa, ih = (long long)cam->image_height * aa;
+    if (iw > (1 << 24) || ih > (1 << 24)) return fail(RT_ERR_ARG, "internal resolution too large");
+    return RT_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+const char* rt_last_error(void) { return g_err.c_str(); }
+int rt_abi_version(void) { return RT_ABI_VERSION; }
+
+int rt_device_count(int* count) {
+    if (!count) return fail(RT_ERR_ARG, "count is NULL");
+    int n = 0;
+    hipError_t e = hipGetDeviceCount(&n);
+    *count = e == hipSuccess ? n : 0;
+    return RT_OK;
+}
+
+int rt_scene_create(const rt_scene_desc* desc, const rt_options* opts, rt_scene** out) {
+    if (!desc || !out) return fail(RT_ERR_ARG, "desc/out is NULL");
+    *out = nullptr;
+    rt_scene* s = new (std::nothrow) rt_scene();
+    if (!s) return fail(RT_ERR_ARG, "out of host memory");
+    rtx::HostScene& h = s->host;
+    for (int i = 0; i < 3; ++i) h.bg[i] = desc->background_color[i];
+    h.eps = desc->shadow_ray_epsilon;
+    h.max_depth = desc->max_recursion_depth;
+    h.ambient = rtx::V3{desc->ambient_light.x, desc->ambient_light.y, desc->ambient_light.z};
+    auto v3 = [](const rt_vec3f& v) { return rtx::V3{v.x, v.y, v.z}; };
+    for (int i = 0; i < desc->num_lights; ++i)
+        h.lights.push_back(rtx::LightRec{v3(desc->lights[i].position), v3(desc->lights[i].intensity)});
+    for (int i = 0; i < desc->num_materials; ++i) {
+        const rt_material& m = desc->materials[i];
+        h.materials.push_back(rtx::MaterialRec{m.is_mirror, v3(m.ambient), v3(m.diffuse), v3(m.specular),
+                                               v3(m.mirror), m.phong_exponent});
+    }
+    for (int i = 0; i < desc->num_vertices; ++i) h.verts.push_back(v3(desc->vertices[i]));
+    const int nv = desc->num_vertices, nm = desc->num_materials;
+    for (int i = 0; i < desc->num_triangles; ++i) {
+        const rt_triangle& t = desc->triangles[i];
+        if (t.v0_id < 1 || t.v1_id < 1 || t.v2_id < 1 || t.v0_id > nv || t.v1_id > nv || t.v2_id > nv ||
+            t.material_id < 1 || t.material_id > nm) {
+            delete s;
+            return fail(RT_ERR_ARG, "triangle " + std::to_string(i) + " references a missing vertex or material");
+        }
+        h.tris.push_back(rtx::TriRec{t.material_id, t.v0_id, t.v1_id, t.v2_id, {0, 0, 0}, {0, 0, 0}});
+    }
+    for (int i = 0; i < desc->num_spheres; ++i) {
+        const rt_sphere& sp = desc->spheres[i];
+        if (sp.center_vertex_id < 1 || sp.center_vertex_id > nv || sp.material_id < 1 || sp.material_id > nm) {
+            delete s;
+            return fail(RT_ERR_ARG, "sphere " + std::to_string(i) + " references a missing vertex or material");
+        }
+        h.spheres.push_back(rtx::SphereRec{sp.material_id, sp.center_vertex_id, sp.radius});
+    }
+    int rc = finish_scene(s, opts);
+    if (rc) { delete s; return rc; }
+    *out = s;
+    return RT_OK;
+}
+
+int rt_scene_load_xml(const char* path, const rt_options* opts, rt_scene** out) {
+    if (!path || !out) return fail(RT_ERR_ARG, "path/out is NULL");
+    *out = nullptr;
+    rt_scene* s = new (std::nothrow) rt_scene();
+    if (!s) return fail(RT_ERR_ARG, "out of host memory");
+    std::string err = rtx::load_xml(path, s->host);
+    if (!err.empty()) {
+        delete s;
+        return fail(err.find("cannot be loaded") != std::string::npos ? RT_ERR_IO : RT_ERR_PARSE, err);
+    }
+    int rc = finish_scene(s, opts);
+    if (rc) { delete s; return rc; }
+    *out = s;
+    return RT_OK;
+}
+
+void rt_scene_destroy(rt_scene* scene) {
+    if (!scene) return;
+    if (!scene->host_only) (void)hipSetDevice(scene->device);
+    delete scene;
+}
+
+int rt_scene_num_cameras(const rt_scene* s) { return s ? (int)s->host.cameras.size() : 0; }
+
+int rt_scene_get_camera(const rt_scene* s, int index, rt_camera* cam, char* name, int name_len) {
+    if (!s || !cam) return fail(RT_ERR_ARG, "scene/cam is NULL");
+    if (index < 0 || index >= (int)s->host.cameras.size()) return fail(RT_ERR_ARG, "camera index out of range");
+    const rtx::CameraRec& c = s->host.cameras[index];
+    cam->position = rt_vec3f{c.position.x, c.position.y, c.position.z};
+    cam->gaze = rt_vec3f{c.gaze.x, c.gaze.y, c.gaze.z};
+    cam->up = rt_vec3f{c.up.x, c.up.y, c.up.z};
+    for (int i = 0; i < 4; ++i) cam->near_plane[i] = c.near_plane[i];
+    cam->near_distance = c.near_distance;
+    cam->image_width = c.width;
+    cam->image_height = c.height;
+    if (name && name_len > 0) std::snprintf(name, name_len, "%s", c.name.c_str());
+    return RT_OK;
+}
+
+int rt_scene_bvh_info(const rt_scene* s, rt_bvh_info* info) {
+    if (!s || !info) return fail(RT_ERR_ARG, "scene/info is NULL");
+    info->nodes = (int)s->bvh.nodes.size();
+    info->leaves = s->bvh.leaves;
+    info->max_leaf_prims = s->bvh.max_leaf;
+    info->max_depth = s->bvh.max_depth;
+    info->max_stack = s->bvh.max_stack;
+    info->triangles = (int)s->host.tris.size();
+    info->spheres = (int)s->host.spheres.size();
+    info->build_ms = s->bvh.build_ms;
+    return RT_OK;
+}
+
+int rt_scene_set_max_depth(rt_scene* s, int d) {
+    if (!s) return fail(RT_ERR_ARG, "scene is NULL");
+    if (d < -1 || d > 64) return fail(RT_ERR_ARG, "max_recursion_depth out of range [-1, 64]");
+    s->host.max_depth = d;
+    s->dev.max_depth = d;
+    return RT_OK;
+}
+
+int rt_scene_export_nodes(const rt_scene* s, void* out, int capacity) {
+    if (!s) return fail(RT_ERR_ARG, "scene is NULL");
+    const int n = (int)s->bvh.nodes.size();
+    if (out && capacity > 0) std::memcpy(out, s->bvh.nodes.data(), (size_t)std::min(n, capacity) * sizeof(dl::Node));
+    return n;
+}
+
+int rt_slab_rows(int height, int stripe_rows, int nranks) {
+    if (height < 1 || stripe_rows < 1 || nranks < 1) return 0;
+    const int stripes = (height + stripe_rows - 1) / stripe_rows;
+    return ((stripes + nranks - 1) / nranks) * stripe_rows;
+}
+
+int rt_render_device(rt_scene* s, const rt_camera* cam, int aa, int stripe_rows, int rank, int nranks,
+                     void* out_dev, void* stream, int flags) {
+    if (!s || !out_dev) return fail(RT_ERR_ARG, "scene/out is NULL");
+    if (s->host_only) return fail(RT_ERR_NO_DEVICE, "scene was created with RT_OPT_HOST_ONLY");
+    int rc = check_camera(cam, aa);
+    if (rc) return rc;
+    if (stripe_rows < 1 || nranks < 1 || rank < 0 || rank >= nranks) return fail(RT_ERR_ARG, "bad stripe/rank");
+    HIP_TRY(hipSetDevice(s->device));
+    const rtk::Eye eye = make_eye(*cam, cam->image_width * aa, cam->image_height * aa);
+    rtk::FrameParams p;
+    p.width = cam->image_width;
+    p.height = cam->image_height;
+    p.aa = aa;
+    p.stripe_rows = stripe_rows;
+    p.rank = rank;
+    p.nranks = nranks;
+    p.slab_rows = rt_slab_rows(cam->image_height, stripe_rows, nranks);
+    p.out = static_cast<uint8_t*>(out_dev);
+    p.counters = s->d_counters;
+    HIP_TRY(rtk::launch_render(s->dev, eye, p, (flags & RT_RENDER_COUNT) != 0, static_cast<hipStream_t>(stream)));
+    return RT_OK;
+}
+
+int rt_unshuffle_stripes(const void* slabs, void* image, int width, int height, int stripe_rows, int nranks,
+                         void* stream) {
+    if (!slabs || !image || width < 1 || height < 1 || stripe_rows < 1 || nranks < 1)
+        return fail(RT_ERR_ARG, "bad unshuffle arguments");
+    HIP_TRY(rtk::launch_unshuffle(static_cast<const uint8_t*>(slabs), static_cast<uint8_t*>(image), width, height,
+                                  stripe_rows, nranks, rt_slab_rows(height, stripe_rows, nranks),
+                                  static_cast<hipStream_t>(stream)));
+    return RT_OK;
+}
+
+int rt_counters_reset(rt_scene* s, void* stream) {
+    if (!s) return fail(RT_ERR_ARG, "scene is NULL");
+    HIP_TRY(hipSetDevice(s->device));
+    HIP_TRY(hipMemsetAsync(s->d_counters, 0, 8 * sizeof(unsigned long long), static_cast<hipStream_t>(stream)));
+    return RT_OK;
+}
+
+int rt_counters_read(rt_scene* s, rt_stats* st) {
+    if (!s || !st) return fail(RT_ERR_ARG, "scene/stats is NULL");
+    HIP_TRY(hipSetDevice(s->device));
+    HIP_TRY(hipDeviceSynchronize());
+    unsigned long long c[8];
+    HIP_TRY(hipMemcpy(c, s->d_counters, sizeof(c), hipMemcpyDeviceToHost));
+    st->primary_rays = c[0]; st->shadow_rays = c[1]; st->reflection_rays = c[2];
+    st->node_visits = c[3]; st->tri_tests = c[4]; st->sphere_tests = c[5];
+    return RT_OK;
+}
+
+int rt_render(rt_scene* s, const rt_camera* cam, int aa, uint8_t* out_rgb, rt_stats* stats) {
+    if (!s || !out_rgb) return fail(RT_ERR_ARG, "scene/out is NULL");
+    if (s->host_only) return fail(RT_ERR_NO_DEVICE, "scene was created with RT_OPT_HOST_ONLY");
+    int rc = check_camera(cam, aa);
+    if (rc) return rc;
+    const auto t0 = std::chrono::steady_clock::now();
+    HIP_TRY(hipSetDevice(s->device));
+    const size_t bytes = (size_t)cam->image_width * cam->image_height * 3;
+    if (bytes > s->out_cap) {
+        (void)hipFree(s->d_out);
+        s->d_out = nullptr;
+        s->out_cap = 0;
+        HIP_TRY(hipMalloc(reinterpret_cast<void**>(&s->d_out), bytes));
+        s->out_cap = bytes;
+    }
+    const bool count = stats != nullptr;
+    if (count) HIP_TRY(hipMemset(s->d_counters, 0, 8 * sizeof(unsigned long long)));
+    HIP_TRY(hipEventRecord(s->ev0, nullptr));
+    rc = rt_render_device(s, cam, aa, cam->image_height, 0, 1, s->d_out, nullptr, count ? RT_RENDER_COUNT : 0);
+    if (rc) return rc;
+    HIP_TRY(hipEventRecord(s->ev1, nullptr));
+    HIP_TRY(hipMemcpy(out_rgb, s->d_out, bytes, hipMemcpyDeviceToHost));
+    HIP_TRY(hipEventSynchronize(s->ev1));
+    if (stats) {
+        rc = rt_counters_read(s, stats);
+        if (rc) return rc;
+        float ms = 0;
+        HIP_TRY(hipEventElapsedTime(&ms, s->ev0, s->ev1));
+        stats->kernel_ms = ms;
+        stats->wall_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+    }
+    return RT_OK;
+}
+
+int rt_primary_hits(rt_scene* s, const rt_camera* cam, int aa, float* t_out, int32_t* m_out) {
+    if (!s) return fail(RT_ERR_ARG, "scene is NULL");
+    if (s->host_only) return fail(RT_ERR_NO_DEVICE, "scene was created with RT_OPT_HOST_ONLY");
+    int rc = check_camera(cam, aa);
+    if (rc) return rc;
+    HIP_TRY(hipSetDevice(s->device));
+    const int W = cam->image_width * aa, H = cam->image_height * aa;
+    const size_t n = (size_t)W * H;
+    float* dt = nullptr;
+    int* dm = nullptr;
+    HIP_TRY(hipMalloc(reinterpret_cast<void**>(&dt), n * 4));
+    if (hipMalloc(reinterpret_cast<void**>(&dm), n * 4) != hipSuccess) {
+        (void)hipFree(dt);
+        return fail(RT_ERR_HIP, "hipMalloc failed");
+    }
+    const rtk::Eye eye = make_eye(*cam, W, H);
+    hipError_t e = rtk::launch_primary_hits(s->dev, eye, W, H, dt, dm, nullptr);
+    if (e == hipSuccess && t_out) e = hipMemcpy(t_out, dt, n * 4, hipMemcpyDeviceToHost);
+    if (e == hipSuccess && m_out) e = hipMemcpy(m_out, dm, n * 4, hipMemcpyDeviceToHost);
+    if (e == hipSuccess) e = hipDeviceSynchronize();
+    (void)hipFree(dt);
+    (void)hipFree(dm);
+    if (e != hipSuccess) return fail(RT_ERR_HIP, std::string("primary hits: ") + hipGetErrorName(e));
+    return RT_OK;
+}
+
+int rt_downsample_host(const uint8_t* in, int width, int height, int factor, uint8_t* out) {
+    // ImageProcessor::downSample (raytracer.cpp:459-484); width/height are the
+    // INPUT (internal) dims, output is (width/factor) x (height/factor).
+    if (!in || !out || factor < 1 || width < factor || height < factor) return fail(RT_ERR_ARG, "bad downsample args");
+    const int nw = width / factor, nh = height / factor, ff = factor * factor;
+    for (int i = 0; i < nh; ++i)
+        for (int j = 0; j < nw; ++j) {
+            int sum[3] = {0, 0, 0};
+            for (int k = 0; k < factor; ++k)
+                for (int l = 0; l < factor; ++l) {
+                    const uint8_t* px = in + ((size_t)(i * factor + k) * width + j * factor + l) * 3;
+                    sum[0] += px[0]; sum[1] += px[1]; sum[2] += px[2];
+                }
+            uint8_t* o = out + ((size_t)i * nw + j) * 3;
+            o[0] = (uint8_t)(sum[0] / ff); o[1] = (uint8_t)(sum[1] / ff); o[2] = (uint8_t)(sum[2] / ff);
+        }
+    return RT_OK;
+}
+
+}  // extern "C"

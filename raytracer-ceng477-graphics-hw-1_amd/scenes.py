@@ -1,0 +1,89 @@
+"""Scene fixtures and the derived benchmark scenes.
+
+The reference ships its scenes as XML (`inputs/*.xml`); copies live gzip'd in
+tests/golden/scenes/.  BASELINE.json's configs are *derived* from them by
+editing the XML text only (so both the reference harness and this framework's
+loader parse exactly the same bytes):
+
+  C1  simple.xml verbatim
+  C2  cornellbox.xml, only <Camera id="2"> (800x800), MaxRecursionDepth 0
+  C3  horse_and_mug.xml, 1920x1080, NearPlane -1 1 -0.5625 0.5625, depth 6
+  C5  C3 at 7680x4320 (rendered with SSAA factor 4 = 16 spp)
+"""
+from __future__ import annotations
+
+import gzip
+import os
+import re
+from pathlib import Path
+
+ROOT = Path(__file__).resolve().parent.parent
+SCENE_DIR = ROOT / "tests" / "golden" / "scenes"
+
+
+def scene_text(name: str) -> str:
+    """Text of a reference scene (e.g. 'horse_and_mug.xml')."""
+    with gzip.open(SCENE_DIR / (name + ".gz"), "rt") as f:
+        return f.read()
+
+
+def _sub(tag: str, value: str, text: str) -> str:
+    pat = re.compile(r"(<%s>)(.*?)(</%s>)" % (tag, tag), re.S)
+    out, n = pat.subn(lambda m: m.group(1) + value + m.group(3), text)
+    if n == 0:
+        raise ValueError(f"tag <{tag}> not found")
+    return out
+
+
+def derive_xml(text: str, depth: int | None = None, res: tuple[int, int] | None = None,
+               near: tuple[float, float, float, float] | None = None,
+               keep_camera: str | None = None, image_name: str | None = None) -> str:
+    """Apply the §8d edits to a scene's XML text."""
+    if keep_camera is not None:
+        cams = re.compile(r"\s*<Camera id=\"([^\"]*)\">.*?</Camera>", re.S)
+        text = cams.sub(lambda m: m.group(0) if m.group(1) == keep_camera else "", text)
+    if depth is not None:
+        text = _sub("MaxRecursionDepth", str(depth), text)
+    if res is not None:
+        text = _sub("ImageResolution", f"{res[0]} {res[1]}", text)
+    if near is not None:
+        text = _sub("NearPlane", " ".join(_fmt(v) for v in near), text)
+    if image_name is not None:
+        text = _sub("ImageName", image_name, text)
+    return text
+
+
+def _fmt(v: float) -> str:
+    return repr(float(v)) if float(v) != int(v) else str(int(v))
+
+
+# name -> (scene file, derive kwargs)
+CONFIGS: dict[str, tuple[str, dict]] = {
+    "C1_simple": ("simple.xml", {}),
+    "C2_cornellbox_800_d0": ("cornellbox.xml", dict(keep_camera="2", depth=0,
+                                                     image_name="cornellbox_800_d0.ppm")),
+    "hm_verbatim": ("horse_and_mug.xml", {}),
+    "C3_hm_1080p_d6": ("horse_and_mug.xml", dict(depth=6, res=(1920, 1080),
+                                                 near=(-1, 1, -0.5625, 0.5625),
+                                                 image_name="horse_and_mug_1080p_d6.ppm")),
+    "C5_hm_8k_d6": ("horse_and_mug.xml", dict(depth=6, res=(7680, 4320),
+                                              near=(-1, 1, -0.5625, 0.5625),
+                                              image_name="horse_and_mug_8k_d6.ppm")),
+}
+
+
+def config_xml(name: str) -> str:
+    """XML text of a named config: a §8d derived scene or any reference scene file."""
+    if name in CONFIGS:
+        scene, kw = CONFIGS[name]
+        return derive_xml(scene_text(scene), **kw)
+    return scene_text(name if name.endswith(".xml") else name + ".xml")
+
+
+def write_config(name: str, directory: str | os.PathLike) -> str:
+    """Write the config's XML into `directory`; return its path."""
+    d = Path(directory)
+    d.mkdir(parents=True, exist_ok=True)
+    p = d / (name if name.endswith(".xml") else name + ".xml")
+    p.write_text(config_xml(name))
+    return str(p)

@@ -1,0 +1,162 @@
+"""GPU parity: the HIP path (through the C-ABI) against the reference goldens.
+
+Bar (BASELINE.json north_star): integer RGB bit-exact after the same
+clamp/quantise/SSAA; primary hit-t within 1e-4 (we also report exact-bit
+agreement); work counters equal to the oracle's (same traversal order).
+"""
+from __future__ import annotations
+
+import hashlib
+
+import numpy as np
+import pytest
+
+from conftest import GOLDEN_DIR, config_path, golden_by_name, load_golden_image
+from test_oracle import CPU_GOLDENS
+
+pytestmark = pytest.mark.gpu
+
+T_TOL = 1e-4   # north_star: float hit-t within 1e-4
+
+
+@pytest.fixture(scope="module")
+def torch_cuda():
+    torch = pytest.importorskip("torch")
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    torch.cuda.init()
+    return torch
+
+
+def _counters(c):
+    return (c["primary"], c["shadow"], c["reflection"], c["node_visits"], c["tri_tests"], c["sphere_tests"])
+
+
+def _stats(s):
+    return (s["primary_rays"], s["shadow_rays"], s["reflection_rays"], s["node_visits"], s["tri_tests"],
+            s["sphere_tests"])
+
+
+@pytest.mark.parametrize("name", CPU_GOLDENS)
+def test_render_bit_exact(name, goldens, pkg, scene_dir, torch_cuda):
+    g = golden_by_name(goldens, name)
+    with pkg.Scene.from_xml(config_path(scene_dir, g["config"]), device=0) as s:
+        cams = s.cameras()
+        for cam in g["cameras"]:
+            c, _ = cams[cam["camera"]]
+            img, st = s.render(c, aa=g["aa"], stats=True)
+            ref = load_golden_image(cam)
+            bad = int((img != ref).any(axis=2).sum())
+            assert bad == 0, f"{name}/{cam['image']}: {bad} pixels differ (max |d| " \
+                             f"{int(np.abs(img.astype(int) - ref).max())})"
+            assert _stats(st) == _counters(cam["counters"]), f"{name}: work counters differ from oracle"
+            # the non-counting (bench) kernel variant must produce the same bytes
+            img2, _ = s.render(c, aa=g["aa"], stats=False)
+            assert np.array_equal(img2, ref)
+
+
+@pytest.mark.parametrize("name", ["C1_simple_aa1", "C2_cornellbox_800_d0_aa1", "hm_verbatim_aa1",
+                                  "C3_hm_1080p_d6_aa1"])
+def test_primary_hit_t(name, goldens, pkg, scene_dir, torch_cuda):
+    g = golden_by_name(goldens, name)
+    z = np.load(GOLDEN_DIR / g["primary_hits"]["file"], allow_pickle=False)
+    with pkg.Scene.from_xml(config_path(scene_dir, g["config"]), device=0) as s:
+        t, m = s.primary_hits(s.camera(0), aa=g["aa"])
+    ft, fm = t.reshape(-1), m.reshape(-1)
+    assert np.array_equal(fm[z["idx"]], z["material"])
+    assert np.max(np.abs(ft[z["idx"]] - z["t"])) <= T_TOL
+    # stronger than the bar: the full-frame t array is bit-identical
+    assert hashlib.sha256(ft.tobytes()).hexdigest() == g["primary_hits"]["sha256_t"]
+    assert hashlib.sha256(fm.tobytes()).hexdigest() == g["primary_hits"]["sha256_material"]
+
+
+@pytest.mark.parametrize("nranks,stripe", [(2, 8), (3, 8), (8, 8), (4, 5)])
+def test_stripes_unshuffle_equals_full_frame(nranks, stripe, goldens, pkg, scene_dir, torch_cuda):
+    """The multi-GPU partition rendered rank by rank on one GPU + device unshuffle."""
+    torch = torch_cuda
+    g = golden_by_name(goldens, "C3_hm_1080p_d6_aa1")
+    ref = load_golden_image(g["cameras"][0])
+    with pkg.Scene.from_xml(config_path(scene_dir, g["config"]), device=0) as s:
+        cam = s.camera(0)
+        W, H = cam.image_width, cam.image_height
+        rows = pkg.slab_rows(H, stripe, nranks)
+        assert rows == pkg.stripes.slab_rows(H, stripe, nranks)
+        slabs = torch.zeros((nranks, rows, W, 3), dtype=torch.uint8, device="cuda:0")
+        stream = torch.cuda.current_stream().cuda_stream
+        for r in range(nranks):
+            s.render_device(cam, 1, slabs[r].data_ptr(), stream, stripe_rows=stripe, rank=r, nranks=nranks)
+        img = torch.empty((H, W, 3), dtype=torch.uint8, device="cuda:0")
+        pkg.unshuffle_stripes(slabs.data_ptr(), img.data_ptr(), W, H, stripe, nranks, stream)
+        torch.cuda.synchronize()
+        got = img.cpu().numpy()
+        assert np.array_equal(got, ref)
+        # host mirror of the mapping agrees with the device kernel
+        assert np.array_equal(pkg.stripes.unshuffle(slabs.cpu().numpy(), H, stripe), ref)
+
+
+def test_device_counters_accumulate(goldens, pkg, scene_dir, torch_cuda):
+    torch = torch_cuda
+    g = golden_by_name(goldens, "C2_cornellbox_800_d0_aa1")
+    cam_g = g["cameras"][0]
+    with pkg.Scene.from_xml(config_path(scene_dir, g["config"]), device=0) as s:
+        cam = s.camera(0)
+        out = torch.empty((cam.image_height, cam.image_width, 3), dtype=torch.uint8, device="cuda:0")
+        stream = torch.cuda.current_stream().cuda_stream
+        s.counters_reset(stream)
+        s.render_device(cam, 1, out.data_ptr(), stream, count=True)
+        s.render_device(cam, 1, out.data_ptr(), stream, count=True)
+        st = s.counters_read()
+        assert _stats(st) == tuple(2 * v for v in _counters(cam_g["counters"]))
+        assert np.array_equal(out.cpu().numpy(), load_golden_image(cam_g))
+
+
+def test_max_depth_override_matches_derived_scene(goldens, pkg, scene_dir, torch_cuda):
+    """cornellbox.xml camera 2 with MaxRecursionDepth forced to 0 == the C2 golden."""
+    g = golden_by_name(goldens, "C2_cornellbox_800_d0_aa1")
+    with pkg.Scene.from_xml(config_path(scene_dir, "cornellbox.xml"), device=0) as s:
+        s.set_max_depth(0)
+        img, _ = s.render(s.camera(1), aa=1)
+    assert np.array_equal(img, load_golden_image(g["cameras"][0]))
+
+
+def test_edge_scenes_vs_oracle(pkg, oracle, tmp_path, torch_cuda):
+    """Empty object list (all background), negative depth (all black), odd sizes, AA 5."""
+    base = pkg.scenes.scene_text("simple.xml")
+    empty = base.split("<Objects>")[0] + "<Objects>\n</Objects>\n</Scene>\n"
+    cases = {
+        "empty": pkg.scenes.derive_xml(empty, res=(37, 23)),
+        "neg_depth": pkg.scenes.derive_xml(base, depth=-1, res=(17, 9)),
+        "odd_aa5": pkg.scenes.derive_xml(base, res=(33, 19)),
+        "mirror_odd": pkg.scenes.derive_xml(pkg.scenes.scene_text("mirror_spheres.xml"), res=(61, 45)),
+    }
+    for name, xml in cases.items():
+        p = tmp_path / f"{name}.xml"
+        p.write_text(xml.replace('<BackgroundColor>0 0 0</BackgroundColor>',
+                                 '<BackgroundColor>7 200 31</BackgroundColor>'))
+        aa = 5 if name == "odd_aa5" else 1
+        ref, _ = oracle.OracleScene(p).render(0, aa=aa)
+        with pkg.Scene.from_xml(p, device=0) as s:
+            img, _ = s.render(s.camera(0), aa=aa)
+        assert np.array_equal(img, ref), name
+
+
+def test_bad_arguments_fail_loudly(pkg, scene_dir, torch_cuda):
+    with pkg.Scene.from_xml(config_path(scene_dir, "simple.xml"), device=0) as s:
+        cam = s.camera(0)
+        with pytest.raises(pkg.RtError):
+            s.render(cam, aa=0)
+        with pytest.raises(pkg.RtError):
+            s.render_device(cam, 1, 0)      # NULL output
+        with pytest.raises(pkg.RtError):
+            s.render_device(cam, 1, 1 << 20, stripe_rows=8, rank=3, nranks=2)
+
+
+@pytest.mark.parametrize("name", ["C5_hm_8k_d6_aa4"])
+def test_full_size_c5_sha(name, goldens, pkg, scene_dir, torch_cuda):
+    """BASELINE config 5 at full size (7680x4320, 16 spp): sha256 of the RGB bytes."""
+    g = golden_by_name(goldens, name)
+    cam_g = g["cameras"][0]
+    with pkg.Scene.from_xml(config_path(scene_dir, g["config"]), device=0) as s:
+        img, st = s.render(s.camera(0), aa=4, stats=True)
+    assert hashlib.sha256(img.tobytes()).hexdigest() == cam_g["sha256_rgb"]
+    assert _stats(st) == _counters(cam_g["counters"])

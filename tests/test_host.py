@@ -1,0 +1,210 @@
+"""CPU tests of the product's host side: the C-ABI library loads and exports
+every declared symbol, the XML loader and BVH builder reproduce the reference's
+(via the pinned oracle), write_ppm is byte-identical, error paths."""
+from __future__ import annotations
+
+import ctypes
+import hashlib
+import re
+
+import numpy as np
+import pytest
+
+from conftest import ROOT, config_path, golden_by_name, load_golden_image
+
+ALL_SCENES = ["simple.xml", "simple_shading.xml", "simple_reflectance.xml", "cornellbox.xml",
+              "mirror_spheres.xml", "marbles.xml", "monkey.xml", "bunny.xml", "berserker.xml", "car.xml",
+              "low_poly.xml", "dragon_lowres.xml", "horse_and_mug.xml", "C2_cornellbox_800_d0",
+              "C3_hm_1080p_d6"]
+
+
+def declared_functions() -> list[str]:
+    text = (ROOT / "include" / "rt" / "rt.h").read_text()
+    text = re.sub(r"/\*.*?\*/", "", text, flags=re.S)
+    return sorted(set(re.findall(r"\b(rt_[a-z0-9_]+)\s*\(", text)))
+
+
+def test_library_exports_every_declared_symbol(pkg):
+    L = pkg.lib()
+    names = declared_functions()
+    assert len(names) >= 20
+    for n in names:
+        assert hasattr(L, n), n
+    bound = {s[0] for s in pkg._SIGS}
+    assert set(names) == bound, "ctypes bindings out of sync with rt.h"
+    assert L.rt_abi_version() == 1
+
+
+def test_cli_binary_built(pkg):
+    assert pkg.CLI_PATH.exists()
+
+
+@pytest.mark.parametrize("scene", ALL_SCENES)
+def test_bvh_identical_to_oracle(scene, pkg, oracle, scene_dir):
+    path = config_path(scene_dir, scene)
+    s = pkg.Scene.from_xml(path, host_only=True)
+    o = oracle.OracleScene(path)
+    a, b = s.export_nodes(), o.export_nodes()
+    assert a.shape == b.shape
+    assert a.tobytes() == b.tobytes(), "BVH differs from the reference build (bvh.h:48-163)"
+    info, oinfo = s.bvh_info(), o.bvh_info()
+    assert info["nodes"] == oinfo["nodes"] and info["leaves"] == oinfo["leaves"]
+    assert info["max_leaf_prims"] == oinfo["max_leaf"]
+    assert info["triangles"] == oinfo["triangles"] and info["spheres"] == oinfo["spheres"]
+    assert info["max_stack"] <= 64
+
+
+def test_horse_and_mug_bvh_stats(pkg, scene_dir):
+    # 50 079 nodes / 25 040 leaves / max leaf 29 / depth 19
+    s = pkg.Scene.from_xml(config_path(scene_dir, "horse_and_mug.xml"), host_only=True)
+    info = s.bvh_info()
+    assert (info["nodes"], info["leaves"], info["max_leaf_prims"], info["max_depth"]) == (50079, 25040, 29, 19)
+    assert (info["triangles"], info["spheres"]) == (31582, 2)
+
+
+@pytest.mark.parametrize("scene", ["cornellbox.xml", "car.xml", "berserker.xml", "C3_hm_1080p_d6"])
+def test_cameras_parsed_like_reference(scene, pkg, oracle, scene_dir):
+    path = config_path(scene_dir, scene)
+    cams = pkg.Scene.from_xml(path, host_only=True).cameras()
+    ocams = oracle.OracleScene(path).cameras()
+    assert [(c.image_width, c.image_height, n) for c, n in cams] == ocams
+
+
+def test_derived_scene_edits(pkg):
+    x = pkg.scenes.config_xml("C3_hm_1080p_d6")
+    assert "<MaxRecursionDepth>6</MaxRecursionDepth>" in x
+    assert "<ImageResolution>1920 1080</ImageResolution>" in x
+    assert "<NearPlane>-1 1 -0.5625 0.5625</NearPlane>" in x
+    c2 = pkg.scenes.config_xml("C2_cornellbox_800_d0")
+    assert c2.count("<Camera id=") == 1 and '<Camera id="2">' in c2
+
+
+@pytest.mark.parametrize("name", ["C1_simple_aa1", "C2_cornellbox_800_d0_aa1", "hm_verbatim_aa1"])
+def test_write_ppm_byte_identical(name, pkg, oracle, goldens, tmp_path):
+    cam = golden_by_name(goldens, name)["cameras"][0]
+    img = load_golden_image(cam)
+    p1, p2 = tmp_path / "a.ppm", tmp_path / "b.ppm"
+    pkg.write_ppm(p1, img)
+    oracle.write_ppm(p2, img)
+    h1 = hashlib.sha256(p1.read_bytes()).hexdigest()
+    assert h1 == cam["sha256_ppm"], "rt_write_ppm output differs from the reference's write_ppm"
+    assert p1.read_bytes() == p2.read_bytes()
+
+
+def test_write_ppm_edge_shapes(pkg, oracle, tmp_path):
+    rng = np.random.default_rng(0)
+    for h, w in [(1, 1), (3, 1), (1, 5), (7, 13)]:
+        img = rng.integers(0, 256, size=(h, w, 3), dtype=np.uint8)
+        pkg.write_ppm(tmp_path / "a.ppm", img)
+        oracle.write_ppm(tmp_path / "b.ppm", img)
+        assert (tmp_path / "a.ppm").read_bytes() == (tmp_path / "b.ppm").read_bytes()
+
+
+def test_write_ppm_unwritable_path(pkg):
+    with pytest.raises(pkg.RtError) as e:
+        pkg.write_ppm("/nonexistent_dir/x.ppm", np.zeros((2, 2, 3), np.uint8))
+    assert e.value.code == -2
+
+
+@pytest.mark.parametrize("factor", [1, 2, 3, 4])
+def test_downsample_host_floor_mean(pkg, factor):
+    rng = np.random.default_rng(factor)
+    img = rng.integers(0, 256, size=(8 * factor, 12 * factor, 3), dtype=np.uint8)
+    out = pkg.downsample_host(img, factor)
+    ref = img.reshape(8, factor, 12, factor, 3).astype(np.int64).sum(axis=(1, 3)) // (factor * factor)
+    assert np.array_equal(out, ref.astype(np.uint8))
+
+
+def test_load_errors(pkg, tmp_path):
+    with pytest.raises(pkg.RtError) as e:
+        pkg.Scene.from_xml(tmp_path / "missing.xml", host_only=True)
+    assert e.value.code == -2
+    bad = tmp_path / "bad.xml"
+    bad.write_text("<Scene><Cameras></Cameras>")   # no Lights/Materials/...
+    with pytest.raises(pkg.RtError):
+        pkg.Scene.from_xml(bad, host_only=True)
+    broken = tmp_path / "broken.xml"
+    broken.write_text("<Scene><Lights><AmbientLight>1 1 1</AmbientLight></Lights></Scene>")
+    with pytest.raises(pkg.RtError):
+        pkg.Scene.from_xml(broken, host_only=True)
+
+
+def test_invalid_ids_rejected(pkg, tmp_path):
+    x = pkg.scenes.scene_text("simple.xml").replace("<Center>8</Center>", "<Center>99</Center>")
+    p = tmp_path / "badid.xml"
+    p.write_text(x)
+    with pytest.raises(pkg.RtError):
+        pkg.Scene.from_xml(p, host_only=True)
+
+
+def test_host_only_scene_cannot_render(pkg, scene_dir):
+    s = pkg.Scene.from_xml(config_path(scene_dir, "simple.xml"), host_only=True)
+    with pytest.raises(pkg.RtError) as e:
+        s.render(s.camera(0))
+    assert e.value.code == -5
+
+
+def test_scene_create_from_desc_matches_xml(pkg, oracle, scene_dir):
+    """rt_scene_create with borrowed host arrays builds the same BVH as the XML path."""
+    import xml.etree.ElementTree as ET
+    root = ET.fromstring(pkg.scenes.scene_text("simple.xml"))
+    L = pkg.lib()
+
+    def v3(t):
+        x, y, z = (float(v) for v in t.split())
+        return pkg.Vec3f(x, y, z)
+
+    class Light(ctypes.Structure):
+        _fields_ = [("position", pkg.Vec3f), ("intensity", pkg.Vec3f)]
+
+    class Mat(ctypes.Structure):
+        _fields_ = [("is_mirror", ctypes.c_int), ("ambient", pkg.Vec3f), ("diffuse", pkg.Vec3f),
+                    ("specular", pkg.Vec3f), ("mirror", pkg.Vec3f), ("phong_exponent", ctypes.c_float)]
+
+    class Tri(ctypes.Structure):
+        _fields_ = [("material_id", ctypes.c_int), ("v0_id", ctypes.c_int), ("v1_id", ctypes.c_int),
+                    ("v2_id", ctypes.c_int)]
+
+    class Sph(ctypes.Structure):
+        _fields_ = [("material_id", ctypes.c_int), ("center_vertex_id", ctypes.c_int), ("radius", ctypes.c_float)]
+
+    class Desc(ctypes.Structure):
+        _fields_ = [("background_color", ctypes.c_int * 3), ("shadow_ray_epsilon", ctypes.c_float),
+                    ("max_recursion_depth", ctypes.c_int), ("ambient_light", pkg.Vec3f),
+                    ("lights", ctypes.POINTER(Light)), ("num_lights", ctypes.c_int),
+                    ("materials", ctypes.POINTER(Mat)), ("num_materials", ctypes.c_int),
+                    ("vertices", ctypes.POINTER(pkg.Vec3f)), ("num_vertices", ctypes.c_int),
+                    ("triangles", ctypes.POINTER(Tri)), ("num_triangles", ctypes.c_int),
+                    ("spheres", ctypes.POINTER(Sph)), ("num_spheres", ctypes.c_int)]
+
+    lights = [Light(v3(pl.find("Position").text), v3(pl.find("Intensity").text))
+              for pl in root.find("Lights").findall("PointLight")]
+    mats = [Mat(1 if m.get("type") == "mirror" else 0, v3(m.find("AmbientReflectance").text),
+                v3(m.find("DiffuseReflectance").text), v3(m.find("SpecularReflectance").text),
+                v3(m.find("MirrorReflectance").text), float(m.find("PhongExponent").text))
+            for m in root.find("Materials").findall("Material")]
+    nums = root.find("VertexData").text.split()
+    verts = [pkg.Vec3f(float(nums[i]), float(nums[i + 1]), float(nums[i + 2])) for i in range(0, len(nums), 3)]
+    objs = root.find("Objects")
+    tris = [Tri(int(t.find("Material").text), *[int(v) for v in t.find("Indices").text.split()])
+            for t in objs.findall("Triangle")]
+    for m in objs.findall("Mesh"):
+        f = [int(v) for v in m.find("Faces").text.split()]
+        tris += [Tri(int(m.find("Material").text), f[i], f[i + 1], f[i + 2]) for i in range(0, len(f), 3)]
+    sph = [Sph(int(s.find("Material").text), int(s.find("Center").text), float(s.find("Radius").text))
+           for s in objs.findall("Sphere")]
+    arr = lambda T, xs: (T * len(xs))(*xs)  # noqa: E731
+    d = Desc((ctypes.c_int * 3)(0, 0, 0), 1e-3, 6, v3(root.find("Lights").find("AmbientLight").text),
+             arr(Light, lights), len(lights), arr(Mat, mats), len(mats), arr(pkg.Vec3f, verts), len(verts),
+             arr(Tri, tris), len(tris), arr(Sph, sph), len(sph))
+    h = ctypes.c_void_p()
+    opts = pkg.Options(-1, pkg.RT_OPT_HOST_ONLY)
+    assert L.rt_scene_create(ctypes.byref(d), ctypes.byref(opts), ctypes.byref(h)) == 0, L.rt_last_error()
+    s = pkg.Scene(h.value)
+    ref = oracle.OracleScene(config_path(scene_dir, "simple.xml")).export_nodes()
+    assert s.export_nodes().tobytes() == ref.tobytes()
+    # an out-of-range vertex id is rejected with RT_ERR_ARG
+    tris[0].v0_id = 999
+    d.triangles = arr(Tri, tris)
+    h2 = ctypes.c_void_p()
+    assert L.rt_scene_create(ctypes.byref(d), ctypes.byref(opts), ctypes.byref(h2)) == -1
