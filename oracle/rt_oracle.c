@@ -640,12 +640,22 @@ typedef struct {
 } ctx_t;
 
 /* RayTracer::rayTrace (:385-452) — recursive, as the reference. */
+/* diagnostics: max node visits of a single traversal, [0]=closest [1]=shadow, by depth */
+uint32_t ro_debug_maxvisits[2][64];
+
+static void note_visits(int kind, int depth, uint64_t before, uint64_t after) {
+    uint32_t v = (uint32_t)(after - before);
+    if (depth < 64 && v > ro_debug_maxvisits[kind][depth]) ro_debug_maxvisits[kind][depth] = v; /* racy max: diagnostics only */
+}
+
 static v3 ray_trace(ctx_t* x, ray_t* ray, int depth) {
     const ro_scene* s = x->s;
     v3 color = {0, 0, 0};
     if (depth > x->max_depth) return color;                          /* :387-389 */
     if (depth > 0) x->c.reflection_rays++;
+    uint64_t nb = x->w.node;
     hit_t h = closest_hit(s, ray, &x->w);                            /* :390 */
+    note_visits(0, depth, nb, x->w.node);
     if (!h.exists) {                                                 /* :442-449 */
         if (depth > 0) return color;
         v3 bg = {(float)s->bg[0], (float)s->bg[1], (float)s->bg[2]};
@@ -662,7 +672,10 @@ static v3 ray_trace(ctx_t* x, ray_t* ray, int depth) {
         v3 ldir_real = v_norm(v_sub(L->position, v_add(ray->o, v_mul(ray->d, h.t))));
         ray_t lray = make_ray(p, ldir);
         x->c.shadow_rays++;
-        if (!any_hit(s, &lray, dist, &x->w)) {
+        uint64_t sb = x->w.node;
+        int occl = any_hit(s, &lray, dist, &x->w);
+        note_visits(1, depth, sb, x->w.node);
+        if (!occl) {
             float cos_t = v_dot(ldir_real, h.n);
             v3 E = v_div(L->intensity, dist * dist);
             float theta = (float)(acos((double)cos_t) * 180 / 3.1415);
@@ -717,6 +730,7 @@ typedef struct {
     const ro_scene* s; const ro_camera* cam; eye_t eye;
     int aa, W, row_begin, row_end, tid, T, max_depth;
     uint8_t* out;
+    uint32_t* work;   /* optional: node visits per output pixel (diagnostics) */
     ro_counters c;
 } job_t;
 
@@ -728,6 +742,7 @@ static void* render_worker(void* arg) {
     for (int orow = j->row_begin + j->tid; orow < j->row_end; orow += j->T) {
         for (int ocol = 0; ocol < W; ++ocol) {
             int sum[3] = {0, 0, 0};
+            const uint64_t nodes_before = x.w.node;
             for (int k = 0; k < F; ++k)
                 for (int l = 0; l < F; ++l) {
                     ray_t r = eye_gen(&j->eye, orow * F + k, ocol * F + l);
@@ -738,6 +753,7 @@ static void* render_worker(void* arg) {
                 }
             uint8_t* o = j->out + ((size_t)(orow - j->row_begin) * W + ocol) * 3;
             o[0] = (uint8_t)(sum[0] / (F * F)); o[1] = (uint8_t)(sum[1] / (F * F)); o[2] = (uint8_t)(sum[2] / (F * F));
+            if (j->work) j->work[(size_t)(orow - j->row_begin) * W + ocol] = (uint32_t)(x.w.node - nodes_before);
         }
     }
     free(samp);
@@ -746,8 +762,20 @@ static void* render_worker(void* arg) {
     return NULL;
 }
 
+static int render_impl(const ro_scene* s, int cam, int aa, int threads, int row_begin, int row_end,
+                       int max_depth_override, uint8_t* out, ro_counters* counters, uint32_t* work);
+
 int ro_render(const ro_scene* s, int cam, int aa, int threads, int row_begin, int row_end,
               int max_depth_override, uint8_t* out, ro_counters* counters) {
+    return render_impl(s, cam, aa, threads, row_begin, row_end, max_depth_override, out, counters, NULL);
+}
+
+int ro_work_map(const ro_scene* s, int cam, int aa, int threads, uint8_t* out, uint32_t* work) {
+    return render_impl(s, cam, aa, threads, 0, -1, -1000, out, NULL, work);
+}
+
+static int render_impl(const ro_scene* s, int cam, int aa, int threads, int row_begin, int row_end,
+                       int max_depth_override, uint8_t* out, ro_counters* counters, uint32_t* work) {
     if (!s || cam < 0 || cam >= s->ncam || aa < 1 || !out) return -1;
     const ro_camera* c = &s->cams[cam];
     if (row_begin < 0) row_begin = 0;
@@ -762,6 +790,7 @@ int ro_render(const ro_scene* s, int cam, int aa, int threads, int row_begin, in
         j->row_begin = row_begin; j->row_end = row_end; j->tid = i; j->T = threads;
         j->max_depth = max_depth_override < -999 ? s->max_depth : max_depth_override;
         j->out = out;
+        j->work = work;
         if (threads == 1) render_worker(j); else pthread_create(&th[i], NULL, render_worker, j);
     }
     ro_counters tot; memset(&tot, 0, sizeof(tot));

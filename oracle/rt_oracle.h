@@ -55,6 +55,10 @@ int ro_export_nodes(const ro_scene* s, void* out, int capacity);
 int ro_render(const ro_scene* s, int cam, int aa, int threads, int row_begin, int row_end,
               int max_depth_override, uint8_t* out, ro_counters* counters);
 
+/* Diagnostics: full-frame render that also records BVH node visits per
+ * output pixel (all samples, all bounces, shadow rays included). */
+int ro_work_map(const ro_scene* s, int cam, int aa, int threads, uint8_t* out, uint32_t* work);
+
 /* Primary closest-hit at internal resolution (W*aa x H*aa): t (tSmall, -1 on
  * miss) and material id (0 on miss). Either pointer may be NULL. */
 int ro_primary_hits(const ro_scene* s, int cam, int aa, float* t, int32_t* material);

@@ -25,6 +25,9 @@ LIB_PATH = PKG_DIR / "librt_hip.so"
 CLI_PATH = PKG_DIR / "raytracer"
 
 RT_OPT_HOST_ONLY = 1
+RT_OPT_MEGAKERNEL = 2
+RT_OPT_WAVEFRONT = 4
+PATHS = ("chain", "wavefront", "megakernel")
 RT_RENDER_COUNT = 1
 
 
@@ -138,9 +141,13 @@ class Scene:
         self._h = ctypes.c_void_p(handle)
 
     @classmethod
-    def from_xml(cls, path: str | os.PathLike, device: int = -1, host_only: bool = False) -> "Scene":
+    def from_xml(cls, path: str | os.PathLike, device: int = -1, host_only: bool = False,
+                 render_path: str = "chain") -> "Scene":
+        """render_path: "chain" (default), "wavefront" or "megakernel" (all bit-identical)."""
         h = ctypes.c_void_p()
-        opts = Options(device, RT_OPT_HOST_ONLY if host_only else 0)
+        flags = RT_OPT_HOST_ONLY if host_only else 0
+        flags |= {"chain": 0, "wavefront": RT_OPT_WAVEFRONT, "megakernel": RT_OPT_MEGAKERNEL}[render_path]
+        opts = Options(device, flags)
         _check(lib().rt_scene_load_xml(str(path).encode(), ctypes.byref(opts), ctypes.byref(h)))
         return cls(h.value)
 

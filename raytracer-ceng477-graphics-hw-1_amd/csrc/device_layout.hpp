@@ -49,6 +49,26 @@ struct alignas(16) Light {
     float ix, iy, iz, pad1;
 };
 
+// Child-pair layout ("children in parent", 64 B = one load per expansion):
+// pair p holds the boxes of BOTH children of interior node N plus N's split
+// axis, so expanding N tests both child boxes from one 64-B record and a
+// miss never costs a dependent load.  Child info word:
+//   >= 0          interior child: index of ITS child pair
+//   kLeafBit | count << 25 | start      leaf child, count in [1, 63]
+//   kLeafBit | 0 << 25 | big           leaf child with > 63 prims: LeafBig[big]
+// Leaves keep the reference's primitive order (triangles, then spheres).
+struct alignas(16) Pair {
+    float l_minx, l_miny, l_minz; int32_t l_info;    // left child  (node i+1)
+    float l_maxx, l_maxy, l_maxz; int32_t axis;      // parent's split axis
+    float r_minx, r_miny, r_minz; int32_t r_info;    // right child (rightIndex)
+    float r_maxx, r_maxy, r_maxz; int32_t pad;
+};
+struct LeafBig { int32_t start, count; };
+constexpr int kLeafCountShift = 25;
+constexpr int32_t kLeafStartMask = (1 << kLeafCountShift) - 1;
+constexpr int kLeafMaxCount = 63;
+
+static_assert(sizeof(Pair) == 64, "pair size");
 static_assert(sizeof(Node) == 32, "node size");
 static_assert(sizeof(Prim) == 48, "prim size");
 static_assert(sizeof(Material) == 64, "material size");

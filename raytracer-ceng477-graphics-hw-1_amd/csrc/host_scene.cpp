@@ -457,6 +457,37 @@ std::string build_bvh(const HostScene& s, FlatBVH& out) {
         }
     }
     (void)ibits; (void)fbits;
+
+    // Child-pair layout: one pair per interior node, numbered in pre-order.
+    std::vector<int32_t> pair_of(out.nodes.size(), -1);
+    int32_t npairs = 0;
+    for (size_t f = 0; f < out.nodes.size(); ++f)
+        if (out.nodes[f].b >= 0) pair_of[f] = npairs++;
+    auto info_of = [&](size_t f) -> int32_t {
+        const dl::Node& n = out.nodes[f];
+        if (n.b >= 0) return pair_of[f];
+        const int32_t count = (n.b & dl::kNtriMask) + ((n.b >> dl::kNtriBits) & dl::kMaxLeafSpheres);
+        if (count >= 1 && count <= dl::kLeafMaxCount && n.a <= dl::kLeafStartMask)
+            return dl::kLeafBit | (count << dl::kLeafCountShift) | n.a;
+        out.leaf_big.push_back(dl::LeafBig{n.a, count});
+        return dl::kLeafBit | (int32_t)(out.leaf_big.size() - 1);
+    };
+    out.pairs.resize(npairs);
+    for (size_t f = 0; f < out.nodes.size(); ++f) {
+        const dl::Node& n = out.nodes[f];
+        if (n.b < 0) continue;
+        const dl::Node& L = out.nodes[f + 1];
+        const dl::Node& R = out.nodes[n.a];
+        dl::Pair& p = out.pairs[pair_of[f]];
+        p.l_minx = L.minx; p.l_miny = L.miny; p.l_minz = L.minz; p.l_info = info_of(f + 1);
+        p.l_maxx = L.maxx; p.l_maxy = L.maxy; p.l_maxz = L.maxz; p.axis = n.b;
+        p.r_minx = R.minx; p.r_miny = R.miny; p.r_minz = R.minz; p.r_info = info_of(n.a);
+        p.r_maxx = R.maxx; p.r_maxy = R.maxy; p.r_maxz = R.maxz; p.pad = 0;
+    }
+    if ((int)out.leaf_big.size() > dl::kLeafStartMask) return "Error: too many large BVH leaves";
+    out.root_lo[0] = out.nodes[0].minx; out.root_lo[1] = out.nodes[0].miny; out.root_lo[2] = out.nodes[0].minz;
+    out.root_hi[0] = out.nodes[0].maxx; out.root_hi[1] = out.nodes[0].maxy; out.root_hi[2] = out.nodes[0].maxz;
+    out.root_info = info_of(0);
     // Ordered DFS pushes two children per interior pop: stack <= depth + 2.
     out.max_stack = out.max_depth + 2;
     if (out.max_stack > dl::kMaxStack) return "Error: BVH deeper than the device stack";

@@ -50,6 +50,11 @@ struct FlatBVH {
     std::vector<dl::Node> nodes;        // pre-order, left child = i + 1
     std::vector<dl::Prim> prims;        // leaf primitive copies, leaf-contiguous
     std::vector<dl::TriShade> tri_shade;  // per triangle id: normal + material
+    // child-pair layout of the same tree (device_layout.hpp dl::Pair)
+    std::vector<dl::Pair> pairs;
+    std::vector<dl::LeafBig> leaf_big;
+    float root_lo[3] = {0, 0, 0}, root_hi[3] = {0, 0, 0};
+    int32_t root_info = 0;
     int leaves = 0, max_leaf = 0, max_depth = 0, max_stack = 0;
     double build_ms = 0;
 };

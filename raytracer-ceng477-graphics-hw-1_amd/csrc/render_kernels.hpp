@@ -24,6 +24,12 @@ struct DevScene {
     float eps;            // ShadowRayEpsilon
     float bgx, bgy, bgz;  // BackgroundColor as float (raytracer.cpp:446-447)
     float cos_thr;        // smallest float c with (float)(acos(c)*180/3.1415) <= 90.01
+    // child-pair layout of the same BVH (traverse2.hpp)
+    const dl::Pair* pairs;
+    const dl::LeafBig* leaf_big;
+    float root_lo[3], root_hi[3];
+    int root_info;
+    int pair_stack;       // LDS stack entries (8 B each) for the pair traversal
 
     // Sphere prims carry ~sphere_index in p0.w (negative), triangles their id.
     __device__ __forceinline__ bool prim_is_sphere(int, const float4 p0) const {

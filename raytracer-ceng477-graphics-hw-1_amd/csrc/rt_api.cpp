@@ -4,7 +4,9 @@
 
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <chrono>
+#include <cstdlib>
 #include <cmath>
 #include <cstdio>
 #include <cstring>
@@ -14,6 +16,8 @@
 
 #include "host_scene.hpp"
 #include "render_kernels.hpp"
+#include "pathchain.hpp"
+#include "wavefront.hpp"
 #include "rt_internal.hpp"
 
 namespace {
@@ -93,8 +97,51 @@ struct rt_scene {
     uint8_t* d_out = nullptr;
     size_t out_cap = 0;
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
+    dl::Pair* d_pairs = nullptr;
+    dl::LeafBig* d_leafbig = nullptr;
+    enum Path { kChain, kWavefront, kMegakernel } path = kChain;
+    int grid_blocks = 2048;
+    // chain-path workspace (grown on demand)
+    struct {
+        int cap = 0, levels = 0, nlights = 0;
+        float4* rec = nullptr;
+        int* pinfo = nullptr;
+        float4* sray = nullptr;
+        uint8_t* occ = nullptr;
+        unsigned* scount = nullptr;
+        unsigned scap = 0;
+    } cw;
+
+    void free_cw() {
+        (void)hipFree(cw.rec); (void)hipFree(cw.pinfo); (void)hipFree(cw.sray); (void)hipFree(cw.occ);
+        (void)hipFree(cw.scount);
+        cw.rec = cw.sray = nullptr; cw.pinfo = nullptr; cw.occ = nullptr; cw.scount = nullptr;
+        cw.cap = cw.levels = cw.nlights = 0; cw.scap = 0;
+    }
+    // wavefront workspace (grown on demand)
+    struct {
+        int cap = 0, levels = 0, nlights = 0;
+        float4* q[2] = {nullptr, nullptr};
+        float4* hit = nullptr;
+        float4* sray = nullptr;
+        uint8_t* occ = nullptr;
+        float4* R = nullptr;
+        int* child = nullptr;
+        unsigned* counts = nullptr;
+        size_t bytes = 0;
+    } ws;
+
+    void free_ws() {
+        (void)hipFree(ws.q[0]); (void)hipFree(ws.q[1]); (void)hipFree(ws.hit); (void)hipFree(ws.sray);
+        (void)hipFree(ws.occ); (void)hipFree(ws.R); (void)hipFree(ws.child); (void)hipFree(ws.counts);
+        ws.q[0] = ws.q[1] = nullptr; ws.hit = ws.sray = ws.R = nullptr; ws.occ = nullptr; ws.child = nullptr;
+        ws.counts = nullptr; ws.cap = ws.levels = ws.nlights = 0; ws.bytes = 0;
+    }
 
     ~rt_scene() {
+        free_ws();
+        free_cw();
+        (void)hipFree(d_pairs); (void)hipFree(d_leafbig);
         (void)hipFree(d_nodes); (void)hipFree(d_prims); (void)hipFree(d_tri); (void)hipFree(d_mats); (void)hipFree(d_lights);
         (void)hipFree(d_counters); (void)hipFree(d_out);
         if (ev0) (void)hipEventDestroy(ev0);
@@ -146,10 +193,27 @@ int finish_scene(rt_scene* s, const rt_options* opts) {
     if ((rc = upload(&s->d_tri, s->bvh.tri_shade))) return rc;
     if ((rc = upload(&s->d_mats, mats))) return rc;
     if ((rc = upload(&s->d_lights, lights))) return rc;
+    if ((rc = upload(&s->d_pairs, s->bvh.pairs))) return rc;
+    if ((rc = upload(&s->d_leafbig, s->bvh.leaf_big))) return rc;
     HIP_TRY(hipMalloc(reinterpret_cast<void**>(&s->d_counters), 8 * sizeof(unsigned long long)));
     HIP_TRY(hipMemset(s->d_counters, 0, 8 * sizeof(unsigned long long)));
     HIP_TRY(hipEventCreate(&s->ev0));
     HIP_TRY(hipEventCreate(&s->ev1));
+
+    {
+        hipDeviceProp_t prop;
+        HIP_TRY(hipGetDeviceProperties(&prop, s->device));
+        s->grid_blocks = std::max(1, prop.multiProcessorCount) * 8;
+    }
+    s->path = rt_scene::kChain;
+    if (opts && (opts->flags & RT_OPT_WAVEFRONT)) s->path = rt_scene::kWavefront;
+    if (opts && (opts->flags & RT_OPT_MEGAKERNEL)) s->path = rt_scene::kMegakernel;
+    if (const char* e = std::getenv("RT_PATH")) {
+        const std::string v(e);
+        if (v == "mega") s->path = rt_scene::kMegakernel;
+        else if (v == "wave") s->path = rt_scene::kWavefront;
+        else if (v == "chain") s->path = rt_scene::kChain;
+    }
 
     rtk::DevScene& d = s->dev;
     d.nodes = s->d_nodes; d.prims = s->d_prims; d.tri_shade = s->d_tri; d.mats = s->d_mats; d.lights = s->d_lights;
@@ -160,6 +224,14 @@ int finish_scene(rt_scene* s, const rt_options* opts) {
     d.eps = s->host.eps;
     d.bgx = (float)s->host.bg[0]; d.bgy = (float)s->host.bg[1]; d.bgz = (float)s->host.bg[2];
     d.cos_thr = cos_threshold();
+    d.pairs = s->d_pairs;
+    d.leaf_big = s->d_leafbig;
+    for (int i = 0; i < 3; ++i) {
+        d.root_lo[i] = s->bvh.root_lo[i];
+        d.root_hi[i] = s->bvh.root_hi[i];
+    }
+    d.root_info = s->bvh.root_info;
+    d.pair_stack = std::max(2, s->bvh.max_stack);
     return RT_OK;
 }
 
@@ -192,6 +264,119 @@ int check_camera(const rt_camera* cam, int aa) {
     if (cam->image_width < 1 || cam->image_height < 1) return fail(RT_ERR_ARG, "empty image");
     const long long iw = (long long)cam->image_width * aa, ih = (long long)cam->image_height * aa;
     if (iw > (1 << 24) || ih > (1 << 24)) return fail(RT_ERR_ARG, "internal resolution too large");
+    return RT_OK;
+}
+
+constexpr size_t kTargetSamples = size_t(8) << 20;   // level-0 samples per chunk
+
+template <typename T>
+int alloc_dev(T** p, size_t n) {
+    HIP_TRY(hipMalloc(reinterpret_cast<void**>(p), std::max<size_t>(n, 1) * sizeof(T)));
+    return RT_OK;
+}
+
+int ensure_workspace(rt_scene* s, int cap, int levels, int nlights) {
+    auto& w = s->ws;
+    if (w.cap >= cap && w.levels >= levels && w.nlights >= nlights) return RT_OK;
+    cap = std::max(cap, w.cap);
+    levels = std::max(levels, w.levels);
+    nlights = std::max(nlights, std::max(1, w.nlights));
+    s->free_ws();
+    const size_t c = (size_t)cap;
+    int rc;
+    if ((rc = alloc_dev(&w.q[0], 2 * c)) || (rc = alloc_dev(&w.q[1], 2 * c)) || (rc = alloc_dev(&w.hit, 2 * c)) ||
+        (rc = alloc_dev(&w.sray, 2 * c * nlights)) || (rc = alloc_dev(&w.occ, c * nlights)) ||
+        (rc = alloc_dev(&w.R, c * levels)) || (rc = alloc_dev(&w.child, c * levels)) ||
+        (rc = alloc_dev(&w.counts, 2 * (size_t)levels + 2))) {
+        s->free_ws();
+        return rc;
+    }
+    w.cap = cap; w.levels = levels; w.nlights = nlights;
+    w.bytes = c * (32 * 3 + 32 * nlights + nlights + 20 * levels);
+    return RT_OK;
+}
+
+// Chunked wavefront frame: chunks are whole groups of 8*aa slab-local
+// internal rows (whole output rows, whole 8x8 tiles).
+int render_wavefront(rt_scene* s, const rtk::Eye& eye, const rtk::FrameParams& f, bool count, hipStream_t st) {
+    const int levels = std::max(s->dev.max_depth, 0) + 1;
+    const int nl = std::max(s->dev.nlights, 1);
+    const int wi = f.width * f.aa;
+    const int tiles_x = (wi + 7) / 8;
+    const int li = f.slab_rows * f.aa;                           // slab-local internal rows
+    const int unit = 8 * f.aa;                                   // rows per chunk unit
+    const size_t unit_samples = (size_t)tiles_x * f.aa * 64;
+    const size_t units_total = (size_t)(li + unit - 1) / unit;
+    size_t units = std::max<size_t>(1, kTargetSamples / unit_samples);
+    units = std::min(units, units_total);
+    const int chunk_rows = (int)units * unit;
+    const size_t cap = units * unit_samples;
+    if (cap * nl >= (size_t)INT32_MAX) return fail(RT_ERR_LIMIT, "frame chunk too large for the wavefront path");
+    int rc = ensure_workspace(s, (int)cap, levels, nl);
+    if (rc) return rc;
+    rtw::WfParams p;
+    p.width = f.width; p.height = f.height; p.aa = f.aa; p.stripe_rows = f.stripe_rows;
+    p.rank = f.rank; p.nranks = f.nranks; p.slab_rows = f.slab_rows;
+    p.wi = wi; p.tiles_x = tiles_x; p.cap = s->ws.cap; p.nlights = s->dev.nlights;
+    p.q[0] = s->ws.q[0]; p.q[1] = s->ws.q[1]; p.hit = s->ws.hit; p.sray = s->ws.sray; p.occ = s->ws.occ;
+    p.R = s->ws.R; p.child = s->ws.child;
+    p.qcount = s->ws.counts; p.scount = s->ws.counts + levels + 1;
+    p.out = f.out; p.counters = f.counters;
+    for (int r0 = 0; r0 < li; r0 += chunk_rows) {
+        p.chunk_row0 = r0;
+        p.chunk_rows = std::min(chunk_rows, li - r0);
+        p.n0 = tiles_x * ((p.chunk_rows + 7) / 8) * 64;
+        HIP_TRY(rtw::launch_frame_chunk(s->dev, eye, p, s->grid_blocks, count, st));
+    }
+    return RT_OK;
+}
+
+// Chain path: chunks of whole 8*aa-row groups, workspace sized for the worst
+// case (every sample recording every level) so no queue can overflow.
+constexpr size_t kChainTargetSamples = size_t(4) << 20;
+constexpr size_t kChainBudgetBytes = size_t(6) << 30;
+
+int render_chain(rt_scene* s, const rtk::Eye& eye, const rtk::FrameParams& f, bool count, hipStream_t st) {
+    const int levels = std::max(s->dev.max_depth, 0) + 1;
+    const int nl = std::max(s->dev.nlights, 1);
+    const int wi = f.width * f.aa;
+    const int tiles_x = (wi + 7) / 8;
+    const int li = f.slab_rows * f.aa;
+    const int unit = 8 * f.aa;
+    const size_t unit_samples = (size_t)tiles_x * f.aa * 64;
+    const size_t units_total = (size_t)(li + unit - 1) / unit;
+    const size_t per_sample = (size_t)levels * (48 + 32 * nl + nl) + 4;
+    const size_t target = std::max<size_t>(unit_samples, std::min(kChainTargetSamples, kChainBudgetBytes / per_sample));
+    const size_t units = std::min(units_total, std::max<size_t>(1, target / unit_samples));
+    const int chunk_rows = (int)units * unit;
+    const size_t cap = units * unit_samples;
+    if (cap * levels * nl >= (size_t)INT32_MAX) return fail(RT_ERR_LIMIT, "frame chunk too large for the chain path");
+    auto& w = s->cw;
+    if (w.cap < (int)cap || w.levels < levels || w.nlights < nl) {
+        const int ncap = std::max<int>(w.cap, (int)cap), nlev = std::max(w.levels, levels),
+                  nnl = std::max(w.nlights, nl);
+        s->free_cw();
+        const size_t c = (size_t)ncap, rl = c * nlev;
+        int rc;
+        if ((rc = alloc_dev(&w.rec, 3 * rl)) || (rc = alloc_dev(&w.pinfo, c)) || (rc = alloc_dev(&w.sray, 2 * rl * nnl)) ||
+            (rc = alloc_dev(&w.occ, rl * nnl)) || (rc = alloc_dev(&w.scount, 1))) {
+            s->free_cw();
+            return rc;
+        }
+        w.cap = ncap; w.levels = nlev; w.nlights = nnl; w.scap = (unsigned)(rl * nnl);
+    }
+    rtc::PcParams p;
+    p.width = f.width; p.height = f.height; p.aa = f.aa; p.stripe_rows = f.stripe_rows;
+    p.rank = f.rank; p.nranks = f.nranks; p.slab_rows = f.slab_rows;
+    p.wi = wi; p.tiles_x = tiles_x; p.cap = w.cap; p.levels = levels; p.nlights = s->dev.nlights;
+    p.rec = w.rec; p.pinfo = w.pinfo; p.sray = w.sray; p.occ = w.occ; p.scount = w.scount; p.scap = w.scap;
+    p.out = f.out; p.counters = f.counters;
+    for (int r0 = 0; r0 < li; r0 += chunk_rows) {
+        p.chunk_row0 = r0;
+        p.chunk_rows = std::min(chunk_rows, li - r0);
+        p.n0 = tiles_x * ((p.chunk_rows + 7) / 8) * 64;
+        HIP_TRY(rtc::launch_chain_chunk(s->dev, eye, p, s->grid_blocks, count, st));
+    }
     return RT_OK;
 }
 
@@ -345,8 +530,13 @@ int rt_render_device(rt_scene* s, const rt_camera* cam, int aa, int stripe_rows,
     p.slab_rows = rt_slab_rows(cam->image_height, stripe_rows, nranks);
     p.out = static_cast<uint8_t*>(out_dev);
     p.counters = s->d_counters;
-    HIP_TRY(rtk::launch_render(s->dev, eye, p, (flags & RT_RENDER_COUNT) != 0, static_cast<hipStream_t>(stream)));
-    return RT_OK;
+    const bool count = (flags & RT_RENDER_COUNT) != 0;
+    if (s->path == rt_scene::kMegakernel) {
+        HIP_TRY(rtk::launch_render(s->dev, eye, p, count, static_cast<hipStream_t>(stream)));
+        return RT_OK;
+    }
+    if (s->path == rt_scene::kWavefront) return render_wavefront(s, eye, p, count, static_cast<hipStream_t>(stream));
+    return render_chain(s, eye, p, count, static_cast<hipStream_t>(stream));
 }
 
 int rt_unshuffle_stripes(const void* slabs, void* image, int width, int height, int stripe_rows, int nranks,

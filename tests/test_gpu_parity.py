@@ -37,10 +37,11 @@ def _stats(s):
             s["sphere_tests"])
 
 
+@pytest.mark.parametrize("path", ["chain", "wavefront", "megakernel"])
 @pytest.mark.parametrize("name", CPU_GOLDENS)
-def test_render_bit_exact(name, goldens, pkg, scene_dir, torch_cuda):
+def test_render_bit_exact(name, path, goldens, pkg, scene_dir, torch_cuda):
     g = golden_by_name(goldens, name)
-    with pkg.Scene.from_xml(config_path(scene_dir, g["config"]), device=0) as s:
+    with pkg.Scene.from_xml(config_path(scene_dir, g["config"]), device=0, render_path=path) as s:
         cams = s.cameras()
         for cam in g["cameras"]:
             c, _ = cams[cam["camera"]]
@@ -70,13 +71,17 @@ def test_primary_hit_t(name, goldens, pkg, scene_dir, torch_cuda):
     assert hashlib.sha256(fm.tobytes()).hexdigest() == g["primary_hits"]["sha256_material"]
 
 
-@pytest.mark.parametrize("nranks,stripe", [(2, 8), (3, 8), (8, 8), (4, 5)])
-def test_stripes_unshuffle_equals_full_frame(nranks, stripe, goldens, pkg, scene_dir, torch_cuda):
+@pytest.mark.parametrize("path", ["chain", "wavefront", "megakernel"])
+@pytest.mark.parametrize("nranks,stripe,gname", [(2, 8, "C3_hm_1080p_d6_aa1"), (3, 8, "C3_hm_1080p_d6_aa1"),
+                                                 (8, 8, "C3_hm_1080p_d6_aa1"), (4, 5, "C3_hm_1080p_d6_aa1"),
+                                                 (3, 8, "C3_hm_1080p_d6_aa2")])
+def test_stripes_unshuffle_equals_full_frame(nranks, stripe, gname, path, goldens, pkg, scene_dir, torch_cuda):
     """The multi-GPU partition rendered rank by rank on one GPU + device unshuffle."""
     torch = torch_cuda
-    g = golden_by_name(goldens, "C3_hm_1080p_d6_aa1")
+    g = golden_by_name(goldens, gname)
     ref = load_golden_image(g["cameras"][0])
-    with pkg.Scene.from_xml(config_path(scene_dir, g["config"]), device=0) as s:
+    aa = g["aa"]
+    with pkg.Scene.from_xml(config_path(scene_dir, g["config"]), device=0, render_path=path) as s:
         cam = s.camera(0)
         W, H = cam.image_width, cam.image_height
         rows = pkg.slab_rows(H, stripe, nranks)
@@ -84,7 +89,7 @@ def test_stripes_unshuffle_equals_full_frame(nranks, stripe, goldens, pkg, scene
         slabs = torch.zeros((nranks, rows, W, 3), dtype=torch.uint8, device="cuda:0")
         stream = torch.cuda.current_stream().cuda_stream
         for r in range(nranks):
-            s.render_device(cam, 1, slabs[r].data_ptr(), stream, stripe_rows=stripe, rank=r, nranks=nranks)
+            s.render_device(cam, aa, slabs[r].data_ptr(), stream, stripe_rows=stripe, rank=r, nranks=nranks)
         img = torch.empty((H, W, 3), dtype=torch.uint8, device="cuda:0")
         pkg.unshuffle_stripes(slabs.data_ptr(), img.data_ptr(), W, H, stripe, nranks, stream)
         torch.cuda.synchronize()
@@ -94,11 +99,12 @@ def test_stripes_unshuffle_equals_full_frame(nranks, stripe, goldens, pkg, scene
         assert np.array_equal(pkg.stripes.unshuffle(slabs.cpu().numpy(), H, stripe), ref)
 
 
-def test_device_counters_accumulate(goldens, pkg, scene_dir, torch_cuda):
+@pytest.mark.parametrize("path", ["chain", "wavefront", "megakernel"])
+def test_device_counters_accumulate(path, goldens, pkg, scene_dir, torch_cuda):
     torch = torch_cuda
     g = golden_by_name(goldens, "C2_cornellbox_800_d0_aa1")
     cam_g = g["cameras"][0]
-    with pkg.Scene.from_xml(config_path(scene_dir, g["config"]), device=0) as s:
+    with pkg.Scene.from_xml(config_path(scene_dir, g["config"]), device=0, render_path=path) as s:
         cam = s.camera(0)
         out = torch.empty((cam.image_height, cam.image_width, 3), dtype=torch.uint8, device="cuda:0")
         stream = torch.cuda.current_stream().cuda_stream
@@ -119,7 +125,8 @@ def test_max_depth_override_matches_derived_scene(goldens, pkg, scene_dir, torch
     assert np.array_equal(img, load_golden_image(g["cameras"][0]))
 
 
-def test_edge_scenes_vs_oracle(pkg, oracle, tmp_path, torch_cuda):
+@pytest.mark.parametrize("path", ["chain", "wavefront", "megakernel"])
+def test_edge_scenes_vs_oracle(path, pkg, oracle, tmp_path, torch_cuda):
     """Empty object list (all background), negative depth (all black), odd sizes, AA 5."""
     base = pkg.scenes.scene_text("simple.xml")
     empty = base.split("<Objects>")[0] + "<Objects>\n</Objects>\n</Scene>\n"
@@ -135,7 +142,7 @@ def test_edge_scenes_vs_oracle(pkg, oracle, tmp_path, torch_cuda):
                                  '<BackgroundColor>7 200 31</BackgroundColor>'))
         aa = 5 if name == "odd_aa5" else 1
         ref, _ = oracle.OracleScene(p).render(0, aa=aa)
-        with pkg.Scene.from_xml(p, device=0) as s:
+        with pkg.Scene.from_xml(p, device=0, render_path=path) as s:
             img, _ = s.render(s.camera(0), aa=aa)
         assert np.array_equal(img, ref), name
 
@@ -151,12 +158,13 @@ def test_bad_arguments_fail_loudly(pkg, scene_dir, torch_cuda):
             s.render_device(cam, 1, 1 << 20, stripe_rows=8, rank=3, nranks=2)
 
 
+@pytest.mark.parametrize("path", ["chain", "wavefront", "megakernel"])
 @pytest.mark.parametrize("name", ["C5_hm_8k_d6_aa4"])
-def test_full_size_c5_sha(name, goldens, pkg, scene_dir, torch_cuda):
+def test_full_size_c5_sha(name, path, goldens, pkg, scene_dir, torch_cuda):
     """BASELINE config 5 at full size (7680x4320, 16 spp): sha256 of the RGB bytes."""
     g = golden_by_name(goldens, name)
     cam_g = g["cameras"][0]
-    with pkg.Scene.from_xml(config_path(scene_dir, g["config"]), device=0) as s:
+    with pkg.Scene.from_xml(config_path(scene_dir, g["config"]), device=0, render_path=path) as s:
         img, st = s.render(s.camera(0), aa=4, stats=True)
     assert hashlib.sha256(img.tobytes()).hexdigest() == cam_g["sha256_rgb"]
     assert _stats(st) == _counters(cam_g["counters"])
