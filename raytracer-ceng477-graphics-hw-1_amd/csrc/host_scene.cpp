@@ -458,11 +458,32 @@ std::string build_bvh(const HostScene& s, FlatBVH& out) {
     }
     (void)ibits; (void)fbits;
 
-    // Child-pair layout: one pair per interior node, numbered in pre-order.
+    // Child-pair layout: one pair per interior node.  The top levels (every
+    // walk passes through them) are numbered first, breadth-first, so a
+    // kernel can cache pairs [0, top_pairs) in LDS; the rest follow in
+    // pre-order, which keeps a node's left-child pair next to its own.
     std::vector<int32_t> pair_of(out.nodes.size(), -1);
     int32_t npairs = 0;
-    for (size_t f = 0; f < out.nodes.size(); ++f)
-        if (out.nodes[f].b >= 0) pair_of[f] = npairs++;
+    {
+        std::vector<int> depth(out.nodes.size(), 0);
+        std::vector<int> per_level(64, 0);
+        for (size_t f = 0; f < out.nodes.size(); ++f) {
+            const dl::Node& n = out.nodes[f];
+            if (n.b < 0) continue;
+            per_level[std::min(depth[f], 63)]++;
+            depth[f + 1] = depth[f] + 1;
+            depth[n.a] = depth[f] + 1;
+        }
+        int top_levels = 0, top_count = 0;
+        while (top_levels < 63 && top_count + per_level[top_levels] <= dl::kTopPairs && per_level[top_levels] > 0)
+            top_count += per_level[top_levels++];
+        for (int lvl = 0; lvl < top_levels; ++lvl)
+            for (size_t f = 0; f < out.nodes.size(); ++f)
+                if (out.nodes[f].b >= 0 && depth[f] == lvl) pair_of[f] = npairs++;
+        out.top_pairs = npairs;
+        for (size_t f = 0; f < out.nodes.size(); ++f)
+            if (out.nodes[f].b >= 0 && pair_of[f] < 0) pair_of[f] = npairs++;
+    }
     auto info_of = [&](size_t f) -> int32_t {
         const dl::Node& n = out.nodes[f];
         if (n.b >= 0) return pair_of[f];

@@ -55,6 +55,7 @@ struct FlatBVH {
     std::vector<dl::LeafBig> leaf_big;
     float root_lo[3] = {0, 0, 0}, root_hi[3] = {0, 0, 0};
     int32_t root_info = 0;
+    int top_pairs = 0;               // pairs [0, top_pairs) = the top levels, breadth-first
     int leaves = 0, max_leaf = 0, max_depth = 0, max_stack = 0;
     double build_ms = 0;
 };

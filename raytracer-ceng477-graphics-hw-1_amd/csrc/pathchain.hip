@@ -1,4 +1,25 @@
 // Chain renderer kernels (see pathchain.hpp).
+//
+// Work distribution without global atomics.  A single device-scope counter
+// saturates at ~88 grabs/us on MI355X (MI355X_MICROARCH.md, "dequeue"), i.e.
+// ~0.4 ms per frame for the ~32 K sample grabs plus ~60 K shadow-queue appends
+// of a 1080p frame.  Instead every workgroup of the persistent grid owns a
+// fixed, interleaved set of 256-sample units (unit u -> block u mod G) and a
+// private region of the shadow-ray queue; lanes take samples and queue slots
+// through LDS atomics (one per wave per refill).  k_occlude's block b walks
+// the rays of region b.
+//
+// Lanes of a wave refill together once at most PcParams.refill of them are
+// still walking (refill = 0: a wave takes new samples only when all its lanes
+// are done; coherence of the 8x8 tiles is kept).
+//
+// Memory behaviour (rocprofv3, C3 frame): the walks are bound by vector-L1
+// miss handling (TCP_PENDING_STALL ~50 % of cycles, ~330-cycle L2 latency).
+// Hence: the top BVH levels (which every walk crosses) are read from an LDS
+// copy; the traversal stack keeps its first entries in LDS; streaming records
+// (shadow rays, hit records) use non-temporal accesses; shadow rays are
+// queued light-major within each wave, so a wave of k_occlude walks rays
+// toward one light from neighbouring surface points.
 #include <hip/hip_runtime.h>
 
 #include "pathchain.hpp"
@@ -12,72 +33,200 @@ namespace rtc {
 namespace {
 
 constexpr int kBlock = 256;
+constexpr int kLdsStack = 8;     // stack entries kept in LDS (deeper ones in private memory)
+
+enum LaneState : int { kIdle = 0, kTrav = 1, kDone = 2 };
+
+// LDS, named directly so every access is a ds_read/ds_write (a generic
+// pointer to them would compile to flat loads that wait on vmcnt + lgkmcnt).
+__shared__ float4 g_top[4 * dl::kTopPairs];   // top BVH pairs, 16 KiB
+__shared__ int2 g_stk[kLdsStack * kBlock];     // first stack entries, [entry][thread], 16 KiB
+__shared__ unsigned g_head;                    // block-local work queue head
+__shared__ unsigned g_scnt;                    // block-local shadow-ray count (hit lanes)
+
+struct FetchTop {
+    __device__ static __forceinline__ void pair(const rtk::DevScene& s, int p, float4& l0, float4& l1, float4& r0,
+                                                float4& r1) {
+        if (p < s.top_pairs) {
+            l0 = g_top[4 * p]; l1 = g_top[4 * p + 1]; r0 = g_top[4 * p + 2]; r1 = g_top[4 * p + 3];
+        } else {
+            FetchGlobal::pair(s, p, l0, l1, r0, r1);
+        }
+    }
+};
+
+struct StackTwoTier {        // entries [0, kLdsStack) in LDS, deeper ones private
+    int2 deep[dl::kMaxStack - kLdsStack];
+    __device__ __forceinline__ void put(int i, int2 v) {
+        if (i < kLdsStack) g_stk[i * kBlock + threadIdx.x] = v;
+        else deep[i - kLdsStack] = v;
+    }
+    __device__ __forceinline__ int2 at(int i) const {
+        if (i < kLdsStack) return g_stk[i * kBlock + threadIdx.x];
+        return deep[i - kLdsStack];
+    }
+};
+
+template <bool PRIV>
+struct StackSel {
+    using type = StackTwoTier;
+};
+template <>
+struct StackSel<true> {
+    using type = StackPriv;
+};
+
+__device__ __forceinline__ void block_init(const rtk::DevScene& s) {
+    if (threadIdx.x == 0) {
+        g_head = 0;
+        g_scnt = 0;
+    }
+    const float4* src = reinterpret_cast<const float4*>(s.pairs);
+    for (int i = threadIdx.x; i < 4 * s.top_pairs; i += kBlock) g_top[i] = src[i];
+    __syncthreads();
+}
+
+__device__ __forceinline__ unsigned lane_rank(unsigned long long mask) {
+    const int lane = threadIdx.x & 63;
+    return (unsigned)__popcll(mask & ((1ull << lane) - 1ull));
+}
+
+// One LDS atomic per wave: popc(mask) consecutive indices from *ctr.
+__device__ __forceinline__ unsigned wave_grab_lds(unsigned* ctr, unsigned long long mask) {
+    const int lane = threadIdx.x & 63;
+    const int leader = __ffsll((unsigned long long)mask) - 1;
+    unsigned base = 0;
+    if (lane == leader) base = atomicAdd(ctr, (unsigned)__popcll(mask));
+    return __shfl(base, leader, 64);
+}
+
+typedef float nt4 __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ void st_nt(float4* p, float4 v) {
+    const nt4 x = {v.x, v.y, v.z, v.w};
+    __builtin_nontemporal_store(x, reinterpret_cast<nt4*>(p));
+}
+__device__ __forceinline__ float4 ld_nt(const float4* p) {
+    const nt4 x = __builtin_nontemporal_load(reinterpret_cast<const nt4*>(p));
+    return make_float4(x.x, x.y, x.z, x.w);
+}
+
+// Block b's samples: units b, b+G, b+2G, ... of 256 consecutive slots.
+__device__ __forceinline__ unsigned block_samples(unsigned n0, unsigned G) {
+    const unsigned units = (n0 + 255u) / 256u;
+    if (blockIdx.x >= units) return 0;
+    const unsigned mine = (units - 1u - blockIdx.x) / G + 1u;
+    const unsigned last_unit = blockIdx.x + (mine - 1u) * G;
+    return (mine - 1u) * 256u + min(256u, n0 - last_unit * 256u);
+}
+__device__ __forceinline__ unsigned block_sample(unsigned v, unsigned G) {
+    return (blockIdx.x + (v >> 8) * G) * 256u + (v & 255u);
+}
 
 // ---------------------------------------------------------------------------
 // k_chain: closest-hit chain of every sample (raytracer.cpp:385-439 minus the
 // shading): record each hit, queue its shadow rays, follow mirrors.
 // ---------------------------------------------------------------------------
-template <bool COUNT>
+template <bool COUNT, bool PRIV>
 __global__ __launch_bounds__(kBlock) void k_chain(rtk::DevScene s, rtk::Eye e, PcParams p) {
-    extern __shared__ int2 stk_lds[];
-    int2* stk = stk_lds + threadIdx.x;
+    block_init(s);
+    typename StackSel<PRIV>::type stk;
     Work w;
     uint32_t nprim = 0, nrefl = 0;
-    const unsigned n = (unsigned)p.n0;
+    const unsigned G = gridDim.x;
+    const unsigned nb = block_samples((unsigned)p.n0, G);
     const int nl = s.nlights;
-    for (unsigned i0 = blockIdx.x * kBlock; i0 < n; i0 += gridDim.x * kBlock) {
-        const unsigned path = i0 + threadIdx.x;
-        Ray r;
-        const bool valid = path < n && slab_sample_ray(e, p, path, &r);
-        int nlev = 0, kind = kEndZero;
-        if (valid) {
-            nprim++;
-            for (int k = 0; k <= s.max_depth; ++k) {                        // :387-389
-                if (k > 0) nrefl++;
-                const HitRec h = closest_hit2<COUNT, kBlock>(s, r, stk, w);  // :390
-                if (h.prim < 0) {                                          // :442-449
-                    kind = k == 0 ? kEndBg : kEndZero;
-                    break;
-                }
-                V nn;
-                int mat;
+    float4* sray = p.sray + 2 * (size_t)blockIdx.x * p.block_scap;
+    int st = kIdle;
+    bool exhausted = nb == 0;
+    unsigned path = 0;
+    int k = 0;
+    Ray r;
+    Walk wk;
+    while (true) {
+        // (1) epilogue of finished walks: record, queue shadow rays, reflect
+        if (st == kDone) {
+            const HitRec h = wk.best;
+            const bool hit = h.prim >= 0;
+            V nn{0.0f, 0.0f, 0.0f}, hitp{0.0f, 0.0f, 0.0f}, pnt{0.0f, 0.0f, 0.0f};
+            int mat = 0;
+            if (hit) {
                 hit_surface(s, r, h, &nn, &mat);
-                const V hitp = add(r.o, mul(r.d, h.t));
+                hitp = add(r.o, mul(r.d, h.t));
                 float4* rc = p.rec + ((size_t)k * p.cap + path) * 3;
-                rc[0] = make_float4(hitp.x, hitp.y, hitp.z, __int_as_float(mat));
-                rc[1] = make_float4(nn.x, nn.y, nn.z, h.t);
-                rc[2] = make_float4(r.d.x, r.d.y, r.d.z, 0.0f);
-                nlev = k + 1;
-                const V pnt = add(hitp, mul(nn, s.eps));                    // :397
-                // one shadow ray per light (:399-404), traced by k_occlude
-                const unsigned slot = atomicAdd(p.scount, (unsigned)nl);
+                st_nt(rc + 0, make_float4(hitp.x, hitp.y, hitp.z, __int_as_float(mat)));
+                st_nt(rc + 1, make_float4(nn.x, nn.y, nn.z, h.t));
+                st_nt(rc + 2, make_float4(r.d.x, r.d.y, r.d.z, 0.0f));
+                pnt = add(hitp, mul(nn, s.eps));                                 // :397
+            }
+            // one shadow ray per light (:399-404), light-major within the wave
+            const unsigned long long hm = __ballot(hit);
+            if (hit) {
+                const unsigned cnt = (unsigned)__popcll(hm);
+                const unsigned base = wave_grab_lds(&g_scnt, hm);
+                const unsigned rank = lane_rank(hm);
                 for (int l = 0; l < nl; ++l) {
                     const float4 lp = ld4(&s.lights[l].px);
                     const V lpos{lp.x, lp.y, lp.z};
                     const float dist = len(sub(lpos, pnt));
                     const V ldir = nrm(sub(lpos, pnt));
                     const int owner = (int)(((size_t)k * p.cap + path) * nl + l);
-                    if (slot + l < p.scap) {
-                        p.sray[2 * (slot + l)] = make_float4(pnt.x, pnt.y, pnt.z, __int_as_float(owner));
-                        p.sray[2 * (slot + l) + 1] = make_float4(ldir.x, ldir.y, ldir.z, dist);
-                    }
+                    const unsigned slot = base * nl + l * cnt + rank;
+                    st_nt(sray + 2 * slot, make_float4(pnt.x, pnt.y, pnt.z, __int_as_float(owner)));
+                    st_nt(sray + 2 * slot + 1, make_float4(ldir.x, ldir.y, ldir.z, dist));
                 }
-                if (!s.mats[mat - 1].is_mirror) {
-                    kind = kEndLast;
-                    break;
-                }
-                if (k >= s.max_depth) {            // child would be beyond MaxRecursionDepth: 0
-                    kind = kEndZero;
-                    break;
-                }
-                const V d2 = nrm(r.d);                                     // :431-435
+            }
+            if (!hit) {                                                          // :442-449
+                p.pinfo[path] = k | ((k == 0 ? kEndBg : kEndZero) << 8);
+                st = kIdle;
+            } else if (!s.mats[mat - 1].is_mirror) {
+                p.pinfo[path] = (k + 1) | (kEndLast << 8);
+                st = kIdle;
+            } else if (k >= s.max_depth) {        // child beyond MaxRecursionDepth: 0 (:387-389)
+                p.pinfo[path] = (k + 1) | (kEndZero << 8);
+                st = kIdle;
+            } else {
+                const V d2 = nrm(r.d);                                         // :431-435
                 const V n2 = nrm(nn);
                 const float rcos = dot(neg(d2), n2);
                 r = make_ray(pnt, add(d2, mul(mul(n2, 2.0f), rcos)));
+                ++k;
+                nrefl++;
+                st = walk_begin<COUNT>(s, r, wk, w) ? kTrav : kDone;
             }
         }
-        if (path < n) p.pinfo[path] = nlev | (kind << 8);
+        // (2) refill idle lanes with this block's next samples
+        if (!exhausted) {
+            const unsigned long long idle = __ballot(st == kIdle);
+            if (idle) {
+                const unsigned base = wave_grab_lds(&g_head, idle);
+                if (base + (unsigned)__popcll(idle) >= nb) exhausted = true;
+                if (st == kIdle) {
+                    const unsigned v = base + lane_rank(idle);
+                    if (v < nb) {
+                        const unsigned idx = block_sample(v, G);
+                        if (slab_sample_ray(e, p, idx, &r)) {
+                            path = idx;
+                            k = 0;
+                            nprim++;
+                            if (s.max_depth < 0) p.pinfo[path] = 0 | (kEndZero << 8);   // depth 0 > max: black
+                            else st = walk_begin<COUNT>(s, r, wk, w) ? kTrav : kDone;
+                        }
+                    }
+                }
+            }
+        }
+        if (!__any(st != kIdle)) {
+            if (exhausted) break;
+            continue;
+        }
+        // (3) walk until enough lanes need service
+        const int thresh = exhausted ? 0 : p.refill;
+        while (__popcll(__ballot(st == kTrav)) > thresh) {
+            if (st == kTrav && closest_step<COUNT, FetchTop>(s, r, stk, wk, w)) st = kDone;
+        }
     }
+    __syncthreads();
+    if (threadIdx.x == 0) p.bcount[blockIdx.x] = g_scnt * (unsigned)nl;
     if (COUNT) {
         wave_add_counter(&p.counters[0], nprim);
         wave_add_counter(&p.counters[2], nrefl);
@@ -88,20 +237,102 @@ __global__ __launch_bounds__(kBlock) void k_chain(rtk::DevScene s, rtk::Eye e, P
 }
 
 // ---------------------------------------------------------------------------
-// k_occlude: any-hit of every queued shadow ray (raytracer.cpp:227-280)
+// k_scan: exclusive prefix of the per-block shadow counts (one workgroup).
 // ---------------------------------------------------------------------------
-template <bool COUNT>
+__global__ __launch_bounds__(1024) void k_scan(PcParams p) {
+    __shared__ unsigned part[1024];
+    const int G = p.grid;
+    const int per = (G + 1023) / 1024;
+    const int b0 = threadIdx.x * per;
+    unsigned sum = 0;
+    for (int i = b0; i < min(G, b0 + per); ++i) sum += p.bcount[i];
+    part[threadIdx.x] = sum;
+    __syncthreads();
+    for (int off = 1; off < 1024; off <<= 1) {            // Hillis-Steele inclusive scan
+        const unsigned v = threadIdx.x >= (unsigned)off ? part[threadIdx.x - off] : 0u;
+        __syncthreads();
+        part[threadIdx.x] += v;
+        __syncthreads();
+    }
+    unsigned run = threadIdx.x == 0 ? 0u : part[threadIdx.x - 1];
+    for (int i = b0; i < min(G, b0 + per); ++i) {
+        p.bprefix[i] = run;
+        run += p.bcount[i];
+    }
+    if (threadIdx.x == 1023) p.bprefix[G] = part[1023];
+}
+
+// ---------------------------------------------------------------------------
+// k_occlude: any-hit of every queued shadow ray (raytracer.cpp:227-280).
+// The rays of all k_chain regions form one index space (prefix sums); each
+// workgroup takes an equal slice of it, so a region full of mirror bounces
+// is spread over the whole grid.
+// ---------------------------------------------------------------------------
+template <bool COUNT, bool PRIV>
 __global__ __launch_bounds__(kBlock) void k_occlude(rtk::DevScene s, PcParams p) {
-    extern __shared__ int2 stk_lds[];
-    int2* stk = stk_lds + threadIdx.x;
+    const int GC = p.grid;
+    const unsigned* g_prefix = p.bprefix;     // read-only here; searched once per wave grab
+    block_init(s);
+    typename StackSel<PRIV>::type stk;
     Work w;
     uint32_t nrays = 0;
-    const unsigned n = min(*p.scount, p.scap);
-    for (unsigned i = blockIdx.x * kBlock + threadIdx.x; i < n; i += gridDim.x * kBlock) {
-        const float4 a = p.sray[2 * i], b = p.sray[2 * i + 1];
-        const Ray r = make_ray(V{a.x, a.y, a.z}, V{b.x, b.y, b.z});
-        nrays++;
-        p.occ[__float_as_int(a.w)] = any_hit2<COUNT, kBlock>(s, r, b.w, stk, w) ? 1 : 0;
+    const unsigned long long total = g_prefix[GC];
+    const unsigned lo = (unsigned)(total * blockIdx.x / gridDim.x);
+    const unsigned hi = (unsigned)(total * (blockIdx.x + 1) / gridDim.x);
+    const unsigned n = hi - lo;
+    bool active = false, exhausted = n == 0;
+    Ray r;
+    float tlim = 0.0f;
+    int owner = 0;
+    Walk wk;
+    while (true) {
+        if (!exhausted) {
+            const unsigned long long idle = __ballot(!active);
+            if (idle) {
+                const unsigned base = wave_grab_lds(&g_head, idle);
+                if (base + (unsigned)__popcll(idle) >= n) exhausted = true;
+                // region of the wave's first index (binary search, wave-uniform), then per lane
+                int reg = 0;
+                {
+                    const unsigned j0 = lo + base;
+                    int a = 0, b = GC;                       // g_prefix[a] <= j0 < g_prefix[b]
+                    while (b - a > 1) {
+                        const int m = (a + b) >> 1;
+                        if (g_prefix[m] <= j0) a = m; else b = m;
+                    }
+                    reg = a;
+                }
+                if (!active) {
+                    const unsigned idx = base + lane_rank(idle);
+                    if (idx < n) {
+                        const unsigned j = lo + idx;
+                        while (j >= g_prefix[reg + 1]) ++reg;
+                        const float4* sray = p.sray + 2 * ((size_t)reg * p.block_scap + (j - g_prefix[reg]));
+                        const float4 a = ld_nt(sray), b = ld_nt(sray + 1);
+                        r = make_ray(V{a.x, a.y, a.z}, V{b.x, b.y, b.z});
+                        tlim = b.w;
+                        owner = __float_as_int(a.w);
+                        nrays++;
+                        if (walk_begin<COUNT>(s, r, wk, w)) active = true;
+                        else p.occ[owner] = 0;
+                    }
+                }
+            }
+        }
+        if (!__any(active)) {
+            if (exhausted) break;
+            continue;
+        }
+        const int thresh = exhausted ? 0 : p.refill;
+        while (__popcll(__ballot(active)) > thresh) {
+            if (active) {
+                const int res = any_step<COUNT, FetchTop>(s, r, tlim, stk, wk, w);
+                if (res) {
+                    p.occ[owner] = res == 2 ? 1 : 0;
+                    active = false;
+                }
+            }
+        }
     }
     if (COUNT) {
         wave_add_counter(&p.counters[1], nrays);
@@ -115,7 +346,7 @@ __global__ __launch_bounds__(kBlock) void k_occlude(rtk::DevScene s, PcParams p)
 __device__ __forceinline__ V shade_level(const rtk::DevScene& s, const PcParams& p, unsigned path, int k,
                                          int* mat_out) {
     const float4* rc = p.rec + ((size_t)k * p.cap + path) * 3;
-    const float4 a = rc[0], b = rc[1], c = rc[2];
+    const float4 a = ld_nt(rc), b = ld_nt(rc + 1), c = ld_nt(rc + 2);
     const int mat = __float_as_int(a.w);
     *mat_out = mat;
     const V hitp{a.x, a.y, a.z}, n_{b.x, b.y, b.z}, d{c.x, c.y, c.z};
@@ -194,19 +425,44 @@ __global__ __launch_bounds__(kBlock) void k_compose(rtk::DevScene s, PcParams p)
 
 }  // namespace
 
-hipError_t launch_chain_chunk(const rtk::DevScene& s, const rtk::Eye& e, const PcParams& p, int grid_blocks,
-                              bool count, hipStream_t st) {
-    const size_t lds = (size_t)s.pair_stack * kBlock * sizeof(int2);
-    const dim3 blk(kBlock);
-    hipError_t err = hipMemsetAsync(p.scount, 0, sizeof(unsigned), st);
-    if (err != hipSuccess) return err;
-    const int g0 = std::min(grid_blocks, (p.n0 + kBlock - 1) / kBlock);
-    if (count) hipLaunchKernelGGL(k_chain<true>, dim3(g0), blk, lds, st, s, e, p);
-    else hipLaunchKernelGGL(k_chain<false>, dim3(g0), blk, lds, st, s, e, p);
-    if (count) hipLaunchKernelGGL(k_occlude<true>, dim3(grid_blocks), blk, lds, st, s, p);
-    else hipLaunchKernelGGL(k_occlude<false>, dim3(grid_blocks), blk, lds, st, s, p);
+hipError_t chain_occupancy(bool priv_stack, int* chain_blocks_per_cu, int* occlude_blocks_per_cu) {
+    hipError_t e;
+    if (priv_stack) {
+        e = hipOccupancyMaxActiveBlocksPerMultiprocessor(chain_blocks_per_cu, k_chain<false, true>, kBlock, 0);
+        if (e == hipSuccess)
+            e = hipOccupancyMaxActiveBlocksPerMultiprocessor(occlude_blocks_per_cu, k_occlude<false, true>, kBlock, 0);
+    } else {
+        e = hipOccupancyMaxActiveBlocksPerMultiprocessor(chain_blocks_per_cu, k_chain<false, false>, kBlock, 0);
+        if (e == hipSuccess)
+            e = hipOccupancyMaxActiveBlocksPerMultiprocessor(occlude_blocks_per_cu, k_occlude<false, false>, kBlock, 0);
+    }
+    return e;
+}
+
+unsigned chain_block_scap(int n0, int grid, int levels, int nlights) {
+    const unsigned units = ((unsigned)n0 + 255u) / 256u;
+    const unsigned per_block = (units + (unsigned)grid - 1u) / (unsigned)grid;
+    return per_block * 256u * (unsigned)levels * (unsigned)nlights;
+}
+
+hipError_t launch_chain_chunk(const rtk::DevScene& s, const rtk::Eye& e, const PcParams& p, bool count,
+                              hipStream_t st) {
+    const dim3 blk(kBlock), grid(p.grid);
+#define RT_CHAIN_LAUNCH(C, P)                                                        \
+    do {                                                                             \
+        hipLaunchKernelGGL((k_chain<C, P>), grid, blk, 0, st, s, e, p);               \
+        hipLaunchKernelGGL(k_scan, dim3(1), dim3(1024), 0, st, p);                     \
+        hipLaunchKernelGGL((k_occlude<C, P>), dim3(p.ogrid), blk, 0, st, s, p);        \
+    } while (0)
+    if (count) {
+        if (p.priv_stack) RT_CHAIN_LAUNCH(true, true); else RT_CHAIN_LAUNCH(true, false);
+    } else {
+        if (p.priv_stack) RT_CHAIN_LAUNCH(false, true); else RT_CHAIN_LAUNCH(false, false);
+    }
+#undef RT_CHAIN_LAUNCH
     const int npix = (p.chunk_rows / p.aa) * p.width;
-    hipLaunchKernelGGL(k_compose, dim3(std::min(grid_blocks, (npix + kBlock - 1) / kBlock)), blk, 0, st, s, p);
+    hipLaunchKernelGGL(k_compose, dim3(std::max(1, std::min(p.grid, (npix + kBlock - 1) / kBlock))), blk, 0, st, s,
+                       p);
     return hipGetLastError();
 }
 

@@ -39,15 +39,29 @@ struct PcParams {
     int nlights;
     float4* rec;      // [levels][cap][3]: {hitp.xyz, mat}, {n.xyz, t}, {d.xyz, 0}
     int* pinfo;       // [cap]: nlev | kind << 8
-    float4* sray;     // [scap][2]: {p.xyz, owner}, {ldir.xyz, dist}; owner = (level*cap+path)*nl + l
+    float4* sray;     // [grid][block_scap][2]: {p.xyz, owner}, {ldir.xyz, dist}; owner = (level*cap+path)*nl + l
     uint8_t* occ;     // [levels][cap][nl]
-    unsigned* scount; // shadow rays appended
-    unsigned scap;    // shadow queue capacity
+    unsigned* bcount; // [grid]: shadow rays queued by each k_chain workgroup
+    unsigned* bprefix;    // [grid + 1]: exclusive prefix of bcount (k_scan)
+    unsigned block_scap;  // shadow-queue slots per workgroup (worst case, see chain_block_scap)
+    int grid;         // k_chain persistent grid (= number of shadow-queue regions)
+    int ogrid;        // k_occlude persistent grid
+    int refill;       // a wave refills once <= refill of its lanes are still walking
+    int priv_stack;   // 1: traversal stack in private memory, 0: first entries in LDS
     uint8_t* out;
     unsigned long long* counters;
 };
 
-hipError_t launch_chain_chunk(const rtk::DevScene& s, const rtk::Eye& e, const PcParams& p, int grid_blocks,
-                              bool count, hipStream_t stream);
+// Worst-case shadow-queue slots per workgroup: every sample of the block
+// recording every level, one ray per light.
+unsigned chain_block_scap(int n0, int grid, int levels, int nlights);
+
+// Resident workgroups per CU of the (non-counting) k_chain / k_occlude: the
+// persistent grids are sized so every workgroup starts at t = 0 (a late-
+// starting workgroup that owns slow pixels would stretch the frame).
+hipError_t chain_occupancy(bool priv_stack, int* chain_blocks_per_cu, int* occlude_blocks_per_cu);
+
+hipError_t launch_chain_chunk(const rtk::DevScene& s, const rtk::Eye& e, const PcParams& p, bool count,
+                              hipStream_t stream);
 
 }  // namespace rtc

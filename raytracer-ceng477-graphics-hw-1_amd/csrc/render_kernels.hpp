@@ -30,6 +30,7 @@ struct DevScene {
     float root_lo[3], root_hi[3];
     int root_info;
     int pair_stack;       // LDS stack entries (8 B each) for the pair traversal
+    int top_pairs;        // pairs [0, top_pairs) are the top BVH levels (cached in LDS)
 
     // Sphere prims carry ~sphere_index in p0.w (negative), triangles their id.
     __device__ __forceinline__ bool prim_is_sphere(int, const float4 p0) const {

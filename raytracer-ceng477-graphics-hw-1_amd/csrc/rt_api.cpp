@@ -101,6 +101,10 @@ struct rt_scene {
     dl::LeafBig* d_leafbig = nullptr;
     enum Path { kChain, kWavefront, kMegakernel } path = kChain;
     int grid_blocks = 2048;
+    int num_cus = 256;
+    int chain_grid = 0, occl_grid = 0;   // resident-sized persistent grids (lazily queried)
+    int tune_refill = 0;        // RT_REFILL
+    int tune_priv_stack = 0;    // RT_STACK=priv|lds
     // chain-path workspace (grown on demand)
     struct {
         int cap = 0, levels = 0, nlights = 0;
@@ -108,15 +112,17 @@ struct rt_scene {
         int* pinfo = nullptr;
         float4* sray = nullptr;
         uint8_t* occ = nullptr;
-        unsigned* scount = nullptr;
-        unsigned scap = 0;
+        unsigned* bcount = nullptr;
+        unsigned* bprefix = nullptr;
+        size_t scap = 0;
+        int grid = 0;
     } cw;
 
     void free_cw() {
         (void)hipFree(cw.rec); (void)hipFree(cw.pinfo); (void)hipFree(cw.sray); (void)hipFree(cw.occ);
-        (void)hipFree(cw.scount);
-        cw.rec = cw.sray = nullptr; cw.pinfo = nullptr; cw.occ = nullptr; cw.scount = nullptr;
-        cw.cap = cw.levels = cw.nlights = 0; cw.scap = 0;
+        (void)hipFree(cw.bcount); (void)hipFree(cw.bprefix);
+        cw.rec = cw.sray = nullptr; cw.pinfo = nullptr; cw.occ = nullptr; cw.bcount = cw.bprefix = nullptr;
+        cw.cap = cw.levels = cw.nlights = cw.grid = 0; cw.scap = 0;
     }
     // wavefront workspace (grown on demand)
     struct {
@@ -204,6 +210,7 @@ int finish_scene(rt_scene* s, const rt_options* opts) {
         hipDeviceProp_t prop;
         HIP_TRY(hipGetDeviceProperties(&prop, s->device));
         s->grid_blocks = std::max(1, prop.multiProcessorCount) * 8;
+        s->num_cus = std::max(1, prop.multiProcessorCount);
     }
     s->path = rt_scene::kChain;
     if (opts && (opts->flags & RT_OPT_WAVEFRONT)) s->path = rt_scene::kWavefront;
@@ -214,6 +221,8 @@ int finish_scene(rt_scene* s, const rt_options* opts) {
         else if (v == "wave") s->path = rt_scene::kWavefront;
         else if (v == "chain") s->path = rt_scene::kChain;
     }
+    if (const char* e = std::getenv("RT_REFILL")) s->tune_refill = std::max(0, std::min(63, std::atoi(e)));
+    if (const char* e = std::getenv("RT_STACK")) s->tune_priv_stack = std::string(e) != "lds";
 
     rtk::DevScene& d = s->dev;
     d.nodes = s->d_nodes; d.prims = s->d_prims; d.tri_shade = s->d_tri; d.mats = s->d_mats; d.lights = s->d_lights;
@@ -232,6 +241,8 @@ int finish_scene(rt_scene* s, const rt_options* opts) {
     }
     d.root_info = s->bvh.root_info;
     d.pair_stack = std::max(2, s->bvh.max_stack);
+    d.top_pairs = s->bvh.top_pairs;
+    if (const char* e = std::getenv("RT_TOP")) d.top_pairs = std::min(d.top_pairs, std::max(0, std::atoi(e)));
     return RT_OK;
 }
 
@@ -351,31 +362,50 @@ int render_chain(rt_scene* s, const rtk::Eye& eye, const rtk::FrameParams& f, bo
     const int chunk_rows = (int)units * unit;
     const size_t cap = units * unit_samples;
     if (cap * levels * nl >= (size_t)INT32_MAX) return fail(RT_ERR_LIMIT, "frame chunk too large for the chain path");
+    if (s->chain_grid == 0) {
+        int cb = 0, ob = 0;
+        HIP_TRY(rtc::chain_occupancy(s->tune_priv_stack != 0, &cb, &ob));
+        s->chain_grid = std::max(1, cb) * s->num_cus;
+        s->occl_grid = std::max(1, ob) * s->num_cus;
+        if (const char* e = std::getenv("RT_GRID")) s->chain_grid = s->occl_grid = std::max(1, std::atoi(e));
+    }
+    auto grid_for = [&](int n0) { return std::max(1, std::min(s->chain_grid, (n0 + 255) / 256)); };
+    const int full_grid = grid_for((int)cap);
+    const size_t sray_need = (size_t)full_grid * rtc::chain_block_scap((int)cap, full_grid, levels, nl);
     auto& w = s->cw;
-    if (w.cap < (int)cap || w.levels < levels || w.nlights < nl) {
+    if (w.cap < (int)cap || w.levels < levels || w.nlights < nl || w.scap < sray_need ||
+        w.grid < full_grid) {
         const int ncap = std::max<int>(w.cap, (int)cap), nlev = std::max(w.levels, levels),
-                  nnl = std::max(w.nlights, nl);
+                  nnl = std::max(w.nlights, nl), ngrid = std::max(w.grid, full_grid);
+        const size_t nsray = std::max<size_t>(w.scap, sray_need);
         s->free_cw();
         const size_t c = (size_t)ncap, rl = c * nlev;
         int rc;
-        if ((rc = alloc_dev(&w.rec, 3 * rl)) || (rc = alloc_dev(&w.pinfo, c)) || (rc = alloc_dev(&w.sray, 2 * rl * nnl)) ||
-            (rc = alloc_dev(&w.occ, rl * nnl)) || (rc = alloc_dev(&w.scount, 1))) {
+        if ((rc = alloc_dev(&w.rec, 3 * rl)) || (rc = alloc_dev(&w.pinfo, c)) || (rc = alloc_dev(&w.sray, 2 * nsray)) ||
+            (rc = alloc_dev(&w.occ, rl * nnl)) || (rc = alloc_dev(&w.bcount, (size_t)ngrid)) ||
+            (rc = alloc_dev(&w.bprefix, (size_t)ngrid + 1))) {
             s->free_cw();
             return rc;
         }
-        w.cap = ncap; w.levels = nlev; w.nlights = nnl; w.scap = (unsigned)(rl * nnl);
+        w.cap = ncap; w.levels = nlev; w.nlights = nnl; w.scap = nsray; w.grid = ngrid;
     }
     rtc::PcParams p;
     p.width = f.width; p.height = f.height; p.aa = f.aa; p.stripe_rows = f.stripe_rows;
     p.rank = f.rank; p.nranks = f.nranks; p.slab_rows = f.slab_rows;
     p.wi = wi; p.tiles_x = tiles_x; p.cap = w.cap; p.levels = levels; p.nlights = s->dev.nlights;
-    p.rec = w.rec; p.pinfo = w.pinfo; p.sray = w.sray; p.occ = w.occ; p.scount = w.scount; p.scap = w.scap;
+    p.rec = w.rec; p.pinfo = w.pinfo; p.sray = w.sray; p.occ = w.occ; p.bcount = w.bcount; p.bprefix = w.bprefix;
+    p.ogrid = s->occl_grid;
+    p.refill = s->tune_refill;
+    p.priv_stack = s->tune_priv_stack;
     p.out = f.out; p.counters = f.counters;
     for (int r0 = 0; r0 < li; r0 += chunk_rows) {
         p.chunk_row0 = r0;
         p.chunk_rows = std::min(chunk_rows, li - r0);
         p.n0 = tiles_x * ((p.chunk_rows + 7) / 8) * 64;
-        HIP_TRY(rtc::launch_chain_chunk(s->dev, eye, p, s->grid_blocks, count, st));
+        p.grid = grid_for(p.n0);
+        p.block_scap = rtc::chain_block_scap(p.n0, p.grid, levels, nl);
+        if ((size_t)p.grid * p.block_scap > w.scap) return fail(RT_ERR_LIMIT, "internal: shadow queue too small");
+        HIP_TRY(rtc::launch_chain_chunk(s->dev, eye, p, count, st));
     }
     return RT_OK;
 }

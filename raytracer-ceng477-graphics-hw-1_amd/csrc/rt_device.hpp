@@ -69,6 +69,34 @@ __device__ __forceinline__ bool box_hit(const Ray& r, const float4 lo, const flo
     return tmax >= smax(0.0f, tmin);
 }
 
+// Same test with v_min/v_max(3) instead of compare+select.  Valid only when
+// no slab value can be NaN, i.e. the ray origin and 1/dir are finite
+// (ray_nan_free): then min/max agree with std::min/std::max except for the
+// sign of a zero result, and tmin/tmax are only ever compared (never used in
+// arithmetic), where -0 == +0.  Halves the box test's instruction count.
+__device__ __forceinline__ bool box_hit_fast(const Ray& r, const float4 lo, const float4 hi, float* t) {
+    const float tx1 = (lo.x - r.o.x) * r.inv.x;
+    const float tx2 = (hi.x - r.o.x) * r.inv.x;
+    const float ty1 = (lo.y - r.o.y) * r.inv.y;
+    const float ty2 = (hi.y - r.o.y) * r.inv.y;
+    const float tz1 = (lo.z - r.o.z) * r.inv.z;
+    const float tz2 = (hi.z - r.o.z) * r.inv.z;
+    const float tmin = __builtin_fmaxf(__builtin_fmaxf(__builtin_fminf(tx1, tx2), __builtin_fminf(ty1, ty2)),
+                                       __builtin_fminf(tz1, tz2));
+    const float tmax = __builtin_fminf(__builtin_fminf(__builtin_fmaxf(tx1, tx2), __builtin_fmaxf(ty1, ty2)),
+                                       __builtin_fmaxf(tz1, tz2));
+    *t = tmin;
+    return tmax >= __builtin_fmaxf(0.0f, tmin);
+}
+
+// Finite origin, finite dir (so 1/dir != 0) and finite 1/dir: every
+// (bound - o) * inv is finite or +-inf, never NaN (bounds are finite).
+__device__ __forceinline__ bool ray_nan_free(const Ray& r) {
+    return __builtin_isfinite(r.o.x) && __builtin_isfinite(r.o.y) && __builtin_isfinite(r.o.z) &&
+           __builtin_isfinite(r.d.x) && __builtin_isfinite(r.d.y) && __builtin_isfinite(r.d.z) &&
+           __builtin_isfinite(r.inv.x) && __builtin_isfinite(r.inv.y) && __builtin_isfinite(r.inv.z);
+}
+
 // det (raytracer.cpp:15-19), rows m0 m1 m2.
 __device__ __forceinline__ float det3(float m00, float m01, float m02, float m10, float m11, float m12,
                                       float m20, float m21, float m22) {

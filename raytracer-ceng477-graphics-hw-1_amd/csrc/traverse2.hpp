@@ -177,4 +177,176 @@ __device__ __forceinline__ bool any_hit2(const rtk::DevScene& s, const Ray& r, f
     return false;
 }
 
+// ---------------------------------------------------------------------------
+// Resumable form of the same two walks, one node expansion (or one leaf) per
+// call, for persistent kernels that refill finished lanes with new rays.
+// Pairs [0, s.top_pairs) (the top levels) are read from an LDS copy.
+// ---------------------------------------------------------------------------
+struct Walk {
+    int cur;       // node to process (pair index or leaf code)
+    int sp;        // stack depth
+    float tmax;    // closest-hit pruning bound
+    HitRec best;   // closest-hit result so far
+    bool fast;     // ray_nan_free: box tests may use v_min/v_max
+};
+
+// Both child boxes of a pair; the min/max form when every active lane's ray
+// is NaN-free (wave-uniform branch, so no divergence between the two forms).
+__device__ __forceinline__ void box_pair(const Ray& r, bool fast, const float4 l0, const float4 l1, const float4 r0,
+                                         const float4 r1, bool& hl, bool& hr, float& tl, float& tr) {
+    if (__all(fast)) {
+        hl = box_hit_fast(r, l0, l1, &tl);
+        hr = box_hit_fast(r, r0, r1, &tr);
+    } else {
+        hl = box_hit(r, l0, l1, &tl);
+        hr = box_hit(r, r0, r1, &tr);
+    }
+}
+
+// Memory policies.  The walks are templated on
+//   FETCH::pair(s, p, l0, l1, r0, r1)    read child pair p
+//   STK::put(i, v) / STK::at(i)           per-lane stack entry i
+// Entry {info, tmin bits} (closest) or {info, hit flag} (any).  LDS-backed
+// policies must name their __shared__ arrays directly (not through a stored
+// generic pointer), or hipcc falls back to flat loads that wait on both
+// vmcnt and lgkmcnt — see pathchain.hip.
+struct FetchGlobal {
+    __device__ static __forceinline__ void pair(const rtk::DevScene& s, int p, float4& l0, float4& l1, float4& r0,
+                                                float4& r1) {
+        const float4* q = reinterpret_cast<const float4*>(&s.pairs[p]);
+        l0 = q[0]; l1 = q[1]; r0 = q[2]; r1 = q[3];
+    }
+};
+
+struct StackPriv {            // private (scratch) memory
+    int2 e[dl::kMaxStack];
+    __device__ __forceinline__ void put(int i, int2 v) { e[i] = v; }
+    __device__ __forceinline__ int2 at(int i) const { return e[i]; }
+};
+
+// Root test (the reference's first pop).  false: nothing to traverse.
+template <bool COUNT>
+__device__ __forceinline__ bool walk_begin(const rtk::DevScene& s, const Ray& r, Walk& k, Work& w) {
+    k.best = HitRec{-1.0f, -1};
+    k.tmax = FLT_MAX;
+    k.sp = 0;
+    k.cur = s.root_info;
+    k.fast = ray_nan_free(r);
+    if (s.nnodes <= 0) return false;
+    if (COUNT) w.nodes++;
+    float bt;
+    const float4 lo = make_float4(s.root_lo[0], s.root_lo[1], s.root_lo[2], 0.0f);
+    const float4 hi = make_float4(s.root_hi[0], s.root_hi[1], s.root_hi[2], 0.0f);
+    return box_hit(r, lo, hi, &bt) && bt <= k.tmax;   // bt NaN prunes, as in the reference
+}
+
+// One closest-hit step; returns true when the walk is finished (result in k.best).
+template <bool COUNT, class FETCH, class STK>
+__device__ __forceinline__ bool closest_step(const rtk::DevScene& s, const Ray& r, STK& stk, Walk& k, Work& w) {
+    if (k.cur >= 0) {
+        float4 l0, l1, r0, r1;
+        FETCH::pair(s, k.cur, l0, l1, r0, r1);
+        if (COUNT) w.nodes += 2;
+        float tl, tr;
+        bool hl, hr;
+        box_pair(r, k.fast, l0, l1, r0, r1, hl, hr, tl, tr);
+        const bool left_first = comp(r.d, __float_as_int(l1.w)) > 0;
+        const int il = __float_as_int(l0.w), ir = __float_as_int(r0.w);
+        const bool hn = left_first ? hl : hr, hf = left_first ? hr : hl;
+        const float tn = left_first ? tl : tr, tf = left_first ? tr : tl;
+        const int in_ = left_first ? il : ir, if_ = left_first ? ir : il;
+        if (hf) {
+            stk.put(k.sp, make_int2(if_, __float_as_int(tf)));
+            ++k.sp;
+        }
+        if (hn && tn <= k.tmax) {
+            k.cur = in_;
+            return false;
+        }
+    } else {
+        int a, cnt;
+        leaf_range(s, k.cur, &a, &cnt);
+        for (int i = a; i < a + cnt; ++i) {
+            const float4* pr = reinterpret_cast<const float4*>(&s.prims[i]);
+            const float4 p0 = pr[0], p1 = pr[1];
+            float t;
+            bool h;
+            if (__float_as_int(p0.w) >= 0) {
+                if (COUNT) w.tris++;
+                h = tri_hit(r, p0, p1, pr[2], &t);
+            } else {
+                if (COUNT) w.spheres++;
+                h = sphere_hit(r, p0, p1, &t);
+            }
+            if (h && (t < k.best.t || k.best.t == -1.0f)) {
+                k.best.t = t;
+                k.best.prim = i;
+                k.tmax = t;
+            }
+        }
+    }
+    while (k.sp > 0) {
+        --k.sp;
+        const int2 e = stk.at(k.sp);
+        if (__int_as_float(e.y) <= k.tmax) {
+            k.cur = e.x;
+            return false;
+        }
+    }
+    return true;
+}
+
+// One any-hit step: 0 = continue, 1 = finished unoccluded, 2 = finished occluded.
+template <bool COUNT, class FETCH, class STK>
+__device__ __forceinline__ int any_step(const rtk::DevScene& s, const Ray& r, float tlim, STK& stk, Walk& k,
+                                        Work& w) {
+    if (k.cur >= 0) {
+        float4 l0, l1, r0, r1;
+        FETCH::pair(s, k.cur, l0, l1, r0, r1);
+        float tl, tr;
+        bool hl, hr;
+        box_pair(r, k.fast, l0, l1, r0, r1, hl, hr, tl, tr);
+        const bool left_first = comp(r.d, __float_as_int(l1.w)) > 0;
+        const int il = __float_as_int(l0.w), ir = __float_as_int(r0.w);
+        const bool hn = left_first ? hl : hr, hf = left_first ? hr : hl;
+        const int in_ = left_first ? il : ir, if_ = left_first ? ir : il;
+        if (COUNT) w.nodes++;
+        if (hf || COUNT) {
+            stk.put(k.sp, make_int2(if_, hf ? 1 : 0));
+            ++k.sp;
+        }
+        if (hn) {
+            k.cur = in_;
+            return 0;
+        }
+    } else {
+        int a, cnt;
+        leaf_range(s, k.cur, &a, &cnt);
+        for (int i = a; i < a + cnt; ++i) {
+            const float4* pr = reinterpret_cast<const float4*>(&s.prims[i]);
+            const float4 p0 = pr[0], p1 = pr[1];
+            float t;
+            bool h;
+            if (__float_as_int(p0.w) >= 0) {
+                if (COUNT) w.tris++;
+                h = tri_hit(r, p0, p1, pr[2], &t);
+            } else {
+                if (COUNT) w.spheres++;
+                h = sphere_hit(r, p0, p1, &t);
+            }
+            if (h && t < tlim) return 2;
+        }
+    }
+    while (k.sp > 0) {
+        --k.sp;
+        const int2 e = stk.at(k.sp);
+        if (COUNT) w.nodes++;
+        if (e.y) {
+            k.cur = e.x;
+            return 0;
+        }
+    }
+    return 1;
+}
+
 }  // namespace rtd

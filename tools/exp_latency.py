@@ -54,9 +54,9 @@ def timeit(scene, cam, reps=5):
 
 
 res = {}
-for mega in (True, False):
-    name = "mega" if mega else "wave"
-    s = pkg.Scene.from_xml(xml, device=0, megakernel=mega)
+for mega in ("chain", "megakernel"):
+    name = mega
+    s = pkg.Scene.from_xml(xml, device=0, render_path=mega)
     cam = s.camera(0)
     res[name] = {"full": timeit(s, cam)}
     for sz in (8, 16, 64, 256):
