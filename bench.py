@@ -126,9 +126,11 @@ def main() -> int:
     stream = torch.cuda.current_stream(dev)
     sp = stream.cuda_stream
     if world > 1:
-        gathered = [torch.empty_like(slab) for _ in range(world)] if rank == 0 else None
         gbuf = torch.empty((world, rows, W, 3), dtype=torch.uint8, device=dev) if rank == 0 else None
         image = torch.empty((H, W, 3), dtype=torch.uint8, device=dev) if rank == 0 else None
+
+        def unshuffle_dev(g, img):    # rank-0 kernel: slabs -> row order (rt_unshuffle_stripes)
+            pkg.unshuffle_stripes(g.data_ptr(), img.data_ptr(), W, H, S, world, sp)
 
     # Counting pass (not timed): exact per-rank work for the byte model.
     scene.counters_reset(sp)
@@ -150,9 +152,7 @@ def main() -> int:
         if ev_pair is not None:
             ev_pair[1].record(stream)
         if world > 1:
-            dist.gather(slab, gather_list=[gbuf[i] for i in range(world)] if rank == 0 else None, dst=0)
-            if rank == 0:
-                pkg.unshuffle_stripes(gbuf.data_ptr(), image.data_ptr(), W, H, S, world, sp)
+            pkg.frame.assemble_frame(slab, H, S, unshuffle=unshuffle_dev, gbuf=gbuf, image=image)
 
     for _ in range(a.warmup):
         step()

@@ -85,9 +85,12 @@ typedef struct rt_scene_desc {
 #define RT_OPT_HOST_ONLY 1   /* load + BVH build only, no device upload (no GPU needed) */
 /* Render paths (all bit-identical; default = chain: closest-hit chains in one
  * kernel, shadow rays and shading deferred).  Env RT_PATH=chain|wave|mega
- * overrides at scene creation. */
+ * overrides at scene creation (also =fused). */
 #define RT_OPT_MEGAKERNEL 2  /* one kernel per frame, whole recursion per lane   */
 #define RT_OPT_WAVEFRONT 4   /* per-bounce queues, 3 kernels per recursion level */
+#define RT_OPT_CHAIN 8       /* chain kernel + deferred any-hit kernel + compose    */
+#define RT_OPT_FUSED 16      /* chains and shadow rays in one persistent kernel
+                                (per-wave task queues) + compose                  */
 
 typedef struct rt_options {
     int device;       /* HIP device ordinal; -1 = current device            */

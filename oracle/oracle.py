@@ -54,6 +54,7 @@ def lib() -> ctypes.CDLL:
         L.ro_primary_hits.argtypes = [P, ctypes.c_int, ctypes.c_int, P, P]
         L.ro_write_ppm.argtypes = [ctypes.c_char_p, P, ctypes.c_int, ctypes.c_int]
         L.ro_export_nodes.argtypes = [P, P, ctypes.c_int]
+        L.ro_work_map.argtypes = [P, ctypes.c_int, ctypes.c_int, ctypes.c_int, P, P]
         _lib = L
     return _lib
 

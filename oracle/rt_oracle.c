@@ -564,6 +564,10 @@ static inline int sphere_test(const ro_scene* s, const ray_t* r, const ro_sphere
 
 #define RO_STACK 64
 
+/* diagnostics: per-node visit histogram [0]=closest-hit [1]=any-hit (NULL = off) */
+uint64_t* ro_debug_node_hist[2];
+#define NOTE_NODE(k, ni) do { if (ro_debug_node_hist[k]) __atomic_fetch_add(&ro_debug_node_hist[k][ni], 1, __ATOMIC_RELAXED); } while (0)
+
 /* Ray::getFirstIntersection (:177-225) */
 static hit_t closest_hit(const ro_scene* s, const ray_t* r, work_t* w) {
     hit_t best; best.t = -1; best.exists = 0; best.mat = -1; best.n.x = best.n.y = best.n.z = -1;
@@ -574,7 +578,7 @@ static hit_t closest_hit(const ro_scene* s, const ray_t* r, work_t* w) {
         int ni = stack[--sp];
         const ro_node* n = &s->nodes[ni];
         float bt; int ex = box_test(r, n, &bt);
-        w->node++;
+        w->node++; NOTE_NODE(0, ni);
         if (ex && bt <= tMax) {
             if (!n->leaf) {
                 if (v_get(r->d, n->axis) > 0) { stack[sp++] = n->right; stack[sp++] = ni + 1; }
@@ -613,7 +617,7 @@ static int any_hit(const ro_scene* s, const ray_t* r, float tlim, work_t* w) {
     while (sp > 0) {
         int ni = stack[--sp];
         const ro_node* n = &s->nodes[ni];
-        float bt; w->node++;
+        float bt; w->node++; NOTE_NODE(1, ni);
         if (!box_test(r, n, &bt)) continue;
         if (!n->leaf) {
             if (v_get(r->d, n->axis) > 0) { stack[sp++] = n->right; stack[sp++] = ni + 1; }

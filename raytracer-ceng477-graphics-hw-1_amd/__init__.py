@@ -19,15 +19,18 @@ import numpy as np
 
 from . import scenes  # noqa: F401  (re-export: scene fixtures / derived configs)
 from . import stripes  # noqa: F401
+from . import frame  # noqa: F401  (multi-GPU slab gather + reassembly)
 
 PKG_DIR = Path(__file__).resolve().parent
-LIB_PATH = PKG_DIR / "librt_hip.so"
+LIB_PATH = Path(os.environ["RT_LIB"]) if os.environ.get("RT_LIB") else PKG_DIR / "librt_hip.so"   # RT_LIB: experiments
 CLI_PATH = PKG_DIR / "raytracer"
 
 RT_OPT_HOST_ONLY = 1
 RT_OPT_MEGAKERNEL = 2
 RT_OPT_WAVEFRONT = 4
-PATHS = ("chain", "wavefront", "megakernel")
+RT_OPT_CHAIN = 8
+RT_OPT_FUSED = 16
+PATHS = ("chain", "wavefront", "megakernel", "fused")
 RT_RENDER_COUNT = 1
 
 
@@ -143,10 +146,12 @@ class Scene:
     @classmethod
     def from_xml(cls, path: str | os.PathLike, device: int = -1, host_only: bool = False,
                  render_path: str = "chain") -> "Scene":
-        """render_path: "chain" (default), "wavefront" or "megakernel" (all bit-identical)."""
+        """render_path: "chain", "fused", "wavefront", "megakernel" or "default" (the library's
+        default path); all are bit-identical."""
         h = ctypes.c_void_p()
         flags = RT_OPT_HOST_ONLY if host_only else 0
-        flags |= {"chain": 0, "wavefront": RT_OPT_WAVEFRONT, "megakernel": RT_OPT_MEGAKERNEL}[render_path]
+        flags |= {"chain": RT_OPT_CHAIN, "wavefront": RT_OPT_WAVEFRONT, "megakernel": RT_OPT_MEGAKERNEL,
+                  "fused": RT_OPT_FUSED, "default": 0}[render_path]
         opts = Options(device, flags)
         _check(lib().rt_scene_load_xml(str(path).encode(), ctypes.byref(opts), ctypes.byref(h)))
         return cls(h.value)

@@ -64,7 +64,10 @@ struct alignas(16) Pair {
     float r_maxx, r_maxy, r_maxz; int32_t pad;
 };
 struct LeafBig { int32_t start, count; };
-constexpr int kTopPairs = 256;   // top-level pairs cached in LDS (16 KiB per workgroup)
+#ifndef RT_TOP_PAIRS
+#define RT_TOP_PAIRS 256
+#endif
+constexpr int kTopPairs = RT_TOP_PAIRS;   // top-level pairs cached in LDS (64 B each, per workgroup)
 constexpr int kLeafCountShift = 25;
 constexpr int32_t kLeafStartMask = (1 << kLeafCountShift) - 1;
 constexpr int kLeafMaxCount = 63;

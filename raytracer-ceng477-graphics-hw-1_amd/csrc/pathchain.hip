@@ -33,6 +33,9 @@ namespace rtc {
 namespace {
 
 constexpr int kBlock = 256;
+#ifndef RT_WAVES_PER_EU
+#define RT_WAVES_PER_EU 1
+#endif
 constexpr int kLdsStack = 8;     // stack entries kept in LDS (deeper ones in private memory)
 
 enum LaneState : int { kIdle = 0, kTrav = 1, kDone = 2 };
@@ -43,6 +46,7 @@ __shared__ float4 g_top[4 * dl::kTopPairs];   // top BVH pairs, 16 KiB
 __shared__ int2 g_stk[kLdsStack * kBlock];     // first stack entries, [entry][thread], 16 KiB
 __shared__ unsigned g_head;                    // block-local work queue head
 __shared__ unsigned g_scnt;                    // block-local shadow-ray count (hit lanes)
+__shared__ unsigned g_pref[kMaxChainGrid + 1]; // k_occlude: shadow-queue region prefix
 
 struct FetchTop {
     __device__ static __forceinline__ void pair(const rtk::DevScene& s, int p, float4& l0, float4& l1, float4& r0,
@@ -118,8 +122,17 @@ __device__ __forceinline__ unsigned block_samples(unsigned n0, unsigned G) {
     const unsigned last_unit = blockIdx.x + (mine - 1u) * G;
     return (mine - 1u) * 256u + min(256u, n0 - last_unit * 256u);
 }
-__device__ __forceinline__ unsigned block_sample(unsigned v, unsigned G) {
-    return (blockIdx.x + (v >> 8) * G) * 256u + (v & 255u);
+// Within a full unit, `spread` > 1 interleaves its 4 tiles over consecutive
+// v (a wave takes 64/spread-sample strips of `spread` tiles), so one heavy
+// 8x8 tile is shared by several waves instead of serialising one.
+__device__ __forceinline__ unsigned block_sample(unsigned v, unsigned G, unsigned n0, unsigned spread) {
+    const unsigned unit = blockIdx.x + (v >> 8) * G;
+    unsigned u = v & 255u;
+    if (spread > 1u && (unit + 1u) * 256u <= n0) {
+        const unsigned grp = u / (64u * spread), j = u % (64u * spread);
+        u = (grp * spread + j % spread) * 64u + j / spread;
+    }
+    return unit * 256u + u;
 }
 
 // ---------------------------------------------------------------------------
@@ -127,7 +140,7 @@ __device__ __forceinline__ unsigned block_sample(unsigned v, unsigned G) {
 // shading): record each hit, queue its shadow rays, follow mirrors.
 // ---------------------------------------------------------------------------
 template <bool COUNT, bool PRIV>
-__global__ __launch_bounds__(kBlock) void k_chain(rtk::DevScene s, rtk::Eye e, PcParams p) {
+__global__ __launch_bounds__(kBlock, RT_WAVES_PER_EU) void k_chain(rtk::DevScene s, rtk::Eye e, PcParams p) {
     block_init(s);
     typename StackSel<PRIV>::type stk;
     Work w;
@@ -142,6 +155,7 @@ __global__ __launch_bounds__(kBlock) void k_chain(rtk::DevScene s, rtk::Eye e, P
     int k = 0;
     Ray r;
     Walk wk;
+    unsigned t_grab = 0;
     while (true) {
         // (1) epilogue of finished walks: record, queue shadow rays, reflect
         if (st == kDone) {
@@ -178,12 +192,15 @@ __global__ __launch_bounds__(kBlock) void k_chain(rtk::DevScene s, rtk::Eye e, P
             if (!hit) {                                                          // :442-449
                 p.pinfo[path] = k | ((k == 0 ? kEndBg : kEndZero) << 8);
                 st = kIdle;
+                if (p.trace) { p.trace[2 * path] = t_grab; p.trace[2 * path + 1] = (unsigned)wall_clock64(); }
             } else if (!s.mats[mat - 1].is_mirror) {
                 p.pinfo[path] = (k + 1) | (kEndLast << 8);
                 st = kIdle;
+                if (p.trace) { p.trace[2 * path] = t_grab; p.trace[2 * path + 1] = (unsigned)wall_clock64(); }
             } else if (k >= s.max_depth) {        // child beyond MaxRecursionDepth: 0 (:387-389)
                 p.pinfo[path] = (k + 1) | (kEndZero << 8);
                 st = kIdle;
+                if (p.trace) { p.trace[2 * path] = t_grab; p.trace[2 * path + 1] = (unsigned)wall_clock64(); }
             } else {
                 const V d2 = nrm(r.d);                                         // :431-435
                 const V n2 = nrm(nn);
@@ -203,10 +220,11 @@ __global__ __launch_bounds__(kBlock) void k_chain(rtk::DevScene s, rtk::Eye e, P
                 if (st == kIdle) {
                     const unsigned v = base + lane_rank(idle);
                     if (v < nb) {
-                        const unsigned idx = block_sample(v, G);
+                        const unsigned idx = block_sample(v, G, (unsigned)p.n0, (unsigned)p.spread);
                         if (slab_sample_ray(e, p, idx, &r)) {
                             path = idx;
                             k = 0;
+                            if (p.trace) t_grab = (unsigned)wall_clock64();
                             nprim++;
                             if (s.max_depth < 0) p.pinfo[path] = 0 | (kEndZero << 8);   // depth 0 > max: black
                             else st = walk_begin<COUNT>(s, r, wk, w) ? kTrav : kDone;
@@ -220,8 +238,9 @@ __global__ __launch_bounds__(kBlock) void k_chain(rtk::DevScene s, rtk::Eye e, P
             continue;
         }
         // (3) walk until enough lanes need service
+        if (s.prio) wave_priority(st == kTrav ? k : 0);
         const int thresh = exhausted ? 0 : p.refill;
-        while (__popcll(__ballot(st == kTrav)) > thresh) {
+        while (__popcll(__ballot(st == kTrav)) > thresh && __popcll(__ballot(st == kDone)) < p.service) {
             if (st == kTrav && closest_step<COUNT, FetchTop>(s, r, stk, wk, w)) st = kDone;
         }
     }
@@ -269,17 +288,17 @@ __global__ __launch_bounds__(1024) void k_scan(PcParams p) {
 // is spread over the whole grid.
 // ---------------------------------------------------------------------------
 template <bool COUNT, bool PRIV>
-__global__ __launch_bounds__(kBlock) void k_occlude(rtk::DevScene s, PcParams p) {
+__global__ __launch_bounds__(kBlock, RT_WAVES_PER_EU) void k_occlude(rtk::DevScene s, PcParams p) {
     const int GC = p.grid;
-    const unsigned* g_prefix = p.bprefix;     // read-only here; searched once per wave grab
-    block_init(s);
+    for (int i = threadIdx.x; i <= GC; i += kBlock) g_pref[i] = p.bprefix[i];
+    block_init(s);                                   // (its barrier also publishes g_pref)
     typename StackSel<PRIV>::type stk;
     Work w;
     uint32_t nrays = 0;
-    const unsigned long long total = g_prefix[GC];
-    const unsigned lo = (unsigned)(total * blockIdx.x / gridDim.x);
-    const unsigned hi = (unsigned)(total * (blockIdx.x + 1) / gridDim.x);
-    const unsigned n = hi - lo;
+    const unsigned t_start = p.trace ? (unsigned)wall_clock64() : 0u;
+    const unsigned total = g_pref[GC];
+    const unsigned G = gridDim.x, b = blockIdx.x;
+    const unsigned n = b < total ? (total - b + G - 1u) / G : 0u;   // rays j = b, b+G, b+2G, ...
     bool active = false, exhausted = n == 0;
     Ray r;
     float tlim = 0.0f;
@@ -291,29 +310,22 @@ __global__ __launch_bounds__(kBlock) void k_occlude(rtk::DevScene s, PcParams p)
             if (idle) {
                 const unsigned base = wave_grab_lds(&g_head, idle);
                 if (base + (unsigned)__popcll(idle) >= n) exhausted = true;
-                // region of the wave's first index (binary search, wave-uniform), then per lane
-                int reg = 0;
-                {
-                    const unsigned j0 = lo + base;
-                    int a = 0, b = GC;                       // g_prefix[a] <= j0 < g_prefix[b]
-                    while (b - a > 1) {
-                        const int m = (a + b) >> 1;
-                        if (g_prefix[m] <= j0) a = m; else b = m;
-                    }
-                    reg = a;
-                }
                 if (!active) {
                     const unsigned idx = base + lane_rank(idle);
                     if (idx < n) {
-                        const unsigned j = lo + idx;
-                        while (j >= g_prefix[reg + 1]) ++reg;
-                        const float4* sray = p.sray + 2 * ((size_t)reg * p.block_scap + (j - g_prefix[reg]));
-                        const float4 a = ld_nt(sray), b = ld_nt(sray + 1);
-                        r = make_ray(V{a.x, a.y, a.z}, V{b.x, b.y, b.z});
-                        tlim = b.w;
+                        const unsigned j = b + idx * G;
+                        int lo = 0, hi = GC;                       // g_pref[lo] <= j < g_pref[hi]
+                        while (hi - lo > 1) {
+                            const int m = (lo + hi) >> 1;
+                            if (g_pref[m] <= j) lo = m; else hi = m;
+                        }
+                        const float4* sray = p.sray + 2 * ((size_t)lo * p.block_scap + (j - g_pref[lo]));
+                        const float4 a = ld_nt(sray), c = ld_nt(sray + 1);
+                        r = make_ray(V{a.x, a.y, a.z}, V{c.x, c.y, c.z});
+                        tlim = c.w;
                         owner = __float_as_int(a.w);
                         nrays++;
-                        if (walk_begin<COUNT>(s, r, wk, w)) active = true;
+                        if (walk_begin<COUNT>(s, r, wk, w, true)) active = true;
                         else p.occ[owner] = 0;
                     }
                 }
@@ -323,7 +335,7 @@ __global__ __launch_bounds__(kBlock) void k_occlude(rtk::DevScene s, PcParams p)
             if (exhausted) break;
             continue;
         }
-        const int thresh = exhausted ? 0 : p.refill;
+        const int thresh = exhausted ? 0 : p.orefill;
         while (__popcll(__ballot(active)) > thresh) {
             if (active) {
                 const int res = any_step<COUNT, FetchTop>(s, r, tlim, stk, wk, w);
@@ -334,8 +346,231 @@ __global__ __launch_bounds__(kBlock) void k_occlude(rtk::DevScene s, PcParams p)
             }
         }
     }
+    if (p.trace && threadIdx.x == 0) {
+        p.trace[2 * ((size_t)p.cap + blockIdx.x)] = t_start;
+        p.trace[2 * ((size_t)p.cap + blockIdx.x) + 1] = (unsigned)wall_clock64();
+    }
     if (COUNT) {
         wave_add_counter(&p.counters[1], nrays);
+        wave_add_counter(&p.counters[3], w.nodes);
+        wave_add_counter(&p.counters[4], w.tris);
+        wave_add_counter(&p.counters[5], w.spheres);
+    }
+}
+
+// ---------------------------------------------------------------------------
+// k_fused: chains and shadow rays in ONE persistent kernel, by wave role.
+// Waves [0, P) of a workgroup are producers: exactly k_chain's loop (closest-
+// hit chains, uninterrupted by shadow work), except that each finished hit
+// appends one u32 task per light (owner id) to the wave's own queue and
+// publishes the new tail with a workgroup-scope release.  The other waves are
+// consumers from the start, and producers turn into consumers once the
+// workgroup's samples are gone: they take published tasks from any producer
+// queue (LDS CAS on the taken count), re-derive the shadow ray from the hit
+// record and walk it (any-hit).  Shadow work thus overlaps the chains instead
+// of waiting for the slowest chain of the frame (k_chain -> k_occlude).
+// Queue capacity is the worst case (every sample of the workgroup recording
+// every level), so no queue can overflow.
+// ---------------------------------------------------------------------------
+__shared__ unsigned g_pub[kBlock / 64];    // per producer wave: tasks published
+__shared__ unsigned g_take[kBlock / 64];   // per producer wave: tasks taken
+__shared__ unsigned g_live;                // producer waves still producing
+
+__device__ __forceinline__ unsigned lds_acquire(unsigned* p) {
+    return __hip_atomic_load(p, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+__device__ __forceinline__ void lds_release(unsigned* p, unsigned v) {
+    __hip_atomic_store(p, v, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+
+template <bool COUNT>
+__global__ __launch_bounds__(kBlock, RT_WAVES_PER_EU) void k_fused(rtk::DevScene s, rtk::Eye e, PcParams p) {
+    const int wave = (int)(threadIdx.x >> 6), lane = (int)(threadIdx.x & 63);
+    const int P = p.producers;
+    if (threadIdx.x < kBlock / 64) {
+        g_pub[threadIdx.x] = 0;
+        g_take[threadIdx.x] = 0;
+    }
+    if (threadIdx.x == 0) g_live = (unsigned)P;
+    block_init(s);
+    StackPriv stk;
+    Work w;
+    uint32_t nprim = 0, nrefl = 0, nshadow = 0;
+    const int nl = s.nlights;
+    unsigned* const qbase = p.wq + (size_t)blockIdx.x * (kBlock / 64) * p.wq_cap;
+    Ray r;
+    Walk wk;
+    if (wave < P) {
+        // ---- producer: k_chain's loop ----
+        const unsigned G = gridDim.x;
+        const unsigned nb = block_samples((unsigned)p.n0, G);
+        unsigned* q = qbase + (size_t)wave * p.wq_cap;
+        unsigned pub = 0;                                   // wave-uniform
+        int st = kIdle;
+        bool exhausted = nb == 0;
+        unsigned path = 0;
+        int k = 0;
+        unsigned t_grab = 0;
+        while (true) {
+            const bool done = st == kDone;
+            const bool hit = done && wk.best.prim >= 0;
+            const unsigned long long hm = __ballot(hit);
+            const unsigned hcnt = (unsigned)__popcll(hm);
+            const unsigned base = pub;
+            pub += hcnt * (unsigned)nl;
+            if (done) {
+                const HitRec h = wk.best;
+                V nn{0.0f, 0.0f, 0.0f}, pnt{0.0f, 0.0f, 0.0f};
+                int mat = 0;
+                if (hit) {
+                    hit_surface(s, r, h, &nn, &mat);
+                    const V hitp = add(r.o, mul(r.d, h.t));
+                    float4* rc = p.rec + ((size_t)k * p.cap + path) * 3;
+                    rc[0] = make_float4(hitp.x, hitp.y, hitp.z, __int_as_float(mat));
+                    rc[1] = make_float4(nn.x, nn.y, nn.z, h.t);
+                    rc[2] = make_float4(r.d.x, r.d.y, r.d.z, 0.0f);
+                    pnt = add(hitp, mul(nn, s.eps));                              // :397
+                    const unsigned rank = lane_rank(hm);
+                    const unsigned own0 = (unsigned)(((size_t)k * p.cap + path) * nl);
+                    for (int l = 0; l < nl; ++l) q[base + (unsigned)l * hcnt + rank] = own0 + (unsigned)l;
+                }
+                if (!hit) {                                                       // :442-449
+                    p.pinfo[path] = k | ((k == 0 ? kEndBg : kEndZero) << 8);
+                    st = kIdle;
+                } else if (!s.mats[mat - 1].is_mirror) {
+                    p.pinfo[path] = (k + 1) | (kEndLast << 8);
+                    st = kIdle;
+                } else if (k >= s.max_depth) {      // child beyond MaxRecursionDepth: 0 (:387-389)
+                    p.pinfo[path] = (k + 1) | (kEndZero << 8);
+                    st = kIdle;
+                } else {
+                    const V d2 = nrm(r.d);                                       // :431-435
+                    const V n2 = nrm(nn);
+                    const float rcos = dot(neg(d2), n2);
+                    r = make_ray(pnt, add(d2, mul(mul(n2, 2.0f), rcos)));
+                    ++k;
+                    nrefl++;
+                    st = walk_begin<COUNT>(s, r, wk, w) ? kTrav : kDone;
+                }
+                if (p.trace && st == kIdle) {
+                    p.trace[2 * path] = t_grab;
+                    p.trace[2 * path + 1] = (unsigned)wall_clock64();
+                }
+            }
+            if (hcnt && lane == 0) lds_release(&g_pub[wave], pub);   // records + tasks before the tail
+            if (!exhausted) {
+                const unsigned long long idle = __ballot(st == kIdle);
+                if (idle) {
+                    const unsigned gb = wave_grab_lds(&g_head, idle);
+                    if (gb + (unsigned)__popcll(idle) >= nb) exhausted = true;
+                    if (st == kIdle) {
+                        const unsigned v = gb + lane_rank(idle);
+                        if (v < nb) {
+                            const unsigned idx = block_sample(v, G, (unsigned)p.n0, (unsigned)p.spread);
+                            if (slab_sample_ray(e, p, idx, &r)) {
+                                path = idx;
+                                k = 0;
+                                nprim++;
+                                if (p.trace) t_grab = (unsigned)wall_clock64();
+                                if (s.max_depth < 0) p.pinfo[path] = 0 | (kEndZero << 8);   // depth 0 > max: black
+                                else st = walk_begin<COUNT>(s, r, wk, w) ? kTrav : kDone;
+                            }
+                        }
+                    }
+                }
+            }
+            if (!__any(st != kIdle)) {
+                if (exhausted) break;
+                continue;
+            }
+            const int thresh = exhausted ? 0 : p.refill;
+            while (__popcll(__ballot(st == kTrav)) > thresh && __popcll(__ballot(st == kDone)) < p.service) {
+                if (st == kTrav && closest_step<COUNT, FetchTop>(s, r, stk, wk, w)) st = kDone;
+            }
+        }
+        if (lane == 0) __hip_atomic_fetch_add(&g_live, -1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+    }
+    // ---- consumer: shadow tasks from every producer queue ----
+    {
+        bool active = false;
+        float tlim = 0.0f;
+        unsigned owner = 0;
+        int spin = 0;
+        while (true) {
+            const unsigned long long idle = __ballot(!active);
+            unsigned gq = 0, gt = 0, gn = 0;
+            bool live = true;
+            if (idle) {
+                const unsigned ni = (unsigned)__popcll(idle);
+                if (lane == __ffsll((unsigned long long)idle) - 1) {
+                    live = lds_acquire(&g_live) != 0;    // read before the queues: a 0 here means every tail is final
+                    for (int i = 0; i < P && gn == 0; ++i) {
+                        const int qq = (wave + i) % P;
+                        while (true) {
+                            const unsigned t = __hip_atomic_load(&g_take[qq], __ATOMIC_RELAXED,
+                                                                 __HIP_MEMORY_SCOPE_WORKGROUP);
+                            const unsigned pb = lds_acquire(&g_pub[qq]);
+                            if (pb <= t) break;
+                            const unsigned n = min(ni, pb - t);
+                            unsigned expect = t;
+                            if (__hip_atomic_compare_exchange_strong(&g_take[qq], &expect, t + n, __ATOMIC_RELAXED,
+                                                                     __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)) {
+                                gq = (unsigned)qq; gt = t; gn = n;
+                                break;
+                            }
+                        }
+                    }
+                }
+                const int leader = __ffsll((unsigned long long)idle) - 1;
+                gq = __shfl(gq, leader, 64);
+                gt = __shfl(gt, leader, 64);
+                gn = __shfl(gn, leader, 64);
+                live = __shfl((int)live, leader, 64) != 0;
+                if (!active) {
+                    const unsigned rank = lane_rank(idle);
+                    if (rank < gn) {
+                        owner = qbase[(size_t)gq * p.wq_cap + gt + rank];
+                        const unsigned lvp = owner / (unsigned)nl;
+                        const int l = (int)(owner - lvp * (unsigned)nl);
+                        const float4* rc = p.rec + (size_t)lvp * 3;
+                        const float4 a = rc[0], b = rc[1];
+                        const V pnt = add(V{a.x, a.y, a.z}, mul(V{b.x, b.y, b.z}, s.eps));   // :397
+                        const float4 lp = ld4(&s.lights[l].px);
+                        const V lpos{lp.x, lp.y, lp.z};
+                        tlim = len(sub(lpos, pnt));                                          // :400-404
+                        r = make_ray(pnt, nrm(sub(lpos, pnt)));
+                        nshadow++;
+                        if (walk_begin<COUNT>(s, r, wk, w, true)) active = true;
+                        else p.occ[owner] = 0;
+                    }
+                }
+            }
+            if (!__any(active)) {
+                if (gn == 0) {
+                    if (!live) break;                 // producers done and every queue drained
+                    __builtin_amdgcn_s_sleep(2);
+                    ++spin;
+                }
+                continue;
+            }
+            // walk until enough lanes are free (all of them once nothing is queued)
+            const int thresh = (gn > 0 || live) ? p.crefill : 0;
+            while (__popcll(__ballot(active)) > thresh) {
+                if (active) {
+                    const int res = any_step<COUNT, FetchTop>(s, r, tlim, stk, wk, w);
+                    if (res) {
+                        p.occ[owner] = res == 2 ? 1 : 0;
+                        active = false;
+                    }
+                }
+            }
+        }
+        (void)spin;
+    }
+    if (COUNT) {
+        wave_add_counter(&p.counters[0], nprim);
+        wave_add_counter(&p.counters[1], nshadow);
+        wave_add_counter(&p.counters[2], nrefl);
         wave_add_counter(&p.counters[3], w.nodes);
         wave_add_counter(&p.counters[4], w.tris);
         wave_add_counter(&p.counters[5], w.spheres);
@@ -437,6 +672,26 @@ hipError_t chain_occupancy(bool priv_stack, int* chain_blocks_per_cu, int* occlu
             e = hipOccupancyMaxActiveBlocksPerMultiprocessor(occlude_blocks_per_cu, k_occlude<false, false>, kBlock, 0);
     }
     return e;
+}
+
+hipError_t fused_occupancy(int* blocks_per_cu) {
+    return hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks_per_cu, k_fused<false>, kBlock, 0);
+}
+
+unsigned fused_wave_qcap(int n0, int grid, int levels, int nlights) {
+    return chain_block_scap(n0, grid, levels, nlights);   // a producer wave may take all of its block's samples
+}
+
+hipError_t launch_fused_chunk(const rtk::DevScene& s, const rtk::Eye& e, const PcParams& p, bool count,
+                              hipStream_t st) {
+    if (count)
+        hipLaunchKernelGGL(k_fused<true>, dim3(p.grid), dim3(kBlock), 0, st, s, e, p);
+    else
+        hipLaunchKernelGGL(k_fused<false>, dim3(p.grid), dim3(kBlock), 0, st, s, e, p);
+    const int npix = (p.chunk_rows / p.aa) * p.width;
+    hipLaunchKernelGGL(k_compose, dim3(std::max(1, std::min(p.grid, (npix + kBlock - 1) / kBlock))), dim3(kBlock),
+                       0, st, s, p);
+    return hipGetLastError();
 }
 
 unsigned chain_block_scap(int n0, int grid, int levels, int nlights) {

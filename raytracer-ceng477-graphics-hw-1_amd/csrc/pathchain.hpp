@@ -25,6 +25,8 @@
 
 namespace rtc {
 
+constexpr int kMaxChainGrid = 2048;   // k_chain workgroups (k_occlude keeps their prefix in LDS)
+
 enum PathKind : int {
     kEndBg = 0,     // deepest ray missed at depth 0: background
     kEndZero = 1,   // deepest ray missed at depth > 0, or beyond MaxRecursionDepth: black
@@ -47,9 +49,18 @@ struct PcParams {
     int grid;         // k_chain persistent grid (= number of shadow-queue regions)
     int ogrid;        // k_occlude persistent grid
     int refill;       // a wave refills once <= refill of its lanes are still walking
+    int orefill;      // the same for k_occlude
+    int service;      // ... or once >= service of its lanes finished a walk (epilogue, next bounce)
     int priv_stack;   // 1: traversal stack in private memory, 0: first entries in LDS
+    int spread;       // tiles interleaved per wave within a 256-sample unit (1, 2 or 4)
     uint8_t* out;
     unsigned long long* counters;
+    unsigned* wq;     // k_fused: per-wave task queues, [grid*4][wq_cap] u32 shadow-task owner ids
+    unsigned wq_cap;
+    int producers;    // k_fused: chain-producing waves per workgroup (1..4), the rest consume
+    int crefill;      // k_fused consumers refill once <= crefill lanes are still walking
+    unsigned* trace;  // diagnostics (RT_TRACE): [cap][2] sample {grab, chain end}, then [ogrid][2] k_occlude
+                      // workgroup {start, end}; wall clock; or null
 };
 
 // Worst-case shadow-queue slots per workgroup: every sample of the block
@@ -60,6 +71,12 @@ unsigned chain_block_scap(int n0, int grid, int levels, int nlights);
 // persistent grids are sized so every workgroup starts at t = 0 (a late-
 // starting workgroup that owns slow pixels would stretch the frame).
 hipError_t chain_occupancy(bool priv_stack, int* chain_blocks_per_cu, int* occlude_blocks_per_cu);
+
+// Fused path: k_fused (chains + shadow rays, per-wave task queues) + k_compose.
+hipError_t fused_occupancy(int* blocks_per_cu);
+unsigned fused_wave_qcap(int n0, int grid, int levels, int nlights);
+hipError_t launch_fused_chunk(const rtk::DevScene& s, const rtk::Eye& e, const PcParams& p, bool count,
+                              hipStream_t stream);
 
 hipError_t launch_chain_chunk(const rtk::DevScene& s, const rtk::Eye& e, const PcParams& p, bool count,
                               hipStream_t stream);

@@ -197,6 +197,7 @@ __device__ V trace_path(const DevScene& s, Ray ray, int* stk, float* fold, Count
             const float rc = dot(neg(d2), n2);
             ray = make_ray(p, add(d2, mul(mul(n2, 2.0f), rc)));
             ++depth;
+            if (s.prio) wave_priority(depth);
             continue;
         }
         c = vclamp(L, 0.0f, FLT_MAX);                                          // :451
@@ -232,6 +233,7 @@ __global__ __launch_bounds__(kBlock) void k_render(DevScene s, Eye e, FrameParam
     const int ocol = (blockIdx.x * 2 + (wave & 1)) * 8 + (lane & 7);
     const int lrow = (blockIdx.y * 2 + (wave >> 1)) * 8 + (lane >> 3);
     Counts cnt{0, 0, 0, 0, 0, 0};
+    const unsigned t_start = p.trace ? (unsigned)wall_clock64() : 0u;
     bool active = ocol < p.width && lrow < p.slab_rows;
     int grow = 0;
     if (active) {
@@ -252,6 +254,11 @@ __global__ __launch_bounds__(kBlock) void k_render(DevScene s, Eye e, FrameParam
         const uint32_t ff = (uint32_t)(F * F);                               // downSample :459-484
         uint8_t* o = p.out + ((size_t)lrow * p.width + ocol) * 3;
         o[0] = (uint8_t)(sr / ff); o[1] = (uint8_t)(sg / ff); o[2] = (uint8_t)(sb / ff);
+        if (p.trace) {
+            const size_t q = (size_t)lrow * p.width + ocol;
+            p.trace[2 * q] = t_start;
+            p.trace[2 * q + 1] = (unsigned)wall_clock64();
+        }
     }
     if (COUNT) {
         const unsigned long long v[6] = {cnt.primary, cnt.shadow, cnt.reflection, cnt.nodes, cnt.tris, cnt.spheres};

@@ -31,6 +31,7 @@ struct DevScene {
     int root_info;
     int pair_stack;       // LDS stack entries (8 B each) for the pair traversal
     int top_pairs;        // pairs [0, top_pairs) are the top BVH levels (cached in LDS)
+    int prio;             // 1: raise wave priority with recursion depth (RT_PRIO=0 disables)
 
     // Sphere prims carry ~sphere_index in p0.w (negative), triangles their id.
     __device__ __forceinline__ bool prim_is_sphere(int, const float4 p0) const {
@@ -52,6 +53,7 @@ struct FrameParams {
     int slab_rows;        // rows in this rank's slab
     uint8_t* out;         // slab_rows * width * 3
     unsigned long long* counters;  // 6 x u64 (RT_RENDER_COUNT)
+    unsigned* trace;      // diagnostics (RT_TRACE): per output pixel {wave start, pixel end} wall clock, or null
 };
 
 size_t render_lds_bytes(const DevScene& s);

@@ -99,12 +99,21 @@ struct rt_scene {
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
     dl::Pair* d_pairs = nullptr;
     dl::LeafBig* d_leafbig = nullptr;
-    enum Path { kChain, kWavefront, kMegakernel } path = kChain;
+    enum Path { kChain, kWavefront, kMegakernel, kFused } path = kChain;
     int grid_blocks = 2048;
     int num_cus = 256;
     int chain_grid = 0, occl_grid = 0;   // resident-sized persistent grids (lazily queried)
-    int tune_refill = 0;        // RT_REFILL
-    int tune_priv_stack = 0;    // RT_STACK=priv|lds
+    int tune_refill = -1;       // RT_REFILL (-1: path default)
+    int tune_service = -1;      // RT_SERVICE (-1: path default)
+    int fused_grid = 0;
+    int tune_producers = 3;     // RT_PROD
+    int tune_crefill = 16;      // RT_CREFILL
+    int tune_spread = 1;        // RT_SPREAD
+    int tune_orefill = 32;      // RT_OREFILL
+    int tune_priv_stack = 1;    // RT_STACK=priv|lds (chain path)
+    std::string trace_file;     // RT_TRACE: dump per-sample wall-clock timings after each render (diagnostics)
+    unsigned* d_trace = nullptr;
+    size_t trace_cap = 0;
     // chain-path workspace (grown on demand)
     struct {
         int cap = 0, levels = 0, nlights = 0;
@@ -114,15 +123,16 @@ struct rt_scene {
         uint8_t* occ = nullptr;
         unsigned* bcount = nullptr;
         unsigned* bprefix = nullptr;
-        size_t scap = 0;
+        unsigned* wq = nullptr;
+        size_t scap = 0, wq_n = 0;
         int grid = 0;
     } cw;
 
     void free_cw() {
         (void)hipFree(cw.rec); (void)hipFree(cw.pinfo); (void)hipFree(cw.sray); (void)hipFree(cw.occ);
-        (void)hipFree(cw.bcount); (void)hipFree(cw.bprefix);
-        cw.rec = cw.sray = nullptr; cw.pinfo = nullptr; cw.occ = nullptr; cw.bcount = cw.bprefix = nullptr;
-        cw.cap = cw.levels = cw.nlights = cw.grid = 0; cw.scap = 0;
+        (void)hipFree(cw.bcount); (void)hipFree(cw.bprefix); (void)hipFree(cw.wq);
+        cw.rec = cw.sray = nullptr; cw.pinfo = nullptr; cw.occ = nullptr; cw.bcount = cw.bprefix = cw.wq = nullptr;
+        cw.cap = cw.levels = cw.nlights = cw.grid = 0; cw.scap = cw.wq_n = 0;
     }
     // wavefront workspace (grown on demand)
     struct {
@@ -149,7 +159,7 @@ struct rt_scene {
         free_cw();
         (void)hipFree(d_pairs); (void)hipFree(d_leafbig);
         (void)hipFree(d_nodes); (void)hipFree(d_prims); (void)hipFree(d_tri); (void)hipFree(d_mats); (void)hipFree(d_lights);
-        (void)hipFree(d_counters); (void)hipFree(d_out);
+        (void)hipFree(d_counters); (void)hipFree(d_out); (void)hipFree(d_trace);
         if (ev0) (void)hipEventDestroy(ev0);
         if (ev1) (void)hipEventDestroy(ev1);
     }
@@ -215,14 +225,26 @@ int finish_scene(rt_scene* s, const rt_options* opts) {
     s->path = rt_scene::kChain;
     if (opts && (opts->flags & RT_OPT_WAVEFRONT)) s->path = rt_scene::kWavefront;
     if (opts && (opts->flags & RT_OPT_MEGAKERNEL)) s->path = rt_scene::kMegakernel;
+    if (opts && (opts->flags & RT_OPT_CHAIN)) s->path = rt_scene::kChain;
+    if (opts && (opts->flags & RT_OPT_FUSED)) s->path = rt_scene::kFused;
     if (const char* e = std::getenv("RT_PATH")) {
         const std::string v(e);
         if (v == "mega") s->path = rt_scene::kMegakernel;
         else if (v == "wave") s->path = rt_scene::kWavefront;
         else if (v == "chain") s->path = rt_scene::kChain;
+        else if (v == "fused") s->path = rt_scene::kFused;
     }
     if (const char* e = std::getenv("RT_REFILL")) s->tune_refill = std::max(0, std::min(63, std::atoi(e)));
+    if (const char* e = std::getenv("RT_SERVICE")) s->tune_service = std::max(1, std::min(64, std::atoi(e)));
+    if (const char* e = std::getenv("RT_SPREAD")) {
+        const int v = std::atoi(e);
+        s->tune_spread = v >= 4 ? 4 : v >= 2 ? 2 : 1;
+    }
+    if (const char* e = std::getenv("RT_OREFILL")) s->tune_orefill = std::max(0, std::min(63, std::atoi(e)));
+    if (const char* e = std::getenv("RT_PROD")) s->tune_producers = std::max(1, std::min(4, std::atoi(e)));
+    if (const char* e = std::getenv("RT_CREFILL")) s->tune_crefill = std::max(0, std::min(63, std::atoi(e)));
     if (const char* e = std::getenv("RT_STACK")) s->tune_priv_stack = std::string(e) != "lds";
+    if (const char* e = std::getenv("RT_TRACE")) s->trace_file = e;
 
     rtk::DevScene& d = s->dev;
     d.nodes = s->d_nodes; d.prims = s->d_prims; d.tri_shade = s->d_tri; d.mats = s->d_mats; d.lights = s->d_lights;
@@ -242,6 +264,8 @@ int finish_scene(rt_scene* s, const rt_options* opts) {
     d.root_info = s->bvh.root_info;
     d.pair_stack = std::max(2, s->bvh.max_stack);
     d.top_pairs = s->bvh.top_pairs;
+    d.prio = 1;
+    if (const char* e = std::getenv("RT_PRIO")) d.prio = std::atoi(e) != 0;
     if (const char* e = std::getenv("RT_TOP")) d.top_pairs = std::min(d.top_pairs, std::max(0, std::atoi(e)));
     return RT_OK;
 }
@@ -307,6 +331,35 @@ int ensure_workspace(rt_scene* s, int cap, int levels, int nlights) {
     return RT_OK;
 }
 
+// RT_TRACE diagnostics: a device buffer of n u32 and, after the frame, a raw
+// dump {magic, path, a, b, n, payload...} (see tools/trace_report.py).
+unsigned* trace_buffer(rt_scene* s, size_t n) {
+    if (s->trace_file.empty()) return nullptr;
+    if (s->trace_cap < n) {
+        (void)hipFree(s->d_trace);
+        s->d_trace = nullptr;
+        s->trace_cap = 0;
+        if (hipMalloc(reinterpret_cast<void**>(&s->d_trace), n * sizeof(unsigned)) != hipSuccess) return nullptr;
+        s->trace_cap = n;
+    }
+    (void)hipMemset(s->d_trace, 0, n * sizeof(unsigned));
+    return s->d_trace;
+}
+
+void trace_dump(rt_scene* s, hipStream_t st, unsigned path, unsigned a, unsigned b, size_t n) {
+    if (s->trace_file.empty() || !s->d_trace) return;
+    std::vector<unsigned> h(n);
+    if (hipStreamSynchronize(st) != hipSuccess ||
+        hipMemcpy(h.data(), s->d_trace, n * sizeof(unsigned), hipMemcpyDeviceToHost) != hipSuccess)
+        return;
+    if (FILE* f = std::fopen(s->trace_file.c_str(), "wb")) {
+        const unsigned hdr[5] = {0x52545452u, path, a, b, (unsigned)n};
+        std::fwrite(hdr, sizeof(unsigned), 5, f);
+        std::fwrite(h.data(), sizeof(unsigned), n, f);
+        std::fclose(f);
+    }
+}
+
 // Chunked wavefront frame: chunks are whole groups of 8*aa slab-local
 // internal rows (whole output rows, whole 8x8 tiles).
 int render_wavefront(rt_scene* s, const rtk::Eye& eye, const rtk::FrameParams& f, bool count, hipStream_t st) {
@@ -362,32 +415,38 @@ int render_chain(rt_scene* s, const rtk::Eye& eye, const rtk::FrameParams& f, bo
     const int chunk_rows = (int)units * unit;
     const size_t cap = units * unit_samples;
     if (cap * levels * nl >= (size_t)INT32_MAX) return fail(RT_ERR_LIMIT, "frame chunk too large for the chain path");
+    const bool fused = s->path == rt_scene::kFused;
     if (s->chain_grid == 0) {
-        int cb = 0, ob = 0;
-        HIP_TRY(rtc::chain_occupancy(s->tune_priv_stack != 0, &cb, &ob));
-        s->chain_grid = std::max(1, cb) * s->num_cus;
+        int cb = 0, ob = 0, fb = 0;
+        HIP_TRY(rtc::chain_occupancy(s->tune_priv_stack == 1, &cb, &ob));
+        HIP_TRY(rtc::fused_occupancy(&fb));
+        s->chain_grid = std::min(rtc::kMaxChainGrid, std::max(1, cb) * s->num_cus);
         s->occl_grid = std::max(1, ob) * s->num_cus;
-        if (const char* e = std::getenv("RT_GRID")) s->chain_grid = s->occl_grid = std::max(1, std::atoi(e));
+        s->fused_grid = std::max(1, fb) * s->num_cus;
+        if (const char* e = std::getenv("RT_GRID"))
+            s->chain_grid = s->occl_grid = s->fused_grid = std::max(1, std::min(rtc::kMaxChainGrid, std::atoi(e)));
     }
-    auto grid_for = [&](int n0) { return std::max(1, std::min(s->chain_grid, (n0 + 255) / 256)); };
+    const int max_grid = fused ? s->fused_grid : s->chain_grid;
+    auto grid_for = [&](int n0) { return std::max(1, std::min(max_grid, (n0 + 255) / 256)); };
     const int full_grid = grid_for((int)cap);
-    const size_t sray_need = (size_t)full_grid * rtc::chain_block_scap((int)cap, full_grid, levels, nl);
+    const size_t sray_need = fused ? 0 : (size_t)full_grid * rtc::chain_block_scap((int)cap, full_grid, levels, nl);
+    const size_t wq_need = fused ? (size_t)full_grid * 4 * rtc::fused_wave_qcap((int)cap, full_grid, levels, nl) : 0;
     auto& w = s->cw;
-    if (w.cap < (int)cap || w.levels < levels || w.nlights < nl || w.scap < sray_need ||
+    if (w.cap < (int)cap || w.levels < levels || w.nlights < nl || w.scap < sray_need || w.wq_n < wq_need ||
         w.grid < full_grid) {
         const int ncap = std::max<int>(w.cap, (int)cap), nlev = std::max(w.levels, levels),
                   nnl = std::max(w.nlights, nl), ngrid = std::max(w.grid, full_grid);
-        const size_t nsray = std::max<size_t>(w.scap, sray_need);
+        const size_t nsray = std::max<size_t>(w.scap, sray_need), nwq = std::max(w.wq_n, wq_need);
         s->free_cw();
         const size_t c = (size_t)ncap, rl = c * nlev;
         int rc;
         if ((rc = alloc_dev(&w.rec, 3 * rl)) || (rc = alloc_dev(&w.pinfo, c)) || (rc = alloc_dev(&w.sray, 2 * nsray)) ||
             (rc = alloc_dev(&w.occ, rl * nnl)) || (rc = alloc_dev(&w.bcount, (size_t)ngrid)) ||
-            (rc = alloc_dev(&w.bprefix, (size_t)ngrid + 1))) {
+            (rc = alloc_dev(&w.bprefix, (size_t)ngrid + 1)) || (rc = alloc_dev(&w.wq, nwq))) {
             s->free_cw();
             return rc;
         }
-        w.cap = ncap; w.levels = nlev; w.nlights = nnl; w.scap = nsray; w.grid = ngrid;
+        w.cap = ncap; w.levels = nlev; w.nlights = nnl; w.scap = nsray; w.grid = ngrid; w.wq_n = nwq;
     }
     rtc::PcParams p;
     p.width = f.width; p.height = f.height; p.aa = f.aa; p.stripe_rows = f.stripe_rows;
@@ -395,18 +454,33 @@ int render_chain(rt_scene* s, const rtk::Eye& eye, const rtk::FrameParams& f, bo
     p.wi = wi; p.tiles_x = tiles_x; p.cap = w.cap; p.levels = levels; p.nlights = s->dev.nlights;
     p.rec = w.rec; p.pinfo = w.pinfo; p.sray = w.sray; p.occ = w.occ; p.bcount = w.bcount; p.bprefix = w.bprefix;
     p.ogrid = s->occl_grid;
-    p.refill = s->tune_refill;
-    p.priv_stack = s->tune_priv_stack;
+    p.refill = s->tune_refill >= 0 ? s->tune_refill : 0;
+    p.service = s->tune_service >= 0 ? s->tune_service : 64;
+    p.producers = s->tune_producers;
+    p.orefill = s->tune_orefill;
+    p.spread = s->tune_spread;
+    p.crefill = s->tune_crefill;
+    p.priv_stack = s->tune_priv_stack == 1;
+    p.wq = w.wq;
     p.out = f.out; p.counters = f.counters;
+    const size_t trace_n = 2 * ((size_t)w.cap + (size_t)s->occl_grid);
+    p.trace = trace_buffer(s, trace_n);
     for (int r0 = 0; r0 < li; r0 += chunk_rows) {
         p.chunk_row0 = r0;
         p.chunk_rows = std::min(chunk_rows, li - r0);
         p.n0 = tiles_x * ((p.chunk_rows + 7) / 8) * 64;
         p.grid = grid_for(p.n0);
+        if (fused) {
+            p.wq_cap = rtc::fused_wave_qcap(p.n0, p.grid, levels, nl);
+            if ((size_t)p.grid * 4 * p.wq_cap > w.wq_n) return fail(RT_ERR_LIMIT, "internal: task queue too small");
+            HIP_TRY(rtc::launch_fused_chunk(s->dev, eye, p, count, st));
+            continue;
+        }
         p.block_scap = rtc::chain_block_scap(p.n0, p.grid, levels, nl);
         if ((size_t)p.grid * p.block_scap > w.scap) return fail(RT_ERR_LIMIT, "internal: shadow queue too small");
         HIP_TRY(rtc::launch_chain_chunk(s->dev, eye, p, count, st));
     }
+    if (p.trace) trace_dump(s, st, 0, (unsigned)w.cap, (unsigned)s->occl_grid, trace_n);   // last chunk only
     return RT_OK;
 }
 
@@ -560,9 +634,13 @@ int rt_render_device(rt_scene* s, const rt_camera* cam, int aa, int stripe_rows,
     p.slab_rows = rt_slab_rows(cam->image_height, stripe_rows, nranks);
     p.out = static_cast<uint8_t*>(out_dev);
     p.counters = s->d_counters;
+    p.trace = nullptr;
     const bool count = (flags & RT_RENDER_COUNT) != 0;
     if (s->path == rt_scene::kMegakernel) {
+        const size_t trace_n = 2 * (size_t)p.slab_rows * p.width;
+        p.trace = trace_buffer(s, trace_n);
         HIP_TRY(rtk::launch_render(s->dev, eye, p, count, static_cast<hipStream_t>(stream)));
+        if (p.trace) trace_dump(s, static_cast<hipStream_t>(stream), 2, (unsigned)p.width, (unsigned)p.slab_rows, trace_n);
         return RT_OK;
     }
     if (s->path == rt_scene::kWavefront) return render_wavefront(s, eye, p, count, static_cast<hipStream_t>(stream));

@@ -225,8 +225,11 @@ struct StackPriv {            // private (scratch) memory
 };
 
 // Root test (the reference's first pop).  false: nothing to traverse.
+// Any-hit pops test the box only (raytracer.cpp:268-271); closest-hit also
+// needs bt <= tMax (:184), which prunes a NaN bt.
 template <bool COUNT>
-__device__ __forceinline__ bool walk_begin(const rtk::DevScene& s, const Ray& r, Walk& k, Work& w) {
+__device__ __forceinline__ bool walk_begin(const rtk::DevScene& s, const Ray& r, Walk& k, Work& w,
+                                           bool any = false) {
     k.best = HitRec{-1.0f, -1};
     k.tmax = FLT_MAX;
     k.sp = 0;
@@ -237,7 +240,7 @@ __device__ __forceinline__ bool walk_begin(const rtk::DevScene& s, const Ray& r,
     float bt;
     const float4 lo = make_float4(s.root_lo[0], s.root_lo[1], s.root_lo[2], 0.0f);
     const float4 hi = make_float4(s.root_hi[0], s.root_hi[1], s.root_hi[2], 0.0f);
-    return box_hit(r, lo, hi, &bt) && bt <= k.tmax;   // bt NaN prunes, as in the reference
+    return box_hit(r, lo, hi, &bt) && (any || bt <= k.tmax);
 }
 
 // One closest-hit step; returns true when the walk is finished (result in k.best).
@@ -342,6 +345,75 @@ __device__ __forceinline__ int any_step(const rtk::DevScene& s, const Ray& r, fl
         const int2 e = stk.at(k.sp);
         if (COUNT) w.nodes++;
         if (e.y) {
+            k.cur = e.x;
+            return 0;
+        }
+    }
+    return 1;
+}
+
+// One step of EITHER walk, selected per lane by `any`, on one code path (no
+// divergence between lanes doing closest-hit and lanes doing any-hit):
+//   closest  tmax = best t so far; entries {info, tmin} pruned at pop by
+//            tmin <= tmax (the reference's test-at-pop);
+//   any      k.tmax = +inf; entries {info, 0 (child hit) | NaN (missed, COUNT
+//            builds only)}, so the same pop test expands exactly the hit ones;
+//            a hit closer than tlim ends the walk (occluded).
+// Returns 0 = continue, 1 = finished (closest: k.best; any: unoccluded),
+// 2 = finished occluded.
+template <bool COUNT, class FETCH, class STK>
+__device__ __forceinline__ int dual_step(const rtk::DevScene& s, const Ray& r, bool any, float tlim, STK& stk,
+                                         Walk& k, Work& w) {
+    if (k.cur >= 0) {
+        float4 l0, l1, r0, r1;
+        FETCH::pair(s, k.cur, l0, l1, r0, r1);
+        float tl, tr;
+        bool hl, hr;
+        box_pair(r, k.fast, l0, l1, r0, r1, hl, hr, tl, tr);
+        const bool left_first = comp(r.d, __float_as_int(l1.w)) > 0;
+        const int il = __float_as_int(l0.w), ir = __float_as_int(r0.w);
+        const bool hn = left_first ? hl : hr, hf = left_first ? hr : hl;
+        const float tn = left_first ? tl : tr, tf = left_first ? tr : tl;
+        const int in_ = left_first ? il : ir, if_ = left_first ? ir : il;
+        if (COUNT) w.nodes += any ? 1 : 2;
+        if (hf || (COUNT && any)) {
+            const float key = any ? (hf ? 0.0f : __int_as_float(0x7fc00000)) : tf;
+            stk.put(k.sp, make_int2(if_, __float_as_int(key)));
+            ++k.sp;
+        }
+        if (hn && (any || tn <= k.tmax)) {
+            k.cur = in_;
+            return 0;
+        }
+    } else {
+        int a, cnt;
+        leaf_range(s, k.cur, &a, &cnt);
+        for (int i = a; i < a + cnt; ++i) {
+            const float4* pr = reinterpret_cast<const float4*>(&s.prims[i]);
+            const float4 p0 = pr[0], p1 = pr[1];
+            float t;
+            bool h;
+            if (__float_as_int(p0.w) >= 0) {
+                if (COUNT) w.tris++;
+                h = tri_hit(r, p0, p1, pr[2], &t);
+            } else {
+                if (COUNT) w.spheres++;
+                h = sphere_hit(r, p0, p1, &t);
+            }
+            if (any) {
+                if (h && t < tlim) return 2;
+            } else if (h && (t < k.best.t || k.best.t == -1.0f)) {
+                k.best.t = t;
+                k.best.prim = i;
+                k.tmax = t;
+            }
+        }
+    }
+    while (k.sp > 0) {
+        --k.sp;
+        const int2 e = stk.at(k.sp);
+        if (COUNT && any) w.nodes++;               // any-hit: far child counted when popped
+        if (__int_as_float(e.y) <= k.tmax) {
             k.cur = e.x;
             return 0;
         }

@@ -12,6 +12,8 @@ import numpy as np
 import pytest
 
 from conftest import GOLDEN_DIR, config_path, golden_by_name, load_golden_image
+
+PATHS = ["fused", "chain", "wavefront", "megakernel"]
 from test_oracle import CPU_GOLDENS
 
 pytestmark = pytest.mark.gpu
@@ -37,7 +39,7 @@ def _stats(s):
             s["sphere_tests"])
 
 
-@pytest.mark.parametrize("path", ["chain", "wavefront", "megakernel"])
+@pytest.mark.parametrize("path", PATHS)
 @pytest.mark.parametrize("name", CPU_GOLDENS)
 def test_render_bit_exact(name, path, goldens, pkg, scene_dir, torch_cuda):
     g = golden_by_name(goldens, name)
@@ -71,7 +73,7 @@ def test_primary_hit_t(name, goldens, pkg, scene_dir, torch_cuda):
     assert hashlib.sha256(fm.tobytes()).hexdigest() == g["primary_hits"]["sha256_material"]
 
 
-@pytest.mark.parametrize("path", ["chain", "wavefront", "megakernel"])
+@pytest.mark.parametrize("path", PATHS)
 @pytest.mark.parametrize("nranks,stripe,gname", [(2, 8, "C3_hm_1080p_d6_aa1"), (3, 8, "C3_hm_1080p_d6_aa1"),
                                                  (8, 8, "C3_hm_1080p_d6_aa1"), (4, 5, "C3_hm_1080p_d6_aa1"),
                                                  (3, 8, "C3_hm_1080p_d6_aa2")])
@@ -99,7 +101,7 @@ def test_stripes_unshuffle_equals_full_frame(nranks, stripe, gname, path, golden
         assert np.array_equal(pkg.stripes.unshuffle(slabs.cpu().numpy(), H, stripe), ref)
 
 
-@pytest.mark.parametrize("path", ["chain", "wavefront", "megakernel"])
+@pytest.mark.parametrize("path", PATHS)
 def test_device_counters_accumulate(path, goldens, pkg, scene_dir, torch_cuda):
     torch = torch_cuda
     g = golden_by_name(goldens, "C2_cornellbox_800_d0_aa1")
@@ -125,7 +127,7 @@ def test_max_depth_override_matches_derived_scene(goldens, pkg, scene_dir, torch
     assert np.array_equal(img, load_golden_image(g["cameras"][0]))
 
 
-@pytest.mark.parametrize("path", ["chain", "wavefront", "megakernel"])
+@pytest.mark.parametrize("path", PATHS)
 def test_edge_scenes_vs_oracle(path, pkg, oracle, tmp_path, torch_cuda):
     """Empty object list (all background), negative depth (all black), odd sizes, AA 5."""
     base = pkg.scenes.scene_text("simple.xml")
@@ -158,7 +160,7 @@ def test_bad_arguments_fail_loudly(pkg, scene_dir, torch_cuda):
             s.render_device(cam, 1, 1 << 20, stripe_rows=8, rank=3, nranks=2)
 
 
-@pytest.mark.parametrize("path", ["chain", "wavefront", "megakernel"])
+@pytest.mark.parametrize("path", PATHS)
 @pytest.mark.parametrize("name", ["C5_hm_8k_d6_aa4"])
 def test_full_size_c5_sha(name, path, goldens, pkg, scene_dir, torch_cuda):
     """BASELINE config 5 at full size (7680x4320, 16 spp): sha256 of the RGB bytes."""

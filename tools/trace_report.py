@@ -1,0 +1,105 @@
+#!/usr/bin/env python3
+"""Diagnostics: render the C3 frame once per render path with RT_TRACE set and
+summarise the per-sample wall-clock trace (100 MHz counter, 10 ns ticks):
+when samples start / finish, how many are in flight over time, the slowest
+ones.  Answers "is the frame bound by bulk throughput or by its tail?".
+
+  python tools/trace_report.py [chain|megakernel ...]
+"""
+import json
+import os
+import sys
+import tempfile
+from pathlib import Path
+
+import numpy as np
+import torch
+
+sys.path.insert(0, str(Path(__file__).resolve().parent.parent))
+import __graft_entry__ as graft  # noqa: E402
+
+TICK_US = 0.01
+
+
+def load(path):
+    raw = np.fromfile(path, dtype=np.uint32)
+    assert raw[0] == 0x52545452
+    kind, a, b, n = (int(x) for x in raw[1:5])
+    return kind, a, b, raw[5:5 + n]
+
+
+def rel(x, t0):
+    return ((x.astype(np.int64) - int(t0)) & 0xffffffff).astype(np.int64) * TICK_US
+
+
+def summarise(name, starts, ends, W=None):
+    ok = ends != 0
+    idx = np.nonzero(ok)[0]
+    t0 = starts[ok].min()
+    s, e = rel(starts[ok], t0), rel(ends[ok], t0)
+    dur = e - s
+    span = e.max()
+    out = {"path": name, "samples": int(ok.sum()), "span_us": round(float(span), 1)}
+    out["end_pct_us"] = {p: round(float(np.percentile(e, p)), 1) for p in (50, 90, 99, 99.9, 100)}
+    out["start_pct_us"] = {p: round(float(np.percentile(s, p)), 1) for p in (50, 90, 99, 100)}
+    out["dur_pct_us"] = {p: round(float(np.percentile(dur, p)), 1) for p in (50, 90, 99, 99.9, 100)}
+    bins = np.linspace(0, span, 21)
+    inflight = [int(((s <= t) & (e > t)).sum()) for t in bins[:-1]]
+    out["inflight_by_5pct"] = inflight
+    top = np.argsort(dur)[::-1][:8]
+    rows = []
+    for j in top:
+        q = int(idx[j])
+        rows.append({"q": q, "rc": [q // W, q % W] if W else None, "start": round(float(s[j]), 1),
+                     "dur": round(float(dur[j]), 1)})
+    out["slowest"] = rows
+    last = np.argsort(e)[::-1][:5]
+    out["last_to_finish"] = [{"q": int(idx[j]), "start": round(float(s[j]), 1), "dur": round(float(dur[j]), 1)}
+                             for j in last]
+    return out
+
+
+def main():
+    paths = sys.argv[1:] or ["chain", "megakernel"]
+    pkg = graft.import_pkg()
+    d = tempfile.mkdtemp()
+    xml = pkg.scenes.write_config("C3_hm_1080p_d6", d)
+    dev = torch.device("cuda", 0)
+    st = torch.cuda.current_stream(dev)
+    res = []
+    for path in paths:
+        tf = os.path.join(d, f"trace_{path}.bin")
+        os.environ["RT_TRACE"] = tf
+        sc = pkg.Scene.from_xml(xml, device=0, render_path=path)
+        cam = sc.camera(0)
+        out = torch.empty((cam.image_height, cam.image_width, 3), dtype=torch.uint8, device=dev)
+        for _ in range(3):
+            sc.render_device(cam, 1, out.data_ptr(), st.cuda_stream)
+        torch.cuda.synchronize()
+        kind, a, b, tr = load(tf)
+        if kind == 2:     # megakernel: per output pixel
+            res.append(summarise(path, tr[0::2], tr[1::2], W=a))
+        else:             # chain: samples then k_occlude blocks
+            cap, og = a, b
+            smp = tr[:2 * cap]
+            r = summarise(path + "/k_chain", smp[0::2], smp[1::2])
+            ob = tr[2 * cap:2 * (cap + og)]
+            okb = ob[1::2] != 0
+            if not okb.any():
+                res.append(r)
+                sc.close()
+                del os.environ["RT_TRACE"]
+                continue
+            t0 = smp[0::2][smp[1::2] != 0].min()
+            os_, oe = rel(ob[0::2][okb], t0), rel(ob[1::2][okb], t0)
+            r["k_occlude_blocks"] = {"start_min": round(float(os_.min()), 1), "start_max": round(float(os_.max()), 1),
+                                     "end_pct_us": {p: round(float(np.percentile(oe, p)), 1) for p in (0, 50, 90, 99, 100)}}
+            res.append(r)
+        sc.close()
+        del os.environ["RT_TRACE"]
+    for r in res:
+        print(json.dumps(r))
+
+
+if __name__ == "__main__":
+    main()

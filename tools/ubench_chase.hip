@@ -10,14 +10,15 @@
 
 #define CHECK(x) do { hipError_t e = (x); if (e != hipSuccess) { printf("%s: %s\n", #x, hipGetErrorString(e)); exit(1); } } while (0)
 
-template <int VALU>
+template <int VALU, int NLD>
 __global__ __launch_bounds__(256) void chase(const float4* __restrict__ tab, int n, int steps, int* out) {
     const int tid = blockIdx.x * blockDim.x + threadIdx.x;
     int i = (int)(((long long)tid * 7919) % n);
     float acc = 0.0f;
     for (int s = 0; s < steps; ++s) {
         const float4* q = tab + 4 * (size_t)i;
-        const float4 a = q[0], b = q[1], c = q[2], d = q[3];
+        const float4 a = q[0];
+        const float4 b = NLD > 1 ? q[1] : a, c = NLD > 2 ? q[2] : a, d = NLD > 3 ? q[3] : a;
         float x = a.x + b.y + c.z + d.x;
 #pragma unroll
         for (int k = 0; k < VALU; ++k) x = x * 1.0001f + 0.5f;   // dependent VALU chain
@@ -47,12 +48,14 @@ int main(int argc, char** argv) {
     CHECK(hipEventCreate(&e1));
     int cus = 256;
     printf("{\"table_bytes\": %zu, \"steps\": %d}\n", h.size() * 4, steps);
-    for (int wpc : {1, 2, 4, 8, 16, 24, 32}) {          // waves per CU
-        for (int valu : {0, 64}) {
+    for (int wpc : {1, 4, 8, 16, 32}) {          // waves per CU
+        for (int valu : {0, 1, 2, 4}) {   // 0: 4 loads, else valu = loads per step, no VALU chain
             const int blocks = cus * wpc / 4;               // 4 waves per 256-thread block
             auto run = [&]() {
-                if (valu == 0) hipLaunchKernelGGL(chase<0>, dim3(blocks), dim3(256), 0, 0, d, n, steps, out);
-                else hipLaunchKernelGGL(chase<64>, dim3(blocks), dim3(256), 0, 0, d, n, steps, out);
+                if (valu == 0) hipLaunchKernelGGL((chase<64, 4>), dim3(blocks), dim3(256), 0, 0, d, n, steps, out);
+                else if (valu == 1) hipLaunchKernelGGL((chase<0, 1>), dim3(blocks), dim3(256), 0, 0, d, n, steps, out);
+                else if (valu == 2) hipLaunchKernelGGL((chase<0, 2>), dim3(blocks), dim3(256), 0, 0, d, n, steps, out);
+                else hipLaunchKernelGGL((chase<0, 4>), dim3(blocks), dim3(256), 0, 0, d, n, steps, out);
             };
             if (blocks < 1) continue;
             run();
