@@ -33,6 +33,14 @@ HBM_PEAK_GBPS = 8000.0     # MI355X spec (MI355X_MICROARCH.md; 6.29 TB/s measure
 # Algorithmic bytes per unit of work
 B_NODE, B_TRI, B_SPH, B_PIX = 32, 36, 16, 3
 
+# kernels one frame launches, per render path (the roofline covers all of them)
+PATH_KERNELS = {
+    "chain": ["k_chain", "k_scan", "k_occlude", "k_compose"],
+    "fused": ["k_fused", "k_compose"],
+    "megakernel": ["k_render"],
+    "wavefront": ["k_trace", "k_shadow", "k_shade", "k_fold", "k_resolve"],
+}
+
 CONFIGS = {
     "C3": ("C3_hm_1080p_d6", "horse_and_mug.xml 1920x1080, MaxRecursionDepth 6, full BVH + mirror recursion"),
     "C2": ("C2_cornellbox_800_d0", "cornellbox.xml camera 2 800x800, primary+shadow only (depth 0)"),
@@ -48,6 +56,7 @@ def parse():
     ap.add_argument("--config", default="C3", choices=sorted(CONFIGS))
     ap.add_argument("--aa", type=int, default=None, help="SSAA factor (default 1; C5: 4)")
     ap.add_argument("--stripe-rows", type=int, default=8)
+    ap.add_argument("--path", default="chain", choices=sorted(PATH_KERNELS), help="render path (all bit-identical)")
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="CPU baseline budget (rank 0, N=1)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     return ap.parse_args()
@@ -117,7 +126,7 @@ def main() -> int:
     xml = pkg.scenes.write_config(config, tmpdir)
 
     t0 = time.perf_counter()
-    scene = pkg.Scene.from_xml(xml, device=local)
+    scene = pkg.Scene.from_xml(xml, device=local, render_path=a.path)
     load_s = time.perf_counter() - t0
     cam = scene.camera(0)
     W, H, S = cam.image_width, cam.image_height, a.stripe_rows
@@ -173,6 +182,13 @@ def main() -> int:
         dist.all_reduce(tmax, op=dist.ReduceOp.MAX)
     elapsed, kern_ms_max = tmax.tolist()
 
+    traffic, traffic_src = None, None
+    tfile = ROOT / "profiles" / "traffic.json"
+    if tfile.exists():       # HBM bytes per frame from the committed rocprofv3 FETCH/WRITE passes
+        t = json.loads(tfile.read_text())
+        if t.get("config") == config and t.get("path") == a.path and t.get("hbm_bytes_per_frame"):
+            traffic = int(t["hbm_bytes_per_frame"] / world)
+            traffic_src = f"profiles/{t.get('tag')}_traffic.json (rocprofv3 2*FETCH_SIZE+WRITE_SIZE, N=1 frame / N)"
     if rank == 0:
         ms = elapsed / a.steps * 1e3
         value = ps_frame * a.steps / elapsed / 1e6
@@ -190,8 +206,10 @@ def main() -> int:
                        "mray_s_all": round((ps_frame + refl_frame) * a.steps / elapsed / 1e6, 3),
                        "scene_load_s": round(load_s, 4)},
             "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
-                         "frac": round(achieved / HBM_PEAK_GBPS, 4), "traffic": None,
-                         "kernel": "k_render", "kernel_ms": round(kern_ms, 4),
+                         "frac": round(achieved / HBM_PEAK_GBPS, 4), "traffic": traffic,
+                         "traffic_source": traffic_src,
+                         "path": a.path, "kernels": PATH_KERNELS[a.path],
+                         "kernel": "one frame = " + " + ".join(PATH_KERNELS[a.path]), "kernel_ms": round(kern_ms, 4),
                          "alg_bytes_per_launch": int(alg_bytes),
                          "counts_per_launch": {k: cnt[k] for k in ("node_visits", "tri_tests", "sphere_tests")}},
         }
