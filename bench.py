@@ -182,6 +182,15 @@ def main() -> int:
         dist.all_reduce(tmax, op=dist.ReduceOp.MAX)
     elapsed, kern_ms_max = tmax.tolist()
 
+    # PCIe-inclusive figure (rank 0, N=1 only; never `value`): rt_render = upload camera, render, D2H copy
+    host_ms = None
+    if world == 1:
+        scene.render(cam, aa)
+        t1 = time.perf_counter()
+        for _ in range(5):
+            scene.render(cam, aa)
+        host_ms = (time.perf_counter() - t1) / 5 * 1e3
+
     traffic, traffic_src = None, None
     tfile = ROOT / "profiles" / "traffic.json"
     if tfile.exists():       # HBM bytes per frame from the committed rocprofv3 FETCH/WRITE passes
@@ -204,7 +213,8 @@ def main() -> int:
                        "parallelism": f"stripes{S}x{world}" + ("+rccl_gather" if world > 1 else ""),
                        "primary_rays": prim_frame, "shadow_rays": shadow_frame, "reflection_rays": refl_frame,
                        "mray_s_all": round((ps_frame + refl_frame) * a.steps / elapsed / 1e6, 3),
-                       "scene_load_s": round(load_s, 4)},
+                       "scene_load_s": round(load_s, 4),
+                       "host_buffer_ms_per_frame": round(host_ms, 4) if host_ms else None},
             "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
                          "frac": round(achieved / HBM_PEAK_GBPS, 4), "traffic": traffic,
                          "traffic_source": traffic_src,
