@@ -493,7 +493,9 @@ int ro_export_nodes(const ro_scene* s, void* out, int capacity) {
 /* ------------------------------------------------------------------------- */
 typedef struct { v3 o, d, inv; } ray_t;
 typedef struct { float t; v3 n; int mat; int exists; } hit_t;
-typedef struct { uint64_t node, tri, sph; } work_t;
+typedef struct { uint64_t node, tri, sph, node_closest; } work_t;
+/* diagnostics: ro_work_map counts closest-hit visits only when set */
+int ro_debug_work_closest_only;
 
 /* Ray::Ray (:61-67).  NOTE: the ctor body's `direction = direction.normalize();`
  * assigns to the *parameter* (it shadows the member), so the member direction
@@ -578,7 +580,7 @@ static hit_t closest_hit(const ro_scene* s, const ray_t* r, work_t* w) {
         int ni = stack[--sp];
         const ro_node* n = &s->nodes[ni];
         float bt; int ex = box_test(r, n, &bt);
-        w->node++; NOTE_NODE(0, ni);
+        w->node++; w->node_closest++; NOTE_NODE(0, ni);
         if (ex && bt <= tMax) {
             if (!n->leaf) {
                 if (v_get(r->d, n->axis) > 0) { stack[sp++] = n->right; stack[sp++] = ni + 1; }
@@ -746,7 +748,7 @@ static void* render_worker(void* arg) {
     for (int orow = j->row_begin + j->tid; orow < j->row_end; orow += j->T) {
         for (int ocol = 0; ocol < W; ++ocol) {
             int sum[3] = {0, 0, 0};
-            const uint64_t nodes_before = x.w.node;
+            const uint64_t nodes_before = ro_debug_work_closest_only ? x.w.node_closest : x.w.node;
             for (int k = 0; k < F; ++k)
                 for (int l = 0; l < F; ++l) {
                     ray_t r = eye_gen(&j->eye, orow * F + k, ocol * F + l);
@@ -757,7 +759,7 @@ static void* render_worker(void* arg) {
                 }
             uint8_t* o = j->out + ((size_t)(orow - j->row_begin) * W + ocol) * 3;
             o[0] = (uint8_t)(sum[0] / (F * F)); o[1] = (uint8_t)(sum[1] / (F * F)); o[2] = (uint8_t)(sum[2] / (F * F));
-            if (j->work) j->work[(size_t)(orow - j->row_begin) * W + ocol] = (uint32_t)(x.w.node - nodes_before);
+            if (j->work) j->work[(size_t)(orow - j->row_begin) * W + ocol] = (uint32_t)((ro_debug_work_closest_only ? x.w.node_closest : x.w.node) - nodes_before);
         }
     }
     free(samp);

@@ -2,7 +2,9 @@
 #include "host_scene.hpp"
 
 #include <cfloat>
+#include <algorithm>
 #include <chrono>
+#include <functional>
 #include <cmath>
 #include <cstdio>
 #include <cstdlib>
@@ -386,6 +388,8 @@ inline float ibits(int32_t i) { float f; std::memcpy(&f, &i, 4); return f; }
 
 }  // namespace
 
+void build_shadow_tree(FlatBVH& out);
+
 std::string build_bvh(const HostScene& s, FlatBVH& out) {
     auto t0 = std::chrono::steady_clock::now();
     out = FlatBVH();
@@ -512,8 +516,157 @@ std::string build_bvh(const HostScene& s, FlatBVH& out) {
     // Ordered DFS pushes two children per interior pop: stack <= depth + 2.
     out.max_stack = out.max_depth + 2;
     if (out.max_stack > dl::kMaxStack) return "Error: BVH deeper than the device stack";
+    build_shadow_tree(out);
+    if (out.smax_depth + 2 > dl::kMaxStack) return "Error: occlusion tree deeper than the device stack";
     out.build_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
     return "";
+}
+
+// Occlusion (any-hit) tree.  The reference's any-hit answer is "some
+// primitive of a leaf whose box the ray hits has t < dist" (raytracer.cpp:
+// 227-280: no t pruning, the first such primitive in any order ends the
+// walk).  For a NaN-free ray the slab test is monotone under box nesting
+// (subtract and multiply are monotone in the plane coordinate), so a leaf
+// box hit implies every enclosing box is hit: the reference's reachable
+// leaves are exactly the leaves whose own box is hit, whatever hierarchy sits
+// above them.  This tree keeps the reference's leaves (same prim ranges, same
+// exact leaf boxes, tested exactly) and puts a binned-SAH hierarchy of union
+// boxes above them, so shadow rays visit far fewer nodes with the same
+// answers.  Kernels use it only for NaN-free rays outside counting passes.
+void build_shadow_tree(FlatBVH& out) {
+    struct Leaf { float lo[3], hi[3], c[3]; int32_t info; };
+    std::vector<Leaf> leaves;
+    auto add_leaf = [&](const float* lo, const float* hi, int32_t info) {
+        Leaf l;
+        for (int a = 0; a < 3; ++a) { l.lo[a] = lo[a]; l.hi[a] = hi[a]; l.c[a] = 0.5f * (lo[a] + hi[a]); }
+        l.info = info;
+        leaves.push_back(l);
+    };
+    for (const dl::Pair& p : out.pairs) {
+        if (p.l_info < 0) { const float lo[3] = {p.l_minx, p.l_miny, p.l_minz}, hi[3] = {p.l_maxx, p.l_maxy, p.l_maxz}; add_leaf(lo, hi, p.l_info); }
+        if (p.r_info < 0) { const float lo[3] = {p.r_minx, p.r_miny, p.r_minz}, hi[3] = {p.r_maxx, p.r_maxy, p.r_maxz}; add_leaf(lo, hi, p.r_info); }
+    }
+    for (int a = 0; a < 3; ++a) { out.sroot_lo[a] = out.root_lo[a]; out.sroot_hi[a] = out.root_hi[a]; }
+    out.spairs.clear();
+    out.smax_depth = 0;
+    if (leaves.size() < 2) {           // empty tree or a single root leaf: same as the reference
+        out.sroot_info = out.root_info;
+        return;
+    }
+    struct Box {
+        float lo[3] = {FLT_MAX, FLT_MAX, FLT_MAX}, hi[3] = {-FLT_MAX, -FLT_MAX, -FLT_MAX};
+        void grow(const float* l, const float* h) {
+            for (int a = 0; a < 3; ++a) { lo[a] = std::min(lo[a], l[a]); hi[a] = std::max(hi[a], h[a]); }
+        }
+        double area() const {
+            const double dx = std::max(0.0, (double)hi[0] - lo[0]), dy = std::max(0.0, (double)hi[1] - lo[1]),
+                         dz = std::max(0.0, (double)hi[2] - lo[2]);
+            return dx * dy + dy * dz + dz * dx;
+        }
+    };
+    // binned SAH over leaf centroids; each tree leaf is one reference leaf
+    struct TNode { Box box; int left = -1, right = -1, axis = 0; int32_t info = 0; };
+    std::vector<TNode> tn;
+    std::vector<int> idx(leaves.size());
+    for (size_t i = 0; i < idx.size(); ++i) idx[i] = (int)i;
+    std::function<int(int, int, int)> build = [&](int b, int e, int depth) -> int {
+        TNode node;
+        for (int i = b; i < e; ++i) node.box.grow(leaves[idx[i]].lo, leaves[idx[i]].hi);
+        out.smax_depth = std::max(out.smax_depth, depth);
+        const int me = (int)tn.size();
+        tn.push_back(node);
+        if (e - b == 1) {
+            tn[me].info = leaves[idx[b]].info;
+            return me;
+        }
+        Box cb;
+        for (int i = b; i < e; ++i) cb.grow(leaves[idx[i]].c, leaves[idx[i]].c);
+        constexpr int kBins = 32;
+        double best = 1e300;
+        int best_axis = -1, best_split = 0;
+        for (int a = 0; a < 3; ++a) {
+            const double ext = (double)cb.hi[a] - cb.lo[a];
+            if (!(ext > 0)) continue;
+            Box bb[kBins];
+            int cnt[kBins] = {0};
+            for (int i = b; i < e; ++i) {
+                const Leaf& l = leaves[idx[i]];
+                int k = (int)((l.c[a] - cb.lo[a]) / ext * kBins);
+                k = std::min(kBins - 1, std::max(0, k));
+                bb[k].grow(l.lo, l.hi);
+                cnt[k]++;
+            }
+            double right_area[kBins];
+            int right_cnt[kBins];
+            Box acc;
+            int n = 0;
+            for (int k = kBins - 1; k > 0; --k) {
+                if (cnt[k]) acc.grow(bb[k].lo, bb[k].hi);
+                n += cnt[k];
+                right_area[k] = acc.area();
+                right_cnt[k] = n;
+            }
+            Box lacc;
+            int ln = 0;
+            for (int k = 1; k < kBins; ++k) {
+                if (cnt[k - 1]) lacc.grow(bb[k - 1].lo, bb[k - 1].hi);
+                ln += cnt[k - 1];
+                if (ln == 0 || right_cnt[k] == 0) continue;
+                const double cost = lacc.area() * ln + right_area[k] * right_cnt[k];
+                if (cost < best) { best = cost; best_axis = a; best_split = k; }
+            }
+        }
+        int mid;
+        int axis = best_axis;
+        if (best_axis < 0) {                       // all centroids equal: split by count
+            axis = 0;
+            mid = (b + e) / 2;
+        } else {
+            const double ext = (double)cb.hi[axis] - cb.lo[axis];
+            auto it = std::partition(idx.begin() + b, idx.begin() + e, [&](int i) {
+                int k = (int)((leaves[i].c[axis] - cb.lo[axis]) / ext * kBins);
+                k = std::min(kBins - 1, std::max(0, k));
+                return k < best_split;
+            });
+            mid = (int)(it - idx.begin());
+            if (mid == b || mid == e) mid = (b + e) / 2;
+        }
+        const int l = build(b, mid, depth + 1);
+        const int r = build(mid, e, depth + 1);
+        tn[me].left = l;
+        tn[me].right = r;
+        tn[me].axis = axis;
+        return me;
+    };
+    const int root = build(0, (int)leaves.size(), 0);
+    // pairs in pre-order of interior nodes
+    std::vector<int32_t> pair_of(tn.size(), -1);
+    int32_t np = 0;
+    {
+        std::vector<int> st{root};
+        while (!st.empty()) {
+            const int n = st.back();
+            st.pop_back();
+            if (tn[n].left < 0) continue;
+            pair_of[n] = np++;
+            st.push_back(tn[n].right);
+            st.push_back(tn[n].left);
+        }
+    }
+    auto info = [&](int n) { return tn[n].left < 0 ? tn[n].info : pair_of[n]; };
+    out.spairs.resize(np);
+    for (size_t n = 0; n < tn.size(); ++n) {
+        if (tn[n].left < 0) continue;
+        const TNode& L = tn[tn[n].left];
+        const TNode& R = tn[tn[n].right];
+        dl::Pair& p = out.spairs[pair_of[n]];
+        p.l_minx = L.box.lo[0]; p.l_miny = L.box.lo[1]; p.l_minz = L.box.lo[2]; p.l_info = info(tn[n].left);
+        p.l_maxx = L.box.hi[0]; p.l_maxy = L.box.hi[1]; p.l_maxz = L.box.hi[2]; p.axis = tn[n].axis;
+        p.r_minx = R.box.lo[0]; p.r_miny = R.box.lo[1]; p.r_minz = R.box.lo[2]; p.r_info = info(tn[n].right);
+        p.r_maxx = R.box.hi[0]; p.r_maxy = R.box.hi[1]; p.r_maxz = R.box.hi[2]; p.pad = 0;
+    }
+    for (int a = 0; a < 3; ++a) { out.sroot_lo[a] = tn[root].box.lo[a]; out.sroot_hi[a] = tn[root].box.hi[a]; }
+    out.sroot_info = info(root);
 }
 
 }  // namespace rtx

@@ -56,6 +56,12 @@ struct FlatBVH {
     float root_lo[3] = {0, 0, 0}, root_hi[3] = {0, 0, 0};
     int32_t root_info = 0;
     int top_pairs = 0;               // pairs [0, top_pairs) = the top levels, breadth-first
+    // Occlusion tree: an SAH hierarchy over the SAME leaves (same prim ranges,
+    // same exact leaf boxes) with union boxes above them (build_shadow_tree).
+    std::vector<dl::Pair> spairs;
+    float sroot_lo[3] = {0, 0, 0}, sroot_hi[3] = {0, 0, 0};
+    int32_t sroot_info = 0;
+    int smax_depth = 0;
     int leaves = 0, max_leaf = 0, max_depth = 0, max_stack = 0;
     double build_ms = 0;
 };

@@ -36,59 +36,55 @@ constexpr int kBlock = 256;
 #ifndef RT_WAVES_PER_EU
 #define RT_WAVES_PER_EU 1
 #endif
-constexpr int kLdsStack = 8;     // stack entries kept in LDS (deeper ones in private memory)
 
 enum LaneState : int { kIdle = 0, kTrav = 1, kDone = 2 };
 
 // LDS, named directly so every access is a ds_read/ds_write (a generic
 // pointer to them would compile to flat loads that wait on vmcnt + lgkmcnt).
-__shared__ float4 g_top[4 * dl::kTopPairs];   // top BVH pairs, 16 KiB
-__shared__ int2 g_stk[kLdsStack * kBlock];     // first stack entries, [entry][thread], 16 KiB
+
+#ifndef RT_LDS_STACK
+#define RT_LDS_STACK 12
+#endif
+// Traversal stack: entries [0, kLdsStackEntries) in LDS ([entry][thread], so
+// a wave's lanes hit distinct banks), deeper ones in scratch.  LDS keeps the
+// pushes and pops off the vector-memory (TA) path that the node fetches use.
+constexpr int kLdsStackEntries = RT_LDS_STACK;
+struct StackLds {
+    int2 deep[dl::kMaxStack > kLdsStackEntries ? dl::kMaxStack - kLdsStackEntries : 1];
+    __device__ __forceinline__ void put(int i, int2 v);
+    __device__ __forceinline__ int2 at(int i);
+};
+#if RT_LDS_STACK > 0
+__shared__ int2 g_lstk[kLdsStackEntries * kBlock];
+__device__ __forceinline__ void StackLds::put(int i, int2 v) {
+    if (i < kLdsStackEntries) g_lstk[i * kBlock + threadIdx.x] = v;
+    else deep[i - kLdsStackEntries] = v;
+}
+__device__ __forceinline__ int2 StackLds::at(int i) {
+    if (i < kLdsStackEntries) return g_lstk[i * kBlock + threadIdx.x];
+    return deep[i - kLdsStackEntries];
+}
+using WalkStack = StackLds;
+#else
+using WalkStack = StackPriv;
+#endif
 __shared__ unsigned g_head;                    // block-local work queue head
 __shared__ unsigned g_scnt;                    // block-local shadow-ray count (hit lanes)
 __shared__ unsigned g_pref[kMaxChainGrid + 1]; // k_occlude: shadow-queue region prefix
 
-struct FetchTop {
-    __device__ static __forceinline__ void pair(const rtk::DevScene& s, int p, float4& l0, float4& l1, float4& r0,
-                                                float4& r1) {
-        if (p < s.top_pairs) {
-            l0 = g_top[4 * p]; l1 = g_top[4 * p + 1]; r0 = g_top[4 * p + 2]; r1 = g_top[4 * p + 3];
-        } else {
-            FetchGlobal::pair(s, p, l0, l1, r0, r1);
-        }
-    }
-};
-
-struct StackTwoTier {        // entries [0, kLdsStack) in LDS, deeper ones private
-    int2 deep[dl::kMaxStack - kLdsStack];
-    __device__ __forceinline__ void put(int i, int2 v) {
-        if (i < kLdsStack) g_stk[i * kBlock + threadIdx.x] = v;
-        else deep[i - kLdsStack] = v;
-    }
-    __device__ __forceinline__ int2 at(int i) const {
-        if (i < kLdsStack) return g_stk[i * kBlock + threadIdx.x];
-        return deep[i - kLdsStack];
-    }
-};
-
-template <bool PRIV>
-struct StackSel {
-    using type = StackTwoTier;
-};
-template <>
-struct StackSel<true> {
-    using type = StackPriv;
-};
+// Pair fetches go to global memory: caching the top BVH levels in LDS showed
+// no gain (their loads are wave-coherent and hit the L1).
+using FetchTop = FetchGlobal;
 
 __device__ __forceinline__ void block_init(const rtk::DevScene& s) {
     if (threadIdx.x == 0) {
         g_head = 0;
         g_scnt = 0;
     }
-    const float4* src = reinterpret_cast<const float4*>(s.pairs);
-    for (int i = threadIdx.x; i < 4 * s.top_pairs; i += kBlock) g_top[i] = src[i];
     __syncthreads();
 }
+
+__device__ __forceinline__ int lane_id() { return (int)(threadIdx.x & 63); }
 
 __device__ __forceinline__ unsigned lane_rank(unsigned long long mask) {
     const int lane = threadIdx.x & 63;
@@ -105,10 +101,6 @@ __device__ __forceinline__ unsigned wave_grab_lds(unsigned* ctr, unsigned long l
 }
 
 typedef float nt4 __attribute__((ext_vector_type(4)));
-__device__ __forceinline__ void st_nt(float4* p, float4 v) {
-    const nt4 x = {v.x, v.y, v.z, v.w};
-    __builtin_nontemporal_store(x, reinterpret_cast<nt4*>(p));
-}
 __device__ __forceinline__ float4 ld_nt(const float4* p) {
     const nt4 x = __builtin_nontemporal_load(reinterpret_cast<const nt4*>(p));
     return make_float4(x.x, x.y, x.z, x.w);
@@ -136,19 +128,278 @@ __device__ __forceinline__ unsigned block_sample(unsigned v, unsigned G, unsigne
 }
 
 // ---------------------------------------------------------------------------
-// k_chain: closest-hit chain of every sample (raytracer.cpp:385-439 minus the
-// shading): record each hit, queue its shadow rays, follow mirrors.
+// Wide walk: one ray, the whole wave.  For the frame's tail, where a wave has
+// only a few long walks left and its other lanes would idle.
+//
+// The wave expands the ray's box-reachable subtree in parallel (every child
+// whose box the ray hits, exactly the reference's box test, ignoring tMax;
+// up to 64 nodes or primitives per round), tests every reachable primitive,
+// and keeps the first minimum by (t, DFS position).  DFS position = the path
+// of near(0)/far(1) choices from the root (near = left iff d[axis] > 0,
+// raytracer.cpp:200-206), MSB first, then the primitive's slot in its leaf.
+//
+// Exactness.  The reference visits a subset V of the reachable set R (its
+// pops also need bt <= tMax, :184) and returns the first minimum of V.  Let w
+// be the first minimum of R.  tMax never drops below the final best, so if
+// every box on w's path has bt <= t_w, the reference reaches w: w is in V,
+// hence it is also V's first minimum.  Otherwise (non-conservative pruning:
+// the box t is in un-normalised direction units), or if any candidate t is
+// NaN or exactly -1 (the `best.t == -1` sentinel rule), or the item stack
+// would overflow, the caller falls back to the exact narrow walk.
+// Any-hit: the reference's answer is "some reachable primitive hits with
+// t < dist" whatever the order (no t pruning), so the wide walk is exact.
 // ---------------------------------------------------------------------------
-template <bool COUNT, bool PRIV>
-__global__ __launch_bounds__(kBlock, RT_WAVES_PER_EU) void k_chain(rtk::DevScene s, rtk::Eye e, PcParams p) {
-    block_init(s);
-    typename StackSel<PRIV>::type stk;
+constexpr int kWideCap = 256;                              // items per wave
+__shared__ int g_wcode[(kBlock / 64) * kWideCap];          // >= 0 pair, < 0 ~prim
+__shared__ unsigned g_wkey[(kBlock / 64) * kWideCap];      // path bits (MSB first) | depth (5 bits)
+__shared__ float g_wmax[(kBlock / 64) * kWideCap];         // max box t on the path (+inf for NaN)
+
+struct WideOut {
+    float t;
+    int prim;     // closest: winner slot or -1; any: 1 = occluded
+    int status;   // 0 = exact result, 1 = fall back to the narrow walk
+};
+
+__device__ __forceinline__ Ray ray_bcast(const Ray& r, int L) {
+    Ray q;
+    q.o = V{__shfl(r.o.x, L, 64), __shfl(r.o.y, L, 64), __shfl(r.o.z, L, 64)};
+    q.d = V{__shfl(r.d.x, L, 64), __shfl(r.d.y, L, 64), __shfl(r.d.z, L, 64)};
+    q.inv = V{__shfl(r.inv.x, L, 64), __shfl(r.inv.y, L, 64), __shfl(r.inv.z, L, 64)};
+    return q;
+}
+
+__device__ __forceinline__ float wave_minf(float v) {
+    for (int off = 32; off > 0; off >>= 1) v = fminf(v, __shfl_xor(v, off, 64));
+    return v;
+}
+__device__ __forceinline__ unsigned wave_minu(unsigned v) {
+    for (int off = 32; off > 0; off >>= 1) v = min(v, (unsigned)__shfl_xor((int)v, off, 64));
+    return v;
+}
+__device__ __forceinline__ float nan_to_inf(float t) { return t == t ? t : __int_as_float(0x7f800000); }
+
+template <bool ANY>
+__device__ WideOut wide_walk(const rtk::DevScene& s, const Ray& R, float tlim) {
+    const int lane = (int)(threadIdx.x & 63);
+    const int base = (int)(threadIdx.x >> 6) * kWideCap;
+    const float kInf = __int_as_float(0x7f800000);
+    WideOut out{-1.0f, ANY ? 0 : -1, 0};
+    if (s.nnodes <= 0) return out;
+    float bt0;
+    {
+        const float4 lo = make_float4(s.root_lo[0], s.root_lo[1], s.root_lo[2], 0.0f);
+        const float4 hi = make_float4(s.root_hi[0], s.root_hi[1], s.root_hi[2], 0.0f);
+        if (!box_hit(R, lo, hi, &bt0)) return out;
+    }
+    const bool fast = ray_nan_free(R);
+    int top;
+    if (s.root_info >= 0) {
+        if (lane == 0) {
+            g_wcode[base] = s.root_info;
+            g_wkey[base] = 0u;
+            g_wmax[base] = nan_to_inf(bt0);
+        }
+        top = 1;
+    } else {
+        int a, c;
+        leaf_range(s, s.root_info, &a, &c);
+        if (c > kWideCap) return WideOut{-1.0f, -1, 1};
+        for (int j = lane; j < c; j += 64) {
+            g_wcode[base + j] = ~(a + j);
+            g_wkey[base + j] = 0u;
+            g_wmax[base + j] = nan_to_inf(bt0);
+        }
+        top = c;
+    }
+    float bt = kInf, bm = 0.0f;          // lane-local best candidate (closest)
+    unsigned bk = 0xffffffffu, bp = 0xffffffffu;
+    bool odd = false, occl = false;
+    while (top > 0) {
+        const int n = min(64, top);
+        top -= n;
+        int code = 0;
+        unsigned key = 0;
+        float mx = 0.0f;
+        const bool has = lane < n;
+        if (has) {
+            code = g_wcode[base + top + lane];
+            key = g_wkey[base + top + lane];
+            mx = g_wmax[base + top + lane];
+        }
+        // children to push: ci[k] (info), ck[k] (key), cm[k] (path max), cs/cn (items: 1 or the leaf's prims)
+        int ci0 = 0, ci1 = 0, cs0 = 0, cs1 = 0, cn0 = 0, cn1 = 0;
+        unsigned ck0 = 0, ck1 = 0;
+        float cm0 = 0.0f, cm1 = 0.0f;
+        if (has && code >= 0) {
+            float4 l0, l1, r0, r1;
+            FetchTop::pair(s, code, l0, l1, r0, r1);
+            float tl, tr;
+            bool hl, hr;
+            if (fast) {
+                hl = box_hit_fast(R, l0, l1, &tl);
+                hr = box_hit_fast(R, r0, r1, &tr);
+            } else {
+                hl = box_hit(R, l0, l1, &tl);
+                hr = box_hit(R, r0, r1, &tr);
+            }
+            const unsigned depth = (key & 31u) + 1u;
+            const unsigned bit = 1u << (31u - depth);
+            const unsigned kb = (key & ~31u) | depth;
+            const bool left_first = comp(R.d, __float_as_int(l1.w)) > 0;
+            if (hl) {
+                ci0 = __float_as_int(l0.w);
+                ck0 = kb | (left_first ? 0u : bit);
+                cm0 = fmaxf(mx, nan_to_inf(tl));
+                if (ci0 >= 0) cn0 = 1;
+                else leaf_range(s, ci0, &cs0, &cn0);
+            }
+            if (hr) {
+                ci1 = __float_as_int(r0.w);
+                ck1 = kb | (left_first ? bit : 0u);
+                cm1 = fmaxf(mx, nan_to_inf(tr));
+                if (ci1 >= 0) cn1 = 1;
+                else leaf_range(s, ci1, &cs1, &cn1);
+            }
+        } else if (has) {
+            const int i = ~code;
+            const float4* pr = reinterpret_cast<const float4*>(&s.prims[i]);
+            const float4 p0 = pr[0], p1 = pr[1];
+            float t;
+            bool h;
+            if (__float_as_int(p0.w) >= 0) h = tri_hit(R, p0, p1, pr[2], &t);
+            else h = sphere_hit(R, p0, p1, &t);
+            if (h) {
+                if (ANY) {
+                    if (t < tlim) occl = true;
+                } else if (t != t || t == -1.0f) {
+                    odd = true;
+                } else if (t < bt || (t == bt && (key < bk || (key == bk && (unsigned)i < bp)))) {
+                    bt = t; bk = key; bp = (unsigned)i; bm = mx;
+                }
+            }
+        }
+        if (ANY && __any(occl)) return WideOut{-1.0f, 1, 0};
+        // push: exclusive prefix of the per-lane item counts
+        const int cnt = cn0 + cn1;
+        int inc = cnt;
+        for (int off = 1; off < 64; off <<= 1) {
+            const int y = __shfl_up(inc, off, 64);
+            if (lane >= off) inc += y;
+        }
+        const int total = __shfl(inc, 63, 64);
+        if (top + total > kWideCap) return WideOut{-1.0f, -1, 1};
+        int w = base + top + inc - cnt;
+        if (cn0) {
+            if (ci0 >= 0) {
+                g_wcode[w] = ci0; g_wkey[w] = ck0; g_wmax[w] = cm0; ++w;
+            } else {
+                for (int j = 0; j < cn0; ++j, ++w) { g_wcode[w] = ~(cs0 + j); g_wkey[w] = ck0; g_wmax[w] = cm0; }
+            }
+        }
+        if (cn1) {
+            if (ci1 >= 0) {
+                g_wcode[w] = ci1; g_wkey[w] = ck1; g_wmax[w] = cm1;
+            } else {
+                for (int j = 0; j < cn1; ++j, ++w) { g_wcode[w] = ~(cs1 + j); g_wkey[w] = ck1; g_wmax[w] = cm1; }
+            }
+        }
+        top += total;
+    }
+    if (ANY) return out;
+    if (__any(odd)) return WideOut{-1.0f, -1, 1};
+    const float tmin = wave_minf(bt);
+    if (!(tmin < kInf)) return out;                               // no reachable hit: the reference has none either
+    const unsigned kmin = wave_minu(bt == tmin ? bk : 0xffffffffu);
+    const unsigned pmin = wave_minu(bt == tmin && bk == kmin ? bp : 0xffffffffu);
+    const unsigned long long win = __ballot(bt == tmin && bk == kmin && bp == pmin);
+    const float wm = __shfl(bm, __ffsll((unsigned long long)win) - 1, 64);
+    if (!(wm <= tmin)) return WideOut{-1.0f, -1, 1};            // the reference might prune w's path
+    return WideOut{tmin, (int)pmin, 0};
+}
+
+// ---------------------------------------------------------------------------
+// Chain phases.  Phase A (k_chain) walks every sample's closest-hit chain up
+// to level `kinline`; a mirror bounce below it is handed on as a
+// continuation task (the record's owner id; the reflected ray is re-derived
+// from the record, raytracer.cpp:430-435).  Phase B (the chain role of k_mix)
+// walks those continuations to the end, while the other k_mix workgroups
+// already run phase A's shadow rays.  So the long mirror chains of a few
+// pixels overlap the bulk of the shadow work instead of preceding all of it.
+// Shadow tasks are u32 owner ids ((level*cap + sample)*nlights + light); the
+// shadow ray is re-derived from the hit record by the walking lane
+// (raytracer.cpp:397-404), bit-identically.
+// Work is split per workgroup (interleaved, no global atomics): samples by
+// 256-sample units, continuation and shadow tasks by index j -> j mod G.
+// ---------------------------------------------------------------------------
+__shared__ unsigned g_ccnt;    // block-local continuation count
+
+struct PhaseOut {              // where a chain phase writes its tasks
+    unsigned* sq;              // shadow tasks, region blk at sq + blk * scap
+    unsigned scap;
+    unsigned* scount;          // tasks per region
+    unsigned* cq;              // continuations (phase A only), region blk at cq + blk * ccap
+    unsigned ccap;
+    unsigned* ccount;
+    int kinline;               // deepest level walked here
+};
+
+__device__ __forceinline__ unsigned region_search(unsigned j, int nreg) {   // g_pref[r] <= j < g_pref[r+1]
+    int lo = 0, hi = nreg;
+    while (hi - lo > 1) {
+        const int m = (lo + hi) >> 1;
+        if (g_pref[m] <= j) lo = m; else hi = m;
+    }
+    return (unsigned)lo;
+}
+
+// Reflected ray of recorded level lvp = k*cap + sample (raytracer.cpp:430-435).
+__device__ __forceinline__ Ray reflect_from_record(const rtk::DevScene& s, const PcParams& p, size_t lvp) {
+    const float4* rc = p.rec + lvp * 3;
+    const float4 a = rc[0], b = rc[1], c = rc[2];
+    const V hitp{a.x, a.y, a.z}, nn{b.x, b.y, b.z}, d{c.x, c.y, c.z};
+    const V pnt = add(hitp, mul(nn, s.eps));                                            // :397
+    const V d2 = nrm(d);
+    const V n2 = nrm(nn);
+    const float rcos = dot(neg(d2), n2);
+    return make_ray(pnt, add(d2, mul(mul(n2, 2.0f), rcos)));
+}
+
+// Shadow ray of task `owner` (raytracer.cpp:397-404).
+__device__ __forceinline__ Ray shadow_from_record(const rtk::DevScene& s, const PcParams& p, unsigned owner,
+                                                  float* tlim) {
+    const unsigned lvp = owner / (unsigned)s.nlights;
+    const int l = (int)(owner - lvp * (unsigned)s.nlights);
+    const float4* rc = p.rec + (size_t)lvp * 3;
+    const float4 a = rc[0], b = rc[1];
+    const V pnt = add(V{a.x, a.y, a.z}, mul(V{b.x, b.y, b.z}, s.eps));
+    const float4 lp = ld4(&s.lights[l].px);
+    const V lpos{lp.x, lp.y, lp.z};
+    *tlim = len(sub(lpos, pnt));
+    return make_ray(pnt, nrm(sub(lpos, pnt)));
+}
+
+// Samples of workgroup blk (of G): units blk, blk+G, ... of 256 slots.
+__device__ __forceinline__ unsigned group_samples(unsigned n0, unsigned G, unsigned blk) {
+    const unsigned units = (n0 + 255u) / 256u;
+    if (blk >= units) return 0;
+    const unsigned mine = (units - 1u - blk) / G + 1u;
+    const unsigned last_unit = blk + (mine - 1u) * G;
+    return (mine - 1u) * 256u + min(256u, n0 - last_unit * 256u);
+}
+
+// closest-hit chains of one phase (raytracer.cpp:385-439 minus the shading):
+// record each hit, queue its shadow tasks, follow (or hand on) mirrors.
+template <bool COUNT, bool CONT, bool WIDE = false>
+__device__ void chain_body(const rtk::DevScene& s, const rtk::Eye& e, const PcParams& p, unsigned blk, unsigned G,
+                           const PhaseOut& o) {
+    WalkStack stk;
     Work w;
     uint32_t nprim = 0, nrefl = 0;
-    const unsigned G = gridDim.x;
-    const unsigned nb = block_samples((unsigned)p.n0, G);
     const int nl = s.nlights;
-    float4* sray = p.sray + 2 * (size_t)blockIdx.x * p.block_scap;
+    unsigned nb;
+    if (CONT) nb = blk < g_pref[p.grid] ? (g_pref[p.grid] - blk + G - 1u) / G : 0u;
+    else nb = group_samples((unsigned)p.n0, G, blk);
+    unsigned* const sq = o.sq + (size_t)blk * o.scap;
     int st = kIdle;
     bool exhausted = nb == 0;
     unsigned path = 0;
@@ -156,62 +407,61 @@ __global__ __launch_bounds__(kBlock, RT_WAVES_PER_EU) void k_chain(rtk::DevScene
     Ray r;
     Walk wk;
     unsigned t_grab = 0;
+    int wsteps = 0;          // narrow steps of the current walk (wide-walk trigger)
+    bool nowide = false;     // the wide walk fell back for this walk
     while (true) {
-        // (1) epilogue of finished walks: record, queue shadow rays, reflect
+        // (1) epilogue of finished walks: record, queue shadow tasks, reflect or hand on
         if (st == kDone) {
             const HitRec h = wk.best;
             const bool hit = h.prim >= 0;
-            V nn{0.0f, 0.0f, 0.0f}, hitp{0.0f, 0.0f, 0.0f}, pnt{0.0f, 0.0f, 0.0f};
+            V nn{0.0f, 0.0f, 0.0f}, hitp{0.0f, 0.0f, 0.0f};
             int mat = 0;
             if (hit) {
                 hit_surface(s, r, h, &nn, &mat);
                 hitp = add(r.o, mul(r.d, h.t));
                 float4* rc = p.rec + ((size_t)k * p.cap + path) * 3;
-                st_nt(rc + 0, make_float4(hitp.x, hitp.y, hitp.z, __int_as_float(mat)));
-                st_nt(rc + 1, make_float4(nn.x, nn.y, nn.z, h.t));
-                st_nt(rc + 2, make_float4(r.d.x, r.d.y, r.d.z, 0.0f));
-                pnt = add(hitp, mul(nn, s.eps));                                 // :397
+                rc[0] = make_float4(hitp.x, hitp.y, hitp.z, __int_as_float(mat));
+                rc[1] = make_float4(nn.x, nn.y, nn.z, h.t);
+                rc[2] = make_float4(r.d.x, r.d.y, r.d.z, 0.0f);
             }
-            // one shadow ray per light (:399-404), light-major within the wave
+            // one shadow task per light (:399-404), light-major within the wave
             const unsigned long long hm = __ballot(hit);
             if (hit) {
                 const unsigned cnt = (unsigned)__popcll(hm);
                 const unsigned base = wave_grab_lds(&g_scnt, hm);
                 const unsigned rank = lane_rank(hm);
-                for (int l = 0; l < nl; ++l) {
-                    const float4 lp = ld4(&s.lights[l].px);
-                    const V lpos{lp.x, lp.y, lp.z};
-                    const float dist = len(sub(lpos, pnt));
-                    const V ldir = nrm(sub(lpos, pnt));
-                    const int owner = (int)(((size_t)k * p.cap + path) * nl + l);
-                    const unsigned slot = base * nl + l * cnt + rank;
-                    st_nt(sray + 2 * slot, make_float4(pnt.x, pnt.y, pnt.z, __int_as_float(owner)));
-                    st_nt(sray + 2 * slot + 1, make_float4(ldir.x, ldir.y, ldir.z, dist));
-                }
+                const unsigned own0 = (unsigned)(((size_t)k * p.cap + path) * nl);
+                for (int l = 0; l < nl; ++l) sq[base * nl + l * cnt + rank] = own0 + (unsigned)l;
             }
+            bool ends = true;
             if (!hit) {                                                          // :442-449
                 p.pinfo[path] = k | ((k == 0 ? kEndBg : kEndZero) << 8);
-                st = kIdle;
-                if (p.trace) { p.trace[2 * path] = t_grab; p.trace[2 * path + 1] = (unsigned)wall_clock64(); }
             } else if (!s.mats[mat - 1].is_mirror) {
                 p.pinfo[path] = (k + 1) | (kEndLast << 8);
-                st = kIdle;
-                if (p.trace) { p.trace[2 * path] = t_grab; p.trace[2 * path + 1] = (unsigned)wall_clock64(); }
             } else if (k >= s.max_depth) {        // child beyond MaxRecursionDepth: 0 (:387-389)
                 p.pinfo[path] = (k + 1) | (kEndZero << 8);
-                st = kIdle;
-                if (p.trace) { p.trace[2 * path] = t_grab; p.trace[2 * path + 1] = (unsigned)wall_clock64(); }
             } else {
-                const V d2 = nrm(r.d);                                         // :431-435
-                const V n2 = nrm(nn);
-                const float rcos = dot(neg(d2), n2);
-                r = make_ray(pnt, add(d2, mul(mul(n2, 2.0f), rcos)));
+                ends = false;
+            }
+            const bool handoff = !ends && k >= o.kinline;                      // deeper levels: next phase
+            const unsigned long long cm = __ballot(handoff);
+            if (handoff) {
+                const unsigned base = wave_grab_lds(&g_ccnt, cm);
+                o.cq[(size_t)blk * o.ccap + base + lane_rank(cm)] = (unsigned)((size_t)k * p.cap + path);
+            }
+            if (ends || handoff) {
+                st = kIdle;
+                if (p.trace && !CONT) { p.trace[2 * path] = t_grab; p.trace[2 * path + 1] = (unsigned)wall_clock64(); }
+            } else {
+                r = reflect_from_record(s, p, (size_t)k * p.cap + path);
                 ++k;
                 nrefl++;
+                wsteps = nowide ? 0 : (wsteps < 0 ? p.wide_min : 0);
+                nowide = false;
                 st = walk_begin<COUNT>(s, r, wk, w) ? kTrav : kDone;
             }
         }
-        // (2) refill idle lanes with this block's next samples
+        // (2) refill idle lanes with this workgroup's next samples / continuations
         if (!exhausted) {
             const unsigned long long idle = __ballot(st == kIdle);
             if (idle) {
@@ -220,14 +470,29 @@ __global__ __launch_bounds__(kBlock, RT_WAVES_PER_EU) void k_chain(rtk::DevScene
                 if (st == kIdle) {
                     const unsigned v = base + lane_rank(idle);
                     if (v < nb) {
-                        const unsigned idx = block_sample(v, G, (unsigned)p.n0, (unsigned)p.spread);
-                        if (slab_sample_ray(e, p, idx, &r)) {
-                            path = idx;
-                            k = 0;
-                            if (p.trace) t_grab = (unsigned)wall_clock64();
-                            nprim++;
-                            if (s.max_depth < 0) p.pinfo[path] = 0 | (kEndZero << 8);   // depth 0 > max: black
-                            else st = walk_begin<COUNT>(s, r, wk, w) ? kTrav : kDone;
+                        if (CONT) {
+                            const unsigned j = blk + v * G;
+                            const unsigned reg = region_search(j, p.grid);
+                            const unsigned lvp = p.cq[(size_t)reg * p.ccapA + (j - g_pref[reg])];
+                            path = lvp % (unsigned)p.cap;
+                            k = (int)(lvp / (unsigned)p.cap) + 1;
+                            r = reflect_from_record(s, p, lvp);
+                            nrefl++;
+                            wsteps = 0;
+                            nowide = false;
+                            st = walk_begin<COUNT>(s, r, wk, w) ? kTrav : kDone;
+                        } else {
+                            const unsigned idx = (blk + (v >> 8) * G) * 256u + (v & 255u);
+                            if (slab_sample_ray(e, p, idx, &r)) {
+                                path = idx;
+                                k = 0;
+                                wsteps = 0;
+                                nowide = false;
+                                if (p.trace) t_grab = (unsigned)wall_clock64();
+                                nprim++;
+                                if (s.max_depth < 0) p.pinfo[path] = 0 | (kEndZero << 8);   // depth 0 > max: black
+                                else st = walk_begin<COUNT>(s, r, wk, w) ? kTrav : kDone;
+                            }
                         }
                     }
                 }
@@ -238,14 +503,47 @@ __global__ __launch_bounds__(kBlock, RT_WAVES_PER_EU) void k_chain(rtk::DevScene
             continue;
         }
         // (3) walk until enough lanes need service
-        if (s.prio) wave_priority(st == kTrav ? k : 0);
-        const int thresh = exhausted ? 0 : p.refill;
-        while (__popcll(__ballot(st == kTrav)) > thresh && __popcll(__ballot(st == kDone)) < p.service) {
-            if (st == kTrav && closest_step<COUNT, FetchTop>(s, r, stk, wk, w)) st = kDone;
+        const int thresh = exhausted ? 0 : (CONT ? p.brefill : p.refill);
+        if (WIDE && !COUNT && p.wide > 0) {
+            // tail: a few long walks left in this wave -> each one with the whole wave
+            const int nt = __popcll(__ballot(st == kTrav));
+            const unsigned long long wable = __ballot(st == kTrav && !nowide && (wsteps < 0 || wsteps >= p.wide_min));
+            if (wable && nt <= p.wide && nt > thresh) {
+                unsigned long long m = wable;
+                while (m) {
+                    const int L = __ffsll((unsigned long long)m) - 1;
+                    m &= m - 1;
+                    const WideOut wo = wide_walk<false>(s, ray_bcast(r, L), 0.0f);
+                    if (lane_id() == L) {
+                        if (wo.status == 0) {
+                            wk.best = HitRec{wo.t, wo.prim};
+                            st = kDone;
+                            wsteps = -1;           // heavy chain: let its next walk go wide at once
+                        } else {
+                            nowide = true;
+                        }
+                    }
+                }
+                continue;
+            }
+        }
+        while (true) {
+            const int nt = __popcll(__ballot(st == kTrav));
+            if (nt <= thresh || __popcll(__ballot(st == kDone)) >= p.service) break;
+            if (WIDE && !COUNT && p.wide > 0 && nt <= p.wide &&
+                __ballot(st == kTrav && !nowide && (wsteps < 0 || wsteps >= p.wide_min)))
+                break;
+            if (st == kTrav) {
+                ++wsteps;
+                if (closest_step<COUNT, FetchTop>(s, r, stk, wk, w)) st = kDone;
+            }
         }
     }
     __syncthreads();
-    if (threadIdx.x == 0) p.bcount[blockIdx.x] = g_scnt * (unsigned)nl;
+    if (threadIdx.x == 0) {
+        o.scount[blk] = g_scnt * (unsigned)nl;
+        if (!CONT) o.ccount[blk] = g_ccnt;
+    }
     if (COUNT) {
         wave_add_counter(&p.counters[0], nprim);
         wave_add_counter(&p.counters[2], nrefl);
@@ -255,54 +553,21 @@ __global__ __launch_bounds__(kBlock, RT_WAVES_PER_EU) void k_chain(rtk::DevScene
     }
 }
 
-// ---------------------------------------------------------------------------
-// k_scan: exclusive prefix of the per-block shadow counts (one workgroup).
-// ---------------------------------------------------------------------------
-__global__ __launch_bounds__(1024) void k_scan(PcParams p) {
-    __shared__ unsigned part[1024];
-    const int G = p.grid;
-    const int per = (G + 1023) / 1024;
-    const int b0 = threadIdx.x * per;
-    unsigned sum = 0;
-    for (int i = b0; i < min(G, b0 + per); ++i) sum += p.bcount[i];
-    part[threadIdx.x] = sum;
-    __syncthreads();
-    for (int off = 1; off < 1024; off <<= 1) {            // Hillis-Steele inclusive scan
-        const unsigned v = threadIdx.x >= (unsigned)off ? part[threadIdx.x - off] : 0u;
-        __syncthreads();
-        part[threadIdx.x] += v;
-        __syncthreads();
-    }
-    unsigned run = threadIdx.x == 0 ? 0u : part[threadIdx.x - 1];
-    for (int i = b0; i < min(G, b0 + per); ++i) {
-        p.bprefix[i] = run;
-        run += p.bcount[i];
-    }
-    if (threadIdx.x == 1023) p.bprefix[G] = part[1023];
-}
-
-// ---------------------------------------------------------------------------
-// k_occlude: any-hit of every queued shadow ray (raytracer.cpp:227-280).
-// The rays of all k_chain regions form one index space (prefix sums); each
-// workgroup takes an equal slice of it, so a region full of mirror bounces
-// is spread over the whole grid.
-// ---------------------------------------------------------------------------
-template <bool COUNT, bool PRIV>
-__global__ __launch_bounds__(kBlock, RT_WAVES_PER_EU) void k_occlude(rtk::DevScene s, PcParams p) {
-    const int GC = p.grid;
-    for (int i = threadIdx.x; i <= GC; i += kBlock) g_pref[i] = p.bprefix[i];
-    block_init(s);                                   // (its barrier also publishes g_pref)
-    typename StackSel<PRIV>::type stk;
+// any-hit of shadow tasks j = blk, blk+G, ... of the regions whose prefix is
+// in g_pref[0..nreg] (raytracer.cpp:227-280).
+template <bool COUNT>
+__device__ void occlude_body(const rtk::DevScene& s, const PcParams& p, unsigned blk, unsigned G,
+                             const unsigned* sq, unsigned scap, int nreg) {
+    WalkStack stk;
     Work w;
     uint32_t nrays = 0;
     const unsigned t_start = p.trace ? (unsigned)wall_clock64() : 0u;
-    const unsigned total = g_pref[GC];
-    const unsigned G = gridDim.x, b = blockIdx.x;
-    const unsigned n = b < total ? (total - b + G - 1u) / G : 0u;   // rays j = b, b+G, b+2G, ...
+    const unsigned total = g_pref[nreg];
+    const unsigned n = blk < total ? (total - blk + G - 1u) / G : 0u;
     bool active = false, exhausted = n == 0;
     Ray r;
     float tlim = 0.0f;
-    int owner = 0;
+    unsigned owner = 0;
     Walk wk;
     while (true) {
         if (!exhausted) {
@@ -313,17 +578,10 @@ __global__ __launch_bounds__(kBlock, RT_WAVES_PER_EU) void k_occlude(rtk::DevSce
                 if (!active) {
                     const unsigned idx = base + lane_rank(idle);
                     if (idx < n) {
-                        const unsigned j = b + idx * G;
-                        int lo = 0, hi = GC;                       // g_pref[lo] <= j < g_pref[hi]
-                        while (hi - lo > 1) {
-                            const int m = (lo + hi) >> 1;
-                            if (g_pref[m] <= j) lo = m; else hi = m;
-                        }
-                        const float4* sray = p.sray + 2 * ((size_t)lo * p.block_scap + (j - g_pref[lo]));
-                        const float4 a = ld_nt(sray), c = ld_nt(sray + 1);
-                        r = make_ray(V{a.x, a.y, a.z}, V{c.x, c.y, c.z});
-                        tlim = c.w;
-                        owner = __float_as_int(a.w);
+                        const unsigned j = blk + idx * G;
+                        const unsigned reg = region_search(j, nreg);
+                        owner = sq[(size_t)reg * scap + (j - g_pref[reg])];
+                        r = shadow_from_record(s, p, owner, &tlim);
                         nrays++;
                         if (walk_begin<COUNT>(s, r, wk, w, true)) active = true;
                         else p.occ[owner] = 0;
@@ -346,9 +604,9 @@ __global__ __launch_bounds__(kBlock, RT_WAVES_PER_EU) void k_occlude(rtk::DevSce
             }
         }
     }
-    if (p.trace && threadIdx.x == 0) {
-        p.trace[2 * ((size_t)p.cap + blockIdx.x)] = t_start;
-        p.trace[2 * ((size_t)p.cap + blockIdx.x) + 1] = (unsigned)wall_clock64();
+    if (p.trace && threadIdx.x == 0 && blk < (unsigned)p.ogrid) {
+        p.trace[2 * ((size_t)p.cap + blk)] = t_start;
+        p.trace[2 * ((size_t)p.cap + blk) + 1] = (unsigned)wall_clock64();
     }
     if (COUNT) {
         wave_add_counter(&p.counters[1], nrays);
@@ -356,6 +614,78 @@ __global__ __launch_bounds__(kBlock, RT_WAVES_PER_EU) void k_occlude(rtk::DevSce
         wave_add_counter(&p.counters[4], w.tris);
         wave_add_counter(&p.counters[5], w.spheres);
     }
+}
+
+__device__ __forceinline__ void load_prefix(const unsigned* pref, int n) {
+    for (int i = threadIdx.x; i <= n; i += kBlock) g_pref[i] = pref[i];
+}
+
+__device__ __forceinline__ PhaseOut phase_a(const PcParams& p) {
+    return PhaseOut{p.sqA, p.scapA, p.scntA, p.cq, p.ccapA, p.ccnt, p.kinline};
+}
+__device__ __forceinline__ PhaseOut phase_b(const PcParams& p) {
+    return PhaseOut{p.sqB, p.scapB, p.scntB, nullptr, 0u, nullptr, 1 << 30};
+}
+
+// Phase A: every sample, levels [0, kinline].
+template <bool COUNT>
+__global__ __launch_bounds__(kBlock, RT_WAVES_PER_EU) void k_chain(rtk::DevScene s, rtk::Eye e, PcParams p) {
+    if (threadIdx.x == 0) g_ccnt = 0;
+    block_init(s);
+    chain_body<COUNT, false>(s, e, p, blockIdx.x, gridDim.x, phase_a(p));
+}
+
+// Exclusive prefix of n counts (one 1024-thread workgroup): out[0..n].
+__device__ void scan_counts(const unsigned* cnt, unsigned* out, int n) {
+    __shared__ unsigned part[1024];
+    const int per = (n + 1023) / 1024;
+    const int b0 = threadIdx.x * per;
+    unsigned sum = 0;
+    for (int i = b0; i < min(n, b0 + per); ++i) sum += cnt[i];
+    part[threadIdx.x] = sum;
+    __syncthreads();
+    for (int off = 1; off < 1024; off <<= 1) {            // Hillis-Steele inclusive scan
+        const unsigned v = threadIdx.x >= (unsigned)off ? part[threadIdx.x - off] : 0u;
+        __syncthreads();
+        part[threadIdx.x] += v;
+        __syncthreads();
+    }
+    unsigned run = threadIdx.x == 0 ? 0u : part[threadIdx.x - 1];
+    for (int i = b0; i < min(n, b0 + per); ++i) {
+        out[i] = run;
+        run += cnt[i];
+    }
+    if (threadIdx.x == 1023) out[n] = part[1023];
+    __syncthreads();
+}
+
+// After phase A: prefixes of its shadow tasks and continuations.
+__global__ __launch_bounds__(1024) void k_scan_a(PcParams p) {
+    scan_counts(p.scntA, p.sprefA, p.grid);
+    scan_counts(p.ccnt, p.cpref, p.grid);
+}
+__global__ __launch_bounds__(1024) void k_scan_b(PcParams p) { scan_counts(p.scntB, p.sprefB, p.gb); }
+
+// Workgroups [0, gb): phase B chains (continuations); the rest: phase A's shadow tasks.
+template <bool COUNT>
+__global__ __launch_bounds__(kBlock, RT_WAVES_PER_EU) void k_mix(rtk::DevScene s, rtk::Eye e, PcParams p) {
+    const bool chain = blockIdx.x < (unsigned)p.gb;
+    if (threadIdx.x == 0) g_ccnt = 0;
+    load_prefix(chain ? p.cpref : p.sprefA, p.grid);
+    block_init(s);
+    if (chain) {
+        if (p.bprio) __builtin_amdgcn_s_setprio(3);    // the deep chains are the frame's critical path
+        chain_body<COUNT, true>(s, e, p, blockIdx.x, (unsigned)p.gb, phase_b(p));
+    }
+    else occlude_body<COUNT>(s, p, blockIdx.x - p.gb, gridDim.x - p.gb, p.sqA, p.scapA, p.grid);
+}
+
+// Phase B's shadow tasks.
+template <bool COUNT>
+__global__ __launch_bounds__(kBlock, RT_WAVES_PER_EU) void k_occlude(rtk::DevScene s, PcParams p) {
+    load_prefix(p.sprefB, p.gb);
+    block_init(s);
+    occlude_body<COUNT>(s, p, blockIdx.x, gridDim.x, p.sqB, p.scapB, p.gb);
 }
 
 // ---------------------------------------------------------------------------
@@ -393,7 +723,7 @@ __global__ __launch_bounds__(kBlock, RT_WAVES_PER_EU) void k_fused(rtk::DevScene
     }
     if (threadIdx.x == 0) g_live = (unsigned)P;
     block_init(s);
-    StackPriv stk;
+    WalkStack stk;
     Work w;
     uint32_t nprim = 0, nrefl = 0, nshadow = 0;
     const int nl = s.nlights;
@@ -660,17 +990,11 @@ __global__ __launch_bounds__(kBlock) void k_compose(rtk::DevScene s, PcParams p)
 
 }  // namespace
 
-hipError_t chain_occupancy(bool priv_stack, int* chain_blocks_per_cu, int* occlude_blocks_per_cu) {
-    hipError_t e;
-    if (priv_stack) {
-        e = hipOccupancyMaxActiveBlocksPerMultiprocessor(chain_blocks_per_cu, k_chain<false, true>, kBlock, 0);
-        if (e == hipSuccess)
-            e = hipOccupancyMaxActiveBlocksPerMultiprocessor(occlude_blocks_per_cu, k_occlude<false, true>, kBlock, 0);
-    } else {
-        e = hipOccupancyMaxActiveBlocksPerMultiprocessor(chain_blocks_per_cu, k_chain<false, false>, kBlock, 0);
-        if (e == hipSuccess)
-            e = hipOccupancyMaxActiveBlocksPerMultiprocessor(occlude_blocks_per_cu, k_occlude<false, false>, kBlock, 0);
-    }
+hipError_t chain_occupancy(int* chain_blocks_per_cu, int* mix_blocks_per_cu, int* occlude_blocks_per_cu) {
+    hipError_t e = hipOccupancyMaxActiveBlocksPerMultiprocessor(chain_blocks_per_cu, k_chain<false>, kBlock, 0);
+    if (e == hipSuccess) e = hipOccupancyMaxActiveBlocksPerMultiprocessor(mix_blocks_per_cu, k_mix<false>, kBlock, 0);
+    if (e == hipSuccess)
+        e = hipOccupancyMaxActiveBlocksPerMultiprocessor(occlude_blocks_per_cu, k_occlude<false>, kBlock, 0);
     return e;
 }
 
@@ -702,19 +1026,20 @@ unsigned chain_block_scap(int n0, int grid, int levels, int nlights) {
 
 hipError_t launch_chain_chunk(const rtk::DevScene& s, const rtk::Eye& e, const PcParams& p, bool count,
                               hipStream_t st) {
-    const dim3 blk(kBlock), grid(p.grid);
-#define RT_CHAIN_LAUNCH(C, P)                                                        \
-    do {                                                                             \
-        hipLaunchKernelGGL((k_chain<C, P>), grid, blk, 0, st, s, e, p);               \
-        hipLaunchKernelGGL(k_scan, dim3(1), dim3(1024), 0, st, p);                     \
-        hipLaunchKernelGGL((k_occlude<C, P>), dim3(p.ogrid), blk, 0, st, s, p);        \
-    } while (0)
-    if (count) {
-        if (p.priv_stack) RT_CHAIN_LAUNCH(true, true); else RT_CHAIN_LAUNCH(true, false);
-    } else {
-        if (p.priv_stack) RT_CHAIN_LAUNCH(false, true); else RT_CHAIN_LAUNCH(false, false);
+    const dim3 blk(kBlock);
+    const bool phase_b = p.kinline < s.max_depth;     // any continuation possible
+    if (count) hipLaunchKernelGGL(k_chain<true>, dim3(p.grid), blk, 0, st, s, e, p);
+    else hipLaunchKernelGGL(k_chain<false>, dim3(p.grid), blk, 0, st, s, e, p);
+    hipLaunchKernelGGL(k_scan_a, dim3(1), dim3(1024), 0, st, p);
+    PcParams q = p;
+    if (!phase_b) q.gb = 0;
+    if (count) hipLaunchKernelGGL(k_mix<true>, dim3(q.gb + p.ogrid), blk, 0, st, s, e, q);
+    else hipLaunchKernelGGL(k_mix<false>, dim3(q.gb + p.ogrid), blk, 0, st, s, e, q);
+    if (phase_b) {
+        hipLaunchKernelGGL(k_scan_b, dim3(1), dim3(1024), 0, st, p);
+        if (count) hipLaunchKernelGGL(k_occlude<true>, dim3(p.ogrid), blk, 0, st, s, p);
+        else hipLaunchKernelGGL(k_occlude<false>, dim3(p.ogrid), blk, 0, st, s, p);
     }
-#undef RT_CHAIN_LAUNCH
     const int npix = (p.chunk_rows / p.aa) * p.width;
     hipLaunchKernelGGL(k_compose, dim3(std::max(1, std::min(p.grid, (npix + kBlock - 1) / kBlock))), blk, 0, st, s,
                        p);

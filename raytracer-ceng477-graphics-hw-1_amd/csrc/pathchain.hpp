@@ -41,18 +41,33 @@ struct PcParams {
     int nlights;
     float4* rec;      // [levels][cap][3]: {hitp.xyz, mat}, {n.xyz, t}, {d.xyz, 0}
     int* pinfo;       // [cap]: nlev | kind << 8
-    float4* sray;     // [grid][block_scap][2]: {p.xyz, owner}, {ldir.xyz, dist}; owner = (level*cap+path)*nl + l
     uint8_t* occ;     // [levels][cap][nl]
-    unsigned* bcount; // [grid]: shadow rays queued by each k_chain workgroup
-    unsigned* bprefix;    // [grid + 1]: exclusive prefix of bcount (k_scan)
-    unsigned block_scap;  // shadow-queue slots per workgroup (worst case, see chain_block_scap)
+    // phase A (k_chain: levels [0, kinline]) and phase B (k_mix chain role: deeper levels).
+    // Task queues hold u32 owner ids; per-workgroup regions, counts, exclusive prefixes.
+    unsigned* sqA;    // shadow tasks of A: [grid][scapA], owner = (level*cap + sample)*nl + light
+    unsigned scapA;
+    unsigned* scntA;  // [grid]
+    unsigned* sprefA; // [grid + 1]
+    unsigned* cq;     // continuations of A: [grid][ccapA], owner = level*cap + sample of the last record
+    unsigned ccapA;
+    unsigned* ccnt;   // [grid]
+    unsigned* cpref;  // [grid + 1]
+    unsigned* sqB;    // shadow tasks of B: [gb][scapB]
+    unsigned scapB;
+    unsigned* scntB;  // [gb]
+    unsigned* sprefB; // [gb + 1]
+    int kinline;      // deepest level phase A walks (>= max_depth: no phase B)
+    int gb;           // k_mix workgroups in the chain role (the other p.ogrid ones occlude A's tasks)
     int grid;         // k_chain persistent grid (= number of shadow-queue regions)
     int ogrid;        // k_occlude persistent grid
     int refill;       // a wave refills once <= refill of its lanes are still walking
-    int orefill;      // the same for k_occlude
+    int orefill;      // the same for the shadow (any-hit) walks
+    int brefill;      // the same for phase-B chains
+    int bprio;        // 1: phase-B chain waves run at the highest issue priority
     int service;      // ... or once >= service of its lanes finished a walk (epilogue, next bounce)
-    int priv_stack;   // 1: traversal stack in private memory, 0: first entries in LDS
     int spread;       // tiles interleaved per wave within a 256-sample unit (1, 2 or 4)
+    int wide;         // wide (whole-wave) walks when <= wide lanes of a wave still walk; 0 = off
+    int wide_min;     // ... and the walk already took >= wide_min narrow steps
     uint8_t* out;
     unsigned long long* counters;
     unsigned* wq;     // k_fused: per-wave task queues, [grid*4][wq_cap] u32 shadow-task owner ids
@@ -63,14 +78,14 @@ struct PcParams {
                       // workgroup {start, end}; wall clock; or null
 };
 
-// Worst-case shadow-queue slots per workgroup: every sample of the block
-// recording every level, one ray per light.
+// Worst-case task-queue slots per workgroup: every sample of the workgroup
+// recording `levels` levels, one task per light.
 unsigned chain_block_scap(int n0, int grid, int levels, int nlights);
 
-// Resident workgroups per CU of the (non-counting) k_chain / k_occlude: the
-// persistent grids are sized so every workgroup starts at t = 0 (a late-
+// Resident workgroups per CU of the (non-counting) k_chain / k_mix / k_occlude:
+// the persistent grids are sized so every workgroup starts at t = 0 (a late-
 // starting workgroup that owns slow pixels would stretch the frame).
-hipError_t chain_occupancy(bool priv_stack, int* chain_blocks_per_cu, int* occlude_blocks_per_cu);
+hipError_t chain_occupancy(int* chain_blocks_per_cu, int* mix_blocks_per_cu, int* occlude_blocks_per_cu);
 
 // Fused path: k_fused (chains + shadow rays, per-wave task queues) + k_compose.
 hipError_t fused_occupancy(int* blocks_per_cu);

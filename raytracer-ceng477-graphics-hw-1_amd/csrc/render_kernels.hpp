@@ -32,6 +32,11 @@ struct DevScene {
     int pair_stack;       // LDS stack entries (8 B each) for the pair traversal
     int top_pairs;        // pairs [0, top_pairs) are the top BVH levels (cached in LDS)
     int prio;             // 1: raise wave priority with recursion depth (RT_PRIO=0 disables)
+    // occlusion tree (host_scene.cpp build_shadow_tree): same leaves, SAH hierarchy above them
+    const dl::Pair* spairs;
+    float sroot_lo[3], sroot_hi[3];
+    int sroot_info;
+    int use_stree;        // 1: NaN-free shadow rays walk the occlusion tree (RT_STREE=0 disables)
 
     // Sphere prims carry ~sphere_index in p0.w (negative), triangles their id.
     __device__ __forceinline__ bool prim_is_sphere(int, const float4 p0) const {

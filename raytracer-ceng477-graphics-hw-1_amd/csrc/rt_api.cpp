@@ -98,11 +98,12 @@ struct rt_scene {
     size_t out_cap = 0;
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
     dl::Pair* d_pairs = nullptr;
+    dl::Pair* d_spairs = nullptr;
     dl::LeafBig* d_leafbig = nullptr;
     enum Path { kChain, kWavefront, kMegakernel, kFused } path = kChain;
     int grid_blocks = 2048;
     int num_cus = 256;
-    int chain_grid = 0, occl_grid = 0;   // resident-sized persistent grids (lazily queried)
+    int chain_grid = 0, occl_grid = 0, mix_grid = 0;   // resident-sized persistent grids (lazily queried)
     int tune_refill = -1;       // RT_REFILL (-1: path default)
     int tune_service = -1;      // RT_SERVICE (-1: path default)
     int fused_grid = 0;
@@ -110,30 +111,19 @@ struct rt_scene {
     int tune_crefill = 16;      // RT_CREFILL
     int tune_spread = 1;        // RT_SPREAD
     int tune_orefill = 32;      // RT_OREFILL
-    int tune_priv_stack = 1;    // RT_STACK=priv|lds (chain path)
+    int tune_brefill = 32;      // RT_BREFILL
+    int tune_bprio = 1;         // RT_BPRIO
+    int tune_wide = 0;          // RT_WIDE
+    int tune_wide_min = 24;     // RT_WIDE_MIN
+    int tune_kinline = 1;       // RT_KINLINE: deepest level of phase A
+    int tune_gb = 0;            // RT_GB: phase-B chain workgroups in k_mix (0 = two per CU)
     std::string trace_file;     // RT_TRACE: dump per-sample wall-clock timings after each render (diagnostics)
     unsigned* d_trace = nullptr;
     size_t trace_cap = 0;
-    // chain-path workspace (grown on demand)
-    struct {
-        int cap = 0, levels = 0, nlights = 0;
-        float4* rec = nullptr;
-        int* pinfo = nullptr;
-        float4* sray = nullptr;
-        uint8_t* occ = nullptr;
-        unsigned* bcount = nullptr;
-        unsigned* bprefix = nullptr;
-        unsigned* wq = nullptr;
-        size_t scap = 0, wq_n = 0;
-        int grid = 0;
-    } cw;
+    // chain-path workspace: one device arena (grown on demand), carved per frame
+    char* arena = nullptr;
+    size_t arena_bytes = 0;
 
-    void free_cw() {
-        (void)hipFree(cw.rec); (void)hipFree(cw.pinfo); (void)hipFree(cw.sray); (void)hipFree(cw.occ);
-        (void)hipFree(cw.bcount); (void)hipFree(cw.bprefix); (void)hipFree(cw.wq);
-        cw.rec = cw.sray = nullptr; cw.pinfo = nullptr; cw.occ = nullptr; cw.bcount = cw.bprefix = cw.wq = nullptr;
-        cw.cap = cw.levels = cw.nlights = cw.grid = 0; cw.scap = cw.wq_n = 0;
-    }
     // wavefront workspace (grown on demand)
     struct {
         int cap = 0, levels = 0, nlights = 0;
@@ -156,8 +146,8 @@ struct rt_scene {
 
     ~rt_scene() {
         free_ws();
-        free_cw();
-        (void)hipFree(d_pairs); (void)hipFree(d_leafbig);
+        (void)hipFree(arena);
+        (void)hipFree(d_pairs); (void)hipFree(d_leafbig); (void)hipFree(d_spairs);
         (void)hipFree(d_nodes); (void)hipFree(d_prims); (void)hipFree(d_tri); (void)hipFree(d_mats); (void)hipFree(d_lights);
         (void)hipFree(d_counters); (void)hipFree(d_out); (void)hipFree(d_trace);
         if (ev0) (void)hipEventDestroy(ev0);
@@ -211,6 +201,7 @@ int finish_scene(rt_scene* s, const rt_options* opts) {
     if ((rc = upload(&s->d_lights, lights))) return rc;
     if ((rc = upload(&s->d_pairs, s->bvh.pairs))) return rc;
     if ((rc = upload(&s->d_leafbig, s->bvh.leaf_big))) return rc;
+    if ((rc = upload(&s->d_spairs, s->bvh.spairs))) return rc;
     HIP_TRY(hipMalloc(reinterpret_cast<void**>(&s->d_counters), 8 * sizeof(unsigned long long)));
     HIP_TRY(hipMemset(s->d_counters, 0, 8 * sizeof(unsigned long long)));
     HIP_TRY(hipEventCreate(&s->ev0));
@@ -240,10 +231,15 @@ int finish_scene(rt_scene* s, const rt_options* opts) {
         const int v = std::atoi(e);
         s->tune_spread = v >= 4 ? 4 : v >= 2 ? 2 : 1;
     }
+    if (const char* e = std::getenv("RT_BPRIO")) s->tune_bprio = std::atoi(e) != 0;
+    if (const char* e = std::getenv("RT_BREFILL")) s->tune_brefill = std::max(0, std::min(63, std::atoi(e)));
     if (const char* e = std::getenv("RT_OREFILL")) s->tune_orefill = std::max(0, std::min(63, std::atoi(e)));
+    if (const char* e = std::getenv("RT_WIDE")) s->tune_wide = std::max(0, std::min(64, std::atoi(e)));
+    if (const char* e = std::getenv("RT_WIDE_MIN")) s->tune_wide_min = std::max(0, std::atoi(e));
+    if (const char* e = std::getenv("RT_KINLINE")) s->tune_kinline = std::max(0, std::atoi(e));
+    if (const char* e = std::getenv("RT_GB")) s->tune_gb = std::max(0, std::atoi(e));
     if (const char* e = std::getenv("RT_PROD")) s->tune_producers = std::max(1, std::min(4, std::atoi(e)));
     if (const char* e = std::getenv("RT_CREFILL")) s->tune_crefill = std::max(0, std::min(63, std::atoi(e)));
-    if (const char* e = std::getenv("RT_STACK")) s->tune_priv_stack = std::string(e) != "lds";
     if (const char* e = std::getenv("RT_TRACE")) s->trace_file = e;
 
     rtk::DevScene& d = s->dev;
@@ -264,7 +260,15 @@ int finish_scene(rt_scene* s, const rt_options* opts) {
     d.root_info = s->bvh.root_info;
     d.pair_stack = std::max(2, s->bvh.max_stack);
     d.top_pairs = s->bvh.top_pairs;
-    d.prio = 1;
+    d.prio = 0;
+    d.spairs = s->d_spairs;
+    for (int i = 0; i < 3; ++i) {
+        d.sroot_lo[i] = s->bvh.sroot_lo[i];
+        d.sroot_hi[i] = s->bvh.sroot_hi[i];
+    }
+    d.sroot_info = s->bvh.sroot_info;
+    d.use_stree = s->bvh.spairs.empty() ? 0 : 1;
+    if (const char* e = std::getenv("RT_STREE")) d.use_stree = d.use_stree && std::atoi(e) != 0;
     if (const char* e = std::getenv("RT_PRIO")) d.prio = std::atoi(e) != 0;
     if (const char* e = std::getenv("RT_TOP")) d.top_pairs = std::min(d.top_pairs, std::max(0, std::atoi(e)));
     return RT_OK;
@@ -400,6 +404,17 @@ int render_wavefront(rt_scene* s, const rtk::Eye& eye, const rtk::FrameParams& f
 constexpr size_t kChainTargetSamples = size_t(4) << 20;
 constexpr size_t kChainBudgetBytes = size_t(6) << 30;
 
+// Bump layout of the chain-path workspace (one device arena, grown on demand).
+struct ArenaLayout {
+    size_t off = 0;
+    template <typename T>
+    size_t take(size_t n) {                   // returns the byte offset of n T's, 256-B aligned
+        const size_t o = off;
+        off += (std::max<size_t>(n, 1) * sizeof(T) + 255) & ~size_t(255);
+        return o;
+    }
+};
+
 int render_chain(rt_scene* s, const rtk::Eye& eye, const rtk::FrameParams& f, bool count, hipStream_t st) {
     const int levels = std::max(s->dev.max_depth, 0) + 1;
     const int nl = std::max(s->dev.nlights, 1);
@@ -409,7 +424,7 @@ int render_chain(rt_scene* s, const rtk::Eye& eye, const rtk::FrameParams& f, bo
     const int unit = 8 * f.aa;
     const size_t unit_samples = (size_t)tiles_x * f.aa * 64;
     const size_t units_total = (size_t)(li + unit - 1) / unit;
-    const size_t per_sample = (size_t)levels * (48 + 32 * nl + nl) + 4;
+    const size_t per_sample = (size_t)levels * (48 + 8 * nl + nl) + 16;
     const size_t target = std::max<size_t>(unit_samples, std::min(kChainTargetSamples, kChainBudgetBytes / per_sample));
     const size_t units = std::min(units_total, std::max<size_t>(1, target / unit_samples));
     const int chunk_rows = (int)units * unit;
@@ -417,70 +432,92 @@ int render_chain(rt_scene* s, const rtk::Eye& eye, const rtk::FrameParams& f, bo
     if (cap * levels * nl >= (size_t)INT32_MAX) return fail(RT_ERR_LIMIT, "frame chunk too large for the chain path");
     const bool fused = s->path == rt_scene::kFused;
     if (s->chain_grid == 0) {
-        int cb = 0, ob = 0, fb = 0;
-        HIP_TRY(rtc::chain_occupancy(s->tune_priv_stack == 1, &cb, &ob));
+        int cb = 0, mb = 0, ob = 0, fb = 0;
+        HIP_TRY(rtc::chain_occupancy(&cb, &mb, &ob));
         HIP_TRY(rtc::fused_occupancy(&fb));
         s->chain_grid = std::min(rtc::kMaxChainGrid, std::max(1, cb) * s->num_cus);
+        s->mix_grid = std::max(1, mb) * s->num_cus;
         s->occl_grid = std::max(1, ob) * s->num_cus;
         s->fused_grid = std::max(1, fb) * s->num_cus;
-        if (const char* e = std::getenv("RT_GRID"))
-            s->chain_grid = s->occl_grid = s->fused_grid = std::max(1, std::min(rtc::kMaxChainGrid, std::atoi(e)));
+        if (const char* e = std::getenv("RT_CGRID")) s->chain_grid = std::max(1, std::min(rtc::kMaxChainGrid, std::atoi(e)));
+        if (const char* e = std::getenv("RT_OGRID")) s->occl_grid = std::max(1, std::atoi(e));
+        if (const char* e = std::getenv("RT_MGRID")) s->mix_grid = std::max(2, std::atoi(e));
     }
     const int max_grid = fused ? s->fused_grid : s->chain_grid;
     auto grid_for = [&](int n0) { return std::max(1, std::min(max_grid, (n0 + 255) / 256)); };
-    const int full_grid = grid_for((int)cap);
-    const size_t sray_need = fused ? 0 : (size_t)full_grid * rtc::chain_block_scap((int)cap, full_grid, levels, nl);
-    const size_t wq_need = fused ? (size_t)full_grid * 4 * rtc::fused_wave_qcap((int)cap, full_grid, levels, nl) : 0;
-    auto& w = s->cw;
-    if (w.cap < (int)cap || w.levels < levels || w.nlights < nl || w.scap < sray_need || w.wq_n < wq_need ||
-        w.grid < full_grid) {
-        const int ncap = std::max<int>(w.cap, (int)cap), nlev = std::max(w.levels, levels),
-                  nnl = std::max(w.nlights, nl), ngrid = std::max(w.grid, full_grid);
-        const size_t nsray = std::max<size_t>(w.scap, sray_need), nwq = std::max(w.wq_n, wq_need);
-        s->free_cw();
-        const size_t c = (size_t)ncap, rl = c * nlev;
-        int rc;
-        if ((rc = alloc_dev(&w.rec, 3 * rl)) || (rc = alloc_dev(&w.pinfo, c)) || (rc = alloc_dev(&w.sray, 2 * nsray)) ||
-            (rc = alloc_dev(&w.occ, rl * nnl)) || (rc = alloc_dev(&w.bcount, (size_t)ngrid)) ||
-            (rc = alloc_dev(&w.bprefix, (size_t)ngrid + 1)) || (rc = alloc_dev(&w.wq, nwq))) {
-            s->free_cw();
-            return rc;
-        }
-        w.cap = ncap; w.levels = nlev; w.nlights = nnl; w.scap = nsray; w.grid = ngrid; w.wq_n = nwq;
+    const int G = grid_for((int)cap);
+    // phase split: A walks levels [0, kinline], B the rest (k_mix chain role, gb workgroups)
+    const int kinline = std::max(0, s->tune_kinline);
+    const bool phase_b = kinline < s->dev.max_depth;
+    const int gb = phase_b ? std::max(1, std::min(s->mix_grid - 1, s->tune_gb > 0 ? s->tune_gb : 2 * s->num_cus)) : 0;
+    const int levels_a = std::min(kinline, std::max(s->dev.max_depth, 0)) + 1;
+    const unsigned scapA = rtc::chain_block_scap((int)cap, G, levels_a, nl);
+    const unsigned ccapA = rtc::chain_block_scap((int)cap, G, 1, 1);
+    const unsigned scapB = phase_b ? (unsigned)(((cap + gb - 1) / gb) * (size_t)(levels - levels_a) * nl) : 0u;
+    const unsigned wq_cap = fused ? rtc::fused_wave_qcap((int)cap, G, levels, nl) : 0u;
+
+    ArenaLayout L;
+    const size_t o_rec = L.take<float4>(3 * cap * levels), o_pinfo = L.take<int>(cap),
+                 o_occ = L.take<uint8_t>(cap * levels * nl);
+    size_t o_sqA = 0, o_scntA = 0, o_sprefA = 0, o_cq = 0, o_ccnt = 0, o_cpref = 0, o_sqB = 0, o_scntB = 0,
+           o_sprefB = 0, o_wq = 0;
+    if (fused) {
+        o_wq = L.take<unsigned>((size_t)G * 4 * wq_cap);
+    } else {
+        o_sqA = L.take<unsigned>((size_t)G * scapA); o_scntA = L.take<unsigned>(G); o_sprefA = L.take<unsigned>(G + 1);
+        o_cq = L.take<unsigned>((size_t)G * ccapA); o_ccnt = L.take<unsigned>(G); o_cpref = L.take<unsigned>(G + 1);
+        o_sqB = L.take<unsigned>((size_t)gb * scapB); o_scntB = L.take<unsigned>(gb + 1);
+        o_sprefB = L.take<unsigned>(gb + 2);
     }
+    if (s->arena_bytes < L.off) {
+        (void)hipFree(s->arena);
+        s->arena = nullptr;
+        s->arena_bytes = 0;
+        HIP_TRY(hipMalloc(reinterpret_cast<void**>(&s->arena), L.off));
+        s->arena_bytes = L.off;
+    }
+    auto at = [&](size_t o) { return static_cast<void*>(s->arena + o); };
     rtc::PcParams p;
     p.width = f.width; p.height = f.height; p.aa = f.aa; p.stripe_rows = f.stripe_rows;
     p.rank = f.rank; p.nranks = f.nranks; p.slab_rows = f.slab_rows;
-    p.wi = wi; p.tiles_x = tiles_x; p.cap = w.cap; p.levels = levels; p.nlights = s->dev.nlights;
-    p.rec = w.rec; p.pinfo = w.pinfo; p.sray = w.sray; p.occ = w.occ; p.bcount = w.bcount; p.bprefix = w.bprefix;
-    p.ogrid = s->occl_grid;
+    p.wi = wi; p.tiles_x = tiles_x; p.cap = (int)cap; p.levels = levels; p.nlights = s->dev.nlights;
+    p.rec = static_cast<float4*>(at(o_rec));
+    p.pinfo = static_cast<int*>(at(o_pinfo));
+    p.occ = static_cast<uint8_t*>(at(o_occ));
+    p.sqA = static_cast<unsigned*>(at(o_sqA)); p.scapA = scapA;
+    p.scntA = static_cast<unsigned*>(at(o_scntA)); p.sprefA = static_cast<unsigned*>(at(o_sprefA));
+    p.cq = static_cast<unsigned*>(at(o_cq)); p.ccapA = ccapA;
+    p.ccnt = static_cast<unsigned*>(at(o_ccnt)); p.cpref = static_cast<unsigned*>(at(o_cpref));
+    p.sqB = static_cast<unsigned*>(at(o_sqB)); p.scapB = scapB;
+    p.scntB = static_cast<unsigned*>(at(o_scntB)); p.sprefB = static_cast<unsigned*>(at(o_sprefB));
+    p.kinline = phase_b ? kinline : 1 << 30;
+    p.gb = gb;
+    p.ogrid = phase_b ? std::max(1, s->mix_grid - gb) : s->mix_grid;
     p.refill = s->tune_refill >= 0 ? s->tune_refill : 0;
     p.service = s->tune_service >= 0 ? s->tune_service : 64;
     p.producers = s->tune_producers;
     p.orefill = s->tune_orefill;
+    p.brefill = s->tune_brefill;
+    p.bprio = s->tune_bprio;
+    p.wide = s->bvh.max_depth <= 26 ? s->tune_wide : 0;   // path keys hold 26 levels
+    p.wide_min = s->tune_wide_min;
     p.spread = s->tune_spread;
     p.crefill = s->tune_crefill;
-    p.priv_stack = s->tune_priv_stack == 1;
-    p.wq = w.wq;
+    p.wq = static_cast<unsigned*>(at(o_wq));
+    p.wq_cap = wq_cap;
     p.out = f.out; p.counters = f.counters;
-    const size_t trace_n = 2 * ((size_t)w.cap + (size_t)s->occl_grid);
+    const size_t trace_n = 2 * (cap + (size_t)std::max(s->mix_grid, s->occl_grid));
     p.trace = trace_buffer(s, trace_n);
     for (int r0 = 0; r0 < li; r0 += chunk_rows) {
         p.chunk_row0 = r0;
         p.chunk_rows = std::min(chunk_rows, li - r0);
         p.n0 = tiles_x * ((p.chunk_rows + 7) / 8) * 64;
         p.grid = grid_for(p.n0);
-        if (fused) {
-            p.wq_cap = rtc::fused_wave_qcap(p.n0, p.grid, levels, nl);
-            if ((size_t)p.grid * 4 * p.wq_cap > w.wq_n) return fail(RT_ERR_LIMIT, "internal: task queue too small");
-            HIP_TRY(rtc::launch_fused_chunk(s->dev, eye, p, count, st));
-            continue;
-        }
-        p.block_scap = rtc::chain_block_scap(p.n0, p.grid, levels, nl);
-        if ((size_t)p.grid * p.block_scap > w.scap) return fail(RT_ERR_LIMIT, "internal: shadow queue too small");
-        HIP_TRY(rtc::launch_chain_chunk(s->dev, eye, p, count, st));
+        if (p.grid > G) return fail(RT_ERR_LIMIT, "internal: chain grid exceeds the workspace");
+        if (fused) HIP_TRY(rtc::launch_fused_chunk(s->dev, eye, p, count, st));
+        else HIP_TRY(rtc::launch_chain_chunk(s->dev, eye, p, count, st));
     }
-    if (p.trace) trace_dump(s, st, 0, (unsigned)w.cap, (unsigned)s->occl_grid, trace_n);   // last chunk only
+    if (p.trace) trace_dump(s, st, 0, (unsigned)cap, (unsigned)p.ogrid, trace_n);   // last chunk only
     return RT_OK;
 }
 

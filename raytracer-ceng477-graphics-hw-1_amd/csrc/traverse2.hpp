@@ -183,6 +183,7 @@ __device__ __forceinline__ bool any_hit2(const rtk::DevScene& s, const Ray& r, f
 // Pairs [0, s.top_pairs) (the top levels) are read from an LDS copy.
 // ---------------------------------------------------------------------------
 struct Walk {
+    const dl::Pair* tree;   // pair array the walk indexes (the BVH, or the occlusion tree)
     int cur;       // node to process (pair index or leaf code)
     int sp;        // stack depth
     float tmax;    // closest-hit pruning bound
@@ -218,26 +219,57 @@ struct FetchGlobal {
     }
 };
 
-struct StackPriv {            // private (scratch) memory
-    int2 e[dl::kMaxStack];
-    __device__ __forceinline__ void put(int i, int2 v) { e[i] = v; }
-    __device__ __forceinline__ int2 at(int i) const { return e[i]; }
+// Fetch from the walk's own tree (BVH or occlusion tree).
+__device__ __forceinline__ void fetch_pair(const Walk& k, float4& l0, float4& l1, float4& r0, float4& r1) {
+    const float4* q = reinterpret_cast<const float4*>(&k.tree[k.cur]);
+    l0 = q[0]; l1 = q[1]; r0 = q[2]; r1 = q[3];
+}
+
+// Private (scratch) stack whose top entry lives in registers.  The walks use
+// it strictly LIFO: put(sp, v) then ++sp (push), --sp then at(sp) (pop).  A
+// pop returns the register copy at once and starts the scratch load of the
+// entry below, which has completed by the time it is needed (after the next
+// node fetch), so pops no longer put a scratch round trip on the walk's
+// dependency chain.
+struct StackPriv {
+    int2 e[dl::kMaxStack];   // entries [0, sp-1); entry sp-1 is `top`
+    int2 top;
+    __device__ __forceinline__ void put(int i, int2 v) {
+        if (i > 0) e[i - 1] = top;
+        top = v;
+    }
+    __device__ __forceinline__ int2 at(int i) {
+        const int2 v = top;
+        if (i > 0) top = e[i - 1];
+        return v;
+    }
 };
 
 // Root test (the reference's first pop).  false: nothing to traverse.
 // Any-hit pops test the box only (raytracer.cpp:268-271); closest-hit also
 // needs bt <= tMax (:184), which prunes a NaN bt.
+// Any-hit walks of NaN-free rays use the occlusion tree outside counting
+// passes (exact by the monotonicity argument at build_shadow_tree); counting
+// passes and other rays walk the reference BVH.
 template <bool COUNT>
 __device__ __forceinline__ bool walk_begin(const rtk::DevScene& s, const Ray& r, Walk& k, Work& w,
                                            bool any = false) {
     k.best = HitRec{-1.0f, -1};
     k.tmax = FLT_MAX;
     k.sp = 0;
-    k.cur = s.root_info;
     k.fast = ray_nan_free(r);
     if (s.nnodes <= 0) return false;
     if (COUNT) w.nodes++;
     float bt;
+    if (!COUNT && any && k.fast && s.use_stree) {
+        k.tree = s.spairs;
+        k.cur = s.sroot_info;
+        const float4 lo = make_float4(s.sroot_lo[0], s.sroot_lo[1], s.sroot_lo[2], 0.0f);
+        const float4 hi = make_float4(s.sroot_hi[0], s.sroot_hi[1], s.sroot_hi[2], 0.0f);
+        return box_hit(r, lo, hi, &bt);
+    }
+    k.tree = s.pairs;
+    k.cur = s.root_info;
     const float4 lo = make_float4(s.root_lo[0], s.root_lo[1], s.root_lo[2], 0.0f);
     const float4 hi = make_float4(s.root_hi[0], s.root_hi[1], s.root_hi[2], 0.0f);
     return box_hit(r, lo, hi, &bt) && (any || bt <= k.tmax);
@@ -248,7 +280,7 @@ template <bool COUNT, class FETCH, class STK>
 __device__ __forceinline__ bool closest_step(const rtk::DevScene& s, const Ray& r, STK& stk, Walk& k, Work& w) {
     if (k.cur >= 0) {
         float4 l0, l1, r0, r1;
-        FETCH::pair(s, k.cur, l0, l1, r0, r1);
+        fetch_pair(k, l0, l1, r0, r1);
         if (COUNT) w.nodes += 2;
         float tl, tr;
         bool hl, hr;
@@ -305,7 +337,7 @@ __device__ __forceinline__ int any_step(const rtk::DevScene& s, const Ray& r, fl
                                         Work& w) {
     if (k.cur >= 0) {
         float4 l0, l1, r0, r1;
-        FETCH::pair(s, k.cur, l0, l1, r0, r1);
+        fetch_pair(k, l0, l1, r0, r1);
         float tl, tr;
         bool hl, hr;
         box_pair(r, k.fast, l0, l1, r0, r1, hl, hr, tl, tr);
@@ -366,7 +398,7 @@ __device__ __forceinline__ int dual_step(const rtk::DevScene& s, const Ray& r, b
                                          Walk& k, Work& w) {
     if (k.cur >= 0) {
         float4 l0, l1, r0, r1;
-        FETCH::pair(s, k.cur, l0, l1, r0, r1);
+        fetch_pair(k, l0, l1, r0, r1);
         float tl, tr;
         bool hl, hr;
         box_pair(r, k.fast, l0, l1, r0, r1, hl, hr, tl, tr);

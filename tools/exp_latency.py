@@ -7,6 +7,7 @@ for both render paths.  Crops are re-projected cameras (narrower near plane),
 so rays differ in the last ulp from the full frame; only timing matters here.
 """
 import json
+import os
 import sys
 import tempfile
 from pathlib import Path
@@ -54,15 +55,17 @@ def timeit(scene, cam, reps=5):
 
 
 res = {}
-for mega in ("chain", "megakernel"):
+PATHS_RUN = sys.argv[1:] or ["chain", "megakernel"]
+QUICK = bool(int(os.environ.get("EXP_QUICK", "0")))
+for mega in PATHS_RUN:
     name = mega
     s = pkg.Scene.from_xml(xml, device=0, render_path=mega)
     cam = s.camera(0)
     res[name] = {"full": timeit(s, cam)}
-    for sz in (8, 16, 64, 256):
+    for sz in ((8,) if QUICK else (8, 16, 64, 256)):
         res[name][f"crop{sz}"] = timeit(s, crop(cam, 505 - sz // 2, 1310 - sz // 2, sz, sz))
     res[name]["crop_1px"] = timeit(s, crop(cam, 510, 1312, 1, 1))
-    for dep in range(0, 7):
+    for dep in (() if QUICK else range(0, 7)):
         s.set_max_depth(dep)
         res[name][f"depth{dep}"] = timeit(s, cam)
     s.close()
