@@ -50,19 +50,27 @@ enum LaneState : int { kIdle = 0, kTrav = 1, kDone = 2 };
 // pushes and pops off the vector-memory (TA) path that the node fetches use.
 constexpr int kLdsStackEntries = RT_LDS_STACK;
 struct StackLds {
-    int2 deep[dl::kMaxStack > kLdsStackEntries ? dl::kMaxStack - kLdsStackEntries : 1];
+    // Deep tier as two int arrays: loads shaped unlike the LDS int2 read, so
+    // the compiler cannot sink both tiers into one flat load through a
+    // selected pointer (which waits on vmcnt and lgkmcnt at every pop).
+    int dx[dl::kMaxStack > kLdsStackEntries ? dl::kMaxStack - kLdsStackEntries : 1];
+    int dy[dl::kMaxStack > kLdsStackEntries ? dl::kMaxStack - kLdsStackEntries : 1];
     __device__ __forceinline__ void put(int i, int2 v);
     __device__ __forceinline__ int2 at(int i);
 };
 #if RT_LDS_STACK > 0
 __shared__ int2 g_lstk[kLdsStackEntries * kBlock];
 __device__ __forceinline__ void StackLds::put(int i, int2 v) {
-    if (i < kLdsStackEntries) g_lstk[i * kBlock + threadIdx.x] = v;
-    else deep[i - kLdsStackEntries] = v;
+    if (i < kLdsStackEntries) {
+        g_lstk[i * kBlock + threadIdx.x] = v;
+    } else {
+        dx[i - kLdsStackEntries] = v.x;
+        dy[i - kLdsStackEntries] = v.y;
+    }
 }
 __device__ __forceinline__ int2 StackLds::at(int i) {
     if (i < kLdsStackEntries) return g_lstk[i * kBlock + threadIdx.x];
-    return deep[i - kLdsStackEntries];
+    return make_int2(dx[i - kLdsStackEntries], dy[i - kLdsStackEntries]);
 }
 using WalkStack = StackLds;
 #else
@@ -944,26 +952,46 @@ __device__ __forceinline__ V shade_level(const rtk::DevScene& s, const PcParams&
     return L;
 }
 
-// Recursive clamp-and-add evaluated deepest-first (raytracer.cpp:436-451).
+// k_shade: Blinn-Phong of every recorded level, one lane per (level, sample)
+// record (the levels of a path are independent here; only the fold below is
+// sequential).  L replaces the record's ray direction (rec[2].xyz), which
+// nothing needs after shading.
+__global__ __launch_bounds__(kBlock) void k_shade(rtk::DevScene s, PcParams p) {
+    const size_t n = (size_t)p.levels * (size_t)p.n0;
+    for (size_t i = (size_t)blockIdx.x * kBlock + threadIdx.x; i < n; i += (size_t)gridDim.x * kBlock) {
+        const int k = (int)(i / (size_t)p.n0);
+        const unsigned path = (unsigned)(i - (size_t)k * p.n0);
+        if (!slab_slot_valid(p, path)) continue;
+        if (k >= (p.pinfo[path] & 0xff)) continue;
+        int mat;
+        const V L = shade_level(s, p, path, k, &mat);
+        p.rec[((size_t)k * p.cap + path) * 3 + 2] = make_float4(L.x, L.y, L.z, 0.0f);
+    }
+}
+
+// Recursive clamp-and-add evaluated deepest-first (raytracer.cpp:436-451)
+// over the shaded records.
 __device__ __forceinline__ V path_color(const rtk::DevScene& s, const PcParams& p, unsigned path) {
     const int info = p.pinfo[path];
     const int nlev = info & 0xff, kind = info >> 8;
     V c = kind == kEndBg ? V{s.bgx, s.bgy, s.bgz} : V{0.0f, 0.0f, 0.0f};
     int k = nlev - 1;
-    int mat;
     if (kind == kEndLast) {
-        c = vclamp(shade_level(s, p, path, k, &mat), 0.0f, FLT_MAX);
+        const float4 L = p.rec[((size_t)k * p.cap + path) * 3 + 2];
+        c = vclamp(V{L.x, L.y, L.z}, 0.0f, FLT_MAX);
         --k;
     }
     for (; k >= 0; --k) {
-        const V L = shade_level(s, p, path, k, &mat);
+        const float4* rc = p.rec + ((size_t)k * p.cap + path) * 3;
+        const float4 L = rc[2];
+        const int mat = __float_as_int(rc[0].w);
         const float4 km = ld4(&s.mats[mat - 1].kmx);
-        c = vclamp(add(L, had(c, V{km.x, km.y, km.z})), 0.0f, FLT_MAX);
+        c = vclamp(add(V{L.x, L.y, L.z}, had(c, V{km.x, km.y, km.z})), 0.0f, FLT_MAX);
     }
     return c;
 }
 
-// k_compose: shading + fold + toPixel + ImageProcessor::downSample per output pixel
+// k_compose: fold + toPixel + ImageProcessor::downSample per output pixel
 __global__ __launch_bounds__(kBlock) void k_compose(rtk::DevScene s, PcParams p) {
     const int lr0 = p.chunk_row0 / p.aa;
     const int nrows = p.chunk_rows / p.aa;
@@ -1013,8 +1041,10 @@ hipError_t launch_fused_chunk(const rtk::DevScene& s, const rtk::Eye& e, const P
     else
         hipLaunchKernelGGL(k_fused<false>, dim3(p.grid), dim3(kBlock), 0, st, s, e, p);
     const int npix = (p.chunk_rows / p.aa) * p.width;
-    hipLaunchKernelGGL(k_compose, dim3(std::max(1, std::min(p.grid, (npix + kBlock - 1) / kBlock))), dim3(kBlock),
-                       0, st, s, p);
+    const size_t nrec = (size_t)p.levels * (size_t)p.n0;
+    hipLaunchKernelGGL(k_shade, dim3((unsigned)std::max<size_t>(1, std::min<size_t>(65535, (nrec + kBlock - 1) / kBlock))),
+                       dim3(kBlock), 0, st, s, p);
+    hipLaunchKernelGGL(k_compose, dim3(std::max(1, (npix + kBlock - 1) / kBlock)), dim3(kBlock), 0, st, s, p);
     return hipGetLastError();
 }
 
@@ -1041,8 +1071,10 @@ hipError_t launch_chain_chunk(const rtk::DevScene& s, const rtk::Eye& e, const P
         else hipLaunchKernelGGL(k_occlude<false>, dim3(p.ogrid), blk, 0, st, s, p);
     }
     const int npix = (p.chunk_rows / p.aa) * p.width;
-    hipLaunchKernelGGL(k_compose, dim3(std::max(1, std::min(p.grid, (npix + kBlock - 1) / kBlock))), blk, 0, st, s,
-                       p);
+    const size_t nrec = (size_t)p.levels * (size_t)p.n0;          // a lane per record, then a lane per pixel
+    hipLaunchKernelGGL(k_shade, dim3((unsigned)std::max<size_t>(1, std::min<size_t>(65535, (nrec + kBlock - 1) / kBlock))),
+                       blk, 0, st, s, p);
+    hipLaunchKernelGGL(k_compose, dim3(std::max(1, (npix + kBlock - 1) / kBlock)), blk, 0, st, s, p);
     return hipGetLastError();
 }
 

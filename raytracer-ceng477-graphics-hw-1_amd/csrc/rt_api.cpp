@@ -116,7 +116,7 @@ struct rt_scene {
     int tune_wide = 0;          // RT_WIDE
     int tune_wide_min = 24;     // RT_WIDE_MIN
     int tune_kinline = 1;       // RT_KINLINE: deepest level of phase A
-    int tune_gb = 0;            // RT_GB: phase-B chain workgroups in k_mix (0 = two per CU)
+    int tune_gb = 0;            // RT_GB: phase-B chain workgroups in k_mix (0 = 1.25 per CU)
     std::string trace_file;     // RT_TRACE: dump per-sample wall-clock timings after each render (diagnostics)
     unsigned* d_trace = nullptr;
     size_t trace_cap = 0;
@@ -269,6 +269,9 @@ int finish_scene(rt_scene* s, const rt_options* opts) {
     d.sroot_info = s->bvh.sroot_info;
     d.use_stree = s->bvh.spairs.empty() ? 0 : 1;
     if (const char* e = std::getenv("RT_STREE")) d.use_stree = d.use_stree && std::atoi(e) != 0;
+    // diagnostics: RT_STREE=2 also lets counting passes walk the occlusion tree (counts then
+    // measure the tree actually walked, not the reference's)
+    if (const char* e = std::getenv("RT_STREE")) d.use_stree = d.use_stree ? std::atoi(e) : 0;
     if (const char* e = std::getenv("RT_PRIO")) d.prio = std::atoi(e) != 0;
     if (const char* e = std::getenv("RT_TOP")) d.top_pairs = std::min(d.top_pairs, std::max(0, std::atoi(e)));
     return RT_OK;
@@ -449,7 +452,7 @@ int render_chain(rt_scene* s, const rtk::Eye& eye, const rtk::FrameParams& f, bo
     // phase split: A walks levels [0, kinline], B the rest (k_mix chain role, gb workgroups)
     const int kinline = std::max(0, s->tune_kinline);
     const bool phase_b = kinline < s->dev.max_depth;
-    const int gb = phase_b ? std::max(1, std::min(s->mix_grid - 1, s->tune_gb > 0 ? s->tune_gb : 2 * s->num_cus)) : 0;
+    const int gb = phase_b ? std::max(1, std::min(s->mix_grid - 1, s->tune_gb > 0 ? s->tune_gb : 5 * s->num_cus / 4)) : 0;
     const int levels_a = std::min(kinline, std::max(s->dev.max_depth, 0)) + 1;
     const unsigned scapA = rtc::chain_block_scap((int)cap, G, levels_a, nl);
     const unsigned ccapA = rtc::chain_block_scap((int)cap, G, 1, 1);

@@ -261,7 +261,7 @@ __device__ __forceinline__ bool walk_begin(const rtk::DevScene& s, const Ray& r,
     if (s.nnodes <= 0) return false;
     if (COUNT) w.nodes++;
     float bt;
-    if (!COUNT && any && k.fast && s.use_stree) {
+    if ((!COUNT || s.use_stree == 2) && any && k.fast && s.use_stree) {
         k.tree = s.spairs;
         k.cur = s.sroot_info;
         const float4 lo = make_float4(s.sroot_lo[0], s.sroot_lo[1], s.sroot_lo[2], 0.0f);

@@ -56,6 +56,20 @@ __device__ __forceinline__ bool slab_sample_ray(const rtk::Eye& e, const P& p, u
     return true;
 }
 
+// Does slot s of the chunk hold a sample of this rank's slab (slab_sample_ray's checks)?
+template <class P>
+__device__ __forceinline__ bool slab_slot_valid(const P& p, unsigned s) {
+    const unsigned tile = s >> 6, lane = s & 63;
+    const int tx = (int)(tile % (unsigned)p.tiles_x), ty = (int)(tile / (unsigned)p.tiles_x);
+    const int ix = tx * 8 + (int)(lane & 7);
+    const int iyc = ty * 8 + (int)(lane >> 3);
+    if (ix >= p.wi || iyc >= p.chunk_rows) return false;
+    const int lr = (p.chunk_row0 + iyc) / p.aa;
+    if (lr >= p.slab_rows) return false;
+    const int stripe = lr / p.stripe_rows;
+    return (stripe * p.nranks + p.rank) * p.stripe_rows + (lr - stripe * p.stripe_rows) < p.height;
+}
+
 // Inverse of the tile ordering: chunk-relative internal pixel -> slot.
 __device__ __forceinline__ unsigned slab_slot(int tiles_x, int ix, int iyc) {
     return ((unsigned)((iyc >> 3) * tiles_x + (ix >> 3)) << 6) | (unsigned)((iyc & 7) * 8 + (ix & 7));
