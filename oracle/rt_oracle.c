@@ -568,7 +568,9 @@ static inline int sphere_test(const ro_scene* s, const ray_t* r, const ro_sphere
 
 /* diagnostics: per-node visit histogram [0]=closest-hit [1]=any-hit (NULL = off) */
 uint64_t* ro_debug_node_hist[2];
-#define NOTE_NODE(k, ni) do { if (ro_debug_node_hist[k]) __atomic_fetch_add(&ro_debug_node_hist[k][ni], 1, __ATOMIC_RELAXED); } while (0)
+/* diagnostics (single-threaded callers only): mark visited nodes in a byte map */
+static uint8_t* g_visit_mark;
+#define NOTE_NODE(k, ni) do { if (ro_debug_node_hist[k]) __atomic_fetch_add(&ro_debug_node_hist[k][ni], 1, __ATOMIC_RELAXED); if (g_visit_mark) g_visit_mark[ni] = 1; } while (0)
 
 /* Ray::getFirstIntersection (:177-225) */
 static hit_t closest_hit(const ro_scene* s, const ray_t* r, work_t* w) {
@@ -808,6 +810,59 @@ static int render_impl(const ro_scene* s, int cam, int aa, int threads, int row_
     }
     if (counters) *counters = tot;
     free(jobs); free(th);
+    return 0;
+}
+
+/* Diagnostics: packet coherence of primary rays.  For every 8x8 tile:
+ * union of BVH nodes its 64 closest-hit walks visit, the sum and the max of
+ * per-ray visits, and whether all rays agree on every interior node's
+ * near/far order (sign of d[axis]).  out[0..3] = sums over tiles of union,
+ * per-ray sum, per-tile max, tiles with disagreeing signs. */
+int ro_debug_tile_mode;
+int ro_debug_tile_stats(const ro_scene* s, int cam, double* out) {
+    if (!s || cam < 0 || cam >= s->ncam) return -1;
+    const ro_camera* c = &s->cams[cam];
+    int W = c->width, H = c->height;
+    eye_t eye = eye_init(c, W, H);
+    work_t w = {0, 0, 0};
+    uint8_t* mark = (uint8_t*)calloc((size_t)s->nnodes + 1, 1);
+    out[0] = out[1] = out[2] = out[3] = 0;
+    for (int ty = 0; ty < H; ty += 8)
+        for (int tx = 0; tx < W; tx += 8) {
+            memset(mark, 0, (size_t)s->nnodes);
+            g_visit_mark = mark;
+            double mx = 0; int sgn[3] = {0, 0, 0}; int first = 1, dis = 0;
+            for (int y = ty; y < ty + 8 && y < H; ++y)
+                for (int x = tx; x < tx + 8 && x < W; ++x) {
+                    ray_t r = eye_gen(&eye, y, x);
+                    int sg[3] = {r.d.x > 0, r.d.y > 0, r.d.z > 0};
+                    if (first) { sgn[0] = sg[0]; sgn[1] = sg[1]; sgn[2] = sg[2]; first = 0; }
+                    else if (sg[0] != sgn[0] || sg[1] != sgn[1] || sg[2] != sgn[2]) dis = 1;
+                    uint64_t n0 = w.node;
+                    hit_t h = closest_hit(s, &r, &w);
+                    double v = (double)(w.node - n0);
+                    if (ro_debug_tile_mode == 1) {          /* shadow ray to light 0 instead */
+                        if (!h.exists || s->nlights < 1) continue;
+                        g_visit_mark = NULL;
+                        v3 hp = v_add(r.o, v_mul(r.d, h.t));
+                        v3 p = v_add(hp, v_mul(h.n, s->eps));
+                        v3 lp = s->lights[0].position;
+                        float dist = v_len(v_sub(lp, p));
+                        ray_t sr = make_ray(p, v_norm(v_sub(lp, p)));
+                        g_visit_mark = mark;
+                        n0 = w.node;
+                        (void)any_hit(s, &sr, dist, &w);
+                        v = (double)(w.node - n0);
+                    }
+                    out[1] += v;
+                    if (v > mx) mx = v;
+                }
+            g_visit_mark = NULL;
+            size_t u = 0;
+            for (int i = 0; i < s->nnodes; ++i) u += mark[i];
+            out[0] += (double)u; out[2] += mx; out[3] += dis;
+        }
+    free(mark);
     return 0;
 }
 

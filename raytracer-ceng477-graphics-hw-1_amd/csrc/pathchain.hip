@@ -36,6 +36,9 @@ constexpr int kBlock = 256;
 #ifndef RT_WAVES_PER_EU
 #define RT_WAVES_PER_EU 1
 #endif
+#ifndef RT_OCC_WAVES_PER_EU
+#define RT_OCC_WAVES_PER_EU 1     // k_mix / k_occlude (the any-hit bulk)
+#endif
 
 enum LaneState : int { kIdle = 0, kTrav = 1, kDone = 2 };
 
@@ -395,6 +398,156 @@ __device__ __forceinline__ unsigned group_samples(unsigned n0, unsigned G, unsig
     return (mine - 1u) * 256u + min(256u, n0 - last_unit * 256u);
 }
 
+// Task index space [0, T) dealt to G workgroups in chunks of `ch`
+// consecutive tasks (chunk c -> workgroup c mod G).  ch = 1 (default) spreads
+// the spatially clustered heavy tasks (mirror regions) over every workgroup;
+// larger chunks give a wave neighbouring tasks (more coherent fetches) at the
+// price of that balance.
+__device__ __forceinline__ unsigned chunk_count(unsigned T, unsigned G, unsigned blk, unsigned ch) {
+    const unsigned nch = (T + ch - 1u) / ch;
+    if (blk >= nch) return 0u;
+    const unsigned m = (nch - 1u - blk) / G + 1u;
+    const unsigned short_last = ((nch - 1u) % G == blk) ? nch * ch - T : 0u;
+    return m * ch - short_last;
+}
+__device__ __forceinline__ unsigned chunk_task(unsigned v, unsigned G, unsigned blk, unsigned ch) {
+    return (blk + (v / ch) * G) * ch + v % ch;
+}
+
+// ---------------------------------------------------------------------------
+// Packet closest-hit walk: the wave walks ONE shared DFS; every node and
+// leaf fetch is wave-uniform (scalar loads), each lane keeps its own tMax and
+// best hit.  Exact when every active lane agrees on the near/far predicate
+// d[axis] > 0 for all three axes (caller checks): then the shared order IS
+// each lane's own order (raytracer.cpp:200-206), a lane is active exactly on
+// the nodes its own walk pops with a passing test (box hit at the parent,
+// bt <= its tMax at the pop, :184), in the same sequence, so its leaf tests
+// and updates (:210-222) happen in the same order.  Stack entries: node and
+// lane mask wave-uniform (LDS, per wave), each lane's deferred bt in its own
+// WalkStack slot.  8x8 tiles of eye rays agree almost everywhere and visit
+// ~1.2x the nodes of their average ray, so one uniform walk replaces 64
+// divergent ones.
+// ---------------------------------------------------------------------------
+#ifndef RT_PACKET_WALK
+#define RT_PACKET_WALK 0     // measured slower than per-lane walks on C3 (latency-bound); kept, exact
+#endif
+constexpr int kPktDepth = dl::kMaxStack;
+__shared__ int g_pnode[(kBlock / 64) * kPktDepth];
+__shared__ unsigned long long g_pmask[(kBlock / 64) * kPktDepth];
+
+__device__ __forceinline__ int uni(int v) { return __builtin_amdgcn_readfirstlane(v); }
+
+template <bool COUNT>
+__device__ HitRec packet_closest(const rtk::DevScene& s, const Ray& r, bool act, WalkStack& stk, Work& w) {
+    const int lane = lane_id();
+    const int base = uni((int)(threadIdx.x >> 6) * kPktDepth);
+    HitRec best{-1.0f, -1};
+    float tmax = FLT_MAX;
+    if (s.nnodes <= 0) return best;
+    const bool fast = __all(!act || ray_nan_free(r));
+    unsigned long long A;
+    {
+        float bt;
+        const float4 lo = make_float4(s.root_lo[0], s.root_lo[1], s.root_lo[2], 0.0f);
+        const float4 hi = make_float4(s.root_hi[0], s.root_hi[1], s.root_hi[2], 0.0f);
+        if (COUNT && act) w.nodes++;
+        A = __ballot(act && box_hit(r, lo, hi, &bt) && bt <= tmax);
+    }
+    int cur = s.root_info;
+    int sp = 0;
+    // near/far predicate of the (agreeing) active lanes, per axis
+    const int lead = __ffsll((unsigned long long)__ballot(act)) - 1;
+    const int sx = __shfl((int)(r.d.x > 0.0f), lead, 64), sy = __shfl((int)(r.d.y > 0.0f), lead, 64),
+              sz = __shfl((int)(r.d.z > 0.0f), lead, 64);
+    while (true) {
+        if (A) {
+            const bool in = (A >> lane) & 1ull;
+            if (cur >= 0) {
+                const float4* q = reinterpret_cast<const float4*>(&s.pairs[uni(cur)]);
+                const float4 l0 = q[0], l1 = q[1], r0 = q[2], r1 = q[3];
+                float tl, tr;
+                bool hl, hr;
+                if (fast) {
+                    hl = box_hit_fast(r, l0, l1, &tl);
+                    hr = box_hit_fast(r, r0, r1, &tr);
+                } else {
+                    hl = box_hit(r, l0, l1, &tl);
+                    hr = box_hit(r, r0, r1, &tr);
+                }
+                const int axis = __float_as_int(l1.w);
+                const bool left_first = (axis == 0 ? sx : (axis == 1 ? sy : sz)) != 0;
+                const bool hn = left_first ? hl : hr, hf = left_first ? hr : hl;
+                const float tn = left_first ? tl : tr, tf = left_first ? tr : tl;
+                const int in_ = left_first ? __float_as_int(l0.w) : __float_as_int(r0.w);
+                const int if_ = left_first ? __float_as_int(r0.w) : __float_as_int(l0.w);
+                if (COUNT && in) w.nodes += 2;
+                const unsigned long long mf = __ballot(in && hf);
+                if (mf) {
+                    stk.put(sp, make_int2(0, __float_as_int(tf)));
+                    if (lane == 0) {
+                        g_pnode[base + sp] = if_;
+                        g_pmask[base + sp] = mf;
+                    }
+                    ++sp;
+                }
+                A = __ballot(in && hn && tn <= tmax);
+                if (A) {
+                    cur = in_;
+                    continue;
+                }
+            } else {
+                int a, cnt;
+                leaf_range(s, cur, &a, &cnt);
+                a = uni(a);
+                cnt = uni(cnt);
+                for (int i = a; i < a + cnt; ++i) {
+                    const float4* pr = reinterpret_cast<const float4*>(&s.prims[i]);
+                    const float4 p0 = pr[0], p1 = pr[1];
+                    float t;
+                    bool h;
+                    if (__float_as_int(p0.w) >= 0) {
+                        if (COUNT && in) w.tris++;
+                        h = tri_hit(r, p0, p1, pr[2], &t);
+                    } else {
+                        if (COUNT && in) w.spheres++;
+                        h = sphere_hit(r, p0, p1, &t);
+                    }
+                    if (in && h && (t < best.t || best.t == -1.0f)) {
+                        best.t = t;
+                        best.prim = i;
+                        tmax = t;
+                    }
+                }
+                A = 0;
+            }
+        }
+        // pop until some lane's deferred test passes
+        if (sp == 0) break;
+        while (sp > 0) {
+            --sp;
+            const int2 e = stk.at(sp);
+            const int node = uni(g_pnode[base + sp]);
+            const unsigned long long m = g_pmask[base + sp];
+            A = __ballot(((m >> lane) & 1ull) && __int_as_float(e.y) <= tmax);
+            if (A) {
+                cur = node;
+                break;
+            }
+        }
+        if (!A) break;
+    }
+    return best;
+}
+
+// Do the active lanes agree on d[axis] > 0 for every axis (packet walk exact)?
+__device__ __forceinline__ bool packet_ok(const Ray& r, bool act) {
+    const unsigned long long m = __ballot(act);
+    if (!m) return false;
+    const unsigned long long bx = __ballot(act && r.d.x > 0.0f), by = __ballot(act && r.d.y > 0.0f),
+                             bz = __ballot(act && r.d.z > 0.0f);
+    return (bx == 0 || bx == m) && (by == 0 || by == m) && (bz == 0 || bz == m);
+}
+
 // closest-hit chains of one phase (raytracer.cpp:385-439 minus the shading):
 // record each hit, queue its shadow tasks, follow (or hand on) mirrors.
 template <bool COUNT, bool CONT, bool WIDE = false>
@@ -405,7 +558,7 @@ __device__ void chain_body(const rtk::DevScene& s, const rtk::Eye& e, const PcPa
     uint32_t nprim = 0, nrefl = 0;
     const int nl = s.nlights;
     unsigned nb;
-    if (CONT) nb = blk < g_pref[p.grid] ? (g_pref[p.grid] - blk + G - 1u) / G : 0u;
+    if (CONT) nb = chunk_count(g_pref[p.grid], G, blk, (unsigned)p.tchunk);
     else nb = group_samples((unsigned)p.n0, G, blk);
     unsigned* const sq = o.sq + (size_t)blk * o.scap;
     int st = kIdle;
@@ -417,6 +570,7 @@ __device__ void chain_body(const rtk::DevScene& s, const rtk::Eye& e, const PcPa
     unsigned t_grab = 0;
     int wsteps = 0;          // narrow steps of the current walk (wide-walk trigger)
     bool nowide = false;     // the wide walk fell back for this walk
+    bool fresh = false;      // lane just took an eye ray (packet walk pending)
     while (true) {
         // (1) epilogue of finished walks: record, queue shadow tasks, reflect or hand on
         if (st == kDone) {
@@ -479,7 +633,7 @@ __device__ void chain_body(const rtk::DevScene& s, const rtk::Eye& e, const PcPa
                     const unsigned v = base + lane_rank(idle);
                     if (v < nb) {
                         if (CONT) {
-                            const unsigned j = blk + v * G;
+                            const unsigned j = chunk_task(v, G, blk, (unsigned)p.tchunk);
                             const unsigned reg = region_search(j, p.grid);
                             const unsigned lvp = p.cq[(size_t)reg * p.ccapA + (j - g_pref[reg])];
                             path = lvp % (unsigned)p.cap;
@@ -499,12 +653,27 @@ __device__ void chain_body(const rtk::DevScene& s, const rtk::Eye& e, const PcPa
                                 if (p.trace) t_grab = (unsigned)wall_clock64();
                                 nprim++;
                                 if (s.max_depth < 0) p.pinfo[path] = 0 | (kEndZero << 8);   // depth 0 > max: black
+                                else if (RT_PACKET_WALK && p.packet) fresh = true;
                                 else st = walk_begin<COUNT>(s, r, wk, w) ? kTrav : kDone;
                             }
                         }
                     }
                 }
             }
+        }
+        if (RT_PACKET_WALK && !CONT && p.packet && __any(fresh)) {
+            // fresh eye rays of this wave (a tile): one packet walk when they agree on the
+            // near/far predicates and no other lane of the wave has entries on its stack
+            if (packet_ok(r, fresh) && __all(st != kTrav || wk.sp == 0)) {
+                const HitRec h = packet_closest<COUNT>(s, r, fresh, stk, w);
+                if (fresh) {
+                    wk.best = h;
+                    st = kDone;
+                }
+            } else if (fresh) {
+                st = walk_begin<COUNT>(s, r, wk, w) ? kTrav : kDone;
+            }
+            fresh = false;
         }
         if (!__any(st != kIdle)) {
             if (exhausted) break;
@@ -571,7 +740,7 @@ __device__ void occlude_body(const rtk::DevScene& s, const PcParams& p, unsigned
     uint32_t nrays = 0;
     const unsigned t_start = p.trace ? (unsigned)wall_clock64() : 0u;
     const unsigned total = g_pref[nreg];
-    const unsigned n = blk < total ? (total - blk + G - 1u) / G : 0u;
+    const unsigned n = chunk_count(total, G, blk, (unsigned)p.tchunk);
     bool active = false, exhausted = n == 0;
     Ray r;
     float tlim = 0.0f;
@@ -586,7 +755,7 @@ __device__ void occlude_body(const rtk::DevScene& s, const PcParams& p, unsigned
                 if (!active) {
                     const unsigned idx = base + lane_rank(idle);
                     if (idx < n) {
-                        const unsigned j = blk + idx * G;
+                        const unsigned j = chunk_task(idx, G, blk, (unsigned)p.tchunk);
                         const unsigned reg = region_search(j, nreg);
                         owner = sq[(size_t)reg * scap + (j - g_pref[reg])];
                         r = shadow_from_record(s, p, owner, &tlim);
@@ -676,7 +845,7 @@ __global__ __launch_bounds__(1024) void k_scan_b(PcParams p) { scan_counts(p.scn
 
 // Workgroups [0, gb): phase B chains (continuations); the rest: phase A's shadow tasks.
 template <bool COUNT>
-__global__ __launch_bounds__(kBlock, RT_WAVES_PER_EU) void k_mix(rtk::DevScene s, rtk::Eye e, PcParams p) {
+__global__ __launch_bounds__(kBlock, RT_OCC_WAVES_PER_EU) void k_mix(rtk::DevScene s, rtk::Eye e, PcParams p) {
     const bool chain = blockIdx.x < (unsigned)p.gb;
     if (threadIdx.x == 0) g_ccnt = 0;
     load_prefix(chain ? p.cpref : p.sprefA, p.grid);
@@ -690,7 +859,7 @@ __global__ __launch_bounds__(kBlock, RT_WAVES_PER_EU) void k_mix(rtk::DevScene s
 
 // Phase B's shadow tasks.
 template <bool COUNT>
-__global__ __launch_bounds__(kBlock, RT_WAVES_PER_EU) void k_occlude(rtk::DevScene s, PcParams p) {
+__global__ __launch_bounds__(kBlock, RT_OCC_WAVES_PER_EU) void k_occlude(rtk::DevScene s, PcParams p) {
     load_prefix(p.sprefB, p.gb);
     block_init(s);
     occlude_body<COUNT>(s, p, blockIdx.x, gridDim.x, p.sqB, p.scapB, p.gb);

@@ -58,6 +58,8 @@ struct PcParams {
     unsigned* sprefB; // [gb + 1]
     int kinline;      // deepest level phase A walks (>= max_depth: no phase B)
     int gb;           // k_mix workgroups in the chain role (the other p.ogrid ones occlude A's tasks)
+    int tchunk;       // continuation / shadow tasks are dealt to workgroups in chunks of this many
+    int packet;       // 1: eye rays of a wave walk as one packet when exact (packet_closest)
     int grid;         // k_chain persistent grid (= number of shadow-queue regions)
     int ogrid;        // k_occlude persistent grid
     int refill;       // a wave refills once <= refill of its lanes are still walking

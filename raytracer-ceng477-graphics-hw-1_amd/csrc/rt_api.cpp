@@ -113,6 +113,8 @@ struct rt_scene {
     int tune_orefill = 32;      // RT_OREFILL
     int tune_brefill = 32;      // RT_BREFILL
     int tune_bprio = 1;         // RT_BPRIO
+    int tune_tchunk = 1;        // RT_TCHUNK
+    int tune_packet = 1;        // RT_PACKET
     int tune_wide = 0;          // RT_WIDE
     int tune_wide_min = 24;     // RT_WIDE_MIN
     int tune_kinline = 1;       // RT_KINLINE: deepest level of phase A
@@ -231,6 +233,8 @@ int finish_scene(rt_scene* s, const rt_options* opts) {
         const int v = std::atoi(e);
         s->tune_spread = v >= 4 ? 4 : v >= 2 ? 2 : 1;
     }
+    if (const char* e = std::getenv("RT_PACKET")) s->tune_packet = std::atoi(e) != 0;
+    if (const char* e = std::getenv("RT_TCHUNK")) s->tune_tchunk = std::max(1, std::min(4096, std::atoi(e)));
     if (const char* e = std::getenv("RT_BPRIO")) s->tune_bprio = std::atoi(e) != 0;
     if (const char* e = std::getenv("RT_BREFILL")) s->tune_brefill = std::max(0, std::min(63, std::atoi(e)));
     if (const char* e = std::getenv("RT_OREFILL")) s->tune_orefill = std::max(0, std::min(63, std::atoi(e)));
@@ -502,6 +506,8 @@ int render_chain(rt_scene* s, const rtk::Eye& eye, const rtk::FrameParams& f, bo
     p.orefill = s->tune_orefill;
     p.brefill = s->tune_brefill;
     p.bprio = s->tune_bprio;
+    p.tchunk = s->tune_tchunk;
+    p.packet = s->tune_packet && s->bvh.max_stack <= dl::kMaxStack;
     p.wide = s->bvh.max_depth <= 26 ? s->tune_wide : 0;   // path keys hold 26 levels
     p.wide_min = s->tune_wide_min;
     p.spread = s->tune_spread;
