@@ -64,6 +64,26 @@ struct alignas(16) Pair {
     float r_maxx, r_maxy, r_maxz; int32_t pad;
 };
 struct LeafBig { int32_t start, count; };
+
+// Occlusion tree node, 4-wide, 64 B (four dwordx4 loads test four children):
+//   {origin.xyz, exps}  exps = ex | ey << 8 | ez << 16 | nchild << 24, scale_a = 2^(e_a - 127)
+//   {qlo[4][3] bytes, qhi[4][3] bytes}          child c box, axis a:
+//       lo = origin_a + qlo[c][a] * scale_a,  hi = origin_a + qhi[c][a] * scale_a  (float, exact
+//       power-of-two scale; the host verifies every decoded box CONTAINS the child's exact box)
+//   {child[4]}  >= 0: quad index; < 0: kLeafBit | index into QLeaf (a reference leaf)
+//   {pad[2]}
+// Leaves are the reference BVH's leaves; QLeaf holds their EXACT boxes, tested
+// exactly before the leaf's primitives (see build_shadow_tree).
+struct alignas(16) Quad {
+    float ox, oy, oz; uint32_t exps;
+    uint32_t q[6];        // bytes: qlo c0..c3 x,y,z (12), then qhi c0..c3 x,y,z (12)
+    int32_t child[4];
+    int32_t pad[2];
+};
+struct alignas(16) QLeaf {
+    float minx, miny, minz; int32_t info;    // info: the reference leaf code (kLeafBit | count | start)
+    float maxx, maxy, maxz; int32_t pad;
+};
 #ifndef RT_TOP_PAIRS
 #define RT_TOP_PAIRS 256
 #endif
@@ -73,6 +93,8 @@ constexpr int32_t kLeafStartMask = (1 << kLeafCountShift) - 1;
 constexpr int kLeafMaxCount = 63;
 
 static_assert(sizeof(Pair) == 64, "pair size");
+static_assert(sizeof(Quad) == 64, "quad size");
+static_assert(sizeof(QLeaf) == 32, "qleaf size");
 static_assert(sizeof(Node) == 32, "node size");
 static_assert(sizeof(Prim) == 48, "prim size");
 static_assert(sizeof(Material) == 64, "material size");

@@ -667,6 +667,82 @@ void build_shadow_tree(FlatBVH& out) {
     }
     for (int a = 0; a < 3; ++a) { out.sroot_lo[a] = tn[root].box.lo[a]; out.sroot_hi[a] = tn[root].box.hi[a]; }
     out.sroot_info = info(root);
+
+    // 4-wide collapse with quantized child boxes (dl::Quad).  Every decoded
+    // box is verified, with the device's own float arithmetic, to CONTAIN the
+    // child's box, so containment (all the any-hit argument needs) holds.
+    auto pow2 = [](int e) { return ibits(e << 23); };                       // 2^(e-127), e in [1, 254]
+    auto dec = [](float o, int q, float sc) { return o + (float)q * sc; };  // device decode, no contraction
+    out.quads.clear();
+    out.qleaves.clear();
+    out.qmax_depth = 0;
+    bool contain_ok = true;
+    std::function<int32_t(int, int)> emit = [&](int n, int depth) -> int32_t {
+        out.qmax_depth = std::max(out.qmax_depth, depth);
+        const TNode& t = tn[n];
+        if (t.left < 0) {
+            dl::QLeaf l{};
+            l.minx = t.box.lo[0]; l.miny = t.box.lo[1]; l.minz = t.box.lo[2]; l.info = t.info;
+            l.maxx = t.box.hi[0]; l.maxy = t.box.hi[1]; l.maxz = t.box.hi[2]; l.pad = 0;
+            out.qleaves.push_back(l);
+            return dl::kLeafBit | (int32_t)(out.qleaves.size() - 1);
+        }
+        std::vector<int> ch{t.left, t.right};
+        while (ch.size() < 4) {
+            int best = -1;
+            double ba = -1.0;
+            for (size_t i = 0; i < ch.size(); ++i)
+                if (tn[ch[i]].left >= 0 && tn[ch[i]].box.area() > ba) { ba = tn[ch[i]].box.area(); best = (int)i; }
+            if (best < 0) break;
+            const int c = ch[best];
+            ch[best] = tn[c].left;
+            ch.insert(ch.begin() + best + 1, tn[c].right);
+        }
+        const int me = (int)out.quads.size();
+        out.quads.emplace_back();
+        int32_t codes[4] = {INT32_MAX, INT32_MAX, INT32_MAX, INT32_MAX};
+        for (size_t i = 0; i < ch.size(); ++i) codes[i] = emit(ch[i], depth + 1);
+        dl::Quad q{};
+        const float o[3] = {t.box.lo[0], t.box.lo[1], t.box.lo[2]};
+        int e[3];
+        float sc[3];
+        for (int a = 0; a < 3; ++a) {
+            e[a] = 1;
+            const double ext = (double)t.box.hi[a] - o[a];
+            if (ext > 0) e[a] = std::max(1, std::min(254, (int)std::ceil(std::log2(ext / 255.0)) + 127));
+            while (e[a] < 254 && dec(o[a], 255, pow2(e[a])) < t.box.hi[a]) ++e[a];
+            sc[a] = pow2(e[a]);
+        }
+        uint8_t ql[4][3] = {}, qh[4][3] = {};
+        for (size_t i = 0; i < ch.size(); ++i)
+            for (int a = 0; a < 3; ++a) {
+                const float lo = tn[ch[i]].box.lo[a], hi = tn[ch[i]].box.hi[a];
+                int qlo = (int)std::floor(((double)lo - o[a]) / sc[a]);
+                qlo = std::max(0, std::min(255, qlo));
+                while (qlo > 0 && dec(o[a], qlo, sc[a]) > lo) --qlo;
+                int qhi = (int)std::ceil(((double)hi - o[a]) / sc[a]);
+                qhi = std::max(0, std::min(255, qhi));
+                while (qhi < 255 && dec(o[a], qhi, sc[a]) < hi) ++qhi;
+                // the decoded box must contain the child's exact box (the device decodes identically)
+                if (dec(o[a], qlo, sc[a]) > lo || dec(o[a], qhi, sc[a]) < hi) contain_ok = false;
+                ql[i][a] = (uint8_t)qlo;
+                qh[i][a] = (uint8_t)qhi;
+            }
+        q.ox = o[0]; q.oy = o[1]; q.oz = o[2];
+        q.exps = (uint32_t)e[0] | (uint32_t)e[1] << 8 | (uint32_t)e[2] << 16 | (uint32_t)ch.size() << 24;
+        uint8_t bytes[24];
+        for (int i = 0; i < 4; ++i)
+            for (int a = 0; a < 3; ++a) { bytes[i * 3 + a] = ql[i][a]; bytes[12 + i * 3 + a] = qh[i][a]; }
+        std::memcpy(q.q, bytes, 24);
+        for (int i = 0; i < 4; ++i) q.child[i] = codes[i];
+        out.quads[me] = q;
+        return me;
+    };
+    out.qroot = emit(root, 0);
+    if (!contain_ok || 3 * out.qmax_depth + 4 > dl::kMaxStack) {   // fall back to the binary occlusion tree
+        out.quads.clear();
+        out.qleaves.clear();
+    }
 }
 
 }  // namespace rtx

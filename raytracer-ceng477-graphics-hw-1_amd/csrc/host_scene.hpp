@@ -62,6 +62,11 @@ struct FlatBVH {
     float sroot_lo[3] = {0, 0, 0}, sroot_hi[3] = {0, 0, 0};
     int32_t sroot_info = 0;
     int smax_depth = 0;
+    // the same occlusion tree collapsed to 4-wide nodes with quantized child boxes
+    std::vector<dl::Quad> quads;
+    std::vector<dl::QLeaf> qleaves;
+    int32_t qroot = 0;               // >= 0 quad index, < 0 kLeafBit | qleaf index
+    int qmax_depth = 0;
     int leaves = 0, max_leaf = 0, max_depth = 0, max_stack = 0;
     double build_ms = 0;
 };

@@ -36,6 +36,9 @@ constexpr int kBlock = 256;
 #ifndef RT_WAVES_PER_EU
 #define RT_WAVES_PER_EU 1
 #endif
+#ifndef RT_WIDE_B
+#define RT_WIDE_B 0           // wide walks for phase-B tails (RT_WIDE > 0 at run time)
+#endif
 #ifndef RT_OCC_WAVES_PER_EU
 #define RT_OCC_WAVES_PER_EU 1     // k_mix / k_occlude (the any-hit bulk)
 #endif
@@ -773,7 +776,7 @@ __device__ void occlude_body(const rtk::DevScene& s, const PcParams& p, unsigned
         const int thresh = exhausted ? 0 : p.orefill;
         while (__popcll(__ballot(active)) > thresh) {
             if (active) {
-                const int res = any_step<COUNT, FetchTop>(s, r, tlim, stk, wk, w);
+                const int res = occl_step<COUNT, FetchTop>(s, r, tlim, stk, wk, w);
                 if (res) {
                     p.occ[owner] = res == 2 ? 1 : 0;
                     active = false;
@@ -852,9 +855,9 @@ __global__ __launch_bounds__(kBlock, RT_OCC_WAVES_PER_EU) void k_mix(rtk::DevSce
     block_init(s);
     if (chain) {
         if (p.bprio) __builtin_amdgcn_s_setprio(3);    // the deep chains are the frame's critical path
-        chain_body<COUNT, true>(s, e, p, blockIdx.x, (unsigned)p.gb, phase_b(p));
+        chain_body<COUNT, true, RT_WIDE_B>(s, e, p, blockIdx.x, (unsigned)p.gb, phase_b(p));
     }
-    else occlude_body<COUNT>(s, p, blockIdx.x - p.gb, gridDim.x - p.gb, p.sqA, p.scapA, p.grid);
+    else if (!p.exp_skip_occ) occlude_body<COUNT>(s, p, blockIdx.x - p.gb, gridDim.x - p.gb, p.sqA, p.scapA, p.grid);
 }
 
 // Phase B's shadow tasks.
@@ -1064,7 +1067,7 @@ __global__ __launch_bounds__(kBlock, RT_WAVES_PER_EU) void k_fused(rtk::DevScene
             const int thresh = (gn > 0 || live) ? p.crefill : 0;
             while (__popcll(__ballot(active)) > thresh) {
                 if (active) {
-                    const int res = any_step<COUNT, FetchTop>(s, r, tlim, stk, wk, w);
+                    const int res = occl_step<COUNT, FetchTop>(s, r, tlim, stk, wk, w);
                     if (res) {
                         p.occ[owner] = res == 2 ? 1 : 0;
                         active = false;

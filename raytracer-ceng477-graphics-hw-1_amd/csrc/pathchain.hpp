@@ -60,6 +60,7 @@ struct PcParams {
     int gb;           // k_mix workgroups in the chain role (the other p.ogrid ones occlude A's tasks)
     int tchunk;       // continuation / shadow tasks are dealt to workgroups in chunks of this many
     int packet;       // 1: eye rays of a wave walk as one packet when exact (packet_closest)
+    int exp_skip_occ; // experiments only (RT_EXP_SKIP_OCC): k_mix's occlusion role does nothing (wrong images)
     int grid;         // k_chain persistent grid (= number of shadow-queue regions)
     int ogrid;        // k_occlude persistent grid
     int refill;       // a wave refills once <= refill of its lanes are still walking

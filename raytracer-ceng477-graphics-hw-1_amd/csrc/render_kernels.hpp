@@ -36,7 +36,11 @@ struct DevScene {
     const dl::Pair* spairs;
     float sroot_lo[3], sroot_hi[3];
     int sroot_info;
-    int use_stree;        // 1: NaN-free shadow rays walk the occlusion tree (RT_STREE=0 disables)
+    int use_stree;        // NaN-free shadow rays walk: 0 the BVH, 1 the binary occlusion tree, 2 its 4-wide form
+    int count_stree;      // diagnostics: counting passes walk the occlusion tree too (counts then differ)
+    const dl::Quad* quads;
+    const dl::QLeaf* qleaves;
+    int qroot;
 
     // Sphere prims carry ~sphere_index in p0.w (negative), triangles their id.
     __device__ __forceinline__ bool prim_is_sphere(int, const float4 p0) const {

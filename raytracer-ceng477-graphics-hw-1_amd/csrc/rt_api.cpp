@@ -99,6 +99,8 @@ struct rt_scene {
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
     dl::Pair* d_pairs = nullptr;
     dl::Pair* d_spairs = nullptr;
+    dl::Quad* d_quads = nullptr;
+    dl::QLeaf* d_qleaves = nullptr;
     dl::LeafBig* d_leafbig = nullptr;
     enum Path { kChain, kWavefront, kMegakernel, kFused } path = kChain;
     int grid_blocks = 2048;
@@ -149,7 +151,7 @@ struct rt_scene {
     ~rt_scene() {
         free_ws();
         (void)hipFree(arena);
-        (void)hipFree(d_pairs); (void)hipFree(d_leafbig); (void)hipFree(d_spairs);
+        (void)hipFree(d_pairs); (void)hipFree(d_leafbig); (void)hipFree(d_spairs); (void)hipFree(d_quads); (void)hipFree(d_qleaves);
         (void)hipFree(d_nodes); (void)hipFree(d_prims); (void)hipFree(d_tri); (void)hipFree(d_mats); (void)hipFree(d_lights);
         (void)hipFree(d_counters); (void)hipFree(d_out); (void)hipFree(d_trace);
         if (ev0) (void)hipEventDestroy(ev0);
@@ -204,6 +206,8 @@ int finish_scene(rt_scene* s, const rt_options* opts) {
     if ((rc = upload(&s->d_pairs, s->bvh.pairs))) return rc;
     if ((rc = upload(&s->d_leafbig, s->bvh.leaf_big))) return rc;
     if ((rc = upload(&s->d_spairs, s->bvh.spairs))) return rc;
+    if ((rc = upload(&s->d_quads, s->bvh.quads))) return rc;
+    if ((rc = upload(&s->d_qleaves, s->bvh.qleaves))) return rc;
     HIP_TRY(hipMalloc(reinterpret_cast<void**>(&s->d_counters), 8 * sizeof(unsigned long long)));
     HIP_TRY(hipMemset(s->d_counters, 0, 8 * sizeof(unsigned long long)));
     HIP_TRY(hipEventCreate(&s->ev0));
@@ -271,11 +275,17 @@ int finish_scene(rt_scene* s, const rt_options* opts) {
         d.sroot_hi[i] = s->bvh.sroot_hi[i];
     }
     d.sroot_info = s->bvh.sroot_info;
-    d.use_stree = s->bvh.spairs.empty() ? 0 : 1;
-    if (const char* e = std::getenv("RT_STREE")) d.use_stree = d.use_stree && std::atoi(e) != 0;
-    // diagnostics: RT_STREE=2 also lets counting passes walk the occlusion tree (counts then
-    // measure the tree actually walked, not the reference's)
-    if (const char* e = std::getenv("RT_STREE")) d.use_stree = d.use_stree ? std::atoi(e) : 0;
+    d.quads = s->d_quads;
+    d.qleaves = s->d_qleaves;
+    d.qroot = s->bvh.qroot;
+    // occlusion tree for NaN-free shadow rays: 2 = 4-wide quantized form, 1 = binary, 0 = off (RT_STREE)
+    d.use_stree = !s->bvh.quads.empty() ? 2 : (s->bvh.spairs.empty() ? 0 : 1);
+    if (const char* e = std::getenv("RT_STREE")) {
+        const int v = std::atoi(e);
+        d.use_stree = v <= 0 ? 0 : (v >= 2 && !s->bvh.quads.empty() ? 2 : (s->bvh.spairs.empty() ? 0 : 1));
+    }
+    // diagnostics: counting passes walk the occlusion tree too (counts then measure that tree)
+    d.count_stree = std::getenv("RT_STREE_COUNT") ? 1 : 0;
     if (const char* e = std::getenv("RT_PRIO")) d.prio = std::atoi(e) != 0;
     if (const char* e = std::getenv("RT_TOP")) d.top_pairs = std::min(d.top_pairs, std::max(0, std::atoi(e)));
     return RT_OK;
@@ -508,6 +518,7 @@ int render_chain(rt_scene* s, const rtk::Eye& eye, const rtk::FrameParams& f, bo
     p.bprio = s->tune_bprio;
     p.tchunk = s->tune_tchunk;
     p.packet = s->tune_packet && s->bvh.max_stack <= dl::kMaxStack;
+    p.exp_skip_occ = std::getenv("RT_EXP_SKIP_OCC") ? 1 : 0;
     p.wide = s->bvh.max_depth <= 26 ? s->tune_wide : 0;   // path keys hold 26 levels
     p.wide_min = s->tune_wide_min;
     p.spread = s->tune_spread;

@@ -261,7 +261,12 @@ __device__ __forceinline__ bool walk_begin(const rtk::DevScene& s, const Ray& r,
     if (s.nnodes <= 0) return false;
     if (COUNT) w.nodes++;
     float bt;
-    if ((!COUNT || s.use_stree == 2) && any && k.fast && s.use_stree) {
+    if ((!COUNT || s.count_stree) && any && k.fast && s.use_stree == 2) {
+        k.tree = nullptr;                    // 4-wide occlusion tree (quad_any_step)
+        k.cur = s.qroot;
+        return true;
+    }
+    if ((!COUNT || s.count_stree) && any && k.fast && s.use_stree) {
         k.tree = s.spairs;
         k.cur = s.sroot_info;
         const float4 lo = make_float4(s.sroot_lo[0], s.sroot_lo[1], s.sroot_lo[2], 0.0f);
@@ -384,6 +389,85 @@ __device__ __forceinline__ int any_step(const rtk::DevScene& s, const Ray& r, fl
     return 1;
 }
 
+// One any-hit step over the 4-wide occlusion tree (dl::Quad), NaN-free rays
+// only (walk_begin).  Interior: decode and test the (conservative) child
+// boxes, continue with the first hit child, push the others.  Leaf item: test
+// the reference leaf's EXACT box, then its primitives (raytracer.cpp:264-277).
+// Order is free: the any-hit answer does not depend on it.
+// 0 = continue, 1 = finished unoccluded, 2 = finished occluded.
+template <bool COUNT, class STK>
+__device__ __forceinline__ int quad_any_step(const rtk::DevScene& s, const Ray& r, float tlim, STK& stk, Walk& k,
+                                             Work& w) {
+    if (k.cur >= 0) {
+        const float4* q = reinterpret_cast<const float4*>(&s.quads[k.cur]);
+        const float4 q0 = q[0], q1 = q[1], q2 = q[2], q3 = q[3];
+        const uint32_t ex = __float_as_uint(q0.w);
+        const int n = (int)(ex >> 24);
+        const float sx = __uint_as_float((ex & 255u) << 23), sy = __uint_as_float(((ex >> 8) & 255u) << 23),
+                    sz = __uint_as_float(((ex >> 16) & 255u) << 23);
+        const uint32_t qb[6] = {__float_as_uint(q1.x), __float_as_uint(q1.y), __float_as_uint(q1.z),
+                                __float_as_uint(q1.w), __float_as_uint(q2.x), __float_as_uint(q2.y)};
+        const int ch[4] = {__float_as_int(q2.z), __float_as_int(q2.w), __float_as_int(q3.x), __float_as_int(q3.y)};
+        int next = 0;
+        bool have = false;
+#pragma unroll
+        for (int c = 0; c < 4; ++c) {
+            const int b0 = c * 3, b1 = 12 + c * 3;
+            auto byte = [&](int i) { return (float)((qb[i >> 2] >> ((i & 3) * 8)) & 255u); };
+            const float4 lo = make_float4(q0.x + byte(b0) * sx, q0.y + byte(b0 + 1) * sy, q0.z + byte(b0 + 2) * sz, 0.0f);
+            const float4 hi = make_float4(q0.x + byte(b1) * sx, q0.y + byte(b1 + 1) * sy, q0.z + byte(b1 + 2) * sz, 0.0f);
+            float t;
+            if (c < n && box_hit_fast(r, lo, hi, &t)) {
+                if (COUNT) w.nodes++;
+                if (!have) {
+                    next = ch[c];
+                    have = true;
+                } else {
+                    stk.put(k.sp, make_int2(ch[c], 0));
+                    ++k.sp;
+                }
+            }
+        }
+        if (have) {
+            k.cur = next;
+            return 0;
+        }
+    } else {
+        const float4* L = reinterpret_cast<const float4*>(&s.qleaves[k.cur & ~dl::kLeafBit]);
+        const float4 lo = L[0], hi = L[1];
+        float bt;
+        if (box_hit_fast(r, lo, hi, &bt)) {          // the reference leaf's exact box (NaN-free ray)
+            int a, cnt;
+            leaf_range(s, __float_as_int(lo.w), &a, &cnt);
+            for (int i = a; i < a + cnt; ++i) {
+                const float4* pr = reinterpret_cast<const float4*>(&s.prims[i]);
+                const float4 p0 = pr[0], p1 = pr[1];
+                float t;
+                bool h;
+                if (__float_as_int(p0.w) >= 0) {
+                    if (COUNT) w.tris++;
+                    h = tri_hit(r, p0, p1, pr[2], &t);
+                } else {
+                    if (COUNT) w.spheres++;
+                    h = sphere_hit(r, p0, p1, &t);
+                }
+                if (h && t < tlim) return 2;
+            }
+        }
+    }
+    if (k.sp > 0) {
+        --k.sp;
+        k.cur = stk.at(k.sp).x;
+        return 0;
+    }
+    return 1;
+}
+
+// Any-hit step on whichever tree the walk is on.
+template <bool COUNT, class FETCH, class STK>
+__device__ __forceinline__ int occl_step(const rtk::DevScene& s, const Ray& r, float tlim, STK& stk, Walk& k,
+                                         Work& w);
+
 // One step of EITHER walk, selected per lane by `any`, on one code path (no
 // divergence between lanes doing closest-hit and lanes doing any-hit):
 //   closest  tmax = best t so far; entries {info, tmin} pruned at pop by
@@ -451,6 +535,13 @@ __device__ __forceinline__ int dual_step(const rtk::DevScene& s, const Ray& r, b
         }
     }
     return 1;
+}
+
+template <bool COUNT, class FETCH, class STK>
+__device__ __forceinline__ int occl_step(const rtk::DevScene& s, const Ray& r, float tlim, STK& stk, Walk& k,
+                                         Work& w) {
+    if (k.tree == nullptr) return quad_any_step<COUNT>(s, r, tlim, stk, k, w);
+    return any_step<COUNT, FETCH>(s, r, tlim, stk, k, w);
 }
 
 }  // namespace rtd
