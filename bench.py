@@ -35,8 +35,8 @@ B_NODE, B_TRI, B_SPH, B_PIX = 32, 36, 16, 3
 
 # kernels one frame launches, per render path (the roofline covers all of them)
 PATH_KERNELS = {
-    "chain": ["k_chain", "k_scan_a", "k_mix", "k_scan_b", "k_occlude", "k_shade", "k_compose"],
-    "fused": ["k_fused", "k_shade", "k_compose"],
+    "chain": ["k_chain", "k_pack_a", "k_mix", "k_pack_b", "k_occlude", "k_finish", "k_finish_any"],
+    "fused": ["k_fused", "k_finish", "k_finish_any"],
     "megakernel": ["k_render"],
     "wavefront": ["k_trace", "k_shadow", "k_shade", "k_fold", "k_resolve"],
 }

@@ -39,6 +39,12 @@ constexpr int kBlock = 256;
 #ifndef RT_WIDE_B
 #define RT_WIDE_B 0           // wide walks for phase-B tails (RT_WIDE > 0 at run time)
 #endif
+#ifndef RT_FINISH_PREFETCH
+#define RT_FINISH_PREFETCH 1   // k_finish: next level's record in flight while shading
+#endif
+#ifndef RT_FINISH_WAVES
+#define RT_FINISH_WAVES 1
+#endif
 #ifndef RT_OCC_WAVES_PER_EU
 #define RT_OCC_WAVES_PER_EU 1     // k_mix / k_occlude (the any-hit bulk)
 #endif
@@ -84,7 +90,6 @@ using WalkStack = StackPriv;
 #endif
 __shared__ unsigned g_head;                    // block-local work queue head
 __shared__ unsigned g_scnt;                    // block-local shadow-ray count (hit lanes)
-__shared__ unsigned g_pref[kMaxChainGrid + 1]; // k_occlude: shadow-queue region prefix
 
 // Pair fetches go to global memory: caching the top BVH levels in LDS showed
 // no gain (their loads are wave-coherent and hit the L1).
@@ -357,15 +362,6 @@ struct PhaseOut {              // where a chain phase writes its tasks
     int kinline;               // deepest level walked here
 };
 
-__device__ __forceinline__ unsigned region_search(unsigned j, int nreg) {   // g_pref[r] <= j < g_pref[r+1]
-    int lo = 0, hi = nreg;
-    while (hi - lo > 1) {
-        const int m = (lo + hi) >> 1;
-        if (g_pref[m] <= j) lo = m; else hi = m;
-    }
-    return (unsigned)lo;
-}
-
 // Reflected ray of recorded level lvp = k*cap + sample (raytracer.cpp:430-435).
 __device__ __forceinline__ Ray reflect_from_record(const rtk::DevScene& s, const PcParams& p, size_t lvp) {
     const float4* rc = p.rec + lvp * 3;
@@ -561,7 +557,7 @@ __device__ void chain_body(const rtk::DevScene& s, const rtk::Eye& e, const PcPa
     uint32_t nprim = 0, nrefl = 0;
     const int nl = s.nlights;
     unsigned nb;
-    if (CONT) nb = chunk_count(g_pref[p.grid], G, blk, (unsigned)p.tchunk);
+    if (CONT) nb = chunk_count(p.totals[1], G, blk, (unsigned)p.tchunk);
     else nb = group_samples((unsigned)p.n0, G, blk);
     unsigned* const sq = o.sq + (size_t)blk * o.scap;
     int st = kIdle;
@@ -637,8 +633,7 @@ __device__ void chain_body(const rtk::DevScene& s, const rtk::Eye& e, const PcPa
                     if (v < nb) {
                         if (CONT) {
                             const unsigned j = chunk_task(v, G, blk, (unsigned)p.tchunk);
-                            const unsigned reg = region_search(j, p.grid);
-                            const unsigned lvp = p.cq[(size_t)reg * p.ccapA + (j - g_pref[reg])];
+                            const unsigned lvp = p.cflat[j];
                             path = lvp % (unsigned)p.cap;
                             k = (int)(lvp / (unsigned)p.cap) + 1;
                             r = reflect_from_record(s, p, lvp);
@@ -715,7 +710,7 @@ __device__ void chain_body(const rtk::DevScene& s, const rtk::Eye& e, const PcPa
                 break;
             if (st == kTrav) {
                 ++wsteps;
-                if (closest_step<COUNT, FetchTop>(s, r, stk, wk, w)) st = kDone;
+                if (closest_step<COUNT, FetchTop, WalkStack, CONT>(s, r, stk, wk, w)) st = kDone;
             }
         }
     }
@@ -733,16 +728,15 @@ __device__ void chain_body(const rtk::DevScene& s, const rtk::Eye& e, const PcPa
     }
 }
 
-// any-hit of shadow tasks j = blk, blk+G, ... of the regions whose prefix is
-// in g_pref[0..nreg] (raytracer.cpp:227-280).
+// any-hit of the packed shadow tasks j = blk, blk+G, ... < total
+// (raytracer.cpp:227-280).
 template <bool COUNT>
 __device__ void occlude_body(const rtk::DevScene& s, const PcParams& p, unsigned blk, unsigned G,
-                             const unsigned* sq, unsigned scap, int nreg) {
+                             const unsigned* tasks, unsigned total) {
     WalkStack stk;
     Work w;
     uint32_t nrays = 0;
     const unsigned t_start = p.trace ? (unsigned)wall_clock64() : 0u;
-    const unsigned total = g_pref[nreg];
     const unsigned n = chunk_count(total, G, blk, (unsigned)p.tchunk);
     bool active = false, exhausted = n == 0;
     Ray r;
@@ -759,8 +753,7 @@ __device__ void occlude_body(const rtk::DevScene& s, const PcParams& p, unsigned
                     const unsigned idx = base + lane_rank(idle);
                     if (idx < n) {
                         const unsigned j = chunk_task(idx, G, blk, (unsigned)p.tchunk);
-                        const unsigned reg = region_search(j, nreg);
-                        owner = sq[(size_t)reg * scap + (j - g_pref[reg])];
+                        owner = tasks[j];
                         r = shadow_from_record(s, p, owner, &tlim);
                         nrays++;
                         if (walk_begin<COUNT>(s, r, wk, w, true)) active = true;
@@ -796,10 +789,6 @@ __device__ void occlude_body(const rtk::DevScene& s, const PcParams& p, unsigned
     }
 }
 
-__device__ __forceinline__ void load_prefix(const unsigned* pref, int n) {
-    for (int i = threadIdx.x; i <= n; i += kBlock) g_pref[i] = pref[i];
-}
-
 __device__ __forceinline__ PhaseOut phase_a(const PcParams& p) {
     return PhaseOut{p.sqA, p.scapA, p.scntA, p.cq, p.ccapA, p.ccnt, p.kinline};
 }
@@ -815,57 +804,63 @@ __global__ __launch_bounds__(kBlock, RT_WAVES_PER_EU) void k_chain(rtk::DevScene
     chain_body<COUNT, false>(s, e, p, blockIdx.x, gridDim.x, phase_a(p));
 }
 
-// Exclusive prefix of n counts (one 1024-thread workgroup): out[0..n].
-__device__ void scan_counts(const unsigned* cnt, unsigned* out, int n) {
-    __shared__ unsigned part[1024];
-    const int per = (n + 1023) / 1024;
-    const int b0 = threadIdx.x * per;
-    unsigned sum = 0;
-    for (int i = b0; i < min(n, b0 + per); ++i) sum += cnt[i];
-    part[threadIdx.x] = sum;
+// Region b of a per-workgroup queue (q[b*cap ..], cnt[b] entries) copied to
+// its place in the packed array: the consumers then index tasks directly.
+// Workgroup 0 stores the total.
+__device__ void pack_region(const unsigned* q, unsigned cap, const unsigned* cnt, int nreg, unsigned* flat,
+                            unsigned* total, unsigned b) {
+    __shared__ unsigned s_before, s_all;
+    if (threadIdx.x == 0) { s_before = 0; s_all = 0; }
     __syncthreads();
-    for (int off = 1; off < 1024; off <<= 1) {            // Hillis-Steele inclusive scan
-        const unsigned v = threadIdx.x >= (unsigned)off ? part[threadIdx.x - off] : 0u;
-        __syncthreads();
-        part[threadIdx.x] += v;
-        __syncthreads();
+    unsigned before = 0, all = 0;
+#pragma unroll 8
+    for (int i = threadIdx.x; i < nreg; i += kBlock) {
+        const unsigned c = cnt[i];
+        all += c;
+        if ((unsigned)i < b) before += c;
     }
-    unsigned run = threadIdx.x == 0 ? 0u : part[threadIdx.x - 1];
-    for (int i = b0; i < min(n, b0 + per); ++i) {
-        out[i] = run;
-        run += cnt[i];
+    if (all) atomicAdd(&s_all, all);
+    if (before) atomicAdd(&s_before, before);
+    __syncthreads();
+    const unsigned off = s_before, n = cnt[b];
+    const unsigned* src = q + (size_t)b * cap;
+    unsigned k = threadIdx.x;
+    for (; k + 3 * kBlock < n; k += 4 * kBlock) {          // four loads in flight per lane
+        const unsigned v0 = src[k], v1 = src[k + kBlock], v2 = src[k + 2 * kBlock], v3 = src[k + 3 * kBlock];
+        flat[off + k] = v0; flat[off + k + kBlock] = v1; flat[off + k + 2 * kBlock] = v2; flat[off + k + 3 * kBlock] = v3;
     }
-    if (threadIdx.x == 1023) out[n] = part[1023];
+    for (; k < n; k += kBlock) flat[off + k] = src[k];
+    if (b == 0 && threadIdx.x == 0) *total = s_all;
     __syncthreads();
 }
 
-// After phase A: prefixes of its shadow tasks and continuations.
-__global__ __launch_bounds__(1024) void k_scan_a(PcParams p) {
-    scan_counts(p.scntA, p.sprefA, p.grid);
-    scan_counts(p.ccnt, p.cpref, p.grid);
+// After phase A: pack its shadow tasks and continuations (one workgroup per region).
+__global__ __launch_bounds__(kBlock) void k_pack_a(PcParams p) {
+    pack_region(p.sqA, p.scapA, p.scntA, p.grid, p.sflatA, &p.totals[0], blockIdx.x);
+    pack_region(p.cq, p.ccapA, p.ccnt, p.grid, p.cflat, &p.totals[1], blockIdx.x);
 }
-__global__ __launch_bounds__(1024) void k_scan_b(PcParams p) { scan_counts(p.scntB, p.sprefB, p.gb); }
+__global__ __launch_bounds__(kBlock) void k_pack_b(PcParams p) {
+    pack_region(p.sqB, p.scapB, p.scntB, p.gb, p.sflatB, &p.totals[2], blockIdx.x);
+}
 
 // Workgroups [0, gb): phase B chains (continuations); the rest: phase A's shadow tasks.
 template <bool COUNT>
 __global__ __launch_bounds__(kBlock, RT_OCC_WAVES_PER_EU) void k_mix(rtk::DevScene s, rtk::Eye e, PcParams p) {
     const bool chain = blockIdx.x < (unsigned)p.gb;
     if (threadIdx.x == 0) g_ccnt = 0;
-    load_prefix(chain ? p.cpref : p.sprefA, p.grid);
     block_init(s);
     if (chain) {
         if (p.bprio) __builtin_amdgcn_s_setprio(3);    // the deep chains are the frame's critical path
         chain_body<COUNT, true, RT_WIDE_B>(s, e, p, blockIdx.x, (unsigned)p.gb, phase_b(p));
     }
-    else if (!p.exp_skip_occ) occlude_body<COUNT>(s, p, blockIdx.x - p.gb, gridDim.x - p.gb, p.sqA, p.scapA, p.grid);
+    else if (!p.exp_skip_occ) occlude_body<COUNT>(s, p, blockIdx.x - p.gb, gridDim.x - p.gb, p.sflatA, p.totals[0]);
 }
 
 // Phase B's shadow tasks.
 template <bool COUNT>
 __global__ __launch_bounds__(kBlock, RT_OCC_WAVES_PER_EU) void k_occlude(rtk::DevScene s, PcParams p) {
-    load_prefix(p.sprefB, p.gb);
     block_init(s);
-    occlude_body<COUNT>(s, p, blockIdx.x, gridDim.x, p.sqB, p.scapB, p.gb);
+    occlude_body<COUNT>(s, p, blockIdx.x, gridDim.x, p.sflatB, p.totals[2]);
 }
 
 // ---------------------------------------------------------------------------
@@ -1188,7 +1183,199 @@ __global__ __launch_bounds__(kBlock) void k_compose(rtk::DevScene s, PcParams p)
     }
 }
 
+// Small scenes (<= kFinishMats materials, <= kFinishLights lights): k_finish
+// keeps the materials and lights in LDS (their loads
+// then wait on lgkmcnt, not on the prefetched records' vmcnt).
+constexpr int kFinishMats = 64, kFinishLights = 4;
+__shared__ dl::Material g_fmats[kFinishMats];
+__shared__ dl::Light g_flights[kFinishLights];
+
+template <bool LDS>
+__device__ __forceinline__ const dl::Material& fin_mat(const rtk::DevScene& s, int i) {
+    if (LDS) return g_fmats[i];
+    return s.mats[i];
+}
+template <bool LDS>
+__device__ __forceinline__ const dl::Light& fin_light(const rtk::DevScene& s, int i) {
+    if (LDS) return g_flights[i];
+    return s.lights[i];
+}
+
+// Blinn-Phong of one record from its already-loaded words and material
+// (shade_level's arithmetic, raytracer.cpp:391-425); occ bit l set = light l
+// occluded (lights >= 32 read their byte directly).
+template <bool LDS>
+__device__ __forceinline__ V shade_words(const rtk::DevScene& s, const PcParams& p, size_t rid, const float4 a,
+                                         const float4 b, const float4 c, const float4 mA, const float4 mD,
+                                         const float4 mS, uint32_t occ32) {
+    const V hitp{a.x, a.y, a.z}, n_{b.x, b.y, b.z}, d{c.x, c.y, c.z};
+    V L{0.0f, 0.0f, 0.0f};
+    L = add(L, V{mA.x, mA.y, mA.z});                                                  // :394-395
+    const V pnt = add(hitp, mul(n_, s.eps));                                           // :397
+    // LDS (small scenes): <= kFinishLights lights, a fully unrolled loop and no byte loads
+    const int nl = LDS ? kFinishLights : s.nlights;
+#pragma unroll 1
+    for (int l = 0; l < nl; ++l) {
+        if (LDS && l >= s.nlights) break;
+        const bool occluded = (LDS || l < 32) ? ((occ32 >> l) & 1u) != 0 : p.occ[rid * s.nlights + l] != 0;
+        if (occluded) continue;
+        const dl::Light& Lt = fin_light<LDS>(s, l);
+        const float4 lp = ld4(&Lt.px), li4 = ld4(&Lt.ix);
+        const V lpos{lp.x, lp.y, lp.z};
+        const float dist = len(sub(lpos, pnt));
+        const V ldir = nrm(sub(lpos, pnt));
+        const V ldir_real = nrm(sub(lpos, hitp));
+        const float cos_t = dot(ldir_real, n_);
+        const V E = divs(V{li4.x, li4.y, li4.z}, dist * dist);
+        if (cos_t >= s.cos_thr && cos_t <= 1.0f) {
+            const V hh = nrm(add(ldir, neg(nrm(d))));
+            const float base = smax(0.0f, dot(nrm(n_), hh));
+#ifdef RT_EXP_FASTPOW
+            const float ca = __powf(base, mA.w);      // experiment only: NOT the reference's rounding
+#else
+            const float ca = (float)pow((double)base, (double)mA.w);
+#endif
+            L = add(L, had(mul(V{mS.x, mS.y, mS.z}, ca), E));
+        }
+        const float cl = smax(0.0f, smin(1.0f, cos_t));
+        L = add(L, had(mul(V{mD.x, mD.y, mD.z}, cl), E));
+    }
+    return L;
+}
+
+// Occlusion bytes of record rid.  Up to four lights: the two aligned dwords
+// covering them, loaded together and decoded only where the bits are used, so
+// the loads stay in flight with the prefetched record (a byte loop waits for
+// every outstanding load).  The occlusion array is padded by 8 bytes for the
+// second dword.  More lights: decoded from the bytes at use.
+struct OccRaw {
+    uint32_t w0, w1;
+    size_t off;       // byte offset of the record's first light
+};
+template <bool SMALL>
+__device__ __forceinline__ OccRaw occ_load(const PcParams& p, size_t rid, int nl) {
+    OccRaw o;
+    o.off = rid * (size_t)nl;
+    if (SMALL) {
+        const uint32_t* wd = reinterpret_cast<const uint32_t*>(p.occ) + (o.off >> 2);
+        o.w0 = wd[0];
+        o.w1 = wd[1];
+    } else {
+        o.w0 = o.w1 = 0;
+    }
+    return o;
+}
+template <bool SMALL>
+__device__ __forceinline__ uint32_t occ_bits(const PcParams& p, const OccRaw& o, int nl) {
+    uint32_t m = 0;
+    if (SMALL) {
+        const uint64_t v = ((uint64_t)o.w0 | ((uint64_t)o.w1 << 32)) >> ((o.off & 3u) * 8u);
+#pragma unroll
+        for (int l = 0; l < 4; ++l)
+            if (l < nl && ((v >> (8 * l)) & 0xffu)) m |= 1u << l;
+    } else {
+        for (int l = 0; l < nl && l < 32; ++l) m |= (p.occ[o.off + l] ? 1u : 0u) << l;
+    }
+    return m;
+}
+
+// Shade and fold one sample's recorded levels deepest-first, the next
+// (shallower) level's record and occlusion bytes in flight while the current
+// one is shaded: c_k = clamp(L_k + c_{k+1} (x) km_k) (raytracer.cpp:436-451).
+template <bool LDS>
+__device__ __forceinline__ V path_shade_fold(const rtk::DevScene& s, const PcParams& p, unsigned path) {
+    const int info = p.pinfo[path];
+    const int nlev = info & 0xff, kind = info >> 8;
+    V c = kind == kEndBg ? V{s.bgx, s.bgy, s.bgz} : V{0.0f, 0.0f, 0.0f};
+    if (nlev == 0) return c;
+    const int nl = s.nlights;
+    size_t rid = (size_t)(nlev - 1) * p.cap + path;
+    float4 a = p.rec[rid * 3], b = p.rec[rid * 3 + 1], d = p.rec[rid * 3 + 2];
+    OccRaw oc = occ_load<LDS>(p, rid, nl);
+    for (int k = nlev - 1; k >= 0; --k) {
+        const dl::Material& M = fin_mat<LDS>(s, __float_as_int(a.w) - 1);   // before the prefetch (vmcnt order)
+        const float4 mA = ld4(&M.kax), mD = ld4(&M.kdx), mS = ld4(&M.ksx), km = ld4(&M.kmx);
+        const size_t rn = (size_t)max(k - 1, 0) * p.cap + path;
+#if RT_FINISH_PREFETCH
+        const float4 na = p.rec[rn * 3], nb = p.rec[rn * 3 + 1], nd = p.rec[rn * 3 + 2];
+        const OccRaw noc = occ_load<LDS>(p, rn, nl);
+#endif
+        const V L = shade_words<LDS>(s, p, rid, a, b, d, mA, mD, mS, occ_bits<LDS>(p, oc, nl));
+        if (kind == kEndLast && k == nlev - 1) c = vclamp(L, 0.0f, FLT_MAX);
+        else c = vclamp(add(L, had(c, V{km.x, km.y, km.z})), 0.0f, FLT_MAX);
+#if RT_FINISH_PREFETCH
+        rid = rn; a = na; b = nb; d = nd; oc = noc;
+#else
+        if (k > 0) {
+            rid = rn; a = p.rec[rn * 3]; b = p.rec[rn * 3 + 1]; d = p.rec[rn * 3 + 2];
+            oc = occ_load<LDS>(p, rn, nl);
+        }
+#endif
+    }
+    return c;
+}
+
+template <bool LDS>
+__device__ __forceinline__ void finish_pixels(const rtk::DevScene& s, const PcParams& p) {
+    const int lr0 = p.chunk_row0 / p.aa;
+    const int nrows = p.chunk_rows / p.aa;
+    const int npix = nrows * p.width;
+    const int F = p.aa;
+    for (int q = blockIdx.x * kBlock + threadIdx.x; q < npix; q += gridDim.x * kBlock) {
+        const int rr = q / p.width, ocol = q - rr * p.width;
+        const int lr = lr0 + rr;
+        if (lr >= p.slab_rows) continue;
+        const int stripe = lr / p.stripe_rows;
+        const int g = (stripe * p.nranks + p.rank) * p.stripe_rows + (lr - stripe * p.stripe_rows);
+        if (g >= p.height) continue;
+        uint32_t sr = 0, sg = 0, sb = 0;
+        for (int k = 0; k < F; ++k)
+            for (int l = 0; l < F; ++l) {
+                const V c = path_shade_fold<LDS>(s, p, slab_slot(p.tiles_x, ocol * F + l, rr * F + k));
+                sr += quantise(c.x); sg += quantise(c.y); sb += quantise(c.z);
+            }
+        const uint32_t ff = (uint32_t)(F * F);
+        uint8_t* o = p.out + ((size_t)lr * p.width + ocol) * 3;
+        o[0] = (uint8_t)(sr / ff); o[1] = (uint8_t)(sg / ff); o[2] = (uint8_t)(sb / ff);
+    }
+}
+
+// k_finish: k_shade + k_compose in one pass, one lane per output pixel, with
+// the scene's materials and lights in LDS (host checks they fit);
+// k_finish_any: the same for larger scenes, tables read from global memory.
+__global__ __launch_bounds__(kBlock, RT_FINISH_WAVES) void k_finish(rtk::DevScene s, PcParams p) {
+    float4* dm = reinterpret_cast<float4*>(g_fmats);
+    const float4* sm = reinterpret_cast<const float4*>(s.mats);
+    for (int i = threadIdx.x; i < s.nmats * 4; i += kBlock) dm[i] = sm[i];
+    float4* dl_ = reinterpret_cast<float4*>(g_flights);
+    const float4* sl = reinterpret_cast<const float4*>(s.lights);
+    for (int i = threadIdx.x; i < s.nlights * 2; i += kBlock) dl_[i] = sl[i];
+    __syncthreads();
+    finish_pixels<true>(s, p);
+}
+__global__ __launch_bounds__(kBlock, RT_FINISH_WAVES) void k_finish_any(rtk::DevScene s, PcParams p) {
+    finish_pixels<false>(s, p);
+}
+
 }  // namespace
+
+// Shading + fold + SSAA: k_finish (a lane per pixel, default) or k_shade (a
+// lane per record) then k_compose (p.shade_split).
+void launch_finish(const rtk::DevScene& s, const PcParams& p, hipStream_t st) {
+    const int npix = (p.chunk_rows / p.aa) * p.width;
+    const dim3 pgrid(std::max(1, (npix + kBlock - 1) / kBlock));
+    if (!p.shade_split) {
+        if (s.nmats <= kFinishMats && s.nlights <= kFinishLights)
+            hipLaunchKernelGGL(k_finish, pgrid, dim3(kBlock), 0, st, s, p);
+        else
+            hipLaunchKernelGGL(k_finish_any, pgrid, dim3(kBlock), 0, st, s, p);
+        return;
+    }
+    const size_t nrec = (size_t)p.levels * (size_t)p.n0;
+    hipLaunchKernelGGL(k_shade, dim3((unsigned)std::max<size_t>(1, std::min<size_t>(65535, (nrec + kBlock - 1) / kBlock))),
+                       dim3(kBlock), 0, st, s, p);
+    hipLaunchKernelGGL(k_compose, pgrid, dim3(kBlock), 0, st, s, p);
+}
 
 hipError_t chain_occupancy(int* chain_blocks_per_cu, int* mix_blocks_per_cu, int* occlude_blocks_per_cu) {
     hipError_t e = hipOccupancyMaxActiveBlocksPerMultiprocessor(chain_blocks_per_cu, k_chain<false>, kBlock, 0);
@@ -1212,11 +1399,7 @@ hipError_t launch_fused_chunk(const rtk::DevScene& s, const rtk::Eye& e, const P
         hipLaunchKernelGGL(k_fused<true>, dim3(p.grid), dim3(kBlock), 0, st, s, e, p);
     else
         hipLaunchKernelGGL(k_fused<false>, dim3(p.grid), dim3(kBlock), 0, st, s, e, p);
-    const int npix = (p.chunk_rows / p.aa) * p.width;
-    const size_t nrec = (size_t)p.levels * (size_t)p.n0;
-    hipLaunchKernelGGL(k_shade, dim3((unsigned)std::max<size_t>(1, std::min<size_t>(65535, (nrec + kBlock - 1) / kBlock))),
-                       dim3(kBlock), 0, st, s, p);
-    hipLaunchKernelGGL(k_compose, dim3(std::max(1, (npix + kBlock - 1) / kBlock)), dim3(kBlock), 0, st, s, p);
+    launch_finish(s, p, st);
     return hipGetLastError();
 }
 
@@ -1232,21 +1415,17 @@ hipError_t launch_chain_chunk(const rtk::DevScene& s, const rtk::Eye& e, const P
     const bool phase_b = p.kinline < s.max_depth;     // any continuation possible
     if (count) hipLaunchKernelGGL(k_chain<true>, dim3(p.grid), blk, 0, st, s, e, p);
     else hipLaunchKernelGGL(k_chain<false>, dim3(p.grid), blk, 0, st, s, e, p);
-    hipLaunchKernelGGL(k_scan_a, dim3(1), dim3(1024), 0, st, p);
+    hipLaunchKernelGGL(k_pack_a, dim3(p.grid), blk, 0, st, p);
     PcParams q = p;
     if (!phase_b) q.gb = 0;
     if (count) hipLaunchKernelGGL(k_mix<true>, dim3(q.gb + p.ogrid), blk, 0, st, s, e, q);
     else hipLaunchKernelGGL(k_mix<false>, dim3(q.gb + p.ogrid), blk, 0, st, s, e, q);
     if (phase_b) {
-        hipLaunchKernelGGL(k_scan_b, dim3(1), dim3(1024), 0, st, p);
+        hipLaunchKernelGGL(k_pack_b, dim3(p.gb), blk, 0, st, p);
         if (count) hipLaunchKernelGGL(k_occlude<true>, dim3(p.ogrid), blk, 0, st, s, p);
         else hipLaunchKernelGGL(k_occlude<false>, dim3(p.ogrid), blk, 0, st, s, p);
     }
-    const int npix = (p.chunk_rows / p.aa) * p.width;
-    const size_t nrec = (size_t)p.levels * (size_t)p.n0;          // a lane per record, then a lane per pixel
-    hipLaunchKernelGGL(k_shade, dim3((unsigned)std::max<size_t>(1, std::min<size_t>(65535, (nrec + kBlock - 1) / kBlock))),
-                       blk, 0, st, s, p);
-    hipLaunchKernelGGL(k_compose, dim3(std::max(1, (npix + kBlock - 1) / kBlock)), blk, 0, st, s, p);
+    launch_finish(s, p, st);
     return hipGetLastError();
 }
 

@@ -25,7 +25,7 @@
 
 namespace rtc {
 
-constexpr int kMaxChainGrid = 2048;   // k_chain workgroups (k_occlude keeps their prefix in LDS)
+constexpr int kMaxChainGrid = 2048;   // k_chain workgroups (= task-queue regions)
 
 enum PathKind : int {
     kEndBg = 0,     // deepest ray missed at depth 0: background
@@ -47,19 +47,21 @@ struct PcParams {
     unsigned* sqA;    // shadow tasks of A: [grid][scapA], owner = (level*cap + sample)*nl + light
     unsigned scapA;
     unsigned* scntA;  // [grid]
-    unsigned* sprefA; // [grid + 1]
+    unsigned* sflatA; // A's shadow tasks packed in region order (k_pack_a), totals[0] of them
     unsigned* cq;     // continuations of A: [grid][ccapA], owner = level*cap + sample of the last record
     unsigned ccapA;
     unsigned* ccnt;   // [grid]
-    unsigned* cpref;  // [grid + 1]
+    unsigned* cflat;  // continuations packed (k_pack_a), totals[1] of them
     unsigned* sqB;    // shadow tasks of B: [gb][scapB]
     unsigned scapB;
     unsigned* scntB;  // [gb]
-    unsigned* sprefB; // [gb + 1]
+    unsigned* sflatB; // B's shadow tasks packed (k_pack_b), totals[2] of them
+    unsigned* totals; // [3]
     int kinline;      // deepest level phase A walks (>= max_depth: no phase B)
     int gb;           // k_mix workgroups in the chain role (the other p.ogrid ones occlude A's tasks)
     int tchunk;       // continuation / shadow tasks are dealt to workgroups in chunks of this many
     int packet;       // 1: eye rays of a wave walk as one packet when exact (packet_closest)
+    int shade_split;  // 1: k_shade (a lane per record) + k_compose instead of k_finish
     int exp_skip_occ; // experiments only (RT_EXP_SKIP_OCC): k_mix's occlusion role does nothing (wrong images)
     int grid;         // k_chain persistent grid (= number of shadow-queue regions)
     int ogrid;        // k_occlude persistent grid

@@ -19,6 +19,7 @@ struct DevScene {
     const dl::Light* lights;
     int nnodes;
     int nlights;
+    int nmats;
     int max_depth;        // MaxRecursionDepth
     int stack_entries;    // LDS traversal-stack entries per thread
     float eps;            // ShadowRayEpsilon

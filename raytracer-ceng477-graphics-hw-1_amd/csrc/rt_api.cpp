@@ -254,6 +254,7 @@ int finish_scene(rt_scene* s, const rt_options* opts) {
     d.nodes = s->d_nodes; d.prims = s->d_prims; d.tri_shade = s->d_tri; d.mats = s->d_mats; d.lights = s->d_lights;
     d.nnodes = (int)s->bvh.nodes.size();
     d.nlights = (int)lights.size();
+    d.nmats = (int)mats.size();
     d.max_depth = s->host.max_depth;
     d.stack_entries = std::max(2, s->bvh.max_stack);
     d.eps = s->host.eps;
@@ -475,16 +476,17 @@ int render_chain(rt_scene* s, const rtk::Eye& eye, const rtk::FrameParams& f, bo
 
     ArenaLayout L;
     const size_t o_rec = L.take<float4>(3 * cap * levels), o_pinfo = L.take<int>(cap),
-                 o_occ = L.take<uint8_t>(cap * levels * nl);
-    size_t o_sqA = 0, o_scntA = 0, o_sprefA = 0, o_cq = 0, o_ccnt = 0, o_cpref = 0, o_sqB = 0, o_scntB = 0,
-           o_sprefB = 0, o_wq = 0;
+                 o_occ = L.take<uint8_t>(cap * levels * nl + 8);   // + 8: k_finish reads aligned dwords
+    size_t o_sqA = 0, o_scntA = 0, o_sflatA = 0, o_cq = 0, o_ccnt = 0, o_cflat = 0, o_sqB = 0, o_scntB = 0,
+           o_sflatB = 0, o_totals = 0, o_wq = 0;
     if (fused) {
         o_wq = L.take<unsigned>((size_t)G * 4 * wq_cap);
     } else {
-        o_sqA = L.take<unsigned>((size_t)G * scapA); o_scntA = L.take<unsigned>(G); o_sprefA = L.take<unsigned>(G + 1);
-        o_cq = L.take<unsigned>((size_t)G * ccapA); o_ccnt = L.take<unsigned>(G); o_cpref = L.take<unsigned>(G + 1);
+        o_sqA = L.take<unsigned>((size_t)G * scapA); o_scntA = L.take<unsigned>(G);
+        o_sflatA = L.take<unsigned>(cap * levels_a * nl);
+        o_cq = L.take<unsigned>((size_t)G * ccapA); o_ccnt = L.take<unsigned>(G); o_cflat = L.take<unsigned>(cap);
         o_sqB = L.take<unsigned>((size_t)gb * scapB); o_scntB = L.take<unsigned>(gb + 1);
-        o_sprefB = L.take<unsigned>(gb + 2);
+        o_sflatB = L.take<unsigned>(cap * (levels - levels_a) * nl); o_totals = L.take<unsigned>(4);
     }
     if (s->arena_bytes < L.off) {
         (void)hipFree(s->arena);
@@ -502,11 +504,12 @@ int render_chain(rt_scene* s, const rtk::Eye& eye, const rtk::FrameParams& f, bo
     p.pinfo = static_cast<int*>(at(o_pinfo));
     p.occ = static_cast<uint8_t*>(at(o_occ));
     p.sqA = static_cast<unsigned*>(at(o_sqA)); p.scapA = scapA;
-    p.scntA = static_cast<unsigned*>(at(o_scntA)); p.sprefA = static_cast<unsigned*>(at(o_sprefA));
+    p.scntA = static_cast<unsigned*>(at(o_scntA)); p.sflatA = static_cast<unsigned*>(at(o_sflatA));
     p.cq = static_cast<unsigned*>(at(o_cq)); p.ccapA = ccapA;
-    p.ccnt = static_cast<unsigned*>(at(o_ccnt)); p.cpref = static_cast<unsigned*>(at(o_cpref));
+    p.ccnt = static_cast<unsigned*>(at(o_ccnt)); p.cflat = static_cast<unsigned*>(at(o_cflat));
     p.sqB = static_cast<unsigned*>(at(o_sqB)); p.scapB = scapB;
-    p.scntB = static_cast<unsigned*>(at(o_scntB)); p.sprefB = static_cast<unsigned*>(at(o_sprefB));
+    p.scntB = static_cast<unsigned*>(at(o_scntB)); p.sflatB = static_cast<unsigned*>(at(o_sflatB));
+    p.totals = static_cast<unsigned*>(at(o_totals));
     p.kinline = phase_b ? kinline : 1 << 30;
     p.gb = gb;
     p.ogrid = phase_b ? std::max(1, s->mix_grid - gb) : s->mix_grid;
@@ -519,6 +522,7 @@ int render_chain(rt_scene* s, const rtk::Eye& eye, const rtk::FrameParams& f, bo
     p.tchunk = s->tune_tchunk;
     p.packet = s->tune_packet && s->bvh.max_stack <= dl::kMaxStack;
     p.exp_skip_occ = std::getenv("RT_EXP_SKIP_OCC") ? 1 : 0;
+    p.shade_split = std::getenv("RT_SHADE_SPLIT") ? std::atoi(std::getenv("RT_SHADE_SPLIT")) : 0;
     p.wide = s->bvh.max_depth <= 26 ? s->tune_wide : 0;   // path keys hold 26 levels
     p.wide_min = s->tune_wide_min;
     p.spread = s->tune_spread;

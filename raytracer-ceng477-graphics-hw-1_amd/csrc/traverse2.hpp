@@ -37,6 +37,42 @@ __device__ __forceinline__ void leaf_range(const rtk::DevScene& s, int info, int
     }
 }
 
+// The primitives [a, a+cnt) of a leaf, each passed to f(i, p0, p1, p2) with
+// all three of its float4 already loaded (a sphere ignores p2), stopping when
+// f returns true.  The three loads of a primitive are issued together (left
+// to itself the compiler sinks p2 - and parts of p1 - into the triangle branch,
+// a second dependent round trip), and the next primitive's loads are in flight
+// while the current one is tested.
+#ifndef RT_CLOSEST_PIPE
+#define RT_CLOSEST_PIPE 0     // closest-hit leaves through for_prims too
+#endif
+#ifndef RT_PRIM_PREFETCH
+#define RT_PRIM_PREFETCH 1
+#endif
+__device__ __forceinline__ void prim_ready(const float4& a, const float4& b, const float4& c) {
+    asm volatile("" ::"v"(a.x), "v"(a.y), "v"(a.z), "v"(a.w), "v"(b.x), "v"(b.y), "v"(b.z), "v"(b.w), "v"(c.x),
+                 "v"(c.y), "v"(c.z), "v"(c.w));
+}
+template <class F>
+__device__ __forceinline__ bool for_prims(const rtk::DevScene& s, int a, int cnt, F&& f) {
+    if (cnt <= 0) return false;
+    const float4* base = reinterpret_cast<const float4*>(s.prims);
+    float4 c0 = base[3 * a], c1 = base[3 * a + 1], c2 = base[3 * a + 2];
+    for (int i = a; i < a + cnt; ++i) {
+        prim_ready(c0, c1, c2);
+        const float4 p0 = c0, p1 = c1, p2 = c2;
+#if RT_PRIM_PREFETCH
+        const int nx = min(i + 1, a + cnt - 1);
+#else
+        const int nx = i + 1;
+        if (nx < a + cnt)
+#endif
+        { c0 = base[3 * nx]; c1 = base[3 * nx + 1]; c2 = base[3 * nx + 2]; }
+        if (f(i, p0, p1, p2)) return true;
+    }
+    return false;
+}
+
 template <bool COUNT, int STRIDE>
 __device__ __forceinline__ HitRec closest_hit2(const rtk::DevScene& s, const Ray& r, int2* stk, Work& w) {
     HitRec best{-1.0f, -1};
@@ -281,7 +317,7 @@ __device__ __forceinline__ bool walk_begin(const rtk::DevScene& s, const Ray& r,
 }
 
 // One closest-hit step; returns true when the walk is finished (result in k.best).
-template <bool COUNT, class FETCH, class STK>
+template <bool COUNT, class FETCH, class STK, bool PIPE = false>
 __device__ __forceinline__ bool closest_step(const rtk::DevScene& s, const Ray& r, STK& stk, Walk& k, Work& w) {
     if (k.cur >= 0) {
         float4 l0, l1, r0, r1;
@@ -306,14 +342,12 @@ __device__ __forceinline__ bool closest_step(const rtk::DevScene& s, const Ray& 
     } else {
         int a, cnt;
         leaf_range(s, k.cur, &a, &cnt);
-        for (int i = a; i < a + cnt; ++i) {
-            const float4* pr = reinterpret_cast<const float4*>(&s.prims[i]);
-            const float4 p0 = pr[0], p1 = pr[1];
+        auto test = [&](int i, const float4& p0, const float4& p1, const float4& p2) {
             float t;
             bool h;
             if (__float_as_int(p0.w) >= 0) {
                 if (COUNT) w.tris++;
-                h = tri_hit(r, p0, p1, pr[2], &t);
+                h = tri_hit(r, p0, p1, p2, &t);
             } else {
                 if (COUNT) w.spheres++;
                 h = sphere_hit(r, p0, p1, &t);
@@ -322,6 +356,16 @@ __device__ __forceinline__ bool closest_step(const rtk::DevScene& s, const Ray& 
                 k.best.t = t;
                 k.best.prim = i;
                 k.tmax = t;
+            }
+            return false;
+        };
+        if (PIPE || RT_CLOSEST_PIPE) {
+            for_prims(s, a, cnt, test);
+        } else {
+            // plain loop: the pipelined one costs k_chain a wave per SIMD (VGPRs)
+            for (int i = a; i < a + cnt; ++i) {
+                const float4* pr = reinterpret_cast<const float4*>(&s.prims[i]);
+                test(i, pr[0], pr[1], pr[2]);
             }
         }
     }
@@ -362,20 +406,19 @@ __device__ __forceinline__ int any_step(const rtk::DevScene& s, const Ray& r, fl
     } else {
         int a, cnt;
         leaf_range(s, k.cur, &a, &cnt);
-        for (int i = a; i < a + cnt; ++i) {
-            const float4* pr = reinterpret_cast<const float4*>(&s.prims[i]);
-            const float4 p0 = pr[0], p1 = pr[1];
-            float t;
-            bool h;
-            if (__float_as_int(p0.w) >= 0) {
-                if (COUNT) w.tris++;
-                h = tri_hit(r, p0, p1, pr[2], &t);
-            } else {
-                if (COUNT) w.spheres++;
-                h = sphere_hit(r, p0, p1, &t);
-            }
-            if (h && t < tlim) return 2;
-        }
+        if (for_prims(s, a, cnt, [&](int, const float4& p0, const float4& p1, const float4& p2) {
+                float t;
+                bool h;
+                if (__float_as_int(p0.w) >= 0) {
+                    if (COUNT) w.tris++;
+                    h = tri_hit(r, p0, p1, p2, &t);
+                } else {
+                    if (COUNT) w.spheres++;
+                    h = sphere_hit(r, p0, p1, &t);
+                }
+                return h && t < tlim;
+            }))
+            return 2;
     }
     while (k.sp > 0) {
         --k.sp;
@@ -439,20 +482,19 @@ __device__ __forceinline__ int quad_any_step(const rtk::DevScene& s, const Ray& 
         if (box_hit_fast(r, lo, hi, &bt)) {          // the reference leaf's exact box (NaN-free ray)
             int a, cnt;
             leaf_range(s, __float_as_int(lo.w), &a, &cnt);
-            for (int i = a; i < a + cnt; ++i) {
-                const float4* pr = reinterpret_cast<const float4*>(&s.prims[i]);
-                const float4 p0 = pr[0], p1 = pr[1];
-                float t;
-                bool h;
-                if (__float_as_int(p0.w) >= 0) {
-                    if (COUNT) w.tris++;
-                    h = tri_hit(r, p0, p1, pr[2], &t);
-                } else {
-                    if (COUNT) w.spheres++;
-                    h = sphere_hit(r, p0, p1, &t);
-                }
-                if (h && t < tlim) return 2;
-            }
+            if (for_prims(s, a, cnt, [&](int, const float4& p0, const float4& p1, const float4& p2) {
+                    float t;
+                    bool h;
+                    if (__float_as_int(p0.w) >= 0) {
+                        if (COUNT) w.tris++;
+                        h = tri_hit(r, p0, p1, p2, &t);
+                    } else {
+                        if (COUNT) w.spheres++;
+                        h = sphere_hit(r, p0, p1, &t);
+                    }
+                    return h && t < tlim;
+                }))
+                return 2;
         }
     }
     if (k.sp > 0) {

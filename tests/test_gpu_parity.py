@@ -127,6 +127,15 @@ def test_max_depth_override_matches_derived_scene(goldens, pkg, scene_dir, torch
     assert np.array_equal(img, load_golden_image(g["cameras"][0]))
 
 
+def _extra_lights(xml, n):
+    """The scene with n more point lights (positions/intensities spread around the first)."""
+    extra = "".join(
+        f'<PointLight id="{100 + i}"><Position>{-3 + 1.5 * i} {2 + 0.5 * i} {1 - i}</Position>'
+        f"<Intensity>{900 * (i + 1)} {700 * (i + 2)} {500 * (i + 3)}</Intensity></PointLight>\n"
+        for i in range(n))
+    return xml.replace("</Lights>", extra + "</Lights>", 1)
+
+
 @pytest.mark.parametrize("path", PATHS)
 def test_edge_scenes_vs_oracle(path, pkg, oracle, tmp_path, torch_cuda):
     """Empty object list (all background), negative depth (all black), odd sizes, AA 5."""
@@ -137,6 +146,9 @@ def test_edge_scenes_vs_oracle(path, pkg, oracle, tmp_path, torch_cuda):
         "neg_depth": pkg.scenes.derive_xml(base, depth=-1, res=(17, 9)),
         "odd_aa5": pkg.scenes.derive_xml(base, res=(33, 19)),
         "mirror_odd": pkg.scenes.derive_xml(pkg.scenes.scene_text("mirror_spheres.xml"), res=(61, 45)),
+        # > 4 lights: k_finish_any (materials / lights from global memory, byte-wise occlusion)
+        "six_lights": pkg.scenes.derive_xml(_extra_lights(pkg.scenes.scene_text("mirror_spheres.xml"), 5),
+                                            res=(41, 37)),
     }
     for name, xml in cases.items():
         p = tmp_path / f"{name}.xml"
