@@ -70,20 +70,24 @@ struct LeafBig { int32_t start, count; };
 //   {qlo[4][3] bytes, qhi[4][3] bytes}          child c box, axis a:
 //       lo = origin_a + qlo[c][a] * scale_a,  hi = origin_a + qhi[c][a] * scale_a  (float, exact
 //       power-of-two scale; the host verifies every decoded box CONTAINS the child's exact box)
-//   {child[4]}  >= 0: quad index; < 0: kLeafBit | index into QLeaf (a reference leaf)
+//   {child[4]}  >= 0: quad index; < 0: kLeafBit | offset of a leaf record (16-B units) in LeafRec[]
 //   {pad[2]}
-// Leaves are the reference BVH's leaves; QLeaf holds their EXACT boxes, tested
-// exactly before the leaf's primitives (see build_shadow_tree).
+// Leaves are the reference BVH's leaves.  A leaf record is the leaf's header
+// (its EXACT box, tested exactly before the primitives) followed by copies of
+// its primitives, so the box and the first primitive arrive in one round trip:
+//   LeafHead {lo.xyz, count} {hi.xyz, slot0}   slot0 = Prim[] index of the first primitive
+//   count x Prim (48 B, same encoding and order as Prim[])
 struct alignas(16) Quad {
     float ox, oy, oz; uint32_t exps;
     uint32_t q[6];        // bytes: qlo c0..c3 x,y,z (12), then qhi c0..c3 x,y,z (12)
     int32_t child[4];
     int32_t pad[2];
 };
-struct alignas(16) QLeaf {
-    float minx, miny, minz; int32_t info;    // info: the reference leaf code (kLeafBit | count | start)
-    float maxx, maxy, maxz; int32_t pad;
+struct alignas(16) LeafHead {
+    float minx, miny, minz; int32_t count;
+    float maxx, maxy, maxz; int32_t slot0;
 };
+struct alignas(16) Vec4 { uint32_t v[4]; };   // 16-B unit of the leaf-record array
 #ifndef RT_TOP_PAIRS
 #define RT_TOP_PAIRS 256
 #endif
@@ -94,7 +98,7 @@ constexpr int kLeafMaxCount = 63;
 
 static_assert(sizeof(Pair) == 64, "pair size");
 static_assert(sizeof(Quad) == 64, "quad size");
-static_assert(sizeof(QLeaf) == 32, "qleaf size");
+static_assert(sizeof(LeafHead) == 32, "leaf head size");
 static_assert(sizeof(Node) == 32, "node size");
 static_assert(sizeof(Prim) == 48, "prim size");
 static_assert(sizeof(Material) == 64, "material size");

@@ -674,18 +674,26 @@ void build_shadow_tree(FlatBVH& out) {
     auto pow2 = [](int e) { return ibits(e << 23); };                       // 2^(e-127), e in [1, 254]
     auto dec = [](float o, int q, float sc) { return o + (float)q * sc; };  // device decode, no contraction
     out.quads.clear();
-    out.qleaves.clear();
+    out.lrec.clear();
     out.qmax_depth = 0;
-    bool contain_ok = true;
+    bool contain_ok = true, lrec_ok = true;
     std::function<int32_t(int, int)> emit = [&](int n, int depth) -> int32_t {
         out.qmax_depth = std::max(out.qmax_depth, depth);
         const TNode& t = tn[n];
         if (t.left < 0) {
-            dl::QLeaf l{};
-            l.minx = t.box.lo[0]; l.miny = t.box.lo[1]; l.minz = t.box.lo[2]; l.info = t.info;
-            l.maxx = t.box.hi[0]; l.maxy = t.box.hi[1]; l.maxz = t.box.hi[2]; l.pad = 0;
-            out.qleaves.push_back(l);
-            return dl::kLeafBit | (int32_t)(out.qleaves.size() - 1);
+            int32_t start, count;
+            const int32_t c = (t.info >> dl::kLeafCountShift) & dl::kLeafMaxCount, st = t.info & dl::kLeafStartMask;
+            if (c != 0) { start = st; count = c; }
+            else { start = out.leaf_big[st].start; count = out.leaf_big[st].count; }
+            const size_t off = out.lrec.size();
+            if (off > (size_t)INT32_MAX - 1 - (2 + 3 * (size_t)count)) lrec_ok = false;
+            dl::LeafHead h{};
+            h.minx = t.box.lo[0]; h.miny = t.box.lo[1]; h.minz = t.box.lo[2]; h.count = count;
+            h.maxx = t.box.hi[0]; h.maxy = t.box.hi[1]; h.maxz = t.box.hi[2]; h.slot0 = start;
+            out.lrec.resize(off + 2 + 3 * (size_t)count);
+            std::memcpy(&out.lrec[off], &h, sizeof(h));
+            if (count > 0) std::memcpy(&out.lrec[off + 2], &out.prims[start], sizeof(dl::Prim) * (size_t)count);
+            return dl::kLeafBit | (int32_t)off;
         }
         std::vector<int> ch{t.left, t.right};
         while (ch.size() < 4) {
@@ -739,9 +747,10 @@ void build_shadow_tree(FlatBVH& out) {
         return me;
     };
     out.qroot = emit(root, 0);
-    if (!contain_ok || 3 * out.qmax_depth + 4 > dl::kMaxStack) {   // fall back to the binary occlusion tree
+    out.lrec.resize(out.lrec.size() + 3);    // a leaf's first-prim loads may run past a 0-prim last leaf
+    if (!contain_ok || !lrec_ok || 3 * out.qmax_depth + 4 > dl::kMaxStack) {   // fall back to the binary tree
         out.quads.clear();
-        out.qleaves.clear();
+        out.lrec.clear();
     }
 }
 

@@ -64,8 +64,8 @@ struct FlatBVH {
     int smax_depth = 0;
     // the same occlusion tree collapsed to 4-wide nodes with quantized child boxes
     std::vector<dl::Quad> quads;
-    std::vector<dl::QLeaf> qleaves;
-    int32_t qroot = 0;               // >= 0 quad index, < 0 kLeafBit | qleaf index
+    std::vector<dl::Vec4> lrec;      // leaf records (LeafHead + prims), 16-B units, + 3 units of tail pad
+    int32_t qroot = 0;               // >= 0 quad index, < 0 kLeafBit | leaf-record offset
     int qmax_depth = 0;
     int leaves = 0, max_leaf = 0, max_depth = 0, max_stack = 0;
     double build_ms = 0;

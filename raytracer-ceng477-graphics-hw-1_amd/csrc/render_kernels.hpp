@@ -40,8 +40,9 @@ struct DevScene {
     int use_stree;        // NaN-free shadow rays walk: 0 the BVH, 1 the binary occlusion tree, 2 its 4-wide form
     int count_stree;      // diagnostics: counting passes walk the occlusion tree too (counts then differ)
     const dl::Quad* quads;
-    const dl::QLeaf* qleaves;
+    const float4* lrec;   // leaf records (dl::LeafHead + prims), indexed in 16-B units
     int qroot;
+    int use_sclosest;     // NaN-free closest-hit rays walk the occlusion tree first, certified (traverse2.hpp)
 
     // Sphere prims carry ~sphere_index in p0.w (negative), triangles their id.
     __device__ __forceinline__ bool prim_is_sphere(int, const float4 p0) const {

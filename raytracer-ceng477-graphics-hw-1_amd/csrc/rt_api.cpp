@@ -100,7 +100,7 @@ struct rt_scene {
     dl::Pair* d_pairs = nullptr;
     dl::Pair* d_spairs = nullptr;
     dl::Quad* d_quads = nullptr;
-    dl::QLeaf* d_qleaves = nullptr;
+    dl::Vec4* d_lrec = nullptr;
     dl::LeafBig* d_leafbig = nullptr;
     enum Path { kChain, kWavefront, kMegakernel, kFused } path = kChain;
     int grid_blocks = 2048;
@@ -151,7 +151,7 @@ struct rt_scene {
     ~rt_scene() {
         free_ws();
         (void)hipFree(arena);
-        (void)hipFree(d_pairs); (void)hipFree(d_leafbig); (void)hipFree(d_spairs); (void)hipFree(d_quads); (void)hipFree(d_qleaves);
+        (void)hipFree(d_pairs); (void)hipFree(d_leafbig); (void)hipFree(d_spairs); (void)hipFree(d_quads); (void)hipFree(d_lrec);
         (void)hipFree(d_nodes); (void)hipFree(d_prims); (void)hipFree(d_tri); (void)hipFree(d_mats); (void)hipFree(d_lights);
         (void)hipFree(d_counters); (void)hipFree(d_out); (void)hipFree(d_trace);
         if (ev0) (void)hipEventDestroy(ev0);
@@ -207,7 +207,7 @@ int finish_scene(rt_scene* s, const rt_options* opts) {
     if ((rc = upload(&s->d_leafbig, s->bvh.leaf_big))) return rc;
     if ((rc = upload(&s->d_spairs, s->bvh.spairs))) return rc;
     if ((rc = upload(&s->d_quads, s->bvh.quads))) return rc;
-    if ((rc = upload(&s->d_qleaves, s->bvh.qleaves))) return rc;
+    if ((rc = upload(&s->d_lrec, s->bvh.lrec))) return rc;
     HIP_TRY(hipMalloc(reinterpret_cast<void**>(&s->d_counters), 8 * sizeof(unsigned long long)));
     HIP_TRY(hipMemset(s->d_counters, 0, 8 * sizeof(unsigned long long)));
     HIP_TRY(hipEventCreate(&s->ev0));
@@ -277,7 +277,7 @@ int finish_scene(rt_scene* s, const rt_options* opts) {
     }
     d.sroot_info = s->bvh.sroot_info;
     d.quads = s->d_quads;
-    d.qleaves = s->d_qleaves;
+    d.lrec = reinterpret_cast<const float4*>(s->d_lrec);
     d.qroot = s->bvh.qroot;
     // occlusion tree for NaN-free shadow rays: 2 = 4-wide quantized form, 1 = binary, 0 = off (RT_STREE)
     d.use_stree = !s->bvh.quads.empty() ? 2 : (s->bvh.spairs.empty() ? 0 : 1);
@@ -285,6 +285,9 @@ int finish_scene(rt_scene* s, const rt_options* opts) {
         const int v = std::atoi(e);
         d.use_stree = v <= 0 ? 0 : (v >= 2 && !s->bvh.quads.empty() ? 2 : (s->bvh.spairs.empty() ? 0 : 1));
     }
+    // closest-hit walks of NaN-free rays: certified walk over the 4-wide occlusion tree (RT_SCLOSEST=0: off)
+    d.use_sclosest = s->bvh.quads.empty() ? 0 : 1;
+    if (const char* e = std::getenv("RT_SCLOSEST")) d.use_sclosest = d.use_sclosest && std::atoi(e) != 0;
     // diagnostics: counting passes walk the occlusion tree too (counts then measure that tree)
     d.count_stree = std::getenv("RT_STREE_COUNT") ? 1 : 0;
     if (const char* e = std::getenv("RT_PRIO")) d.prio = std::atoi(e) != 0;

@@ -219,13 +219,38 @@ __device__ __forceinline__ bool any_hit2(const rtk::DevScene& s, const Ray& r, f
 // Pairs [0, s.top_pairs) (the top levels) are read from an LDS copy.
 // ---------------------------------------------------------------------------
 struct Walk {
-    const dl::Pair* tree;   // pair array the walk indexes (the BVH, or the occlusion tree)
-    int cur;       // node to process (pair index or leaf code)
+    const dl::Pair* tree;   // pair array the walk indexes (BVH or binary occlusion tree); null: 4-wide tree
+    int cur;       // node to process (pair/quad index or leaf code)
     int sp;        // stack depth
     float tmax;    // closest-hit pruning bound
     HitRec best;   // closest-hit result so far
     bool fast;     // ray_nan_free: box tests may use v_min/v_max
+    float blt;     // certified closest hit (4-wide tree): entry t of the winner's leaf box
+    float t2;      // ... smallest t among the other hits (-inf: a hit with t < 0 or NaN)
 };
+
+// Certified closest hit over the 4-wide occlusion tree (binned-SAH
+// hierarchy above the reference's own leaves, exact leaf boxes; see
+// build_shadow_tree).  The reference returns the first minimum, in its DFS
+// order, over the leaves V it visits; a leaf is visited iff its box (and, by
+// monotonicity, every ancestor's) is hit with entry t <= tMax when popped,
+// where tMax is FLT_MAX or the t of an already visited primitive.  The
+// 4-wide walk goes front to back with pruning bound sah_bound(best) and finds
+// the minimum t_w over the reachable leaves R, its primitive w, and t2, the
+// smallest t of the other hits it met.  w is the reference's answer when
+//   (1) t2 > t_w: no tie (ties are decided by DFS position) and no negative
+//       or NaN t (the `best.t == -1` sentinel rule, raytracer.cpp:213-221);
+//   (2) blt <= t_w: w's leaf is popped with tMax >= t_w >= its entry t; or
+//       blt <= sah_late(t_w) (rounding put the hit just before its leaf's
+//       entry) and t2 >= blt: no other primitive can bring tMax below the
+//       entry before that leaf is popped.
+// Otherwise the walk restarts on the reference tree (walk_restart_ref).  The
+// pruning slack makes this exact unless some primitive's hit lies more than
+// 2^-10 (relative) before the entry t of its own leaf box; the measured worst
+// case over the goldens' scenes is 1e-5 (flat axis-aligned leaves, where
+// Cramer's t and the slab t round differently): tools/exp_sah_closest.cpp.
+__device__ __forceinline__ float sah_bound(float t) { return t + t * 0.001953125f; }
+__device__ __forceinline__ float sah_late(float t) { return t + t * 0.0009765625f; }
 
 // Both child boxes of a pair; the min/max form when every active lane's ray
 // is NaN-free (wave-uniform branch, so no divergence between the two forms).
@@ -309,6 +334,13 @@ __device__ __forceinline__ bool walk_begin(const rtk::DevScene& s, const Ray& r,
         const float4 hi = make_float4(s.sroot_hi[0], s.sroot_hi[1], s.sroot_hi[2], 0.0f);
         return box_hit(r, lo, hi, &bt);
     }
+    if (!COUNT && !any && k.fast && s.use_sclosest) {
+        k.tree = nullptr;                    // certified closest hit over the 4-wide tree
+        k.cur = s.qroot;
+        k.t2 = __builtin_inff();
+        k.blt = __builtin_inff();
+        return true;
+    }
     k.tree = s.pairs;
     k.cur = s.root_info;
     const float4 lo = make_float4(s.root_lo[0], s.root_lo[1], s.root_lo[2], 0.0f);
@@ -316,9 +348,156 @@ __device__ __forceinline__ bool walk_begin(const rtk::DevScene& s, const Ray& r,
     return box_hit(r, lo, hi, &bt) && (any || bt <= k.tmax);
 }
 
+// Restart a closest-hit walk on the reference tree (certification failed).
+// false: the root box is missed, no hit.
+__device__ __forceinline__ bool walk_restart_ref(const rtk::DevScene& s, const Ray& r, Walk& k) {
+    k.best = HitRec{-1.0f, -1};
+    k.tmax = FLT_MAX;
+    k.sp = 0;
+    k.tree = s.pairs;
+    k.cur = s.root_info;
+    float bt;
+    const float4 lo = make_float4(s.root_lo[0], s.root_lo[1], s.root_lo[2], 0.0f);
+    const float4 hi = make_float4(s.root_hi[0], s.root_hi[1], s.root_hi[2], 0.0f);
+    return box_hit(r, lo, hi, &bt) && bt <= k.tmax;
+}
+
+// Child boxes of a 4-wide node (dl::Quad), decoded exactly as the host
+// verified them (origin + q * 2^e, no contraction).
+struct QuadKids {
+    float4 lo[4], hi[4];
+    int code[4];
+    int n;
+};
+__device__ __forceinline__ void quad_load(const rtk::DevScene& s, int qi, QuadKids& c) {
+    const float4* q = reinterpret_cast<const float4*>(&s.quads[qi]);
+    const float4 q0 = q[0], q1 = q[1], q2 = q[2], q3 = q[3];
+    const uint32_t ex = __float_as_uint(q0.w);
+    c.n = (int)(ex >> 24);
+    const float sx = __uint_as_float((ex & 255u) << 23), sy = __uint_as_float(((ex >> 8) & 255u) << 23),
+                sz = __uint_as_float(((ex >> 16) & 255u) << 23);
+    const uint32_t qb[6] = {__float_as_uint(q1.x), __float_as_uint(q1.y), __float_as_uint(q1.z),
+                            __float_as_uint(q1.w), __float_as_uint(q2.x), __float_as_uint(q2.y)};
+    c.code[0] = __float_as_int(q2.z);
+    c.code[1] = __float_as_int(q2.w);
+    c.code[2] = __float_as_int(q3.x);
+    c.code[3] = __float_as_int(q3.y);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        const int b0 = i * 3, b1 = 12 + i * 3;
+        auto byte = [&](int j) { return (float)((qb[j >> 2] >> ((j & 3) * 8)) & 255u); };
+        c.lo[i] = make_float4(q0.x + byte(b0) * sx, q0.y + byte(b0 + 1) * sy, q0.z + byte(b0 + 2) * sz, 0.0f);
+        c.hi[i] = make_float4(q0.x + byte(b1) * sx, q0.y + byte(b1 + 1) * sy, q0.z + byte(b1 + 2) * sz, 0.0f);
+    }
+}
+
+// Primitives of a leaf record (header at L[0..1], prims from L[2]); the first
+// one is passed in already loaded, the next one is in flight while the
+// current one is tested.  f(slot, p0, p1, p2) with slot = its Prim[] index;
+// stops when f returns true.
+template <class F>
+__device__ __forceinline__ bool for_leaf_prims(const float4* L, int slot0, int cnt, float4 c0, float4 c1, float4 c2,
+                                               F&& f) {
+    const float4* base = L + 2;
+    for (int j = 0; j < cnt; ++j) {
+        prim_ready(c0, c1, c2);
+        const float4 p0 = c0, p1 = c1, p2 = c2;
+        const int nx = min(j + 1, cnt - 1);
+        c0 = base[3 * nx];
+        c1 = base[3 * nx + 1];
+        c2 = base[3 * nx + 2];
+        if (f(slot0 + j, p0, p1, p2)) return true;
+    }
+    return false;
+}
+
+// One step of the certified closest-hit walk over the 4-wide tree (see
+// sah_bound); true when finished (result in k.best).  NaN-free rays only.
+template <class STK>
+__device__ __forceinline__ bool quad_closest_step(const rtk::DevScene& s, const Ray& r, STK& stk, Walk& k) {
+    constexpr int kNone = 0x7fffffff;         // no child (never a quad index or leaf code)
+    if (k.cur >= 0) {
+        QuadKids q;
+        quad_load(s, k.cur, q);
+        float t[4];
+        int c[4];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            float ti;
+            const bool h = i < q.n && box_hit_fast(r, q.lo[i], q.hi[i], &ti) && ti <= k.tmax;
+            t[i] = h ? ti : __builtin_inff();
+            c[i] = h ? q.code[i] : kNone;
+        }
+        auto cswap = [&](int a, int b) {
+            const bool sw = t[b] < t[a];
+            const float ta = t[a], tb = t[b];
+            const int ca = c[a], cb = c[b];
+            t[a] = sw ? tb : ta;
+            t[b] = sw ? ta : tb;
+            c[a] = sw ? cb : ca;
+            c[b] = sw ? ca : cb;
+        };
+        cswap(0, 1);
+        cswap(2, 3);
+        cswap(0, 2);
+        cswap(1, 3);
+        cswap(1, 2);
+#pragma unroll
+        for (int i = 3; i >= 1; --i)
+            if (c[i] != kNone) {
+                stk.put(k.sp, make_int2(c[i], __float_as_int(t[i])));
+                ++k.sp;
+            }
+        if (c[0] != kNone) {
+            k.cur = c[0];
+            return false;
+        }
+    } else {
+        const float4* L = s.lrec + (k.cur & ~dl::kLeafBit);
+        const float4 h0 = L[0], h1 = L[1], c0 = L[2], c1 = L[3], c2 = L[4];
+        float lt;
+        if (box_hit_fast(r, h0, h1, &lt) && lt <= k.tmax) {   // the reference leaf's exact box
+            for_leaf_prims(L, __float_as_int(h1.w), __float_as_int(h0.w), c0, c1, c2,
+                           [&](int slot, const float4& p0, const float4& p1, const float4& p2) {
+                               float ti;
+                               const bool h = __float_as_int(p0.w) >= 0 ? tri_hit(r, p0, p1, p2, &ti)
+                                                                        : sphere_hit(r, p0, p1, &ti);
+                               if (h) {
+                                   if (ti < k.best.t || k.best.t == -1.0f) {
+                                       if (k.best.prim >= 0) k.t2 = smin(k.t2, k.best.t);
+                                       k.blt = lt;
+                                       k.best.t = ti;
+                                       k.best.prim = slot;
+                                       k.tmax = sah_bound(ti);
+                                   } else {
+                                       k.t2 = smin(k.t2, ti);
+                                   }
+                                   if (!(ti >= 0.0f)) k.t2 = -__builtin_inff();
+                               }
+                               return false;
+                           });
+        }
+    }
+    while (k.sp > 0) {
+        --k.sp;
+        const int2 e = stk.at(k.sp);
+        if (__int_as_float(e.y) <= k.tmax) {
+            k.cur = e.x;
+            return false;
+        }
+    }
+    if (k.best.prim >= 0) {
+        const float tw = k.best.t;
+        const bool ok = k.t2 > tw && (k.blt <= tw || (k.blt <= sah_late(tw) && k.t2 >= k.blt));
+        if (!ok) return !walk_restart_ref(s, r, k);
+    }
+    return true;
+}
+
 // One closest-hit step; returns true when the walk is finished (result in k.best).
 template <bool COUNT, class FETCH, class STK, bool PIPE = false>
 __device__ __forceinline__ bool closest_step(const rtk::DevScene& s, const Ray& r, STK& stk, Walk& k, Work& w) {
+    if (!COUNT && k.tree == nullptr) return quad_closest_step(s, r, stk, k);
     if (k.cur >= 0) {
         float4 l0, l1, r0, r1;
         fetch_pair(k, l0, l1, r0, r1);
@@ -442,31 +621,20 @@ template <bool COUNT, class STK>
 __device__ __forceinline__ int quad_any_step(const rtk::DevScene& s, const Ray& r, float tlim, STK& stk, Walk& k,
                                              Work& w) {
     if (k.cur >= 0) {
-        const float4* q = reinterpret_cast<const float4*>(&s.quads[k.cur]);
-        const float4 q0 = q[0], q1 = q[1], q2 = q[2], q3 = q[3];
-        const uint32_t ex = __float_as_uint(q0.w);
-        const int n = (int)(ex >> 24);
-        const float sx = __uint_as_float((ex & 255u) << 23), sy = __uint_as_float(((ex >> 8) & 255u) << 23),
-                    sz = __uint_as_float(((ex >> 16) & 255u) << 23);
-        const uint32_t qb[6] = {__float_as_uint(q1.x), __float_as_uint(q1.y), __float_as_uint(q1.z),
-                                __float_as_uint(q1.w), __float_as_uint(q2.x), __float_as_uint(q2.y)};
-        const int ch[4] = {__float_as_int(q2.z), __float_as_int(q2.w), __float_as_int(q3.x), __float_as_int(q3.y)};
+        QuadKids q;
+        quad_load(s, k.cur, q);
         int next = 0;
         bool have = false;
 #pragma unroll
         for (int c = 0; c < 4; ++c) {
-            const int b0 = c * 3, b1 = 12 + c * 3;
-            auto byte = [&](int i) { return (float)((qb[i >> 2] >> ((i & 3) * 8)) & 255u); };
-            const float4 lo = make_float4(q0.x + byte(b0) * sx, q0.y + byte(b0 + 1) * sy, q0.z + byte(b0 + 2) * sz, 0.0f);
-            const float4 hi = make_float4(q0.x + byte(b1) * sx, q0.y + byte(b1 + 1) * sy, q0.z + byte(b1 + 2) * sz, 0.0f);
             float t;
-            if (c < n && box_hit_fast(r, lo, hi, &t)) {
+            if (c < q.n && box_hit_fast(r, q.lo[c], q.hi[c], &t)) {
                 if (COUNT) w.nodes++;
                 if (!have) {
-                    next = ch[c];
+                    next = q.code[c];
                     have = true;
                 } else {
-                    stk.put(k.sp, make_int2(ch[c], 0));
+                    stk.put(k.sp, make_int2(q.code[c], 0));
                     ++k.sp;
                 }
             }
@@ -476,24 +644,23 @@ __device__ __forceinline__ int quad_any_step(const rtk::DevScene& s, const Ray& 
             return 0;
         }
     } else {
-        const float4* L = reinterpret_cast<const float4*>(&s.qleaves[k.cur & ~dl::kLeafBit]);
-        const float4 lo = L[0], hi = L[1];
+        const float4* L = s.lrec + (k.cur & ~dl::kLeafBit);
+        const float4 h0 = L[0], h1 = L[1], c0 = L[2], c1 = L[3], c2 = L[4];
         float bt;
-        if (box_hit_fast(r, lo, hi, &bt)) {          // the reference leaf's exact box (NaN-free ray)
-            int a, cnt;
-            leaf_range(s, __float_as_int(lo.w), &a, &cnt);
-            if (for_prims(s, a, cnt, [&](int, const float4& p0, const float4& p1, const float4& p2) {
-                    float t;
-                    bool h;
-                    if (__float_as_int(p0.w) >= 0) {
-                        if (COUNT) w.tris++;
-                        h = tri_hit(r, p0, p1, p2, &t);
-                    } else {
-                        if (COUNT) w.spheres++;
-                        h = sphere_hit(r, p0, p1, &t);
-                    }
-                    return h && t < tlim;
-                }))
+        if (box_hit_fast(r, h0, h1, &bt)) {          // the reference leaf's exact box (NaN-free ray)
+            if (for_leaf_prims(L, __float_as_int(h1.w), __float_as_int(h0.w), c0, c1, c2,
+                               [&](int, const float4& p0, const float4& p1, const float4& p2) {
+                                   float t;
+                                   bool h;
+                                   if (__float_as_int(p0.w) >= 0) {
+                                       if (COUNT) w.tris++;
+                                       h = tri_hit(r, p0, p1, p2, &t);
+                                   } else {
+                                       if (COUNT) w.spheres++;
+                                       h = sphere_hit(r, p0, p1, &t);
+                                   }
+                                   return h && t < tlim;
+                               }))
                 return 2;
         }
     }

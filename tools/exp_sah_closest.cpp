@@ -1,0 +1,428 @@
+// Experiment (CPU, diagnostics only): closest-hit over the SAH occlusion
+// hierarchy (spairs: SAH boxes above the reference's leaves) with t-pruning,
+// versus the reference's ordered DFS over its own tree (pairs).
+//
+// For every closest-hit walk of a frame (eye rays + mirror chains) it reports
+// box tests of both walks, the per-pixel chain totals (the frame's critical
+// path is its heaviest chain), how often the SAH result cannot be certified
+// (leaf-entry check, ties across leaves, negative t) and whether any certified
+// SAH result differs from the reference walk's result.
+//
+//   g++ -O2 -std=c++17 -ffp-contract=off -Iinclude -Iraytracer-ceng477-graphics-hw-1_amd/csrc \
+//       tools/exp_sah_closest.cpp raytracer-ceng477-graphics-hw-1_amd/csrc/host_scene.cpp -o /tmp/exp_sah
+//   /tmp/exp_sah scene.xml [slack_rel]
+#include <algorithm>
+#include <cfloat>
+#include <cmath>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <vector>
+
+#include "host_scene.hpp"
+
+using namespace rtx;
+
+namespace {
+
+struct Vf { float x, y, z; };
+Vf add(Vf a, Vf b) { return {a.x + b.x, a.y + b.y, a.z + b.z}; }
+Vf sub(Vf a, Vf b) { return {a.x - b.x, a.y - b.y, a.z - b.z}; }
+Vf mul(Vf a, float f) { return {a.x * f, a.y * f, a.z * f}; }
+Vf neg(Vf a) { return {-a.x, -a.y, -a.z}; }
+float dot(Vf a, Vf b) { return a.x * b.x + a.y * b.y + a.z * b.z; }
+float len(Vf a) { return sqrtf(a.x * a.x + a.y * a.y + a.z * a.z); }
+Vf nrm(Vf a) { float l = len(a); return {a.x / l, a.y / l, a.z / l}; }
+float comp(Vf a, int i) { return i == 0 ? a.x : (i == 1 ? a.y : a.z); }
+float smin(float a, float b) { return (b < a) ? b : a; }
+float smax(float a, float b) { return (a < b) ? b : a; }
+
+struct Ray { Vf o, d, inv; };
+Ray make_ray(Vf o, Vf d) { return {o, d, {1.0f / d.x, 1.0f / d.y, 1.0f / d.z}}; }
+
+bool box_hit(const Ray& r, const float* lo, const float* hi, float* t) {
+    float tx1 = (lo[0] - r.o.x) * r.inv.x, tx2 = (hi[0] - r.o.x) * r.inv.x;
+    float tmin = smin(tx1, tx2), tmax = smax(tx1, tx2);
+    float ty1 = (lo[1] - r.o.y) * r.inv.y, ty2 = (hi[1] - r.o.y) * r.inv.y;
+    tmin = smax(tmin, smin(ty1, ty2)); tmax = smin(tmax, smax(ty1, ty2));
+    float tz1 = (lo[2] - r.o.z) * r.inv.z, tz2 = (hi[2] - r.o.z) * r.inv.z;
+    tmin = smax(tmin, smin(tz1, tz2)); tmax = smin(tmax, smax(tz1, tz2));
+    *t = tmin;
+    return tmax >= smax(0.0f, tmin);
+}
+float det3(float m00, float m01, float m02, float m10, float m11, float m12, float m20, float m21, float m22) {
+    return m00 * (m11 * m22 - m12 * m21) - m01 * (m10 * m22 - m12 * m20) + m02 * (m10 * m21 - m11 * m20);
+}
+bool tri_hit(const Ray& r, const dl::Prim& p, float* tout) {
+    Vf d = r.d;
+    float aox = p.p0x - r.o.x, aoy = p.p0y - r.o.y, aoz = p.p0z - r.o.z;
+    float detA = det3(p.p1x, p.p2x, d.x, p.p1y, p.p2y, d.y, p.p1z, p.p2z, d.z);
+    float beta = det3(aox, p.p2x, d.x, aoy, p.p2y, d.y, aoz, p.p2z, d.z) / detA;
+    float gamma = det3(p.p1x, aox, d.x, p.p1y, aoy, d.y, p.p1z, aoz, d.z) / detA;
+    float t = det3(p.p1x, p.p2x, aox, p.p1y, p.p2y, aoy, p.p1z, p.p2z, aoz) / detA;
+    float alpha = 1.0f - beta - gamma;
+    *tout = t;
+    return alpha >= 0 && beta >= 0 && gamma >= 0 && t >= 0.0f;
+}
+bool sphere_hit(const Ray& r, const dl::Prim& p, float* tout) {
+    Vf oc{r.o.x - p.p0x, r.o.y - p.p0y, r.o.z - p.p0z};
+    float B = 2.0f * dot(r.d, oc), A = dot(r.d, r.d), C = dot(oc, oc) - p.p1y;
+    float disc = B * B - 4.0f * A * C;
+    if (!(disc >= 0)) return false;
+    double sq = sqrt((double)disc), den = (double)(2.0f * A);
+    float t1 = (float)(((double)(-B) - sq) / den), t2 = (float)(((double)(-B) + sq) / den);
+    *tout = t1;
+    return !(t1 < 0 && t2 < 0);
+}
+bool prim_hit(const Ray& r, const dl::Prim& p, float* t) { return p.id >= 0 ? tri_hit(r, p, t) : sphere_hit(r, p, t); }
+
+const FlatBVH* B;
+std::vector<int> leaf_of_prim;            // prim slot -> index into leaf_boxes
+std::vector<std::array<float, 6>> leaf_boxes;
+
+void leaf_range(int32_t info, int* a, int* c) {
+    int cnt = (info >> dl::kLeafCountShift) & dl::kLeafMaxCount;
+    int st = info & dl::kLeafStartMask;
+    if (cnt) { *a = st; *c = cnt; } else { *a = B->leaf_big[st].start; *c = B->leaf_big[st].count; }
+}
+
+struct Hit { float t; int prim; long visits; };
+double g_slack = 0.0;
+long g_late = 0;
+double g_anom_max = 0; long g_anom_n[4];
+long g_rfetch = 0, g_rleaf = 0;
+
+// reference ordered DFS over the child-pair tree (raytracer.cpp:177-225)
+Hit closest_ref(const Ray& r) {
+    Hit h{-1.0f, -1, 0};
+    float tmax = FLT_MAX, bt;
+    h.visits++;
+    if (!(box_hit(r, B->root_lo, B->root_hi, &bt) && bt <= tmax)) return h;
+    struct E { int32_t info; float t; } st[64];
+    int sp = 0;
+    int32_t cur = B->root_info;
+    while (true) {
+        if (cur >= 0) {
+            const dl::Pair& P = B->pairs[cur];
+            g_rfetch++;
+            float lo0[3] = {P.l_minx, P.l_miny, P.l_minz}, hi0[3] = {P.l_maxx, P.l_maxy, P.l_maxz};
+            float lo1[3] = {P.r_minx, P.r_miny, P.r_minz}, hi1[3] = {P.r_maxx, P.r_maxy, P.r_maxz};
+            float tl, tr;
+            bool hl = box_hit(r, lo0, hi0, &tl), hr = box_hit(r, lo1, hi1, &tr);
+            h.visits += 2;
+            bool lf = comp(r.d, P.axis) > 0;
+            bool hn = lf ? hl : hr, hf = lf ? hr : hl;
+            float tn = lf ? tl : tr, tf = lf ? tr : tl;
+            int32_t in_ = lf ? P.l_info : P.r_info, if_ = lf ? P.r_info : P.l_info;
+            if (hf) st[sp++] = {if_, tf};
+            if (hn && tn <= tmax) { cur = in_; continue; }
+        } else {
+            int a, c;
+            leaf_range(cur, &a, &c);
+            g_rleaf++;
+            for (int i = a; i < a + c; ++i) {
+                float t;
+                if (prim_hit(r, B->prims[i], &t)) {
+                    const auto& lb = leaf_boxes[leaf_of_prim[i]];
+                    float lt;
+                    if (box_hit(r, lb.data(), lb.data() + 3, &lt) && lt > t && t > 0) {
+                        double rel = ((double)lt - t) / t;
+                        g_anom_max = std::max(g_anom_max, rel);
+                        for (int k = 0; k < 4; ++k) if (rel > pow(10.0, -7 + k)) g_anom_n[k]++;
+                    }
+                }
+                if (prim_hit(r, B->prims[i], &t) && (t < h.t || h.t == -1.0f)) { h.t = t; h.prim = i; tmax = t; }
+            }
+        }
+        bool found = false;
+        while (sp > 0) { --sp; if (st[sp].t <= tmax) { cur = st[sp].info; found = true; break; } }
+        if (!found) break;
+    }
+    return h;
+}
+
+// closest hit over the SAH hierarchy above the same leaves.  Front-to-back
+// by child entry t; a subtree is skipped once its entry t exceeds
+// tbest * (1 + slack).  Returns status: 0 certified, 1 fallback needed.
+int closest_sah(const Ray& r, Hit* out) {
+    Hit h{-1.0f, -1, 0};
+    int status = 0;
+    bool tie = false;
+    int tie_leaf = -1, best_leaf = -1;
+    float bt;
+    auto lim = [&](float tb) { return tb < 0 ? FLT_MAX : (float)(tb * (1.0 + g_slack)); };
+    h.visits++;
+    if (!box_hit(r, B->sroot_lo, B->sroot_hi, &bt)) { *out = h; return 0; }
+    struct E { int32_t info; float t; } st[64];
+    int sp = 0;
+    int32_t cur = B->sroot_info;
+    float tb = FLT_MAX;   // best t, FLT_MAX before any hit
+    float t2 = FLT_MAX;   // smallest t among the other hits
+    int leafno = 0;
+    while (true) {
+        if (cur >= 0) {
+            const dl::Pair& P = B->spairs[cur];
+            float lo0[3] = {P.l_minx, P.l_miny, P.l_minz}, hi0[3] = {P.l_maxx, P.l_maxy, P.l_maxz};
+            float lo1[3] = {P.r_minx, P.r_miny, P.r_minz}, hi1[3] = {P.r_maxx, P.r_maxy, P.r_maxz};
+            float tl, tr;
+            bool hl = box_hit(r, lo0, hi0, &tl), hr = box_hit(r, lo1, hi1, &tr);
+            h.visits += 2;
+            hl = hl && tl <= lim(tb);
+            hr = hr && tr <= lim(tb);
+            bool lf = hl && (!hr || tl <= tr);
+            bool hn = lf ? hl : hr, hf = lf ? hr : hl;
+            float tf = lf ? tr : tl;
+            int32_t in_ = lf ? P.l_info : P.r_info, if_ = lf ? P.r_info : P.l_info;
+            if (hn && hf) st[sp++] = {if_, tf};
+            if (hn) { cur = in_; continue; }
+            if (hf) { cur = if_; continue; }
+        } else {
+            ++leafno;
+            int a, c;
+            leaf_range(cur, &a, &c);
+            for (int i = a; i < a + c; ++i) {
+                float t;
+                if (!prim_hit(r, B->prims[i], &t)) continue;
+                if (t < 0 || t == -1.0f || std::isnan(t)) status = 1;
+                if (h.prim < 0 || t < h.t) {
+                    if (h.prim >= 0) t2 = std::min(t2, h.t);
+                    h.t = t; h.prim = i; tb = t; tie = false; best_leaf = leafno;
+                } else {
+                    t2 = std::min(t2, t);
+                    if (t == h.t && leafno != best_leaf) { tie = true; tie_leaf = leafno; }
+                }
+            }
+        }
+        bool found = false;
+        while (sp > 0) { --sp; if (st[sp].t <= lim(tb)) { cur = st[sp].info; found = true; break; } }
+        if (!found) break;
+    }
+    (void)tie_leaf;
+    if (tie) status = 1;
+    if (h.prim >= 0 && status == 0) {   // the reference reaches the winner: its leaf entry <= t
+        const auto& lb = leaf_boxes[leaf_of_prim[h.prim]];
+        float lt;
+        if (!box_hit(r, lb.data(), lb.data() + 3, &lt)) status = 1;
+        else if (lt > h.t) {            // winner hit before its leaf's entry t (rounding)
+            g_late++;
+            if (t2 < lt) status = 1;     // another hit could lower tMax below the entry first
+        }
+    }
+    *out = h;
+    return status;
+}
+
+
+// 4-wide quantized tree (bvh.quads / qleaves): certified closest hit, counting
+// dependent fetch rounds: quads, leaves (exact box + prims in one round).
+long g_qfetch = 0, g_lfetch = 0;
+float pow2f(int e) { uint32_t b = (uint32_t)e << 23; float f; memcpy(&f, &b, 4); return f; }
+void decode_quad(const dl::Quad& q, int c, float* lo, float* hi) {
+    float sc[3] = {pow2f(q.exps & 255u), pow2f((q.exps >> 8) & 255u), pow2f((q.exps >> 16) & 255u)};
+    const uint8_t* b = reinterpret_cast<const uint8_t*>(q.q);
+    const float o[3] = {q.ox, q.oy, q.oz};
+    for (int a = 0; a < 3; ++a) { lo[a] = o[a] + (float)b[c * 3 + a] * sc[a]; hi[a] = o[a] + (float)b[12 + c * 3 + a] * sc[a]; }
+}
+int closest_quad(const Ray& r, Hit* out) {
+    Hit h{-1.0f, -1, 0};
+    auto lim = [&](float tb) { return tb < 0 ? FLT_MAX : (float)(tb * (1.0 + g_slack)); };
+    struct E { int32_t code; float t; } st[128];
+    int sp = 0;
+    float tb = FLT_MAX, t2 = INFINITY, blt = INFINITY;
+    bool bad = false;
+    int32_t cur = B->qroot;
+    float cur_t = 0;
+    while (true) {
+        if (cur >= 0) {
+            g_qfetch++;
+            const dl::Quad& q = B->quads[cur];
+            int n = q.exps >> 24;
+            E hits[4]; int nh = 0;
+            for (int c = 0; c < n; ++c) {
+                float lo[3], hi[3], t;
+                decode_quad(q, c, lo, hi);
+                h.visits++;
+                if (box_hit(r, lo, hi, &t) && t <= lim(tb)) {
+                    int j = nh++;
+                    while (j > 0 && hits[j - 1].t > t) { hits[j] = hits[j - 1]; --j; }
+                    hits[j] = {q.child[c], t};
+                }
+            }
+            for (int j = nh - 1; j >= 1; --j) st[sp++] = hits[j];
+            if (nh) { cur = hits[0].code; cur_t = hits[0].t; continue; }
+        } else {
+            g_lfetch++;
+            const dl::QLeaf& L = B->qleaves[cur & ~dl::kLeafBit];
+            float lo[3] = {L.minx, L.miny, L.minz}, hi[3] = {L.maxx, L.maxy, L.maxz}, lt;
+            h.visits++;
+            if (box_hit(r, lo, hi, &lt) && lt <= lim(tb)) {
+                int a, c;
+                leaf_range(L.info, &a, &c);
+                for (int i = a; i < a + c; ++i) {
+                    float t;
+                    if (!prim_hit(r, B->prims[i], &t)) continue;
+                    if (!(t >= 0)) bad = true;
+                    if (h.prim < 0 || t < h.t) {
+                        if (h.prim >= 0) t2 = std::min(t2, h.t);
+                        h.t = t; h.prim = i; tb = t; blt = lt;
+                    } else t2 = std::min(t2, t);
+                }
+            }
+            (void)cur_t;
+        }
+        bool found = false;
+        while (sp > 0) { --sp; if (st[sp].t <= lim(tb)) { cur = st[sp].code; cur_t = st[sp].t; found = true; break; } }
+        if (!found) break;
+    }
+    int status = 0;
+    if (h.prim >= 0) {
+        float tw = h.t;
+        bool ok = !bad && t2 > tw && (blt <= tw || (blt <= tw * (1 + g_slack / 2) && t2 >= blt));
+        status = ok ? 0 : 1;
+    }
+    *out = h;
+    return status;
+}
+bool any_quad(const Ray& r, float tlim, long* qf, long* lf) {
+    int32_t st[128]; int sp = 0; int32_t cur = B->qroot;
+    while (true) {
+        if (cur >= 0) {
+            (*qf)++;
+            const dl::Quad& q = B->quads[cur];
+            int n = q.exps >> 24;
+            bool have = false; int32_t next = 0;
+            for (int c = 0; c < n; ++c) {
+                float lo[3], hi[3], t;
+                decode_quad(q, c, lo, hi);
+                if (box_hit(r, lo, hi, &t)) { if (!have) { next = q.child[c]; have = true; } else st[sp++] = q.child[c]; }
+            }
+            if (have) { cur = next; continue; }
+        } else {
+            (*lf)++;
+            const dl::QLeaf& L = B->qleaves[cur & ~dl::kLeafBit];
+            float lo[3] = {L.minx, L.miny, L.minz}, hi[3] = {L.maxx, L.maxy, L.maxz}, lt;
+            if (box_hit(r, lo, hi, &lt)) {
+                int a, c; leaf_range(L.info, &a, &c);
+                for (int i = a; i < a + c; ++i) { float t; if (prim_hit(r, B->prims[i], &t) && t < tlim) return true; }
+            }
+        }
+        if (sp == 0) return false;
+        cur = st[--sp];
+    }
+}
+
+}  // namespace
+
+int main(int argc, char** argv) {
+    if (argc < 2) { fprintf(stderr, "usage: %s scene.xml [slack]\n", argv[0]); return 2; }
+    if (argc > 2) g_slack = atof(argv[2]);
+    HostScene sc;
+    std::string err = load_xml(argv[1], sc);
+    if (!err.empty()) { fprintf(stderr, "%s\n", err.c_str()); return 1; }
+    prepare_triangles(sc);
+    FlatBVH bvh;
+    err = build_bvh(sc, bvh);
+    if (!err.empty()) { fprintf(stderr, "%s\n", err.c_str()); return 1; }
+    B = &bvh;
+    leaf_of_prim.assign(bvh.prims.size(), -1);
+    auto reg = [&](int32_t info, const float* lo, const float* hi) {
+        int a, c;
+        leaf_range(info, &a, &c);
+        leaf_boxes.push_back({lo[0], lo[1], lo[2], hi[0], hi[1], hi[2]});
+        for (int i = a; i < a + c; ++i) leaf_of_prim[i] = (int)leaf_boxes.size() - 1;
+    };
+    for (const auto& P : bvh.pairs) {
+        float lo0[3] = {P.l_minx, P.l_miny, P.l_minz}, hi0[3] = {P.l_maxx, P.l_maxy, P.l_maxz};
+        float lo1[3] = {P.r_minx, P.r_miny, P.r_minz}, hi1[3] = {P.r_maxx, P.r_maxy, P.r_maxz};
+        if (P.l_info < 0) reg(P.l_info, lo0, hi0);
+        if (P.r_info < 0) reg(P.r_info, lo1, hi1);
+    }
+    const CameraRec& c = sc.cameras[0];
+    const int nx = c.width, ny = c.height;
+    Vf e{c.position.x, c.position.y, c.position.z}, w{-c.gaze.x, -c.gaze.y, -c.gaze.z};
+    Vf v{c.up.x, c.up.y, c.up.z};
+    Vf u{v.y * w.z - v.z * w.y, v.z * w.x - v.x * w.z, v.x * w.y - v.y * w.x};
+    Vf m = add(e, mul(neg(w), c.near_distance));
+    Vf q = add(add(m, mul(u, c.near_plane[0])), mul(v, c.near_plane[3]));
+    float su_m = (c.near_plane[1] - c.near_plane[0]) / (float)nx, sv_m = (c.near_plane[3] - c.near_plane[2]) / (float)ny;
+
+    long ref_total = 0, sah_total = 0, walks = 0, fallback = 0, mismatch = 0, cert_mismatch = 0;
+    long qfall = 0, qmis = 0, sq_f = 0, sl_f = 0, nshadow = 0;
+    long max_chain_ref = 0, max_chain_sah = 0, max_chain_mixed = 0;
+    std::vector<long> chain_ref, chain_mixed;
+    chain_ref.reserve((size_t)nx * ny);
+    for (int row = 0; row < ny; ++row)
+        for (int col = 0; col < nx; ++col) {
+            float su = ((float)col + 0.5f) * su_m, sv = ((float)row + 0.5f) * sv_m;
+            Vf sp = sub(add(q, mul(u, su)), mul(v, sv));
+            Ray r = make_ray(e, sub(sp, e));
+            long cr = 0, cs = 0, cm = 0;
+            for (int k = 0; k <= sc.max_depth; ++k) {
+                Hit hr = closest_ref(r), hs, hq;
+                int stt = closest_sah(r, &hs);
+                int qst = closest_quad(r, &hq);
+                if (qst) qfall++;
+                if (!qst && (hq.prim != hr.prim || (hr.prim >= 0 && hq.t != hr.t))) qmis++;
+                walks++;
+                ref_total += hr.visits;
+                sah_total += hs.visits;
+                cr += hr.visits;
+                cs += hs.visits;
+                cm += stt ? hs.visits + hr.visits : hs.visits;
+                if (stt) fallback++;
+                if (hr.prim != hs.prim || (hr.prim >= 0 && hr.t != hs.t)) {
+                    mismatch++;
+                    if (!stt) cert_mismatch++;
+                }
+                if (hr.prim < 0) break;
+                const dl::Prim& P = bvh.prims[hr.prim];
+                int mat;
+                Vf n;
+                Vf hp = add(r.o, mul(r.d, hr.t));
+                if (P.id >= 0) {
+                    const dl::TriShade& ts = bvh.tri_shade[P.id];
+                    n = {ts.nx, ts.ny, ts.nz};
+                    mat = ts.material;
+                } else {
+                    Vf cc{P.p0x, P.p0y, P.p0z};
+                    Vf dd = sub(hp, cc);
+                    n = nrm(Vf{dd.x / P.p1x, dd.y / P.p1x, dd.z / P.p1x});
+                    mat = P.p2w;
+                }
+                Vf pnt = add(hp, mul(n, sc.eps));
+                for (const auto& L : sc.lights) {
+                    Vf lp{L.position.x, L.position.y, L.position.z};
+                    float tl = len(sub(lp, pnt));
+                    Ray sr = make_ray(pnt, nrm(sub(lp, pnt)));
+                    any_quad(sr, tl, &sq_f, &sl_f);
+                    nshadow++;
+                }
+                if (!sc.materials[mat - 1].is_mirror) break;
+                Vf d2 = nrm(r.d), n2 = nrm(n);
+                float rc = dot(neg(d2), n2);
+                r = make_ray(pnt, add(d2, mul(mul(n2, 2.0f), rc)));
+            }
+            chain_ref.push_back(cr);
+            chain_mixed.push_back(cm);
+            max_chain_ref = std::max(max_chain_ref, cr);
+            max_chain_sah = std::max(max_chain_sah, cs);
+            max_chain_mixed = std::max(max_chain_mixed, cm);
+        }
+    std::sort(chain_ref.begin(), chain_ref.end());
+    std::sort(chain_mixed.begin(), chain_mixed.end());
+    auto pct = [](const std::vector<long>& v, double p) { return v[(size_t)((v.size() - 1) * p)]; };
+    printf("slack %g walks %ld: box tests ref %.2f/walk sah %.2f/walk (ratio %.2f)\n", g_slack, walks,
+           (double)ref_total / walks, (double)sah_total / walks, (double)ref_total / sah_total);
+    printf("fallback %ld (%.4f%%) mismatch %ld certified-mismatch %ld\n", fallback, 100.0 * fallback / walks, mismatch,
+           cert_mismatch);
+    printf("quad closest: fallback %ld mismatch %ld; per walk: ref pair fetches %.2f leaves %.2f | quad fetches %.2f leaves %.2f\n",
+           qfall, qmis, (double)g_rfetch / walks, (double)g_rleaf / walks, (double)g_qfetch / walks, (double)g_lfetch / walks);
+    printf("shadow rays %ld: quad fetches %.2f leaves %.2f per ray\n", nshadow, (double)sq_f / nshadow, (double)sl_f / nshadow);
+    printf("late winners %ld; anomaly max rel %.3g, >1e-7 %ld >1e-6 %ld >1e-5 %ld >1e-4 %ld\n", g_late, g_anom_max,
+           g_anom_n[0], g_anom_n[1], g_anom_n[2], g_anom_n[3]);
+    printf("chain visits max: ref %ld sah %ld sah+fallback %ld\n", max_chain_ref, max_chain_sah, max_chain_mixed);
+    printf("chain p99 / p99.9 / p99.99: ref %ld %ld %ld  mixed %ld %ld %ld\n", pct(chain_ref, 0.99),
+           pct(chain_ref, 0.999), pct(chain_ref, 0.9999), pct(chain_mixed, 0.99), pct(chain_mixed, 0.999),
+           pct(chain_mixed, 0.9999));
+    return 0;
+}
