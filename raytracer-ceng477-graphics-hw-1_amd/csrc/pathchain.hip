@@ -34,7 +34,7 @@ namespace {
 
 constexpr int kBlock = 256;
 #ifndef RT_WAVES_PER_EU
-#define RT_WAVES_PER_EU 1
+#define RT_WAVES_PER_EU 5     // k_chain: 96 VGPRs, 5 waves/SIMD (a few spills beat 4 waves: C3 1.36 -> 1.32 ms)
 #endif
 #ifndef RT_WIDE_B
 #define RT_WIDE_B 0           // wide walks for phase-B tails (RT_WIDE > 0 at run time)
@@ -46,7 +46,7 @@ constexpr int kBlock = 256;
 #define RT_FINISH_WAVES 1
 #endif
 #ifndef RT_OCC_WAVES_PER_EU
-#define RT_OCC_WAVES_PER_EU 1     // k_mix / k_occlude (the any-hit bulk)
+#define RT_OCC_WAVES_PER_EU 5     // k_mix / k_occlude (the any-hit bulk); 5/5 measured best of 4..6
 #endif
 
 enum LaneState : int { kIdle = 0, kTrav = 1, kDone = 2 };

@@ -62,9 +62,10 @@ for mega in PATHS_RUN:
     s = pkg.Scene.from_xml(xml, device=0, render_path=mega)
     cam = s.camera(0)
     res[name] = {"full": timeit(s, cam)}
+    R0, C0 = (int(x) for x in os.environ.get("EXP_PIXEL", "510,1312").split(","))
     for sz in ((8,) if QUICK else (8, 16, 64, 256)):
-        res[name][f"crop{sz}"] = timeit(s, crop(cam, 505 - sz // 2, 1310 - sz // 2, sz, sz))
-    res[name]["crop_1px"] = timeit(s, crop(cam, 510, 1312, 1, 1))
+        res[name][f"crop{sz}"] = timeit(s, crop(cam, R0 - sz // 2, C0 - sz // 2, sz, sz))
+    res[name]["crop_1px"] = timeit(s, crop(cam, R0, C0, 1, 1))
     for dep in (() if QUICK else range(0, 7)):
         s.set_max_depth(dep)
         res[name][f"depth{dep}"] = timeit(s, cam)

@@ -252,12 +252,11 @@ int closest_quad(const Ray& r, Hit* out) {
             if (nh) { cur = hits[0].code; cur_t = hits[0].t; continue; }
         } else {
             g_lfetch++;
-            const dl::QLeaf& L = B->qleaves[cur & ~dl::kLeafBit];
+            const dl::LeafHead& L = *reinterpret_cast<const dl::LeafHead*>(&B->lrec[cur & ~dl::kLeafBit]);
             float lo[3] = {L.minx, L.miny, L.minz}, hi[3] = {L.maxx, L.maxy, L.maxz}, lt;
             h.visits++;
             if (box_hit(r, lo, hi, &lt) && lt <= lim(tb)) {
-                int a, c;
-                leaf_range(L.info, &a, &c);
+                int a = L.slot0, c = L.count;
                 for (int i = a; i < a + c; ++i) {
                     float t;
                     if (!prim_hit(r, B->prims[i], &t)) continue;
@@ -299,10 +298,10 @@ bool any_quad(const Ray& r, float tlim, long* qf, long* lf) {
             if (have) { cur = next; continue; }
         } else {
             (*lf)++;
-            const dl::QLeaf& L = B->qleaves[cur & ~dl::kLeafBit];
+            const dl::LeafHead& L = *reinterpret_cast<const dl::LeafHead*>(&B->lrec[cur & ~dl::kLeafBit]);
             float lo[3] = {L.minx, L.miny, L.minz}, hi[3] = {L.maxx, L.maxy, L.maxz}, lt;
             if (box_hit(r, lo, hi, &lt)) {
-                int a, c; leaf_range(L.info, &a, &c);
+                int a = L.slot0, c = L.count;
                 for (int i = a; i < a + c; ++i) { float t; if (prim_hit(r, B->prims[i], &t) && t < tlim) return true; }
             }
         }
@@ -347,6 +346,9 @@ int main(int argc, char** argv) {
     float su_m = (c.near_plane[1] - c.near_plane[0]) / (float)nx, sv_m = (c.near_plane[3] - c.near_plane[2]) / (float)ny;
 
     long ref_total = 0, sah_total = 0, walks = 0, fallback = 0, mismatch = 0, cert_mismatch = 0;
+    std::vector<long> chain_qb;
+    long best_qb = -1; int best_rc[2] = {0, 0};
+    long max_cqa = 0, max_walk_q = 0, walks_b = 0;
     long qfall = 0, qmis = 0, sq_f = 0, sl_f = 0, nshadow = 0;
     long max_chain_ref = 0, max_chain_sah = 0, max_chain_mixed = 0;
     std::vector<long> chain_ref, chain_mixed;
@@ -356,11 +358,16 @@ int main(int argc, char** argv) {
             float su = ((float)col + 0.5f) * su_m, sv = ((float)row + 0.5f) * sv_m;
             Vf sp = sub(add(q, mul(u, su)), mul(v, sv));
             Ray r = make_ray(e, sub(sp, e));
-            long cr = 0, cs = 0, cm = 0;
+            long cr = 0, cs = 0, cm = 0, cq_a = 0, cq_b = 0;
             for (int k = 0; k <= sc.max_depth; ++k) {
                 Hit hr = closest_ref(r), hs, hq;
                 int stt = closest_sah(r, &hs);
+                const long qf0 = g_qfetch + g_lfetch;
                 int qst = closest_quad(r, &hq);
+                const long qrounds = g_qfetch + g_lfetch - qf0;
+                if (k >= 2) cq_b += qrounds; else cq_a += qrounds;
+                if (k >= 2) { walks_b++; }
+                max_walk_q = std::max(max_walk_q, qrounds);
                 if (qst) qfall++;
                 if (!qst && (hq.prim != hr.prim || (hr.prim >= 0 && hq.t != hr.t))) qmis++;
                 walks++;
@@ -403,14 +410,17 @@ int main(int argc, char** argv) {
                 r = make_ray(pnt, add(d2, mul(mul(n2, 2.0f), rc)));
             }
             chain_ref.push_back(cr);
+            chain_qb.push_back(cq_b);
+            if (cq_b > best_qb) { best_qb = cq_b; best_rc[0] = row; best_rc[1] = col; }
+            max_cqa = std::max(max_cqa, cq_a);
             chain_mixed.push_back(cm);
             max_chain_ref = std::max(max_chain_ref, cr);
             max_chain_sah = std::max(max_chain_sah, cs);
             max_chain_mixed = std::max(max_chain_mixed, cm);
         }
+    auto pct = [](const std::vector<long>& v, double p) { return v[(size_t)((v.size() - 1) * p)]; };
     std::sort(chain_ref.begin(), chain_ref.end());
     std::sort(chain_mixed.begin(), chain_mixed.end());
-    auto pct = [](const std::vector<long>& v, double p) { return v[(size_t)((v.size() - 1) * p)]; };
     printf("slack %g walks %ld: box tests ref %.2f/walk sah %.2f/walk (ratio %.2f)\n", g_slack, walks,
            (double)ref_total / walks, (double)sah_total / walks, (double)ref_total / sah_total);
     printf("fallback %ld (%.4f%%) mismatch %ld certified-mismatch %ld\n", fallback, 100.0 * fallback / walks, mismatch,
@@ -418,6 +428,10 @@ int main(int argc, char** argv) {
     printf("quad closest: fallback %ld mismatch %ld; per walk: ref pair fetches %.2f leaves %.2f | quad fetches %.2f leaves %.2f\n",
            qfall, qmis, (double)g_rfetch / walks, (double)g_rleaf / walks, (double)g_qfetch / walks, (double)g_lfetch / walks);
     printf("shadow rays %ld: quad fetches %.2f leaves %.2f per ray\n", nshadow, (double)sq_f / nshadow, (double)sl_f / nshadow);
+    std::sort(chain_qb.begin(), chain_qb.end());
+    printf("quad fetch rounds: phase-A chain max %ld, phase-B chain max %ld p99.99 %ld p99.9 %ld, max single walk %ld, phase-B walks %ld\n",
+           max_cqa, chain_qb.back(), pct(chain_qb, 0.9999), pct(chain_qb, 0.999), max_walk_q, walks_b);
+    printf("heaviest phase-B chain at row %d col %d\n", best_rc[0], best_rc[1]);
     printf("late winners %ld; anomaly max rel %.3g, >1e-7 %ld >1e-6 %ld >1e-5 %ld >1e-4 %ld\n", g_late, g_anom_max,
            g_anom_n[0], g_anom_n[1], g_anom_n[2], g_anom_n[3]);
     printf("chain visits max: ref %ld sah %ld sah+fallback %ld\n", max_chain_ref, max_chain_sah, max_chain_mixed);
