@@ -33,7 +33,7 @@
 extern "C" {
 #endif
 
-#define RT_ABI_VERSION 1
+#define RT_ABI_VERSION 2
 
 typedef enum rt_status {
     RT_OK = 0,
@@ -95,6 +95,9 @@ typedef struct rt_scene_desc {
 typedef struct rt_options {
     int device;       /* HIP device ordinal; -1 = current device            */
     int flags;        /* RT_OPT_* bits                                       */
+    int build_threads;/* host threads for the BVH build (bvh.h:48-163); 0 =
+                         env RT_BUILD_THREADS or hardware concurrency (<= 16),
+                         1 = serial.  The tree never depends on it.  (ABI 2) */
 } rt_options;
 
 typedef struct rt_stats {
@@ -111,7 +114,12 @@ typedef struct rt_stats {
 typedef struct rt_bvh_info {
     int nodes, leaves, max_leaf_prims, max_depth, max_stack;
     int triangles, spheres;
-    double build_ms;
+    double build_ms;         /* whole host build                                  */
+    double ref_ms;           /* the reference tree (bvh.h:48-163) alone  (ABI 2) */
+    double wide_ms;          /* the 4-wide SAH tree over the same leaves (ABI 2) */
+    int build_threads;       /* threads the build used                   (ABI 2) */
+    int wide_nodes;          /* 4-wide nodes                             (ABI 2) */
+    uint64_t wide_hash;      /* FNV-1a of the 4-wide nodes + leaf records (ABI 2) */
 } rt_bvh_info;
 
 /* ---- errors / devices ---- */

@@ -52,7 +52,7 @@ class Camera(ctypes.Structure):
 
 
 class Options(ctypes.Structure):
-    _fields_ = [("device", ctypes.c_int), ("flags", ctypes.c_int)]
+    _fields_ = [("device", ctypes.c_int), ("flags", ctypes.c_int), ("build_threads", ctypes.c_int)]
 
 
 class Stats(ctypes.Structure):
@@ -68,7 +68,9 @@ class Stats(ctypes.Structure):
 class BvhInfo(ctypes.Structure):
     _fields_ = [("nodes", ctypes.c_int), ("leaves", ctypes.c_int), ("max_leaf_prims", ctypes.c_int),
                 ("max_depth", ctypes.c_int), ("max_stack", ctypes.c_int), ("triangles", ctypes.c_int),
-                ("spheres", ctypes.c_int), ("build_ms", ctypes.c_double)]
+                ("spheres", ctypes.c_int), ("build_ms", ctypes.c_double),
+                ("ref_ms", ctypes.c_double), ("wide_ms", ctypes.c_double), ("build_threads", ctypes.c_int),
+                ("wide_nodes", ctypes.c_int), ("wide_hash", ctypes.c_uint64)]
 
     def as_dict(self) -> dict:
         return {k: getattr(self, k) for k, _ in self._fields_}
@@ -145,14 +147,15 @@ class Scene:
 
     @classmethod
     def from_xml(cls, path: str | os.PathLike, device: int = -1, host_only: bool = False,
-                 render_path: str = "chain") -> "Scene":
+                 render_path: str = "chain", build_threads: int = 0) -> "Scene":
         """render_path: "chain", "fused", "wavefront", "megakernel" or "default" (the library's
-        default path); all are bit-identical."""
+        default path); all are bit-identical.  build_threads: host BVH build threads (0: default,
+        1: serial); the tree does not depend on it."""
         h = ctypes.c_void_p()
         flags = RT_OPT_HOST_ONLY if host_only else 0
         flags |= {"chain": RT_OPT_CHAIN, "wavefront": RT_OPT_WAVEFRONT, "megakernel": RT_OPT_MEGAKERNEL,
                   "fused": RT_OPT_FUSED, "default": 0}[render_path]
-        opts = Options(device, flags)
+        opts = Options(device, flags, build_threads)
         _check(lib().rt_scene_load_xml(str(path).encode(), ctypes.byref(opts), ctypes.byref(h)))
         return cls(h.value)
 

@@ -5,6 +5,8 @@
 #include <algorithm>
 #include <chrono>
 #include <functional>
+#include <future>
+#include <thread>
 #include <cmath>
 #include <cstdio>
 #include <cstdlib>
@@ -278,37 +280,84 @@ struct BNode {
     V3 lo, hi;
     int axis = 0, depth = 0;
     int left = -1, right = -1;
-    std::vector<int> tris, sph;
+    int t0 = 0, t1 = 0, s0 = 0, s1 = 0;   // leaf: its triangles pt[t0, t1), spheres ps[s0, s1)
 };
+
+// Fork-join depth for `threads` workers: subtrees above it are built as
+// concurrent tasks (each into its own node pool, spliced afterwards).  The
+// tree depends only on the split rule, never on thread timing.
+int fork_depth(int threads) {
+    int d = 0;
+    while ((1 << d) < threads && d < 6) ++d;
+    return threads <= 1 ? 0 : d + 1;
+}
+
+template <class N>
+int splice_pool(std::vector<N>& dst, std::vector<N>&& src, int root) {
+    if (root < 0) return -1;
+    const int off = (int)dst.size();
+    for (N& n : src) {
+        if (n.left >= 0) n.left += off;
+        if (n.right >= 0) n.right += off;
+        dst.push_back(std::move(n));
+    }
+    return root + off;
+}
+
+// Per-triangle box (the three vertices folded with the reference's `<` / `>`
+// updates, parser.h:272-317) and split key, computed once: a node's box is the
+// same fold over its triangles' boxes (min/max of the same values; NaN never
+// wins a comparison in either form), so every node box is bit-identical.
+struct TriBox { float lo[3], hi[3], c[3]; };
+
+// The reference recursion (bvh.h:48-79) over index ranges: a node's
+// triangles are pt[t0, t1) and spheres ps[s0, s1); a split is a stable
+// in-place partition (left keys first, order kept, as bvh.h:138-150 fills its
+// two vectors), so a leaf's range lists its primitives in the reference's
+// order.  Subtrees below a split touch disjoint ranges, so the top levels run
+// as concurrent tasks, each into its own node pool (spliced afterwards).
+constexpr int kForkMin = 2048;   // a split forks only when both sides have this many primitives
 
 class Builder {
   public:
-    explicit Builder(const HostScene& s) : s_(s) {}
+    Builder(const HostScene& s, const std::vector<TriBox>& tb, std::vector<int>& pt, std::vector<int>& ps, int fork)
+        : s_(s), tb_(tb), pt_(pt), ps_(ps), fork_(fork) {}
     std::vector<BNode> nodes;
 
-    int build(std::vector<int> tris, std::vector<int> sph, int depth) {       // bvh.h:48-79
-        if (tris.empty() && sph.empty()) return -1;
-        int id = (int)nodes.size();
+    int build(int t0, int t1, int s0, int s1, int depth) {
+        if (t0 == t1 && s0 == s1) return -1;
+        const int id = (int)nodes.size();
         nodes.emplace_back();
-        nodes[id].depth = depth;
-        bounds(tris, sph, nodes[id].lo, nodes[id].hi);
-        if (tris.size() + sph.size() <= 1 || depth >= kMaxDepth) {
-            nodes[id].tris = std::move(tris);
-            nodes[id].sph = std::move(sph);
+        BNode nd;
+        nd.depth = depth;
+        bounds(t0, t1, s0, s1, nd.lo, nd.hi);
+        int tm = 0, sm = 0;
+        bool leaf = (t1 - t0) + (s1 - s0) <= 1 || depth >= kMaxDepth;
+        if (!leaf) {
+            nd.axis = widest(nd.lo, nd.hi);
+            leaf = !split(nd.axis, nd.lo, nd.hi, t0, t1, s0, s1, &tm, &sm);
+        }
+        if (leaf) {
+            nd.t0 = t0; nd.t1 = t1; nd.s0 = s0; nd.s1 = s1;
+            nodes[id] = nd;
             return id;
         }
-        const int axis = widest(nodes[id].lo, nodes[id].hi);
-        nodes[id].axis = axis;
-        std::vector<int> lt, ls, rt, rs;
-        if (!split(axis, nodes[id].lo, nodes[id].hi, tris, sph, lt, ls, rt, rs)) {
-            nodes[id].tris = std::move(tris);
-            nodes[id].sph = std::move(sph);
-            return id;
+        nodes[id] = nd;
+        int r, l;
+        const int nl = (tm - t0) + (sm - s0), nr = (t1 - tm) + (s1 - sm);
+        if (depth < fork_ && std::min(nl, nr) >= kForkMin) {
+            Builder rb(s_, tb_, pt_, ps_, fork_), lb(s_, tb_, pt_, ps_, fork_);
+            rb.nodes.reserve(2 * (size_t)nr + 1);     // one allocation per pool (page faults are costly)
+            lb.nodes.reserve(2 * (size_t)nl + 1);
+            auto fr = std::async(std::launch::async, [&] { return rb.build(tm, t1, sm, s1, depth + 1); });
+            const int lr = lb.build(t0, tm, s0, sm, depth + 1);
+            const int rr = fr.get();
+            r = splice_pool(nodes, std::move(rb.nodes), rr);
+            l = splice_pool(nodes, std::move(lb.nodes), lr);
+        } else {
+            r = build(tm, t1, sm, s1, depth + 1);     // right first (bvh.h:69-70)
+            l = build(t0, tm, s0, sm, depth + 1);
         }
-        tris.clear(); tris.shrink_to_fit();
-        sph.clear(); sph.shrink_to_fit();
-        int r = build(std::move(rt), std::move(rs), depth + 1);     // right first (bvh.h:69-70)
-        int l = build(std::move(lt), std::move(ls), depth + 1);
         nodes[id].right = r;
         nodes[id].left = l;
         return id;
@@ -316,34 +365,33 @@ class Builder {
 
   private:
     const HostScene& s_;
+    const std::vector<TriBox>& tb_;
+    std::vector<int>& pt_;
+    std::vector<int>& ps_;
+    int fork_;
+    std::vector<int> scratch_;
 
     // Scene::getBoundingBox + extendBoundingBox (parser.h:272-317)
-    void bounds(const std::vector<int>& tris, const std::vector<int>& sph, V3& lo, V3& hi) const {
-        lo = V3{FLT_MAX, FLT_MAX, FLT_MAX};
-        hi = V3{-FLT_MAX, -FLT_MAX, -FLT_MAX};
-        for (int t : tris) {
-            const TriRec& tr = s_.tris[t];
-            for (int vid : {tr.v0, tr.v1, tr.v2}) {
-                const V3& v = s_.verts[vid - 1];
-                if (v.x < lo.x) lo.x = v.x;
-                if (v.y < lo.y) lo.y = v.y;
-                if (v.z < lo.z) lo.z = v.z;
-                if (v.x > hi.x) hi.x = v.x;
-                if (v.y > hi.y) hi.y = v.y;
-                if (v.z > hi.z) hi.z = v.z;
+    void bounds(int t0, int t1, int s0, int s1, V3& lo, V3& hi) const {
+        float l[3] = {FLT_MAX, FLT_MAX, FLT_MAX}, h[3] = {-FLT_MAX, -FLT_MAX, -FLT_MAX};
+        for (int i = t0; i < t1; ++i) {
+            const TriBox& b = tb_[pt_[i]];
+            for (int ax = 0; ax < 3; ++ax) {
+                if (b.lo[ax] < l[ax]) l[ax] = b.lo[ax];
+                if (b.hi[ax] > h[ax]) h[ax] = b.hi[ax];
             }
         }
-        float* plo = &lo.x;
-        float* phi = &hi.x;
-        for (int k : sph) {
-            const SphereRec& sp = s_.spheres[k];
+        for (int i = s0; i < s1; ++i) {
+            const SphereRec& sp = s_.spheres[ps_[i]];
             const V3& c = s_.verts[sp.center_id - 1];
             const float cc[3] = {c.x, c.y, c.z};
             for (int ax = 0; ax < 3; ++ax) {
-                if (cc[ax] - sp.radius < plo[ax]) plo[ax] = cc[ax] - sp.radius;
-                if (cc[ax] + sp.radius > phi[ax]) phi[ax] = cc[ax] + sp.radius;
+                if (cc[ax] - sp.radius < l[ax]) l[ax] = cc[ax] - sp.radius;
+                if (cc[ax] + sp.radius > h[ax]) h[ax] = cc[ax] + sp.radius;
             }
         }
+        lo = V3{l[0], l[1], l[2]};
+        hi = V3{h[0], h[1], h[2]};
     }
 
     static int widest(const V3& lo, const V3& hi) {                           // parser.h:227-235
@@ -353,29 +401,51 @@ class Builder {
         return w;
     }
 
-    float key_tri(int t, int axis) const { return vget(s_.tris[t].center, axis); }
+    float key_tri(int t, int axis) const { return tb_[t].c[axis]; }
     float key_sph(int k, int axis) const { return vget(s_.verts[s_.spheres[k].center_id - 1], axis); }
 
+    // Stable partition of v[b, e) by pred (true first); returns the split point.
+    template <class P>
+    int stable_split(std::vector<int>& v, int b, int e, P pred) {
+        scratch_.clear();
+        int w = b;
+        for (int i = b; i < e; ++i) {
+            if (pred(v[i])) v[w++] = v[i];
+            else scratch_.push_back(v[i]);
+        }
+        std::copy(scratch_.begin(), scratch_.end(), v.begin() + w);
+        return w;
+    }
+
     // BVHNode::partition (bvh.h:111-163): spatial midpoint of the widest axis,
-    // moved toward the populated side up to 19 times; stable order.
-    bool split(int axis, const V3& lo, const V3& hi, const std::vector<int>& tris, const std::vector<int>& sph,
-               std::vector<int>& lt, std::vector<int>& ls, std::vector<int>& rt, std::vector<int>& rs) const {
+    // moved toward the populated side up to 19 times.  One pass finds the
+    // smallest and largest non-NaN key and whether a NaN key exists: "no key
+    // < mid" is !(kmin < mid), "every key < mid" is !nan && kmax < mid, so a
+    // retry costs O(1) instead of a pass.
+    bool split(int axis, const V3& lo, const V3& hi, int t0, int t1, int s0, int s1, int* tm, int* sm) {
+        float kmin = INFINITY, kmax = -INFINITY;
+        bool nan = false;
+        auto see = [&](float k) {
+            if (k != k) { nan = true; return; }
+            if (k < kmin) kmin = k;
+            if (k > kmax) kmax = k;
+        };
+        for (int i = t0; i < t1; ++i) see(key_tri(pt_[i], axis));
+        for (int i = s0; i < s1; ++i) see(key_sph(ps_[i], axis));
         float start = vget(lo, axis), end = vget(hi, axis);
         float mid = (start + end) / 2;
         for (int attempt = 0; attempt < kMaxTries; ++attempt) {
-            size_t left = 0;
-            for (int t : tris) left += key_tri(t, axis) < mid;
-            for (int k : sph) left += key_sph(k, axis) < mid;
-            const size_t right = tris.size() + sph.size() - left;
-            if (left == 0) {
+            const bool left_empty = !(kmin < mid);
+            const bool right_empty = !nan && kmax < mid;
+            if (left_empty) {
                 start = mid;
                 mid = (start + end) / 2;
-            } else if (right == 0) {
+            } else if (right_empty) {
                 end = mid;
                 mid = (start + end) / 2;
             } else {
-                for (int t : tris) (key_tri(t, axis) < mid ? lt : rt).push_back(t);
-                for (int k : sph) (key_sph(k, axis) < mid ? ls : rs).push_back(k);
+                *tm = stable_split(pt_, t0, t1, [&](int t) { return key_tri(t, axis) < mid; });
+                *sm = stable_split(ps_, s0, s1, [&](int k) { return key_sph(k, axis) < mid; });
                 return true;
             }
         }
@@ -388,17 +458,42 @@ inline float ibits(int32_t i) { float f; std::memcpy(&f, &i, 4); return f; }
 
 }  // namespace
 
-void build_shadow_tree(FlatBVH& out);
+void build_shadow_tree(FlatBVH& out, int threads);
 
-std::string build_bvh(const HostScene& s, FlatBVH& out) {
+int build_threads(int requested) {
+    if (requested > 0) return std::min(requested, 64);
+    if (const char* e = std::getenv("RT_BUILD_THREADS")) {
+        const int v = std::atoi(e);
+        if (v > 0) return std::min(v, 64);
+    }
+    const unsigned hc = std::thread::hardware_concurrency();
+    return (int)std::max(1u, std::min(hc, 16u));
+}
+
+std::string build_bvh(const HostScene& s, FlatBVH& out, int threads) {
     auto t0 = std::chrono::steady_clock::now();
     out = FlatBVH();
-    Builder b(s);
-    std::vector<int> tris(s.tris.size()), sph(s.spheres.size());
-    for (size_t i = 0; i < tris.size(); ++i) tris[i] = (int)i;
-    for (size_t i = 0; i < sph.size(); ++i) sph[i] = (int)i;
-    b.nodes.reserve(2 * (tris.size() + sph.size()) + 1);
-    const int root = b.build(std::move(tris), std::move(sph), 0);
+    out.threads = build_threads(threads);
+    std::vector<TriBox> tb(s.tris.size());
+    for (size_t i = 0; i < tb.size(); ++i) {
+        const TriRec& tr = s.tris[i];
+        TriBox& b = tb[i];
+        for (int ax = 0; ax < 3; ++ax) { b.lo[ax] = FLT_MAX; b.hi[ax] = -FLT_MAX; b.c[ax] = vget(tr.center, ax); }
+        for (int vid : {tr.v0, tr.v1, tr.v2}) {
+            const V3& v = s.verts[vid - 1];
+            for (int ax = 0; ax < 3; ++ax) {
+                if (vget(v, ax) < b.lo[ax]) b.lo[ax] = vget(v, ax);
+                if (vget(v, ax) > b.hi[ax]) b.hi[ax] = vget(v, ax);
+            }
+        }
+    }
+    std::vector<int> pt(s.tris.size()), ps(s.spheres.size());
+    for (size_t i = 0; i < pt.size(); ++i) pt[i] = (int)i;
+    for (size_t i = 0; i < ps.size(); ++i) ps[i] = (int)i;
+    Builder b(s, tb, pt, ps, fork_depth(out.threads));
+    b.nodes.reserve(2 * (pt.size() + ps.size()) + 1);
+    const int root = b.build(0, (int)pt.size(), 0, (int)ps.size(), 0);
+    out.ref_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
 
     out.tri_shade.resize(s.tris.size());
     for (size_t i = 0; i < s.tris.size(); ++i) {
@@ -435,13 +530,15 @@ std::string build_bvh(const HostScene& s, FlatBVH& out) {
             o.b = n.axis;
             continue;
         }
-        if ((int)n.tris.size() > dl::kNtriMask || (int)n.sph.size() > dl::kMaxLeafSpheres)
+        const int ntri = n.t1 - n.t0, nsph = n.s1 - n.s0;
+        if (ntri > dl::kNtriMask || nsph > dl::kMaxLeafSpheres)
             return "Error: BVH leaf exceeds the device encoding limits";
         out.leaves++;
-        out.max_leaf = std::max(out.max_leaf, (int)(n.tris.size() + n.sph.size()));
+        out.max_leaf = std::max(out.max_leaf, ntri + nsph);
         o.a = (int32_t)out.prims.size();
-        o.b = dl::kLeafBit | ((int32_t)n.sph.size() << dl::kNtriBits) | (int32_t)n.tris.size();
-        for (int t : n.tris) {
+        o.b = dl::kLeafBit | ((int32_t)nsph << dl::kNtriBits) | (int32_t)ntri;
+        for (int j = n.t0; j < n.t1; ++j) {
+            const int t = pt[j];
             const TriRec& tr = s.tris[t];
             const V3 a = s.verts[tr.v0 - 1], bb = s.verts[tr.v1 - 1], c = s.verts[tr.v2 - 1];
             dl::Prim p{};
@@ -450,7 +547,8 @@ std::string build_bvh(const HostScene& s, FlatBVH& out) {
             p.p2x = a.x - c.x; p.p2y = a.y - c.y; p.p2z = a.z - c.z; p.p2w = 0;
             out.prims.push_back(p);
         }
-        for (int k : n.sph) {
+        for (int j = n.s0; j < n.s1; ++j) {
+            const int k = ps[j];
             const SphereRec& sp = s.spheres[k];
             const V3 c = s.verts[sp.center_id - 1];
             dl::Prim p{};
@@ -516,7 +614,10 @@ std::string build_bvh(const HostScene& s, FlatBVH& out) {
     // Ordered DFS pushes two children per interior pop: stack <= depth + 2.
     out.max_stack = out.max_depth + 2;
     if (out.max_stack > dl::kMaxStack) return "Error: BVH deeper than the device stack";
-    build_shadow_tree(out);
+    const auto t1 = std::chrono::steady_clock::now();
+    out.flat_ms = std::chrono::duration<double, std::milli>(t1 - t0).count() - out.ref_ms;
+    build_shadow_tree(out, out.threads);
+    out.stree_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t1).count();
     if (out.smax_depth + 2 > dl::kMaxStack) return "Error: occlusion tree deeper than the device stack";
     out.build_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
     return "";
@@ -533,7 +634,7 @@ std::string build_bvh(const HostScene& s, FlatBVH& out) {
 // exact leaf boxes, tested exactly) and puts a binned-SAH hierarchy of union
 // boxes above them, so shadow rays visit far fewer nodes with the same
 // answers.  Kernels use it only for NaN-free rays outside counting passes.
-void build_shadow_tree(FlatBVH& out) {
+void build_shadow_tree(FlatBVH& out, int threads) {
     struct Leaf { float lo[3], hi[3], c[3]; int32_t info; };
     std::vector<Leaf> leaves;
     auto add_leaf = [&](const float* lo, const float* hi, int32_t info) {
@@ -566,13 +667,26 @@ void build_shadow_tree(FlatBVH& out) {
     };
     // binned SAH over leaf centroids; each tree leaf is one reference leaf
     struct TNode { Box box; int left = -1, right = -1, axis = 0; int32_t info = 0; };
-    std::vector<TNode> tn;
     std::vector<int> idx(leaves.size());
     for (size_t i = 0; i < idx.size(); ++i) idx[i] = (int)i;
-    std::function<int(int, int, int)> build = [&](int b, int e, int depth) -> int {
+    // Subtrees are independent (disjoint ranges of idx): the top levels are
+    // built as concurrent tasks into their own node pools, spliced afterwards.
+    struct Sah {
+        const std::vector<Leaf>& leaves;
+        std::vector<int>& idx;
+        int fork;
+        std::vector<TNode> tn;
+        int smax_depth = 0;
+        int (*fn)(Sah&, int, int, int);
+        int build(int b, int e, int depth) { return fn(*this, b, e, depth); }
+    };
+    auto sah_build = [](Sah& me_, int b, int e, int depth) -> int {
+        const std::vector<Leaf>& leaves = me_.leaves;
+        std::vector<int>& idx = me_.idx;
+        std::vector<TNode>& tn = me_.tn;
         TNode node;
         for (int i = b; i < e; ++i) node.box.grow(leaves[idx[i]].lo, leaves[idx[i]].hi);
-        out.smax_depth = std::max(out.smax_depth, depth);
+        me_.smax_depth = std::max(me_.smax_depth, depth);
         const int me = (int)tn.size();
         tn.push_back(node);
         if (e - b == 1) {
@@ -581,14 +695,15 @@ void build_shadow_tree(FlatBVH& out) {
         }
         Box cb;
         for (int i = b; i < e; ++i) cb.grow(leaves[idx[i]].c, leaves[idx[i]].c);
-        constexpr int kBins = 32;
+        constexpr int kMaxBins = 32;
+        const int kBins = std::min(kMaxBins, e - b);   // O(n) per node: small nodes use fewer bins
         double best = 1e300;
         int best_axis = -1, best_split = 0;
         for (int a = 0; a < 3; ++a) {
             const double ext = (double)cb.hi[a] - cb.lo[a];
             if (!(ext > 0)) continue;
-            Box bb[kBins];
-            int cnt[kBins] = {0};
+            Box bb[kMaxBins];
+            int cnt[kMaxBins] = {0};
             for (int i = b; i < e; ++i) {
                 const Leaf& l = leaves[idx[i]];
                 int k = (int)((l.c[a] - cb.lo[a]) / ext * kBins);
@@ -596,8 +711,8 @@ void build_shadow_tree(FlatBVH& out) {
                 bb[k].grow(l.lo, l.hi);
                 cnt[k]++;
             }
-            double right_area[kBins];
-            int right_cnt[kBins];
+            double right_area[kMaxBins];
+            int right_cnt[kMaxBins];
             Box acc;
             int n = 0;
             for (int k = kBins - 1; k > 0; --k) {
@@ -631,14 +746,31 @@ void build_shadow_tree(FlatBVH& out) {
             mid = (int)(it - idx.begin());
             if (mid == b || mid == e) mid = (b + e) / 2;
         }
-        const int l = build(b, mid, depth + 1);
-        const int r = build(mid, e, depth + 1);
+        int l, r;
+        if (depth < me_.fork) {
+            Sah lb{leaves, idx, me_.fork, {}, 0, me_.fn}, rb{leaves, idx, me_.fork, {}, 0, me_.fn};
+            lb.tn.reserve(2 * (size_t)(mid - b));       // one allocation per pool (page faults are costly)
+            rb.tn.reserve(2 * (size_t)(e - mid));
+            auto fr = std::async(std::launch::async, [&, mid, e, depth] { return rb.build(mid, e, depth + 1); });
+            const int lr = lb.build(b, mid, depth + 1);
+            const int rr = fr.get();
+            l = splice_pool(tn, std::move(lb.tn), lr);
+            r = splice_pool(tn, std::move(rb.tn), rr);
+            me_.smax_depth = std::max({me_.smax_depth, lb.smax_depth, rb.smax_depth});
+        } else {
+            l = me_.build(b, mid, depth + 1);
+            r = me_.build(mid, e, depth + 1);
+        }
         tn[me].left = l;
         tn[me].right = r;
         tn[me].axis = axis;
         return me;
     };
-    const int root = build(0, (int)leaves.size(), 0);
+    Sah top{leaves, idx, fork_depth(threads), {}, 0, +sah_build};
+    top.tn.reserve(2 * leaves.size());
+    const int root = top.build(0, (int)leaves.size(), 0);
+    std::vector<TNode> tn = std::move(top.tn);
+    out.smax_depth = top.smax_depth;
     // pairs in pre-order of interior nodes
     std::vector<int32_t> pair_of(tn.size(), -1);
     int32_t np = 0;
@@ -747,6 +879,7 @@ void build_shadow_tree(FlatBVH& out) {
         return me;
     };
     out.qroot = emit(root, 0);
+
     out.lrec.resize(out.lrec.size() + 3);    // a leaf's first-prim loads may run past a 0-prim last leaf
     if (!contain_ok || !lrec_ok || 3 * out.qmax_depth + 4 > dl::kMaxStack) {   // fall back to the binary tree
         out.quads.clear();

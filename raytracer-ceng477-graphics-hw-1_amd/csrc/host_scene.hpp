@@ -69,6 +69,8 @@ struct FlatBVH {
     int qmax_depth = 0;
     int leaves = 0, max_leaf = 0, max_depth = 0, max_stack = 0;
     double build_ms = 0;
+    double ref_ms = 0, flat_ms = 0, stree_ms = 0;
+    int threads = 1;                 // host threads the build used   // phases of build_ms: reference tree, flatten, 4-wide tree
 };
 
 // parser.cpp:6-218 semantics.  Returns empty string on success, else message.
@@ -77,7 +79,11 @@ std::string load_xml(const char* path, HostScene& out);
 // raytracer.cpp:342-348: per-triangle normal and centre.
 void prepare_triangles(HostScene& s);
 
-// bvh.h:48-163 + the GPU flatten. Returns empty string or an error message.
-std::string build_bvh(const HostScene& s, FlatBVH& out);
+// bvh.h:48-163 + the GPU flatten + the 4-wide tree. Returns empty string or an
+// error message.  threads: host build threads (0: RT_BUILD_THREADS, else the
+// hardware concurrency capped at 16; 1: serial).  The output does not depend
+// on the thread count.
+std::string build_bvh(const HostScene& s, FlatBVH& out, int threads = 0);
+int build_threads(int requested);
 
 }  // namespace rtx

@@ -174,7 +174,7 @@ int select_device(const rt_options* opts, int* dev) {
 
 int finish_scene(rt_scene* s, const rt_options* opts) {
     rtx::prepare_triangles(s->host);
-    std::string err = rtx::build_bvh(s->host, s->bvh);
+    std::string err = rtx::build_bvh(s->host, s->bvh, opts ? opts->build_threads : 0);
     if (!err.empty()) return fail(RT_ERR_LIMIT, err);
     s->host_only = opts && (opts->flags & RT_OPT_HOST_ONLY);
     if (s->host_only) return RT_OK;
@@ -655,6 +655,19 @@ int rt_scene_bvh_info(const rt_scene* s, rt_bvh_info* info) {
     info->triangles = (int)s->host.tris.size();
     info->spheres = (int)s->host.spheres.size();
     info->build_ms = s->bvh.build_ms;
+    info->ref_ms = s->bvh.ref_ms;
+    info->wide_ms = s->bvh.stree_ms;
+    info->build_threads = s->bvh.threads;
+    info->wide_nodes = (int)s->bvh.quads.size();
+    uint64_t h = 1469598103934665603ull;           // FNV-1a over the 4-wide tree's bytes
+    auto mix = [&h](const void* p, size_t n) {
+        const unsigned char* b = static_cast<const unsigned char*>(p);
+        for (size_t i = 0; i < n; ++i) { h ^= b[i]; h *= 1099511628211ull; }
+    };
+    mix(s->bvh.quads.data(), s->bvh.quads.size() * sizeof(dl::Quad));
+    mix(s->bvh.lrec.data(), s->bvh.lrec.size() * sizeof(dl::Vec4));
+    mix(&s->bvh.qroot, sizeof(s->bvh.qroot));
+    info->wide_hash = h;
     return RT_OK;
 }
 

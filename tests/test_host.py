@@ -32,7 +32,7 @@ def test_library_exports_every_declared_symbol(pkg):
         assert hasattr(L, n), n
     bound = {s[0] for s in pkg._SIGS}
     assert set(names) == bound, "ctypes bindings out of sync with rt.h"
-    assert L.rt_abi_version() == 1
+    assert L.rt_abi_version() == 2
 
 
 def test_cli_binary_built(pkg):
@@ -52,6 +52,23 @@ def test_bvh_identical_to_oracle(scene, pkg, oracle, scene_dir):
     assert info["max_leaf_prims"] == oinfo["max_leaf"]
     assert info["triangles"] == oinfo["triangles"] and info["spheres"] == oinfo["spheres"]
     assert info["max_stack"] <= 64
+
+
+@pytest.mark.parametrize("scene", ["cornellbox.xml", "bunny.xml", "car.xml", "dragon_lowres.xml",
+                                   "C3_hm_1080p_d6"])
+@pytest.mark.parametrize("threads", [2, 3, 8, 16])
+def test_parallel_build_equals_serial(scene, threads, pkg, oracle, scene_dir):
+    # (f2) the parallel build: the reference tree stays bit-identical to the oracle's (bvh.h:48-163)
+    # and the 4-wide tree is the same bytes whatever the thread count.
+    path = config_path(scene_dir, scene)
+    ser = pkg.Scene.from_xml(path, host_only=True, build_threads=1)
+    par = pkg.Scene.from_xml(path, host_only=True, build_threads=threads)
+    assert par.export_nodes().tobytes() == oracle.OracleScene(path).export_nodes().tobytes()
+    assert par.export_nodes().tobytes() == ser.export_nodes().tobytes()
+    a, b = ser.bvh_info(), par.bvh_info()
+    assert (a["build_threads"], b["build_threads"]) == (1, threads)
+    assert a["wide_nodes"] == b["wide_nodes"] and a["wide_hash"] == b["wide_hash"]
+    assert a["wide_nodes"] > 0
 
 
 def test_horse_and_mug_bvh_stats(pkg, scene_dir):
