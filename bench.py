@@ -71,13 +71,17 @@ def cpu_baseline(xml: str, aa: int, rays_ps_per_frame: int, budget_s: float) -> 
     except AttributeError:
         cores = os.cpu_count() or 1
     threads = max(1, min(16, cores))
+    host = {}        # the reference's own XML load and BVH build times (parser.cpp, bvh.h), for the host rows
     harness = ROOT / "oracle" / "_ref" / "ref_harness"
     if harness.exists():
         def run(reps):
             out = subprocess.run([str(harness), xml, "--aa", str(aa), "--threads", str(threads), "--reps", str(reps)],
                                  check=True, capture_output=True, text=True, cwd=tempfile.gettempdir()).stdout
-            ev = [json.loads(l) for l in out.splitlines() if '"render"' in l][0]
-            return ev["median_s"]
+            evs = [json.loads(l) for l in out.splitlines() if l.startswith("{")]
+            for e in evs:
+                if e.get("event") in ("load", "bvh"):
+                    host[f"ref_{e['event']}_ms"] = round(e["seconds"] * 1e3, 3)
+            return [e for e in evs if e.get("event") == "render"][0]["median_s"]
         first = run(1)
         reps = int(max(1, min(50, budget_s / max(first, 1e-3))))
         med = run(reps) if reps > 1 else first
@@ -97,7 +101,7 @@ def cpu_baseline(xml: str, aa: int, rays_ps_per_frame: int, budget_s: float) -> 
         med = sorted(ts)[len(ts) // 2]
         kind = "port"
     return {"value": round(rays_ps_per_frame / med / 1e6, 3), "unit": "Mray/s", "cores": threads, "kind": kind,
-            "ms_per_frame": round(med * 1e3, 3),
+            "ms_per_frame": round(med * 1e3, 3), **host,
             "sample": f"{reps} full frames of the same workload (median), render only, {threads} threads"}
 
 
@@ -128,6 +132,7 @@ def main() -> int:
     t0 = time.perf_counter()
     scene = pkg.Scene.from_xml(xml, device=local, render_path=a.path)
     load_s = time.perf_counter() - t0
+    binfo = scene.bvh_info()
     cam = scene.camera(0)
     W, H, S = cam.image_width, cam.image_height, a.stripe_rows
     rows = pkg.slab_rows(H, S, world)
@@ -214,6 +219,8 @@ def main() -> int:
                        "primary_rays": prim_frame, "shadow_rays": shadow_frame, "reflection_rays": refl_frame,
                        "mray_s_all": round((ps_frame + refl_frame) * a.steps / elapsed / 1e6, 3),
                        "scene_load_s": round(load_s, 4),
+                       "host_build": {"bvh_build_ms": round(binfo["build_ms"], 2), "ref_tree_ms": round(binfo["ref_ms"], 2),
+                                      "wide_tree_ms": round(binfo["wide_ms"], 2), "threads": binfo["build_threads"]},
                        "host_buffer_ms_per_frame": round(host_ms, 4) if host_ms else None},
             "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
                          "frac": round(achieved / HBM_PEAK_GBPS, 4), "traffic": traffic,

@@ -114,7 +114,9 @@ Image render_threads(RayTracer& rt, Camera& cam, int T, int rows_limit) {
 int main(int argc, char** argv) {
     Args a = parse(argc, argv);
     parser::Scene scene;
+    const double tl0 = now_s();
     scene.loadFromXml(a.scene);
+    printf("{\"event\": \"load\", \"seconds\": %.6f}\n", now_s() - tl0);
     if (a.max_depth != -1000) scene.max_recursion_depth = a.max_depth;
     for (auto& c : scene.cameras) {
         if (a.width > 0) { c.image_width = a.width; c.image_height = a.height; }

@@ -13,39 +13,55 @@
 #include <cstring>
 #include <fstream>
 #include <sstream>
+#include <string_view>
+#include <type_traits>
 
 namespace rtx {
 
 // ---------------------------------------------------------------------------
-// XML: a small DOM (elements, attributes, first text run).  tinyxml2 4.0.1 is
-// used by the reference only to hand element text to a std::stringstream
-// (parser.cpp:9-217); numbers therefore follow istream >> float / >> int,
-// i.e. strtof / strtol on whitespace-separated tokens.
+// XML: a small DOM over the file buffer (elements, attributes, the first text
+// run as an offset range, no copies).  tinyxml2 4.0.1 is used by the reference
+// only to hand element text to a std::stringstream (parser.cpp:9-217); numbers
+// therefore follow istream >> float / >> int, i.e. strtof / strtol on
+// whitespace-separated tokens.  Element text always ends at the next '<' and
+// the buffer is NUL-terminated, so strtof/strtol never read past it.
+// Large number lists (VertexData, Faces) are split at whitespace into chunks
+// parsed by concurrent threads; every token is parsed by the same call as in
+// the serial reading, so the values are identical.
 // ---------------------------------------------------------------------------
 namespace {
 
 struct Elem {
     std::string name;
-    std::string attrs;
-    std::string text;
+    size_t attr_off = 0, attr_len = 0;
+    size_t text_off = 0, text_len = 0;
+    bool has_text = false;
     std::vector<int> kids;
 };
 
 class Dom {
   public:
     std::vector<Elem> el;
+    const std::string* src = nullptr;
 
     bool parse(const std::string& s, std::string& err) {
+        src = &s;
         el.clear();
-        el.push_back(Elem{"#document", "", "", {}});
+        el.reserve(1024);
+        el.push_back(Elem{"#document"});
         std::vector<int> open{0};
+        const char* base = s.data();
         size_t i = 0, n = s.size();
         while (i < n) {
             if (s[i] != '<') {
-                size_t j = s.find('<', i);
-                if (j == std::string::npos) j = n;
+                const void* lt = std::memchr(base + i, '<', n - i);
+                const size_t j = lt ? (size_t)(static_cast<const char*>(lt) - base) : n;
                 Elem& cur = el[open.back()];
-                if (cur.kids.empty() && cur.text.empty()) cur.text.assign(s, i, j - i);
+                if (cur.kids.empty() && !cur.has_text) {
+                    cur.text_off = i;
+                    cur.text_len = j - i;
+                    cur.has_text = j > i;
+                }
                 i = j;
                 continue;
             }
@@ -82,7 +98,8 @@ class Dom {
             }
             if (k >= n) { err = "unterminated tag"; return false; }
             bool self_close = s[k - 1] == '/';
-            e.attrs.assign(s, j, k - j);
+            e.attr_off = j;
+            e.attr_len = k - j;
             int id = (int)el.size();
             el.push_back(std::move(e));
             el[open.back()].kids.push_back(id);
@@ -105,12 +122,18 @@ class Dom {
             if (el[k].name == name) out.push_back(k);
         return out;
     }
+    const char* text(int k) const { return src->data() + (el[k].has_text ? el[k].text_off : src->size()); }
+    size_t text_len(int k) const { return el[k].has_text ? el[k].text_len : 0; }
+    bool attr_has(int k, const char* needle) const {
+        return std::string_view(src->data() + el[k].attr_off, el[k].attr_len).find(needle) != std::string_view::npos;
+    }
 };
 
-// Token reader over one element's text.
+// Token reader over one element's text (a pointer into the NUL-terminated
+// file buffer; the text is followed by '<' or the end of the buffer).
 class Tok {
   public:
-    explicit Tok(const std::string& t) : s_(t), p_(s_.c_str()) {}
+    explicit Tok(const char* p) : p_(p) {}
     bool f(float& v) {
         char* e;
         float x = std::strtof(p_, &e);
@@ -125,17 +148,76 @@ class Tok {
     }
     bool v3(V3& v) { return f(v.x) && f(v.y) && f(v.z); }
     bool word(std::string& w) {
-        while (*p_ && std::isspace((unsigned char)*p_)) ++p_;
+        while (*p_ && *p_ != '<' && std::isspace((unsigned char)*p_)) ++p_;
         const char* b = p_;
-        while (*p_ && !std::isspace((unsigned char)*p_)) ++p_;
+        while (*p_ && *p_ != '<' && !std::isspace((unsigned char)*p_)) ++p_;
         w.assign(b, p_ - b);
         return !w.empty();
     }
 
   private:
-    std::string s_;
     const char* p_;
 };
+
+// All tokens of a number list [p, p+len) (floats or ints), stopping at the
+// first token that does not parse, exactly like repeated Tok::f / Tok::i.
+// Texts above kParMin bytes are split at whitespace into `threads` chunks
+// parsed concurrently; a chunk that stops early ends the list there.
+constexpr size_t kParMin = 64 * 1024;
+
+template <class T>
+std::vector<T> number_list(const char* p, size_t len, int threads) {
+    auto scan = [](const char* b, const char* e, std::vector<T>& out) -> bool {   // false: stopped early
+        const char* q = b;
+        while (true) {
+            while (q < e && std::isspace((unsigned char)*q)) ++q;
+            if (q >= e) return true;
+            char* end;
+            T v;
+            if constexpr (std::is_same<T, float>::value) v = std::strtof(q, &end);
+            else v = (T)std::strtol(q, &end, 10);
+            if (end == q) return false;
+            out.push_back(v);
+            q = end;
+        }
+    };
+    std::vector<T> out;
+    const int nch = len < kParMin ? 1 : std::max(1, std::min(threads, 16));
+    if (nch == 1) {
+        out.reserve(len / 6);
+        scan(p, p + len, out);
+        return out;
+    }
+    std::vector<const char*> cut{p};
+    for (int c = 1; c < nch; ++c) {
+        const char* q = std::max(cut.back(), p + len * c / nch);
+        while (q < p + len && !std::isspace((unsigned char)*q)) ++q;     // a cut never splits a token
+        cut.push_back(q);
+    }
+    cut.push_back(p + len);
+    std::vector<std::vector<T>> part(nch);
+    std::vector<char> full(nch, 1);
+    std::vector<std::future<void>> fs;
+    for (int c = 1; c < nch; ++c)
+        fs.push_back(std::async(std::launch::async, [&, c] {
+            part[c].reserve((cut[c + 1] - cut[c]) / 6);
+            full[c] = scan(cut[c], cut[c + 1], part[c]);
+        }));
+    part[0].reserve((cut[1] - cut[0]) / 6);
+    full[0] = scan(cut[0], cut[1], part[0]);
+    for (auto& f : fs) f.get();
+    size_t total = 0;
+    for (int c = 0; c < nch; ++c) {
+        total += part[c].size();
+        if (!full[c]) break;
+    }
+    out.reserve(total);
+    for (int c = 0; c < nch; ++c) {
+        out.insert(out.end(), part[c].begin(), part[c].end());
+        if (!full[c]) break;
+    }
+    return out;
+}
 
 struct Need {
     const Dom& d;
@@ -145,38 +227,50 @@ struct Need {
         if (k < 0 && err.empty()) err = std::string("Error: missing element <") + name + ">";
         return k;
     }
-    const std::string& text(int parent, const char* name) {
-        static const std::string empty;
+    const char* text(int parent, const char* name) {
         int k = get(parent, name);
-        return k < 0 ? empty : d.el[k].text;
+        return k < 0 ? "" : d.text(k);
     }
 };
 
+bool read_file(const char* path, std::string& out) {
+    FILE* f = std::fopen(path, "rb");
+    if (!f) return false;
+    std::fseek(f, 0, SEEK_END);
+    const long n = std::ftell(f);
+    std::fseek(f, 0, SEEK_SET);
+    if (n < 0) { std::fclose(f); return false; }
+    out.resize((size_t)n);
+    const size_t got = n > 0 ? std::fread(&out[0], 1, (size_t)n, f) : 0;
+    std::fclose(f);
+    out.resize(got);
+    return true;
+}
+
 }  // namespace
 
-std::string load_xml(const char* path, HostScene& sc) {
-    std::ifstream in(path, std::ios::binary);
-    if (!in) return "Error: The xml file cannot be loaded.";          // parser.cpp:14
-    std::stringstream buf;
-    buf << in.rdbuf();
+std::string load_xml(const char* path, HostScene& sc, int threads) {
+    std::string buf;
+    if (!read_file(path, buf)) return "Error: The xml file cannot be loaded.";   // parser.cpp:14
+    threads = build_threads(threads);
     Dom d;
     std::string err;
-    if (!d.parse(buf.str(), err)) return "Error: The xml file cannot be loaded. (" + err + ")";
+    if (!d.parse(buf, err)) return "Error: The xml file cannot be loaded. (" + err + ")";
     if (d.el[0].kids.empty()) return "Error: Root is not found.";   // parser.cpp:20
     int root = d.el[0].kids.front();
     Need need{d, err};
     sc = HostScene();
 
     if (int e = d.child(root, "BackgroundColor"); e >= 0) {          // parser.cpp:24-33
-        Tok t(d.el[e].text);
+        Tok t(d.text(e));
         t.i(sc.bg[0]); t.i(sc.bg[1]); t.i(sc.bg[2]);
     }
     if (int e = d.child(root, "ShadowRayEpsilon"); e >= 0) {         // :36-45 (default 0.001)
-        Tok t(d.el[e].text);
+        Tok t(d.text(e));
         t.f(sc.eps);
     }
     if (int e = d.child(root, "MaxRecursionDepth"); e >= 0) {        // :48-57 (default 0)
-        Tok t(d.el[e].text);
+        Tok t(d.text(e));
         t.i(sc.max_depth);
     }
     int cams = need.get(root, "Cameras");                            // :60-90
@@ -204,7 +298,7 @@ std::string load_xml(const char* path, HostScene& sc) {
     int mats = need.get(root, "Materials");                          // :114-140
     for (int m : d.children(mats, "Material")) {
         MaterialRec M{};
-        M.is_mirror = d.el[m].attrs.find("type=\"mirror\"") != std::string::npos;  // :119
+        M.is_mirror = d.attr_has(m, "type=\"mirror\"");              // :119
         Tok(need.text(m, "AmbientReflectance")).v3(M.ambient);
         Tok(need.text(m, "DiffuseReflectance")).v3(M.diffuse);
         Tok(need.text(m, "SpecularReflectance")).v3(M.specular);
@@ -212,10 +306,10 @@ std::string load_xml(const char* path, HostScene& sc) {
         Tok(need.text(m, "PhongExponent")).f(M.phong);
         sc.materials.push_back(M);
     }
-    {                                                                // :143-151
-        Tok t(need.text(root, "VertexData"));
-        V3 v;
-        while (t.v3(v)) sc.verts.push_back(v);
+    if (int e = need.get(root, "VertexData"); e >= 0) {              // :143-151, complete triples
+        const std::vector<float> v = number_list<float>(d.text(e), d.text_len(e), threads);
+        sc.verts.resize(v.size() / 3);
+        for (size_t i = 0; i < sc.verts.size(); ++i) sc.verts[i] = V3{v[3 * i], v[3 * i + 1], v[3 * i + 2]};
     }
     int objs = need.get(root, "Objects");
     // raytracer.cpp:336-341: standalone triangles first, then mesh faces.
@@ -229,9 +323,12 @@ std::string load_xml(const char* path, HostScene& sc) {
     for (int me : d.children(objs, "Mesh")) {                        // :154-177
         int mat = 0;
         Tok(need.text(me, "Material")).i(mat);
-        Tok f(need.text(me, "Faces"));
-        int a, b, c;
-        while (f.i(a) && f.i(b) && f.i(c)) sc.tris.push_back(TriRec{mat, a, b, c, {0, 0, 0}, {0, 0, 0}});
+        const int fe = need.get(me, "Faces");
+        if (fe < 0) continue;
+        const std::vector<int> f = number_list<int>(d.text(fe), d.text_len(fe), threads);
+        const size_t nf = f.size() / 3;
+        sc.tris.reserve(sc.tris.size() + nf);
+        for (size_t i = 0; i < nf; ++i) sc.tris.push_back(TriRec{mat, f[3 * i], f[3 * i + 1], f[3 * i + 2], {0, 0, 0}, {0, 0, 0}});
     }
     for (int sp : d.children(objs, "Sphere")) {                      // :198-217
         SphereRec S{};

@@ -74,7 +74,8 @@ struct FlatBVH {
 };
 
 // parser.cpp:6-218 semantics.  Returns empty string on success, else message.
-std::string load_xml(const char* path, HostScene& out);
+// threads: for the large number lists (0: build_threads default, 1: serial).
+std::string load_xml(const char* path, HostScene& out, int threads = 0);
 
 // raytracer.cpp:342-348: per-triangle normal and centre.
 void prepare_triangles(HostScene& s);

@@ -611,7 +611,7 @@ int rt_scene_load_xml(const char* path, const rt_options* opts, rt_scene** out) 
     *out = nullptr;
     rt_scene* s = new (std::nothrow) rt_scene();
     if (!s) return fail(RT_ERR_ARG, "out of host memory");
-    std::string err = rtx::load_xml(path, s->host);
+    std::string err = rtx::load_xml(path, s->host, opts ? opts->build_threads : 0);
     if (!err.empty()) {
         delete s;
         return fail(err.find("cannot be loaded") != std::string::npos ? RT_ERR_IO : RT_ERR_PARSE, err);

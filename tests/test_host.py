@@ -71,6 +71,33 @@ def test_parallel_build_equals_serial(scene, threads, pkg, oracle, scene_dir):
     assert a["wide_nodes"] > 0
 
 
+def test_parallel_loader_stops_like_serial(pkg, tmp_path):
+    # (f3) large number lists are parsed in concurrent chunks; a token that does not parse
+    # must end the list exactly where the serial strtof/strtol reading ends it (parser.cpp:143-177).
+    n = 30000
+    verts = " ".join(f"{(i % 97) * 0.013:.6f} {(i % 89) * 0.021:.6f} {(i % 83) * 0.017:.6f}" for i in range(n))
+    cut = verts.index(" ", len(verts) // 2)
+    verts = verts[:cut] + " 1.5x7 " + verts[cut:]          # "1.5x7": 1.5 parses, "x7" stops the list
+    faces = " ".join(f"{1 + i % 500} {1 + (i + 1) % 500} {1 + (i + 7) % 500}" for i in range(20000))
+    faces += " 3 4 zz 5 6 7"
+    xml = f"""<Scene><MaxRecursionDepth>1</MaxRecursionDepth><Cameras><Camera id="1"><Position>0 1 8</Position>
+<Gaze>0 0 -1</Gaze><Up>0 1 0</Up><NearPlane>-1 1 -1 1</NearPlane><NearDistance>1</NearDistance>
+<ImageResolution>8 8</ImageResolution><ImageName>t.ppm</ImageName></Camera></Cameras>
+<Lights><AmbientLight>1 1 1</AmbientLight><PointLight id="1"><Position>0 4 4</Position><Intensity>9 9 9</Intensity>
+</PointLight></Lights><Materials><Material id="1"><AmbientReflectance>1 1 1</AmbientReflectance>
+<DiffuseReflectance>1 1 1</DiffuseReflectance><SpecularReflectance>1 1 1</SpecularReflectance>
+<MirrorReflectance>0 0 0</MirrorReflectance><PhongExponent>1</PhongExponent></Material></Materials><VertexData>{verts}</VertexData>
+<Objects><Mesh id="1"><Material>1</Material><Faces>{faces}</Faces></Mesh></Objects></Scene>"""
+    p = tmp_path / "big.xml"
+    p.write_text(xml)
+    a = pkg.Scene.from_xml(p, host_only=True, build_threads=1)
+    b = pkg.Scene.from_xml(p, host_only=True, build_threads=8)
+    ia, ib = a.bvh_info(), b.bvh_info()
+    assert ia["triangles"] == ib["triangles"] == 20000      # "3 4 zz": the incomplete triple is dropped
+    assert a.export_nodes().tobytes() == b.export_nodes().tobytes()
+    assert ia["wide_hash"] == ib["wide_hash"]
+
+
 def test_horse_and_mug_bvh_stats(pkg, scene_dir):
     # SURVEY.md §4: 50 079 nodes / 25 040 leaves / max leaf 29 / depth 19
     s = pkg.Scene.from_xml(config_path(scene_dir, "horse_and_mug.xml"), host_only=True)
