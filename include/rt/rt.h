@@ -170,6 +170,18 @@ int rt_render(rt_scene* scene, const rt_camera* cam, int aa_factor,
 int rt_render_device(rt_scene* scene, const rt_camera* cam, int aa_factor,
                      int stripe_rows, int rank, int nranks,
                      void* out_dev, void* stream, int flags);
+/* Multi-camera batching (raytracer.cpp:505-519 renders the cameras one after
+ * another): renders cams[0..n) at SSAA factor `aa` with the frames running
+ * concurrently on the device (chain path: up to 4 frames in flight, each on
+ * its own stream and workspace, forked from and joined back into `stream`).
+ * outs_dev[i] must hold cams[i] W*H*3 bytes; each image is identical to
+ * rt_render of that camera.  (ABI 2) */
+int rt_render_cameras_device(rt_scene* scene, const rt_camera* cams, int n, int aa_factor,
+                             void* const* outs_dev, void* stream, int flags);
+/* The same into caller-allocated host buffers, synchronous (the drop-in main's
+ * camera loop).  stats (nullable) sums the work counters over the cameras. */
+int rt_render_cameras(rt_scene* scene, const rt_camera* cams, int n, int aa_factor,
+                      uint8_t* const* outs, rt_stats* stats);
 /* Rows in one rank's slab (max over ranks, so all slabs have equal size). */
 int rt_slab_rows(int height, int stripe_rows, int nranks);
 /* Rank-0 reassembly: slabs[nranks][slab_rows][W][3] (gathered) -> image[H][W][3]. */

@@ -97,6 +97,10 @@ _SIGS = [
     ("rt_render", ctypes.c_int, [_P, ctypes.POINTER(Camera), ctypes.c_int, _P, ctypes.POINTER(Stats)]),
     ("rt_render_device", ctypes.c_int, [_P, ctypes.POINTER(Camera), ctypes.c_int, ctypes.c_int, ctypes.c_int,
                                         ctypes.c_int, _P, _P, ctypes.c_int]),
+    ("rt_render_cameras", ctypes.c_int, [_P, ctypes.POINTER(Camera), ctypes.c_int, ctypes.c_int, _P,
+                                         ctypes.POINTER(Stats)]),
+    ("rt_render_cameras_device", ctypes.c_int, [_P, ctypes.POINTER(Camera), ctypes.c_int, ctypes.c_int, _P, _P,
+                                                ctypes.c_int]),
     ("rt_slab_rows", ctypes.c_int, [ctypes.c_int, ctypes.c_int, ctypes.c_int]),
     ("rt_unshuffle_stripes", ctypes.c_int, [_P, _P, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int, _P]),
     ("rt_counters_reset", ctypes.c_int, [_P, _P]),
@@ -207,6 +211,25 @@ class Scene:
 
     def set_max_depth(self, depth: int) -> None:
         _check(lib().rt_scene_set_max_depth(self._h, depth))
+
+    def render_cameras(self, cams: list, aa: int = 1, stats: bool = False) -> tuple[list, Optional[dict]]:
+        """All cameras in one batched call (rt_render_cameras: frames run concurrently on the GPU);
+        returns one (H, W, 3) uint8 array per camera, each identical to render() of that camera."""
+        n = len(cams)
+        arr = (Camera * n)(*cams)
+        imgs = [np.empty((c.image_height, c.image_width, 3), dtype=np.uint8) for c in cams]
+        ptrs = (ctypes.c_void_p * n)(*[im.ctypes.data for im in imgs])
+        st = Stats() if stats else None
+        _check(lib().rt_render_cameras(self._h, arr, n, aa, ptrs, ctypes.byref(st) if st is not None else None))
+        return imgs, (st.as_dict() if st is not None else None)
+
+    def render_cameras_device(self, cams: list, aa: int, out_ptrs: list, stream: int = 0, count: bool = False) -> None:
+        """Asynchronous batched render into device buffers (rt_render_cameras_device)."""
+        n = len(cams)
+        arr = (Camera * n)(*cams)
+        ptrs = (ctypes.c_void_p * n)(*out_ptrs)
+        _check(lib().rt_render_cameras_device(self._h, arr, n, aa, ptrs, ctypes.c_void_p(stream),
+                                              RT_RENDER_COUNT if count else 0))
 
     def render(self, cam: Camera, aa: int = 1, stats: bool = False) -> tuple[np.ndarray, Optional[dict]]:
         """Synchronous render to a host (H, W, 3) uint8 array (rt_render)."""

@@ -1158,6 +1158,14 @@ __device__ __forceinline__ V path_color(const rtk::DevScene& s, const PcParams& 
     return c;
 }
 
+// Output row of slab row lr.  A frame split into out_k interleaved sub-frames
+// (rt_api.cpp render_frame) renders sub-frame out_j's stripes; its stripe m is
+// stripe m*out_k + out_j of the caller's slab.
+__device__ __forceinline__ int out_row(const PcParams& p, int lr) {
+    const int m = lr / p.stripe_rows;
+    return (m * p.out_k + p.out_j) * p.stripe_rows + (lr - m * p.stripe_rows);
+}
+
 // k_compose: fold + toPixel + ImageProcessor::downSample per output pixel
 __global__ __launch_bounds__(kBlock) void k_compose(rtk::DevScene s, PcParams p) {
     const int lr0 = p.chunk_row0 / p.aa;
@@ -1178,7 +1186,7 @@ __global__ __launch_bounds__(kBlock) void k_compose(rtk::DevScene s, PcParams p)
                 sr += quantise(c.x); sg += quantise(c.y); sb += quantise(c.z);
             }
         const uint32_t ff = (uint32_t)(F * F);
-        uint8_t* o = p.out + ((size_t)lr * p.width + ocol) * 3;
+        uint8_t* o = p.out + ((size_t)out_row(p, lr) * p.width + ocol) * 3;
         o[0] = (uint8_t)(sr / ff); o[1] = (uint8_t)(sg / ff); o[2] = (uint8_t)(sb / ff);
     }
 }
@@ -1335,7 +1343,7 @@ __device__ __forceinline__ void finish_pixels(const rtk::DevScene& s, const PcPa
                 sr += quantise(c.x); sg += quantise(c.y); sb += quantise(c.z);
             }
         const uint32_t ff = (uint32_t)(F * F);
-        uint8_t* o = p.out + ((size_t)lr * p.width + ocol) * 3;
+        uint8_t* o = p.out + ((size_t)out_row(p, lr) * p.width + ocol) * 3;
         o[0] = (uint8_t)(sr / ff); o[1] = (uint8_t)(sg / ff); o[2] = (uint8_t)(sb / ff);
     }
 }

@@ -74,6 +74,7 @@ struct PcParams {
     int wide;         // wide (whole-wave) walks when <= wide lanes of a wave still walk; 0 = off
     int wide_min;     // ... and the walk already took >= wide_min narrow steps
     uint8_t* out;
+    int out_k, out_j;   // sub-frame j of k interleaved sub-frames (out_row); 1, 0 for a whole frame
     unsigned long long* counters;
     unsigned* wq;     // k_fused: per-wave task queues, [grid*4][wq_cap] u32 shadow-task owner ids
     unsigned wq_cap;

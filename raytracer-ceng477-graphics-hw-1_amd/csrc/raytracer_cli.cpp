@@ -52,7 +52,7 @@ int main(int argc, char** argv) {
     }
 
     const auto begin1 = std::chrono::steady_clock::now();
-    rt_options opts{device, 0};
+    rt_options opts{device, 0, 0};
     rt_scene* scene = nullptr;
     if (rt_scene_load_xml(scene_path, &opts, &scene) != RT_OK) return die("load");
     if (max_depth != -1000 && rt_scene_set_max_depth(scene, max_depth) != RT_OK) return die("max-depth");
@@ -61,17 +61,25 @@ int main(int argc, char** argv) {
     if (aa > 1) std::printf("Super Sampling Anti aliasing is enabled. (%d*%dx)\n", aa, aa);
 
     const auto begin2 = std::chrono::steady_clock::now();
+    // all cameras in one batched call (frames run concurrently on the GPU), then write_ppm each
     const int ncam = rt_scene_num_cameras(scene);
+    std::vector<rt_camera> cams(ncam);
+    std::vector<std::string> names(ncam);
+    std::vector<std::vector<uint8_t>> imgs(ncam);
+    std::vector<uint8_t*> outs(ncam);
     for (int c = 0; c < ncam; ++c) {
-        rt_camera cam;
         char name[1024];
-        if (rt_scene_get_camera(scene, c, &cam, name, sizeof name) != RT_OK) return die("camera");
+        if (rt_scene_get_camera(scene, c, &cams[c], name, sizeof name) != RT_OK) return die("camera");
+        names[c] = name;
         std::printf("Rendering %s on GPU (SSAA %dx%d)...\n", name, aa, aa);
-        std::fflush(stdout);
-        std::vector<uint8_t> img((size_t)cam.image_width * cam.image_height * 3);
-        if (rt_render(scene, &cam, aa, img.data(), nullptr) != RT_OK) return die("render");
-        if (write && rt_write_ppm(name, img.data(), cam.image_width, cam.image_height) != RT_OK) return die("write_ppm");
+        imgs[c].resize((size_t)cams[c].image_width * cams[c].image_height * 3);
+        outs[c] = imgs[c].data();
     }
+    std::fflush(stdout);
+    if (ncam > 0 && rt_render_cameras(scene, cams.data(), ncam, aa, outs.data(), nullptr) != RT_OK) return die("render");
+    for (int c = 0; c < ncam && write; ++c)
+        if (rt_write_ppm(names[c].c_str(), imgs[c].data(), cams[c].image_width, cams[c].image_height) != RT_OK)
+            return die("write_ppm");
     const double rendered = seconds_since(begin2);
     std::printf("Rendered in %.3f seconds.\n", rendered);
     std::printf("Total: %.3f seconds.\n", rendered + planted);

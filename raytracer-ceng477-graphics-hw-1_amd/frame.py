@@ -58,3 +58,57 @@ def assemble_frame(slab, height: int, stripe_rows: int,
 
     out = stripes.unshuffle(g.cpu().numpy(), height, stripe_rows)
     return torch.from_numpy(out)
+
+
+# ---------------------------------------------------------------------------
+# Multi-camera batching across GPUs (raytracer.cpp:505-519
+# renders the scene's cameras one after another): camera i is rendered by rank
+# i mod N (each rank batches its cameras, rt_render_cameras_device), and rank 0
+# receives every image with ONE gather of fixed-size packed buffers.
+# ---------------------------------------------------------------------------
+def camera_ranks(ncams: int, nranks: int) -> list[int]:
+    """Owner rank of each camera (round-robin, like the stripes)."""
+    return [i % nranks for i in range(ncams)]
+
+
+def _packed_bytes(sizes, nranks: int) -> int:
+    own = camera_ranks(len(sizes), nranks)
+    per = [0] * nranks
+    for i, (h, w) in enumerate(sizes):
+        per[own[i]] += h * w * 3
+    return max(per + [1])
+
+
+def gather_camera_images(local: dict, sizes: list, dst: int = 0, device=None):
+    """local: {camera index: (H, W, 3) uint8 tensor} rendered by this rank (its
+    cameras per camera_ranks); sizes: [(H, W)] of every camera.  Returns the
+    list of all images (index order) on dst, None elsewhere.  One collective."""
+    import torch
+    import torch.distributed as dist
+
+    dist_on = dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1
+    world = dist.get_world_size() if dist_on else 1
+    rank = dist.get_rank() if dist_on else 0
+    own = camera_ranks(len(sizes), world)
+    cap = _packed_bytes(sizes, world)
+    dev = device if device is not None else (next(iter(local.values())).device if local else "cpu")
+    buf = torch.zeros(cap, dtype=torch.uint8, device=dev)
+    off = 0
+    for i, (h, w) in enumerate(sizes):
+        if own[i] == rank:
+            n = h * w * 3
+            buf[off:off + n].copy_(local[i].reshape(-1))
+            off += n
+    if not dist_on:
+        allb = [buf]
+    else:
+        allb = [torch.empty_like(buf) for _ in range(world)] if rank == dst else None
+        dist.gather(buf, gather_list=allb, dst=dst)
+        if rank != dst:
+            return None
+    out, offs = [], [0] * world
+    for i, (h, w) in enumerate(sizes):
+        r, n = own[i], h * w * 3
+        out.append(allb[r][offs[r]:offs[r] + n].reshape(h, w, 3))
+        offs[r] += n
+    return out

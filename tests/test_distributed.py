@@ -106,3 +106,52 @@ def test_stripe_partition_covers_every_row_once(pkg, H, S, N):
         ok = rows >= 0
         slabs[r][ok] = img[rows[ok]]
     assert np.array_equal(pkg.stripes.unshuffle(slabs, H, S), img)
+
+
+def _cams_main(rank, world, port, xml, out_json):
+    import sys
+
+    sys.path.insert(0, str(ROOT))
+    import __graft_entry__ as graft
+
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        pkg = graft.import_pkg()
+        orc = graft.import_oracle()
+        sc = orc.OracleScene(xml)
+        cams = sc.cameras()
+        sizes = [(h, w) for (w, h, _) in cams]
+        own = pkg.frame.camera_ranks(len(cams), world)
+        local = {}
+        for i in range(len(cams)):
+            if own[i] == rank:                       # this rank's cameras only
+                img, _ = sc.render(i, aa=1, threads=2)
+                local[i] = torch.from_numpy(img)
+        sc.close()
+        imgs = pkg.frame.gather_camera_images(local, sizes, device="cpu")
+        if rank == 0:
+            with open(out_json, "w") as f:
+                json.dump([hashlib.sha256(im.numpy().tobytes()).hexdigest() for im in imgs], f)
+        else:
+            assert imgs is None
+        dist.barrier()
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 4])
+def test_gloo_camera_batch_gather(world, goldens, scene_dir, tmp_path):
+    # (f4) cameras dealt round-robin over ranks (4 ranks > 3 cameras: one rank idle), one gather
+    g = golden_by_name(goldens, "cornellbox_aa1")
+    out = tmp_path / "cams.json"
+    xml = str(scene_dir / "cornellbox.xml")
+    mp.start_processes(_cams_main, args=(world, _free_port(), xml, str(out)), nprocs=world, join=True,
+                       start_method="spawn")
+    shas = json.loads(out.read_text())
+    assert shas == [c["sha256_rgb"] for c in g["cameras"]]
+
+
+def test_camera_ranks_round_robin(pkg):
+    assert pkg.frame.camera_ranks(5, 2) == [0, 1, 0, 1, 0]
+    assert pkg.frame.camera_ranks(3, 8) == [0, 1, 2]

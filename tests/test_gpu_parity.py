@@ -182,3 +182,63 @@ def test_full_size_c5_sha(name, path, goldens, pkg, scene_dir, torch_cuda):
         img, st = s.render(s.camera(0), aa=4, stats=True)
     assert hashlib.sha256(img.tobytes()).hexdigest() == cam_g["sha256_rgb"]
     assert _stats(st) == _counters(cam_g["counters"])
+
+
+@pytest.mark.parametrize("path", ["chain", "megakernel"])
+@pytest.mark.parametrize("name", ["cornellbox_aa1", "car_aa1", "hm_verbatim_aa2"])
+def test_render_cameras_batched(name, path, goldens, pkg, scene_dir, torch_cuda):
+    # (f4) multi-camera batching (raytracer.cpp:505-519): every camera of the scene in one call,
+    # frames concurrent on the GPU; each image bit-identical to its golden, counters summed.
+    g = golden_by_name(goldens, name)
+    with pkg.Scene.from_xml(config_path(scene_dir, g["config"]), device=0, render_path=path) as s:
+        cams = s.cameras()
+        sel = [cams[c["camera"]][0] for c in g["cameras"]]
+        imgs, st = s.render_cameras(sel, aa=g["aa"], stats=True)
+        for cam, img in zip(g["cameras"], imgs):
+            assert np.array_equal(img, load_golden_image(cam)), f"{name}/{cam['image']}"
+        tot = [sum(c["counters"][k] for c in g["cameras"]) for k in
+               ("primary", "shadow", "reflection", "node_visits", "tri_tests", "sphere_tests")]
+        assert list(_stats(st)) == tot
+        # more frames than concurrent slots (slot reuse), order kept
+        many = (sel * 4)[:9]
+        imgs2, _ = s.render_cameras(many, aa=g["aa"])
+        for i, img in enumerate(imgs2):
+            assert np.array_equal(img, load_golden_image(g["cameras"][i % len(sel)]))
+
+
+def test_render_cameras_device_stream(goldens, pkg, scene_dir, torch_cuda):
+    torch = torch_cuda
+    g = golden_by_name(goldens, "cornellbox_aa1")
+    with pkg.Scene.from_xml(config_path(scene_dir, g["config"]), device=0) as s:
+        cams = [s.cameras()[c["camera"]][0] for c in g["cameras"]]
+        outs = [torch.empty((c.image_height, c.image_width, 3), dtype=torch.uint8, device="cuda") for c in cams]
+        st = torch.cuda.Stream()
+        s.render_cameras_device(cams, 1, [o.data_ptr() for o in outs], st.cuda_stream)
+        st.synchronize()
+        for cam, o in zip(g["cameras"], outs):
+            assert np.array_equal(o.cpu().numpy(), load_golden_image(cam))
+
+
+def test_render_cameras_errors(pkg, scene_dir, torch_cuda):
+    with pkg.Scene.from_xml(config_path(scene_dir, "simple.xml"), device=0) as s:
+        with pytest.raises(pkg.RtError):
+            s.render_cameras([], aa=1)
+        c = s.camera(0)
+        with pytest.raises(pkg.RtError):
+            s.render_cameras([c], aa=0)
+
+
+@pytest.mark.parametrize("name", ["cornellbox_aa1", "car_aa1"])
+def test_cli_drop_in_writes_reference_ppms(name, goldens, pkg, scene_dir, tmp_path, torch_cuda):
+    # the drop-in `raytracer scene.xml` (raytracer.cpp:487-525): every camera's ImageName in CWD,
+    # byte-identical to the reference's write_ppm output (ppm.cpp:4-39)
+    import subprocess
+
+    g = golden_by_name(goldens, name)
+    r = subprocess.run([str(pkg.CLI_PATH), str(config_path(scene_dir, g["config"])), "--aa", str(g["aa"])],
+                       cwd=tmp_path, capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, r.stderr
+    assert "Rendered in" in r.stdout
+    for cam in g["cameras"]:
+        data = (tmp_path / cam["image"]).read_bytes()
+        assert hashlib.sha256(data).hexdigest() == cam["sha256_ppm"], cam["image"]
