@@ -337,6 +337,121 @@ __device__ WideOut wide_walk(const rtk::DevScene& s, const Ray& R, float tlim) {
 }
 
 // ---------------------------------------------------------------------------
+// Cooperative certified closest hit: one ray, the whole wave, over the 4-wide
+// tree (traverse2.hpp, comment at Walk).  The wave keeps a stack of items
+// {node or leaf code, entry t} in LDS and expands up to 64 of them per round,
+// one per lane: a quad yields its children whose (conservative) box the ray
+// hits with entry t <= sah_bound(best); a leaf record is tested exactly (exact
+// box, then its primitives in order).  best is the wave minimum after every
+// round.  Every leaf whose entry t is <= sah_bound(t_final) is visited, as in
+// the one-lane walk, so the same certification applies: the winner's t must
+// be a strict minimum (no other hit with t <= t_w, no negative or NaN t), and
+// its leaf entry t blt <= t_w, or blt <= sah_late(t_w) with every other hit at
+// or beyond blt.  A heavy walk of ~40 dependent rounds takes ~tree-depth
+// rounds here.  status 1: stack overflow or not certified (narrow walk).
+// ---------------------------------------------------------------------------
+constexpr int kCoopCap = 128;                              // items per wave
+__shared__ int g_ccode[(kBlock / 64) * kCoopCap];          // quad index or leaf code
+__shared__ float g_ct[(kBlock / 64) * kCoopCap];           // entry t
+
+__device__ WideOut coop_closest(const rtk::DevScene& s, const Ray& R) {
+    const int lane = (int)(threadIdx.x & 63);
+    const int base = (int)(threadIdx.x >> 6) * kCoopCap;
+    const float kInf = __int_as_float(0x7f800000);
+    float bt = kInf, bt2 = kInf, bl = kInf;    // lane-local: best t, second t, best's leaf entry t
+    int bp = -1;
+    bool bad = false;
+    if (lane == 0) {
+        g_ccode[base] = s.qroot;
+        g_ct[base] = 0.0f;
+    }
+    int top = 1;
+    float tb = kInf;                            // wave-uniform best t so far
+    while (top > 0) {
+        const int n = min(64, top);
+        top -= n;
+        const float bound = tb < kInf ? sah_bound(tb) : kInf;
+        int code = 0;
+        float tin = kInf;
+        const bool has = lane < n;
+        if (has) {
+            code = g_ccode[base + top + lane];
+            tin = g_ct[base + top + lane];
+        }
+        int nc = 0;
+        int cc[4] = {0, 0, 0, 0};
+        float ct[4] = {0.0f, 0.0f, 0.0f, 0.0f};
+        bool cv[4] = {false, false, false, false};
+        if (has && tin <= bound) {
+            if (code >= 0) {
+                QuadKids q;
+                quad_load(s, code, q);
+#pragma unroll
+                for (int i = 0; i < 4; ++i) {
+                    float ti;
+                    cv[i] = i < q.n && box_hit_fast(R, q.lo[i], q.hi[i], &ti) && ti <= bound;
+                    cc[i] = q.code[i];
+                    ct[i] = ti;
+                    nc += cv[i] ? 1 : 0;
+                }
+            } else {
+                const float4* L = s.lrec + (code & ~dl::kLeafBit);
+                const float4 h0 = L[0], h1 = L[1], c0 = L[2], c1 = L[3], c2 = L[4];
+                float lt;
+                if (box_hit_fast(R, h0, h1, &lt) && lt <= bound) {
+                    for_leaf_prims(L, __float_as_int(h1.w), __float_as_int(h0.w), c0, c1, c2,
+                                   [&](int slot, const float4& p0, const float4& p1, const float4& p2) {
+                                       float t;
+                                       const bool h = __float_as_int(p0.w) >= 0 ? tri_hit(R, p0, p1, p2, &t)
+                                                                                : sphere_hit(R, p0, p1, &t);
+                                       if (h) {
+                                           if (!(t >= 0.0f)) bad = true;
+                                           if (t < bt) {
+                                               bt2 = fminf(bt2, bt);
+                                               bt = t;
+                                               bp = slot;
+                                               bl = lt;
+                                           } else {
+                                               bt2 = fminf(bt2, t);
+                                           }
+                                       }
+                                       return false;
+                                   });
+                }
+            }
+        }
+        tb = wave_minf(bt);
+        // push the children: exclusive prefix of the per-lane counts
+        int inc = nc;
+        for (int off = 1; off < 64; off <<= 1) {
+            const int y = __shfl_up(inc, off, 64);
+            if (lane >= off) inc += y;
+        }
+        const int total = __shfl(inc, 63, 64);
+        if (top + total > kCoopCap) return WideOut{-1.0f, -1, 1};
+        int w = base + top + inc - nc;
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+            if (cv[i]) {
+                g_ccode[w] = cc[i];
+                g_ct[w] = ct[i];
+                ++w;
+            }
+        top += total;
+    }
+    if (__any(bad)) return WideOut{-1.0f, -1, 1};
+    if (!(tb < kInf)) return WideOut{-1.0f, -1, 0};            // no hit in any reachable leaf
+    const unsigned long long win = __ballot(bt == tb);
+    if (__popcll(win) != 1) return WideOut{-1.0f, -1, 1};      // a tie across lanes
+    const int W = __ffsll((unsigned long long)win) - 1;
+    const float t2 = wave_minf(lane == W ? bt2 : bt);
+    const float blt = __shfl(bl, W, 64);
+    const int prim = __shfl(bp, W, 64);
+    const bool ok = t2 > tb && (blt <= tb || (blt <= sah_late(tb) && t2 >= blt));
+    return ok ? WideOut{tb, prim, 0} : WideOut{-1.0f, -1, 1};
+}
+
+// ---------------------------------------------------------------------------
 // Chain phases.  Phase A (k_chain) walks every sample's closest-hit chain up
 // to level `kinline`; a mirror bounce below it is handed on as a
 // continuation task (the record's owner id; the reflected ray is re-derived
@@ -688,7 +803,8 @@ __device__ void chain_body(const rtk::DevScene& s, const rtk::Eye& e, const PcPa
                 while (m) {
                     const int L = __ffsll((unsigned long long)m) - 1;
                     m &= m - 1;
-                    const WideOut wo = wide_walk<false>(s, ray_bcast(r, L), 0.0f);
+                    const bool quad = __shfl((int)(wk.tree == nullptr), L, 64) != 0;
+                    const WideOut wo = quad ? coop_closest(s, ray_bcast(r, L)) : WideOut{-1.0f, -1, 1};
                     if (lane_id() == L) {
                         if (wo.status == 0) {
                             wk.best = HitRec{wo.t, wo.prim};
