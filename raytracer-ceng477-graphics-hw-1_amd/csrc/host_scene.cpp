@@ -901,7 +901,7 @@ void build_shadow_tree(FlatBVH& out, int threads) {
     // box is verified, with the device's own float arithmetic, to CONTAIN the
     // child's box, so containment (all the any-hit argument needs) holds.
     auto pow2 = [](int e) { return ibits(e << 23); };                       // 2^(e-127), e in [1, 254]
-    auto dec = [](float o, int q, float sc) { return o + (float)q * sc; };  // device decode, no contraction
+    auto dec = [](float o, int q, float sc) { return std::fma((float)q, sc, o); };  // the device decode (quad_hits)
     out.quads.clear();
     out.lrec.clear();
     out.qmax_depth = 0;

@@ -147,32 +147,8 @@ __device__ __forceinline__ unsigned block_sample(unsigned v, unsigned G, unsigne
 }
 
 // ---------------------------------------------------------------------------
-// Wide walk: one ray, the whole wave.  For the frame's tail, where a wave has
-// only a few long walks left and its other lanes would idle.
-//
-// The wave expands the ray's box-reachable subtree in parallel (every child
-// whose box the ray hits, exactly the reference's box test, ignoring tMax;
-// up to 64 nodes or primitives per round), tests every reachable primitive,
-// and keeps the first minimum by (t, DFS position).  DFS position = the path
-// of near(0)/far(1) choices from the root (near = left iff d[axis] > 0,
-// raytracer.cpp:200-206), MSB first, then the primitive's slot in its leaf.
-//
-// Exactness.  The reference visits a subset V of the reachable set R (its
-// pops also need bt <= tMax, :184) and returns the first minimum of V.  Let w
-// be the first minimum of R.  tMax never drops below the final best, so if
-// every box on w's path has bt <= t_w, the reference reaches w: w is in V,
-// hence it is also V's first minimum.  Otherwise (non-conservative pruning:
-// the box t is in un-normalised direction units), or if any candidate t is
-// NaN or exactly -1 (the `best.t == -1` sentinel rule), or the item stack
-// would overflow, the caller falls back to the exact narrow walk.
-// Any-hit: the reference's answer is "some reachable primitive hits with
-// t < dist" whatever the order (no t pruning), so the wide walk is exact.
+// Whole-wave walks: one ray, the whole wave (coop_closest below).
 // ---------------------------------------------------------------------------
-constexpr int kWideCap = 256;                              // items per wave
-__shared__ int g_wcode[(kBlock / 64) * kWideCap];          // >= 0 pair, < 0 ~prim
-__shared__ unsigned g_wkey[(kBlock / 64) * kWideCap];      // path bits (MSB first) | depth (5 bits)
-__shared__ float g_wmax[(kBlock / 64) * kWideCap];         // max box t on the path (+inf for NaN)
-
 struct WideOut {
     float t;
     int prim;     // closest: winner slot or -1; any: 1 = occluded
@@ -191,151 +167,6 @@ __device__ __forceinline__ float wave_minf(float v) {
     for (int off = 32; off > 0; off >>= 1) v = fminf(v, __shfl_xor(v, off, 64));
     return v;
 }
-__device__ __forceinline__ unsigned wave_minu(unsigned v) {
-    for (int off = 32; off > 0; off >>= 1) v = min(v, (unsigned)__shfl_xor((int)v, off, 64));
-    return v;
-}
-__device__ __forceinline__ float nan_to_inf(float t) { return t == t ? t : __int_as_float(0x7f800000); }
-
-template <bool ANY>
-__device__ WideOut wide_walk(const rtk::DevScene& s, const Ray& R, float tlim) {
-    const int lane = (int)(threadIdx.x & 63);
-    const int base = (int)(threadIdx.x >> 6) * kWideCap;
-    const float kInf = __int_as_float(0x7f800000);
-    WideOut out{-1.0f, ANY ? 0 : -1, 0};
-    if (s.nnodes <= 0) return out;
-    float bt0;
-    {
-        const float4 lo = make_float4(s.root_lo[0], s.root_lo[1], s.root_lo[2], 0.0f);
-        const float4 hi = make_float4(s.root_hi[0], s.root_hi[1], s.root_hi[2], 0.0f);
-        if (!box_hit(R, lo, hi, &bt0)) return out;
-    }
-    const bool fast = ray_nan_free(R);
-    int top;
-    if (s.root_info >= 0) {
-        if (lane == 0) {
-            g_wcode[base] = s.root_info;
-            g_wkey[base] = 0u;
-            g_wmax[base] = nan_to_inf(bt0);
-        }
-        top = 1;
-    } else {
-        int a, c;
-        leaf_range(s, s.root_info, &a, &c);
-        if (c > kWideCap) return WideOut{-1.0f, -1, 1};
-        for (int j = lane; j < c; j += 64) {
-            g_wcode[base + j] = ~(a + j);
-            g_wkey[base + j] = 0u;
-            g_wmax[base + j] = nan_to_inf(bt0);
-        }
-        top = c;
-    }
-    float bt = kInf, bm = 0.0f;          // lane-local best candidate (closest)
-    unsigned bk = 0xffffffffu, bp = 0xffffffffu;
-    bool odd = false, occl = false;
-    while (top > 0) {
-        const int n = min(64, top);
-        top -= n;
-        int code = 0;
-        unsigned key = 0;
-        float mx = 0.0f;
-        const bool has = lane < n;
-        if (has) {
-            code = g_wcode[base + top + lane];
-            key = g_wkey[base + top + lane];
-            mx = g_wmax[base + top + lane];
-        }
-        // children to push: ci[k] (info), ck[k] (key), cm[k] (path max), cs/cn (items: 1 or the leaf's prims)
-        int ci0 = 0, ci1 = 0, cs0 = 0, cs1 = 0, cn0 = 0, cn1 = 0;
-        unsigned ck0 = 0, ck1 = 0;
-        float cm0 = 0.0f, cm1 = 0.0f;
-        if (has && code >= 0) {
-            float4 l0, l1, r0, r1;
-            FetchTop::pair(s, code, l0, l1, r0, r1);
-            float tl, tr;
-            bool hl, hr;
-            if (fast) {
-                hl = box_hit_fast(R, l0, l1, &tl);
-                hr = box_hit_fast(R, r0, r1, &tr);
-            } else {
-                hl = box_hit(R, l0, l1, &tl);
-                hr = box_hit(R, r0, r1, &tr);
-            }
-            const unsigned depth = (key & 31u) + 1u;
-            const unsigned bit = 1u << (31u - depth);
-            const unsigned kb = (key & ~31u) | depth;
-            const bool left_first = comp(R.d, __float_as_int(l1.w)) > 0;
-            if (hl) {
-                ci0 = __float_as_int(l0.w);
-                ck0 = kb | (left_first ? 0u : bit);
-                cm0 = fmaxf(mx, nan_to_inf(tl));
-                if (ci0 >= 0) cn0 = 1;
-                else leaf_range(s, ci0, &cs0, &cn0);
-            }
-            if (hr) {
-                ci1 = __float_as_int(r0.w);
-                ck1 = kb | (left_first ? bit : 0u);
-                cm1 = fmaxf(mx, nan_to_inf(tr));
-                if (ci1 >= 0) cn1 = 1;
-                else leaf_range(s, ci1, &cs1, &cn1);
-            }
-        } else if (has) {
-            const int i = ~code;
-            const float4* pr = reinterpret_cast<const float4*>(&s.prims[i]);
-            const float4 p0 = pr[0], p1 = pr[1];
-            float t;
-            bool h;
-            if (__float_as_int(p0.w) >= 0) h = tri_hit(R, p0, p1, pr[2], &t);
-            else h = sphere_hit(R, p0, p1, &t);
-            if (h) {
-                if (ANY) {
-                    if (t < tlim) occl = true;
-                } else if (t != t || t == -1.0f) {
-                    odd = true;
-                } else if (t < bt || (t == bt && (key < bk || (key == bk && (unsigned)i < bp)))) {
-                    bt = t; bk = key; bp = (unsigned)i; bm = mx;
-                }
-            }
-        }
-        if (ANY && __any(occl)) return WideOut{-1.0f, 1, 0};
-        // push: exclusive prefix of the per-lane item counts
-        const int cnt = cn0 + cn1;
-        int inc = cnt;
-        for (int off = 1; off < 64; off <<= 1) {
-            const int y = __shfl_up(inc, off, 64);
-            if (lane >= off) inc += y;
-        }
-        const int total = __shfl(inc, 63, 64);
-        if (top + total > kWideCap) return WideOut{-1.0f, -1, 1};
-        int w = base + top + inc - cnt;
-        if (cn0) {
-            if (ci0 >= 0) {
-                g_wcode[w] = ci0; g_wkey[w] = ck0; g_wmax[w] = cm0; ++w;
-            } else {
-                for (int j = 0; j < cn0; ++j, ++w) { g_wcode[w] = ~(cs0 + j); g_wkey[w] = ck0; g_wmax[w] = cm0; }
-            }
-        }
-        if (cn1) {
-            if (ci1 >= 0) {
-                g_wcode[w] = ci1; g_wkey[w] = ck1; g_wmax[w] = cm1;
-            } else {
-                for (int j = 0; j < cn1; ++j, ++w) { g_wcode[w] = ~(cs1 + j); g_wkey[w] = ck1; g_wmax[w] = cm1; }
-            }
-        }
-        top += total;
-    }
-    if (ANY) return out;
-    if (__any(odd)) return WideOut{-1.0f, -1, 1};
-    const float tmin = wave_minf(bt);
-    if (!(tmin < kInf)) return out;                               // no reachable hit: the reference has none either
-    const unsigned kmin = wave_minu(bt == tmin ? bk : 0xffffffffu);
-    const unsigned pmin = wave_minu(bt == tmin && bk == kmin ? bp : 0xffffffffu);
-    const unsigned long long win = __ballot(bt == tmin && bk == kmin && bp == pmin);
-    const float wm = __shfl(bm, __ffsll((unsigned long long)win) - 1, 64);
-    if (!(wm <= tmin)) return WideOut{-1.0f, -1, 1};            // the reference might prune w's path
-    return WideOut{tmin, (int)pmin, 0};
-}
-
 // ---------------------------------------------------------------------------
 // Cooperative certified closest hit: one ray, the whole wave, over the 4-wide
 // tree (traverse2.hpp, comment at Walk).  The wave keeps a stack of items
@@ -384,14 +215,13 @@ __device__ WideOut coop_closest(const rtk::DevScene& s, const Ray& R) {
         bool cv[4] = {false, false, false, false};
         if (has && tin <= bound) {
             if (code >= 0) {
-                QuadKids q;
-                quad_load(s, code, q);
+                QuadHits q;
+                quad_hits(s, code, R, q);
 #pragma unroll
                 for (int i = 0; i < 4; ++i) {
-                    float ti;
-                    cv[i] = i < q.n && box_hit_fast(R, q.lo[i], q.hi[i], &ti) && ti <= bound;
+                    cv[i] = q.hit[i] && q.t[i] <= bound;
                     cc[i] = q.code[i];
-                    ct[i] = ti;
+                    ct[i] = q.t[i];
                     nc += cv[i] ? 1 : 0;
                 }
             } else {

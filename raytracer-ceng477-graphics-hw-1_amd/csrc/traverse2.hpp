@@ -363,31 +363,66 @@ __device__ __forceinline__ bool walk_restart_ref(const rtk::DevScene& s, const R
 }
 
 // Child boxes of a 4-wide node (dl::Quad), decoded exactly as the host
-// verified them (origin + q * 2^e, no contraction).
-struct QuadKids {
-    float4 lo[4], hi[4];
+// verified them and slab-tested against a NaN-free ray, two children per
+// packed instruction (v_pk_fma_f32 / v_pk_add_f32 / v_pk_mul_f32: IEEE per
+// component, so every value equals the scalar form).  Decode:
+// origin + q * 2^e as one fma, exact because q * 2^e is exact (an 8-bit
+// integer times a power of two); the host checks containment with the same
+// fma.  Slab test: box_hit_fast's, plane by plane (p - o) * inv.
+typedef float f2v __attribute__((ext_vector_type(2)));
+
+struct QuadHits {
+    float t[4];      // entry t of each child box (valid where hit)
+    bool hit[4];     // child exists and its box is hit
     int code[4];
-    int n;
 };
-__device__ __forceinline__ void quad_load(const rtk::DevScene& s, int qi, QuadKids& c) {
+__device__ __forceinline__ void quad_hits(const rtk::DevScene& s, int qi, const Ray& r, QuadHits& c) {
     const float4* q = reinterpret_cast<const float4*>(&s.quads[qi]);
     const float4 q0 = q[0], q1 = q[1], q2 = q[2], q3 = q[3];
     const uint32_t ex = __float_as_uint(q0.w);
-    c.n = (int)(ex >> 24);
-    const float sx = __uint_as_float((ex & 255u) << 23), sy = __uint_as_float(((ex >> 8) & 255u) << 23),
-                sz = __uint_as_float(((ex >> 16) & 255u) << 23);
+    const int n = (int)(ex >> 24);
+    const float sc[3] = {__uint_as_float((ex & 255u) << 23), __uint_as_float(((ex >> 8) & 255u) << 23),
+                         __uint_as_float(((ex >> 16) & 255u) << 23)};
+    const float org[3] = {q0.x, q0.y, q0.z};
+    const float ro[3] = {r.o.x, r.o.y, r.o.z}, ri[3] = {r.inv.x, r.inv.y, r.inv.z};
     const uint32_t qb[6] = {__float_as_uint(q1.x), __float_as_uint(q1.y), __float_as_uint(q1.z),
                             __float_as_uint(q1.w), __float_as_uint(q2.x), __float_as_uint(q2.y)};
     c.code[0] = __float_as_int(q2.z);
     c.code[1] = __float_as_int(q2.w);
     c.code[2] = __float_as_int(q3.x);
     c.code[3] = __float_as_int(q3.y);
+    auto byte = [&](int j) { return (float)((qb[j >> 2] >> ((j & 3) * 8)) & 255u); };
+    float tmn[4], tmx[4];
+#pragma unroll
+    for (int pr = 0; pr < 2; ++pr) {            // children 2pr, 2pr+1
+        const int c0 = 2 * pr, c1 = 2 * pr + 1;
+        f2v lo_t[3], hi_t[3];
+#pragma unroll
+        for (int a = 0; a < 3; ++a) {
+            const f2v s2 = {sc[a], sc[a]}, o2 = {org[a], org[a]};
+            const f2v ql = {byte(c0 * 3 + a), byte(c1 * 3 + a)};
+            const f2v qh = {byte(12 + c0 * 3 + a), byte(12 + c1 * 3 + a)};
+            const f2v lo = __builtin_elementwise_fma(ql, s2, o2);
+            const f2v hi = __builtin_elementwise_fma(qh, s2, o2);
+            const f2v rr = {ro[a], ro[a]}, iv = {ri[a], ri[a]};
+            lo_t[a] = (lo - rr) * iv;
+            hi_t[a] = (hi - rr) * iv;
+        }
+#pragma unroll
+        for (int k = 0; k < 2; ++k) {
+            const int ch = 2 * pr + k;
+            const float x1 = lo_t[0][k], x2 = hi_t[0][k], y1 = lo_t[1][k], y2 = hi_t[1][k], z1 = lo_t[2][k],
+                        z2 = hi_t[2][k];
+            tmn[ch] = __builtin_fmaxf(__builtin_fmaxf(__builtin_fminf(x1, x2), __builtin_fminf(y1, y2)),
+                                      __builtin_fminf(z1, z2));
+            tmx[ch] = __builtin_fminf(__builtin_fminf(__builtin_fmaxf(x1, x2), __builtin_fmaxf(y1, y2)),
+                                      __builtin_fmaxf(z1, z2));
+        }
+    }
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
-        const int b0 = i * 3, b1 = 12 + i * 3;
-        auto byte = [&](int j) { return (float)((qb[j >> 2] >> ((j & 3) * 8)) & 255u); };
-        c.lo[i] = make_float4(q0.x + byte(b0) * sx, q0.y + byte(b0 + 1) * sy, q0.z + byte(b0 + 2) * sz, 0.0f);
-        c.hi[i] = make_float4(q0.x + byte(b1) * sx, q0.y + byte(b1 + 1) * sy, q0.z + byte(b1 + 2) * sz, 0.0f);
+        c.t[i] = tmn[i];
+        c.hit[i] = i < n && tmx[i] >= __builtin_fmaxf(0.0f, tmn[i]);
     }
 }
 
@@ -417,15 +452,14 @@ template <class STK>
 __device__ __forceinline__ bool quad_closest_step(const rtk::DevScene& s, const Ray& r, STK& stk, Walk& k) {
     constexpr int kNone = 0x7fffffff;         // no child (never a quad index or leaf code)
     if (k.cur >= 0) {
-        QuadKids q;
-        quad_load(s, k.cur, q);
+        QuadHits q;
+        quad_hits(s, k.cur, r, q);
         float t[4];
         int c[4];
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
-            float ti;
-            const bool h = i < q.n && box_hit_fast(r, q.lo[i], q.hi[i], &ti) && ti <= k.tmax;
-            t[i] = h ? ti : __builtin_inff();
+            const bool h = q.hit[i] && q.t[i] <= k.tmax;
+            t[i] = h ? q.t[i] : __builtin_inff();
             c[i] = h ? q.code[i] : kNone;
         }
         auto cswap = [&](int a, int b) {
@@ -621,14 +655,13 @@ template <bool COUNT, class STK>
 __device__ __forceinline__ int quad_any_step(const rtk::DevScene& s, const Ray& r, float tlim, STK& stk, Walk& k,
                                              Work& w) {
     if (k.cur >= 0) {
-        QuadKids q;
-        quad_load(s, k.cur, q);
+        QuadHits q;
+        quad_hits(s, k.cur, r, q);
         int next = 0;
         bool have = false;
 #pragma unroll
         for (int c = 0; c < 4; ++c) {
-            float t;
-            if (c < q.n && box_hit_fast(r, q.lo[c], q.hi[c], &t)) {
+            if (q.hit[c]) {
                 if (COUNT) w.nodes++;
                 if (!have) {
                     next = q.code[c];
