@@ -182,6 +182,13 @@ int rt_render_cameras_device(rt_scene* scene, const rt_camera* cams, int n, int 
  * camera loop).  stats (nullable) sums the work counters over the cameras. */
 int rt_render_cameras(rt_scene* scene, const rt_camera* cams, int n, int aa_factor,
                       uint8_t* const* outs, rt_stats* stats);
+/* Diagnostics: dependent-step latency of closest-hit walks.  rays: n x
+ * {o.xyz, dir.xyz}; one wave walks ray i with `lanes` lanes (1..64), `reps`
+ * times; out[4i..4i+3] = {shader cycles of the last rep, steps, winner prim
+ * slot or -1, cycles of the first rep}.  mode 0: the production walk, 1: the
+ * reference tree (ABI 2). */
+int rt_walk_timing(rt_scene* scene, const float* rays, int n, int lanes, int reps, int mode,
+                   unsigned long long* out);
 /* Rows in one rank's slab (max over ranks, so all slabs have equal size). */
 int rt_slab_rows(int height, int stripe_rows, int nranks);
 /* Rank-0 reassembly: slabs[nranks][slab_rows][W][3] (gathered) -> image[H][W][3]. */

@@ -101,6 +101,7 @@ _SIGS = [
                                          ctypes.POINTER(Stats)]),
     ("rt_render_cameras_device", ctypes.c_int, [_P, ctypes.POINTER(Camera), ctypes.c_int, ctypes.c_int, _P, _P,
                                                 ctypes.c_int]),
+    ("rt_walk_timing", ctypes.c_int, [_P, _P, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int, _P]),
     ("rt_slab_rows", ctypes.c_int, [ctypes.c_int, ctypes.c_int, ctypes.c_int]),
     ("rt_unshuffle_stripes", ctypes.c_int, [_P, _P, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int, _P]),
     ("rt_counters_reset", ctypes.c_int, [_P, _P]),
@@ -230,6 +231,14 @@ class Scene:
         ptrs = (ctypes.c_void_p * n)(*out_ptrs)
         _check(lib().rt_render_cameras_device(self._h, arr, n, aa, ptrs, ctypes.c_void_p(stream),
                                               RT_RENDER_COUNT if count else 0))
+
+    def walk_timing(self, rays, lanes: int = 1, reps: int = 3, mode: int = 0) -> np.ndarray:
+        """Diagnostics (rt_walk_timing): rows {cycles, steps, prim, first-rep cycles} per ray."""
+        r = np.ascontiguousarray(np.asarray(rays, dtype=np.float32).reshape(-1, 6))
+        out = np.zeros((len(r), 4), dtype=np.uint64)
+        _check(lib().rt_walk_timing(self._h, r.ctypes.data_as(ctypes.c_void_p), len(r), lanes, reps, mode,
+                                    out.ctypes.data_as(ctypes.c_void_p)))
+        return out
 
     def render(self, cam: Camera, aa: int = 1, stats: bool = False) -> tuple[np.ndarray, Optional[dict]]:
         """Synchronous render to a host (H, W, 3) uint8 array (rt_render)."""

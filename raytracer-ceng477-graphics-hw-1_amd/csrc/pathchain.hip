@@ -1311,6 +1311,53 @@ __global__ __launch_bounds__(kBlock, RT_FINISH_WAVES) void k_finish_any(rtk::Dev
     finish_pixels<false>(s, p);
 }
 
+// Diagnostics (rt_walk_timing): wave 0 of one workgroup walks ray i with
+// lanes [0, lanes) (the same ray in every lane), reps times; lane 0 records
+// the last rep's shader cycles (s_memtime), the steps and the winner.  mode 0:
+// the production closest-hit walk (4-wide tree when certified), 1: the
+// reference tree.  Measures the dependent-step latency of one walk.
+template <int MODE>
+__global__ __launch_bounds__(kBlock) void k_walk_timing(rtk::DevScene s, const float* rays, int n, int lanes, int reps,
+                                                        unsigned long long* out) {
+    constexpr int mode = MODE;
+    block_init(s);
+    if (threadIdx.x >= 64) return;
+    WalkStack stk;
+    Work w;
+    for (int i = 0; i < n; ++i) {
+        const Ray r = make_ray(V{rays[6 * i], rays[6 * i + 1], rays[6 * i + 2]},
+                               V{rays[6 * i + 3], rays[6 * i + 4], rays[6 * i + 5]});
+        unsigned long long t0 = 0, t1 = 0, first = 0;
+        int steps = 0;
+        HitRec h{-1.0f, -1};
+#pragma unroll 1
+        for (int rep = 0; rep < reps; ++rep) {
+            t0 = __builtin_amdgcn_s_memtime();
+            steps = 0;
+            if ((int)threadIdx.x < lanes) {
+                Walk wk;
+                bool go = mode == 0 ? walk_begin<false>(s, r, wk, w) : walk_begin<true>(s, r, wk, w);
+#pragma unroll 1
+                while (go) {
+                    ++steps;
+                    const bool done = mode == 0 ? closest_step<false, FetchTop, WalkStack>(s, r, stk, wk, w)
+                                                : closest_step<true, FetchTop, WalkStack>(s, r, stk, wk, w);
+                    if (done) break;
+                }
+                h = wk.best;
+            }
+            t1 = __builtin_amdgcn_s_memtime();
+            if (rep == 0) first = t1 - t0;
+        }
+        if (threadIdx.x == 0) {
+            out[4 * i] = t1 - t0;
+            out[4 * i + 1] = (unsigned long long)steps;
+            out[4 * i + 2] = (unsigned long long)(long long)h.prim;
+            out[4 * i + 3] = first;
+        }
+    }
+}
+
 }  // namespace
 
 // Shading + fold + SSAA: k_finish (a lane per pixel, default) or k_shade (a
@@ -1354,6 +1401,13 @@ hipError_t launch_fused_chunk(const rtk::DevScene& s, const rtk::Eye& e, const P
     else
         hipLaunchKernelGGL(k_fused<false>, dim3(p.grid), dim3(kBlock), 0, st, s, e, p);
     launch_finish(s, p, st);
+    return hipGetLastError();
+}
+
+hipError_t launch_walk_timing(const rtk::DevScene& s, const float* rays, int n, int lanes, int reps, int mode,
+                              unsigned long long* out, hipStream_t st) {
+    if (mode == 0) hipLaunchKernelGGL(k_walk_timing<0>, dim3(1), dim3(kBlock), 0, st, s, rays, n, lanes, reps, out);
+    else hipLaunchKernelGGL(k_walk_timing<1>, dim3(1), dim3(kBlock), 0, st, s, rays, n, lanes, reps, out);
     return hipGetLastError();
 }
 

@@ -100,6 +100,10 @@ unsigned fused_wave_qcap(int n0, int grid, int levels, int nlights);
 hipError_t launch_fused_chunk(const rtk::DevScene& s, const rtk::Eye& e, const PcParams& p, bool count,
                               hipStream_t stream);
 
+// Diagnostics: dependent-step latency of single closest-hit walks (rt_walk_timing).
+hipError_t launch_walk_timing(const rtk::DevScene& s, const float* rays, int n, int lanes, int reps, int mode,
+                              unsigned long long* out, hipStream_t st);
+
 hipError_t launch_chain_chunk(const rtk::DevScene& s, const rtk::Eye& e, const PcParams& p, bool count,
                               hipStream_t stream);
 

@@ -890,6 +890,26 @@ int rt_render_cameras(rt_scene* s, const rt_camera* cams, int n, int aa, uint8_t
     return RT_OK;
 }
 
+int rt_walk_timing(rt_scene* s, const float* rays, int n, int lanes, int reps, int mode, unsigned long long* out) {
+    if (!s || !rays || !out || n < 1 || lanes < 1 || lanes > 64 || reps < 1) return fail(RT_ERR_ARG, "bad walk-timing arguments");
+    if (s->host_only) return fail(RT_ERR_NO_DEVICE, "scene was created with RT_OPT_HOST_ONLY");
+    HIP_TRY(hipSetDevice(s->device));
+    float* dr = nullptr;
+    unsigned long long* dout = nullptr;
+    HIP_TRY(hipMalloc(reinterpret_cast<void**>(&dr), (size_t)n * 6 * sizeof(float)));
+    if (hipMalloc(reinterpret_cast<void**>(&dout), (size_t)n * 4 * sizeof(unsigned long long)) != hipSuccess) {
+        (void)hipFree(dr);
+        return fail(RT_ERR_HIP, "hipMalloc failed");
+    }
+    hipError_t e = hipMemcpy(dr, rays, (size_t)n * 6 * sizeof(float), hipMemcpyHostToDevice);
+    if (e == hipSuccess) e = rtc::launch_walk_timing(s->dev, dr, n, lanes, reps, mode, dout, nullptr);
+    if (e == hipSuccess) e = hipMemcpy(out, dout, (size_t)n * 4 * sizeof(unsigned long long), hipMemcpyDeviceToHost);
+    (void)hipFree(dr);
+    (void)hipFree(dout);
+    if (e != hipSuccess) return fail(RT_ERR_HIP, std::string("walk timing: ") + hipGetErrorName(e));
+    return RT_OK;
+}
+
 int rt_unshuffle_stripes(const void* slabs, void* image, int width, int height, int stripe_rows, int nranks,
                          void* stream) {
     if (!slabs || !image || width < 1 || height < 1 || stripe_rows < 1 || nranks < 1)

@@ -315,6 +315,8 @@ bool any_quad(const Ray& r, float tlim, long* qf, long* lf) {
 int main(int argc, char** argv) {
     if (argc < 2) { fprintf(stderr, "usage: %s scene.xml [slack]\n", argv[0]); return 2; }
     if (argc > 2) g_slack = atof(argv[2]);
+    int dump_row = -1, dump_col = -1;          // --dump ROW COL: print the pixel's chain rays (o, d) as hex floats
+    if (argc > 5 && !strcmp(argv[3], "--dump")) { dump_row = atoi(argv[4]); dump_col = atoi(argv[5]); }
     HostScene sc;
     std::string err = load_xml(argv[1], sc);
     if (!err.empty()) { fprintf(stderr, "%s\n", err.c_str()); return 1; }
@@ -360,6 +362,8 @@ int main(int argc, char** argv) {
             Ray r = make_ray(e, sub(sp, e));
             long cr = 0, cs = 0, cm = 0, cq_a = 0, cq_b = 0;
             for (int k = 0; k <= sc.max_depth; ++k) {
+                if (row == dump_row && col == dump_col)
+                    printf("RAY %a %a %a %a %a %a\n", r.o.x, r.o.y, r.o.z, r.d.x, r.d.y, r.d.z);
                 Hit hr = closest_ref(r), hs, hq;
                 int stt = closest_sah(r, &hs);
                 const long qf0 = g_qfetch + g_lfetch;
