@@ -333,6 +333,27 @@ __device__ __forceinline__ Ray shadow_from_record(const rtk::DevScene& s, const 
     return make_ray(pnt, nrm(sub(lpos, pnt)));
 }
 
+// The same shadow ray for a task produced by another wave of the workgroup
+// (bq_consume): the record is read past the CU's L1 (sc0 loads), which may
+// still hold an older copy of its line.
+__device__ __forceinline__ float4 ld4_l2(const float4* ptr) {
+    float4 v;
+    asm volatile("global_load_dwordx4 %0, %1, off sc0\n\ts_waitcnt vmcnt(0)" : "=v"(v) : "v"(ptr) : "memory");
+    return v;
+}
+__device__ __forceinline__ Ray shadow_from_record_l2(const rtk::DevScene& s, const PcParams& p, unsigned owner,
+                                                     float* tlim) {
+    const unsigned lvp = owner / (unsigned)s.nlights;
+    const int l = (int)(owner - lvp * (unsigned)s.nlights);
+    const float4* rc = p.rec + (size_t)lvp * 3;
+    const float4 a = ld4_l2(rc), b = ld4_l2(rc + 1);
+    const V pnt = add(V{a.x, a.y, a.z}, mul(V{b.x, b.y, b.z}, s.eps));
+    const float4 lp = ld4(&s.lights[l].px);
+    const V lpos{lp.x, lp.y, lp.z};
+    *tlim = len(sub(lpos, pnt));
+    return make_ray(pnt, nrm(sub(lpos, pnt)));
+}
+
 // Samples of workgroup blk (of G): units blk, blk+G, ... of 256 slots.
 __device__ __forceinline__ unsigned group_samples(unsigned n0, unsigned G, unsigned blk) {
     const unsigned units = (n0 + 255u) / 256u;
@@ -492,6 +513,94 @@ __device__ __forceinline__ bool packet_ok(const Ray& r, bool act) {
     return (bx == 0 || bx == m) && (by == 0 || by == m) && (bz == 0 || bz == m);
 }
 
+// Phase-B shadow tasks go to a workgroup queue in LDS (owner ids) while it has
+// room; the workgroup's waves whose chains are done walk them while the other
+// waves' long mirror chains still run, so those shadow rays no longer wait for
+// k_occlude.  Tasks beyond the queue go to the global queue (k_pack_b +
+// k_occlude) as before.  Protocol (one workgroup, no cross-workgroup waits):
+// slots start kBqEmpty; a producer wave makes its hit records visible to the
+// workgroup (release fence), reserves slots (LDS atomic on g_bq_tail) and
+// writes the owner ids (kBqSkip for a reservation that spilled to the global
+// queue); a consumer lane takes the next slot index (g_bq_head) and waits for
+// it to be written, or gives up once every producer wave has finished
+// (g_bq_prod == 0) and the index is past the final tail.
+#ifndef RT_BQ
+#define RT_BQ 1536
+#endif
+constexpr int kBq = RT_BQ;
+constexpr unsigned kBqEmpty = 0xffffffffu, kBqSkip = 0xfffffffeu;
+__shared__ unsigned g_bq[kBq > 0 ? kBq : 1];
+__shared__ unsigned g_bq_tail, g_bq_head, g_bq_prod;
+
+__device__ __forceinline__ void bq_init() {
+    for (int i = threadIdx.x; i < kBq; i += kBlock) g_bq[i] = kBqEmpty;
+    if (threadIdx.x == 0) {
+        g_bq_tail = 0;
+        g_bq_head = 0;
+        g_bq_prod = kBlock / 64;
+    }
+}
+
+// Walk the workgroup queue's shadow tasks (raytracer.cpp:227-280) until it is
+// drained and every producer wave has finished; returns the rays walked.
+template <bool COUNT>
+__device__ uint32_t bq_consume(const rtk::DevScene& s, const PcParams& p, WalkStack& stk, Work& w) {
+    bool active = false, have = false, out = false;   // walking / holding a slot index / no more slots
+    unsigned slot = 0;
+    Ray r;
+    float tlim = 0.0f;
+    unsigned owner = 0;
+    Walk wk;
+    uint32_t n = 0;
+    while (true) {
+        const unsigned long long want = __ballot(!active && !have && !out);
+        if (want) {
+            const unsigned base = wave_grab_lds(&g_bq_head, want);
+            if (!active && !have && !out) {
+                slot = base + lane_rank(want);
+                if (slot < (unsigned)kBq) have = true;
+                else out = true;
+            }
+        }
+        bool idle = false;
+        if (have) {
+            const unsigned v = __atomic_load_n(&g_bq[slot], __ATOMIC_RELAXED);
+            if (v == kBqEmpty) {
+                // not written yet: wait, unless no producer is left and the slot was never reserved
+                if (__atomic_load_n(&g_bq_prod, __ATOMIC_RELAXED) == 0u &&
+                    slot >= __atomic_load_n(&g_bq_tail, __ATOMIC_RELAXED)) {
+                    have = false;
+                    out = true;
+                } else {
+                    idle = true;
+                }
+            } else {
+                have = false;
+                if (v != kBqSkip) {
+                    owner = v;
+                    r = shadow_from_record_l2(s, p, owner, &tlim);
+                    ++n;
+                    if (walk_begin<COUNT>(s, r, wk, w, true)) active = true;
+                    else p.occ[owner] = 0;
+                }
+            }
+        }
+        if (!__any(active)) {
+            if (__all(out)) break;
+            if (__any(idle)) __builtin_amdgcn_s_sleep(2);
+            continue;
+        }
+        if (active) {
+            const int res = occl_step<COUNT, FetchTop>(s, r, tlim, stk, wk, w);
+            if (res) {
+                p.occ[owner] = res == 2 ? 1 : 0;
+                active = false;
+            }
+        }
+    }
+    return n;
+}
+
 // closest-hit chains of one phase (raytracer.cpp:385-439 minus the shading):
 // record each hit, queue its shadow tasks, follow (or hand on) mirrors.
 template <bool COUNT, bool CONT, bool WIDE = false>
@@ -532,7 +641,32 @@ __device__ void chain_body(const rtk::DevScene& s, const rtk::Eye& e, const PcPa
             }
             // one shadow task per light (:399-404), light-major within the wave
             const unsigned long long hm = __ballot(hit);
-            if (hit) {
+            bool queued = false;
+            if (CONT && kBq > 0 && hm) {
+                // phase B: into the workgroup queue (walked by its finished waves); the records
+                // written above must be visible to the workgroup before the owner ids are
+                __builtin_amdgcn_s_waitcnt(0);     // the record stores have completed (a workgroup fence
+                                                   // alone does not wait for them on gfx950)
+                const unsigned cnt = (unsigned)__popcll(hm), need = cnt * (unsigned)nl;
+                const int leader = __ffsll((unsigned long long)hm) - 1;
+                unsigned base = 0;
+                if (lane_id() == leader) base = atomicAdd(&g_bq_tail, need);
+                base = __shfl(base, leader, 64);
+                const unsigned rank = lane_rank(hm);
+                const unsigned own0 = (unsigned)(((size_t)k * p.cap + path) * nl);
+                if (base + need <= (unsigned)kBq) {
+                    if (hit)
+                        for (int l = 0; l < nl; ++l)
+                            __atomic_store_n(&g_bq[base + l * cnt + rank], own0 + (unsigned)l, __ATOMIC_RELAXED);
+                    queued = true;
+                } else if (hit) {
+                    for (int l = 0; l < nl; ++l) {       // spilled: mark the reserved slots that exist
+                        const unsigned q = base + l * cnt + rank;
+                        if (q < (unsigned)kBq) __atomic_store_n(&g_bq[q], kBqSkip, __ATOMIC_RELAXED);
+                    }
+                }
+            }
+            if (hit && !queued) {
                 const unsigned cnt = (unsigned)__popcll(hm);
                 const unsigned base = wave_grab_lds(&g_scnt, hm);
                 const unsigned rank = lane_rank(hm);
@@ -660,12 +794,18 @@ __device__ void chain_body(const rtk::DevScene& s, const rtk::Eye& e, const PcPa
             }
         }
     }
+    uint32_t nshadow = 0;
+    if (CONT && kBq > 0) {
+        if (lane_id() == 0) atomicSub(&g_bq_prod, 1u);      // this wave produces no more shadow tasks
+        nshadow = bq_consume<COUNT>(s, p, stk, w);
+    }
     __syncthreads();
     if (threadIdx.x == 0) {
         o.scount[blk] = g_scnt * (unsigned)nl;
         if (!CONT) o.ccount[blk] = g_ccnt;
     }
     if (COUNT) {
+        if (CONT) wave_add_counter(&p.counters[1], nshadow);
         wave_add_counter(&p.counters[0], nprim);
         wave_add_counter(&p.counters[2], nrefl);
         wave_add_counter(&p.counters[3], w.nodes);
@@ -794,6 +934,7 @@ template <bool COUNT>
 __global__ __launch_bounds__(kBlock, RT_OCC_WAVES_PER_EU) void k_mix(rtk::DevScene s, rtk::Eye e, PcParams p) {
     const bool chain = blockIdx.x < (unsigned)p.gb;
     if (threadIdx.x == 0) g_ccnt = 0;
+    if (chain && kBq > 0) bq_init();
     block_init(s);
     if (chain) {
         if (p.bprio) __builtin_amdgcn_s_setprio(3);    // the deep chains are the frame's critical path
