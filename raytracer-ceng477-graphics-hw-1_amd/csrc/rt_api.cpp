@@ -120,7 +120,7 @@ struct rt_scene {
     int tune_wide = 0;          // RT_WIDE
     int tune_wide_min = 24;     // RT_WIDE_MIN
     int tune_kinline = 1;       // RT_KINLINE: deepest level of phase A
-    int tune_gb = 0;            // RT_GB: phase-B chain workgroups in k_mix (0 = 1.25 per CU)
+    int tune_gb = 0;            // RT_GB: phase-B chain workgroups in k_mix (0 = 1.5625 per CU: 384-416 best of 256-1024 on C3)
     int tune_bservice = 64;     // RT_BSERVICE: phase-B waves service finished walks once this many lanes are done
     int tune_split = 1;         // RT_SPLIT: a frame runs as this many concurrent interleaved sub-frames (2: +8%, 3: +18% on C3)
     std::string trace_file;     // RT_TRACE: dump per-sample wall-clock timings after each render (diagnostics)
@@ -490,7 +490,7 @@ int render_chain(rt_scene* s, const rtk::Eye& eye, const rtk::FrameParams& f, bo
     // phase split: A walks levels [0, kinline], B the rest (k_mix chain role, gb workgroups)
     const int kinline = std::max(0, s->tune_kinline);
     const bool phase_b = kinline < s->dev.max_depth;
-    const int gb = phase_b ? std::max(1, std::min(s->mix_grid - 1, s->tune_gb > 0 ? s->tune_gb : 5 * s->num_cus / 4)) : 0;
+    const int gb = phase_b ? std::max(1, std::min(s->mix_grid - 1, s->tune_gb > 0 ? s->tune_gb : 25 * s->num_cus / 16)) : 0;
     const int levels_a = std::min(kinline, std::max(s->dev.max_depth, 0)) + 1;
     const unsigned scapA = rtc::chain_block_scap((int)cap, G, levels_a, nl);
     const unsigned ccapA = rtc::chain_block_scap((int)cap, G, 1, 1);
