@@ -319,6 +319,15 @@ __device__ __forceinline__ Ray reflect_from_record(const rtk::DevScene& s, const
     return make_ray(pnt, add(d2, mul(mul(n2, 2.0f), rcos)));
 }
 
+// The same reflected ray from the hit values in registers (phase-B groups).
+__device__ __forceinline__ Ray reflect_from_record_regs(const rtk::DevScene& s, const V hitp, const V nn, const V d) {
+    const V pnt = add(hitp, mul(nn, s.eps));
+    const V d2 = nrm(d);
+    const V n2 = nrm(nn);
+    const float rcos = dot(neg(d2), n2);
+    return make_ray(pnt, add(d2, mul(mul(n2, 2.0f), rcos)));
+}
+
 // Shadow ray of task `owner` (raytracer.cpp:397-404).
 __device__ __forceinline__ Ray shadow_from_record(const rtk::DevScene& s, const PcParams& p, unsigned owner,
                                                   float* tlim) {
@@ -814,6 +823,352 @@ __device__ void chain_body(const rtk::DevScene& s, const rtk::Eye& e, const PcPa
     }
 }
 
+// ---------------------------------------------------------------------------
+// Phase B with four lanes per ray.  A lone wave's walk step is bound by its own
+// instruction latency (~1,750 cycles per 4-wide step, rt_walk_timing), and the
+// frame's tail is a few long serial mirror chains.  Here a group of 4 lanes
+// (a DPP quad) walks one ray of the certified 4-wide walk (traverse2.hpp,
+// comment at Walk): lane q decodes and tests child q of a node, the group
+// picks the nearest with two DPP exchanges and each other hit child pushes
+// itself at its rank (farthest deepest); a leaf's primitives are tested four
+// at a time and reduced.  All group state is replicated in the 4 lanes.  The
+// group's stack is the 4 lanes' LDS stack columns (48 entries, entry e in
+// column e & 3, row e >> 2).  Same visit set and certification as the
+// one-lane walk; a group that overflows its stack, meets a ray that may
+// produce NaN slab values or fails certification restarts the ray on the
+// reference tree with its lane 0 (closest_step).
+// ---------------------------------------------------------------------------
+#ifndef RT_QUAD4
+#define RT_QUAD4 1
+#endif
+constexpr int kG4Stack = 4 * kLdsStackEntries;
+constexpr int kDppX1 = 0xB1, kDppX2 = 0x4E, kDppX3 = 0x1B;   // quad_perm lane ^ 1, ^ 2, ^ 3
+
+template <int CTRL>
+__device__ __forceinline__ int dpp_i(int v) { return __builtin_amdgcn_update_dpp(v, v, CTRL, 0xF, 0xF, false); }
+template <int CTRL>
+__device__ __forceinline__ float dpp_f(float v) { return __int_as_float(dpp_i<CTRL>(__float_as_int(v))); }
+
+__device__ __forceinline__ void g4_put(int e, int2 v) {
+    g_lstk[(e >> 2) * kBlock + (threadIdx.x & ~3u) + (e & 3)] = v;
+}
+__device__ __forceinline__ int2 g4_at(int e) { return g_lstk[(e >> 2) * kBlock + (threadIdx.x & ~3u) + (e & 3)]; }
+
+struct Walk4 {
+    int cur, sp;
+    float tmax;       // pruning bound sah_bound(best)
+    float bt;         // best t (valid when bp >= 0)
+    int bp;           // best primitive slot
+    float blt, t2;    // certification: winner's leaf entry t, smallest other hit t
+    bool bad;         // a hit with t < 0 or NaN
+    bool fail;        // restart on the reference tree
+};
+
+__device__ __forceinline__ void walk4_begin(const rtk::DevScene& s, Walk4& k) {
+    k.cur = s.qroot;
+    k.sp = 0;
+    k.tmax = FLT_MAX;
+    k.bt = -1.0f;
+    k.bp = -1;
+    k.blt = __builtin_inff();
+    k.t2 = __builtin_inff();
+    k.bad = false;
+    k.fail = false;
+}
+
+// One group step; true when the walk is finished (result in k, or k.fail).
+__device__ __forceinline__ bool quad4_step(const rtk::DevScene& s, const Ray& r, Walk4& k) {
+    const int q = (int)(threadIdx.x & 3);
+    const float kInf = __builtin_inff();
+    if (k.cur >= 0) {
+        const float4* Q = reinterpret_cast<const float4*>(&s.quads[k.cur]);
+        const float4 q0 = Q[0], q1 = Q[1], q2 = Q[2], q3 = Q[3];
+        const uint32_t ex = __float_as_uint(q0.w);
+        const int n = (int)(ex >> 24);
+        // this lane's 3 lo bytes (3q..3q+2 of q1.xyz) and 3 hi bytes (3q..3q+2 of q1.w q2.x q2.y)
+        const uint64_t l01 = (uint64_t)__float_as_uint(q1.x) | ((uint64_t)__float_as_uint(q1.y) << 32);
+        const uint64_t l12 = (uint64_t)__float_as_uint(q1.y) | ((uint64_t)__float_as_uint(q1.z) << 32);
+        const uint64_t h01 = (uint64_t)__float_as_uint(q1.w) | ((uint64_t)__float_as_uint(q2.x) << 32);
+        const uint64_t h12 = (uint64_t)__float_as_uint(q2.x) | ((uint64_t)__float_as_uint(q2.y) << 32);
+        const uint32_t lb = (uint32_t)(q < 2 ? l01 >> (24 * q) : l12 >> (24 * q - 32));
+        const uint32_t hb = (uint32_t)(q < 2 ? h01 >> (24 * q) : h12 >> (24 * q - 32));
+        const int code = q == 0 ? __float_as_int(q2.z) : q == 1 ? __float_as_int(q2.w)
+                       : q == 2 ? __float_as_int(q3.x) : __float_as_int(q3.y);
+        const float sx = __uint_as_float((ex & 255u) << 23), sy = __uint_as_float(((ex >> 8) & 255u) << 23),
+                    sz = __uint_as_float(((ex >> 16) & 255u) << 23);
+        const float lx = __builtin_fmaf((float)(lb & 255u), sx, q0.x), ly = __builtin_fmaf((float)((lb >> 8) & 255u), sy, q0.y),
+                    lz = __builtin_fmaf((float)((lb >> 16) & 255u), sz, q0.z);
+        const float hx = __builtin_fmaf((float)(hb & 255u), sx, q0.x), hy = __builtin_fmaf((float)((hb >> 8) & 255u), sy, q0.y),
+                    hz = __builtin_fmaf((float)((hb >> 16) & 255u), sz, q0.z);
+        float t;
+        const bool hit = box_hit_fast(r, make_float4(lx, ly, lz, 0.0f), make_float4(hx, hy, hz, 0.0f), &t);
+        const bool valid = q < n && hit && t <= k.tmax;
+        const float key = valid ? t : kInf;
+        // nearest child: lexicographic minimum of (key, lane)
+        const float k1 = dpp_f<kDppX1>(key), k2 = dpp_f<kDppX2>(key), k3 = dpp_f<kDppX3>(key);
+        const int c1 = dpp_i<kDppX1>(code), c2 = dpp_i<kDppX2>(code), c3 = dpp_i<kDppX3>(code);
+        float m = key;
+        int mi = q;
+        auto take = [&](float kj, int j) {
+            if (kj < m || (kj == m && j < mi)) { m = kj; mi = j; }
+        };
+        take(k1, q ^ 1);
+        take(k2, q ^ 2);
+        take(k3, q ^ 3);
+        const int nv = (key < kInf) + (k1 < kInf) + (k2 < kInf) + (k3 < kInf);
+        if (nv > 0) {
+            // push the other hit children, farthest deepest: my slot = number of other
+            // non-nearest hit children ordered after me (larger key, ties by lane)
+            if (valid && mi != q) {
+                int pos = 0;
+                auto after = [&](float kj, int j) {
+                    if (kj < kInf && j != mi && (kj > key || (kj == key && j < q))) ++pos;
+                };
+                after(k1, q ^ 1);
+                after(k2, q ^ 2);
+                after(k3, q ^ 3);
+                const int e = k.sp + pos;
+                if (e < kG4Stack) g4_put(e, make_int2(code, __float_as_int(key)));
+            }
+            k.sp += nv - 1;
+            if (k.sp > kG4Stack) {
+                k.fail = true;
+                return true;
+            }
+            const int d = mi ^ q;
+            k.cur = d == 0 ? code : d == 1 ? c1 : d == 2 ? c2 : c3;
+            return false;
+        }
+    } else {
+        const float4* L = s.lrec + (k.cur & ~dl::kLeafBit);
+        const float4 h0 = L[0], h1 = L[1];
+        float lt;
+        if (box_hit_fast(r, h0, h1, &lt) && lt <= k.tmax) {   // the reference leaf's exact box
+            const int cnt = __float_as_int(h0.w), slot0 = __float_as_int(h1.w);
+            float m1 = kInf, m2 = kInf;
+            int ms = -1;
+            bool bad = false;
+            for (int j = q; j < cnt; j += 4) {
+                const float4* pr = L + 2 + 3 * j;
+                const float4 p0 = pr[0], p1 = pr[1], p2 = pr[2];
+                float ti;
+                const bool h = __float_as_int(p0.w) >= 0 ? tri_hit(r, p0, p1, p2, &ti) : sphere_hit(r, p0, p1, &ti);
+                if (h) {
+                    if (!(ti >= 0.0f)) bad = true;
+                    if (ti < m1) {
+                        m2 = fminf(m2, m1);
+                        m1 = ti;
+                        ms = slot0 + j;
+                    } else {
+                        m2 = fminf(m2, ti);
+                    }
+                }
+            }
+            // group reduction of (m1, slot, m2): two butterfly rounds
+            auto merge = [&](float o1, int os, float o2) {
+                const bool lt_ = o1 < m1 || (o1 == m1 && os >= 0 && (ms < 0 || os < ms));
+                const float hi = lt_ ? m1 : o1;
+                m2 = fminf(fminf(m2, o2), hi);
+                if (lt_) { m1 = o1; ms = os; }
+            };
+            merge(dpp_f<kDppX1>(m1), dpp_i<kDppX1>(ms), dpp_f<kDppX1>(m2));
+            merge(dpp_f<kDppX2>(m1), dpp_i<kDppX2>(ms), dpp_f<kDppX2>(m2));
+            const int b1 = dpp_i<kDppX1>((int)bad) | (int)bad;
+            bad = (dpp_i<kDppX2>(b1) | b1) != 0;
+            if (bad) k.bad = true;
+            if (ms >= 0) {
+                if (k.bp < 0 || m1 < k.bt) {
+                    if (k.bp >= 0) k.t2 = fminf(k.t2, k.bt);
+                    k.t2 = fminf(k.t2, m2);
+                    k.bt = m1;
+                    k.bp = ms;
+                    k.blt = lt;
+                    k.tmax = sah_bound(m1);
+                } else {
+                    k.t2 = fminf(k.t2, m1);
+                }
+            }
+        }
+    }
+    while (k.sp > 0) {
+        --k.sp;
+        const int2 e = g4_at(k.sp);
+        if (__int_as_float(e.y) <= k.tmax) {
+            k.cur = e.x;
+            return false;
+        }
+    }
+    if (k.bad) k.fail = true;
+    else if (k.bp >= 0) {
+        const float tw = k.bt;
+        k.fail = !(k.t2 > tw && (k.blt <= tw || (k.blt <= sah_late(tw) && k.t2 >= k.blt)));
+    }
+    return true;
+}
+
+// Phase B chains (raytracer.cpp:385-439 minus the shading), one ray per group
+// of 4 lanes; non-counting builds only (the counting pass walks the reference
+// tree with chain_body).
+__device__ void chain4_body(const rtk::DevScene& s, const PcParams& p, unsigned blk, unsigned G, const PhaseOut& o) {
+    WalkStack stk;           // lane 0's private stack for reference-tree restarts
+    Work w;
+    const int nl = s.nlights;
+    const int q = (int)(threadIdx.x & 3);
+    const int lead = (int)(threadIdx.x & 63) & ~3;   // the group's lane 0 in the wave
+    const unsigned nb = chunk_count(p.totals[1], G, blk, (unsigned)p.tchunk);
+    unsigned* const sq = o.sq + (size_t)blk * o.scap;
+    int st = kIdle;
+    bool exhausted = nb == 0;
+    unsigned path = 0;
+    int k = 0;
+    Ray r;
+    Walk4 w4;
+    Walk wk;
+    bool ref = false;        // walking on the reference tree (lane 0)
+    HitRec best{-1.0f, -1};
+    auto start_walk = [&]() {
+        ref = !(ray_nan_free(r) && s.use_sclosest);
+        if (!ref) {
+            walk4_begin(s, w4);
+            st = kTrav;
+        } else {
+            const bool go = walk_begin<false>(s, r, wk, w);     // NaN-capable ray: reference tree
+            st = go ? kTrav : kDone;
+            best = HitRec{-1.0f, -1};
+        }
+    };
+    while (true) {
+        // (1) epilogue of finished walks (all 4 lanes compute; lane 0 writes)
+        if (st == kDone) {
+            const HitRec h = best;
+            const bool hit = h.prim >= 0;
+            V nn{0.0f, 0.0f, 0.0f}, hitp{0.0f, 0.0f, 0.0f};
+            int mat = 0;
+            if (hit) {
+                hit_surface(s, r, h, &nn, &mat);
+                hitp = add(r.o, mul(r.d, h.t));
+                if (q == 0) {
+                    float4* rc = p.rec + ((size_t)k * p.cap + path) * 3;
+                    rc[0] = make_float4(hitp.x, hitp.y, hitp.z, __int_as_float(mat));
+                    rc[1] = make_float4(nn.x, nn.y, nn.z, h.t);
+                    rc[2] = make_float4(r.d.x, r.d.y, r.d.z, 0.0f);
+                }
+            }
+            const bool hit0 = hit && q == 0;
+            const unsigned long long hm = __ballot(hit0);
+            bool queued = false;
+            if (kBq > 0 && hm) {
+                __builtin_amdgcn_s_waitcnt(0);     // the record stores have completed (see chain_body)
+                const unsigned cnt = (unsigned)__popcll(hm), need = cnt * (unsigned)nl;
+                const int leader = __ffsll((unsigned long long)hm) - 1;
+                unsigned base = 0;
+                if (lane_id() == leader) base = atomicAdd(&g_bq_tail, need);
+                base = __shfl(base, leader, 64);
+                const unsigned rank = lane_rank(hm);
+                const unsigned own0 = (unsigned)(((size_t)k * p.cap + path) * nl);
+                if (base + need <= (unsigned)kBq) {
+                    if (hit0)
+                        for (int l = 0; l < nl; ++l)
+                            __atomic_store_n(&g_bq[base + l * cnt + rank], own0 + (unsigned)l, __ATOMIC_RELAXED);
+                    queued = true;
+                } else if (hit0) {
+                    for (int l = 0; l < nl; ++l) {
+                        const unsigned qq = base + l * cnt + rank;
+                        if (qq < (unsigned)kBq) __atomic_store_n(&g_bq[qq], kBqSkip, __ATOMIC_RELAXED);
+                    }
+                }
+            }
+            if (hit0 && !queued) {
+                const unsigned cnt = (unsigned)__popcll(hm);
+                const unsigned base = wave_grab_lds(&g_scnt, hm);
+                const unsigned rank = lane_rank(hm);
+                const unsigned own0 = (unsigned)(((size_t)k * p.cap + path) * nl);
+                for (int l = 0; l < nl; ++l) sq[base * nl + l * cnt + rank] = own0 + (unsigned)l;
+            }
+            bool ends = true;
+            int info = 0;
+            if (!hit) {                                                          // :442-449
+                info = k | ((k == 0 ? kEndBg : kEndZero) << 8);
+            } else if (!s.mats[mat - 1].is_mirror) {
+                info = (k + 1) | (kEndLast << 8);
+            } else if (k >= s.max_depth) {        // child beyond MaxRecursionDepth: 0 (:387-389)
+                info = (k + 1) | (kEndZero << 8);
+            } else {
+                ends = false;
+            }
+            if (ends) {
+                if (q == 0) p.pinfo[path] = info;
+                st = kIdle;
+            } else {
+                r = reflect_from_record_regs(s, hitp, nn, r.d);
+                ++k;
+                start_walk();
+            }
+        }
+        // (2) refill idle groups with continuations
+        if (!exhausted) {
+            const unsigned long long idle = __ballot(st == kIdle && q == 0);
+            if (idle) {
+                const int leader = __ffsll((unsigned long long)idle) - 1;
+                unsigned base = 0;
+                if (lane_id() == leader) base = atomicAdd(&g_head, (unsigned)__popcll(idle));
+                base = __shfl(base, leader, 64);
+                if (base + (unsigned)__popcll(idle) >= nb) exhausted = true;
+                if (st == kIdle) {
+                    const unsigned v = base + (unsigned)__popcll(idle & ((1ull << lead) - 1ull));
+                    if (v < nb) {
+                        const unsigned j = chunk_task(v, G, blk, (unsigned)p.tchunk);
+                        const unsigned lvp = p.cflat[j];
+                        path = lvp % (unsigned)p.cap;
+                        k = (int)(lvp / (unsigned)p.cap) + 1;
+                        r = reflect_from_record(s, p, lvp);
+                        start_walk();
+                    }
+                }
+            }
+        }
+        if (!__any(st != kIdle)) {
+            if (exhausted) break;
+            continue;
+        }
+        // (3) walk until enough groups need service
+        const int thresh = exhausted ? 0 : p.brefill / 4;
+        while (true) {
+            const int nt = __popcll(__ballot(st == kTrav && q == 0));
+            if (nt <= thresh) break;
+            if (st == kTrav) {
+                if (!ref) {
+                    if (quad4_step(s, r, w4)) {
+                        if (w4.fail) {
+                            ref = true;
+                            best = HitRec{-1.0f, -1};
+                            if (!walk_restart_ref(s, r, wk)) st = kDone;
+                        } else {
+                            best = HitRec{w4.bp >= 0 ? w4.bt : -1.0f, w4.bp};
+                            st = kDone;
+                        }
+                    }
+                } else {
+                    bool done = false;
+                    if (q == 0) done = closest_step<false, FetchTop, WalkStack>(s, r, stk, wk, w);
+                    done = __shfl((int)done, lead, 64) != 0;
+                    if (done) {
+                        best.t = __shfl(wk.best.t, lead, 64);
+                        best.prim = __shfl(wk.best.prim, lead, 64);
+                        st = kDone;
+                    }
+                }
+            }
+        }
+    }
+    if (kBq > 0) {
+        if (lane_id() == 0) atomicSub(&g_bq_prod, 1u);      // this wave produces no more shadow tasks
+        bq_consume<false>(s, p, stk, w);
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) o.scount[blk] = g_scnt * (unsigned)nl;
+}
+
 // any-hit of the packed shadow tasks j = blk, blk+G, ... < total
 // (raytracer.cpp:227-280).
 template <bool COUNT>
@@ -938,7 +1293,8 @@ __global__ __launch_bounds__(kBlock, RT_OCC_WAVES_PER_EU) void k_mix(rtk::DevSce
     block_init(s);
     if (chain) {
         if (p.bprio) __builtin_amdgcn_s_setprio(3);    // the deep chains are the frame's critical path
-        chain_body<COUNT, true, RT_WIDE_B>(s, e, p, blockIdx.x, (unsigned)p.gb, phase_b(p));
+        if (!COUNT && RT_QUAD4 && p.quad4) chain4_body(s, p, blockIdx.x, (unsigned)p.gb, phase_b(p));
+        else chain_body<COUNT, true, RT_WIDE_B>(s, e, p, blockIdx.x, (unsigned)p.gb, phase_b(p));
     }
     else if (!p.exp_skip_occ) occlude_body<COUNT>(s, p, blockIdx.x - p.gb, gridDim.x - p.gb, p.sflatA, p.totals[0]);
 }
@@ -1475,7 +1831,45 @@ __global__ __launch_bounds__(kBlock) void k_walk_timing(rtk::DevScene s, const f
         for (int rep = 0; rep < reps; ++rep) {
             t0 = __builtin_amdgcn_s_memtime();
             steps = 0;
-            if ((int)threadIdx.x < lanes) {
+            if (mode == 3) {                     // memory only: dependent quad fetches (first child) from the root
+                if (threadIdx.x == 0) {
+                    int cur = s.qroot;
+#pragma unroll 1
+                    for (int hop = 0; hop < 64; ++hop) {
+                        if (cur < 0) cur = s.qroot;
+                        const float4* Q = reinterpret_cast<const float4*>(&s.quads[cur]);
+                        const float4 q2 = Q[2];
+                        cur = __float_as_int(q2.z) ^ (int)(rays[0] * 0.0f);
+                        ++steps;
+                    }
+                    h = HitRec{0.0f, cur};
+                }
+            } else if (mode == 4) {              // memory only: the same with all four loads of a quad
+                if (threadIdx.x == 0) {
+                    int cur = s.qroot;
+#pragma unroll 1
+                    for (int hop = 0; hop < 64; ++hop) {
+                        if (cur < 0) cur = s.qroot;
+                        const float4* Q = reinterpret_cast<const float4*>(&s.quads[cur]);
+                        const float4 q0 = Q[0], q1 = Q[1], q2 = Q[2], q3 = Q[3];
+                        const int pick = (__float_as_int(q0.x) ^ __float_as_int(q1.y) ^ __float_as_int(q3.y)) & 0;
+                        cur = __float_as_int(q2.z) + pick;
+                        ++steps;
+                    }
+                    h = HitRec{0.0f, cur};
+                }
+            } else if (mode == 2) {
+                if (threadIdx.x < 4) {           // one 4-lane group (chain4_body's walk)
+                    Walk4 w4;
+                    walk4_begin(s, w4);
+#pragma unroll 1
+                    while (true) {
+                        ++steps;
+                        if (quad4_step(s, r, w4)) break;
+                    }
+                    h = HitRec{w4.bt, w4.fail ? -2 : w4.bp};
+                }
+            } else if ((int)threadIdx.x < lanes) {
                 Walk wk;
                 bool go = mode == 0 ? walk_begin<false>(s, r, wk, w) : walk_begin<true>(s, r, wk, w);
 #pragma unroll 1
@@ -1548,7 +1942,10 @@ hipError_t launch_fused_chunk(const rtk::DevScene& s, const rtk::Eye& e, const P
 hipError_t launch_walk_timing(const rtk::DevScene& s, const float* rays, int n, int lanes, int reps, int mode,
                               unsigned long long* out, hipStream_t st) {
     if (mode == 0) hipLaunchKernelGGL(k_walk_timing<0>, dim3(1), dim3(kBlock), 0, st, s, rays, n, lanes, reps, out);
-    else hipLaunchKernelGGL(k_walk_timing<1>, dim3(1), dim3(kBlock), 0, st, s, rays, n, lanes, reps, out);
+    else if (mode == 1) hipLaunchKernelGGL(k_walk_timing<1>, dim3(1), dim3(kBlock), 0, st, s, rays, n, lanes, reps, out);
+    else if (mode == 2) hipLaunchKernelGGL(k_walk_timing<2>, dim3(1), dim3(kBlock), 0, st, s, rays, n, lanes, reps, out);
+    else if (mode == 3) hipLaunchKernelGGL(k_walk_timing<3>, dim3(1), dim3(kBlock), 0, st, s, rays, n, lanes, reps, out);
+    else hipLaunchKernelGGL(k_walk_timing<4>, dim3(1), dim3(kBlock), 0, st, s, rays, n, lanes, reps, out);
     return hipGetLastError();
 }
 

@@ -71,6 +71,7 @@ struct PcParams {
     int bprio;        // 1: phase-B chain waves run at the highest issue priority
     int service;      // ... or once >= service of its lanes finished a walk (epilogue, next bounce)
     int bservice;     // the same for phase-B chains
+    int quad4;        // 1: phase-B chains walk with 4 lanes per ray (chain4_body)
     int spread;       // tiles interleaved per wave within a 256-sample unit (1, 2 or 4)
     int wide;         // wide (whole-wave) walks when <= wide lanes of a wave still walk; 0 = off
     int wide_min;     // ... and the walk already took >= wide_min narrow steps
