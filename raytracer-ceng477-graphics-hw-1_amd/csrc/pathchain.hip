@@ -1552,7 +1552,7 @@ __device__ __forceinline__ V shade_level(const rtk::DevScene& s, const PcParams&
         if (cos_t >= s.cos_thr && cos_t <= 1.0f) {
             const V hh = nrm(add(ldir, neg(nrm(d))));
             const float base = smax(0.0f, dot(nrm(n_), hh));
-            const float ca = (float)pow((double)base, (double)mA.w);
+            const float ca = phong_pow(base, mA.w);
             const float4 mS = ld4(&M.ksx);
             L = add(L, had(mul(V{mS.x, mS.y, mS.z}, ca), E));
         }
@@ -1684,7 +1684,7 @@ __device__ __forceinline__ V shade_words(const rtk::DevScene& s, const PcParams&
 #ifdef RT_EXP_FASTPOW
             const float ca = __powf(base, mA.w);      // experiment only: NOT the reference's rounding
 #else
-            const float ca = (float)pow((double)base, (double)mA.w);
+            const float ca = phong_pow(base, mA.w);
 #endif
             L = add(L, had(mul(V{mS.x, mS.y, mS.z}, ca), E));
         }

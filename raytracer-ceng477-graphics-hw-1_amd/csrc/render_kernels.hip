@@ -179,7 +179,7 @@ __device__ V trace_path(const DevScene& s, Ray ray, int* stk, float* fold, Count
             if (cos_t >= s.cos_thr && cos_t <= 1.0f) {
                 const V hh = nrm(add(lray.d, neg(nrm(ray.d))));
                 const float base = smax(0.0f, dot(nrm(n), hh));
-                const float ca = (float)pow((double)base, (double)mA.w);
+                const float ca = phong_pow(base, mA.w);
                 const float4 mS = ldg4(&M.ksx);
                 L = add(L, had(mul(V{mS.x, mS.y, mS.z}, ca), E));
             }

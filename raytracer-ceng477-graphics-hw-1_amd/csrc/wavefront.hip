@@ -192,7 +192,7 @@ __global__ __launch_bounds__(kBlock) void k_shade(rtk::DevScene s, rtk::Eye e, W
                 if (cos_t >= s.cos_thr && cos_t <= 1.0f) {
                     const V hh = nrm(add(ldir, neg(nrm(r.d))));
                     const float base = smax(0.0f, dot(nrm(n_), hh));
-                    const float ca = (float)pow((double)base, (double)mA.w);
+                    const float ca = phong_pow(base, mA.w);
                     const float4 mS = ld4(&M.ksx);
                     L = add(L, had(mul(V{mS.x, mS.y, mS.z}, ca), E));
                 }
