@@ -533,10 +533,7 @@ __device__ __forceinline__ bool packet_ok(const Ray& r, bool act) {
 // queue); a consumer lane takes the next slot index (g_bq_head) and waits for
 // it to be written, or gives up once every producer wave has finished
 // (g_bq_prod == 0) and the index is past the final tail.
-#ifndef RT_BQ
-#define RT_BQ 1536
-#endif
-constexpr int kBq = RT_BQ;
+constexpr int kBq = kMaxBq;
 constexpr unsigned kBqEmpty = 0xffffffffu, kBqSkip = 0xfffffffeu;
 __shared__ unsigned g_bq[kBq > 0 ? kBq : 1];
 __shared__ unsigned g_bq_tail, g_bq_head, g_bq_prod;
@@ -567,7 +564,7 @@ __device__ uint32_t bq_consume(const rtk::DevScene& s, const PcParams& p, WalkSt
             const unsigned base = wave_grab_lds(&g_bq_head, want);
             if (!active && !have && !out) {
                 slot = base + lane_rank(want);
-                if (slot < (unsigned)kBq) have = true;
+                if (slot < (unsigned)p.bq_cap) have = true;
                 else out = true;
             }
         }
@@ -663,7 +660,7 @@ __device__ void chain_body(const rtk::DevScene& s, const rtk::Eye& e, const PcPa
                 base = __shfl(base, leader, 64);
                 const unsigned rank = lane_rank(hm);
                 const unsigned own0 = (unsigned)(((size_t)k * p.cap + path) * nl);
-                if (base + need <= (unsigned)kBq) {
+                if (base + need <= (unsigned)p.bq_cap) {
                     if (hit)
                         for (int l = 0; l < nl; ++l)
                             __atomic_store_n(&g_bq[base + l * cnt + rank], own0 + (unsigned)l, __ATOMIC_RELAXED);
@@ -671,7 +668,7 @@ __device__ void chain_body(const rtk::DevScene& s, const rtk::Eye& e, const PcPa
                 } else if (hit) {
                     for (int l = 0; l < nl; ++l) {       // spilled: mark the reserved slots that exist
                         const unsigned q = base + l * cnt + rank;
-                        if (q < (unsigned)kBq) __atomic_store_n(&g_bq[q], kBqSkip, __ATOMIC_RELAXED);
+                        if (q < (unsigned)p.bq_cap) __atomic_store_n(&g_bq[q], kBqSkip, __ATOMIC_RELAXED);
                     }
                 }
             }
@@ -1066,7 +1063,7 @@ __device__ void chain4_body(const rtk::DevScene& s, const PcParams& p, unsigned 
                 base = __shfl(base, leader, 64);
                 const unsigned rank = lane_rank(hm);
                 const unsigned own0 = (unsigned)(((size_t)k * p.cap + path) * nl);
-                if (base + need <= (unsigned)kBq) {
+                if (base + need <= (unsigned)p.bq_cap) {
                     if (hit0)
                         for (int l = 0; l < nl; ++l)
                             __atomic_store_n(&g_bq[base + l * cnt + rank], own0 + (unsigned)l, __ATOMIC_RELAXED);
@@ -1074,7 +1071,7 @@ __device__ void chain4_body(const rtk::DevScene& s, const PcParams& p, unsigned 
                 } else if (hit0) {
                     for (int l = 0; l < nl; ++l) {
                         const unsigned qq = base + l * cnt + rank;
-                        if (qq < (unsigned)kBq) __atomic_store_n(&g_bq[qq], kBqSkip, __ATOMIC_RELAXED);
+                        if (qq < (unsigned)p.bq_cap) __atomic_store_n(&g_bq[qq], kBqSkip, __ATOMIC_RELAXED);
                     }
                 }
             }

@@ -26,6 +26,10 @@
 namespace rtc {
 
 constexpr int kMaxChainGrid = 2048;   // k_chain workgroups (= task-queue regions)
+#ifndef RT_BQ
+#define RT_BQ 1536
+#endif
+constexpr int kMaxBq = RT_BQ;          // phase-B workgroup shadow queue (LDS slots, pathchain.hip)
 
 enum PathKind : int {
     kEndBg = 0,     // deepest ray missed at depth 0: background
@@ -72,6 +76,7 @@ struct PcParams {
     int service;      // ... or once >= service of its lanes finished a walk (epilogue, next bounce)
     int bservice;     // the same for phase-B chains
     int quad4;        // 1: phase-B chains walk with 4 lanes per ray (chain4_body)
+    int bq_cap;       // phase-B workgroup shadow queue slots in use (<= kBq; 0: every task to k_occlude)
     int spread;       // tiles interleaved per wave within a 256-sample unit (1, 2 or 4)
     int wide;         // wide (whole-wave) walks when <= wide lanes of a wave still walk; 0 = off
     int wide_min;     // ... and the walk already took >= wide_min narrow steps

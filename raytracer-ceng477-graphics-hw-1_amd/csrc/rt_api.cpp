@@ -121,6 +121,7 @@ struct rt_scene {
     int tune_wide_min = 24;     // RT_WIDE_MIN
     int tune_kinline = 1;       // RT_KINLINE: deepest level of phase A
     int tune_gb = 0;            // RT_GB: phase-B chain workgroups in k_mix (0 = 1.5625 per CU: 384-416 best of 256-1024 on C3)
+    int tune_bq_cap = 1 << 30;  // RT_BQ_CAP: phase-B shadow queue slots (tests force the k_occlude spill path)
     int tune_quad4 = 0;         // RT_QUAD4: phase-B chains with 4 lanes per ray (measured slower: 1.71 vs 1.20 ms)
     int tune_bservice = 64;     // RT_BSERVICE: phase-B waves service finished walks once this many lanes are done
     int tune_split = 1;         // RT_SPLIT: a frame runs as this many concurrent interleaved sub-frames (2: +8%, 3: +18% on C3)
@@ -262,6 +263,7 @@ int finish_scene(rt_scene* s, const rt_options* opts) {
     if (const char* e = std::getenv("RT_WIDE_MIN")) s->tune_wide_min = std::max(0, std::atoi(e));
     if (const char* e = std::getenv("RT_KINLINE")) s->tune_kinline = std::max(0, std::atoi(e));
     if (const char* e = std::getenv("RT_GB")) s->tune_gb = std::max(0, std::atoi(e));
+    if (const char* e = std::getenv("RT_BQ_CAP")) s->tune_bq_cap = std::max(0, std::atoi(e));
     if (const char* e = std::getenv("RT_QUAD4")) s->tune_quad4 = std::atoi(e) != 0;
     if (const char* e = std::getenv("RT_BSERVICE")) s->tune_bservice = std::max(1, std::min(64, std::atoi(e)));
     if (const char* e = std::getenv("RT_SPLIT")) s->tune_split = std::max(1, std::atoi(e));
@@ -543,6 +545,7 @@ int render_chain(rt_scene* s, const rtk::Eye& eye, const rtk::FrameParams& f, bo
     p.service = s->tune_service >= 0 ? s->tune_service : 64;
     p.bservice = s->tune_bservice;
     p.quad4 = s->tune_quad4 && !s->bvh.quads.empty();
+    p.bq_cap = std::min(s->tune_bq_cap, rtc::kMaxBq);
     p.producers = s->tune_producers;
     p.orefill = s->tune_orefill;
     p.brefill = s->tune_brefill;

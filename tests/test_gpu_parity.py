@@ -242,3 +242,21 @@ def test_cli_drop_in_writes_reference_ppms(name, goldens, pkg, scene_dir, tmp_pa
     for cam in g["cameras"]:
         data = (tmp_path / cam["image"]).read_bytes()
         assert hashlib.sha256(data).hexdigest() == cam["sha256_ppm"], cam["image"]
+
+
+@pytest.mark.parametrize("cap", [0, 5, 64])
+@pytest.mark.parametrize("name", ["C3_hm_1080p_d6_aa1", "mirror_spheres_aa1"])
+def test_phase_b_shadow_queue_spill(name, cap, goldens, pkg, scene_dir, torch_cuda, monkeypatch):
+    # phase-B shadow tasks beyond the workgroup LDS queue spill to the global queue (k_pack_b +
+    # k_occlude); tiny caps force partial reservations and SKIP slots: images and counts unchanged
+    monkeypatch.setenv("RT_BQ_CAP", str(cap))
+    g = golden_by_name(goldens, name)
+    with pkg.Scene.from_xml(config_path(scene_dir, g["config"]), device=0) as s:
+        cams = s.cameras()
+        for cam in g["cameras"]:
+            c, _ = cams[cam["camera"]]
+            img, st = s.render(c, aa=g["aa"], stats=True)
+            assert np.array_equal(img, load_golden_image(cam))
+            assert _stats(st) == _counters(cam["counters"])
+            img2, _ = s.render(c, aa=g["aa"], stats=False)
+            assert np.array_equal(img2, load_golden_image(cam))
