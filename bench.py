@@ -146,10 +146,15 @@ def main() -> int:
         def unshuffle_dev(g, img):    # rank-0 kernel: slabs -> row order (rt_unshuffle_stripes)
             pkg.unshuffle_stripes(g.data_ptr(), img.data_ptr(), W, H, S, world, sp)
 
+    def note(msg):      # progress on stderr (long configs such as C5)
+        print(f"[bench rank {rank}] {msg} t={time.perf_counter() - t0:.1f}s", file=sys.stderr, flush=True)
+
+    note(f"scene loaded {W}x{H} aa{aa}")
     # Counting pass (not timed): exact per-rank work for the byte model.
     scene.counters_reset(sp)
     scene.render_device(cam, aa, slab.data_ptr(), sp, S, rank, world, count=True)
     cnt = scene.counters_read()
+    note("counting pass done")
     alg_bytes = (cnt["node_visits"] * B_NODE + cnt["tri_tests"] * B_TRI + cnt["sphere_tests"] * B_SPH
                  + rows * W * aa * aa * B_PIX)
     ps_local = cnt["primary_rays"] + cnt["shadow_rays"]
@@ -170,6 +175,8 @@ def main() -> int:
 
     for _ in range(a.warmup):
         step()
+    torch.cuda.synchronize(dev)
+    note("warmup done")
     evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(a.steps)]
     if world > 1:
         dist.barrier()
@@ -181,6 +188,7 @@ def main() -> int:
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t0
+    note(f"timed {a.steps} steps")
     kern_ms = sum(e0.elapsed_time(e1) for e0, e1 in evs) / a.steps
     tmax = torch.tensor([elapsed, kern_ms], dtype=torch.float64, device=dev)
     if world > 1:

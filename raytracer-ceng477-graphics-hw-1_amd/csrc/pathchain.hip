@@ -797,6 +797,14 @@ __device__ void chain_body(const rtk::DevScene& s, const rtk::Eye& e, const PcPa
             if (st == kTrav) {
                 ++wsteps;
                 if (closest_step<COUNT, FetchTop, WalkStack, CONT>(s, r, stk, wk, w)) st = kDone;
+#ifdef RT_WALK_CAP
+                if (st == kTrav && wsteps > RT_WALK_CAP) {   // diagnostics build: report a runaway walk
+                    printf("RUNAWAY path %u k %d tree %d sp %d cur %d tmax %a best %a/%d o %a %a %a d %a %a %a\n", path, k,
+                           wk.tree == nullptr ? 4 : (wk.tree == s.pairs ? 2 : 1), wk.sp, wk.cur, wk.tmax, wk.best.t,
+                           wk.best.prim, r.o.x, r.o.y, r.o.z, r.d.x, r.d.y, r.d.z);
+                    st = kDone;
+                }
+#endif
             }
         }
     }
