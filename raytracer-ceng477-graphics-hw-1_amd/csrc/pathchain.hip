@@ -796,7 +796,16 @@ __device__ void chain_body(const rtk::DevScene& s, const rtk::Eye& e, const PcPa
                 break;
             if (st == kTrav) {
                 ++wsteps;
+#ifdef RT_WALK_TRACE_PATH
+                const int c0 = wk.cur, sp0 = wk.sp;
+#endif
                 if (closest_step<COUNT, FetchTop, WalkStack, CONT>(s, r, stk, wk, w)) st = kDone;
+#ifdef RT_WALK_TRACE_PATH
+                if (path == RT_WALK_TRACE_PATH && k == 0 && wsteps < 40)
+                    printf("TRACE step %d cur %d sp %d -> cur %d sp %d st %d tree %d e0 %d e1 %d e2 %d\n", wsteps, c0, sp0,
+                           wk.cur, wk.sp, st, wk.tree == nullptr ? 4 : 2, stk.at(0).x, wk.sp > 1 ? stk.at(1).x : -9,
+                           wk.sp > 2 ? stk.at(2).x : -9);
+#endif
 #ifdef RT_WALK_CAP
                 if (st == kTrav && wsteps > RT_WALK_CAP) {   // diagnostics build: report a runaway walk
                     printf("RUNAWAY path %u k %d tree %d sp %d cur %d tmax %a best %a/%d o %a %a %a d %a %a %a\n", path, k,
