@@ -802,9 +802,9 @@ __device__ void chain_body(const rtk::DevScene& s, const rtk::Eye& e, const PcPa
                 if (closest_step<COUNT, FetchTop, WalkStack, CONT>(s, r, stk, wk, w)) st = kDone;
 #ifdef RT_WALK_TRACE_PATH
                 if (path == RT_WALK_TRACE_PATH && k == 0 && wsteps < 40)
-                    printf("TRACE step %d cur %d sp %d -> cur %d sp %d st %d tree %d e0 %d e1 %d e2 %d\n", wsteps, c0, sp0,
-                           wk.cur, wk.sp, st, wk.tree == nullptr ? 4 : 2, stk.at(0).x, wk.sp > 1 ? stk.at(1).x : -9,
-                           wk.sp > 2 ? stk.at(2).x : -9);
+                    printf("TRACE step %d cur %d sp %d -> cur %d sp %d st %d tree %p pairs %p root %d best %a/%d t2 %a blt %a\n",
+                           wsteps, c0, sp0, wk.cur, wk.sp, st, (const void*)wk.tree, (const void*)s.pairs, s.root_info,
+                           wk.best.t, wk.best.prim, wk.t2, wk.blt);
 #endif
 #ifdef RT_WALK_CAP
                 if (st == kTrav && wsteps > RT_WALK_CAP) {   // diagnostics build: report a runaway walk
