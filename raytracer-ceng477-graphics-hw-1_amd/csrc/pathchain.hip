@@ -277,7 +277,7 @@ __device__ WideOut coop_closest(const rtk::DevScene& s, const Ray& R) {
     const float t2 = wave_minf(lane == W ? bt2 : bt);
     const float blt = __shfl(bl, W, 64);
     const int prim = __shfl(bp, W, 64);
-    const bool ok = t2 > tb && (blt <= tb || (blt <= sah_late(tb) && t2 >= blt));
+    const bool ok = sah_certified(tb, t2, blt);
     return ok ? WideOut{tb, prim, 0} : WideOut{-1.0f, -1, 1};
 }
 
@@ -1015,7 +1015,7 @@ __device__ __forceinline__ bool quad4_step(const rtk::DevScene& s, const Ray& r,
     if (k.bad) k.fail = true;
     else if (k.bp >= 0) {
         const float tw = k.bt;
-        k.fail = !(k.t2 > tw && (k.blt <= tw || (k.blt <= sah_late(tw) && k.t2 >= k.blt)));
+        k.fail = !sah_certified(tw, k.t2, k.blt);
     }
     return true;
 }

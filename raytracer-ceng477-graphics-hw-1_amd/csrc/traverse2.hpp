@@ -251,6 +251,15 @@ struct Walk {
 // Cramer's t and the slab t round differently): tools/exp_sah_closest.cpp.
 __device__ __forceinline__ float sah_bound(float t) { return t + t * 0.001953125f; }
 __device__ __forceinline__ float sah_late(float t) { return t + t * 0.0009765625f; }
+// The certification test (conditions (1)-(2) above) for winner t tw, runner-up
+// t2 and winner leaf entry blt.  Bitwise & and | on purpose: one predicate and
+// one branch into walk_restart_ref.  The short-circuit form let the gfx950
+// backend (ROCm 7.2) clear the walk's tree pointer on every lane that passed
+// t2 > tw, including lanes that then failed the blt test and restarted, so
+// those walks re-entered the 4-wide tree and never finished.
+__device__ __forceinline__ bool sah_certified(float tw, float t2, float blt) {
+    return (t2 > tw) & ((blt <= tw) | ((blt <= sah_late(tw)) & (t2 >= blt)));
+}
 
 // Both child boxes of a pair; the min/max form when every active lane's ray
 // is NaN-free (wave-uniform branch, so no divergence between the two forms).
@@ -522,7 +531,7 @@ __device__ __forceinline__ bool quad_closest_step(const rtk::DevScene& s, const 
     }
     if (k.best.prim >= 0) {
         const float tw = k.best.t;
-        const bool ok = k.t2 > tw && (k.blt <= tw || (k.blt <= sah_late(tw) && k.t2 >= k.blt));
+        const bool ok = sah_certified(tw, k.t2, k.blt);
         if (!ok) return !walk_restart_ref(s, r, k);
     }
     return true;
