@@ -43,6 +43,9 @@ struct DevScene {
     const float4* lrec;   // leaf records (dl::LeafHead + prims), indexed in 16-B units
     int qroot;
     int use_sclosest;     // NaN-free closest-hit rays walk the occlusion tree first, certified (traverse2.hpp)
+    int leaf_wait_any;    // the same for any-hit walks (RT_LEAF_WAIT_ANY)
+    int leaf_wait;        // 4-wide walks: a lane at a leaf record waits while fewer than leaf_wait/64 of the
+                          // wave's walking lanes are at one (0: never waits; RT_LEAF_WAIT)
 
     // Sphere prims carry ~sphere_index in p0.w (negative), triangles their id.
     __device__ __forceinline__ bool prim_is_sphere(int, const float4 p0) const {

@@ -457,9 +457,21 @@ __device__ __forceinline__ bool for_leaf_prims(const float4* L, int slot0, int c
 
 // One step of the certified closest-hit walk over the 4-wide tree (see
 // sah_bound); true when finished (result in k.best).  NaN-free rays only.
+// Leaf postponing (SIMD efficiency): the interior and leaf branches of a step
+// are both executed whenever the wave's walking lanes straddle them, so a lane
+// holding a leaf record skips steps while fewer than leaf_wait/64 of the
+// walking lanes hold one; the others' interior steps then run alone.  The
+// visit sequence of every lane is unchanged.
+__device__ __forceinline__ bool leaf_postponed(int wait, const Walk& k) {
+    if (wait <= 0) return false;
+    const unsigned long long lm = __ballot(k.cur < 0), am = __ballot(1);
+    return k.cur < 0 && __popcll(lm) * 64 < __popcll(am) * wait;
+}
+
 template <class STK>
 __device__ __forceinline__ bool quad_closest_step(const rtk::DevScene& s, const Ray& r, STK& stk, Walk& k) {
     constexpr int kNone = 0x7fffffff;         // no child (never a quad index or leaf code)
+    if (leaf_postponed(s.leaf_wait, k)) return false;
     if (k.cur >= 0) {
         QuadHits q;
         quad_hits(s, k.cur, r, q);
@@ -663,6 +675,7 @@ __device__ __forceinline__ int any_step(const rtk::DevScene& s, const Ray& r, fl
 template <bool COUNT, class STK>
 __device__ __forceinline__ int quad_any_step(const rtk::DevScene& s, const Ray& r, float tlim, STK& stk, Walk& k,
                                              Work& w) {
+    if (!COUNT && leaf_postponed(s.leaf_wait_any, k)) return 0;
     if (k.cur >= 0) {
         QuadHits q;
         quad_hits(s, k.cur, r, q);
