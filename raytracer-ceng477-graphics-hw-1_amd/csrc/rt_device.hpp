@@ -121,7 +121,11 @@ __device__ __forceinline__ bool tri_hit(const Ray& r, const float4 a, const floa
 // the reference's glibc pow returns base exactly (its error bound is below one
 // double ulp and base is a double), so the double pow is skipped there.
 __device__ __forceinline__ float phong_pow(float base, float phong) {
+#ifdef RT_EXP_NOPOW
+    return phong == 1.0f ? base : base * base;     // timing experiment only (wrong output)
+#else
     return phong == 1.0f ? base : (float)pow((double)base, (double)phong);
+#endif
 }
 
 // Ray::intersects(Sphere) (raytracer.cpp:70-96) without the normal (computed
