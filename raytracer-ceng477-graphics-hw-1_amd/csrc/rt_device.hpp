@@ -19,6 +19,7 @@
 #include <cstdint>
 
 #include "device_layout.hpp"
+#include "phong_pow.hpp"
 
 namespace rtd {
 
@@ -117,16 +118,9 @@ __device__ __forceinline__ bool tri_hit(const Ray& r, const float4 a, const floa
     return alpha >= 0 && beta >= 0 && gamma >= 0 && t >= 0.0f;
 }
 
-// (float)pow((double)base, (double)phong) (raytracer.cpp:414).  For phong == 1
-// the reference's glibc pow returns base exactly (its error bound is below one
-// double ulp and base is a double), so the double pow is skipped there.
-__device__ __forceinline__ float phong_pow(float base, float phong) {
-#ifdef RT_EXP_NOPOW
-    return phong == 1.0f ? base : base * base;     // timing experiment only (wrong output)
-#else
-    return phong == 1.0f ? base : (float)pow((double)base, (double)phong);
-#endif
-}
+// (float)pow((double)base, (double)phong) (raytracer.cpp:414): phong_pow.hpp
+// (integer exponents by squaring with an exact rounding test, else the double pow).
+using rtp::phong_pow;
 
 // Ray::intersects(Sphere) (raytracer.cpp:70-96) without the normal (computed
 // for the winner only; it is a pure function of ray, sphere and t1).

@@ -252,3 +252,22 @@ def test_scene_create_from_desc_matches_xml(pkg, oracle, scene_dir):
     d.triangles = arr(Tri, tris)
     h2 = ctypes.c_void_p()
     assert L.rt_scene_create(ctypes.byref(d), ctypes.byref(opts), ctypes.byref(h2)) == -1
+
+
+def test_phong_pow_matches_glibc_pow(tmp_path):
+    """phong_pow.hpp (integer exponents by squaring + exact rounding test) equals the
+    reference's (float)pow((double)b, (double)p) (raytracer.cpp:414) on 2.1 M cases."""
+    import shutil
+    import subprocess
+    from pathlib import Path
+    cxx = shutil.which("g++")
+    if cxx is None:
+        pytest.skip("g++ not available")
+    root = Path(__file__).resolve().parent.parent
+    exe = tmp_path / "phong_pow_check"
+    subprocess.run([cxx, "-O2", "-std=c++17", f"-I{root / 'raytracer-ceng477-graphics-hw-1_amd' / 'csrc'}",
+                    str(root / "tests" / "native" / "phong_pow_check.cpp"), "-o", str(exe)], check=True)
+    out = subprocess.run([str(exe), "100000"], capture_output=True, text=True, timeout=120)
+    checked, fast, bad = map(int, out.stdout.split()[-3:])
+    assert bad == 0, out.stdout
+    assert checked == 2_100_000 and fast > checked // 2
