@@ -27,13 +27,24 @@
 namespace rtp {
 
 RT_PP_FN bool pow_int_fast(float base, int n, float* out) {
-    if (!(base > 0.0f) || !(base <= 4.0f) || n < 2 || n > 4096) return false;
+    if (n < 2 || n > 4096 || !(base <= 4.0f)) return false;
+    if (base == 0.0f) {                                    // pow(+-0, n > 0): +0, or the zero itself for odd n
+        *out = (n & 1) ? base : 0.0f;
+        return true;
+    }
+    if (!(base > 0.0f)) return false;
     double x = base, y = 1.0;
     for (int e = n; e; e >>= 1) {
         if (e & 1) y *= x;
         x *= x;
     }
-    if (!(y >= 1e-300) || !(y <= 1e300)) return false;   // double range (no subnormal error growth)
+    if (!(y >= 1e-300)) {
+        // an exact value >= 2^-151 keeps every factor x^k (k <= n) >= 2^-151, far above the
+        // double subnormals, so y would be within the error bound of it; hence the exact
+        // value (and glibc's) is below 2^-151 and rounds to +0 as a float
+        *out = 0.0f;
+        return true;
+    }
     const float f = (float)y;
     const float up = std::nextafter(f, FLT_MAX * 2.0f), dn = std::nextafter(f, -1.0f);
     if (!(up <= FLT_MAX)) return false;                    // f or its neighbour is not finite

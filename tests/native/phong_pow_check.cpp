@@ -23,6 +23,9 @@ int main(int argc, char** argv) {
             }
             if (i == 0) b = 0.0f;
             if (i == 1) b = 1.0f;
+            if (i == 2) b = -0.0f;
+            if (i % 16 == 3) b = 0.0f;                 // smax(0, n.h) clamps often
+            if (i % 16 == 5) b = (float)((double)(r >> 11) * 0x1p-53 * 0.01);   // tiny results (underflow)
             const float want = (float)std::pow((double)b, (double)p);
             float got = rtp::phong_pow(b, p), f;
             if (p != 1.0f && (float)(int)p == p && rtp::pow_int_fast(b, (int)p, &f)) ++fast;
