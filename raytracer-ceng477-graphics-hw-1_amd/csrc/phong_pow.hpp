@@ -56,12 +56,23 @@ RT_PP_FN bool pow_int_fast(float base, int n, float* out) {
     return true;
 }
 
+// The full double pow, out of line on the device: it needs ~55 more VGPRs than
+// the shading kernels' own code and is taken only in rare cases.
+#if defined(__HIPCC__)
+inline __host__ __device__ __attribute__((noinline))
+#else
+inline
+#endif
+float pow_full(float base, float phong) {
+    return (float)std::pow((double)base, (double)phong);
+}
+
 RT_PP_FN float phong_pow(float base, float phong) {
     if (phong == 1.0f) return base;   // glibc pow(x, 1) is x
     const int n = (int)phong;
     float f;
     if (phong >= 2.0f && phong <= 4096.0f && (float)n == phong && pow_int_fast(base, n, &f)) return f;
-    return (float)std::pow((double)base, (double)phong);
+    return pow_full(base, phong);
 }
 
 }  // namespace rtp
