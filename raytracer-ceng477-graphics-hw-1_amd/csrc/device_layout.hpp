@@ -67,9 +67,10 @@ struct LeafBig { int32_t start, count; };
 
 // Occlusion tree node, 4-wide, 64 B (four dwordx4 loads test four children):
 //   {origin.xyz, exps}  exps = ex | ey << 8 | ez << 16 | nchild << 24, scale_a = 2^(e_a - 127)
-//   {qlo[4][3] bytes, qhi[4][3] bytes}          child c box, axis a:
-//       lo = origin_a + qlo[c][a] * scale_a,  hi = origin_a + qhi[c][a] * scale_a  (float, exact
-//       power-of-two scale; the host verifies every decoded box CONTAINS the child's exact box)
+//   {qlo[3][4] bytes, qhi[3][4] bytes}          axis-major: dword a = axis a's byte of children 0..3
+//       lo = origin_a + qlo[a][c] * scale_a,  hi = origin_a + qhi[a][c] * scale_a  (float, exact
+//       power-of-two scale; the host verifies every decoded box CONTAINS the child's exact box);
+//       a ray picks its near/far plane per axis by swapping whole dwords
 //   {child[4]}  >= 0: quad index; < 0: kLeafBit | offset of a leaf record (16-B units) in LeafRec[]
 //   {pad[2]}
 // Leaves are the reference BVH's leaves.  A leaf record is the leaf's header
@@ -79,7 +80,7 @@ struct LeafBig { int32_t start, count; };
 //   count x Prim (48 B, same encoding and order as Prim[])
 struct alignas(16) Quad {
     float ox, oy, oz; uint32_t exps;
-    uint32_t q[6];        // bytes: qlo c0..c3 x,y,z (12), then qhi c0..c3 x,y,z (12)
+    uint32_t q[6];        // qlo x,y,z dwords (children 0..3 in bytes 0..3), then qhi x,y,z
     int32_t child[4];
     int32_t pad[2];
 };

@@ -969,7 +969,7 @@ void build_shadow_tree(FlatBVH& out, int threads) {
         q.exps = (uint32_t)e[0] | (uint32_t)e[1] << 8 | (uint32_t)e[2] << 16 | (uint32_t)ch.size() << 24;
         uint8_t bytes[24];
         for (int i = 0; i < 4; ++i)
-            for (int a = 0; a < 3; ++a) { bytes[i * 3 + a] = ql[i][a]; bytes[12 + i * 3 + a] = qh[i][a]; }
+            for (int a = 0; a < 3; ++a) { bytes[a * 4 + i] = ql[i][a]; bytes[12 + a * 4 + i] = qh[i][a]; }
         std::memcpy(q.q, bytes, 24);
         for (int i = 0; i < 4; ++i) q.child[i] = codes[i];
         out.quads[me] = q;

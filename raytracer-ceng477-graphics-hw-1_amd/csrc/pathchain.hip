@@ -899,13 +899,12 @@ __device__ __forceinline__ bool quad4_step(const rtk::DevScene& s, const Ray& r,
         const float4 q0 = Q[0], q1 = Q[1], q2 = Q[2], q3 = Q[3];
         const uint32_t ex = __float_as_uint(q0.w);
         const int n = (int)(ex >> 24);
-        // this lane's 3 lo bytes (3q..3q+2 of q1.xyz) and 3 hi bytes (3q..3q+2 of q1.w q2.x q2.y)
-        const uint64_t l01 = (uint64_t)__float_as_uint(q1.x) | ((uint64_t)__float_as_uint(q1.y) << 32);
-        const uint64_t l12 = (uint64_t)__float_as_uint(q1.y) | ((uint64_t)__float_as_uint(q1.z) << 32);
-        const uint64_t h01 = (uint64_t)__float_as_uint(q1.w) | ((uint64_t)__float_as_uint(q2.x) << 32);
-        const uint64_t h12 = (uint64_t)__float_as_uint(q2.x) | ((uint64_t)__float_as_uint(q2.y) << 32);
-        const uint32_t lb = (uint32_t)(q < 2 ? l01 >> (24 * q) : l12 >> (24 * q - 32));
-        const uint32_t hb = (uint32_t)(q < 2 ? h01 >> (24 * q) : h12 >> (24 * q - 32));
+        // this lane's lo and hi bytes: byte q of the axis dwords q1.xyz (lo) and q1.w q2.xy (hi)
+        const uint32_t sh = 8u * (uint32_t)q;
+        const uint32_t lb = ((__float_as_uint(q1.x) >> sh) & 255u) | (((__float_as_uint(q1.y) >> sh) & 255u) << 8) |
+                            (((__float_as_uint(q1.z) >> sh) & 255u) << 16);
+        const uint32_t hb = ((__float_as_uint(q1.w) >> sh) & 255u) | (((__float_as_uint(q2.x) >> sh) & 255u) << 8) |
+                            (((__float_as_uint(q2.y) >> sh) & 255u) << 16);
         const int code = q == 0 ? __float_as_int(q2.z) : q == 1 ? __float_as_int(q2.w)
                        : q == 2 ? __float_as_int(q3.x) : __float_as_int(q3.y);
         const float sx = __uint_as_float((ex & 255u) << 23), sy = __uint_as_float(((ex >> 8) & 255u) << 23),

@@ -377,7 +377,13 @@ __device__ __forceinline__ bool walk_restart_ref(const rtk::DevScene& s, const R
 // component, so every value equals the scalar form).  Decode:
 // origin + q * 2^e as one fma, exact because q * 2^e is exact (an 8-bit
 // integer times a power of two); the host checks containment with the same
-// fma.  Slab test: box_hit_fast's, plane by plane (p - o) * inv.
+// fma.  Slab test: box_hit_fast's, plane by plane (p - o) * inv, except that
+// the near plane of each axis is chosen up front by the sign of inv (the
+// axis's lo and hi dwords swap) instead of by a min/max per child: with o,
+// inv and the planes finite, lo <= hi gives (lo - o) * inv <= (hi - o) * inv
+// for inv > 0 and >= for inv < 0 (rounding is monotone), so the near value is
+// exactly box_hit_fast's min and the far value its max (up to the sign of a
+// zero, which no comparison sees).
 typedef float f2v __attribute__((ext_vector_type(2)));
 
 struct QuadHits {
@@ -394,38 +400,30 @@ __device__ __forceinline__ void quad_hits(const rtk::DevScene& s, int qi, const 
                          __uint_as_float(((ex >> 16) & 255u) << 23)};
     const float org[3] = {q0.x, q0.y, q0.z};
     const float ro[3] = {r.o.x, r.o.y, r.o.z}, ri[3] = {r.inv.x, r.inv.y, r.inv.z};
-    const uint32_t qb[6] = {__float_as_uint(q1.x), __float_as_uint(q1.y), __float_as_uint(q1.z),
-                            __float_as_uint(q1.w), __float_as_uint(q2.x), __float_as_uint(q2.y)};
+    const uint32_t lo_w[3] = {__float_as_uint(q1.x), __float_as_uint(q1.y), __float_as_uint(q1.z)};
+    const uint32_t hi_w[3] = {__float_as_uint(q1.w), __float_as_uint(q2.x), __float_as_uint(q2.y)};
     c.code[0] = __float_as_int(q2.z);
     c.code[1] = __float_as_int(q2.w);
     c.code[2] = __float_as_int(q3.x);
     c.code[3] = __float_as_int(q3.y);
-    auto byte = [&](int j) { return (float)((qb[j >> 2] >> ((j & 3) * 8)) & 255u); };
     float tmn[4], tmx[4];
 #pragma unroll
-    for (int pr = 0; pr < 2; ++pr) {            // children 2pr, 2pr+1
-        const int c0 = 2 * pr, c1 = 2 * pr + 1;
-        f2v lo_t[3], hi_t[3];
+    for (int a = 0; a < 3; ++a) {
+        const bool neg = __float_as_int(ri[a]) < 0;
+        const uint32_t nw = neg ? hi_w[a] : lo_w[a], fw = neg ? lo_w[a] : hi_w[a];
+        const f2v s2 = {sc[a], sc[a]}, o2 = {org[a], org[a]}, rr = {ro[a], ro[a]}, iv = {ri[a], ri[a]};
 #pragma unroll
-        for (int a = 0; a < 3; ++a) {
-            const f2v s2 = {sc[a], sc[a]}, o2 = {org[a], org[a]};
-            const f2v ql = {byte(c0 * 3 + a), byte(c1 * 3 + a)};
-            const f2v qh = {byte(12 + c0 * 3 + a), byte(12 + c1 * 3 + a)};
-            const f2v lo = __builtin_elementwise_fma(ql, s2, o2);
-            const f2v hi = __builtin_elementwise_fma(qh, s2, o2);
-            const f2v rr = {ro[a], ro[a]}, iv = {ri[a], ri[a]};
-            lo_t[a] = (lo - rr) * iv;
-            hi_t[a] = (hi - rr) * iv;
-        }
+        for (int pr = 0; pr < 2; ++pr) {            // children 2pr, 2pr+1
+            const f2v qn = {(float)((nw >> (16 * pr)) & 255u), (float)((nw >> (16 * pr + 8)) & 255u)};
+            const f2v qf = {(float)((fw >> (16 * pr)) & 255u), (float)((fw >> (16 * pr + 8)) & 255u)};
+            const f2v tn = (__builtin_elementwise_fma(qn, s2, o2) - rr) * iv;
+            const f2v tf = (__builtin_elementwise_fma(qf, s2, o2) - rr) * iv;
 #pragma unroll
-        for (int k = 0; k < 2; ++k) {
-            const int ch = 2 * pr + k;
-            const float x1 = lo_t[0][k], x2 = hi_t[0][k], y1 = lo_t[1][k], y2 = hi_t[1][k], z1 = lo_t[2][k],
-                        z2 = hi_t[2][k];
-            tmn[ch] = __builtin_fmaxf(__builtin_fmaxf(__builtin_fminf(x1, x2), __builtin_fminf(y1, y2)),
-                                      __builtin_fminf(z1, z2));
-            tmx[ch] = __builtin_fminf(__builtin_fminf(__builtin_fmaxf(x1, x2), __builtin_fmaxf(y1, y2)),
-                                      __builtin_fmaxf(z1, z2));
+            for (int k = 0; k < 2; ++k) {
+                const int ch = 2 * pr + k;
+                tmn[ch] = a == 0 ? tn[k] : __builtin_fmaxf(tmn[ch], tn[k]);
+                tmx[ch] = a == 0 ? tf[k] : __builtin_fminf(tmx[ch], tf[k]);
+            }
         }
     }
 #pragma unroll

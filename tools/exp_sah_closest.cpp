@@ -221,7 +221,7 @@ void decode_quad(const dl::Quad& q, int c, float* lo, float* hi) {
     float sc[3] = {pow2f(q.exps & 255u), pow2f((q.exps >> 8) & 255u), pow2f((q.exps >> 16) & 255u)};
     const uint8_t* b = reinterpret_cast<const uint8_t*>(q.q);
     const float o[3] = {q.ox, q.oy, q.oz};
-    for (int a = 0; a < 3; ++a) { lo[a] = o[a] + (float)b[c * 3 + a] * sc[a]; hi[a] = o[a] + (float)b[12 + c * 3 + a] * sc[a]; }
+    for (int a = 0; a < 3; ++a) { lo[a] = o[a] + (float)b[a * 4 + c] * sc[a]; hi[a] = o[a] + (float)b[12 + a * 4 + c] * sc[a]; }
 }
 int closest_quad(const Ray& r, Hit* out) {
     Hit h{-1.0f, -1, 0};
