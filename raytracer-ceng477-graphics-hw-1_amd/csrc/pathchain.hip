@@ -790,7 +790,9 @@ __device__ void chain_body(const rtk::DevScene& s, const rtk::Eye& e, const PcPa
         }
         while (true) {
             const int nt = __popcll(__ballot(st == kTrav));
-            if (nt <= thresh || __popcll(__ballot(st == kDone)) >= (CONT ? p.bservice : p.service)) break;
+            if (nt <= thresh ||
+                __popcll(__ballot(st == kDone)) >= (CONT ? (exhausted ? p.btail : p.bservice) : p.service))
+                break;
             if (WIDE && !COUNT && p.wide > 0 && nt <= p.wide &&
                 __ballot(st == kTrav && !nowide && (wsteps < 0 || wsteps >= p.wide_min)))
                 break;

@@ -75,6 +75,7 @@ struct PcParams {
     int bprio;        // 1: phase-B chain waves run at the highest issue priority
     int service;      // ... or once >= service of its lanes finished a walk (epilogue, next bounce)
     int bservice;     // the same for phase-B chains
+    int btail;        // phase-B chains once no continuation is left to take: service at this many done lanes
     int quad4;        // 1: phase-B chains walk with 4 lanes per ray (chain4_body)
     int bq_cap;       // phase-B workgroup shadow queue slots in use (<= kBq; 0: every task to k_occlude)
     int spread;       // tiles interleaved per wave within a 256-sample unit (1, 2 or 4)

@@ -124,6 +124,7 @@ struct rt_scene {
     int tune_bq_cap = 1 << 30;  // RT_BQ_CAP: phase-B shadow queue slots (tests force the k_occlude spill path)
     int tune_quad4 = 0;         // RT_QUAD4: phase-B chains with 4 lanes per ray (measured slower: 1.71 vs 1.20 ms)
     int tune_bservice = 64;     // RT_BSERVICE: phase-B waves service finished walks once this many lanes are done
+    int tune_btail = 64;        // RT_BTAIL: the same once the continuations are exhausted (1: 1.24, 4: 1.18, 16: 1.15, 64: 1.14 ms)
     int tune_split = 1;         // RT_SPLIT: a frame runs as this many concurrent interleaved sub-frames (2: +8%, 3: +18% on C3)
     std::string trace_file;     // RT_TRACE: dump per-sample wall-clock timings after each render (diagnostics)
     unsigned* d_trace = nullptr;
@@ -266,6 +267,7 @@ int finish_scene(rt_scene* s, const rt_options* opts) {
     if (const char* e = std::getenv("RT_BQ_CAP")) s->tune_bq_cap = std::max(0, std::atoi(e));
     if (const char* e = std::getenv("RT_QUAD4")) s->tune_quad4 = std::atoi(e) != 0;
     if (const char* e = std::getenv("RT_BSERVICE")) s->tune_bservice = std::max(1, std::min(64, std::atoi(e)));
+    if (const char* e = std::getenv("RT_BTAIL")) s->tune_btail = std::max(1, std::min(64, std::atoi(e)));
     if (const char* e = std::getenv("RT_SPLIT")) s->tune_split = std::max(1, std::atoi(e));
     if (const char* e = std::getenv("RT_PROD")) s->tune_producers = std::max(1, std::min(4, std::atoi(e)));
     if (const char* e = std::getenv("RT_CREFILL")) s->tune_crefill = std::max(0, std::min(63, std::atoi(e)));
@@ -548,6 +550,7 @@ int render_chain(rt_scene* s, const rtk::Eye& eye, const rtk::FrameParams& f, bo
     p.refill = s->tune_refill >= 0 ? s->tune_refill : 0;
     p.service = s->tune_service >= 0 ? s->tune_service : 64;
     p.bservice = s->tune_bservice;
+    p.btail = s->tune_btail;
     p.quad4 = s->tune_quad4 && !s->bvh.quads.empty();
     p.bq_cap = std::min(s->tune_bq_cap, rtc::kMaxBq);
     p.producers = s->tune_producers;
