@@ -33,7 +33,7 @@
 extern "C" {
 #endif
 
-#define RT_ABI_VERSION 2
+#define RT_ABI_VERSION 3
 
 typedef enum rt_status {
     RT_OK = 0,
@@ -178,6 +178,17 @@ int rt_render_device(rt_scene* scene, const rt_camera* cam, int aa_factor,
  * rt_render of that camera.  (ABI 2) */
 int rt_render_cameras_device(rt_scene* scene, const rt_camera* cams, int n, int aa_factor,
                              void* const* outs_dev, void* stream, int flags);
+/* Sharded frame batch (ABI 3): rank `rank` of `nranks` renders its row
+ * stripes (as rt_render_device) of n frames, the frames in flight together
+ * exactly as in rt_render_cameras_device (each frame's slow mirror-chain tail
+ * overlaps the other frames' bulk).  outs_dev[i] holds cams[i]'s slab,
+ * rt_slab_rows(H, stripe_rows, nranks) * W * 3 bytes, identical to
+ * rt_render_device of that camera.  The frame-sequence form of the
+ * reference's per-camera render loop (raytracer.cpp:505-519) for a
+ * multi-GPU serving loop. */
+int rt_render_frames_device(rt_scene* scene, const rt_camera* cams, int n, int aa_factor,
+                            int stripe_rows, int rank, int nranks,
+                            void* const* outs_dev, void* stream, int flags);
 /* The same into caller-allocated host buffers, synchronous (the drop-in main's
  * camera loop).  stats (nullable) sums the work counters over the cameras. */
 int rt_render_cameras(rt_scene* scene, const rt_camera* cams, int n, int aa_factor,

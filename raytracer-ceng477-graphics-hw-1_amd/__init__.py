@@ -101,6 +101,8 @@ _SIGS = [
                                          ctypes.POINTER(Stats)]),
     ("rt_render_cameras_device", ctypes.c_int, [_P, ctypes.POINTER(Camera), ctypes.c_int, ctypes.c_int, _P, _P,
                                                 ctypes.c_int]),
+    ("rt_render_frames_device", ctypes.c_int, [_P, ctypes.POINTER(Camera), ctypes.c_int, ctypes.c_int, ctypes.c_int,
+                                               ctypes.c_int, ctypes.c_int, _P, _P, ctypes.c_int]),
     ("rt_walk_timing", ctypes.c_int, [_P, _P, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int, _P]),
     ("rt_slab_rows", ctypes.c_int, [ctypes.c_int, ctypes.c_int, ctypes.c_int]),
     ("rt_unshuffle_stripes", ctypes.c_int, [_P, _P, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int, _P]),
@@ -231,6 +233,16 @@ class Scene:
         ptrs = (ctypes.c_void_p * n)(*out_ptrs)
         _check(lib().rt_render_cameras_device(self._h, arr, n, aa, ptrs, ctypes.c_void_p(stream),
                                               RT_RENDER_COUNT if count else 0))
+
+    def render_frames_device(self, cams: list, aa: int, out_ptrs: list, stream: int = 0, stripe_rows: int = 8,
+                             rank: int = 0, nranks: int = 1, count: bool = False) -> None:
+        """Asynchronous render of this rank's stripes of several frames, in flight together
+        (rt_render_frames_device); out_ptrs[i] receives frame i's slab, as render_device would."""
+        n = len(cams)
+        arr = (Camera * n)(*cams)
+        ptrs = (ctypes.c_void_p * n)(*out_ptrs)
+        _check(lib().rt_render_frames_device(self._h, arr, n, aa, stripe_rows, rank, nranks, ptrs,
+                                             ctypes.c_void_p(stream), RT_RENDER_COUNT if count else 0))
 
     def walk_timing(self, rays, lanes: int = 1, reps: int = 3, mode: int = 0) -> np.ndarray:
         """Diagnostics (rt_walk_timing): rows {cycles, steps, prim, first-rep cycles} per ray."""

@@ -1634,8 +1634,10 @@ __global__ __launch_bounds__(kBlock) void k_compose(rtk::DevScene s, PcParams p)
         const int rr = q / p.width, ocol = q - rr * p.width;
         const int lr = lr0 + rr;
         if (lr >= p.slab_rows) continue;
-        const int stripe = lr / p.stripe_rows;
-        const int g = (stripe * p.nranks + p.rank) * p.stripe_rows + (lr - stripe * p.stripe_rows);
+        int lf = lr;
+        const int fr = batch_frame(p, &lf);
+        const int stripe = lf / p.stripe_rows;
+        const int g = (stripe * p.nranks + p.rank) * p.stripe_rows + (lf - stripe * p.stripe_rows);
         if (g >= p.height) continue;
         uint32_t sr = 0, sg = 0, sb = 0;
         for (int k = 0; k < F; ++k)
@@ -1644,7 +1646,7 @@ __global__ __launch_bounds__(kBlock) void k_compose(rtk::DevScene s, PcParams p)
                 sr += quantise(c.x); sg += quantise(c.y); sb += quantise(c.z);
             }
         const uint32_t ff = (uint32_t)(F * F);
-        uint8_t* o = p.out + ((size_t)out_row(p, lr) * p.width + ocol) * 3;
+        uint8_t* o = (p.nframes > 1 ? p.fouts[fr] : p.out) + ((size_t)out_row(p, lf) * p.width + ocol) * 3;
         o[0] = (uint8_t)(sr / ff); o[1] = (uint8_t)(sg / ff); o[2] = (uint8_t)(sb / ff);
     }
 }
@@ -1791,8 +1793,10 @@ __device__ __forceinline__ void finish_pixels(const rtk::DevScene& s, const PcPa
         const int rr = q / p.width, ocol = q - rr * p.width;
         const int lr = lr0 + rr;
         if (lr >= p.slab_rows) continue;
-        const int stripe = lr / p.stripe_rows;
-        const int g = (stripe * p.nranks + p.rank) * p.stripe_rows + (lr - stripe * p.stripe_rows);
+        int lf = lr;
+        const int fr = batch_frame(p, &lf);
+        const int stripe = lf / p.stripe_rows;
+        const int g = (stripe * p.nranks + p.rank) * p.stripe_rows + (lf - stripe * p.stripe_rows);
         if (g >= p.height) continue;
         uint32_t sr = 0, sg = 0, sb = 0;
         for (int k = 0; k < F; ++k)
@@ -1801,7 +1805,7 @@ __device__ __forceinline__ void finish_pixels(const rtk::DevScene& s, const PcPa
                 sr += quantise(c.x); sg += quantise(c.y); sb += quantise(c.z);
             }
         const uint32_t ff = (uint32_t)(F * F);
-        uint8_t* o = p.out + ((size_t)out_row(p, lr) * p.width + ocol) * 3;
+        uint8_t* o = (p.nframes > 1 ? p.fouts[fr] : p.out) + ((size_t)out_row(p, lf) * p.width + ocol) * 3;
         o[0] = (uint8_t)(sr / ff); o[1] = (uint8_t)(sg / ff); o[2] = (uint8_t)(sb / ff);
     }
 }

@@ -26,6 +26,7 @@
 namespace rtc {
 
 constexpr int kMaxChainGrid = 2048;   // k_chain workgroups (= task-queue regions)
+constexpr int kMaxFrames = 16;        // frames of one batched launch (rt_render_frames_device)
 #ifndef RT_BQ
 #define RT_BQ 1536
 #endif
@@ -82,6 +83,11 @@ struct PcParams {
     int wide;         // wide (whole-wave) walks when <= wide lanes of a wave still walk; 0 = off
     int wide_min;     // ... and the walk already took >= wide_min narrow steps
     uint8_t* out;
+    // Frame batch: the slab's rows are nframes frames of frame_rows rows each (slab_rows = nframes *
+    // frame_rows); frame f's samples use eyes[f] and its pixels go to fouts[f] (nframes > 1 only).
+    int nframes, frame_rows;
+    rtk::Eye eyes[kMaxFrames];
+    uint8_t* fouts[kMaxFrames];
     int out_k, out_j;   // sub-frame j of k interleaved sub-frames (out_row); 1, 0 for a whole frame
     unsigned long long* counters;
     unsigned* wq;     // k_fused: per-wave task queues, [grid*4][wq_cap] u32 shadow-task owner ids

@@ -69,6 +69,11 @@ struct FrameParams {
     int out_k = 1, out_j = 0;   // chain path: sub-frame j of out_k interleaved sub-frames (pathchain.hip out_row)
     unsigned long long* counters;  // 6 x u64 (RT_RENDER_COUNT)
     unsigned* trace;      // diagnostics (RT_TRACE): per output pixel {wave start, pixel end} wall clock, or null
+    // chain path, frame batches (rt_render_frames_device): slab_rows = nframes * frame_rows virtual
+    // rows, frame f's rows rendered with eyes[f] into outs[f] (host arrays of nframes entries)
+    int nframes = 1, frame_rows = 0;
+    const Eye* eyes = nullptr;
+    uint8_t* const* outs = nullptr;
 };
 
 size_t render_lds_bytes(const DevScene& s);

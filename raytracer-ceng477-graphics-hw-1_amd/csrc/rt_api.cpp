@@ -120,6 +120,7 @@ struct rt_scene {
     int tune_wide = 0;          // RT_WIDE
     int tune_wide_min = 24;     // RT_WIDE_MIN
     int tune_kinline = 1;       // RT_KINLINE: deepest level of phase A
+    int tune_batch = 16;        // RT_BATCH: frames per batched launch (rt_render_frames/cameras; 1 = off)
     int tune_gb = 0;            // RT_GB: phase-B chain workgroups in k_mix (0 = 1.5625 per CU: 384-416 best of 256-1024 on C3)
     int tune_bq_cap = 1 << 30;  // RT_BQ_CAP: phase-B shadow queue slots (tests force the k_occlude spill path)
     int tune_quad4 = 0;         // RT_QUAD4: phase-B chains with 4 lanes per ray (measured slower: 1.71 vs 1.20 ms)
@@ -262,6 +263,7 @@ int finish_scene(rt_scene* s, const rt_options* opts) {
     if (const char* e = std::getenv("RT_OREFILL")) s->tune_orefill = std::max(0, std::min(63, std::atoi(e)));
     if (const char* e = std::getenv("RT_WIDE")) s->tune_wide = std::max(0, std::min(64, std::atoi(e)));
     if (const char* e = std::getenv("RT_WIDE_MIN")) s->tune_wide_min = std::max(0, std::atoi(e));
+    if (const char* e = std::getenv("RT_BATCH")) s->tune_batch = std::max(1, std::atoi(e));
     if (const char* e = std::getenv("RT_KINLINE")) s->tune_kinline = std::max(0, std::atoi(e));
     if (const char* e = std::getenv("RT_GB")) s->tune_gb = std::max(0, std::atoi(e));
     if (const char* e = std::getenv("RT_BQ_CAP")) s->tune_bq_cap = std::max(0, std::atoi(e));
@@ -569,6 +571,15 @@ int render_chain(rt_scene* s, const rtk::Eye& eye, const rtk::FrameParams& f, bo
     p.wq_cap = wq_cap;
     p.out = f.out; p.counters = f.counters;
     p.out_k = f.out_k; p.out_j = f.out_j;
+    p.nframes = std::max(1, f.nframes);
+    p.frame_rows = p.nframes > 1 ? f.frame_rows : f.slab_rows;
+    if (p.nframes > rtc::kMaxFrames || (p.nframes > 1 && (!f.eyes || !f.outs || f.out_k != 1 ||
+                                                          f.frame_rows * p.nframes != f.slab_rows)))
+        return fail(RT_ERR_LIMIT, "internal: bad frame batch");
+    for (int i = 0; i < rtc::kMaxFrames; ++i) {
+        p.eyes[i] = i < p.nframes && p.nframes > 1 ? f.eyes[i] : eye;
+        p.fouts[i] = i < p.nframes && p.nframes > 1 ? f.outs[i] : f.out;
+    }
     const size_t trace_n = 2 * (cap + (size_t)std::max(s->mix_grid, s->occl_grid));
     p.trace = trace_buffer(s, trace_n);
     for (int r0 = 0; r0 < li; r0 += chunk_rows) {
@@ -815,12 +826,87 @@ int rt_render_device(rt_scene* s, const rt_camera* cam, int aa, int stripe_rows,
 // workspace), forked from and joined back into `stream`.  Each frame's tail
 // (its few long mirror chains) overlaps the other frames' bulk.  The chain
 // path runs the slots concurrently; the other paths render one after another.
+// Frame batch: n frames of one size (rank `rank`'s stripes of each) as ONE
+// chain-path launch sequence.  The frames' samples form one virtual slab of
+// n * slab_rows rows (pathchain.hpp PcParams.nframes): one persistent grid
+// walks them all, so one frame's slow mirror-chain tail runs beside the other
+// frames' bulk instead of after it.
+int render_batch(rt_scene* s, const rt_camera* cams, int n, int aa, int stripe_rows, int rank, int nranks,
+                 void* const* outs_dev, hipStream_t stream, int flags, int slot) {
+    if (n == 1)
+        return render_frame(s, cams, aa, stripe_rows, rank, nranks, outs_dev[0], stream, flags, slot);
+    if (n > rtc::kMaxFrames) return fail(RT_ERR_LIMIT, "internal: frame batch too large");
+    if (stripe_rows < 1 || nranks < 1 || rank < 0 || rank >= nranks) return fail(RT_ERR_ARG, "bad stripe/rank");
+    HIP_TRY(hipSetDevice(s->device));
+    rtk::Eye eyes[rtc::kMaxFrames];
+    for (int i = 0; i < n; ++i) eyes[i] = make_eye(cams[i], cams[i].image_width * aa, cams[i].image_height * aa);
+    rtk::FrameParams p;
+    p.width = cams[0].image_width;
+    p.height = cams[0].image_height;
+    p.aa = aa;
+    p.stripe_rows = stripe_rows;
+    p.rank = rank;
+    p.nranks = nranks;
+    p.frame_rows = rt_slab_rows(p.height, stripe_rows, nranks);
+    p.nframes = n;
+    p.slab_rows = p.frame_rows * n;
+    p.eyes = eyes;
+    p.outs = reinterpret_cast<uint8_t* const*>(outs_dev);
+    p.out = static_cast<uint8_t*>(outs_dev[0]);
+    p.counters = s->d_counters;
+    p.trace = nullptr;
+    return render_chain(s, eyes[0], p, (flags & RT_RENDER_COUNT) != 0, stream, slot);
+}
+
+// stripe_rows <= 0: whole frames (each camera's own height); otherwise every
+// frame is this rank's row stripes (rt_render_frames_device).
 int render_cameras(rt_scene* s, const rt_camera* cams, int n, int aa, void* const* outs_dev, hipStream_t stream,
-                   int flags) {
+                   int flags, int stripe_rows = 0, int rank = 0, int nranks = 1) {
+    auto rows_of = [&](int i) { return stripe_rows > 0 ? stripe_rows : cams[i].image_height; };
+    const bool batching = (s->path == rt_scene::kChain || s->path == rt_scene::kFused) && n > 1 &&
+                          s->tune_batch > 1;
+    if (batching) {
+        // consecutive same-size frames, up to kMaxFrames and one chain chunk of samples per batch
+        std::vector<int> starts;
+        for (int i = 0; i < n;) {
+            const auto& c = cams[i];
+            const long long per = (long long)rt_slab_rows(c.image_height, rows_of(i), nranks) * aa *
+                                  ((long long)c.image_width * aa);
+            int j = i + 1;
+            while (j < n && j - i < std::min(s->tune_batch, rtc::kMaxFrames) &&
+                   cams[j].image_width == c.image_width && cams[j].image_height == c.image_height &&
+                   (long long)(j - i + 1) * per <= (long long)kChainTargetSamples)
+                ++j;
+            starts.push_back(i);
+            i = j;
+        }
+        starts.push_back(n);
+        const int nb = (int)starts.size() - 1;
+        if (nb == 1) return render_batch(s, cams, n, aa, rows_of(0), rank, nranks, outs_dev, stream, flags, 0);
+        if (!s->fork_ev) HIP_TRY(hipEventCreateWithFlags(&s->fork_ev, hipEventDisableTiming));
+        HIP_TRY(hipEventRecord(s->fork_ev, stream));
+        const int used = std::min(nb, rt_scene::kSlots);
+        for (int k = 0; k < used; ++k) {
+            if (!s->slot_stream[k]) HIP_TRY(hipStreamCreateWithFlags(&s->slot_stream[k], hipStreamNonBlocking));
+            if (!s->slot_done[k]) HIP_TRY(hipEventCreateWithFlags(&s->slot_done[k], hipEventDisableTiming));
+            HIP_TRY(hipStreamWaitEvent(s->slot_stream[k], s->fork_ev, 0));
+        }
+        for (int b = 0; b < nb; ++b) {
+            const int k = b % rt_scene::kSlots, i = starts[b];
+            const int rc = render_batch(s, cams + i, starts[b + 1] - i, aa, rows_of(i), rank, nranks, outs_dev + i,
+                                        s->slot_stream[k], flags, k);
+            if (rc) return rc;
+        }
+        for (int k = 0; k < used; ++k) {
+            HIP_TRY(hipEventRecord(s->slot_done[k], s->slot_stream[k]));
+            HIP_TRY(hipStreamWaitEvent(stream, s->slot_done[k], 0));
+        }
+        return RT_OK;
+    }
     const bool conc = s->path == rt_scene::kChain && n > 1;
     if (!conc) {
         for (int i = 0; i < n; ++i) {
-            const int rc = render_frame(s, &cams[i], aa, cams[i].image_height, 0, 1, outs_dev[i], stream, flags, 0);
+            const int rc = render_frame(s, &cams[i], aa, rows_of(i), rank, nranks, outs_dev[i], stream, flags, 0);
             if (rc) return rc;
         }
         return RT_OK;
@@ -835,7 +921,7 @@ int render_cameras(rt_scene* s, const rt_camera* cams, int n, int aa, void* cons
     }
     for (int i = 0; i < n; ++i) {
         const int k = i % rt_scene::kSlots;
-        const int rc = render_frame(s, &cams[i], aa, cams[i].image_height, 0, 1, outs_dev[i], s->slot_stream[k],
+        const int rc = render_frame(s, &cams[i], aa, rows_of(i), rank, nranks, outs_dev[i], s->slot_stream[k],
                                     flags, k);
         if (rc) return rc;
     }
@@ -857,6 +943,21 @@ int rt_render_cameras_device(rt_scene* s, const rt_camera* cams, int n, int aa, 
     }
     HIP_TRY(hipSetDevice(s->device));
     return render_cameras(s, cams, n, aa, outs_dev, static_cast<hipStream_t>(stream), flags);
+}
+
+int rt_render_frames_device(rt_scene* s, const rt_camera* cams, int n, int aa, int stripe_rows, int rank,
+                            int nranks, void* const* outs_dev, void* stream, int flags) {
+    if (!s || !cams || !outs_dev || n < 1) return fail(RT_ERR_ARG, "scene/cameras/outputs is NULL or n < 1");
+    if (s->host_only) return fail(RT_ERR_NO_DEVICE, "scene was created with RT_OPT_HOST_ONLY");
+    if (stripe_rows < 1 || nranks < 1 || rank < 0 || rank >= nranks) return fail(RT_ERR_ARG, "bad stripe/rank");
+    for (int i = 0; i < n; ++i) {
+        const int rc = check_camera(&cams[i], aa);
+        if (rc) return rc;
+        if (!outs_dev[i]) return fail(RT_ERR_ARG, "output buffer is NULL");
+    }
+    HIP_TRY(hipSetDevice(s->device));
+    return render_cameras(s, cams, n, aa, outs_dev, static_cast<hipStream_t>(stream), flags, stripe_rows, rank,
+                          nranks);
 }
 
 int rt_render_cameras(rt_scene* s, const rt_camera* cams, int n, int aa, uint8_t* const* outs, rt_stats* stats) {

@@ -35,10 +35,19 @@ __device__ __forceinline__ void wave_add_counter(unsigned long long* c, unsigned
     if ((threadIdx.x & 63) == 0 && v) atomicAdd(c, v);
 }
 
+// Frame batches: virtual slab row lr -> frame index, *lr -> that frame's slab row.
+template <class P>
+__device__ __forceinline__ int batch_frame(const P& p, int* lr) {
+    if (p.nframes <= 1) return 0;
+    const int f = *lr / p.frame_rows;
+    *lr -= f * p.frame_rows;
+    return f;
+}
+
 // Slab-local sample slot -> eye ray.  Slots are ordered by 8x8 internal-pixel
 // tiles (one tile per wave) for ray coherence; slab rows map to global rows
 // through the stripe round-robin.  P needs: wi tiles_x chunk_row0 chunk_rows
-// aa slab_rows stripe_rows nranks rank height.
+// aa slab_rows stripe_rows nranks rank height nframes frame_rows eyes.
 template <class P>
 __device__ __forceinline__ bool slab_sample_ray(const rtk::Eye& e, const P& p, unsigned s, Ray* r) {
     const unsigned tile = s >> 6, lane = s & 63;
@@ -47,12 +56,14 @@ __device__ __forceinline__ bool slab_sample_ray(const rtk::Eye& e, const P& p, u
     const int iyc = ty * 8 + (int)(lane >> 3);
     if (ix >= p.wi || iyc >= p.chunk_rows) return false;
     const int iy = p.chunk_row0 + iyc;
-    const int lr = iy / p.aa, sub = iy - lr * p.aa;
+    int lr = iy / p.aa;
+    const int sub = iy - lr * p.aa;
     if (lr >= p.slab_rows) return false;
+    const int f = batch_frame(p, &lr);
     const int stripe = lr / p.stripe_rows;
     const int g = (stripe * p.nranks + p.rank) * p.stripe_rows + (lr - stripe * p.stripe_rows);
     if (g >= p.height) return false;
-    *r = eye_ray(e, g * p.aa + sub, ix);
+    *r = eye_ray(p.nframes > 1 ? p.eyes[f] : e, g * p.aa + sub, ix);
     return true;
 }
 
@@ -64,8 +75,9 @@ __device__ __forceinline__ bool slab_slot_valid(const P& p, unsigned s) {
     const int ix = tx * 8 + (int)(lane & 7);
     const int iyc = ty * 8 + (int)(lane >> 3);
     if (ix >= p.wi || iyc >= p.chunk_rows) return false;
-    const int lr = (p.chunk_row0 + iyc) / p.aa;
+    int lr = (p.chunk_row0 + iyc) / p.aa;
     if (lr >= p.slab_rows) return false;
+    batch_frame(p, &lr);
     const int stripe = lr / p.stripe_rows;
     return (stripe * p.nranks + p.rank) * p.stripe_rows + (lr - stripe * p.stripe_rows) < p.height;
 }

@@ -188,7 +188,7 @@ def test_full_size_c5_sha(name, path, goldens, pkg, scene_dir, torch_cuda):
     assert _stats(st) == _counters(cam_g["counters"])
 
 
-@pytest.mark.parametrize("path", ["chain", "megakernel"])
+@pytest.mark.parametrize("path", ["chain", "fused", "megakernel"])
 @pytest.mark.parametrize("name", ["cornellbox_aa1", "car_aa1", "hm_verbatim_aa2"])
 def test_render_cameras_batched(name, path, goldens, pkg, scene_dir, torch_cuda):
     # (f4) multi-camera batching (raytracer.cpp:505-519): every camera of the scene in one call,
@@ -208,6 +208,68 @@ def test_render_cameras_batched(name, path, goldens, pkg, scene_dir, torch_cuda)
         imgs2, _ = s.render_cameras(many, aa=g["aa"])
         for i, img in enumerate(imgs2):
             assert np.array_equal(img, load_golden_image(g["cameras"][i % len(sel)]))
+
+
+@pytest.mark.parametrize("batch", ["16", "1"])
+@pytest.mark.parametrize("path", ["chain", "fused"])
+@pytest.mark.parametrize("nranks,nframes,gname", [(1, 2, "C3_hm_1080p_d6_aa1"), (8, 8, "C3_hm_1080p_d6_aa1"),
+                                                  (3, 5, "C3_hm_1080p_d6_aa1"), (8, 3, "C3_hm_1080p_d6_aa2"),
+                                                  (2, 17, "C3_hm_1080p_d6_aa1")])
+def test_render_frames_device_batch(nranks, nframes, gname, path, batch, goldens, pkg, scene_dir, torch_cuda,
+                                    monkeypatch):
+    """Frame batches (rt_render_frames_device, the bench's in-flight frames): every rank's stripes
+    of every frame of one batched launch equal the golden, and the work counters are exactly
+    nframes times the frame's (no frame's work is shared or skipped).  nframes 17 > kMaxFrames
+    (two batches on two slots); RT_BATCH=1: frames concurrent on slots instead of batched."""
+    torch = torch_cuda
+    monkeypatch.setenv("RT_BATCH", batch)
+    g = golden_by_name(goldens, gname)
+    ref = load_golden_image(g["cameras"][0])
+    aa, stripe = g["aa"], 8
+    with pkg.Scene.from_xml(config_path(scene_dir, g["config"]), device=0, render_path=path) as s:
+        cam = s.camera(0)
+        W, H = cam.image_width, cam.image_height
+        rows = pkg.slab_rows(H, stripe, nranks)
+        slabs = torch.zeros((nframes, nranks, rows, W, 3), dtype=torch.uint8, device="cuda:0")
+        stream = torch.cuda.current_stream().cuda_stream
+        s.counters_reset(stream)
+        for r in range(nranks):
+            s.render_frames_device([cam] * nframes, aa, [slabs[f, r].data_ptr() for f in range(nframes)], stream,
+                                   stripe_rows=stripe, rank=r, nranks=nranks, count=True)
+        cnt = s.counters_read()
+        img = torch.empty((H, W, 3), dtype=torch.uint8, device="cuda:0")
+        for f in range(nframes):
+            pkg.unshuffle_stripes(slabs[f].data_ptr(), img.data_ptr(), W, H, stripe, nranks, stream)
+            torch.cuda.synchronize()
+            assert np.array_equal(img.cpu().numpy(), ref), f"frame {f}"
+        c = g["cameras"][0]["counters"]
+        assert _stats(cnt) == tuple(nframes * x for x in _counters(c))
+
+
+@pytest.mark.parametrize("path", ["chain", "fused"])
+def test_render_frames_device_mixed_cameras(path, goldens, pkg, scene_dir, torch_cuda):
+    """One batch holding different cameras of one size (cornellbox's two 800x800 cameras),
+    split over 2 ranks: each frame uses its own eye."""
+    torch = torch_cuda
+    g = golden_by_name(goldens, "cornellbox_aa1")
+    with pkg.Scene.from_xml(config_path(scene_dir, g["config"]), device=0, render_path=path) as s:
+        order = [i for i, c in enumerate(g["cameras"]) if (c["width"], c["height"]) == (800, 800)]
+        assert len(order) == 2
+        order = order + order[::-1] + order
+        cams = [s.cameras()[g["cameras"][i]["camera"]][0] for i in order]
+        W, H = cams[0].image_width, cams[0].image_height
+        assert all((c.image_width, c.image_height) == (W, H) for c in cams)
+        rows = pkg.slab_rows(H, 8, 2)
+        slabs = torch.zeros((len(cams), 2, rows, W, 3), dtype=torch.uint8, device="cuda:0")
+        stream = torch.cuda.current_stream().cuda_stream
+        for r in range(2):
+            s.render_frames_device(cams, 1, [slabs[f, r].data_ptr() for f in range(len(cams))], stream,
+                                   stripe_rows=8, rank=r, nranks=2)
+        img = torch.empty((H, W, 3), dtype=torch.uint8, device="cuda:0")
+        for f, ci in enumerate(order):
+            pkg.unshuffle_stripes(slabs[f].data_ptr(), img.data_ptr(), W, H, 8, 2, stream)
+            torch.cuda.synchronize()
+            assert np.array_equal(img.cpu().numpy(), load_golden_image(g["cameras"][ci])), f"frame {f}"
 
 
 def test_render_cameras_device_stream(goldens, pkg, scene_dir, torch_cuda):
