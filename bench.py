@@ -4,11 +4,16 @@
 on N GPUs of one node.
 
 One "step" = one frame: every rank renders its round-robin row stripes of the
-frame into an HBM slab (one HIP megakernel launch), then for N>1 the slabs are
-gathered to rank 0 with one RCCL collective over xGMI and un-interleaved by a
-rank-0 kernel.  Inputs (scene + BVH) are resident in HBM before
-timing; the frame stays in HBM (no D2H, no write_ppm) — see DESIGN.md for the
-PCIe-inclusive figure.  Scaling is strong (the frame is fixed, split over N).
+frame into an HBM slab, then for N>1 the slabs are gathered to rank 0 with one
+RCCL collective over xGMI and un-interleaved by a rank-0 kernel.
+Frames are submitted --inflight at a time (default 16) as frame batches
+(rt_render_frames_device: one persistent grid walks several frames' samples, so
+one frame's serial mirror-chain tail runs beside the others' bulk; one gather
+per batch).  Every frame's full work is done and counted; the single-frame
+latency is reported beside `value` as config.frame_latency_ms.  Inputs (scene +
+BVH) are resident in HBM before timing; frames stay in HBM (no D2H, no
+write_ppm) — see DESIGN.md for the PCIe-inclusive figure.  Scaling is strong
+(the frame is fixed, split over N).
 
   python bench.py [--gpus N] [--steps K] [--warmup W] [--aa F] [--config C3]
   torchrun --nproc-per-node N bench.py --gpus N ...
@@ -59,6 +64,9 @@ def parse():
     ap.add_argument("--path", default="chain", choices=sorted(PATH_KERNELS), help="render path (all bit-identical)")
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="CPU baseline budget (rank 0, N=1)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--inflight", type=int, default=None,
+                    help="frames submitted together (rt_render_frames_device frame batches; 1 = one frame at a "
+                         "time; default 16, C5 1: its frames are already 250x larger than one launch's chunk)")
     return ap.parse_args()
 
 
@@ -136,12 +144,14 @@ def main() -> int:
     cam = scene.camera(0)
     W, H, S = cam.image_width, cam.image_height, a.stripe_rows
     rows = pkg.slab_rows(H, S, world)
-    slab = torch.empty((rows, W, 3), dtype=torch.uint8, device=dev)
+    F = max(1, a.inflight if a.inflight is not None else (1 if a.config == "C5" else 16))
+    slabs = torch.empty((F, rows, W, 3), dtype=torch.uint8, device=dev)
+    slab = slabs[0]
     stream = torch.cuda.current_stream(dev)
     sp = stream.cuda_stream
+    gbufs = {}
     if world > 1:
-        gbuf = torch.empty((world, rows, W, 3), dtype=torch.uint8, device=dev) if rank == 0 else None
-        image = torch.empty((H, W, 3), dtype=torch.uint8, device=dev) if rank == 0 else None
+        images = [torch.empty((H, W, 3), dtype=torch.uint8, device=dev) for _ in range(F)] if rank == 0 else None
 
         def unshuffle_dev(g, img):    # rank-0 kernel: slabs -> row order (rt_unshuffle_stripes)
             pkg.unshuffle_stripes(g.data_ptr(), img.data_ptr(), W, H, S, world, sp)
@@ -164,36 +174,57 @@ def main() -> int:
         dist.all_reduce(tot)
     ps_frame, prim_frame, shadow_frame, refl_frame = (int(x) for x in tot.tolist())
 
-    def step(ev_pair=None):
+    def step(n, ev_pair=None):
+        """n frames (steps) submitted together: this rank's stripes of each, then (N>1) one gather."""
         if ev_pair is not None:
             ev_pair[0].record(stream)
-        scene.render_device(cam, aa, slab.data_ptr(), sp, S, rank, world)
+        if n == 1:
+            scene.render_device(cam, aa, slab.data_ptr(), sp, S, rank, world)
+        else:
+            scene.render_frames_device([cam] * n, aa, [slabs[f].data_ptr() for f in range(n)], sp, S, rank, world)
         if ev_pair is not None:
             ev_pair[1].record(stream)
         if world > 1:
-            pkg.frame.assemble_frame(slab, H, S, unshuffle=unshuffle_dev, gbuf=gbuf, image=image)
+            if rank == 0 and n not in gbufs:
+                gbufs[n] = torch.empty((world, n, rows, W, 3), dtype=torch.uint8, device=dev)
+            pkg.frame.assemble_frames(slabs[:n], H, S, unshuffle=unshuffle_dev, gbuf=gbufs.get(n), images=images)
 
-    for _ in range(a.warmup):
-        step()
+    def groups(k):
+        return [min(F, k - i) for i in range(0, k, F)]
+
+    for n in groups(max(a.warmup, F)):       # at least one full group: every workspace is allocated
+        step(n)
     torch.cuda.synchronize(dev)
     note("warmup done")
-    evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(a.steps)]
+    gs = groups(a.steps)
+    evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in gs]
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize(dev)
     t0 = time.perf_counter()
-    for i in range(a.steps):
-        step(evs[i])
+    for n, ev in zip(gs, evs):
+        step(n, ev)
     torch.cuda.synchronize(dev)
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t0
     note(f"timed {a.steps} steps")
-    kern_ms = sum(e0.elapsed_time(e1) for e0, e1 in evs) / a.steps
-    tmax = torch.tensor([elapsed, kern_ms], dtype=torch.float64, device=dev)
+    kern_ms = sum(e0.elapsed_time(e1) for e0, e1 in evs) / a.steps      # render time per frame (batch-amortised)
+
+    # single-frame latency (one frame alone on the GPU, this rank's stripes; reported, not `value`)
+    lat = []
+    for _ in range(5):
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record(stream)
+        scene.render_device(cam, aa, slab.data_ptr(), sp, S, rank, world)
+        e1.record(stream)
+        torch.cuda.synchronize(dev)
+        lat.append(e0.elapsed_time(e1))
+    lat_ms = sorted(lat)[len(lat) // 2]
+    tmax = torch.tensor([elapsed, kern_ms, lat_ms], dtype=torch.float64, device=dev)
     if world > 1:
         dist.all_reduce(tmax, op=dist.ReduceOp.MAX)
-    elapsed, kern_ms_max = tmax.tolist()
+    elapsed, kern_ms_max, lat_ms = tmax.tolist()
 
     # PCIe-inclusive figure (rank 0, N=1 only; never `value`): rt_render = upload camera, render, D2H copy
     host_ms = None
@@ -224,6 +255,7 @@ def main() -> int:
             "config": {"workload": config, "description": desc, "width": W, "height": H, "aa": aa,
                        "max_recursion_depth": 6 if config != "C2_cornellbox_800_d0" else 0,
                        "parallelism": f"stripes{S}x{world}" + ("+rccl_gather" if world > 1 else ""),
+                       "frames_in_flight": F, "frame_latency_ms": round(lat_ms, 4),
                        "primary_rays": prim_frame, "shadow_rays": shadow_frame, "reflection_rays": refl_frame,
                        "mray_s_all": round((ps_frame + refl_frame) * a.steps / elapsed / 1e6, 3),
                        "scene_load_s": round(load_s, 4),
@@ -234,7 +266,9 @@ def main() -> int:
                          "frac": round(achieved / HBM_PEAK_GBPS, 4), "traffic": traffic,
                          "traffic_source": traffic_src,
                          "path": a.path, "kernels": PATH_KERNELS[a.path],
-                         "kernel": "one frame = " + " + ".join(PATH_KERNELS[a.path]), "kernel_ms": round(kern_ms, 4),
+                         "kernel": "one frame = " + " + ".join(PATH_KERNELS[a.path])
+                                   + (f" (frames in batches of up to {F}: kernel_ms = batch time / frames)" if F > 1 else ""),
+                         "kernel_ms": round(kern_ms, 4),
                          "alg_bytes_per_launch": int(alg_bytes),
                          "counts_per_launch": {k: cnt[k] for k in ("node_visits", "tri_tests", "sphere_tests")}},
         }

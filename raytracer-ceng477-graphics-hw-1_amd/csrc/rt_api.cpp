@@ -120,6 +120,7 @@ struct rt_scene {
     int tune_wide = 0;          // RT_WIDE
     int tune_wide_min = 24;     // RT_WIDE_MIN
     int tune_kinline = 1;       // RT_KINLINE: deepest level of phase A
+    size_t chunk_samples = size_t(4) << 20;   // RT_CHUNK_SAMPLES: samples per chain-path launch (chunk / batch)
     int tune_batch = 16;        // RT_BATCH: frames per batched launch (rt_render_frames/cameras; 1 = off)
     int tune_gb = 0;            // RT_GB: phase-B chain workgroups in k_mix (0 = 1.5625 per CU: 384-416 best of 256-1024 on C3)
     int tune_bq_cap = 1 << 30;  // RT_BQ_CAP: phase-B shadow queue slots (tests force the k_occlude spill path)
@@ -264,6 +265,8 @@ int finish_scene(rt_scene* s, const rt_options* opts) {
     if (const char* e = std::getenv("RT_WIDE")) s->tune_wide = std::max(0, std::min(64, std::atoi(e)));
     if (const char* e = std::getenv("RT_WIDE_MIN")) s->tune_wide_min = std::max(0, std::atoi(e));
     if (const char* e = std::getenv("RT_BATCH")) s->tune_batch = std::max(1, std::atoi(e));
+    if (const char* e = std::getenv("RT_CHUNK_SAMPLES"))
+        s->chunk_samples = std::max<size_t>(4096, std::min<size_t>(size_t(1) << 26, std::strtoull(e, nullptr, 10)));
     if (const char* e = std::getenv("RT_KINLINE")) s->tune_kinline = std::max(0, std::atoi(e));
     if (const char* e = std::getenv("RT_GB")) s->tune_gb = std::max(0, std::atoi(e));
     if (const char* e = std::getenv("RT_BQ_CAP")) s->tune_bq_cap = std::max(0, std::atoi(e));
@@ -452,8 +455,7 @@ int render_wavefront(rt_scene* s, const rtk::Eye& eye, const rtk::FrameParams& f
 
 // Chain path: chunks of whole 8*aa-row groups, workspace sized for the worst
 // case (every sample recording every level) so no queue can overflow.
-constexpr size_t kChainTargetSamples = size_t(4) << 20;
-constexpr size_t kChainBudgetBytes = size_t(6) << 30;
+constexpr size_t kChainBudgetBytes = size_t(24) << 30;   // per workspace slot (4 slots: 96 of 288 GB HBM)
 
 // Bump layout of the chain-path workspace (one device arena, grown on demand).
 struct ArenaLayout {
@@ -478,7 +480,7 @@ int render_chain(rt_scene* s, const rtk::Eye& eye, const rtk::FrameParams& f, bo
     const size_t unit_samples = (size_t)tiles_x * f.aa * 64;
     const size_t units_total = (size_t)(li + unit - 1) / unit;
     const size_t per_sample = (size_t)levels * (48 + 8 * nl + nl) + 16;
-    const size_t target = std::max<size_t>(unit_samples, std::min(kChainTargetSamples, kChainBudgetBytes / per_sample));
+    const size_t target = std::max<size_t>(unit_samples, std::min(s->chunk_samples, kChainBudgetBytes / per_sample));
     const size_t units = std::min(units_total, std::max<size_t>(1, target / unit_samples));
     const int chunk_rows = (int)units * unit;
     const size_t cap = units * unit_samples;
@@ -875,7 +877,7 @@ int render_cameras(rt_scene* s, const rt_camera* cams, int n, int aa, void* cons
             int j = i + 1;
             while (j < n && j - i < std::min(s->tune_batch, rtc::kMaxFrames) &&
                    cams[j].image_width == c.image_width && cams[j].image_height == c.image_height &&
-                   (long long)(j - i + 1) * per <= (long long)kChainTargetSamples)
+                   (long long)(j - i + 1) * per <= (long long)s->chunk_samples)
                 ++j;
             starts.push_back(i);
             i = j;

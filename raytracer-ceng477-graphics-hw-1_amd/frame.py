@@ -60,6 +60,28 @@ def assemble_frame(slab, height: int, stripe_rows: int,
     return torch.from_numpy(out)
 
 
+def assemble_frames(slabs, height: int, stripe_rows: int,
+                    unshuffle: Optional[Callable] = None, gbuf=None, images=None, dst: int = 0):
+    """A frame batch (rt_render_frames_device): every rank's (F, slab_rows, W, 3)
+    slabs -> F frames on dst, with ONE gather for the whole batch (bigger xGMI
+    messages than F gathers).  images: F (H, W, 3) device outputs for
+    `unshuffle`.  Returns the list of frames on dst, None elsewhere."""
+    import torch
+
+    g = gather_slabs(slabs, gbuf, dst)            # (nranks, F, slab_rows, W, 3)
+    if g is None:
+        return None
+    per = g.transpose(0, 1).contiguous()          # (F, nranks, slab_rows, W, 3): frame-major
+    out = []
+    for f in range(per.shape[0]):
+        if unshuffle is not None:
+            unshuffle(per[f], images[f])
+            out.append(images[f])
+        else:
+            out.append(torch.from_numpy(stripes.unshuffle(per[f].cpu().numpy(), height, stripe_rows)))
+    return out
+
+
 # ---------------------------------------------------------------------------
 # Multi-camera batching across GPUs (SURVEY.md §8f row 4; raytracer.cpp:505-519
 # renders the scene's cameras one after another): camera i is rendered by rank

@@ -59,12 +59,18 @@ def _rank_main(rank, world, port, xml, stripe_rows, aa, out_json):
             lr += n
         sc.close()
         frame = pkg.frame.assemble_frame(torch.from_numpy(slab), H, stripe_rows)
+        # a 3-frame batch (bench --inflight): frames slab, 255 - slab, slab in one gather
+        batch = torch.from_numpy(np.stack([slab, 255 - slab, slab]))
+        frames = pkg.frame.assemble_frames(batch, H, stripe_rows)
         if rank == 0:
             arr = frame.numpy()
+            sha = lambda a: hashlib.sha256(a.tobytes()).hexdigest()  # noqa: E731
             with open(out_json, "w") as f:
-                json.dump({"shape": list(arr.shape), "sha256": hashlib.sha256(arr.tobytes()).hexdigest()}, f)
+                json.dump({"shape": list(arr.shape), "sha256": sha(arr),
+                           "batch": [sha(frames[0].numpy()), sha(255 - frames[1].numpy()), sha(frames[2].numpy())]},
+                          f)
         else:
-            assert frame is None
+            assert frame is None and frames is None
         dist.barrier()
     finally:
         dist.destroy_process_group()
@@ -81,6 +87,7 @@ def test_gloo_stripes_gather_bit_exact(world, stripe_rows, goldens, scene_dir, t
     res = json.loads(out.read_text())
     assert res["shape"] == [cam["height"], cam["width"], 3]
     assert res["sha256"] == cam["sha256_rgb"]
+    assert res["batch"] == [cam["sha256_rgb"]] * 3
 
 
 def test_gather_single_rank_is_identity(pkg):
