@@ -125,11 +125,29 @@ def main() -> int:
         if world == 1 and a.gpus > 1:
             print(f"--gpus {a.gpus} needs torchrun --nproc-per-node {a.gpus}", file=sys.stderr)
             return 2
+    # RT_BENCH_BACKEND=gloo: host-staged gather with every rank on GPU local % device_count, to
+    # rehearse the N>1 path on a one-GPU box (never for a reported number; RCCL is the product path)
+    backend = os.environ.get("RT_BENCH_BACKEND", "nccl")
+    local = local % max(1, torch.cuda.device_count()) if backend == "gloo" else local
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     if world > 1:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        dist.init_process_group("nccl", device_id=dev)
+        if backend == "gloo":
+            dist.init_process_group("gloo")
+        else:
+            dist.init_process_group("nccl", device_id=dev)
+
+    def all_reduce(t, op=None):
+        if world == 1:
+            return t
+        kw = {} if op is None else {"op": op}
+        if backend == "gloo":
+            h = t.cpu()
+            dist.all_reduce(h, **kw)
+            return h.to(t.device)
+        dist.all_reduce(t, **kw)
+        return t
 
     pkg = graft.import_pkg()
     config, desc = CONFIGS[a.config]
@@ -145,16 +163,20 @@ def main() -> int:
     W, H, S = cam.image_width, cam.image_height, a.stripe_rows
     rows = pkg.slab_rows(H, S, world)
     F = max(1, a.inflight if a.inflight is not None else (1 if a.config == "C5" else 16))
-    slabs = torch.empty((F, rows, W, 3), dtype=torch.uint8, device=dev)
-    slab = slabs[0]
+    NB = 2 if world > 1 else 1     # N>1: batch b+1 renders while batch b's slabs are gathered (double buffer)
+    slab_bufs = [torch.empty((F, rows, W, 3), dtype=torch.uint8, device=dev) for _ in range(NB)]
+    slab = slab_bufs[0][0]
     stream = torch.cuda.current_stream(dev)
     sp = stream.cuda_stream
     gbufs = {}
+    freed = [None] * NB            # event: the buffer's previous gather has completed
+    nxt = [0]
     if world > 1:
+        comm = torch.cuda.Stream(dev)     # gather + rank-0 unshuffle, off the render stream
         images = [torch.empty((H, W, 3), dtype=torch.uint8, device=dev) for _ in range(F)] if rank == 0 else None
 
-        def unshuffle_dev(g, img):    # rank-0 kernel: slabs -> row order (rt_unshuffle_stripes)
-            pkg.unshuffle_stripes(g.data_ptr(), img.data_ptr(), W, H, S, world, sp)
+        def unshuffle_dev(g, img):    # rank-0 kernel: slabs -> row order (rt_unshuffle_stripes), comm stream
+            pkg.unshuffle_stripes(g.data_ptr(), img.data_ptr(), W, H, S, world, comm.cuda_stream)
 
     def note(msg):      # progress on stderr (long configs such as C5)
         print(f"[bench rank {rank}] {msg} t={time.perf_counter() - t0:.1f}s", file=sys.stderr, flush=True)
@@ -170,24 +192,37 @@ def main() -> int:
     ps_local = cnt["primary_rays"] + cnt["shadow_rays"]
     tot = torch.tensor([ps_local, cnt["primary_rays"], cnt["shadow_rays"], cnt["reflection_rays"]],
                        dtype=torch.float64, device=dev)
-    if world > 1:
-        dist.all_reduce(tot)
+    tot = all_reduce(tot)
     ps_frame, prim_frame, shadow_frame, refl_frame = (int(x) for x in tot.tolist())
 
     def step(n, ev_pair=None):
         """n frames (steps) submitted together: this rank's stripes of each, then (N>1) one gather."""
+        b = nxt[0]
+        nxt[0] = (b + 1) % NB
+        sl = slab_bufs[b]
+        if freed[b] is not None:
+            stream.wait_event(freed[b])       # its previous batch has left for rank 0
         if ev_pair is not None:
             ev_pair[0].record(stream)
         if n == 1:
-            scene.render_device(cam, aa, slab.data_ptr(), sp, S, rank, world)
+            scene.render_device(cam, aa, sl[0].data_ptr(), sp, S, rank, world)
         else:
-            scene.render_frames_device([cam] * n, aa, [slabs[f].data_ptr() for f in range(n)], sp, S, rank, world)
+            scene.render_frames_device([cam] * n, aa, [sl[f].data_ptr() for f in range(n)], sp, S, rank, world)
         if ev_pair is not None:
             ev_pair[1].record(stream)
-        if world > 1:
-            if rank == 0 and n not in gbufs:
-                gbufs[n] = torch.empty((world, n, rows, W, 3), dtype=torch.uint8, device=dev)
-            pkg.frame.assemble_frames(slabs[:n], H, S, unshuffle=unshuffle_dev, gbuf=gbufs.get(n), images=images)
+        if world == 1:
+            return None
+        if backend == "gloo":
+            return pkg.frame.assemble_frames(sl[:n].cpu(), H, S)
+        if rank == 0 and n not in gbufs:
+            gbufs[n] = torch.empty((world, n, rows, W, 3), dtype=torch.uint8, device=dev)
+        comm.wait_stream(stream)
+        with torch.cuda.stream(comm):
+            out = pkg.frame.assemble_frames(sl[:n], H, S, unshuffle=unshuffle_dev, gbuf=gbufs.get(n), images=images)
+            ev = torch.cuda.Event()
+            ev.record(comm)
+        freed[b] = ev
+        return out
 
     def groups(k):
         return [min(F, k - i) for i in range(0, k, F)]
@@ -203,13 +238,21 @@ def main() -> int:
     torch.cuda.synchronize(dev)
     t0 = time.perf_counter()
     for n, ev in zip(gs, evs):
-        step(n, ev)
+        last = step(n, ev)
     torch.cuda.synchronize(dev)
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t0
     note(f"timed {a.steps} steps")
     kern_ms = sum(e0.elapsed_time(e1) for e0, e1 in evs) / a.steps      # render time per frame (batch-amortised)
+
+    # N>1: the assembled frames equal one GPU's whole-frame render (checked after timing, rank 0)
+    frames_ok = None
+    if world > 1 and rank == 0:
+        full = torch.empty((H, W, 3), dtype=torch.uint8, device=dev)
+        scene.render_device(cam, aa, full.data_ptr(), sp, H, 0, 1)
+        torch.cuda.synchronize(dev)
+        frames_ok = all(torch.equal(f.to(dev), full) for f in last)
 
     # single-frame latency (one frame alone on the GPU, this rank's stripes; reported, not `value`)
     lat = []
@@ -222,8 +265,7 @@ def main() -> int:
         lat.append(e0.elapsed_time(e1))
     lat_ms = sorted(lat)[len(lat) // 2]
     tmax = torch.tensor([elapsed, kern_ms, lat_ms], dtype=torch.float64, device=dev)
-    if world > 1:
-        dist.all_reduce(tmax, op=dist.ReduceOp.MAX)
+    tmax = all_reduce(tmax, dist.ReduceOp.MAX)
     elapsed, kern_ms_max, lat_ms = tmax.tolist()
 
     # PCIe-inclusive figure (rank 0, N=1 only; never `value`): rt_render = upload camera, render, D2H copy
@@ -246,6 +288,8 @@ def main() -> int:
         ms = elapsed / a.steps * 1e3
         value = ps_frame * a.steps / elapsed / 1e6
         achieved = alg_bytes / (kern_ms / 1e3) / 1e9
+        if backend != "nccl":
+            desc += f" [REHEARSAL: {backend} host-staged gather, all ranks on one GPU; not a measurement]"
         line = {
             "metric": "Mray/s (primary+shadow), horse_and_mug 1920x1080 depth 6" if a.config == "C3"
                       else f"Mray/s (primary+shadow), {desc}",
@@ -256,6 +300,10 @@ def main() -> int:
                        "max_recursion_depth": 6 if config != "C2_cornellbox_800_d0" else 0,
                        "parallelism": f"stripes{S}x{world}" + ("+rccl_gather" if world > 1 else ""),
                        "frames_in_flight": F, "frame_latency_ms": round(lat_ms, 4),
+                       # every frame this process rendered on the GPU (counting pass, warmup, timed, latency,
+                       # host-buffer runs): the divisor for whole-run PMC totals (tools/summarize_profile.py)
+                       "frames_rendered_total": 1 + max(a.warmup, F) + a.steps + 5 + (6 if world == 1 else 0),
+                       "assembled_frames_equal_single_gpu": frames_ok,
                        "primary_rays": prim_frame, "shadow_rays": shadow_frame, "reflection_rays": refl_frame,
                        "mray_s_all": round((ps_frame + refl_frame) * a.steps / elapsed / 1e6, 3),
                        "scene_load_s": round(load_s, 4),
@@ -269,7 +317,7 @@ def main() -> int:
                          "kernel": "one frame = " + " + ".join(PATH_KERNELS[a.path])
                                    + (f" (frames in batches of up to {F}: kernel_ms = batch time / frames)" if F > 1 else ""),
                          "kernel_ms": round(kern_ms, 4),
-                         "alg_bytes_per_launch": int(alg_bytes),
+                         "alg_bytes_per_launch": int(alg_bytes), "launch_unit": "one frame (this rank's stripes)",
                          "counts_per_launch": {k: cnt[k] for k in ("node_visits", "tri_tests", "sphere_tests")}},
         }
         if world == 1 and not a.no_cpu_baseline:

@@ -45,12 +45,22 @@ bench = [json.loads(l) for l in open(out / "bench.jsonl") if l.startswith("{")]
 line = bench[-1] if bench else {}
 frame_kernels = line.get("roofline", {}).get("kernels", [])
 tot = 0.0
-for k in frame_kernels:
-    if k in kern:
-        tot += (2.0 * kern[k].get("FETCH_SIZE", 0.0) + kern[k].get("WRITE_SIZE", 0.0)) * 1024.0
+nframes = line.get("config", {}).get("frames_rendered_total")
+if nframes:
+    # frame batches: launches cover different frame counts, so divide the run's totals by its frames
+    for k in frame_kernels:
+        if k in per:
+            tot += (2.0 * sum(per[k].get("FETCH_SIZE", [])) + sum(per[k].get("WRITE_SIZE", []))) * 1024.0
+    tot /= nframes
+else:
+    for k in frame_kernels:
+        if k in kern:
+            tot += (2.0 * kern[k].get("FETCH_SIZE", 0.0) + kern[k].get("WRITE_SIZE", 0.0)) * 1024.0
 res = {"tag": tag, "config": line.get("config", {}).get("workload"), "path": line.get("roofline", {}).get("path"),
        "per_kernel_KiB": kern, "frame_kernels": frame_kernels, "hbm_bytes_per_frame": tot,
-       "note": "2*FETCH_SIZE + WRITE_SIZE per kernel (KiB), summed over one frame's kernels"}
+       "frames_rendered_total": nframes,
+       "note": "2*FETCH_SIZE + WRITE_SIZE per kernel (KiB), summed over one frame's kernels"
+               + (" (run totals / frames_rendered_total)" if nframes else "")}
 (prof / f"{tag}_traffic.json").write_text(json.dumps(res, indent=1))
 (prof / "traffic.json").write_text(json.dumps(res, indent=1))
 shutil.copy(out / "bench.jsonl", prof / f"{tag}_bench.jsonl")
