@@ -120,7 +120,7 @@ struct rt_scene {
     int tune_wide = 0;          // RT_WIDE
     int tune_wide_min = 24;     // RT_WIDE_MIN
     int tune_kinline = 1;       // RT_KINLINE: deepest level of phase A
-    size_t chunk_samples = size_t(4) << 20;   // RT_CHUNK_SAMPLES: samples per chain-path launch (chunk / batch)
+    size_t chunk_samples = size_t(8) << 20;   // RT_CHUNK_SAMPLES: samples per chain-path launch (chunk / batch)
     int tune_batch = 16;        // RT_BATCH: frames per batched launch (rt_render_frames/cameras; 1 = off)
     int tune_gb = 0;            // RT_GB: phase-B chain workgroups in k_mix (0 = 1.5625 per CU: 384-416 best of 256-1024 on C3)
     int tune_bq_cap = 1 << 30;  // RT_BQ_CAP: phase-B shadow queue slots (tests force the k_occlude spill path)

@@ -14,7 +14,7 @@ fi
 i=0
 for cfg in "$@"; do
   i=$((i+1))
-  env $cfg timeout -k 10 300 python bench.py --steps 20 --warmup 3 --no-cpu-baseline > gpurun_out/sweep_$i.log 2>&1
+  env $cfg timeout -k 10 300 python bench.py --steps ${SWEEP_STEPS:-64} --warmup 3 --no-cpu-baseline > gpurun_out/sweep_$i.log 2>&1
   rc=$?
   ms=$(grep '^{' gpurun_out/sweep_$i.log | python -c "import sys,json; d=json.loads(sys.stdin.read()); print(d['ms_per_step'], d['value'])")
   echo "[$cfg] rc=$rc ms/Mray: $ms"
