@@ -60,7 +60,8 @@ def parse():
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--config", default="C3", choices=sorted(CONFIGS))
     ap.add_argument("--aa", type=int, default=None, help="SSAA factor (default 1; C5: 4)")
-    ap.add_argument("--stripe-rows", type=int, default=8)
+    ap.add_argument("--stripe-rows", type=int, default=4,
+                    help="output rows per round-robin stripe (4: best rank balance at N=8, tools/exp_shard.py)")
     ap.add_argument("--path", default="chain", choices=sorted(PATH_KERNELS), help="render path (all bit-identical)")
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="CPU baseline budget (rank 0, N=1)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
