@@ -34,7 +34,8 @@ namespace {
 
 constexpr int kBlock = 256;
 #ifndef RT_WAVES_PER_EU
-#define RT_WAVES_PER_EU 5     // k_chain: 96 VGPRs, 5 waves/SIMD (a few spills beat 4 waves: C3 1.36 -> 1.32 ms)
+#define RT_WAVES_PER_EU 4     // k_chain: 4 waves/SIMD (118 VGPRs).  One frame at a time 5 waves (96 VGPRs)
+                              // won (1.36 -> 1.32 ms); with frame batches 4 wins (0.81-0.82 -> 0.79-0.80 ms/frame)
 #endif
 #ifndef RT_WIDE_B
 #define RT_WIDE_B 0           // wide walks for phase-B tails (RT_WIDE > 0 at run time)
