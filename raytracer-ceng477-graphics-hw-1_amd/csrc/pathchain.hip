@@ -1194,7 +1194,7 @@ __device__ void occlude_body(const rtk::DevScene& s, const PcParams& p, unsigned
     Work w;
     uint32_t nrays = 0;
     const unsigned t_start = p.trace ? (unsigned)wall_clock64() : 0u;
-    const unsigned n = chunk_count(total, G, blk, (unsigned)p.tchunk);
+    const unsigned n = chunk_count(total, G, blk, (unsigned)p.ochunk);
     bool active = false, exhausted = n == 0;
     Ray r;
     float tlim = 0.0f;
@@ -1209,7 +1209,7 @@ __device__ void occlude_body(const rtk::DevScene& s, const PcParams& p, unsigned
                 if (!active) {
                     const unsigned idx = base + lane_rank(idle);
                     if (idx < n) {
-                        const unsigned j = chunk_task(idx, G, blk, (unsigned)p.tchunk);
+                        const unsigned j = chunk_task(idx, G, blk, (unsigned)p.ochunk);
                         owner = tasks[j];
                         r = shadow_from_record(s, p, owner, &tlim);
                         nrays++;

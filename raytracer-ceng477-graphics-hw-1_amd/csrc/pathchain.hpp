@@ -64,7 +64,8 @@ struct PcParams {
     unsigned* totals; // [3]
     int kinline;      // deepest level phase A walks (>= max_depth: no phase B)
     int gb;           // k_mix workgroups in the chain role (the other p.ogrid ones occlude A's tasks)
-    int tchunk;       // continuation / shadow tasks are dealt to workgroups in chunks of this many
+    int tchunk;       // continuation tasks (phase B) are dealt to workgroups in chunks of this many
+    int ochunk;       // ... and shadow tasks (k_mix occlusion role, k_occlude) in chunks of this many
     int packet;       // 1: eye rays of a wave walk as one packet when exact (packet_closest)
     int shade_split;  // 1: k_shade (a lane per record) + k_compose instead of k_finish
     int exp_skip_occ; // experiments only (RT_EXP_SKIP_OCC): k_mix's occlusion role does nothing (wrong images)
