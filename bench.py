@@ -6,7 +6,7 @@ on N GPUs of one node.
 One "step" = one frame: every rank renders its round-robin row stripes of the
 frame into an HBM slab, then for N>1 the slabs are gathered to rank 0 with one
 RCCL collective over xGMI and un-interleaved by a rank-0 kernel.
-Frames are submitted --inflight at a time (default 32) as frame batches
+Frames are submitted --inflight at a time (default 96) as frame batches
 (rt_render_frames_device: one persistent grid walks several frames' samples, so
 one frame's serial mirror-chain tail runs beside the others' bulk; one gather
 per batch).  Every frame's full work is done and counted; the single-frame
@@ -56,7 +56,7 @@ CONFIGS = {
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=50)
+    ap.add_argument("--steps", type=int, default=192)
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--config", default="C3", choices=sorted(CONFIGS))
     ap.add_argument("--aa", type=int, default=None, help="SSAA factor (default 1; C5: 4)")
@@ -67,7 +67,7 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--inflight", type=int, default=None,
                     help="frames submitted together (rt_render_frames_device frame batches; 1 = one frame at a "
-                         "time; default 32, C5 1: its frames are already 250x larger than one launch's chunk)")
+                         "time; default 96, C5 1: its frames are already 250x larger than one launch's chunk)")
     return ap.parse_args()
 
 
@@ -163,7 +163,7 @@ def main() -> int:
     cam = scene.camera(0)
     W, H, S = cam.image_width, cam.image_height, a.stripe_rows
     rows = pkg.slab_rows(H, S, world)
-    F = max(1, a.inflight if a.inflight is not None else (1 if a.config == "C5" else 32))
+    F = max(1, a.inflight if a.inflight is not None else (1 if a.config == "C5" else 96))
     NB = 2 if world > 1 else 1     # N>1: batch b+1 renders while batch b's slabs are gathered (double buffer)
     slab_bufs = [torch.empty((F, rows, W, 3), dtype=torch.uint8, device=dev) for _ in range(NB)]
     slab = slab_bufs[0][0]

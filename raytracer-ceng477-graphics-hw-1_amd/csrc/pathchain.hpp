@@ -26,7 +26,7 @@
 namespace rtc {
 
 constexpr int kMaxChainGrid = 2048;   // k_chain workgroups (= task-queue regions)
-constexpr int kMaxFrames = 16;        // frames of one batched launch (rt_render_frames_device)
+constexpr int kMaxFrames = 32;        // frames of one batched launch (PcParams kernarg: 64 B each) (rt_render_frames_device)
 #ifndef RT_BQ
 #define RT_BQ 1536
 #endif

@@ -126,8 +126,12 @@ struct rt_scene {
     int tune_wide = 0;          // RT_WIDE
     int tune_wide_min = 24;     // RT_WIDE_MIN
     int tune_kinline = 1;       // RT_KINLINE: deepest level of phase A
-    size_t chunk_samples = size_t(8) << 20;   // RT_CHUNK_SAMPLES: samples per chain-path launch (chunk / batch)
-    int tune_batch = 16;        // RT_BATCH: frames per batched launch (rt_render_frames/cameras; 1 = off)
+    // RT_CHUNK_SAMPLES: samples per chain-path launch (chunk / frame batch).  Bigger launches leave
+    // fewer tails per sample: C3 batches 4 M 0.72, 8 M 0.66, 16 M 0.63, 32 M 0.59 ms/frame; C5 8 M
+    // 159.6, 16 M 147.4, 32 M 140.6 ms/frame.  32 M samples = 15 GB of workspace per slot (C3).
+    size_t chunk_samples = size_t(32) << 20;
+    int tune_batch = 32;        // RT_BATCH: frames per batched launch (rt_render_frames/cameras; 1 = off)
+    int tune_slots = 3;         // RT_SLOTS: frame batches in flight together (workspace slots, <= kSlots)
     int tune_gb = 0;            // RT_GB: phase-B chain workgroups in k_mix (0 = 1.5625 per CU: 384-416 best of 256-1024 on C3)
     int tune_bq_cap = 1 << 30;  // RT_BQ_CAP: phase-B shadow queue slots (tests force the k_occlude spill path)
     int tune_quad4 = 0;         // RT_QUAD4: phase-B chains with 4 lanes per ray (measured slower: 1.71 vs 1.20 ms)
@@ -272,6 +276,7 @@ int finish_scene(rt_scene* s, const rt_options* opts) {
     if (const char* e = std::getenv("RT_WIDE")) s->tune_wide = std::max(0, std::min(64, std::atoi(e)));
     if (const char* e = std::getenv("RT_WIDE_MIN")) s->tune_wide_min = std::max(0, std::atoi(e));
     if (const char* e = std::getenv("RT_BATCH")) s->tune_batch = std::max(1, std::atoi(e));
+    if (const char* e = std::getenv("RT_SLOTS")) s->tune_slots = std::max(1, std::atoi(e));
     if (const char* e = std::getenv("RT_CHUNK_SAMPLES"))
         s->chunk_samples = std::max<size_t>(4096, std::min<size_t>(size_t(1) << 26, std::strtoull(e, nullptr, 10)));
     if (const char* e = std::getenv("RT_KINLINE")) s->tune_kinline = std::max(0, std::atoi(e));
@@ -487,7 +492,9 @@ int render_chain(rt_scene* s, const rtk::Eye& eye, const rtk::FrameParams& f, bo
     const size_t unit_samples = (size_t)tiles_x * f.aa * 64;
     const size_t units_total = (size_t)(li + unit - 1) / unit;
     const size_t per_sample = (size_t)levels * (48 + 8 * nl + nl) + 16;
-    const size_t target = std::max<size_t>(unit_samples, std::min(s->chunk_samples, kChainBudgetBytes / per_sample));
+    const size_t id_limit = (size_t)(INT32_MAX - 1) / ((size_t)levels * nl);   // u32 task owner ids (pathchain.hpp)
+    const size_t target = std::max<size_t>(
+        unit_samples, std::min({s->chunk_samples, kChainBudgetBytes / per_sample, id_limit}));
     const size_t units = std::min(units_total, std::max<size_t>(1, target / unit_samples));
     const int chunk_rows = (int)units * unit;
     const size_t cap = units * unit_samples;
@@ -877,13 +884,16 @@ int render_cameras(rt_scene* s, const rt_camera* cams, int n, int aa, void* cons
                           s->tune_batch > 1;
     if (batching) {
         // consecutive same-size frames, up to kMaxFrames and one chain chunk of samples per batch
+        // at least nslot batches when the frames allow (concurrent batches overlap each other's tails)
+        const int nslot = std::max(1, std::min(s->tune_slots, rt_scene::kSlots));
+        const int bmax = std::min({s->tune_batch, rtc::kMaxFrames, (n + nslot - 1) / nslot});
         std::vector<int> starts;
         for (int i = 0; i < n;) {
             const auto& c = cams[i];
             const long long per = (long long)rt_slab_rows(c.image_height, rows_of(i), nranks) * aa *
                                   ((long long)c.image_width * aa);
             int j = i + 1;
-            while (j < n && j - i < std::min(s->tune_batch, rtc::kMaxFrames) &&
+            while (j < n && j - i < bmax &&
                    cams[j].image_width == c.image_width && cams[j].image_height == c.image_height &&
                    (long long)(j - i + 1) * per <= (long long)s->chunk_samples)
                 ++j;
@@ -895,14 +905,14 @@ int render_cameras(rt_scene* s, const rt_camera* cams, int n, int aa, void* cons
         if (nb == 1) return render_batch(s, cams, n, aa, rows_of(0), rank, nranks, outs_dev, stream, flags, 0);
         if (!s->fork_ev) HIP_TRY(hipEventCreateWithFlags(&s->fork_ev, hipEventDisableTiming));
         HIP_TRY(hipEventRecord(s->fork_ev, stream));
-        const int used = std::min(nb, rt_scene::kSlots);
+        const int used = std::min(nb, nslot);
         for (int k = 0; k < used; ++k) {
             if (!s->slot_stream[k]) HIP_TRY(hipStreamCreateWithFlags(&s->slot_stream[k], hipStreamNonBlocking));
             if (!s->slot_done[k]) HIP_TRY(hipEventCreateWithFlags(&s->slot_done[k], hipEventDisableTiming));
             HIP_TRY(hipStreamWaitEvent(s->slot_stream[k], s->fork_ev, 0));
         }
         for (int b = 0; b < nb; ++b) {
-            const int k = b % rt_scene::kSlots, i = starts[b];
+            const int k = b % nslot, i = starts[b];
             const int rc = render_batch(s, cams + i, starts[b + 1] - i, aa, rows_of(i), rank, nranks, outs_dev + i,
                                         s->slot_stream[k], flags, k);
             if (rc) return rc;

@@ -7,7 +7,7 @@ export TMPDIR=/tmp
 i=0
 for cfg in "$@"; do
   i=$((i+1))
-  env $cfg timeout -k 10 200 python bench.py --steps 64 --warmup 3 --no-cpu-baseline > gpurun_out/sb_$i.log 2>&1 || exit 1
+  env $cfg timeout -k 10 200 python bench.py --steps ${SB_STEPS:-64} --warmup 3 --no-cpu-baseline $SB_ARGS > gpurun_out/sb_$i.log 2>&1 || exit 1
   b=$(grep '^{' gpurun_out/sb_$i.log | python3 -c "import sys,json; d=json.loads(sys.stdin.read()); print(d['ms_per_step'], d['value'], d['config']['frame_latency_ms'])")
   env $cfg EXP_F=32 timeout -k 10 100 python3 tools/exp_shard.py 8 > gpurun_out/sb8_$i.log 2>&1 || exit 1
   n8=$(grep '^{' gpurun_out/sb8_$i.log | python3 -c "import sys,json; d=json.loads(sys.stdin.read()); print(d['max_ms'])")
