@@ -313,6 +313,10 @@ def main() -> int:
                        "host_buffer_ms_per_frame": round(host_ms, 4) if host_ms else None},
             "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
                          "frac": round(achieved / HBM_PEAK_GBPS, 4), "traffic": traffic,
+                         # measured HBM rate (PMC bytes per frame / frame time): the scene is L2/MALL-resident,
+                         # so the algorithmic rate above can exceed the HBM peak while this stays far below it
+                         "traffic_gbps": round(traffic / (kern_ms / 1e3) / 1e9, 2) if traffic else None,
+                         "traffic_frac": round(traffic / (kern_ms / 1e3) / 1e9 / HBM_PEAK_GBPS, 4) if traffic else None,
                          "traffic_source": traffic_src,
                          "path": a.path, "kernels": PATH_KERNELS[a.path],
                          "kernel": "one frame = " + " + ".join(PATH_KERNELS[a.path])
