@@ -246,6 +246,30 @@ def test_render_frames_device_batch(nranks, nframes, gname, path, batch, goldens
         assert _stats(cnt) == tuple(nframes * x for x in _counters(c))
 
 
+@pytest.mark.parametrize("slots", ["3", "4"])
+def test_render_frames_device_many_batches(slots, goldens, pkg, scene_dir, torch_cuda, monkeypatch):
+    """70 frames of 8-rank shards: more frames than kMaxFrames (32) per batch and more batches than
+    slots, so batches reuse slot workspaces while others run; every frame equals the golden."""
+    torch = torch_cuda
+    monkeypatch.setenv("RT_SLOTS", slots)
+    g = golden_by_name(goldens, "C3_hm_1080p_d6_aa1")
+    nranks, nframes, stripe = 8, 70, 4
+    with pkg.Scene.from_xml(config_path(scene_dir, g["config"]), device=0) as s:
+        cam = s.camera(0)
+        W, H = cam.image_width, cam.image_height
+        rows = pkg.slab_rows(H, stripe, nranks)
+        slabs = torch.zeros((nframes, nranks, rows, W, 3), dtype=torch.uint8, device="cuda:0")
+        stream = torch.cuda.current_stream().cuda_stream
+        for r in range(nranks):
+            s.render_frames_device([cam] * nframes, 1, [slabs[f, r].data_ptr() for f in range(nframes)], stream,
+                                   stripe_rows=stripe, rank=r, nranks=nranks)
+        ref = torch.from_numpy(load_golden_image(g["cameras"][0])).to("cuda:0")
+        img = torch.empty((H, W, 3), dtype=torch.uint8, device="cuda:0")
+        for f in range(nframes):
+            pkg.unshuffle_stripes(slabs[f].data_ptr(), img.data_ptr(), W, H, stripe, nranks, stream)
+            assert torch.equal(img, ref), f"frame {f}"
+
+
 @pytest.mark.parametrize("path", ["chain", "fused"])
 def test_render_frames_device_mixed_cameras(path, goldens, pkg, scene_dir, torch_cuda):
     """One batch holding different cameras of one size (cornellbox's two 800x800 cameras),
