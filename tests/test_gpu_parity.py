@@ -263,7 +263,7 @@ def test_render_frames_device_many_batches(slots, goldens, pkg, scene_dir, torch
         for r in range(nranks):
             s.render_frames_device([cam] * nframes, 1, [slabs[f, r].data_ptr() for f in range(nframes)], stream,
                                    stripe_rows=stripe, rank=r, nranks=nranks)
-        ref = torch.from_numpy(load_golden_image(g["cameras"][0])).to("cuda:0")
+        ref = torch.from_numpy(load_golden_image(g["cameras"][0]).copy()).to("cuda:0")
         img = torch.empty((H, W, 3), dtype=torch.uint8, device="cuda:0")
         for f in range(nframes):
             pkg.unshuffle_stripes(slabs[f].data_ptr(), img.data_ptr(), W, H, stripe, nranks, stream)
