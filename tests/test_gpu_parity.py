@@ -270,6 +270,33 @@ def test_render_frames_device_many_batches(slots, goldens, pkg, scene_dir, torch
             assert torch.equal(img, ref), f"frame {f}"
 
 
+def test_render_frames_device_many_cameras(goldens, pkg, scene_dir, torch_cuda):
+    """12 cameras, 6 distinct, in one call (batches mixing eyes): each frame equals a lone
+    rt_render_device of its camera."""
+    torch = torch_cuda
+    g = golden_by_name(goldens, "cornellbox_aa1")
+    with pkg.Scene.from_xml(config_path(scene_dir, g["config"]), device=0) as s:
+        base = s.cameras()[1][0]
+        cams = []
+        for i in range(12):
+            c = pkg.Camera()
+            c.position, c.gaze, c.up = base.position, base.gaze, base.up
+            c.near_plane, c.near_distance = base.near_plane, base.near_distance
+            c.image_width, c.image_height = base.image_width, base.image_height
+            c.position.x = base.position.x + 0.01 * (i % 6)      # frames i and i+6 share a camera
+            cams.append(c)
+        W, H = base.image_width, base.image_height
+        outs = torch.zeros((len(cams), H, W, 3), dtype=torch.uint8, device="cuda:0")
+        stream = torch.cuda.current_stream().cuda_stream
+        s.render_frames_device(cams, 1, [o.data_ptr() for o in outs], stream, stripe_rows=H, rank=0, nranks=1)
+        one = torch.empty((H, W, 3), dtype=torch.uint8, device="cuda:0")
+        for i, c in enumerate(cams):
+            s.render_device(c, 1, one.data_ptr(), stream)
+            torch.cuda.synchronize()
+            assert torch.equal(outs[i], one), f"frame {i}"
+        assert not torch.equal(outs[0], outs[1])
+
+
 @pytest.mark.parametrize("path", ["chain", "fused"])
 def test_render_frames_device_mixed_cameras(path, goldens, pkg, scene_dir, torch_cuda):
     """One batch holding different cameras of one size (cornellbox's two 800x800 cameras),
