@@ -33,7 +33,7 @@
 extern "C" {
 #endif
 
-#define RT_ABI_VERSION 3
+#define RT_ABI_VERSION 4
 
 typedef enum rt_status {
     RT_OK = 0,
@@ -42,7 +42,8 @@ typedef enum rt_status {
     RT_ERR_PARSE = -3,      /* XML malformed / missing element              */
     RT_ERR_HIP = -4,        /* HIP runtime error (message has the HIP name) */
     RT_ERR_NO_DEVICE = -5,  /* no gfx950 device visible                     */
-    RT_ERR_LIMIT = -6       /* scene exceeds an encoding limit               */
+    RT_ERR_LIMIT = -6       /* scene exceeds an encoding limit, or a walk hit its
+                               step bound (rt_scene_check)                   */
 } rt_status;
 
 /* ---- scene model: field names and meaning follow parser.h:170-251 ---- */
@@ -207,6 +208,14 @@ int rt_unshuffle_stripes(const void* slabs_dev, void* image_dev, int width, int 
                          int stripe_rows, int nranks, void* stream);
 int rt_counters_reset(rt_scene* scene, void* stream);
 int rt_counters_read(rt_scene* scene, rt_stats* stats);   /* synchronises the device */
+/* Synchronises the scene's device and reports a walk that was cut off since
+ * the last check: every BVH walk has an always-on step bound (64 x the tree's
+ * nodes; a DFS pops each node at most once), and a walk exceeding it ends
+ * early and sets the scene's device error word -> RT_ERR_LIMIT (the frames
+ * rendered since the last check are then invalid).  rt_render,
+ * rt_render_cameras and rt_counters_read check it themselves; asynchronous
+ * callers (rt_render_device, rt_render_frames_device) call this.  (ABI 4) */
+int rt_scene_check(rt_scene* scene);
 
 /* Primary closest-hit per internal pixel ((W*aa) x (H*aa)): t (tSmall, -1 on
  * miss) and material id (0 on miss) into caller-allocated host arrays

@@ -108,6 +108,7 @@ _SIGS = [
     ("rt_unshuffle_stripes", ctypes.c_int, [_P, _P, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int, _P]),
     ("rt_counters_reset", ctypes.c_int, [_P, _P]),
     ("rt_counters_read", ctypes.c_int, [_P, ctypes.POINTER(Stats)]),
+    ("rt_scene_check", ctypes.c_int, [_P]),
     ("rt_primary_hits", ctypes.c_int, [_P, ctypes.POINTER(Camera), ctypes.c_int, _P, _P]),
     ("rt_downsample_host", ctypes.c_int, [_P, ctypes.c_int, ctypes.c_int, ctypes.c_int, _P]),
     ("rt_write_ppm", ctypes.c_int, [ctypes.c_char_p, _P, ctypes.c_int, ctypes.c_int]),
@@ -124,6 +125,8 @@ def lib() -> ctypes.CDLL:
             raise RtError(-5, f"{LIB_PATH} not built (run __graft_entry__.build())")
         L = ctypes.CDLL(str(LIB_PATH))
         for name, res, args in _SIGS:
+            if os.environ.get("RT_LIB") and not hasattr(L, name):
+                continue          # an older experiment build (RT_LIB) may lack newer entry points
             fn = getattr(L, name)
             fn.restype = res
             fn.argtypes = args
@@ -274,6 +277,11 @@ class Scene:
         st = Stats()
         _check(lib().rt_counters_read(self._h, ctypes.byref(st)))
         return st.as_dict()
+
+    def check(self) -> None:
+        """Synchronise and raise RtError(RT_ERR_LIMIT) if a walk was cut off by its step bound since the
+        last check (rt_scene_check)."""
+        _check(lib().rt_scene_check(self._h))
 
     def primary_hits(self, cam: Camera, aa: int = 1) -> tuple[np.ndarray, np.ndarray]:
         H, W = cam.image_height * aa, cam.image_width * aa

@@ -22,7 +22,7 @@ constexpr int32_t kLeafBit = (int32_t)0x80000000u;
 constexpr int kNtriBits = 20;
 constexpr int32_t kNtriMask = (1 << kNtriBits) - 1;
 constexpr int kMaxLeafSpheres = (1 << 11) - 1;
-constexpr int kMaxStack = 64;   // traversal stack entries (BVH depth cap 19 -> <= 20 used)
+constexpr int kMaxStack = 64;   // traversal stack entries (BVH depth cap 19 -> <= 20 used; wide walks: host-checked)
 
 struct alignas(16) Node {
     float minx, miny, minz; int32_t a;
@@ -66,13 +66,15 @@ struct alignas(16) Pair {
 struct LeafBig { int32_t start, count; };
 
 // Occlusion tree node, 4-wide, 64 B (four dwordx4 loads test four children):
-//   {origin.xyz, exps}  exps = ex | ey << 8 | ez << 16 | nchild << 24, scale_a = 2^(e_a - 127)
+//   {origin.xyz, exps}  exps = ex | ey << 8 | ez << 16 | slot mask << 24, scale_a = 2^(e_a - 127)
 //   {qlo[3][4] bytes, qhi[3][4] bytes}          axis-major: dword a = axis a's byte of children 0..3
 //       lo = origin_a + qlo[a][c] * scale_a,  hi = origin_a + qhi[a][c] * scale_a  (float, exact
 //       power-of-two scale; the host verifies every decoded box CONTAINS the child's exact box);
 //       a ray picks its near/far plane per axis by swapping whole dwords
 //   {child[4]}  >= 0: quad index; < 0: kLeafBit | offset of a leaf record (16-B units) in LeafRec[]
-//   {pad[2]}
+//   {order, pad}  reference-order quads (host_scene.cpp build_ref_quads): per octant of the ray
+//       direction (bit a set iff d[a] > 0), one byte of four 2-bit slot indices in the
+//       reference's visiting order; octants 0-3 in `order`, 4-7 in `pad`; 0 in the occlusion tree
 // Leaves are the reference BVH's leaves.  A leaf record is the leaf's header
 // (its EXACT box, tested exactly before the primitives) followed by copies of
 // its primitives, so the box and the first primitive arrive in one round trip:
@@ -82,8 +84,30 @@ struct alignas(16) Quad {
     float ox, oy, oz; uint32_t exps;
     uint32_t q[6];        // qlo x,y,z dwords (children 0..3 in bytes 0..3), then qhi x,y,z
     int32_t child[4];
-    int32_t pad[2];
+    uint32_t order;
+    int32_t pad;
 };
+// Reference-order wide node (closest-hit walks, host_scene.cpp build_ref_wide),
+// 128 B = one L2 line, up to kWideSlots children:
+//   dw 0-3    {origin.xyz, exps}  exps = ex | ey << 8 | ez << 16 | slot mask << 24
+//   dw 4-15   quantized child planes, axis-major: lo x (dw 4-5: bytes of slots 0..7), lo y, lo z,
+//             hi x, hi y, hi z (decoded as in Quad: origin + q * 2^(e - 127), containment verified)
+//   dw 16-23  child codes (>= 0 wide-node index, < 0 kLeafBit | leaf-record offset)
+//   dw 24-31  per octant of the ray direction (bit a set iff d[a] > 0): the rank of slot j in the
+//             reference's visiting order at bits 3j..3j+2
+#ifndef RT_WIDE_SLOTS
+#define RT_WIDE_SLOTS 6
+#endif
+constexpr int kWideSlots = RT_WIDE_SLOTS;     // 2..8, even
+struct alignas(128) Wide {
+    float ox, oy, oz; uint32_t exps;
+    uint32_t q[12];
+    int32_t child[8];
+    uint32_t rank[8];
+};
+static_assert(sizeof(Wide) == 128, "wide node size");
+static_assert(kWideSlots >= 2 && kWideSlots <= 8 && kWideSlots % 2 == 0, "wide node slots");
+
 struct alignas(16) LeafHead {
     float minx, miny, minz; int32_t count;
     float maxx, maxy, maxz; int32_t slot0;

@@ -553,9 +553,73 @@ class Builder {
 inline int32_t fbits(float f) { int32_t i; std::memcpy(&i, &f, 4); return i; }
 inline float ibits(int32_t i) { float f; std::memcpy(&f, &i, 4); return f; }
 
+// One 4-wide node (dl::Quad): the child boxes of the slots in `mask`,
+// quantized to 8 bits per plane on a power-of-two grid anchored at the union
+// box's low corner.  Every decoded box is checked, with the device's own
+// float arithmetic (one fma, quad_hits), to CONTAIN the child's exact box;
+// false if one does not.  Slots outside `mask` get code INT32_MAX.
+// Quantize the boxes of the slots in `mask` (n slots): origin = union low
+// corner, power-of-two scale per axis, 8-bit plane offsets (ql/qh[slot][axis]);
+// false if a decoded box does not contain its exact box.
+bool quantize_boxes(const float (*lo)[3], const float (*hi)[3], int n, unsigned mask, float* o, int* e,
+                    uint8_t (*ql)[3], uint8_t (*qh)[3]) {
+    auto pow2 = [](int x) { return ibits(x << 23); };                       // 2^(x-127), x in [1, 254]
+    auto dec = [](float org, int v, float sc) { return std::fma((float)v, sc, org); };
+    float top[3] = {-FLT_MAX, -FLT_MAX, -FLT_MAX};
+    for (int a = 0; a < 3; ++a) o[a] = FLT_MAX;
+    for (int i = 0; i < n; ++i)
+        if (mask >> i & 1u)
+            for (int a = 0; a < 3; ++a) { o[a] = std::min(o[a], lo[i][a]); top[a] = std::max(top[a], hi[i][a]); }
+    bool ok = true;
+    float sc[3];
+    for (int a = 0; a < 3; ++a) {
+        e[a] = 1;
+        const double ext = (double)top[a] - o[a];
+        if (ext > 0) e[a] = std::max(1, std::min(254, (int)std::ceil(std::log2(ext / 255.0)) + 127));
+        while (e[a] < 254 && dec(o[a], 255, pow2(e[a])) < top[a]) ++e[a];
+        sc[a] = pow2(e[a]);
+    }
+    for (int i = 0; i < n; ++i) {
+        for (int a = 0; a < 3; ++a) { ql[i][a] = 0; qh[i][a] = 0; }
+        if (!(mask >> i & 1u)) continue;
+        for (int a = 0; a < 3; ++a) {
+            int qlo = (int)std::floor(((double)lo[i][a] - o[a]) / sc[a]);
+            qlo = std::max(0, std::min(255, qlo));
+            while (qlo > 0 && dec(o[a], qlo, sc[a]) > lo[i][a]) --qlo;
+            int qhi = (int)std::ceil(((double)hi[i][a] - o[a]) / sc[a]);
+            qhi = std::max(0, std::min(255, qhi));
+            while (qhi < 255 && dec(o[a], qhi, sc[a]) < hi[i][a]) ++qhi;
+            if (dec(o[a], qlo, sc[a]) > lo[i][a] || dec(o[a], qhi, sc[a]) < hi[i][a]) ok = false;
+            ql[i][a] = (uint8_t)qlo;
+            qh[i][a] = (uint8_t)qhi;
+        }
+    }
+    return ok;
+}
+
+bool make_quad(const float (*lo)[3], const float (*hi)[3], const int32_t* codes, unsigned mask, uint32_t order,
+               dl::Quad& q) {
+    float o[3];
+    int e[3];
+    uint8_t ql[4][3], qh[4][3];
+    const bool ok = quantize_boxes(lo, hi, 4, mask, o, e, ql, qh);
+    uint8_t bytes[24] = {};
+    for (int i = 0; i < 4; ++i)
+        for (int a = 0; a < 3; ++a) { bytes[a * 4 + i] = ql[i][a]; bytes[12 + a * 4 + i] = qh[i][a]; }
+    q = dl::Quad{};
+    q.ox = o[0]; q.oy = o[1]; q.oz = o[2];
+    q.exps = (uint32_t)e[0] | (uint32_t)e[1] << 8 | (uint32_t)e[2] << 16 | (mask & 15u) << 24;
+    std::memcpy(q.q, bytes, 24);
+    for (int i = 0; i < 4; ++i) q.child[i] = (mask >> i & 1u) ? codes[i] : INT32_MAX;
+    q.order = order;
+    q.pad = 0;
+    return ok;
+}
+
 }  // namespace
 
 void build_shadow_tree(FlatBVH& out, int threads);
+bool build_ref_wide(FlatBVH& out);
 
 int build_threads(int requested) {
     if (requested > 0) return std::min(requested, 64);
@@ -657,6 +721,27 @@ std::string build_bvh(const HostScene& s, FlatBVH& out, int threads) {
     }
     (void)ibits; (void)fbits;
 
+    // Leaf records (dl::LeafHead + copies of the leaf's prims), one per
+    // reference leaf in pre-order (the closest-hit walk's visit order), shared
+    // by both 4-wide trees.
+    std::vector<int32_t> lrec_of(out.nodes.size(), -1);
+    bool lrec_ok = true;
+    for (size_t f = 0; f < out.nodes.size(); ++f) {
+        const dl::Node& n = out.nodes[f];
+        if (n.b >= 0) continue;
+        const int32_t count = (n.b & dl::kNtriMask) + ((n.b >> dl::kNtriBits) & dl::kMaxLeafSpheres);
+        const size_t off = out.lrec.size();
+        if (off > (size_t)INT32_MAX - 1 - (2 + 3 * (size_t)count)) lrec_ok = false;
+        dl::LeafHead h{};
+        h.minx = n.minx; h.miny = n.miny; h.minz = n.minz; h.count = count;
+        h.maxx = n.maxx; h.maxy = n.maxy; h.maxz = n.maxz; h.slot0 = n.a;
+        out.lrec.resize(off + 2 + 3 * (size_t)count);
+        std::memcpy(&out.lrec[off], &h, sizeof(h));
+        if (count > 0) std::memcpy(&out.lrec[off + 2], &out.prims[n.a], sizeof(dl::Prim) * (size_t)count);
+        lrec_of[f] = (int32_t)off;
+    }
+    out.lrec.resize(out.lrec.size() + 3);    // a leaf's first-prim loads may run past a 0-prim last leaf
+
     // Child-pair layout: one pair per interior node.  The top levels (every
     // walk passes through them) are numbered first, breadth-first, so a
     // kernel can cache pairs [0, top_pairs) in LDS; the rest follow in
@@ -693,6 +778,7 @@ std::string build_bvh(const HostScene& s, FlatBVH& out, int threads) {
         return dl::kLeafBit | (int32_t)(out.leaf_big.size() - 1);
     };
     out.pairs.resize(npairs);
+    out.pair_lrec.assign(2 * (size_t)npairs, -1);
     for (size_t f = 0; f < out.nodes.size(); ++f) {
         const dl::Node& n = out.nodes[f];
         if (n.b < 0) continue;
@@ -703,11 +789,16 @@ std::string build_bvh(const HostScene& s, FlatBVH& out, int threads) {
         p.l_maxx = L.maxx; p.l_maxy = L.maxy; p.l_maxz = L.maxz; p.axis = n.b;
         p.r_minx = R.minx; p.r_miny = R.miny; p.r_minz = R.minz; p.r_info = info_of(n.a);
         p.r_maxx = R.maxx; p.r_maxy = R.maxy; p.r_maxz = R.maxz; p.pad = 0;
+        out.pair_lrec[2 * pair_of[f]] = lrec_of[f + 1];
+        out.pair_lrec[2 * pair_of[f] + 1] = lrec_of[n.a];
     }
     if ((int)out.leaf_big.size() > dl::kLeafStartMask) return "Error: too many large BVH leaves";
     out.root_lo[0] = out.nodes[0].minx; out.root_lo[1] = out.nodes[0].miny; out.root_lo[2] = out.nodes[0].minz;
     out.root_hi[0] = out.nodes[0].maxx; out.root_hi[1] = out.nodes[0].maxy; out.root_hi[2] = out.nodes[0].maxz;
     out.root_info = info_of(0);
+    out.root_lrec = lrec_of[0];
+    if (!lrec_ok) out.lrec.clear();                  // no 4-wide trees: the binary trees only
+    if (!build_ref_wide(out) || out.lrec.empty()) out.wnodes.clear();
     // Ordered DFS pushes two children per interior pop: stack <= depth + 2.
     out.max_stack = out.max_depth + 2;
     if (out.max_stack > dl::kMaxStack) return "Error: BVH deeper than the device stack";
@@ -732,17 +823,25 @@ std::string build_bvh(const HostScene& s, FlatBVH& out, int threads) {
 // boxes above them, so shadow rays visit far fewer nodes with the same
 // answers.  Kernels use it only for NaN-free rays outside counting passes.
 void build_shadow_tree(FlatBVH& out, int threads) {
-    struct Leaf { float lo[3], hi[3], c[3]; int32_t info; };
+    struct Leaf { float lo[3], hi[3], c[3]; int32_t info, rec; };
     std::vector<Leaf> leaves;
-    auto add_leaf = [&](const float* lo, const float* hi, int32_t info) {
+    auto add_leaf = [&](const float* lo, const float* hi, int32_t info, int32_t rec) {
         Leaf l;
         for (int a = 0; a < 3; ++a) { l.lo[a] = lo[a]; l.hi[a] = hi[a]; l.c[a] = 0.5f * (lo[a] + hi[a]); }
         l.info = info;
+        l.rec = rec;
         leaves.push_back(l);
     };
-    for (const dl::Pair& p : out.pairs) {
-        if (p.l_info < 0) { const float lo[3] = {p.l_minx, p.l_miny, p.l_minz}, hi[3] = {p.l_maxx, p.l_maxy, p.l_maxz}; add_leaf(lo, hi, p.l_info); }
-        if (p.r_info < 0) { const float lo[3] = {p.r_minx, p.r_miny, p.r_minz}, hi[3] = {p.r_maxx, p.r_maxy, p.r_maxz}; add_leaf(lo, hi, p.r_info); }
+    for (size_t i = 0; i < out.pairs.size(); ++i) {
+        const dl::Pair& p = out.pairs[i];
+        if (p.l_info < 0) {
+            const float lo[3] = {p.l_minx, p.l_miny, p.l_minz}, hi[3] = {p.l_maxx, p.l_maxy, p.l_maxz};
+            add_leaf(lo, hi, p.l_info, out.pair_lrec[2 * i]);
+        }
+        if (p.r_info < 0) {
+            const float lo[3] = {p.r_minx, p.r_miny, p.r_minz}, hi[3] = {p.r_maxx, p.r_maxy, p.r_maxz};
+            add_leaf(lo, hi, p.r_info, out.pair_lrec[2 * i + 1]);
+        }
     }
     for (int a = 0; a < 3; ++a) { out.sroot_lo[a] = out.root_lo[a]; out.sroot_hi[a] = out.root_hi[a]; }
     out.spairs.clear();
@@ -763,7 +862,7 @@ void build_shadow_tree(FlatBVH& out, int threads) {
         }
     };
     // binned SAH over leaf centroids; each tree leaf is one reference leaf
-    struct TNode { Box box; int left = -1, right = -1, axis = 0; int32_t info = 0; };
+    struct TNode { Box box; int left = -1, right = -1, axis = 0; int32_t info = 0, rec = -1; };
     std::vector<int> idx(leaves.size());
     for (size_t i = 0; i < idx.size(); ++i) idx[i] = (int)i;
     // Subtrees are independent (disjoint ranges of idx): the top levels are
@@ -788,6 +887,7 @@ void build_shadow_tree(FlatBVH& out, int threads) {
         tn.push_back(node);
         if (e - b == 1) {
             tn[me].info = leaves[idx[b]].info;
+            tn[me].rec = leaves[idx[b]].rec;
             return me;
         }
         Box cb;
@@ -897,32 +997,18 @@ void build_shadow_tree(FlatBVH& out, int threads) {
     for (int a = 0; a < 3; ++a) { out.sroot_lo[a] = tn[root].box.lo[a]; out.sroot_hi[a] = tn[root].box.hi[a]; }
     out.sroot_info = info(root);
 
-    // 4-wide collapse with quantized child boxes (dl::Quad).  Every decoded
-    // box is verified, with the device's own float arithmetic, to CONTAIN the
-    // child's box, so containment (all the any-hit argument needs) holds.
-    auto pow2 = [](int e) { return ibits(e << 23); };                       // 2^(e-127), e in [1, 254]
-    auto dec = [](float o, int q, float sc) { return std::fma((float)q, sc, o); };  // the device decode (quad_hits)
+    // 4-wide collapse with quantized child boxes (dl::Quad, make_quad: every
+    // decoded box contains the child's box, all the any-hit argument needs).
+    // Leaves are the shared leaf records.
     out.quads.clear();
-    out.lrec.clear();
     out.qmax_depth = 0;
-    bool contain_ok = true, lrec_ok = true;
+    bool contain_ok = !out.lrec.empty();
     std::function<int32_t(int, int)> emit = [&](int n, int depth) -> int32_t {
         out.qmax_depth = std::max(out.qmax_depth, depth);
         const TNode& t = tn[n];
         if (t.left < 0) {
-            int32_t start, count;
-            const int32_t c = (t.info >> dl::kLeafCountShift) & dl::kLeafMaxCount, st = t.info & dl::kLeafStartMask;
-            if (c != 0) { start = st; count = c; }
-            else { start = out.leaf_big[st].start; count = out.leaf_big[st].count; }
-            const size_t off = out.lrec.size();
-            if (off > (size_t)INT32_MAX - 1 - (2 + 3 * (size_t)count)) lrec_ok = false;
-            dl::LeafHead h{};
-            h.minx = t.box.lo[0]; h.miny = t.box.lo[1]; h.minz = t.box.lo[2]; h.count = count;
-            h.maxx = t.box.hi[0]; h.maxy = t.box.hi[1]; h.maxz = t.box.hi[2]; h.slot0 = start;
-            out.lrec.resize(off + 2 + 3 * (size_t)count);
-            std::memcpy(&out.lrec[off], &h, sizeof(h));
-            if (count > 0) std::memcpy(&out.lrec[off + 2], &out.prims[start], sizeof(dl::Prim) * (size_t)count);
-            return dl::kLeafBit | (int32_t)off;
+            if (t.rec < 0) contain_ok = false;
+            return dl::kLeafBit | t.rec;
         }
         std::vector<int> ch{t.left, t.right};
         while (ch.size() < 4) {
@@ -938,50 +1024,136 @@ void build_shadow_tree(FlatBVH& out, int threads) {
         const int me = (int)out.quads.size();
         out.quads.emplace_back();
         int32_t codes[4] = {INT32_MAX, INT32_MAX, INT32_MAX, INT32_MAX};
-        for (size_t i = 0; i < ch.size(); ++i) codes[i] = emit(ch[i], depth + 1);
-        dl::Quad q{};
-        const float o[3] = {t.box.lo[0], t.box.lo[1], t.box.lo[2]};
-        int e[3];
-        float sc[3];
-        for (int a = 0; a < 3; ++a) {
-            e[a] = 1;
-            const double ext = (double)t.box.hi[a] - o[a];
-            if (ext > 0) e[a] = std::max(1, std::min(254, (int)std::ceil(std::log2(ext / 255.0)) + 127));
-            while (e[a] < 254 && dec(o[a], 255, pow2(e[a])) < t.box.hi[a]) ++e[a];
-            sc[a] = pow2(e[a]);
+        float lo[4][3] = {}, hi[4][3] = {};
+        for (size_t i = 0; i < ch.size(); ++i) {
+            codes[i] = emit(ch[i], depth + 1);
+            for (int a = 0; a < 3; ++a) { lo[i][a] = tn[ch[i]].box.lo[a]; hi[i][a] = tn[ch[i]].box.hi[a]; }
         }
-        uint8_t ql[4][3] = {}, qh[4][3] = {};
-        for (size_t i = 0; i < ch.size(); ++i)
-            for (int a = 0; a < 3; ++a) {
-                const float lo = tn[ch[i]].box.lo[a], hi = tn[ch[i]].box.hi[a];
-                int qlo = (int)std::floor(((double)lo - o[a]) / sc[a]);
-                qlo = std::max(0, std::min(255, qlo));
-                while (qlo > 0 && dec(o[a], qlo, sc[a]) > lo) --qlo;
-                int qhi = (int)std::ceil(((double)hi - o[a]) / sc[a]);
-                qhi = std::max(0, std::min(255, qhi));
-                while (qhi < 255 && dec(o[a], qhi, sc[a]) < hi) ++qhi;
-                // the decoded box must contain the child's exact box (the device decodes identically)
-                if (dec(o[a], qlo, sc[a]) > lo || dec(o[a], qhi, sc[a]) < hi) contain_ok = false;
-                ql[i][a] = (uint8_t)qlo;
-                qh[i][a] = (uint8_t)qhi;
-            }
-        q.ox = o[0]; q.oy = o[1]; q.oz = o[2];
-        q.exps = (uint32_t)e[0] | (uint32_t)e[1] << 8 | (uint32_t)e[2] << 16 | (uint32_t)ch.size() << 24;
-        uint8_t bytes[24];
-        for (int i = 0; i < 4; ++i)
-            for (int a = 0; a < 3; ++a) { bytes[a * 4 + i] = ql[i][a]; bytes[12 + a * 4 + i] = qh[i][a]; }
-        std::memcpy(q.q, bytes, 24);
-        for (int i = 0; i < 4; ++i) q.child[i] = codes[i];
+        dl::Quad q;
+        if (!make_quad(lo, hi, codes, (1u << ch.size()) - 1u, 0u, q)) contain_ok = false;
         out.quads[me] = q;
         return me;
     };
     out.qroot = emit(root, 0);
+    if (!contain_ok || 3 * out.qmax_depth + 4 > dl::kMaxStack) out.quads.clear();   // binary occlusion tree only
+}
 
-    out.lrec.resize(out.lrec.size() + 3);    // a leaf's first-prim loads may run past a 0-prim last leaf
-    if (!contain_ok || !lrec_ok || 3 * out.qmax_depth + 4 > dl::kMaxStack) {   // fall back to the binary tree
-        out.quads.clear();
-        out.lrec.clear();
+// Reference-order wide tree for closest-hit walks: the reference BVH collapsed
+// to dl::Wide nodes of up to dl::kWideSlots children.  The node of interior
+// node N holds a frontier of nodes below N, grown from N's two children by
+// repeatedly replacing the interior slot of largest box area by its two
+// children (as the occlusion tree's collapse does), slots kept in pre-order.
+// The reference visits the nodes below N in DFS order, the left child first
+// iff d[axis] > 0 at every expanded node (raytracer.cpp:200-206), so the
+// visiting order of the slots is a function of the octant of d alone: the
+// node stores, per octant, each slot's rank in that order.  The walk over it
+// (traverse2.hpp wide_closest_step) is exact for NaN-free rays: it visits the
+// reference's leaves in the reference's order with the same tMax (see there).
+// Returns false when a decoded box does not contain its child's box or a walk
+// could overflow the device stack (the walk then keeps the binary tree).
+bool build_ref_wide(FlatBVH& out) {
+    constexpr int W = dl::kWideSlots;
+    out.wnodes.clear();
+    out.wmax_stack = 0;
+    if (out.nodes.empty()) return true;
+    if (out.root_info < 0) {                 // a single leaf
+        out.wroot = dl::kLeafBit | out.root_lrec;
+        return out.root_lrec >= 0;
     }
+    bool ok = true;
+    struct Slot { int32_t info, rec; float lo[3], hi[3]; };   // info: pair index or < 0 (leaf)
+    auto kids = [&](int32_t pi, Slot* a, Slot* b) {
+        const dl::Pair& P = out.pairs[pi];
+        *a = Slot{P.l_info, out.pair_lrec[2 * pi], {P.l_minx, P.l_miny, P.l_minz}, {P.l_maxx, P.l_maxy, P.l_maxz}};
+        *b = Slot{P.r_info, out.pair_lrec[2 * pi + 1], {P.r_minx, P.r_miny, P.r_minz}, {P.r_maxx, P.r_maxy, P.r_maxz}};
+        return P.axis;
+    };
+    auto area = [](const Slot& c) {
+        const double dx = (double)c.hi[0] - c.lo[0], dy = (double)c.hi[1] - c.lo[1], dz = (double)c.hi[2] - c.lo[2];
+        return dx * dy + dy * dz + dz * dx;
+    };
+    // returns the node index; *stack = worst-case stack entries of a walk from this node down
+    std::function<int32_t(int32_t, int*)> emit = [&](int32_t pi, int* stack) -> int32_t {
+        // expansion tree over slot ranges: split (axis, lo, mid, hi) cuts [lo, hi) at mid
+        struct Split { int axis, lo, mid, hi; };
+        std::vector<Slot> fr(2);
+        std::vector<Split> sp{{kids(pi, &fr[0], &fr[1]), 0, 1, 2}};
+        while ((int)fr.size() < W) {
+            int best = -1;
+            double ba = -1.0;
+            for (size_t i = 0; i < fr.size(); ++i)
+                if (fr[i].info >= 0 && area(fr[i]) > ba) { ba = area(fr[i]); best = (int)i; }
+            if (best < 0) break;
+            Slot a, b;
+            const int ax = kids(fr[best].info, &a, &b);
+            fr[best] = a;
+            fr.insert(fr.begin() + best + 1, b);
+            for (Split& e : sp) {
+                if (e.lo > best) e.lo++;
+                if (e.mid > best) e.mid++;
+                if (e.hi > best) e.hi++;
+            }
+            sp.push_back({ax, best, best + 1, best + 2});
+        }
+        const int n = (int)fr.size();
+        dl::Wide w{};
+        for (int oct = 0; oct < 8; ++oct) {
+            int order[8], no = 0;
+            std::function<void(int, int)> visit = [&](int lo, int hi) {
+                if (hi - lo == 1) { if (no < 8) order[no++] = lo; return; }
+                for (const Split& e : sp)
+                    if (e.lo == lo && e.hi == hi) {
+                        const bool left_first = (oct >> e.axis) & 1;
+                        if (left_first) { visit(e.lo, e.mid); visit(e.mid, e.hi); }
+                        else { visit(e.mid, e.hi); visit(e.lo, e.mid); }
+                        return;
+                    }
+                ok = false;
+            };
+            visit(0, n);
+            if (no != n) ok = false;
+            uint32_t rw = 0;
+            for (int r = 0; r < no; ++r) rw |= (uint32_t)r << (3 * order[r]);
+            for (int j = n; j < 8; ++j) rw |= 7u << (3 * j);             // empty slots: never valid
+            w.rank[oct] = rw;
+        }
+        const int me = (int)out.wnodes.size();
+        out.wnodes.emplace_back();
+        float lo[8][3] = {}, hi[8][3] = {};
+        int deepest = 0;
+        for (int i = 0; i < 8; ++i) w.child[i] = INT32_MAX;
+        for (int i = 0; i < n; ++i) {
+            std::memcpy(lo[i], fr[i].lo, sizeof(lo[i]));
+            std::memcpy(hi[i], fr[i].hi, sizeof(hi[i]));
+            if (fr[i].info < 0) {
+                if (fr[i].rec < 0) ok = false;
+                w.child[i] = dl::kLeafBit | fr[i].rec;
+            } else {
+                int st = 0;
+                w.child[i] = emit(fr[i].info, &st);
+                deepest = std::max(deepest, st);
+            }
+        }
+        // a step pushes at most n - 1 entries, then continues below one of them
+        *stack = n - 1 + deepest;
+        float o[3];
+        int e[3];
+        uint8_t ql[8][3], qh[8][3];
+        const unsigned mask = (1u << n) - 1u;
+        if (!quantize_boxes(lo, hi, n, mask, o, e, ql, qh)) ok = false;
+        w.ox = o[0]; w.oy = o[1]; w.oz = o[2];
+        w.exps = (uint32_t)e[0] | (uint32_t)e[1] << 8 | (uint32_t)e[2] << 16 | mask << 24;
+        uint8_t bytes[48] = {};
+        for (int i = 0; i < n; ++i)
+            for (int a = 0; a < 3; ++a) { bytes[a * 8 + i] = ql[i][a]; bytes[24 + a * 8 + i] = qh[i][a]; }
+        std::memcpy(w.q, bytes, 48);
+        out.wnodes[me] = w;
+        return me;
+    };
+    int stack = 0;
+    out.wroot = emit(out.root_info, &stack);
+    out.wmax_stack = stack + 1;
+    return ok && out.wmax_stack <= dl::kMaxStack;
 }
 
 }  // namespace rtx

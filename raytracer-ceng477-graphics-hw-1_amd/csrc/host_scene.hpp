@@ -62,11 +62,19 @@ struct FlatBVH {
     float sroot_lo[3] = {0, 0, 0}, sroot_hi[3] = {0, 0, 0};
     int32_t sroot_info = 0;
     int smax_depth = 0;
-    // the same occlusion tree collapsed to 4-wide nodes with quantized child boxes
+    // leaf records (LeafHead + prims), 16-B units, one per reference leaf in
+    // pre-order, + 3 units of tail pad; shared by both 4-wide trees
+    std::vector<dl::Vec4> lrec;
+    std::vector<int32_t> pair_lrec;  // [2 * pair + side]: leaf record offset of a leaf child, else -1
+    int32_t root_lrec = -1;          // the root's record when the root is a leaf
+    // the occlusion tree collapsed to 4-wide nodes with quantized child boxes (any-hit walks)
     std::vector<dl::Quad> quads;
-    std::vector<dl::Vec4> lrec;      // leaf records (LeafHead + prims), 16-B units, + 3 units of tail pad
     int32_t qroot = 0;               // >= 0 quad index, < 0 kLeafBit | leaf-record offset
     int qmax_depth = 0;
+    // the reference tree collapsed to wide nodes (closest-hit walks, reference order)
+    std::vector<dl::Wide> wnodes;
+    int32_t wroot = 0;
+    int wmax_stack = 0;              // worst-case stack entries of a walk over them
     int leaves = 0, max_leaf = 0, max_depth = 0, max_stack = 0;
     double build_ms = 0;
     double ref_ms = 0, flat_ms = 0, stree_ms = 0;

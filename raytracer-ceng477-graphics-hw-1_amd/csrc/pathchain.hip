@@ -37,9 +37,6 @@ constexpr int kBlock = 256;
 #define RT_WAVES_PER_EU 4     // k_chain: 4 waves/SIMD (118 VGPRs).  One frame at a time 5 waves (96 VGPRs)
                               // won (1.36 -> 1.32 ms); with frame batches 4 wins (0.81-0.82 -> 0.79-0.80 ms/frame)
 #endif
-#ifndef RT_WIDE_B
-#define RT_WIDE_B 0           // wide walks for phase-B tails (RT_WIDE > 0 at run time)
-#endif
 #ifndef RT_FINISH_PREFETCH
 #define RT_FINISH_PREFETCH 1   // k_finish: next level's record in flight while shading
 #endif
@@ -145,141 +142,6 @@ __device__ __forceinline__ unsigned block_sample(unsigned v, unsigned G, unsigne
         u = (grp * spread + j % spread) * 64u + j / spread;
     }
     return unit * 256u + u;
-}
-
-// ---------------------------------------------------------------------------
-// Whole-wave walks: one ray, the whole wave (coop_closest below).
-// ---------------------------------------------------------------------------
-struct WideOut {
-    float t;
-    int prim;     // closest: winner slot or -1; any: 1 = occluded
-    int status;   // 0 = exact result, 1 = fall back to the narrow walk
-};
-
-__device__ __forceinline__ Ray ray_bcast(const Ray& r, int L) {
-    Ray q;
-    q.o = V{__shfl(r.o.x, L, 64), __shfl(r.o.y, L, 64), __shfl(r.o.z, L, 64)};
-    q.d = V{__shfl(r.d.x, L, 64), __shfl(r.d.y, L, 64), __shfl(r.d.z, L, 64)};
-    q.inv = V{__shfl(r.inv.x, L, 64), __shfl(r.inv.y, L, 64), __shfl(r.inv.z, L, 64)};
-    return q;
-}
-
-__device__ __forceinline__ float wave_minf(float v) {
-    for (int off = 32; off > 0; off >>= 1) v = fminf(v, __shfl_xor(v, off, 64));
-    return v;
-}
-// ---------------------------------------------------------------------------
-// Cooperative certified closest hit: one ray, the whole wave, over the 4-wide
-// tree (traverse2.hpp, comment at Walk).  The wave keeps a stack of items
-// {node or leaf code, entry t} in LDS and expands up to 64 of them per round,
-// one per lane: a quad yields its children whose (conservative) box the ray
-// hits with entry t <= sah_bound(best); a leaf record is tested exactly (exact
-// box, then its primitives in order).  best is the wave minimum after every
-// round.  Every leaf whose entry t is <= sah_bound(t_final) is visited, as in
-// the one-lane walk, so the same certification applies: the winner's t must
-// be a strict minimum (no other hit with t <= t_w, no negative or NaN t), and
-// its leaf entry t blt <= t_w, or blt <= sah_late(t_w) with every other hit at
-// or beyond blt.  A heavy walk of ~40 dependent rounds takes ~tree-depth
-// rounds here.  status 1: stack overflow or not certified (narrow walk).
-// ---------------------------------------------------------------------------
-constexpr int kCoopCap = 128;                              // items per wave
-__shared__ int g_ccode[(kBlock / 64) * kCoopCap];          // quad index or leaf code
-__shared__ float g_ct[(kBlock / 64) * kCoopCap];           // entry t
-
-__device__ WideOut coop_closest(const rtk::DevScene& s, const Ray& R) {
-    const int lane = (int)(threadIdx.x & 63);
-    const int base = (int)(threadIdx.x >> 6) * kCoopCap;
-    const float kInf = __int_as_float(0x7f800000);
-    float bt = kInf, bt2 = kInf, bl = kInf;    // lane-local: best t, second t, best's leaf entry t
-    int bp = -1;
-    bool bad = false;
-    if (lane == 0) {
-        g_ccode[base] = s.qroot;
-        g_ct[base] = 0.0f;
-    }
-    int top = 1;
-    float tb = kInf;                            // wave-uniform best t so far
-    while (top > 0) {
-        const int n = min(64, top);
-        top -= n;
-        const float bound = tb < kInf ? sah_bound(tb) : kInf;
-        int code = 0;
-        float tin = kInf;
-        const bool has = lane < n;
-        if (has) {
-            code = g_ccode[base + top + lane];
-            tin = g_ct[base + top + lane];
-        }
-        int nc = 0;
-        int cc[4] = {0, 0, 0, 0};
-        float ct[4] = {0.0f, 0.0f, 0.0f, 0.0f};
-        bool cv[4] = {false, false, false, false};
-        if (has && tin <= bound) {
-            if (code >= 0) {
-                QuadHits q;
-                quad_hits(s, code, R, q);
-#pragma unroll
-                for (int i = 0; i < 4; ++i) {
-                    cv[i] = q.hit[i] && q.t[i] <= bound;
-                    cc[i] = q.code[i];
-                    ct[i] = q.t[i];
-                    nc += cv[i] ? 1 : 0;
-                }
-            } else {
-                const float4* L = s.lrec + (code & ~dl::kLeafBit);
-                const float4 h0 = L[0], h1 = L[1], c0 = L[2], c1 = L[3], c2 = L[4];
-                float lt;
-                if (box_hit_fast(R, h0, h1, &lt) && lt <= bound) {
-                    for_leaf_prims(L, __float_as_int(h1.w), __float_as_int(h0.w), c0, c1, c2,
-                                   [&](int slot, const float4& p0, const float4& p1, const float4& p2) {
-                                       float t;
-                                       const bool h = __float_as_int(p0.w) >= 0 ? tri_hit(R, p0, p1, p2, &t)
-                                                                                : sphere_hit(R, p0, p1, &t);
-                                       if (h) {
-                                           if (!(t >= 0.0f)) bad = true;
-                                           if (t < bt) {
-                                               bt2 = fminf(bt2, bt);
-                                               bt = t;
-                                               bp = slot;
-                                               bl = lt;
-                                           } else {
-                                               bt2 = fminf(bt2, t);
-                                           }
-                                       }
-                                       return false;
-                                   });
-                }
-            }
-        }
-        tb = wave_minf(bt);
-        // push the children: exclusive prefix of the per-lane counts
-        int inc = nc;
-        for (int off = 1; off < 64; off <<= 1) {
-            const int y = __shfl_up(inc, off, 64);
-            if (lane >= off) inc += y;
-        }
-        const int total = __shfl(inc, 63, 64);
-        if (top + total > kCoopCap) return WideOut{-1.0f, -1, 1};
-        int w = base + top + inc - nc;
-#pragma unroll
-        for (int i = 0; i < 4; ++i)
-            if (cv[i]) {
-                g_ccode[w] = cc[i];
-                g_ct[w] = ct[i];
-                ++w;
-            }
-        top += total;
-    }
-    if (__any(bad)) return WideOut{-1.0f, -1, 1};
-    if (!(tb < kInf)) return WideOut{-1.0f, -1, 0};            // no hit in any reachable leaf
-    const unsigned long long win = __ballot(bt == tb);
-    if (__popcll(win) != 1) return WideOut{-1.0f, -1, 1};      // a tie across lanes
-    const int W = __ffsll((unsigned long long)win) - 1;
-    const float t2 = wave_minf(lane == W ? bt2 : bt);
-    const float blt = __shfl(bl, W, 64);
-    const int prim = __shfl(bp, W, 64);
-    const bool ok = sah_certified(tb, t2, blt);
-    return ok ? WideOut{tb, prim, 0} : WideOut{-1.0f, -1, 1};
 }
 
 // ---------------------------------------------------------------------------
@@ -599,7 +461,7 @@ __device__ uint32_t bq_consume(const rtk::DevScene& s, const PcParams& p, WalkSt
         }
         if (active) {
             const int res = occl_step<COUNT, FetchTop>(s, r, tlim, stk, wk, w);
-            if (res) {
+            if (res || walk_runaway(s, wk)) {
                 p.occ[owner] = res == 2 ? 1 : 0;
                 active = false;
             }
@@ -610,7 +472,7 @@ __device__ uint32_t bq_consume(const rtk::DevScene& s, const PcParams& p, WalkSt
 
 // closest-hit chains of one phase (raytracer.cpp:385-439 minus the shading):
 // record each hit, queue its shadow tasks, follow (or hand on) mirrors.
-template <bool COUNT, bool CONT, bool WIDE = false>
+template <bool COUNT, bool CONT>
 __device__ void chain_body(const rtk::DevScene& s, const rtk::Eye& e, const PcParams& p, unsigned blk, unsigned G,
                            const PhaseOut& o) {
     WalkStack stk;
@@ -628,8 +490,6 @@ __device__ void chain_body(const rtk::DevScene& s, const rtk::Eye& e, const PcPa
     Ray r;
     Walk wk;
     unsigned t_grab = 0;
-    int wsteps = 0;          // narrow steps of the current walk (wide-walk trigger)
-    bool nowide = false;     // the wide walk fell back for this walk
     bool fresh = false;      // lane just took an eye ray (packet walk pending)
     while (true) {
         // (1) epilogue of finished walks: record, queue shadow tasks, reflect or hand on
@@ -703,8 +563,6 @@ __device__ void chain_body(const rtk::DevScene& s, const rtk::Eye& e, const PcPa
                 r = reflect_from_record(s, p, (size_t)k * p.cap + path);
                 ++k;
                 nrefl++;
-                wsteps = nowide ? 0 : (wsteps < 0 ? p.wide_min : 0);
-                nowide = false;
                 st = walk_begin<COUNT>(s, r, wk, w) ? kTrav : kDone;
             }
         }
@@ -724,16 +582,12 @@ __device__ void chain_body(const rtk::DevScene& s, const rtk::Eye& e, const PcPa
                             k = (int)(lvp / (unsigned)p.cap) + 1;
                             r = reflect_from_record(s, p, lvp);
                             nrefl++;
-                            wsteps = 0;
-                            nowide = false;
                             st = walk_begin<COUNT>(s, r, wk, w) ? kTrav : kDone;
                         } else {
                             const unsigned idx = (blk + (v >> 8) * G) * 256u + (v & 255u);
                             if (slab_sample_ray(e, p, idx, &r)) {
                                 path = idx;
                                 k = 0;
-                                wsteps = 0;
-                                nowide = false;
                                 if (p.trace) t_grab = (unsigned)wall_clock64();
                                 nprim++;
                                 if (s.max_depth < 0) p.pinfo[path] = 0 | (kEndZero << 8);   // depth 0 > max: black
@@ -765,58 +619,13 @@ __device__ void chain_body(const rtk::DevScene& s, const rtk::Eye& e, const PcPa
         }
         // (3) walk until enough lanes need service
         const int thresh = exhausted ? 0 : (CONT ? p.brefill : p.refill);
-        if (WIDE && !COUNT && p.wide > 0) {
-            // tail: a few long walks left in this wave -> each one with the whole wave
-            const int nt = __popcll(__ballot(st == kTrav));
-            const unsigned long long wable = __ballot(st == kTrav && !nowide && (wsteps < 0 || wsteps >= p.wide_min));
-            if (wable && nt <= p.wide && nt > thresh) {
-                unsigned long long m = wable;
-                while (m) {
-                    const int L = __ffsll((unsigned long long)m) - 1;
-                    m &= m - 1;
-                    const bool quad = __shfl((int)(wk.tree == nullptr), L, 64) != 0;
-                    const WideOut wo = quad ? coop_closest(s, ray_bcast(r, L)) : WideOut{-1.0f, -1, 1};
-                    if (lane_id() == L) {
-                        if (wo.status == 0) {
-                            wk.best = HitRec{wo.t, wo.prim};
-                            st = kDone;
-                            wsteps = -1;           // heavy chain: let its next walk go wide at once
-                        } else {
-                            nowide = true;
-                        }
-                    }
-                }
-                continue;
-            }
-        }
         while (true) {
             const int nt = __popcll(__ballot(st == kTrav));
             if (nt <= thresh ||
                 __popcll(__ballot(st == kDone)) >= (CONT ? (exhausted ? p.btail : p.bservice) : p.service))
                 break;
-            if (WIDE && !COUNT && p.wide > 0 && nt <= p.wide &&
-                __ballot(st == kTrav && !nowide && (wsteps < 0 || wsteps >= p.wide_min)))
-                break;
             if (st == kTrav) {
-                ++wsteps;
-#ifdef RT_WALK_TRACE_PATH
-                const int c0 = wk.cur, sp0 = wk.sp;
-#endif
-                if (closest_step<COUNT, FetchTop, WalkStack, CONT>(s, r, stk, wk, w)) st = kDone;
-#ifdef RT_WALK_TRACE_PATH
-                if (path == RT_WALK_TRACE_PATH && k == 0 && wsteps < 40)
-                    printf("TRACE step %d cur %d sp %d -> cur %d sp %d st %d tree %p pairs %p root %d best %a/%d t2 %a blt %a\n",
-                           wsteps, c0, sp0, wk.cur, wk.sp, st, (const void*)wk.tree, (const void*)s.pairs, s.root_info,
-                           wk.best.t, wk.best.prim, wk.t2, wk.blt);
-#endif
-#ifdef RT_WALK_CAP
-                if (st == kTrav && wsteps > RT_WALK_CAP) {   // diagnostics build: report a runaway walk
-                    printf("RUNAWAY path %u k %d tree %d sp %d cur %d tmax %a best %a/%d o %a %a %a d %a %a %a\n", path, k,
-                           wk.tree == nullptr ? 4 : (wk.tree == s.pairs ? 2 : 1), wk.sp, wk.cur, wk.tmax, wk.best.t,
-                           wk.best.prim, r.o.x, r.o.y, r.o.z, r.d.x, r.d.y, r.d.z);
-                    st = kDone;
-                }
-#endif
+                if (closest_step<COUNT, FetchTop, WalkStack, CONT>(s, r, stk, wk, w) || walk_runaway(s, wk)) st = kDone;
             }
         }
     }
@@ -838,351 +647,6 @@ __device__ void chain_body(const rtk::DevScene& s, const rtk::Eye& e, const PcPa
         wave_add_counter(&p.counters[4], w.tris);
         wave_add_counter(&p.counters[5], w.spheres);
     }
-}
-
-// ---------------------------------------------------------------------------
-// Phase B with four lanes per ray.  A lone wave's walk step is bound by its own
-// instruction latency (~1,750 cycles per 4-wide step, rt_walk_timing), and the
-// frame's tail is a few long serial mirror chains.  Here a group of 4 lanes
-// (a DPP quad) walks one ray of the certified 4-wide walk (traverse2.hpp,
-// comment at Walk): lane q decodes and tests child q of a node, the group
-// picks the nearest with two DPP exchanges and each other hit child pushes
-// itself at its rank (farthest deepest); a leaf's primitives are tested four
-// at a time and reduced.  All group state is replicated in the 4 lanes.  The
-// group's stack is the 4 lanes' LDS stack columns (48 entries, entry e in
-// column e & 3, row e >> 2).  Same visit set and certification as the
-// one-lane walk; a group that overflows its stack, meets a ray that may
-// produce NaN slab values or fails certification restarts the ray on the
-// reference tree with its lane 0 (closest_step).
-// ---------------------------------------------------------------------------
-#ifndef RT_QUAD4
-#define RT_QUAD4 1
-#endif
-constexpr int kG4Stack = 4 * kLdsStackEntries;
-constexpr int kDppX1 = 0xB1, kDppX2 = 0x4E, kDppX3 = 0x1B;   // quad_perm lane ^ 1, ^ 2, ^ 3
-
-template <int CTRL>
-__device__ __forceinline__ int dpp_i(int v) { return __builtin_amdgcn_update_dpp(v, v, CTRL, 0xF, 0xF, false); }
-template <int CTRL>
-__device__ __forceinline__ float dpp_f(float v) { return __int_as_float(dpp_i<CTRL>(__float_as_int(v))); }
-
-__device__ __forceinline__ void g4_put(int e, int2 v) {
-    g_lstk[(e >> 2) * kBlock + (threadIdx.x & ~3u) + (e & 3)] = v;
-}
-__device__ __forceinline__ int2 g4_at(int e) { return g_lstk[(e >> 2) * kBlock + (threadIdx.x & ~3u) + (e & 3)]; }
-
-struct Walk4 {
-    int cur, sp;
-    float tmax;       // pruning bound sah_bound(best)
-    float bt;         // best t (valid when bp >= 0)
-    int bp;           // best primitive slot
-    float blt, t2;    // certification: winner's leaf entry t, smallest other hit t
-    bool bad;         // a hit with t < 0 or NaN
-    bool fail;        // restart on the reference tree
-};
-
-__device__ __forceinline__ void walk4_begin(const rtk::DevScene& s, Walk4& k) {
-    k.cur = s.qroot;
-    k.sp = 0;
-    k.tmax = FLT_MAX;
-    k.bt = -1.0f;
-    k.bp = -1;
-    k.blt = __builtin_inff();
-    k.t2 = __builtin_inff();
-    k.bad = false;
-    k.fail = false;
-}
-
-// One group step; true when the walk is finished (result in k, or k.fail).
-__device__ __forceinline__ bool quad4_step(const rtk::DevScene& s, const Ray& r, Walk4& k) {
-    const int q = (int)(threadIdx.x & 3);
-    const float kInf = __builtin_inff();
-    if (k.cur >= 0) {
-        const float4* Q = reinterpret_cast<const float4*>(&s.quads[k.cur]);
-        const float4 q0 = Q[0], q1 = Q[1], q2 = Q[2], q3 = Q[3];
-        const uint32_t ex = __float_as_uint(q0.w);
-        const int n = (int)(ex >> 24);
-        // this lane's lo and hi bytes: byte q of the axis dwords q1.xyz (lo) and q1.w q2.xy (hi)
-        const uint32_t sh = 8u * (uint32_t)q;
-        const uint32_t lb = ((__float_as_uint(q1.x) >> sh) & 255u) | (((__float_as_uint(q1.y) >> sh) & 255u) << 8) |
-                            (((__float_as_uint(q1.z) >> sh) & 255u) << 16);
-        const uint32_t hb = ((__float_as_uint(q1.w) >> sh) & 255u) | (((__float_as_uint(q2.x) >> sh) & 255u) << 8) |
-                            (((__float_as_uint(q2.y) >> sh) & 255u) << 16);
-        const int code = q == 0 ? __float_as_int(q2.z) : q == 1 ? __float_as_int(q2.w)
-                       : q == 2 ? __float_as_int(q3.x) : __float_as_int(q3.y);
-        const float sx = __uint_as_float((ex & 255u) << 23), sy = __uint_as_float(((ex >> 8) & 255u) << 23),
-                    sz = __uint_as_float(((ex >> 16) & 255u) << 23);
-        const float lx = __builtin_fmaf((float)(lb & 255u), sx, q0.x), ly = __builtin_fmaf((float)((lb >> 8) & 255u), sy, q0.y),
-                    lz = __builtin_fmaf((float)((lb >> 16) & 255u), sz, q0.z);
-        const float hx = __builtin_fmaf((float)(hb & 255u), sx, q0.x), hy = __builtin_fmaf((float)((hb >> 8) & 255u), sy, q0.y),
-                    hz = __builtin_fmaf((float)((hb >> 16) & 255u), sz, q0.z);
-        float t;
-        const bool hit = box_hit_fast(r, make_float4(lx, ly, lz, 0.0f), make_float4(hx, hy, hz, 0.0f), &t);
-        const bool valid = q < n && hit && t <= k.tmax;
-        const float key = valid ? t : kInf;
-        // nearest child: lexicographic minimum of (key, lane)
-        const float k1 = dpp_f<kDppX1>(key), k2 = dpp_f<kDppX2>(key), k3 = dpp_f<kDppX3>(key);
-        const int c1 = dpp_i<kDppX1>(code), c2 = dpp_i<kDppX2>(code), c3 = dpp_i<kDppX3>(code);
-        float m = key;
-        int mi = q;
-        auto take = [&](float kj, int j) {
-            if (kj < m || (kj == m && j < mi)) { m = kj; mi = j; }
-        };
-        take(k1, q ^ 1);
-        take(k2, q ^ 2);
-        take(k3, q ^ 3);
-        const int nv = (key < kInf) + (k1 < kInf) + (k2 < kInf) + (k3 < kInf);
-        if (nv > 0) {
-            // push the other hit children, farthest deepest: my slot = number of other
-            // non-nearest hit children ordered after me (larger key, ties by lane)
-            if (valid && mi != q) {
-                int pos = 0;
-                auto after = [&](float kj, int j) {
-                    if (kj < kInf && j != mi && (kj > key || (kj == key && j < q))) ++pos;
-                };
-                after(k1, q ^ 1);
-                after(k2, q ^ 2);
-                after(k3, q ^ 3);
-                const int e = k.sp + pos;
-                if (e < kG4Stack) g4_put(e, make_int2(code, __float_as_int(key)));
-            }
-            k.sp += nv - 1;
-            if (k.sp > kG4Stack) {
-                k.fail = true;
-                return true;
-            }
-            const int d = mi ^ q;
-            k.cur = d == 0 ? code : d == 1 ? c1 : d == 2 ? c2 : c3;
-            return false;
-        }
-    } else {
-        const float4* L = s.lrec + (k.cur & ~dl::kLeafBit);
-        const float4 h0 = L[0], h1 = L[1];
-        float lt;
-        if (box_hit_fast(r, h0, h1, &lt) && lt <= k.tmax) {   // the reference leaf's exact box
-            const int cnt = __float_as_int(h0.w), slot0 = __float_as_int(h1.w);
-            float m1 = kInf, m2 = kInf;
-            int ms = -1;
-            bool bad = false;
-            for (int j = q; j < cnt; j += 4) {
-                const float4* pr = L + 2 + 3 * j;
-                const float4 p0 = pr[0], p1 = pr[1], p2 = pr[2];
-                float ti;
-                const bool h = __float_as_int(p0.w) >= 0 ? tri_hit(r, p0, p1, p2, &ti) : sphere_hit(r, p0, p1, &ti);
-                if (h) {
-                    if (!(ti >= 0.0f)) bad = true;
-                    if (ti < m1) {
-                        m2 = fminf(m2, m1);
-                        m1 = ti;
-                        ms = slot0 + j;
-                    } else {
-                        m2 = fminf(m2, ti);
-                    }
-                }
-            }
-            // group reduction of (m1, slot, m2): two butterfly rounds
-            auto merge = [&](float o1, int os, float o2) {
-                const bool lt_ = o1 < m1 || (o1 == m1 && os >= 0 && (ms < 0 || os < ms));
-                const float hi = lt_ ? m1 : o1;
-                m2 = fminf(fminf(m2, o2), hi);
-                if (lt_) { m1 = o1; ms = os; }
-            };
-            merge(dpp_f<kDppX1>(m1), dpp_i<kDppX1>(ms), dpp_f<kDppX1>(m2));
-            merge(dpp_f<kDppX2>(m1), dpp_i<kDppX2>(ms), dpp_f<kDppX2>(m2));
-            const int b1 = dpp_i<kDppX1>((int)bad) | (int)bad;
-            bad = (dpp_i<kDppX2>(b1) | b1) != 0;
-            if (bad) k.bad = true;
-            if (ms >= 0) {
-                if (k.bp < 0 || m1 < k.bt) {
-                    if (k.bp >= 0) k.t2 = fminf(k.t2, k.bt);
-                    k.t2 = fminf(k.t2, m2);
-                    k.bt = m1;
-                    k.bp = ms;
-                    k.blt = lt;
-                    k.tmax = sah_bound(m1);
-                } else {
-                    k.t2 = fminf(k.t2, m1);
-                }
-            }
-        }
-    }
-    while (k.sp > 0) {
-        --k.sp;
-        const int2 e = g4_at(k.sp);
-        if (__int_as_float(e.y) <= k.tmax) {
-            k.cur = e.x;
-            return false;
-        }
-    }
-    if (k.bad) k.fail = true;
-    else if (k.bp >= 0) {
-        const float tw = k.bt;
-        k.fail = !sah_certified(tw, k.t2, k.blt);
-    }
-    return true;
-}
-
-// Phase B chains (raytracer.cpp:385-439 minus the shading), one ray per group
-// of 4 lanes; non-counting builds only (the counting pass walks the reference
-// tree with chain_body).
-__device__ void chain4_body(const rtk::DevScene& s, const PcParams& p, unsigned blk, unsigned G, const PhaseOut& o) {
-    WalkStack stk;           // lane 0's private stack for reference-tree restarts
-    Work w;
-    const int nl = s.nlights;
-    const int q = (int)(threadIdx.x & 3);
-    const int lead = (int)(threadIdx.x & 63) & ~3;   // the group's lane 0 in the wave
-    const unsigned nb = chunk_count(p.totals[1], G, blk, (unsigned)p.tchunk);
-    unsigned* const sq = o.sq + (size_t)blk * o.scap;
-    int st = kIdle;
-    bool exhausted = nb == 0;
-    unsigned path = 0;
-    int k = 0;
-    Ray r;
-    Walk4 w4;
-    Walk wk;
-    bool ref = false;        // walking on the reference tree (lane 0)
-    HitRec best{-1.0f, -1};
-    auto start_walk = [&]() {
-        ref = !(ray_nan_free(r) && s.use_sclosest);
-        if (!ref) {
-            walk4_begin(s, w4);
-            st = kTrav;
-        } else {
-            const bool go = walk_begin<false>(s, r, wk, w);     // NaN-capable ray: reference tree
-            st = go ? kTrav : kDone;
-            best = HitRec{-1.0f, -1};
-        }
-    };
-    while (true) {
-        // (1) epilogue of finished walks (all 4 lanes compute; lane 0 writes)
-        if (st == kDone) {
-            const HitRec h = best;
-            const bool hit = h.prim >= 0;
-            V nn{0.0f, 0.0f, 0.0f}, hitp{0.0f, 0.0f, 0.0f};
-            int mat = 0;
-            if (hit) {
-                hit_surface(s, r, h, &nn, &mat);
-                hitp = add(r.o, mul(r.d, h.t));
-                if (q == 0) {
-                    float4* rc = p.rec + ((size_t)k * p.cap + path) * 3;
-                    rc[0] = make_float4(hitp.x, hitp.y, hitp.z, __int_as_float(mat));
-                    rc[1] = make_float4(nn.x, nn.y, nn.z, h.t);
-                    rc[2] = make_float4(r.d.x, r.d.y, r.d.z, 0.0f);
-                }
-            }
-            const bool hit0 = hit && q == 0;
-            const unsigned long long hm = __ballot(hit0);
-            bool queued = false;
-            if (kBq > 0 && hm) {
-                __builtin_amdgcn_s_waitcnt(0);     // the record stores have completed (see chain_body)
-                const unsigned cnt = (unsigned)__popcll(hm), need = cnt * (unsigned)nl;
-                const int leader = __ffsll((unsigned long long)hm) - 1;
-                unsigned base = 0;
-                if (lane_id() == leader) base = atomicAdd(&g_bq_tail, need);
-                base = __shfl(base, leader, 64);
-                const unsigned rank = lane_rank(hm);
-                const unsigned own0 = (unsigned)(((size_t)k * p.cap + path) * nl);
-                if (base + need <= (unsigned)p.bq_cap) {
-                    if (hit0)
-                        for (int l = 0; l < nl; ++l)
-                            __atomic_store_n(&g_bq[base + l * cnt + rank], own0 + (unsigned)l, __ATOMIC_RELAXED);
-                    queued = true;
-                } else if (hit0) {
-                    for (int l = 0; l < nl; ++l) {
-                        const unsigned qq = base + l * cnt + rank;
-                        if (qq < (unsigned)p.bq_cap) __atomic_store_n(&g_bq[qq], kBqSkip, __ATOMIC_RELAXED);
-                    }
-                }
-            }
-            if (hit0 && !queued) {
-                const unsigned cnt = (unsigned)__popcll(hm);
-                const unsigned base = wave_grab_lds(&g_scnt, hm);
-                const unsigned rank = lane_rank(hm);
-                const unsigned own0 = (unsigned)(((size_t)k * p.cap + path) * nl);
-                for (int l = 0; l < nl; ++l) sq[base * nl + l * cnt + rank] = own0 + (unsigned)l;
-            }
-            bool ends = true;
-            int info = 0;
-            if (!hit) {                                                          // :442-449
-                info = k | ((k == 0 ? kEndBg : kEndZero) << 8);
-            } else if (!s.mats[mat - 1].is_mirror) {
-                info = (k + 1) | (kEndLast << 8);
-            } else if (k >= s.max_depth) {        // child beyond MaxRecursionDepth: 0 (:387-389)
-                info = (k + 1) | (kEndZero << 8);
-            } else {
-                ends = false;
-            }
-            if (ends) {
-                if (q == 0) p.pinfo[path] = info;
-                st = kIdle;
-            } else {
-                r = reflect_from_record_regs(s, hitp, nn, r.d);
-                ++k;
-                start_walk();
-            }
-        }
-        // (2) refill idle groups with continuations
-        if (!exhausted) {
-            const unsigned long long idle = __ballot(st == kIdle && q == 0);
-            if (idle) {
-                const int leader = __ffsll((unsigned long long)idle) - 1;
-                unsigned base = 0;
-                if (lane_id() == leader) base = atomicAdd(&g_head, (unsigned)__popcll(idle));
-                base = __shfl(base, leader, 64);
-                if (base + (unsigned)__popcll(idle) >= nb) exhausted = true;
-                if (st == kIdle) {
-                    const unsigned v = base + (unsigned)__popcll(idle & ((1ull << lead) - 1ull));
-                    if (v < nb) {
-                        const unsigned j = chunk_task(v, G, blk, (unsigned)p.tchunk);
-                        const unsigned lvp = p.cflat[j];
-                        path = lvp % (unsigned)p.cap;
-                        k = (int)(lvp / (unsigned)p.cap) + 1;
-                        r = reflect_from_record(s, p, lvp);
-                        start_walk();
-                    }
-                }
-            }
-        }
-        if (!__any(st != kIdle)) {
-            if (exhausted) break;
-            continue;
-        }
-        // (3) walk until enough groups need service
-        const int thresh = exhausted ? 0 : p.brefill / 4;
-        while (true) {
-            const int nt = __popcll(__ballot(st == kTrav && q == 0));
-            if (nt <= thresh) break;
-            if (st == kTrav) {
-                if (!ref) {
-                    if (quad4_step(s, r, w4)) {
-                        if (w4.fail) {
-                            ref = true;
-                            best = HitRec{-1.0f, -1};
-                            if (!walk_restart_ref(s, r, wk)) st = kDone;
-                        } else {
-                            best = HitRec{w4.bp >= 0 ? w4.bt : -1.0f, w4.bp};
-                            st = kDone;
-                        }
-                    }
-                } else {
-                    bool done = false;
-                    if (q == 0) done = closest_step<false, FetchTop, WalkStack>(s, r, stk, wk, w);
-                    done = __shfl((int)done, lead, 64) != 0;
-                    if (done) {
-                        best.t = __shfl(wk.best.t, lead, 64);
-                        best.prim = __shfl(wk.best.prim, lead, 64);
-                        st = kDone;
-                    }
-                }
-            }
-        }
-    }
-    if (kBq > 0) {
-        if (lane_id() == 0) atomicSub(&g_bq_prod, 1u);      // this wave produces no more shadow tasks
-        bq_consume<false>(s, p, stk, w);
-    }
-    __syncthreads();
-    if (threadIdx.x == 0) o.scount[blk] = g_scnt * (unsigned)nl;
 }
 
 // any-hit of the packed shadow tasks j = blk, blk+G, ... < total
@@ -1227,7 +691,7 @@ __device__ void occlude_body(const rtk::DevScene& s, const PcParams& p, unsigned
         while (__popcll(__ballot(active)) > thresh) {
             if (active) {
                 const int res = occl_step<COUNT, FetchTop>(s, r, tlim, stk, wk, w);
-                if (res) {
+                if (res || walk_runaway(s, wk)) {
                     p.occ[owner] = res == 2 ? 1 : 0;
                     active = false;
                 }
@@ -1309,8 +773,7 @@ __global__ __launch_bounds__(kBlock, RT_OCC_WAVES_PER_EU) void k_mix(rtk::DevSce
     block_init(s);
     if (chain) {
         if (p.bprio) __builtin_amdgcn_s_setprio(3);    // the deep chains are the frame's critical path
-        if (!COUNT && RT_QUAD4 && p.quad4) chain4_body(s, p, blockIdx.x, (unsigned)p.gb, phase_b(p));
-        else chain_body<COUNT, true, RT_WIDE_B>(s, e, p, blockIdx.x, (unsigned)p.gb, phase_b(p));
+        chain_body<COUNT, true>(s, e, p, blockIdx.x, (unsigned)p.gb, phase_b(p));
     }
     else if (!p.exp_skip_occ) occlude_body<COUNT>(s, p, blockIdx.x - p.gb, gridDim.x - p.gb, p.sflatA, p.totals[0]);
 }
@@ -1449,7 +912,7 @@ __global__ __launch_bounds__(kBlock, RT_WAVES_PER_EU) void k_fused(rtk::DevScene
             }
             const int thresh = exhausted ? 0 : p.refill;
             while (__popcll(__ballot(st == kTrav)) > thresh && __popcll(__ballot(st == kDone)) < p.service) {
-                if (st == kTrav && closest_step<COUNT, FetchTop>(s, r, stk, wk, w)) st = kDone;
+                if (st == kTrav && (closest_step<COUNT, FetchTop>(s, r, stk, wk, w) || walk_runaway(s, wk))) st = kDone;
             }
         }
         if (lane == 0) __hip_atomic_fetch_add(&g_live, -1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
@@ -1522,7 +985,7 @@ __global__ __launch_bounds__(kBlock, RT_WAVES_PER_EU) void k_fused(rtk::DevScene
             while (__popcll(__ballot(active)) > thresh) {
                 if (active) {
                     const int res = occl_step<COUNT, FetchTop>(s, r, tlim, stk, wk, w);
-                    if (res) {
+                    if (res || walk_runaway(s, wk)) {
                         p.occ[owner] = res == 2 ? 1 : 0;
                         active = false;
                     }
@@ -1831,7 +1294,7 @@ __global__ __launch_bounds__(kBlock, RT_FINISH_WAVES) void k_finish_any(rtk::Dev
 // Diagnostics (rt_walk_timing): wave 0 of one workgroup walks ray i with
 // lanes [0, lanes) (the same ray in every lane), reps times; lane 0 records
 // the last rep's shader cycles (s_memtime), the steps and the winner.  mode 0:
-// the production closest-hit walk (4-wide tree when certified), 1: the
+// the production closest-hit walk (the reference-order quads), 1: the binary
 // reference tree.  Measures the dependent-step latency of one walk.
 template <int MODE>
 __global__ __launch_bounds__(kBlock) void k_walk_timing(rtk::DevScene s, const float* rays, int n, int lanes, int reps,
@@ -1877,17 +1340,6 @@ __global__ __launch_bounds__(kBlock) void k_walk_timing(rtk::DevScene s, const f
                         ++steps;
                     }
                     h = HitRec{0.0f, cur};
-                }
-            } else if (mode == 2) {
-                if (threadIdx.x < 4) {           // one 4-lane group (chain4_body's walk)
-                    Walk4 w4;
-                    walk4_begin(s, w4);
-#pragma unroll 1
-                    while (true) {
-                        ++steps;
-                        if (quad4_step(s, r, w4)) break;
-                    }
-                    h = HitRec{w4.bt, w4.fail ? -2 : w4.bp};
                 }
             } else if ((int)threadIdx.x < lanes) {
                 Walk wk;
@@ -1963,7 +1415,6 @@ hipError_t launch_walk_timing(const rtk::DevScene& s, const float* rays, int n, 
                               unsigned long long* out, hipStream_t st) {
     if (mode == 0) hipLaunchKernelGGL(k_walk_timing<0>, dim3(1), dim3(kBlock), 0, st, s, rays, n, lanes, reps, out);
     else if (mode == 1) hipLaunchKernelGGL(k_walk_timing<1>, dim3(1), dim3(kBlock), 0, st, s, rays, n, lanes, reps, out);
-    else if (mode == 2) hipLaunchKernelGGL(k_walk_timing<2>, dim3(1), dim3(kBlock), 0, st, s, rays, n, lanes, reps, out);
     else if (mode == 3) hipLaunchKernelGGL(k_walk_timing<3>, dim3(1), dim3(kBlock), 0, st, s, rays, n, lanes, reps, out);
     else hipLaunchKernelGGL(k_walk_timing<4>, dim3(1), dim3(kBlock), 0, st, s, rays, n, lanes, reps, out);
     return hipGetLastError();

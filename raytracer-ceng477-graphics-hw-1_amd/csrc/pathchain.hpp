@@ -78,11 +78,8 @@ struct PcParams {
     int service;      // ... or once >= service of its lanes finished a walk (epilogue, next bounce)
     int bservice;     // the same for phase-B chains
     int btail;        // phase-B chains once no continuation is left to take: service at this many done lanes
-    int quad4;        // 1: phase-B chains walk with 4 lanes per ray (chain4_body)
     int bq_cap;       // phase-B workgroup shadow queue slots in use (<= kBq; 0: every task to k_occlude)
     int spread;       // tiles interleaved per wave within a 256-sample unit (1, 2 or 4)
-    int wide;         // wide (whole-wave) walks when <= wide lanes of a wave still walk; 0 = off
-    int wide_min;     // ... and the walk already took >= wide_min narrow steps
     uint8_t* out;
     // Frame batch: the slab's rows are nframes frames of frame_rows rows each (slab_rows = nframes *
     // frame_rows); frame f's samples use eyes[f] and its pixels go to fouts[f] (nframes > 1 only).

@@ -42,8 +42,12 @@ struct DevScene {
     const dl::Quad* quads;
     const float4* lrec;   // leaf records (dl::LeafHead + prims), indexed in 16-B units
     int qroot;
-    int use_sclosest;     // NaN-free closest-hit rays walk the occlusion tree first, certified (traverse2.hpp)
+    const dl::Wide* wnodes;  // the reference tree in wide form (closest hit, reference order)
+    int wroot;
+    int use_wide;         // NaN-free closest-hit rays walk wnodes (traverse2.hpp wide_closest_step)
     int leaf_wait_any;    // the same for any-hit walks (RT_LEAF_WAIT_ANY)
+    unsigned* err;        // device error word (bit 0: a walk exceeded walk_cap), read by the host after renders
+    int walk_cap;         // always-on bound on one walk's step calls (traverse2.hpp walk_runaway)
     int leaf_wait;        // 4-wide walks: a lane at a leaf record waits while fewer than leaf_wait/64 of the
                           // wave's walking lanes are at one (0: never waits; RT_LEAF_WAIT)
 

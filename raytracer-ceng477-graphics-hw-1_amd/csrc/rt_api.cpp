@@ -94,12 +94,14 @@ struct rt_scene {
     dl::Material* d_mats = nullptr;
     dl::Light* d_lights = nullptr;
     unsigned long long* d_counters = nullptr;
+    unsigned* d_err = nullptr;                 // device error word (DevScene.err)
     uint8_t* d_out = nullptr;
     size_t out_cap = 0;
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
     dl::Pair* d_pairs = nullptr;
     dl::Pair* d_spairs = nullptr;
     dl::Quad* d_quads = nullptr;
+    dl::Wide* d_wnodes = nullptr;
     dl::Vec4* d_lrec = nullptr;
     dl::LeafBig* d_leafbig = nullptr;
     enum Path { kChain, kWavefront, kMegakernel, kFused } path = kChain;
@@ -123,8 +125,6 @@ struct rt_scene {
     int tune_tchunk = 0;        // RT_TCHUNK (0: 128 for frame batches, 8 for one frame)
     int tune_ochunk = 256;      // RT_OCHUNK
     int tune_packet = 1;        // RT_PACKET
-    int tune_wide = 0;          // RT_WIDE
-    int tune_wide_min = 24;     // RT_WIDE_MIN
     int tune_kinline = 1;       // RT_KINLINE: deepest level of phase A
     // RT_CHUNK_SAMPLES: samples per chain-path launch (chunk / frame batch).  Bigger launches leave
     // fewer tails per sample: C3 batches 4 M 0.72, 8 M 0.66, 16 M 0.63, 32 M 0.59 ms/frame; C5 8 M
@@ -134,7 +134,6 @@ struct rt_scene {
     int tune_slots = 3;         // RT_SLOTS: frame batches in flight together (workspace slots, <= kSlots)
     int tune_gb = 0;            // RT_GB: phase-B chain workgroups in k_mix (0 = 1.5625 per CU: 384-416 best of 256-1024 on C3)
     int tune_bq_cap = 1 << 30;  // RT_BQ_CAP: phase-B shadow queue slots (tests force the k_occlude spill path)
-    int tune_quad4 = 0;         // RT_QUAD4: phase-B chains with 4 lanes per ray (measured slower: 1.71 vs 1.20 ms)
     int tune_bservice = 64;     // RT_BSERVICE: phase-B waves service finished walks once this many lanes are done
     int tune_btail = 64;        // RT_BTAIL: the same once the continuations are exhausted (1: 1.24, 4: 1.18, 16: 1.15, 64: 1.14 ms)
     int tune_split = 1;         // RT_SPLIT: a frame runs as this many concurrent interleaved sub-frames (2: +8%, 3: +18% on C3)
@@ -181,9 +180,9 @@ struct rt_scene {
         }
         if (fork_ev) (void)hipEventDestroy(fork_ev);
         (void)hipFree(batch_out);
-        (void)hipFree(d_pairs); (void)hipFree(d_leafbig); (void)hipFree(d_spairs); (void)hipFree(d_quads); (void)hipFree(d_lrec);
+        (void)hipFree(d_pairs); (void)hipFree(d_leafbig); (void)hipFree(d_spairs); (void)hipFree(d_quads); (void)hipFree(d_wnodes); (void)hipFree(d_lrec);
         (void)hipFree(d_nodes); (void)hipFree(d_prims); (void)hipFree(d_tri); (void)hipFree(d_mats); (void)hipFree(d_lights);
-        (void)hipFree(d_counters); (void)hipFree(d_out); (void)hipFree(d_trace);
+        (void)hipFree(d_counters); (void)hipFree(d_err); (void)hipFree(d_out); (void)hipFree(d_trace);
         if (ev0) (void)hipEventDestroy(ev0);
         if (ev1) (void)hipEventDestroy(ev1);
     }
@@ -237,9 +236,12 @@ int finish_scene(rt_scene* s, const rt_options* opts) {
     if ((rc = upload(&s->d_leafbig, s->bvh.leaf_big))) return rc;
     if ((rc = upload(&s->d_spairs, s->bvh.spairs))) return rc;
     if ((rc = upload(&s->d_quads, s->bvh.quads))) return rc;
+    if ((rc = upload(&s->d_wnodes, s->bvh.wnodes))) return rc;
     if ((rc = upload(&s->d_lrec, s->bvh.lrec))) return rc;
     HIP_TRY(hipMalloc(reinterpret_cast<void**>(&s->d_counters), 8 * sizeof(unsigned long long)));
     HIP_TRY(hipMemset(s->d_counters, 0, 8 * sizeof(unsigned long long)));
+    HIP_TRY(hipMalloc(reinterpret_cast<void**>(&s->d_err), sizeof(unsigned)));
+    HIP_TRY(hipMemset(s->d_err, 0, sizeof(unsigned)));
     HIP_TRY(hipEventCreate(&s->ev0));
     HIP_TRY(hipEventCreate(&s->ev1));
 
@@ -273,8 +275,6 @@ int finish_scene(rt_scene* s, const rt_options* opts) {
     if (const char* e = std::getenv("RT_BPRIO")) s->tune_bprio = std::atoi(e) != 0;
     if (const char* e = std::getenv("RT_BREFILL")) s->tune_brefill = std::max(0, std::min(63, std::atoi(e)));
     if (const char* e = std::getenv("RT_OREFILL")) s->tune_orefill = std::max(0, std::min(63, std::atoi(e)));
-    if (const char* e = std::getenv("RT_WIDE")) s->tune_wide = std::max(0, std::min(64, std::atoi(e)));
-    if (const char* e = std::getenv("RT_WIDE_MIN")) s->tune_wide_min = std::max(0, std::atoi(e));
     if (const char* e = std::getenv("RT_BATCH")) s->tune_batch = std::max(1, std::atoi(e));
     if (const char* e = std::getenv("RT_SLOTS")) s->tune_slots = std::max(1, std::atoi(e));
     if (const char* e = std::getenv("RT_CHUNK_SAMPLES"))
@@ -282,7 +282,6 @@ int finish_scene(rt_scene* s, const rt_options* opts) {
     if (const char* e = std::getenv("RT_KINLINE")) s->tune_kinline = std::max(0, std::atoi(e));
     if (const char* e = std::getenv("RT_GB")) s->tune_gb = std::max(0, std::atoi(e));
     if (const char* e = std::getenv("RT_BQ_CAP")) s->tune_bq_cap = std::max(0, std::atoi(e));
-    if (const char* e = std::getenv("RT_QUAD4")) s->tune_quad4 = std::atoi(e) != 0;
     if (const char* e = std::getenv("RT_BSERVICE")) s->tune_bservice = std::max(1, std::min(64, std::atoi(e)));
     if (const char* e = std::getenv("RT_BTAIL")) s->tune_btail = std::max(1, std::min(64, std::atoi(e)));
     if (const char* e = std::getenv("RT_SPLIT")) s->tune_split = std::max(1, std::atoi(e));
@@ -325,9 +324,19 @@ int finish_scene(rt_scene* s, const rt_options* opts) {
         const int v = std::atoi(e);
         d.use_stree = v <= 0 ? 0 : (v >= 2 && !s->bvh.quads.empty() ? 2 : (s->bvh.spairs.empty() ? 0 : 1));
     }
-    // closest-hit walks of NaN-free rays: certified walk over the 4-wide occlusion tree (RT_SCLOSEST=0: off)
-    d.use_sclosest = s->bvh.quads.empty() ? 0 : 1;
-    if (const char* e = std::getenv("RT_SCLOSEST")) d.use_sclosest = d.use_sclosest && std::atoi(e) != 0;
+    // closest-hit walks of NaN-free rays: the reference tree's wide form, reference order (RT_WIDE_WALK=0: the
+    // binary form)
+    d.wnodes = s->d_wnodes;
+    d.wroot = s->bvh.wroot;
+    d.use_wide = !s->bvh.nodes.empty() && !s->bvh.lrec.empty() &&
+                 (!s->bvh.wnodes.empty() || (s->bvh.root_info < 0 && s->bvh.root_lrec >= 0));
+    if (const char* e = std::getenv("RT_WIDE_WALK")) d.use_wide = d.use_wide && std::atoi(e) != 0;
+    d.err = s->d_err;
+    {   // walk_runaway: 64 x (every node of the largest tree + leaves); RT_WALK_CAP overrides (tests)
+        const long long nodes = (long long)s->bvh.pairs.size() + s->bvh.leaves + 64;   // the largest tree
+        d.walk_cap = (int)std::min<long long>(INT32_MAX / 2, 64 * nodes);
+        if (const char* e = std::getenv("RT_WALK_CAP")) d.walk_cap = std::max(1, std::atoi(e));
+    }
     d.leaf_wait = 24;   // measured: 0 1.20, 8 1.19, 16-32 1.166, 48 1.22, 64 1.46 ms (C3)
     if (const char* e = std::getenv("RT_LEAF_WAIT")) d.leaf_wait = std::max(0, std::min(64, std::atoi(e)));
     d.leaf_wait_any = d.leaf_wait;
@@ -569,7 +578,6 @@ int render_chain(rt_scene* s, const rtk::Eye& eye, const rtk::FrameParams& f, bo
     p.service = s->tune_service >= 0 ? s->tune_service : 64;
     p.bservice = s->tune_bservice;
     p.btail = s->tune_btail;
-    p.quad4 = s->tune_quad4 && !s->bvh.quads.empty();
     p.bq_cap = std::min(s->tune_bq_cap, rtc::kMaxBq);
     p.producers = s->tune_producers;
     p.orefill = s->tune_orefill;
@@ -580,8 +588,6 @@ int render_chain(rt_scene* s, const rtk::Eye& eye, const rtk::FrameParams& f, bo
     p.packet = s->tune_packet && s->bvh.max_stack <= dl::kMaxStack;
     p.exp_skip_occ = std::getenv("RT_EXP_SKIP_OCC") ? 1 : 0;
     p.shade_split = std::getenv("RT_SHADE_SPLIT") ? std::atoi(std::getenv("RT_SHADE_SPLIT")) : 0;
-    p.wide = s->bvh.max_depth <= 26 ? s->tune_wide : 0;   // path keys hold 26 levels
-    p.wide_min = s->tune_wide_min;
     p.spread = s->tune_spread;
     p.crefill = s->tune_crefill;
     p.wq = static_cast<unsigned*>(at(o_wq));
@@ -610,6 +616,16 @@ int render_chain(rt_scene* s, const rtk::Eye& eye, const rtk::FrameParams& f, bo
     }
     if (p.trace) trace_dump(s, st, 0, (unsigned)cap, (unsigned)p.ogrid, trace_n);   // last chunk only
     return RT_OK;
+}
+
+// The device error word after the device is idle: RT_ERR_LIMIT (and the word
+// cleared) when a walk was cut off by walk_runaway since the last check.
+int check_device_error(rt_scene* s) {
+    unsigned e = 0;
+    HIP_TRY(hipMemcpy(&e, s->d_err, sizeof(e), hipMemcpyDeviceToHost));
+    if (e == 0) return RT_OK;
+    HIP_TRY(hipMemset(s->d_err, 0, sizeof(unsigned)));
+    return fail(RT_ERR_LIMIT, "a BVH walk exceeded its step bound (walk_cap) and was cut off; the frame is invalid");
 }
 
 }  // namespace
@@ -1015,6 +1031,7 @@ int rt_render_cameras(rt_scene* s, const rt_camera* cams, int n, int aa, uint8_t
     }
     HIP_TRY(hipDeviceSynchronize());
     if (rc) return rc;
+    if ((rc = check_device_error(s))) return rc;
     if (stats) {
         rc = rt_counters_read(s, stats);
         if (rc) return rc;
@@ -1069,7 +1086,15 @@ int rt_counters_read(rt_scene* s, rt_stats* st) {
     HIP_TRY(hipMemcpy(c, s->d_counters, sizeof(c), hipMemcpyDeviceToHost));
     st->primary_rays = c[0]; st->shadow_rays = c[1]; st->reflection_rays = c[2];
     st->node_visits = c[3]; st->tri_tests = c[4]; st->sphere_tests = c[5];
-    return RT_OK;
+    return check_device_error(s);
+}
+
+int rt_scene_check(rt_scene* s) {
+    if (!s) return fail(RT_ERR_ARG, "scene is NULL");
+    if (s->host_only) return RT_OK;
+    HIP_TRY(hipSetDevice(s->device));
+    HIP_TRY(hipDeviceSynchronize());
+    return check_device_error(s);
 }
 
 int rt_render(rt_scene* s, const rt_camera* cam, int aa, uint8_t* out_rgb, rt_stats* stats) {
@@ -1095,6 +1120,7 @@ int rt_render(rt_scene* s, const rt_camera* cam, int aa, uint8_t* out_rgb, rt_st
     HIP_TRY(hipEventRecord(s->ev1, nullptr));
     HIP_TRY(hipMemcpy(out_rgb, s->d_out, bytes, hipMemcpyDeviceToHost));
     HIP_TRY(hipEventSynchronize(s->ev1));
+    if ((rc = check_device_error(s))) return rc;
     if (stats) {
         rc = rt_counters_read(s, stats);
         if (rc) return rc;

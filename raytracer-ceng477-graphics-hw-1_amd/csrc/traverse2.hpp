@@ -219,46 +219,27 @@ __device__ __forceinline__ bool any_hit2(const rtk::DevScene& s, const Ray& r, f
 // Pairs [0, s.top_pairs) (the top levels) are read from an LDS copy.
 // ---------------------------------------------------------------------------
 struct Walk {
-    const dl::Pair* tree;   // pair array the walk indexes (BVH or binary occlusion tree); null: 4-wide tree
+    const dl::Pair* tree;   // pair array the walk indexes (BVH or binary occlusion tree); null: a 4-wide tree
     int cur;       // node to process (pair/quad index or leaf code)
     int sp;        // stack depth
-    float tmax;    // closest-hit pruning bound
+    float tmax;    // closest-hit pruning bound (the reference's tMax)
     HitRec best;   // closest-hit result so far
     bool fast;     // ray_nan_free: box tests may use v_min/v_max
-    float blt;     // certified closest hit (4-wide tree): entry t of the winner's leaf box
-    float t2;      // ... smallest t among the other hits (-inf: a hit with t < 0 or NaN)
+    int sgn;       // closest hit on the reference-order wide nodes: bit a set iff d[a] > 0
+    int steps;     // step calls of this walk (walk_runaway)
 };
 
-// Certified closest hit over the 4-wide occlusion tree (binned-SAH
-// hierarchy above the reference's own leaves, exact leaf boxes; see
-// build_shadow_tree).  The reference returns the first minimum, in its DFS
-// order, over the leaves V it visits; a leaf is visited iff its box (and, by
-// monotonicity, every ancestor's) is hit with entry t <= tMax when popped,
-// where tMax is FLT_MAX or the t of an already visited primitive.  The
-// 4-wide walk goes front to back with pruning bound sah_bound(best) and finds
-// the minimum t_w over the reachable leaves R, its primitive w, and t2, the
-// smallest t of the other hits it met.  w is the reference's answer when
-//   (1) t2 > t_w: no tie (ties are decided by DFS position) and no negative
-//       or NaN t (the `best.t == -1` sentinel rule, raytracer.cpp:213-221);
-//   (2) blt <= t_w: w's leaf is popped with tMax >= t_w >= its entry t; or
-//       blt <= sah_late(t_w) (rounding put the hit just before its leaf's
-//       entry) and t2 >= blt: no other primitive can bring tMax below the
-//       entry before that leaf is popped.
-// Otherwise the walk restarts on the reference tree (walk_restart_ref).  The
-// pruning slack makes this exact unless some primitive's hit lies more than
-// 2^-10 (relative) before the entry t of its own leaf box; the measured worst
-// case over the goldens' scenes is 1e-5 (flat axis-aligned leaves, where
-// Cramer's t and the slab t round differently): tools/exp_sah_closest.cpp.
-__device__ __forceinline__ float sah_bound(float t) { return t + t * 0.001953125f; }
-__device__ __forceinline__ float sah_late(float t) { return t + t * 0.0009765625f; }
-// The certification test (conditions (1)-(2) above) for winner t tw, runner-up
-// t2 and winner leaf entry blt.  Bitwise & and | on purpose: one predicate and
-// one branch into walk_restart_ref.  The short-circuit form let the gfx950
-// backend (ROCm 7.2) clear the walk's tree pointer on every lane that passed
-// t2 > tw, including lanes that then failed the blt test and restarted, so
-// those walks re-entered the 4-wide tree and never finished.
-__device__ __forceinline__ bool sah_certified(float tw, float t2, float blt) {
-    return (t2 > tw) & ((blt <= tw) | ((blt <= sah_late(tw)) & (t2 >= blt)));
+// Always-on bound on one walk's step calls.  A DFS pops each node at most
+// once, so a walk takes at most as many expanding steps as its tree has nodes
+// and leaves, plus postponed steps (leaf_postponed: a lane waits only while
+// other lanes of its wave expand); s.walk_cap = 64 x that.  A walk that
+// exceeds it can only be a broken tree or a miscompiled walk: it is ended,
+// and the scene's device error word is set, which the host turns into
+// RT_ERR_LIMIT instead of a kernel that never finishes.
+__device__ __forceinline__ bool walk_runaway(const rtk::DevScene& s, Walk& k) {
+    if (++k.steps <= s.walk_cap) return false;
+    __hip_atomic_fetch_or(s.err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    return true;
 }
 
 // Both child boxes of a pair; the min/max form when every active lane's ray
@@ -327,6 +308,7 @@ __device__ __forceinline__ bool walk_begin(const rtk::DevScene& s, const Ray& r,
     k.best = HitRec{-1.0f, -1};
     k.tmax = FLT_MAX;
     k.sp = 0;
+    k.steps = 0;
     k.fast = ray_nan_free(r);
     if (s.nnodes <= 0) return false;
     if (COUNT) w.nodes++;
@@ -343,11 +325,10 @@ __device__ __forceinline__ bool walk_begin(const rtk::DevScene& s, const Ray& r,
         const float4 hi = make_float4(s.sroot_hi[0], s.sroot_hi[1], s.sroot_hi[2], 0.0f);
         return box_hit(r, lo, hi, &bt);
     }
-    if (!COUNT && !any && k.fast && s.use_sclosest) {
-        k.tree = nullptr;                    // certified closest hit over the 4-wide tree
-        k.cur = s.qroot;
-        k.t2 = __builtin_inff();
-        k.blt = __builtin_inff();
+    if (!COUNT && !any && k.fast && s.use_wide) {
+        k.tree = nullptr;                    // the reference tree's wide form, reference order
+        k.cur = s.wroot;
+        k.sgn = (r.d.x > 0.0f ? 1 : 0) | (r.d.y > 0.0f ? 2 : 0) | (r.d.z > 0.0f ? 4 : 0);
         return true;
     }
     k.tree = s.pairs;
@@ -355,20 +336,6 @@ __device__ __forceinline__ bool walk_begin(const rtk::DevScene& s, const Ray& r,
     const float4 lo = make_float4(s.root_lo[0], s.root_lo[1], s.root_lo[2], 0.0f);
     const float4 hi = make_float4(s.root_hi[0], s.root_hi[1], s.root_hi[2], 0.0f);
     return box_hit(r, lo, hi, &bt) && (any || bt <= k.tmax);
-}
-
-// Restart a closest-hit walk on the reference tree (certification failed).
-// false: the root box is missed, no hit.
-__device__ __forceinline__ bool walk_restart_ref(const rtk::DevScene& s, const Ray& r, Walk& k) {
-    k.best = HitRec{-1.0f, -1};
-    k.tmax = FLT_MAX;
-    k.sp = 0;
-    k.tree = s.pairs;
-    k.cur = s.root_info;
-    float bt;
-    const float4 lo = make_float4(s.root_lo[0], s.root_lo[1], s.root_lo[2], 0.0f);
-    const float4 hi = make_float4(s.root_hi[0], s.root_hi[1], s.root_hi[2], 0.0f);
-    return box_hit(r, lo, hi, &bt) && bt <= k.tmax;
 }
 
 // Child boxes of a 4-wide node (dl::Quad), decoded exactly as the host
@@ -391,11 +358,11 @@ struct QuadHits {
     bool hit[4];     // child exists and its box is hit
     int code[4];
 };
-__device__ __forceinline__ void quad_hits(const rtk::DevScene& s, int qi, const Ray& r, QuadHits& c) {
-    const float4* q = reinterpret_cast<const float4*>(&s.quads[qi]);
+__device__ __forceinline__ void quad_hits(const dl::Quad* quads, int qi, const Ray& r, QuadHits& c) {
+    const float4* q = reinterpret_cast<const float4*>(&quads[qi]);
     const float4 q0 = q[0], q1 = q[1], q2 = q[2], q3 = q[3];
     const uint32_t ex = __float_as_uint(q0.w);
-    const int n = (int)(ex >> 24);
+    const uint32_t mask = ex >> 24;
     const float sc[3] = {__uint_as_float((ex & 255u) << 23), __uint_as_float(((ex >> 8) & 255u) << 23),
                          __uint_as_float(((ex >> 16) & 255u) << 23)};
     const float org[3] = {q0.x, q0.y, q0.z};
@@ -429,7 +396,7 @@ __device__ __forceinline__ void quad_hits(const rtk::DevScene& s, int qi, const 
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
         c.t[i] = tmn[i];
-        c.hit[i] = i < n && tmx[i] >= __builtin_fmaxf(0.0f, tmn[i]);
+        c.hit[i] = ((mask >> i) & 1u) && tmx[i] >= __builtin_fmaxf(0.0f, tmn[i]);
     }
 }
 
@@ -453,8 +420,6 @@ __device__ __forceinline__ bool for_leaf_prims(const float4* L, int slot0, int c
     return false;
 }
 
-// One step of the certified closest-hit walk over the 4-wide tree (see
-// sah_bound); true when finished (result in k.best).  NaN-free rays only.
 // Leaf postponing (SIMD efficiency): the interior and leaf branches of a step
 // are both executed whenever the wave's walking lanes straddle them, so a lane
 // holding a leaf record skips steps while fewer than leaf_wait/64 of the
@@ -466,66 +431,116 @@ __device__ __forceinline__ bool leaf_postponed(int wait, const Walk& k) {
     return k.cur < 0 && __popcll(lm) * 64 < __popcll(am) * wait;
 }
 
+// One step of the closest-hit walk over the reference-order wide nodes
+// (host_scene.cpp build_ref_wide), NaN-free rays only; true when finished
+// (result in k.best).  Exactly the reference's walk (raytracer.cpp:177-225),
+// re-timed:
+//   * order: a node's slots are visited in the reference's DFS order (the
+//     left child first iff d[axis] > 0 at every node of the collapsed levels;
+//     the node stores each slot's rank per octant of d), the first passing
+//     slot next, the other passing ones pushed behind it, highest rank
+//     deepest;
+//   * pruning: a slot passes when its (conservative, quantized) box is hit
+//     with entry t <= tMax, re-checked against the then-current tMax when
+//     popped; a leaf record's EXACT box is tested like the reference's leaf
+//     pop (hit and entry t <= tMax) before its primitives, which are tested
+//     in stored order with the reference's update rule (:210-222);
+//   * why that is exact: boxes nest (a child's exact box lies in its
+//     parent's, a quantized box contains its exact box) and for a NaN-free
+//     ray the slab test is monotone under nesting, so a leaf whose exact test
+//     passes at its pop has every ancestor passing at its earlier pop (larger
+//     or equal tMax); a subtree the reference prunes (box missed, or entry
+//     > tMax) contains only leaves whose exact test fails here too.  Leaves are
+//     therefore tested in the reference's order with the reference's tMax,
+//     so every update - and the final (t, primitive) - is the reference's.
+//     Only interior work differs (skipped intermediate boxes, conservative
+//     quantized tests).  No tolerance, no restart.
 template <class STK>
-__device__ __forceinline__ bool quad_closest_step(const rtk::DevScene& s, const Ray& r, STK& stk, Walk& k) {
-    constexpr int kNone = 0x7fffffff;         // no child (never a quad index or leaf code)
+__device__ __forceinline__ bool wide_closest_step(const rtk::DevScene& s, const Ray& r, STK& stk, Walk& k) {
+    constexpr int W = dl::kWideSlots;
     if (leaf_postponed(s.leaf_wait, k)) return false;
     if (k.cur >= 0) {
-        QuadHits q;
-        quad_hits(s, k.cur, r, q);
-        float t[4];
-        int c[4];
+        const float4* N = reinterpret_cast<const float4*>(&s.wnodes[k.cur]);
+        const float4 q0 = N[0], q1 = N[1], q2 = N[2], q3 = N[3], q4 = N[4];
+        const float4 q5 = W > 4 ? N[5] : q4;
+        const uint32_t rw = reinterpret_cast<const uint32_t*>(&s.wnodes[k.cur])[24 + k.sgn];
+        const uint32_t ex = __float_as_uint(q0.w);
+        const uint32_t mask = ex >> 24;
+        const float sc[3] = {__uint_as_float((ex & 255u) << 23), __uint_as_float(((ex >> 8) & 255u) << 23),
+                             __uint_as_float(((ex >> 16) & 255u) << 23)};
+        const float org[3] = {q0.x, q0.y, q0.z};
+        const float ro[3] = {r.o.x, r.o.y, r.o.z}, ri[3] = {r.inv.x, r.inv.y, r.inv.z};
+        // plane dwords: lo x,y,z then hi x,y,z, two dwords (slots 0-3, 4-7) each
+        const uint32_t pl[12] = {__float_as_uint(q1.x), __float_as_uint(q1.y), __float_as_uint(q1.z),
+                                 __float_as_uint(q1.w), __float_as_uint(q2.x), __float_as_uint(q2.y),
+                                 __float_as_uint(q2.z), __float_as_uint(q2.w), __float_as_uint(q3.x),
+                                 __float_as_uint(q3.y), __float_as_uint(q3.z), __float_as_uint(q3.w)};
+        const int code[8] = {__float_as_int(q4.x), __float_as_int(q4.y), __float_as_int(q4.z), __float_as_int(q4.w),
+                             __float_as_int(q5.x), __float_as_int(q5.y), __float_as_int(q5.z), __float_as_int(q5.w)};
+        float tmn[W], tmx[W];
 #pragma unroll
-        for (int i = 0; i < 4; ++i) {
-            const bool h = q.hit[i] && q.t[i] <= k.tmax;
-            t[i] = h ? q.t[i] : __builtin_inff();
-            c[i] = h ? q.code[i] : kNone;
-        }
-        auto cswap = [&](int a, int b) {
-            const bool sw = t[b] < t[a];
-            const float ta = t[a], tb = t[b];
-            const int ca = c[a], cb = c[b];
-            t[a] = sw ? tb : ta;
-            t[b] = sw ? ta : tb;
-            c[a] = sw ? cb : ca;
-            c[b] = sw ? ca : cb;
-        };
-        cswap(0, 1);
-        cswap(2, 3);
-        cswap(0, 2);
-        cswap(1, 3);
-        cswap(1, 2);
+        for (int a = 0; a < 3; ++a) {
+            const bool neg = __float_as_int(ri[a]) < 0;   // near plane: lo for inv > 0, hi for inv < 0
+            const f2v s2 = {sc[a], sc[a]}, o2 = {org[a], org[a]}, rr = {ro[a], ro[a]}, iv = {ri[a], ri[a]};
 #pragma unroll
-        for (int i = 3; i >= 1; --i)
-            if (c[i] != kNone) {
-                stk.put(k.sp, make_int2(c[i], __float_as_int(t[i])));
-                ++k.sp;
+            for (int pr = 0; pr < W / 2; ++pr) {            // slots 2pr, 2pr+1
+                const int dw = pr >> 1, sh = 16 * (pr & 1);
+                const uint32_t lw = pl[2 * a + dw], hw = pl[6 + 2 * a + dw];
+                const uint32_t nw = neg ? hw : lw, fw = neg ? lw : hw;
+                const f2v qn = {(float)((nw >> sh) & 255u), (float)((nw >> (sh + 8)) & 255u)};
+                const f2v qf = {(float)((fw >> sh) & 255u), (float)((fw >> (sh + 8)) & 255u)};
+                const f2v tn = (__builtin_elementwise_fma(qn, s2, o2) - rr) * iv;
+                const f2v tf = (__builtin_elementwise_fma(qf, s2, o2) - rr) * iv;
+#pragma unroll
+                for (int h = 0; h < 2; ++h) {
+                    const int c = 2 * pr + h;
+                    tmn[c] = a == 0 ? tn[h] : __builtin_fmaxf(tmn[c], tn[h]);
+                    tmx[c] = a == 0 ? tf[h] : __builtin_fminf(tmx[c], tf[h]);
+                }
             }
-        if (c[0] != kNone) {
-            k.cur = c[0];
+        }
+        // valid slots as a mask in RANK order (the reference's visiting order for this octant)
+        uint32_t vm = 0;
+        bool valid[W];
+        uint32_t rank[W];
+#pragma unroll
+        for (int c = 0; c < W; ++c) {
+            rank[c] = (rw >> (3 * c)) & 7u;
+            valid[c] = ((mask >> c) & 1u) && tmx[c] >= __builtin_fmaxf(0.0f, tmn[c]) && tmn[c] <= k.tmax;
+            vm |= valid[c] ? 1u << rank[c] : 0u;
+        }
+        if (vm) {
+            const uint32_t first = (uint32_t)__builtin_ctz(vm);
+            int next = 0;
+#pragma unroll
+            for (int c = 0; c < W; ++c) {
+                if (valid[c]) {
+                    if (rank[c] == first) {
+                        next = code[c];
+                    } else {   // deeper on the stack the later it is visited
+                        const int pos = __builtin_popcount(vm >> (rank[c] + 1u));
+                        stk.put(k.sp + pos, make_int2(code[c], __float_as_int(tmn[c])));
+                    }
+                }
+            }
+            k.sp += __builtin_popcount(vm) - 1;
+            k.cur = next;
             return false;
         }
     } else {
         const float4* L = s.lrec + (k.cur & ~dl::kLeafBit);
         const float4 h0 = L[0], h1 = L[1], c0 = L[2], c1 = L[3], c2 = L[4];
         float lt;
-        if (box_hit_fast(r, h0, h1, &lt) && lt <= k.tmax) {   // the reference leaf's exact box
+        if (box_hit_fast(r, h0, h1, &lt) && lt <= k.tmax) {   // the reference leaf's exact box (:184)
             for_leaf_prims(L, __float_as_int(h1.w), __float_as_int(h0.w), c0, c1, c2,
                            [&](int slot, const float4& p0, const float4& p1, const float4& p2) {
                                float ti;
                                const bool h = __float_as_int(p0.w) >= 0 ? tri_hit(r, p0, p1, p2, &ti)
                                                                         : sphere_hit(r, p0, p1, &ti);
-                               if (h) {
-                                   if (ti < k.best.t || k.best.t == -1.0f) {
-                                       if (k.best.prim >= 0) k.t2 = smin(k.t2, k.best.t);
-                                       k.blt = lt;
-                                       k.best.t = ti;
-                                       k.best.prim = slot;
-                                       k.tmax = sah_bound(ti);
-                                   } else {
-                                       k.t2 = smin(k.t2, ti);
-                                   }
-                                   if (!(ti >= 0.0f)) k.t2 = -__builtin_inff();
+                               if (h && (ti < k.best.t || k.best.t == -1.0f)) {   // :213-221
+                                   k.best.t = ti;
+                                   k.best.prim = slot;
+                                   k.tmax = ti;
                                }
                                return false;
                            });
@@ -539,18 +554,13 @@ __device__ __forceinline__ bool quad_closest_step(const rtk::DevScene& s, const 
             return false;
         }
     }
-    if (k.best.prim >= 0) {
-        const float tw = k.best.t;
-        const bool ok = sah_certified(tw, k.t2, k.blt);
-        if (!ok) return !walk_restart_ref(s, r, k);
-    }
     return true;
 }
 
 // One closest-hit step; returns true when the walk is finished (result in k.best).
 template <bool COUNT, class FETCH, class STK, bool PIPE = false>
 __device__ __forceinline__ bool closest_step(const rtk::DevScene& s, const Ray& r, STK& stk, Walk& k, Work& w) {
-    if (!COUNT && k.tree == nullptr) return quad_closest_step(s, r, stk, k);
+    if (!COUNT && k.tree == nullptr) return wide_closest_step(s, r, stk, k);
     if (k.cur >= 0) {
         float4 l0, l1, r0, r1;
         fetch_pair(k, l0, l1, r0, r1);
@@ -676,7 +686,7 @@ __device__ __forceinline__ int quad_any_step(const rtk::DevScene& s, const Ray& 
     if (!COUNT && leaf_postponed(s.leaf_wait_any, k)) return 0;
     if (k.cur >= 0) {
         QuadHits q;
-        quad_hits(s, k.cur, r, q);
+        quad_hits(s.quads, k.cur, r, q);
         int next = 0;
         bool have = false;
 #pragma unroll

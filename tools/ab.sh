@@ -17,7 +17,7 @@ for cfg in "$@"; do
   [ "$cfg" = "-" ] && cfg="RT_NONE=1"
   env $cfg timeout -k 10 200 python bench.py --steps 30 --warmup 5 --no-cpu-baseline > gpurun_out/ab_$i.log 2>&1
   rc=$?
-  echo "[$cfg] rc=$rc $(grep '^{' gpurun_out/ab_$i.log | python3 -c 'import sys,json; d=json.loads(sys.stdin.read()); print(d["ms_per_step"], d["value"], d["roofline"]["kernel_ms"])')"
+  echo "[$cfg] rc=$rc $(grep '^{' gpurun_out/ab_$i.log | python3 -c 'import sys,json; d=json.loads(sys.stdin.read()); print(d["ms_per_step"], d["value"], d["roofline"]["kernel_ms"], "lat", d["config"]["frame_latency_ms"])')"
   [ $rc -ne 0 ] && { tail -5 gpurun_out/ab_$i.log; exit $rc; }
 done
 exit 0

@@ -18,6 +18,8 @@
 #include <cstdlib>
 #include <cstring>
 #include <vector>
+#include <functional>
+#include <array>
 
 #include "host_scene.hpp"
 
@@ -236,7 +238,7 @@ int closest_quad(const Ray& r, Hit* out) {
         if (cur >= 0) {
             g_qfetch++;
             const dl::Quad& q = B->quads[cur];
-            int n = q.exps >> 24;
+            int n = __builtin_popcount(q.exps >> 24);   // slot mask (contiguous in the occlusion tree)
             E hits[4]; int nh = 0;
             for (int c = 0; c < n; ++c) {
                 float lo[3], hi[3], t;
@@ -282,13 +284,200 @@ int closest_quad(const Ray& r, Hit* out) {
     *out = h;
     return status;
 }
+// Reference-order 4-wide walk (collapse of the reference tree: a quad = node N's
+// children, interior ones replaced by their own children), visiting children in
+// the reference's DFS order (near child first by the sign of d[axis] at N and
+// at each child), child boxes pruned at push and at pop against tMax, the
+// leaf's exact box tested against tMax before its primitives.  Exact by
+// construction for NaN-free rays (nested boxes: a leaf passing its test at its
+// pop implies every ancestor passed at its earlier pop).
+long g_rqfetch = 0, g_rqleaf = 0;
+Hit closest_rquad(const Ray& r) {
+    Hit h{-1.0f, -1, 0};
+    float tmax = FLT_MAX, bt;
+    if (!(box_hit(r, B->root_lo, B->root_hi, &bt) && bt <= tmax)) return h;
+    struct E { int32_t info; float t; } st[128];
+    int sp = 0;
+    int32_t cur = B->root_info;
+    auto box_of = [](const dl::Pair& P, bool left, float* lo, float* hi) {
+        if (left) { lo[0] = P.l_minx; lo[1] = P.l_miny; lo[2] = P.l_minz; hi[0] = P.l_maxx; hi[1] = P.l_maxy; hi[2] = P.l_maxz; }
+        else { lo[0] = P.r_minx; lo[1] = P.r_miny; lo[2] = P.r_minz; hi[0] = P.r_maxx; hi[1] = P.r_maxy; hi[2] = P.r_maxz; }
+    };
+    while (true) {
+        if (cur >= 0) {
+            g_rqfetch++;
+            const dl::Pair& P = B->pairs[cur];
+            int32_t ch[4];
+            float lo[4][3], hi[4][3];
+            int n = 0;
+            const bool lf = comp(r.d, P.axis) > 0;
+            for (int side = 0; side < 2; ++side) {
+                const bool left = (side == 0) == lf;
+                const int32_t info = left ? P.l_info : P.r_info;
+                if (info < 0) {
+                    ch[n] = info;
+                    box_of(P, left, lo[n], hi[n]);
+                    n++;
+                } else {
+                    const dl::Pair& Q = B->pairs[info];
+                    const bool lf2 = comp(r.d, Q.axis) > 0;
+                    for (int s2 = 0; s2 < 2; ++s2) {
+                        const bool l2 = (s2 == 0) == lf2;
+                        ch[n] = l2 ? Q.l_info : Q.r_info;
+                        box_of(Q, l2, lo[n], hi[n]);
+                        n++;
+                    }
+                }
+            }
+            E v[4];
+            int nv = 0;
+            for (int c = 0; c < n; ++c) {
+                float t;
+                if (box_hit(r, lo[c], hi[c], &t) && t <= tmax) v[nv++] = {ch[c], t};
+            }
+            for (int j = nv - 1; j >= 1; --j) st[sp++] = v[j];
+            if (nv) { cur = v[0].info; continue; }
+        } else {
+            int a, c;
+            leaf_range(cur, &a, &c);
+            g_rqleaf++;
+            const auto& lb = leaf_boxes[leaf_of_prim[a]];
+            float lt;
+            if (box_hit(r, lb.data(), lb.data() + 3, &lt) && lt <= tmax)
+                for (int i = a; i < a + c; ++i) {
+                    float t;
+                    if (prim_hit(r, B->prims[i], &t) && (t < h.t || h.t == -1.0f)) { h.t = t; h.prim = i; tmax = t; }
+                }
+        }
+        bool found = false;
+        while (sp > 0) { --sp; if (st[sp].t <= tmax) { cur = st[sp].info; found = true; break; } }
+        if (!found) break;
+    }
+    return h;
+}
+
+// Greedy-filled reference-order quads: a quad's slots are a frontier of up to
+// 4 nodes below an interior node, grown by expanding the interior slot of the
+// largest box area; the slots keep pre-order and each octant of the ray
+// direction has its own slot permutation (the DFS order below every expanded
+// node depends only on the sign of d[axis]).
+int g_width = 4;    // EXP_WIDTH: slots per node
+struct GQuad { int32_t info[8]; float lo[8][3], hi[8][3]; int n; uint8_t perm[8][8]; };
+std::vector<GQuad> g_gq;
+std::vector<int32_t> g_gq_of_pair;
+long g_gqfetch = 0, g_gqleaf = 0;
+struct Item { int32_t info; float lo[3], hi[3]; };
+double box_area(const float* lo, const float* hi) {
+    double dx = hi[0] - lo[0], dy = hi[1] - lo[1], dz = hi[2] - lo[2];
+    return dx * dy + dy * dz + dz * dx;
+}
+int32_t build_gq(int32_t pair) {
+    // expansion tree: node k of the frontier is a leaf of the expansion; expanded
+    // nodes record (axis, first slot of right part)
+    struct Exp { int axis; int lo, mid, hi; };
+    std::vector<Item> fr;
+    std::vector<Exp> ex;
+    auto kids = [&](int32_t p, Item* a, Item* b) {
+        const dl::Pair& P = B->pairs[p];
+        a->info = P.l_info; a->lo[0] = P.l_minx; a->lo[1] = P.l_miny; a->lo[2] = P.l_minz;
+        a->hi[0] = P.l_maxx; a->hi[1] = P.l_maxy; a->hi[2] = P.l_maxz;
+        b->info = P.r_info; b->lo[0] = P.r_minx; b->lo[1] = P.r_miny; b->lo[2] = P.r_minz;
+        b->hi[0] = P.r_maxx; b->hi[1] = P.r_maxy; b->hi[2] = P.r_maxz;
+        return P.axis;
+    };
+    Item a, b;
+    int ax = kids(pair, &a, &b);
+    fr = {a, b};
+    ex.push_back({ax, 0, 1, 2});
+    while ((int)fr.size() < g_width) {
+        int best = -1;
+        double ba = -1;
+        for (size_t i = 0; i < fr.size(); ++i)
+            if (fr[i].info >= 0 && box_area(fr[i].lo, fr[i].hi) > ba) { ba = box_area(fr[i].lo, fr[i].hi); best = (int)i; }
+        if (best < 0) break;
+        Item c, d;
+        ax = kids(fr[best].info, &c, &d);
+        fr[best] = c;
+        fr.insert(fr.begin() + best + 1, d);
+        for (auto& e : ex) { if (e.mid > best) e.mid++; if (e.hi > best) e.hi++; }   // ranges after the split slot shift
+        for (auto& e : ex) { if (e.lo > best) e.lo++; }
+        ex.push_back({ax, best, best + 1, best + 2});
+    }
+    GQuad q{};
+    q.n = (int)fr.size();
+    for (int i = 0; i < q.n; ++i) { q.info[i] = fr[i].info; memcpy(q.lo[i], fr[i].lo, 12); memcpy(q.hi[i], fr[i].hi, 12); }
+    for (int oct = 0; oct < 8; ++oct) {
+        // visit order: recursive over the expansion tree (ex[0] is the root)
+        std::vector<int> order;
+        std::function<void(int, int)> rec = [&](int lo, int hi) {
+            if (hi - lo == 1) { order.push_back(lo); return; }
+            for (const auto& e : ex)
+                if (e.lo == lo && e.hi == hi) {
+                    bool lf = (oct >> e.axis) & 1;
+                    if (lf) { rec(e.lo, e.mid); rec(e.mid, e.hi); } else { rec(e.mid, e.hi); rec(e.lo, e.mid); }
+                    return;
+                }
+            abort();
+        };
+        rec(0, q.n);
+        for (int i = 0; i < q.n; ++i) q.perm[oct][i] = (uint8_t)order[i];
+    }
+    const int me = (int)g_gq.size();
+    g_gq.push_back(q);
+    for (int i = 0; i < q.n; ++i)
+        if (q.info[i] >= 0) {
+            const int32_t c = build_gq(q.info[i]);
+            g_gq[me].info[i] = c;   // child quad index (>= 0), leaves keep their info (< 0)
+        }
+    return me;
+}
+Hit closest_gquad(const Ray& r) {
+    Hit h{-1.0f, -1, 0};
+    float tmax = FLT_MAX;
+    if (B->root_info >= 0 && g_gq.empty()) build_gq(B->root_info);
+    const int oct = (r.d.x > 0) | (r.d.y > 0) << 1 | (r.d.z > 0) << 2;
+    struct E { int32_t info; float t; } st[128];
+    int sp = 0;
+    int32_t cur = B->root_info >= 0 ? 0 : B->root_info;
+    while (true) {
+        if (cur >= 0) {
+            g_gqfetch++;
+            const GQuad& q = g_gq[cur];
+            E v[8];
+            int nv = 0;
+            for (int j = 0; j < q.n; ++j) {
+                const int c = q.perm[oct][j];
+                float t;
+                if (box_hit(r, q.lo[c], q.hi[c], &t) && t <= tmax) v[nv++] = {q.info[c], t};
+            }
+            for (int j = nv - 1; j >= 1; --j) st[sp++] = v[j];
+            if (nv) { cur = v[0].info; continue; }
+        } else {
+            int a, c;
+            leaf_range(cur, &a, &c);
+            g_gqleaf++;
+            const auto& lb = leaf_boxes[leaf_of_prim[a]];
+            float lt;
+            if (box_hit(r, lb.data(), lb.data() + 3, &lt) && lt <= tmax)
+                for (int i = a; i < a + c; ++i) {
+                    float t;
+                    if (prim_hit(r, B->prims[i], &t) && (t < h.t || h.t == -1.0f)) { h.t = t; h.prim = i; tmax = t; }
+                }
+        }
+        bool found = false;
+        while (sp > 0) { --sp; if (st[sp].t <= tmax) { cur = st[sp].info; found = true; break; } }
+        if (!found) break;
+    }
+    return h;
+}
+
 bool any_quad(const Ray& r, float tlim, long* qf, long* lf) {
     int32_t st[128]; int sp = 0; int32_t cur = B->qroot;
     while (true) {
         if (cur >= 0) {
             (*qf)++;
             const dl::Quad& q = B->quads[cur];
-            int n = q.exps >> 24;
+            int n = __builtin_popcount(q.exps >> 24);   // slot mask (contiguous in the occlusion tree)
             bool have = false; int32_t next = 0;
             for (int c = 0; c < n; ++c) {
                 float lo[3], hi[3], t;
@@ -315,6 +504,7 @@ bool any_quad(const Ray& r, float tlim, long* qf, long* lf) {
 int main(int argc, char** argv) {
     if (argc < 2) { fprintf(stderr, "usage: %s scene.xml [slack]\n", argv[0]); return 2; }
     if (argc > 2) g_slack = atof(argv[2]);
+    if (getenv("EXP_WIDTH")) g_width = atoi(getenv("EXP_WIDTH"));
     int dump_row = -1, dump_col = -1;          // --dump ROW COL: print the pixel's chain rays (o, d) as hex floats
     if (argc > 5 && !strcmp(argv[3], "--dump")) { dump_row = atoi(argv[4]); dump_col = atoi(argv[5]); }
     HostScene sc;
@@ -352,6 +542,7 @@ int main(int argc, char** argv) {
     long best_qb = -1; int best_rc[2] = {0, 0};
     long max_cqa = 0, max_walk_q = 0, walks_b = 0;
     long qfall = 0, qmis = 0, sq_f = 0, sl_f = 0, nshadow = 0;
+    long rq_mis = 0, max_crb = 0, gq_mis = 0, max_cgb = 0;
     long max_chain_ref = 0, max_chain_sah = 0, max_chain_mixed = 0;
     std::vector<long> chain_ref, chain_mixed;
     chain_ref.reserve((size_t)nx * ny);
@@ -360,11 +551,22 @@ int main(int argc, char** argv) {
             float su = ((float)col + 0.5f) * su_m, sv = ((float)row + 0.5f) * sv_m;
             Vf sp = sub(add(q, mul(u, su)), mul(v, sv));
             Ray r = make_ray(e, sub(sp, e));
-            long cr = 0, cs = 0, cm = 0, cq_a = 0, cq_b = 0;
+            long cr = 0, cs = 0, cm = 0, cq_a = 0, cq_b = 0, cr_b = 0, cg_b = 0;
             for (int k = 0; k <= sc.max_depth; ++k) {
                 if (row == dump_row && col == dump_col)
                     printf("RAY %a %a %a %a %a %a\n", r.o.x, r.o.y, r.o.z, r.d.x, r.d.y, r.d.z);
                 Hit hr = closest_ref(r), hs, hq;
+                {
+                    const long f0 = g_rqfetch + g_rqleaf;
+                    const Hit hx = closest_rquad(r);
+                    const long fr = g_rqfetch + g_rqleaf - f0;
+                    if (k >= 2) cr_b += fr;
+                    if (hx.prim != hr.prim || (hr.prim >= 0 && hx.t != hr.t)) rq_mis++;
+                    const long g0 = g_gqfetch + g_gqleaf;
+                    const Hit hg = closest_gquad(r);
+                    if (k >= 2) cg_b += g_gqfetch + g_gqleaf - g0;
+                    if (hg.prim != hr.prim || (hr.prim >= 0 && hg.t != hr.t)) gq_mis++;
+                }
                 int stt = closest_sah(r, &hs);
                 const long qf0 = g_qfetch + g_lfetch;
                 int qst = closest_quad(r, &hq);
@@ -415,6 +617,8 @@ int main(int argc, char** argv) {
             }
             chain_ref.push_back(cr);
             chain_qb.push_back(cq_b);
+            max_crb = std::max(max_crb, cr_b);
+            max_cgb = std::max(max_cgb, cg_b);
             if (cq_b > best_qb) { best_qb = cq_b; best_rc[0] = row; best_rc[1] = col; }
             max_cqa = std::max(max_cqa, cq_a);
             chain_mixed.push_back(cm);
@@ -432,6 +636,10 @@ int main(int argc, char** argv) {
     printf("quad closest: fallback %ld mismatch %ld; per walk: ref pair fetches %.2f leaves %.2f | quad fetches %.2f leaves %.2f\n",
            qfall, qmis, (double)g_rfetch / walks, (double)g_rleaf / walks, (double)g_qfetch / walks, (double)g_lfetch / walks);
     printf("shadow rays %ld: quad fetches %.2f leaves %.2f per ray\n", nshadow, (double)sq_f / nshadow, (double)sl_f / nshadow);
+    printf("ref-order quad: mismatch %ld; per walk quad fetches %.2f leaves %.2f; phase-B chain max rounds %ld\n",
+           rq_mis, (double)g_rqfetch / walks, (double)g_rqleaf / walks, max_crb);
+    printf("greedy ref-order quad: mismatch %ld; per walk quad fetches %.2f leaves %.2f; phase-B chain max rounds %ld; quads %zu\n",
+           gq_mis, (double)g_gqfetch / walks, (double)g_gqleaf / walks, max_cgb, g_gq.size());
     std::sort(chain_qb.begin(), chain_qb.end());
     printf("quad fetch rounds: phase-A chain max %ld, phase-B chain max %ld p99.99 %ld p99.9 %ld, max single walk %ld, phase-B walks %ld\n",
            max_cqa, chain_qb.back(), pct(chain_qb, 0.9999), pct(chain_qb, 0.999), max_walk_q, walks_b);

@@ -1,0 +1,45 @@
+#!/usr/bin/env python3
+"""Per-kernel register / scratch / spill table of a HIP source, from the
+compiler's kernel-resource-usage remarks (the Makefile's device flags).
+
+  python tools/resource_usage.py [csrc/pathchain.hip] [extra hipcc flags...]
+"""
+import re
+import subprocess
+import sys
+from pathlib import Path
+
+ROOT = Path(__file__).resolve().parent.parent
+PKG = ROOT / "raytracer-ceng477-graphics-hw-1_amd"
+
+
+def main():
+    src = sys.argv[1] if len(sys.argv) > 1 else "csrc/pathchain.hip"
+    extra = sys.argv[2:]
+    cmd = ["/opt/rocm/bin/hipcc", "-std=c++17", "-O3", "--offload-arch=gfx950", "-ffp-contract=off",
+           "-fno-fast-math", "-fPIC", f"-I{ROOT / 'include'}", "-Icsrc", "--cuda-device-only", "-c", src,
+           "-o", "/tmp/resource_usage.o", "-Rpass-analysis=kernel-resource-usage", *extra]
+    out = subprocess.run(cmd, cwd=PKG, capture_output=True, text=True).stderr
+    rows, cur = [], None
+    for line in out.splitlines():
+        m = re.search(r"remark: +(Function Name|VGPRs|AGPRs|ScratchSize \[bytes/lane\]|Occupancy \[waves/SIMD\]|"
+                      r"SGPRs Spill|VGPRs Spill|LDS Size \[bytes/block\]): (\S+)", line)
+        if not m:
+            continue
+        k, v = m.group(1), m.group(2)
+        if k == "Function Name":
+            cur = {"name": v}
+            rows.append(cur)
+        elif cur is not None:
+            cur[k.split(" [")[0]] = v
+    demangle = subprocess.run(["c++filt"], input="\n".join(r["name"] for r in rows), capture_output=True,
+                              text=True).stdout.splitlines()
+    print(f"{'kernel':60s} {'VGPR':>5s} {'occ':>4s} {'scratch':>8s} {'vspill':>7s} {'sspill':>7s} {'LDS':>7s}")
+    for r, n in zip(rows, demangle):
+        n = re.sub(r"\(.*", "", re.sub(r"\w+::\(anonymous namespace\)::", "", n))
+        print(f"{n[:60]:60s} {r.get('VGPRs', ''):>5s} {r.get('Occupancy', ''):>4s} {r.get('ScratchSize', ''):>8s} "
+              f"{r.get('VGPRs Spill', ''):>7s} {r.get('SGPRs Spill', ''):>7s} {r.get('LDS Size', ''):>7s}")
+
+
+if __name__ == "__main__":
+    main()
