@@ -128,6 +128,26 @@ const char* rt_last_error(void);
 int rt_abi_version(void);
 int rt_device_count(int* count);
 
+/* ---- multi-GPU (ABI 4) ----
+ * SURVEY.md §8(b) "N GPUs, one HIP stream each, one RCCL comm"; the
+ * reference's row-interleaved threads (raytracer.cpp:352-383) become row
+ * stripes over the GPUs of one node.  rt_set_devices(n), n >= 1: scenes
+ * created afterwards (rt_scene_create / rt_scene_load_xml) hold a replica on
+ * each of devices 0..n-1 and one RCCL communicator over them; rt_render and
+ * rt_render_cameras then split every frame into stripe_rows-row stripes dealt
+ * round-robin over the devices (env RT_GROUP_STRIPE, default 8), render them
+ * concurrently (one HIP stream per device), gather the uint8 slabs to device 0
+ * with ONE ncclGather over xGMI, un-interleave them there and copy the frame
+ * to the caller's buffer -- the same bytes as one GPU.  The asynchronous
+ * device-buffer entry points (rt_render_device, rt_render_frames_device,
+ * rt_render_cameras_device) keep using device 0 only: a one-process-per-GPU
+ * caller shards with their stripe/rank arguments instead.  n = 1 runs the
+ * same group path (RCCL communicator of one) on device 0; n = 0 (default):
+ * no group, one device (rt_options.device).  RCCL is loaded on first use. */
+int rt_set_devices(int n);
+/* Devices a scene renders on (1 unless created after rt_set_devices(n >= 1)). */
+int rt_scene_num_devices(const struct rt_scene* scene);
+
 /* ---- scene lifetime ---- */
 typedef struct rt_scene rt_scene;
 

@@ -86,6 +86,8 @@ _SIGS = [
     ("rt_last_error", ctypes.c_char_p, []),
     ("rt_abi_version", ctypes.c_int, []),
     ("rt_device_count", ctypes.c_int, [ctypes.POINTER(ctypes.c_int)]),
+    ("rt_set_devices", ctypes.c_int, [ctypes.c_int]),
+    ("rt_scene_num_devices", ctypes.c_int, [_P]),
     ("rt_scene_create", ctypes.c_int, [_P, ctypes.POINTER(Options), ctypes.POINTER(_P)]),
     ("rt_scene_load_xml", ctypes.c_int, [ctypes.c_char_p, ctypes.POINTER(Options), ctypes.POINTER(_P)]),
     ("rt_scene_destroy", None, [_P]),
@@ -143,6 +145,12 @@ def device_count() -> int:
     n = ctypes.c_int(0)
     _check(lib().rt_device_count(ctypes.byref(n)))
     return n.value
+
+
+def set_devices(n: int) -> None:
+    """rt_set_devices: scenes created afterwards render every frame on GPUs 0..n-1 (row stripes, one
+    RCCL gather to device 0); 1 = the same group path on one GPU; 0 = no group (default)."""
+    _check(lib().rt_set_devices(n))
 
 
 def slab_rows(height: int, stripe_rows: int, nranks: int) -> int:
@@ -277,6 +285,9 @@ class Scene:
         st = Stats()
         _check(lib().rt_counters_read(self._h, ctypes.byref(st)))
         return st.as_dict()
+
+    def num_devices(self) -> int:
+        return lib().rt_scene_num_devices(self._h)
 
     def check(self) -> None:
         """Synchronise and raise RtError(RT_ERR_LIMIT) if a walk was cut off by its step bound since the

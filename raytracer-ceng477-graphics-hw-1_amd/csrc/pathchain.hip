@@ -182,15 +182,6 @@ __device__ __forceinline__ Ray reflect_from_record(const rtk::DevScene& s, const
     return make_ray(pnt, add(d2, mul(mul(n2, 2.0f), rcos)));
 }
 
-// The same reflected ray from the hit values in registers (phase-B groups).
-__device__ __forceinline__ Ray reflect_from_record_regs(const rtk::DevScene& s, const V hitp, const V nn, const V d) {
-    const V pnt = add(hitp, mul(nn, s.eps));
-    const V d2 = nrm(d);
-    const V n2 = nrm(nn);
-    const float rcos = dot(neg(d2), n2);
-    return make_ray(pnt, add(d2, mul(mul(n2, 2.0f), rcos)));
-}
-
 // Shadow ray of task `owner` (raytracer.cpp:397-404).
 __device__ __forceinline__ Ray shadow_from_record(const rtk::DevScene& s, const PcParams& p, unsigned owner,
                                                   float* tlim) {

@@ -8,6 +8,7 @@
 //   --aa F           SSAA factor (1 disables, as DO_SSAA_ANTI_ALIASING false)
 //   --max-depth D    override MaxRecursionDepth
 //   --device N       HIP device ordinal
+//   --gpus N         render every frame on GPUs 0..N-1 (row stripes + one RCCL gather, rt_set_devices)
 //   --no-write       skip write_ppm (timing)
 #include <chrono>
 #include <cstdio>
@@ -33,24 +34,26 @@ int die(const char* what) {
 
 int main(int argc, char** argv) {
     const char* scene_path = nullptr;
-    int aa = 2, max_depth = -1000, device = -1;
+    int aa = 2, max_depth = -1000, device = -1, gpus = 0;
     bool write = true;
     for (int i = 1; i < argc; ++i) {
         if (!std::strcmp(argv[i], "--aa") && i + 1 < argc) aa = std::atoi(argv[++i]);
         else if (!std::strcmp(argv[i], "--max-depth") && i + 1 < argc) max_depth = std::atoi(argv[++i]);
         else if (!std::strcmp(argv[i], "--device") && i + 1 < argc) device = std::atoi(argv[++i]);
+        else if (!std::strcmp(argv[i], "--gpus") && i + 1 < argc) gpus = std::atoi(argv[++i]);
         else if (!std::strcmp(argv[i], "--no-write")) write = false;
         else if (argv[i][0] != '-' && !scene_path) scene_path = argv[i];
         else {
-            std::fprintf(stderr, "usage: %s scene.xml [--aa F] [--max-depth D] [--device N] [--no-write]\n", argv[0]);
+            std::fprintf(stderr, "usage: %s scene.xml [--aa F] [--max-depth D] [--device N] [--gpus N] [--no-write]\n", argv[0]);
             return 2;
         }
     }
     if (!scene_path || aa < 1) {
-        std::fprintf(stderr, "usage: %s scene.xml [--aa F] [--max-depth D] [--device N] [--no-write]\n", argv[0]);
+        std::fprintf(stderr, "usage: %s scene.xml [--aa F] [--max-depth D] [--device N] [--gpus N] [--no-write]\n", argv[0]);
         return 2;
     }
 
+    if (gpus > 0 && rt_set_devices(gpus) != RT_OK) return die("gpus");
     const auto begin1 = std::chrono::steady_clock::now();
     rt_options opts{device, 0, 0};
     rt_scene* scene = nullptr;
@@ -71,7 +74,7 @@ int main(int argc, char** argv) {
         char name[1024];
         if (rt_scene_get_camera(scene, c, &cams[c], name, sizeof name) != RT_OK) return die("camera");
         names[c] = name;
-        std::printf("Rendering %s on GPU (SSAA %dx%d)...\n", name, aa, aa);
+        std::printf("Rendering %s on %d GPU(s) (SSAA %dx%d)...\n", name, rt_scene_num_devices(scene), aa, aa);
         imgs[c].resize((size_t)cams[c].image_width * cams[c].image_height * 3);
         outs[c] = imgs[c].data();
     }

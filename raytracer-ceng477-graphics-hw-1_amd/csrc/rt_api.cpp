@@ -5,6 +5,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <atomic>
 #include <chrono>
 #include <cstdlib>
 #include <cmath>
@@ -23,6 +24,7 @@
 namespace {
 
 thread_local std::string g_err;
+std::atomic<int> g_devices{0};          // rt_set_devices: device group of scenes created afterwards (0: none)
 
 int fail(int code, const std::string& msg) {
     g_err = msg;
@@ -87,6 +89,8 @@ struct rt_scene {
     rtx::FlatBVH bvh;
     int device = 0;
     bool host_only = false;
+    int opt_flags = 0;                         // rt_options.flags at creation (replicas use the same)
+    rt_group* group = nullptr;                 // multi-GPU (rt_set_devices): replicas + RCCL comm, rt_multi.cpp
     rtk::DevScene dev{};
     dl::Node* d_nodes = nullptr;
     dl::Prim* d_prims = nullptr;
@@ -172,6 +176,7 @@ struct rt_scene {
     }
 
     ~rt_scene() {
+        if (group) rt_internal_group_destroy(group);
         free_ws();
         for (int i = 0; i < kSlots; ++i) {
             (void)hipFree(arenas[i].p);
@@ -201,12 +206,29 @@ int select_device(const rt_options* opts, int* dev) {
     return RT_OK;
 }
 
+int upload_scene(rt_scene* s, const rt_options* opts);
+
 int finish_scene(rt_scene* s, const rt_options* opts) {
     rtx::prepare_triangles(s->host);
     std::string err = rtx::build_bvh(s->host, s->bvh, opts ? opts->build_threads : 0);
     if (!err.empty()) return fail(RT_ERR_LIMIT, err);
     s->host_only = opts && (opts->flags & RT_OPT_HOST_ONLY);
+    s->opt_flags = opts ? opts->flags : 0;
     if (s->host_only) return RT_OK;
+    const int ndev = g_devices.load();
+    if (ndev >= 1) {                      // device group: the primary on device 0, replicas on 1..n-1
+        rt_options o = opts ? *opts : rt_options{0, 0, 0};
+        o.device = 0;
+        int rc = upload_scene(s, &o);
+        if (rc) return rc;
+        return rt_internal_group_create(s, ndev, &s->group);
+    }
+    return upload_scene(s, opts);
+}
+
+// Device copies of a built scene (s->host, s->bvh) on opts->device, plus the
+// per-scene tuning knobs.
+int upload_scene(rt_scene* s, const rt_options* opts) {
     int rc = select_device(opts, &s->device);
     if (rc) return rc;
 
@@ -756,6 +778,7 @@ int rt_scene_set_max_depth(rt_scene* s, int d) {
     if (d < -1 || d > 64) return fail(RT_ERR_ARG, "max_recursion_depth out of range [-1, 64]");
     s->host.max_depth = d;
     s->dev.max_depth = d;
+    if (s->group) return rt_internal_group_set_max_depth(s->group, d);
     return RT_OK;
 }
 
@@ -1005,6 +1028,21 @@ int rt_render_cameras(rt_scene* s, const rt_camera* cams, int n, int aa, uint8_t
         if (!outs[i]) return fail(RT_ERR_ARG, "output buffer is NULL");
     }
     const auto t0 = std::chrono::steady_clock::now();
+    if (s->group) {                  // device group: the cameras one after another, each frame on every device
+        rt_stats sum{}, one{};
+        for (int i = 0; i < n; ++i) {
+            const int rc = rt_internal_group_render(s->group, &cams[i], aa, outs[i], stats ? &one : nullptr);
+            if (rc) return rc;
+            sum.primary_rays += one.primary_rays; sum.shadow_rays += one.shadow_rays;
+            sum.reflection_rays += one.reflection_rays; sum.node_visits += one.node_visits;
+            sum.tri_tests += one.tri_tests; sum.sphere_tests += one.sphere_tests; sum.kernel_ms += one.kernel_ms;
+        }
+        if (stats) {
+            *stats = sum;
+            stats->wall_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+        }
+        return RT_OK;
+    }
     HIP_TRY(hipSetDevice(s->device));
     // one device frame per camera (one arena, grown on demand): every frame is
     // launched before any copy, so the frames run concurrently
@@ -1089,6 +1127,25 @@ int rt_counters_read(rt_scene* s, rt_stats* st) {
     return check_device_error(s);
 }
 
+int rt_set_devices(int n) {
+    if (n < 0) return fail(RT_ERR_ARG, "device count must be >= 0");
+    if (n >= 1) {
+        int count = 0;
+        if (hipGetDeviceCount(&count) != hipSuccess || count == 0) return fail(RT_ERR_NO_DEVICE, "no HIP device visible");
+        if (n > count)
+            return fail(RT_ERR_ARG, "rt_set_devices(" + std::to_string(n) + "): only " + std::to_string(count) +
+                                        " devices visible");
+    }
+    g_devices.store(n);
+    return RT_OK;
+}
+
+int rt_scene_num_devices(const rt_scene* s) {
+    if (!s) return fail(RT_ERR_ARG, "scene is NULL");
+    if (s->host_only) return 0;
+    return s->group ? rt_internal_group_size(s->group) : 1;
+}
+
 int rt_scene_check(rt_scene* s) {
     if (!s) return fail(RT_ERR_ARG, "scene is NULL");
     if (s->host_only) return RT_OK;
@@ -1102,6 +1159,7 @@ int rt_render(rt_scene* s, const rt_camera* cam, int aa, uint8_t* out_rgb, rt_st
     if (s->host_only) return fail(RT_ERR_NO_DEVICE, "scene was created with RT_OPT_HOST_ONLY");
     int rc = check_camera(cam, aa);
     if (rc) return rc;
+    if (s->group) return rt_internal_group_render(s->group, cam, aa, out_rgb, stats);
     const auto t0 = std::chrono::steady_clock::now();
     HIP_TRY(hipSetDevice(s->device));
     const size_t bytes = (size_t)cam->image_width * cam->image_height * 3;
@@ -1178,3 +1236,21 @@ int rt_downsample_host(const uint8_t* in, int width, int height, int factor, uin
 }
 
 }  // extern "C"
+
+int rt_internal_replicate(const rt_scene* src, int device, rt_scene** out) {
+    *out = nullptr;
+    rt_scene* s = new (std::nothrow) rt_scene();
+    if (!s) return fail(RT_ERR_ARG, "out of host memory");
+    s->host = src->host;
+    s->bvh = src->bvh;
+    s->opt_flags = src->opt_flags;
+    const rt_options o{device, src->opt_flags, 0};
+    const int rc = upload_scene(s, &o);
+    if (rc) {
+        delete s;
+        return rc;
+    }
+    s->dev.max_depth = src->dev.max_depth;
+    *out = s;
+    return RT_OK;
+}

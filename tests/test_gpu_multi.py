@@ -1,0 +1,102 @@
+"""GPU: the C-ABI's multi-GPU device group (rt_set_devices, rt_multi.cpp) --
+row stripes rendered per device, ONE ncclGather of the uint8 slabs to device 0,
+un-interleave, D2H.  On a one-GPU box the group of one device runs the whole
+path (replica set-up, RCCL communicator, gather, unshuffle, counters); larger
+groups are exercised by the driver's 8-GPU node.  Every image must equal the
+reference golden (raytracer.cpp:487-525 renders, ppm.cpp:4-39 bytes).
+"""
+from __future__ import annotations
+
+import hashlib
+import subprocess
+
+import numpy as np
+import pytest
+
+from conftest import config_path, golden_by_name, load_golden_image
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def torch_cuda():
+    torch = pytest.importorskip("torch")
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    torch.cuda.init()
+    return torch
+
+
+@pytest.fixture
+def group(pkg, torch_cuda):
+    """Scenes created inside the fixture form a device group over every visible GPU."""
+    n = pkg.device_count()
+    pkg.set_devices(n)
+    yield n
+    pkg.set_devices(0)
+
+
+def _stats(s):
+    return (s["primary_rays"], s["shadow_rays"], s["reflection_rays"], s["node_visits"], s["tri_tests"],
+            s["sphere_tests"])
+
+
+def _counters(c):
+    return (c["primary"], c["shadow"], c["reflection"], c["node_visits"], c["tri_tests"], c["sphere_tests"])
+
+
+@pytest.mark.parametrize("stripe", ["8", "3"])
+@pytest.mark.parametrize("name", ["C3_hm_1080p_d6_aa1", "C3_hm_1080p_d6_aa2", "cornellbox_aa1", "C1_simple_aa3"])
+def test_group_render_equals_golden(name, stripe, group, goldens, pkg, scene_dir, monkeypatch):
+    monkeypatch.setenv("RT_GROUP_STRIPE", stripe)
+    g = golden_by_name(goldens, name)
+    with pkg.Scene.from_xml(config_path(scene_dir, g["config"])) as s:
+        assert s.num_devices() == group
+        cams = s.cameras()
+        for cam in g["cameras"]:
+            c, _ = cams[cam["camera"]]
+            img, st = s.render(c, aa=g["aa"], stats=True)
+            assert np.array_equal(img, load_golden_image(cam)), cam["image"]
+            assert _stats(st) == _counters(cam["counters"])          # summed over the devices
+            img2, _ = s.render(c, aa=g["aa"])
+            assert np.array_equal(img2, load_golden_image(cam))
+
+
+def test_group_render_cameras_and_depth_override(group, goldens, pkg, scene_dir):
+    g = golden_by_name(goldens, "cornellbox_aa1")
+    with pkg.Scene.from_xml(config_path(scene_dir, g["config"])) as s:
+        cams = [c for c, _ in s.cameras()]
+        imgs, st = s.render_cameras(cams, aa=1, stats=True)
+        for cam in g["cameras"]:
+            assert np.array_equal(imgs[cam["camera"]], load_golden_image(cam))
+        assert st["primary_rays"] == sum(c["counters"]["primary"] for c in g["cameras"])
+    # MaxRecursionDepth override reaches every replica: C3 scene at depth 2 = the verbatim depth
+    with pkg.Scene.from_xml(config_path(scene_dir, "C3_hm_1080p_d6")) as s, \
+            pkg.Scene.from_xml(config_path(scene_dir, "C3_hm_1080p_d6"), device=0, render_path="chain") as one:
+        s.set_max_depth(2)
+        one.set_max_depth(2)
+        a, _ = s.render(s.camera(0), aa=1)
+        b, _ = one.render(one.camera(0), aa=1)
+        assert np.array_equal(a, b)
+
+
+@pytest.mark.parametrize("name", ["cornellbox_aa1", "car_aa1"])
+def test_cli_gpus_writes_reference_ppms(name, goldens, pkg, scene_dir, tmp_path, torch_cuda):
+    """The drop-in CLI with --gpus (rt_set_devices before the scene load)."""
+    g = golden_by_name(goldens, name)
+    n = pkg.device_count()
+    r = subprocess.run([str(pkg.CLI_PATH), str(config_path(scene_dir, g["config"])), "--aa", str(g["aa"]),
+                        "--gpus", str(n)], cwd=tmp_path, capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, r.stderr
+    assert f"on {n} GPU(s)" in r.stdout
+    for cam in g["cameras"]:
+        data = (tmp_path / cam["image"]).read_bytes()
+        assert hashlib.sha256(data).hexdigest() == cam["sha256_ppm"], cam["image"]
+
+
+def test_set_devices_errors(pkg, torch_cuda):
+    with pytest.raises(pkg.RtError):
+        pkg.set_devices(-1)
+    with pytest.raises(pkg.RtError):
+        pkg.set_devices(pkg.device_count() + 1)
+    pkg.set_devices(0)
