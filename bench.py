@@ -9,11 +9,23 @@ RCCL collective over xGMI and un-interleaved by a rank-0 kernel
 Frames are submitted --inflight at a time (default 96) as frame batches
 (rt_render_frames_device: one persistent grid walks several frames' samples, so
 one frame's serial mirror-chain tail runs beside the others' bulk; one gather
-per batch).  Every frame's full work is done and counted; the single-frame
-latency is reported beside `value` as config.frame_latency_ms.  Inputs (scene +
-BVH) are resident in HBM before timing; frames stay in HBM (no D2H, no
-write_ppm) — see DESIGN.md for the PCIe-inclusive figure.  Scaling is strong
-(the frame is fixed, split over N).
+per batch).  Every frame's full work is done and counted.  `value` is that
+serving throughput with the scene resident in HBM and frames left in HBM (no
+D2H, no write_ppm).  Beside it, first-class: `single_frame` (one frame alone on
+the GPU, device time) and `drop_in` -- SURVEY.md §8(d)'s ms/frame, rt_render's
+wall time from camera upload to the uint8 frame in host memory (PCIe
+included), the drop-in caller's case.  Scaling is strong (the frame is fixed,
+split over N).
+
+Roofline: the walks fetch a small, cache-resident scene, so
+the memory roofline that bounds them is the L2's (MI355X_MICROARCH.md §L2,
+~34.5 TB/s aggregate), not HBM's.  `achieved` = the bytes the TIMED kernels
+fetch and move per frame -- traversal bytes counted by a production-fetch
+counting pass (RT_COUNT_PROD: the same walks as the timed kernels, counting
+their node, leaf-record and primitive loads) plus the workspace bytes of the
+chain path (records, task ids, occlusion bytes, output; a per-ray model of
+pathchain.hip) -- divided by the frame's kernel time.  The HBM bytes actually
+moved (rocprofv3 FETCH_SIZE / WRITE_SIZE, profiles/) are reported beside it.
 
   python bench.py [--gpus N] [--steps K] [--warmup W] [--aa F] [--config C3]
   torchrun --nproc-per-node N bench.py --gpus N ...
@@ -34,9 +46,21 @@ sys.path.insert(0, str(ROOT))
 
 import __graft_entry__ as graft  # noqa: E402
 
-HBM_PEAK_GBPS = 8000.0     # MI355X spec (MI355X_MICROARCH.md; 6.29 TB/s measured float4 copy)
-# Algorithmic bytes per unit of work
+HBM_PEAK_GBPS = 8000.0     # MI355X spec (MI355X_MICROARCH.md §HBM; 6.29 TB/s measured float4 copy)
+L2_PEAK_GBPS = 34500.0     # MI355X_MICROARCH.md §L2: ~34.5 TB/s aggregate over the 8 XCDs
+# The reference's algorithmic bytes per unit of work, reported for comparison
 B_NODE, B_TRI, B_SPH, B_PIX = 32, 36, 16, 3
+
+
+def workspace_bytes(c: dict, nlights: int, out_pixels: int) -> int:
+    """Chain-path workspace bytes of one frame from its exact ray counts (pathchain.hip):
+    every hit writes a 48-B record and is shaded from it again in k_finish (48 B + 8 B of occlusion
+    dwords); every sample writes and reads its 4-B path word; every shadow task id is written,
+    packed (read + write) and read (16 B), its ray re-derived from the record's first 32 B and its
+    1-B result written; every reflection re-reads its 48-B record; every output pixel is 3 B."""
+    hits = c["shadow_rays"] // max(1, nlights)
+    return (hits * (48 + 48 + 8) + c["primary_rays"] * 8 + c["shadow_rays"] * (16 + 32 + 1)
+            + c["reflection_rays"] * 48 + out_pixels * 3)
 
 # kernels one frame launches, per render path (the roofline covers all of them)
 PATH_KERNELS = {
@@ -63,23 +87,42 @@ def parse():
     ap.add_argument("--stripe-rows", type=int, default=4,
                     help="output rows per round-robin stripe (4: best rank balance at N=8, tools/exp_shard.py)")
     ap.add_argument("--path", default="chain", choices=sorted(PATH_KERNELS), help="render path (all bit-identical)")
-    ap.add_argument("--cpu-seconds", type=float, default=10.0, help="CPU baseline budget (rank 0, N=1)")
+    ap.add_argument("--cpu-seconds", type=float, default=15.0, help="CPU baseline budget (rank 0, N=1)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--trace", action="store_true",
+                    help="profiling runs (tools/profile_round.sh): only the counting passes, warmup and timed frames "
+                         "run, so per-frame kernel sums from rocprofv3 can be checked against kernel_ms")
     ap.add_argument("--inflight", type=int, default=None,
                     help="frames submitted together (rt_render_frames_device frame batches; 1 = one frame at a "
                          "time; default 96, C5 1: its frames are already 250x larger than one launch's chunk)")
     return ap.parse_args()
 
 
-def cpu_baseline(xml: str, aa: int, rays_ps_per_frame: int, budget_s: float) -> dict:
-    """Reference CPU renderer timed on this host (rank 0 only).  Prefers the
-    unmodified reference compiled from its sources (oracle/_ref/ref_harness,
-    kind "reference"); falls back to the C restatement (kind "port")."""
+def host_cores() -> dict:
+    """CPUs this process may use: the affinity set, bounded by a cgroup CPU quota if one is set (the GPU
+    boxes give a job a share of a large host: nproc shows the whole machine there)."""
+    nproc = os.cpu_count() or 1
     try:
-        cores = len(os.sched_getaffinity(0))
+        aff = len(os.sched_getaffinity(0))
     except AttributeError:
-        cores = os.cpu_count() or 1
-    threads = max(1, min(16, cores))
+        aff = nproc
+    quota = None
+    try:
+        q, per = Path("/sys/fs/cgroup/cpu.max").read_text().split()[:2]
+        if q != "max":
+            quota = max(1, int(int(q) / int(per)))
+    except (OSError, ValueError):
+        pass
+    return {"nproc": nproc, "affinity": aff, "cgroup_quota": quota, "usable": min(aff, quota or aff)}
+
+
+def cpu_baseline(xml: str, aa: int, rays_ps_per_frame: int, budget_s: float) -> dict:
+    """Reference CPU renderer timed on this host (rank 0 only), with every usable host core as one thread
+    each -- the reference's own default is std::thread::hardware_concurrency() (raytracer.cpp:367).
+    Prefers the unmodified reference compiled from its sources (oracle/_ref/ref_harness, kind
+    "reference"); falls back to the C restatement (kind "port")."""
+    hc = host_cores()
+    threads = max(1, min(256, hc["usable"]))
     host = {}        # the reference's own XML load and BVH build times (parser.cpp, bvh.h), for the host rows
     harness = ROOT / "oracle" / "_ref" / "ref_harness"
     if harness.exists():
@@ -110,8 +153,9 @@ def cpu_baseline(xml: str, aa: int, rays_ps_per_frame: int, budget_s: float) -> 
         med = sorted(ts)[len(ts) // 2]
         kind = "port"
     return {"value": round(rays_ps_per_frame / med / 1e6, 3), "unit": "Mray/s", "cores": threads, "kind": kind,
-            "ms_per_frame": round(med * 1e3, 3), **host,
-            "sample": f"{reps} full frames of the same workload (median), render only, {threads} threads"}
+            "ms_per_frame": round(med * 1e3, 3), **host, "host_cpus": hc,
+            "sample": f"{reps} full frames of the same workload (median), render only, {threads} threads "
+                      f"(all usable cores; nproc {hc['nproc']})"}
 
 
 def main() -> int:
@@ -183,13 +227,29 @@ def main() -> int:
         print(f"[bench rank {rank}] {msg} t={time.perf_counter() - t0:.1f}s", file=sys.stderr, flush=True)
 
     note(f"scene loaded {W}x{H} aa{aa}")
-    # Counting pass (not timed): exact per-rank work for the byte model.
+    # Counting passes (not timed).  (1) the reference's exact work (rays, node visits, tests): the
+    # metric's ray counts, equal to the reference's counters (parity tests); (2) the production walks'
+    # own fetched bytes (RT_COUNT_PROD: a scene whose counting kernels walk the timed kernels' trees).
     scene.counters_reset(sp)
     scene.render_device(cam, aa, slab.data_ptr(), sp, S, rank, world, count=True)
     cnt = scene.counters_read()
-    note("counting pass done")
-    alg_bytes = (cnt["node_visits"] * B_NODE + cnt["tri_tests"] * B_TRI + cnt["sphere_tests"] * B_SPH
-                 + rows * W * aa * aa * B_PIX)
+    ref_alg_bytes = (cnt["node_visits"] * B_NODE + cnt["tri_tests"] * B_TRI + cnt["sphere_tests"] * B_SPH
+                     + rows * W * aa * aa * B_PIX)
+    os.environ["RT_COUNT_PROD"] = "1"
+    try:
+        pscene = pkg.Scene.from_xml(xml, device=local, render_path=a.path)
+    finally:
+        del os.environ["RT_COUNT_PROD"]
+    pscene.counters_reset(sp)
+    pscene.render_device(cam, aa, slab.data_ptr(), sp, S, rank, world, count=True)
+    pcnt = pscene.counters_read()
+    pscene.close()
+    if any(pcnt[k] != cnt[k] for k in ("primary_rays", "shadow_rays", "reflection_rays")):
+        raise RuntimeError(f"production counting pass disagrees on ray counts: {pcnt} vs {cnt}")
+    traversal_bytes = pcnt["node_visits"]
+    ws_bytes = workspace_bytes(cnt, Path(xml).read_text().count("<PointLight"), rows * W)
+    alg_bytes = traversal_bytes + ws_bytes
+    note("counting passes done")
     ps_local = cnt["primary_rays"] + cnt["shadow_rays"]
     tot = torch.tensor([ps_local, cnt["primary_rays"], cnt["shadow_rays"], cnt["reflection_rays"]],
                        dtype=torch.float64, device=dev)
@@ -257,26 +317,29 @@ def main() -> int:
 
     # single-frame latency (one frame alone on the GPU, this rank's stripes; reported, not `value`)
     lat = []
-    for _ in range(5):
+    for _ in range(0 if a.trace else 5):
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         e0.record(stream)
         scene.render_device(cam, aa, slab.data_ptr(), sp, S, rank, world)
         e1.record(stream)
         torch.cuda.synchronize(dev)
         lat.append(e0.elapsed_time(e1))
-    lat_ms = sorted(lat)[len(lat) // 2]
+    lat_ms = sorted(lat)[len(lat) // 2] if lat else float("nan")
     tmax = torch.tensor([elapsed, kern_ms, lat_ms], dtype=torch.float64, device=dev)
     tmax = all_reduce(tmax, dist.ReduceOp.MAX)
     elapsed, kern_ms_max, lat_ms = tmax.tolist()
 
-    # PCIe-inclusive figure (rank 0, N=1 only; never `value`): rt_render = upload camera, render, D2H copy
+    # SURVEY §8(d) ms/frame (rank 0, N=1 only; beside `value`): rt_render wall time = camera upload,
+    # render, D2H of the uint8 frame, one frame at a time
     host_ms = None
-    if world == 1:
+    if world == 1 and not a.trace:
         scene.render(cam, aa)
-        t1 = time.perf_counter()
-        for _ in range(5):
+        ts = []
+        for _ in range(7):
+            t1 = time.perf_counter()
             scene.render(cam, aa)
-        host_ms = (time.perf_counter() - t1) / 5 * 1e3
+            ts.append(time.perf_counter() - t1)
+        host_ms = sorted(ts)[len(ts) // 2] * 1e3
 
     traffic, traffic_src = None, None
     tfile = ROOT / "profiles" / "traffic.json"
@@ -289,6 +352,7 @@ def main() -> int:
         ms = elapsed / a.steps * 1e3
         value = ps_frame * a.steps / elapsed / 1e6
         achieved = alg_bytes / (kern_ms / 1e3) / 1e9
+        traffic_gbps = traffic / (kern_ms / 1e3) / 1e9 if traffic else None
         if backend != "nccl":
             desc += f" [REHEARSAL: {backend} host-staged gather, all ranks on one GPU; not a measurement]"
         line = {
@@ -300,32 +364,50 @@ def main() -> int:
             "config": {"workload": config, "description": desc, "width": W, "height": H, "aa": aa,
                        "max_recursion_depth": 6 if config != "C2_cornellbox_800_d0" else 0,
                        "parallelism": f"stripes{S}x{world}" + ("+rccl_gather" if world > 1 else ""),
-                       "frames_in_flight": F, "frame_latency_ms": round(lat_ms, 4),
+                       "frames_in_flight": F, "frame_latency_ms": round(lat_ms, 4) if lat else None,
+                       "workspace_slots": int(os.environ.get("RT_SLOTS", "3")),
                        # every frame this process rendered on the GPU (counting pass, warmup, timed, latency,
                        # host-buffer runs): the divisor for whole-run PMC totals (tools/summarize_profile.py)
-                       "frames_rendered_total": 1 + max(a.warmup, F) + a.steps + 5 + (6 if world == 1 else 0),
+                       "frames_rendered_total": 2 + max(a.warmup, F) + a.steps
+                                                + (0 if a.trace else 5 + (8 if world == 1 else 0)),
+                       # frames the non-counting kernels rendered in a --trace run (warmup + timed)
+                       "trace_frames": max(a.warmup, F) + a.steps if a.trace else None,
                        "assembled_frames_equal_single_gpu": frames_ok,
                        "primary_rays": prim_frame, "shadow_rays": shadow_frame, "reflection_rays": refl_frame,
                        "mray_s_all": round((ps_frame + refl_frame) * a.steps / elapsed / 1e6, 3),
                        "scene_load_s": round(load_s, 4),
                        "host_build": {"bvh_build_ms": round(binfo["build_ms"], 2), "ref_tree_ms": round(binfo["ref_ms"], 2),
                                       "wide_tree_ms": round(binfo["wide_ms"], 2), "threads": binfo["build_threads"]},
-                       "host_buffer_ms_per_frame": round(host_ms, 4) if host_ms else None},
-            "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
-                         "frac": round(achieved / HBM_PEAK_GBPS, 4), "traffic": traffic,
-                         # measured HBM rate (PMC bytes per frame / frame time): the scene is L2/MALL-resident,
-                         # so the algorithmic rate above can exceed the HBM peak while this stays far below it
-                         "traffic_gbps": round(traffic / (kern_ms / 1e3) / 1e9, 2) if traffic else None,
-                         "traffic_frac": round(traffic / (kern_ms / 1e3) / 1e9 / HBM_PEAK_GBPS, 4) if traffic else None,
-                         "traffic_source": traffic_src,
+                       "value_definition": f"frames submitted {F} at a time as frame batches, scene and frames "
+                                           "resident in HBM, max-over-ranks wall time"},
+            "single_frame": ({"ms": round(lat_ms, 4), "mray_s": round(ps_frame / lat_ms / 1e3, 3),
+                              "definition": "one frame alone on the GPU (rt_render_device), device time"}
+                             if lat else None),
+            "drop_in": ({"ms_per_frame": round(host_ms, 4), "mray_s": round(ps_frame / host_ms / 1e3, 3),
+                         "definition": "SURVEY §8(d): rt_render wall time, camera upload to the uint8 frame in "
+                                       "host memory (PCIe included), one frame at a time"} if host_ms else None),
+            "roofline": {"bound": "l2", "achieved": round(achieved, 2), "peak": L2_PEAK_GBPS, "unit": "GB/s",
+                         "frac": round(achieved / L2_PEAK_GBPS, 4), "traffic": traffic,
+                         "bound_note": "the walks read a ~6 MB cache-resident scene (L2/MALL); the bytes the timed "
+                                       "kernels fetch and move are priced against the L2's aggregate bandwidth; "
+                                       "the HBM bytes they actually move (PMC) are `hbm`",
+                         "alg_bytes_per_launch": int(alg_bytes), "launch_unit": "one frame (this rank's stripes)",
+                         "alg_bytes_split": {"traversal": int(traversal_bytes), "workspace": int(ws_bytes)},
+                         "hbm": {"bytes_per_frame": traffic, "gbps": round(traffic_gbps, 2) if traffic else None,
+                                 "peak": HBM_PEAK_GBPS,
+                                 "frac": round(traffic_gbps / HBM_PEAK_GBPS, 4) if traffic else None,
+                                 "source": traffic_src},
+                         "reference_model": {"bytes_per_frame": int(ref_alg_bytes),
+                                             "note": "SURVEY §8(d) per-operation model of the reference's own walk "
+                                                     "(32 B/node visit, 36 B/triangle test, 16 B/sphere test, 3 B/px)",
+                                             "counts": {k: cnt[k] for k in ("node_visits", "tri_tests",
+                                                                            "sphere_tests")}},
                          "path": a.path, "kernels": PATH_KERNELS[a.path],
                          "kernel": "one frame = " + " + ".join(PATH_KERNELS[a.path])
                                    + (f" (frames in batches of up to {F}: kernel_ms = batch time / frames)" if F > 1 else ""),
-                         "kernel_ms": round(kern_ms, 4),
-                         "alg_bytes_per_launch": int(alg_bytes), "launch_unit": "one frame (this rank's stripes)",
-                         "counts_per_launch": {k: cnt[k] for k in ("node_visits", "tri_tests", "sphere_tests")}},
+                         "kernel_ms": round(kern_ms, 4)},
         }
-        if world == 1 and not a.no_cpu_baseline:
+        if world == 1 and not a.no_cpu_baseline and not a.trace:
             line["cpu_baseline"] = cpu_baseline(xml, aa, ps_frame, a.cpu_seconds)
         print(json.dumps(line), flush=True)
     scene.close()

@@ -38,7 +38,8 @@ struct DevScene {
     float sroot_lo[3], sroot_hi[3];
     int sroot_info;
     int use_stree;        // NaN-free shadow rays walk: 0 the BVH, 1 the binary occlusion tree, 2 its 4-wide form
-    int count_stree;      // diagnostics: counting passes walk the occlusion tree too (counts then differ)
+    int count_prod;       // counting passes walk the production trees and count fetched BYTES in the node
+                          // counter (bench.py roofline; RT_COUNT_PROD at scene creation)
     const dl::Quad* quads;
     const float4* lrec;   // leaf records (dl::LeafHead + prims), indexed in 16-B units
     int qroot;

@@ -363,8 +363,8 @@ int upload_scene(rt_scene* s, const rt_options* opts) {
     if (const char* e = std::getenv("RT_LEAF_WAIT")) d.leaf_wait = std::max(0, std::min(64, std::atoi(e)));
     d.leaf_wait_any = d.leaf_wait;
     if (const char* e = std::getenv("RT_LEAF_WAIT_ANY")) d.leaf_wait_any = std::max(0, std::min(64, std::atoi(e)));
-    // diagnostics: counting passes walk the occlusion tree too (counts then measure that tree)
-    d.count_stree = std::getenv("RT_STREE_COUNT") ? 1 : 0;
+    // measurement: counting passes walk the production trees and count fetched bytes (bench.py)
+    d.count_prod = std::getenv("RT_COUNT_PROD") ? 1 : 0;
     if (const char* e = std::getenv("RT_PRIO")) d.prio = std::atoi(e) != 0;
     if (const char* e = std::getenv("RT_TOP")) d.top_pairs = std::min(d.top_pairs, std::max(0, std::atoi(e)));
     return RT_OK;

@@ -299,9 +299,12 @@ struct StackPriv {
 // Root test (the reference's first pop).  false: nothing to traverse.
 // Any-hit pops test the box only (raytracer.cpp:268-271); closest-hit also
 // needs bt <= tMax (:184), which prunes a NaN bt.
-// Any-hit walks of NaN-free rays use the occlusion tree outside counting
-// passes (exact by the monotonicity argument at build_shadow_tree); counting
-// passes and other rays walk the reference BVH.
+// Any-hit walks of NaN-free rays use the occlusion tree and closest-hit walks
+// the reference tree's wide form outside counting passes (exact: see
+// build_shadow_tree and wide_closest_step); reference counting passes and
+// other rays walk the reference BVH.  Production-fetch counting passes
+// (s.count_prod) walk exactly like the production kernels and count, in
+// w.nodes, the BYTES each walk fetches (bench.py roofline).
 template <bool COUNT>
 __device__ __forceinline__ bool walk_begin(const rtk::DevScene& s, const Ray& r, Walk& k, Work& w,
                                            bool any = false) {
@@ -311,21 +314,21 @@ __device__ __forceinline__ bool walk_begin(const rtk::DevScene& s, const Ray& r,
     k.steps = 0;
     k.fast = ray_nan_free(r);
     if (s.nnodes <= 0) return false;
-    if (COUNT) w.nodes++;
+    if (COUNT && !s.count_prod) w.nodes++;    // the reference's root pop (the root box is a kernel argument)
     float bt;
-    if ((!COUNT || s.count_stree) && any && k.fast && s.use_stree == 2) {
+    if ((!COUNT || s.count_prod) && any && k.fast && s.use_stree == 2) {
         k.tree = nullptr;                    // 4-wide occlusion tree (quad_any_step)
         k.cur = s.qroot;
         return true;
     }
-    if ((!COUNT || s.count_stree) && any && k.fast && s.use_stree) {
+    if ((!COUNT || s.count_prod) && any && k.fast && s.use_stree) {
         k.tree = s.spairs;
         k.cur = s.sroot_info;
         const float4 lo = make_float4(s.sroot_lo[0], s.sroot_lo[1], s.sroot_lo[2], 0.0f);
         const float4 hi = make_float4(s.sroot_hi[0], s.sroot_hi[1], s.sroot_hi[2], 0.0f);
         return box_hit(r, lo, hi, &bt);
     }
-    if (!COUNT && !any && k.fast && s.use_wide) {
+    if ((!COUNT || s.count_prod) && !any && k.fast && s.use_wide) {
         k.tree = nullptr;                    // the reference tree's wide form, reference order
         k.cur = s.wroot;
         k.sgn = (r.d.x > 0.0f ? 1 : 0) | (r.d.y > 0.0f ? 2 : 0) | (r.d.z > 0.0f ? 4 : 0);
@@ -455,11 +458,13 @@ __device__ __forceinline__ bool leaf_postponed(int wait, const Walk& k) {
 //     so every update - and the final (t, primitive) - is the reference's.
 //     Only interior work differs (skipped intermediate boxes, conservative
 //     quantized tests).  No tolerance, no restart.
-template <class STK>
-__device__ __forceinline__ bool wide_closest_step(const rtk::DevScene& s, const Ray& r, STK& stk, Walk& k) {
+template <bool COUNT, class STK>
+__device__ __forceinline__ bool wide_closest_step(const rtk::DevScene& s, const Ray& r, STK& stk, Walk& k,
+                                                  Work& w) {
     constexpr int W = dl::kWideSlots;
-    if (leaf_postponed(s.leaf_wait, k)) return false;
+    if (!COUNT && leaf_postponed(s.leaf_wait, k)) return false;
     if (k.cur >= 0) {
+        if (COUNT) w.nodes += 16 * (W > 4 ? 6 : 5) + 4;   // the node's dwordx4 loads + the octant's rank word
         const float4* N = reinterpret_cast<const float4*>(&s.wnodes[k.cur]);
         const float4 q0 = N[0], q1 = N[1], q2 = N[2], q3 = N[3], q4 = N[4];
         const float4 q5 = W > 4 ? N[5] : q4;
@@ -531,10 +536,16 @@ __device__ __forceinline__ bool wide_closest_step(const rtk::DevScene& s, const 
         const float4* L = s.lrec + (k.cur & ~dl::kLeafBit);
         const float4 h0 = L[0], h1 = L[1], c0 = L[2], c1 = L[3], c2 = L[4];
         float lt;
+        if (COUNT) w.nodes += 80;                 // leaf head + first primitive
         if (box_hit_fast(r, h0, h1, &lt) && lt <= k.tmax) {   // the reference leaf's exact box (:184)
-            for_leaf_prims(L, __float_as_int(h1.w), __float_as_int(h0.w), c0, c1, c2,
+            const int cnt = __float_as_int(h0.w), slot0 = __float_as_int(h1.w);
+            for_leaf_prims(L, slot0, cnt, c0, c1, c2,
                            [&](int slot, const float4& p0, const float4& p1, const float4& p2) {
                                float ti;
+                               if (COUNT) {
+                                   if (slot - slot0 + 1 < cnt) w.nodes += 48;     // the next primitive's loads
+                                   if (__float_as_int(p0.w) >= 0) w.tris++; else w.spheres++;
+                               }
                                const bool h = __float_as_int(p0.w) >= 0 ? tri_hit(r, p0, p1, p2, &ti)
                                                                         : sphere_hit(r, p0, p1, &ti);
                                if (h && (ti < k.best.t || k.best.t == -1.0f)) {   // :213-221
@@ -560,11 +571,11 @@ __device__ __forceinline__ bool wide_closest_step(const rtk::DevScene& s, const 
 // One closest-hit step; returns true when the walk is finished (result in k.best).
 template <bool COUNT, class FETCH, class STK, bool PIPE = false>
 __device__ __forceinline__ bool closest_step(const rtk::DevScene& s, const Ray& r, STK& stk, Walk& k, Work& w) {
-    if (!COUNT && k.tree == nullptr) return wide_closest_step(s, r, stk, k);
+    if ((!COUNT || s.count_prod) && k.tree == nullptr) return wide_closest_step<COUNT>(s, r, stk, k, w);
     if (k.cur >= 0) {
         float4 l0, l1, r0, r1;
         fetch_pair(k, l0, l1, r0, r1);
-        if (COUNT) w.nodes += 2;
+        if (COUNT) w.nodes += s.count_prod ? 64 : 2;
         float tl, tr;
         bool hl, hr;
         box_pair(r, k.fast, l0, l1, r0, r1, hl, hr, tl, tr);
@@ -587,6 +598,7 @@ __device__ __forceinline__ bool closest_step(const rtk::DevScene& s, const Ray& 
         auto test = [&](int i, const float4& p0, const float4& p1, const float4& p2) {
             float t;
             bool h;
+            if (COUNT && s.count_prod) w.nodes += 48;
             if (__float_as_int(p0.w) >= 0) {
                 if (COUNT) w.tris++;
                 h = tri_hit(r, p0, p1, p2, &t);
@@ -636,8 +648,8 @@ __device__ __forceinline__ int any_step(const rtk::DevScene& s, const Ray& r, fl
         const int il = __float_as_int(l0.w), ir = __float_as_int(r0.w);
         const bool hn = left_first ? hl : hr, hf = left_first ? hr : hl;
         const int in_ = left_first ? il : ir, if_ = left_first ? ir : il;
-        if (COUNT) w.nodes++;
-        if (hf || COUNT) {
+        if (COUNT) w.nodes += s.count_prod ? 64 : 1;
+        if (hf || (COUNT && !s.count_prod)) {
             stk.put(k.sp, make_int2(if_, hf ? 1 : 0));
             ++k.sp;
         }
@@ -651,6 +663,7 @@ __device__ __forceinline__ int any_step(const rtk::DevScene& s, const Ray& r, fl
         if (for_prims(s, a, cnt, [&](int, const float4& p0, const float4& p1, const float4& p2) {
                 float t;
                 bool h;
+                if (COUNT && s.count_prod) w.nodes += 48;
                 if (__float_as_int(p0.w) >= 0) {
                     if (COUNT) w.tris++;
                     h = tri_hit(r, p0, p1, p2, &t);
@@ -665,7 +678,7 @@ __device__ __forceinline__ int any_step(const rtk::DevScene& s, const Ray& r, fl
     while (k.sp > 0) {
         --k.sp;
         const int2 e = stk.at(k.sp);
-        if (COUNT) w.nodes++;
+        if (COUNT && !s.count_prod) w.nodes++;
         if (e.y) {
             k.cur = e.x;
             return 0;
@@ -687,12 +700,12 @@ __device__ __forceinline__ int quad_any_step(const rtk::DevScene& s, const Ray& 
     if (k.cur >= 0) {
         QuadHits q;
         quad_hits(s.quads, k.cur, r, q);
+        if (COUNT) w.nodes += 64;
         int next = 0;
         bool have = false;
 #pragma unroll
         for (int c = 0; c < 4; ++c) {
             if (q.hit[c]) {
-                if (COUNT) w.nodes++;
                 if (!have) {
                     next = q.code[c];
                     have = true;
@@ -710,11 +723,14 @@ __device__ __forceinline__ int quad_any_step(const rtk::DevScene& s, const Ray& 
         const float4* L = s.lrec + (k.cur & ~dl::kLeafBit);
         const float4 h0 = L[0], h1 = L[1], c0 = L[2], c1 = L[3], c2 = L[4];
         float bt;
+        if (COUNT) w.nodes += 80;                    // leaf head + first primitive
         if (box_hit_fast(r, h0, h1, &bt)) {          // the reference leaf's exact box (NaN-free ray)
-            if (for_leaf_prims(L, __float_as_int(h1.w), __float_as_int(h0.w), c0, c1, c2,
-                               [&](int, const float4& p0, const float4& p1, const float4& p2) {
+            const int cnt = __float_as_int(h0.w), slot0 = __float_as_int(h1.w);
+            if (for_leaf_prims(L, slot0, cnt, c0, c1, c2,
+                               [&](int slot, const float4& p0, const float4& p1, const float4& p2) {
                                    float t;
                                    bool h;
+                                   if (COUNT && slot - slot0 + 1 < cnt) w.nodes += 48;   // next primitive
                                    if (__float_as_int(p0.w) >= 0) {
                                        if (COUNT) w.tris++;
                                        h = tri_hit(r, p0, p1, p2, &t);

@@ -1,18 +1,22 @@
 #!/usr/bin/env python3
 """Summarise a tools/profile_round.sh run into profiles/:
-  TAG_kernel_stats.csv   rocprofv3 --stats output (per-kernel calls / avg ns)
-  TAG_traffic.json       per-kernel FETCH_SIZE / WRITE_SIZE means and the HBM
-                         bytes per frame: sum over the frame's kernels of
-                         2 x FETCH_SIZE + WRITE_SIZE (MI355X_MICROARCH.md §HBM:
-                         FETCH_SIZE tallies 128-B requests at 64 B on gfx950)
-  TAG_bench.jsonl        the bench JSON line of the same build
-Also writes profiles/traffic.json (the file bench.py reads for `roofline.traffic`).
+  TAG_kernel_stats.csv   rocprofv3 --stats output (per-kernel calls / avg ns) of the bench --trace run
+  TAG_traffic.json       per-frame kernel time and HBM bytes of the timed (non-counting) kernels:
+                         kernel time = sum of their durations / the run's frames (warmup + timed),
+                         checked against the bench line's kernel_ms; HBM bytes = 2 x FETCH_SIZE +
+                         WRITE_SIZE (MI355X_MICROARCH.md §HBM: FETCH_SIZE tallies 128-B requests at
+                         64 B on gfx950) summed the same way
+  TAG_bench.jsonl        the bench JSON lines of the same build (--trace line, then the full line)
+Also writes profiles/traffic.json (the file bench.py reads for `roofline.hbm`).
+Counting-pass kernels (k_*<true>) are excluded; the untemplated kernels they share (k_pack_*, k_finish)
+are charged their counting-pass calls at the average duration.
+
+  python tools/summarize_profile.py TAG gpurun_out/prof_TAG
 """
-import csv
 import collections
+import csv
 import glob
 import json
-import os
 import re
 import shutil
 import sys
@@ -25,43 +29,67 @@ prof.mkdir(exist_ok=True)
 
 
 def kname(s):
-    m = re.search(r"(k_[a-z_0-9]+)", s)
-    return m.group(1) if m else s[:40]
+    """k_name, with '<true>' kept for counting-pass instantiations."""
+    m = re.search(r"(k_[a-z_0-9]+)(<(true|false)>)?", s)
+    if not m:
+        return s[:40]
+    return m.group(1) + ("<true>" if m.group(3) == "true" else "")
 
 
+def lines(path):
+    return [json.loads(l) for l in open(path) if l.startswith("{")] if path.exists() else []
+
+
+trace = (lines(out / "trace.jsonl") or [{}])[-1]
+full = (lines(out / "bench.jsonl") or [{}])[-1]
+frame_kernels = trace.get("roofline", {}).get("kernels", [])
+frames = trace.get("config", {}).get("trace_frames")
+if not frames:
+    sys.exit("trace.jsonl lacks config.trace_frames (run bench.py --trace)")
+
+# kernel time per frame
 stats = glob.glob(str(out / "kt" / "**" / "*kernel_stats.csv"), recursive=True)
+per_kernel_ms, counting_calls = {}, 0
 if stats:
     shutil.copy(stats[0], prof / f"{tag}_kernel_stats.csv")
+    rows = list(csv.DictReader(open(stats[0])))
+    counting_calls = sum(int(r["Calls"]) for r in rows if kname(r["Name"]) == "k_chain<true>")
+    for r in rows:
+        k = kname(r["Name"])
+        if k not in frame_kernels:
+            continue
+        calls, tot = int(r["Calls"]), float(r["TotalDurationNs"])
+        if k in ("k_pack_a", "k_pack_b", "k_finish", "k_finish_any", "k_occlude"):
+            tot -= min(calls, counting_calls) * float(r["AverageNs"])     # the counting passes' launches
+        per_kernel_ms[k] = tot / frames / 1e6
+kernel_ms_sum = sum(per_kernel_ms.values())
 
+# HBM bytes per frame
 per = collections.defaultdict(lambda: collections.defaultdict(list))
 for pas in ("fetch", "write"):
     for f in glob.glob(str(out / pas / "**" / "*counter_collection.csv"), recursive=True):
         for r in csv.DictReader(open(f)):
             per[kname(r["Kernel_Name"])][r["Counter_Name"]].append(float(r["Counter_Value"]))
-kern = {}
-for k, d in per.items():
-    kern[k] = {c: sum(v) / len(v) for c, v in d.items()}
-bench = [json.loads(l) for l in open(out / "bench.jsonl") if l.startswith("{")]
-line = bench[-1] if bench else {}
-frame_kernels = line.get("roofline", {}).get("kernels", [])
-tot = 0.0
-nframes = line.get("config", {}).get("frames_rendered_total")
-if nframes:
-    # frame batches: launches cover different frame counts, so divide the run's totals by its frames
-    for k in frame_kernels:
-        if k in per:
-            tot += (2.0 * sum(per[k].get("FETCH_SIZE", [])) + sum(per[k].get("WRITE_SIZE", []))) * 1024.0
-    tot /= nframes
-else:
-    for k in frame_kernels:
-        if k in kern:
-            tot += (2.0 * kern[k].get("FETCH_SIZE", 0.0) + kern[k].get("WRITE_SIZE", 0.0)) * 1024.0
-res = {"tag": tag, "config": line.get("config", {}).get("workload"), "path": line.get("roofline", {}).get("path"),
-       "per_kernel_KiB": kern, "frame_kernels": frame_kernels, "hbm_bytes_per_frame": tot,
-       "frames_rendered_total": nframes,
-       "note": "2*FETCH_SIZE + WRITE_SIZE per kernel (KiB), summed over one frame's kernels"
-               + (" (run totals / frames_rendered_total)" if nframes else "")}
+hbm = 0.0
+per_kernel_bytes = {}
+for k in frame_kernels:
+    if k in per:
+        b = (2.0 * sum(per[k].get("FETCH_SIZE", [])) + sum(per[k].get("WRITE_SIZE", []))) * 1024.0
+        per_kernel_bytes[k] = b / frames
+        hbm += b
+hbm /= frames
+res = {"tag": tag, "config": trace.get("config", {}).get("workload"), "path": trace.get("roofline", {}).get("path"),
+       "frames": frames, "workspace_slots": trace.get("config", {}).get("workspace_slots"),
+       "frames_in_flight": trace.get("config", {}).get("frames_in_flight"),
+       "kernel_ms_per_frame_rocprof": kernel_ms_sum, "per_kernel_ms_per_frame": per_kernel_ms,
+       "kernel_ms_bench_trace": trace.get("roofline", {}).get("kernel_ms"),
+       "hbm_bytes_per_frame": hbm, "per_kernel_hbm_bytes_per_frame": per_kernel_bytes,
+       "note": "timed (non-counting) kernels only; per frame = run totals / (warmup + timed frames); "
+               "HBM bytes = 2*FETCH_SIZE + WRITE_SIZE"}
 (prof / f"{tag}_traffic.json").write_text(json.dumps(res, indent=1))
 (prof / "traffic.json").write_text(json.dumps(res, indent=1))
-shutil.copy(out / "bench.jsonl", prof / f"{tag}_bench.jsonl")
-print(json.dumps({"hbm_bytes_per_frame": tot, "kernels": frame_kernels}))
+with open(prof / f"{tag}_bench.jsonl", "w") as f:
+    for l in (trace, full):
+        if l:
+            f.write(json.dumps(l) + "\n")
+print(json.dumps({k: res[k] for k in ("kernel_ms_per_frame_rocprof", "kernel_ms_bench_trace", "hbm_bytes_per_frame")}))
