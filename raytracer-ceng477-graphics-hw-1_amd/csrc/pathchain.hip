@@ -756,8 +756,11 @@ __global__ __launch_bounds__(kBlock) void k_pack_b(PcParams p) {
 }
 
 // Workgroups [0, gb): phase B chains (continuations); the rest: phase A's shadow tasks.
+#ifndef RT_MIX_WAVES
+#define RT_MIX_WAVES 4           // 4 waves/SIMD: no VGPR spills (5: 29 spilled); single frame 1.17-1.19 vs 1.22-1.24 ms
+#endif
 template <bool COUNT>
-__global__ __launch_bounds__(kBlock, RT_OCC_WAVES_PER_EU) void k_mix(rtk::DevScene s, rtk::Eye e, PcParams p) {
+__global__ __launch_bounds__(kBlock, RT_MIX_WAVES) void k_mix(rtk::DevScene s, rtk::Eye e, PcParams p) {
     const bool chain = blockIdx.x < (unsigned)p.gb;
     if (threadIdx.x == 0) g_ccnt = 0;
     if (chain && kBq > 0) bq_init();

@@ -471,6 +471,70 @@ Hit closest_gquad(const Ray& r) {
     return h;
 }
 
+// Any-hit over the SAH tree (spairs) collapsed greedily to g_width slots per node
+// (largest-area interior slot expanded first): fetch rounds only.
+struct SNode { int32_t info[8]; float lo[8][3], hi[8][3]; int n; };
+std::vector<SNode> g_sn;
+int32_t build_sn(int32_t pair) {
+    struct It { int32_t info; float lo[3], hi[3]; };
+    auto kids = [&](int32_t p, It* a, It* b) {
+        const dl::Pair& P = B->spairs[p];
+        *a = It{P.l_info, {P.l_minx, P.l_miny, P.l_minz}, {P.l_maxx, P.l_maxy, P.l_maxz}};
+        *b = It{P.r_info, {P.r_minx, P.r_miny, P.r_minz}, {P.r_maxx, P.r_maxy, P.r_maxz}};
+    };
+    std::vector<It> fr(2);
+    kids(pair, &fr[0], &fr[1]);
+    while ((int)fr.size() < g_width) {
+        int best = -1;
+        double ba = -1;
+        for (size_t i = 0; i < fr.size(); ++i)
+            if (fr[i].info >= 0 && box_area(fr[i].lo, fr[i].hi) > ba) { ba = box_area(fr[i].lo, fr[i].hi); best = (int)i; }
+        if (best < 0) break;
+        It c, d;
+        kids(fr[best].info, &c, &d);
+        fr[best] = c;
+        fr.insert(fr.begin() + best + 1, d);
+    }
+    SNode q{};
+    q.n = (int)fr.size();
+    for (int i = 0; i < q.n; ++i) { q.info[i] = fr[i].info; memcpy(q.lo[i], fr[i].lo, 12); memcpy(q.hi[i], fr[i].hi, 12); }
+    const int me = (int)g_sn.size();
+    g_sn.push_back(q);
+    for (int i = 0; i < q.n; ++i)
+        if (q.info[i] >= 0) g_sn[me].info[i] = build_sn(q.info[i]);
+    return me;
+}
+long g_snf = 0, g_snl = 0;
+bool any_wide(const Ray& r, float tlim) {
+    if (g_sn.empty()) build_sn(B->sroot_info);
+    int32_t st[256];
+    int sp = 0;
+    int32_t cur = 0;
+    while (true) {
+        if (cur >= 0) {
+            g_snf++;
+            const SNode& q = g_sn[cur];
+            bool have = false;
+            int32_t next = 0;
+            for (int c = 0; c < q.n; ++c) {
+                float t;
+                if (box_hit(r, q.lo[c], q.hi[c], &t)) { if (!have) { next = q.info[c]; have = true; } else st[sp++] = q.info[c]; }
+            }
+            if (have) { cur = next; continue; }
+        } else {
+            g_snl++;
+            int a, c;
+            leaf_range(cur, &a, &c);
+            const auto& lb = leaf_boxes[leaf_of_prim[a]];
+            float lt;
+            if (box_hit(r, lb.data(), lb.data() + 3, &lt))
+                for (int i = a; i < a + c; ++i) { float t; if (prim_hit(r, B->prims[i], &t) && t < tlim) return true; }
+        }
+        if (sp == 0) return false;
+        cur = st[--sp];
+    }
+}
+
 bool any_quad(const Ray& r, float tlim, long* qf, long* lf) {
     int32_t st[128]; int sp = 0; int32_t cur = B->qroot;
     while (true) {
@@ -542,7 +606,7 @@ int main(int argc, char** argv) {
     long best_qb = -1; int best_rc[2] = {0, 0};
     long max_cqa = 0, max_walk_q = 0, walks_b = 0;
     long qfall = 0, qmis = 0, sq_f = 0, sl_f = 0, nshadow = 0;
-    long rq_mis = 0, max_crb = 0, gq_mis = 0, max_cgb = 0;
+    long rq_mis = 0, max_crb = 0, gq_mis = 0, max_cgb = 0, aw_mis = 0;
     long max_chain_ref = 0, max_chain_sah = 0, max_chain_mixed = 0;
     std::vector<long> chain_ref, chain_mixed;
     chain_ref.reserve((size_t)nx * ny);
@@ -607,7 +671,8 @@ int main(int argc, char** argv) {
                     Vf lp{L.position.x, L.position.y, L.position.z};
                     float tl = len(sub(lp, pnt));
                     Ray sr = make_ray(pnt, nrm(sub(lp, pnt)));
-                    any_quad(sr, tl, &sq_f, &sl_f);
+                    const bool o1 = any_quad(sr, tl, &sq_f, &sl_f);
+                    if (o1 != any_wide(sr, tl)) aw_mis++;
                     nshadow++;
                 }
                 if (!sc.materials[mat - 1].is_mirror) break;
@@ -636,6 +701,8 @@ int main(int argc, char** argv) {
     printf("quad closest: fallback %ld mismatch %ld; per walk: ref pair fetches %.2f leaves %.2f | quad fetches %.2f leaves %.2f\n",
            qfall, qmis, (double)g_rfetch / walks, (double)g_rleaf / walks, (double)g_qfetch / walks, (double)g_lfetch / walks);
     printf("shadow rays %ld: quad fetches %.2f leaves %.2f per ray\n", nshadow, (double)sq_f / nshadow, (double)sl_f / nshadow);
+    printf("shadow rays, SAH collapsed to %d slots: node fetches %.2f leaves %.2f per ray, mismatch %ld\n", g_width,
+           (double)g_snf / nshadow, (double)g_snl / nshadow, aw_mis);
     printf("ref-order quad: mismatch %ld; per walk quad fetches %.2f leaves %.2f; phase-B chain max rounds %ld\n",
            rq_mis, (double)g_rqfetch / walks, (double)g_rqleaf / walks, max_crb);
     printf("greedy ref-order quad: mismatch %ld; per walk quad fetches %.2f leaves %.2f; phase-B chain max rounds %ld; quads %zu\n",
