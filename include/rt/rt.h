@@ -33,7 +33,7 @@
 extern "C" {
 #endif
 
-#define RT_ABI_VERSION 4
+#define RT_ABI_VERSION 5
 
 typedef enum rt_status {
     RT_OK = 0,
@@ -221,6 +221,11 @@ int rt_render_cameras(rt_scene* scene, const rt_camera* cams, int n, int aa_fact
  * reference tree (ABI 2). */
 int rt_walk_timing(rt_scene* scene, const float* rays, int n, int lanes, int reps, int mode,
                    unsigned long long* out);
+/* Diagnostics: out[i] = the device's specular power term for base[i],
+ * exponent[i] -- (float)pow((double)base, (double)exponent) of the C library
+ * (raytracer.cpp:414) -- on the current device (host arrays, synchronous;
+ * ABI 5). */
+int rt_phong_pow(const float* base, const float* exponent, float* out, int n);
 /* Rows in one rank's slab (max over ranks, so all slabs have equal size). */
 int rt_slab_rows(int height, int stripe_rows, int nranks);
 /* Rank-0 reassembly: slabs[nranks][slab_rows][W][3] (gathered) -> image[H][W][3]. */

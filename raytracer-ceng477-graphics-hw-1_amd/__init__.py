@@ -106,6 +106,7 @@ _SIGS = [
     ("rt_render_frames_device", ctypes.c_int, [_P, ctypes.POINTER(Camera), ctypes.c_int, ctypes.c_int, ctypes.c_int,
                                                ctypes.c_int, ctypes.c_int, _P, _P, ctypes.c_int]),
     ("rt_walk_timing", ctypes.c_int, [_P, _P, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int, _P]),
+    ("rt_phong_pow", ctypes.c_int, [_P, _P, _P, ctypes.c_int]),
     ("rt_slab_rows", ctypes.c_int, [ctypes.c_int, ctypes.c_int, ctypes.c_int]),
     ("rt_unshuffle_stripes", ctypes.c_int, [_P, _P, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int, _P]),
     ("rt_counters_reset", ctypes.c_int, [_P, _P]),
@@ -151,6 +152,19 @@ def set_devices(n: int) -> None:
     """rt_set_devices: scenes created afterwards render every frame on GPUs 0..n-1 (row stripes, one
     RCCL gather to device 0); 1 = the same group path on one GPU; 0 = no group (default)."""
     _check(lib().rt_set_devices(n))
+
+
+def phong_pow(base, exponent) -> np.ndarray:
+    """Diagnostics (rt_phong_pow): the device's specular power term,
+    (float)pow((double)base, (double)exponent) as raytracer.cpp:414 computes it."""
+    b = np.ascontiguousarray(base, dtype=np.float32)
+    e = np.ascontiguousarray(exponent, dtype=np.float32)
+    if b.shape != e.shape:
+        raise ValueError("base and exponent differ in shape")
+    out = np.empty_like(b)
+    _check(lib().rt_phong_pow(b.ctypes.data_as(ctypes.c_void_p), e.ctypes.data_as(ctypes.c_void_p),
+                              out.ctypes.data_as(ctypes.c_void_p), b.size))
+    return out
 
 
 def slab_rows(height: int, stripe_rows: int, nranks: int) -> int:

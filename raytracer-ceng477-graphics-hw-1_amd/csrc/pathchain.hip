@@ -1414,6 +1414,18 @@ hipError_t launch_walk_timing(const rtk::DevScene& s, const float* rays, int n, 
     return hipGetLastError();
 }
 
+// Diagnostics (rt_phong_pow): the specular power term exactly as the shading
+// kernels evaluate it (phong_pow: integer fast path, double-double fallback).
+__global__ __launch_bounds__(kBlock) void k_phong_pow(const float* base, const float* expo, float* out, int n) {
+    const int i = (int)(blockIdx.x * kBlock + threadIdx.x);
+    if (i < n) out[i] = phong_pow(base[i], expo[i]);
+}
+
+hipError_t launch_phong_pow(const float* base, const float* expo, float* out, int n, hipStream_t st) {
+    hipLaunchKernelGGL(k_phong_pow, dim3((n + kBlock - 1) / kBlock), dim3(kBlock), 0, st, base, expo, out, n);
+    return hipGetLastError();
+}
+
 unsigned chain_block_scap(int n0, int grid, int levels, int nlights) {
     const unsigned units = ((unsigned)n0 + 255u) / 256u;
     const unsigned per_block = (units + (unsigned)grid - 1u) / (unsigned)grid;

@@ -111,6 +111,8 @@ unsigned fused_wave_qcap(int n0, int grid, int levels, int nlights);
 hipError_t launch_fused_chunk(const rtk::DevScene& s, const rtk::Eye& e, const PcParams& p, bool count,
                               hipStream_t stream);
 
+// Diagnostics: phong_pow on the device (rt_phong_pow).
+hipError_t launch_phong_pow(const float* base, const float* expo, float* out, int n, hipStream_t st);
 // Diagnostics: dependent-step latency of single closest-hit walks (rt_walk_timing).
 hipError_t launch_walk_timing(const rtk::DevScene& s, const float* rays, int n, int lanes, int reps, int mode,
                               unsigned long long* out, hipStream_t st);

@@ -148,7 +148,14 @@ struct rt_scene {
     // on demand, carved per frame); slot 0 serves single renders, slots
     // [0, kSlots) the concurrent frames of rt_render_cameras*.
     static constexpr int kSlots = 4;
-    struct Arena { char* p = nullptr; size_t bytes = 0; } arenas[kSlots];
+    // An arena may be used from any caller stream: `last` is recorded after each
+    // use on `last_stream`, and a use from another stream first waits on it.
+    struct Arena {
+        char* p = nullptr;
+        size_t bytes = 0;
+        hipEvent_t last = nullptr;
+        hipStream_t last_stream = nullptr;
+    } arenas[kSlots];
     hipStream_t slot_stream[kSlots] = {};
     hipEvent_t slot_done[kSlots] = {};
     hipEvent_t fork_ev = nullptr;
@@ -180,6 +187,7 @@ struct rt_scene {
         free_ws();
         for (int i = 0; i < kSlots; ++i) {
             (void)hipFree(arenas[i].p);
+            if (arenas[i].last) (void)hipEventDestroy(arenas[i].last);
             if (slot_stream[i]) (void)hipStreamDestroy(slot_stream[i]);
             if (slot_done[i]) (void)hipEventDestroy(slot_done[i]);
         }
@@ -570,8 +578,10 @@ int render_chain(rt_scene* s, const rtk::Eye& eye, const rtk::FrameParams& f, bo
         o_sqB = L.take<unsigned>((size_t)gb * scapB); o_scntB = L.take<unsigned>(gb + 1);
         o_sflatB = L.take<unsigned>(cap * (levels - levels_a) * nl); o_totals = L.take<unsigned>(4);
     }
+    // order this use after the arena's previous one (possibly on another stream)
+    if (arena.last && arena.last_stream != st) HIP_TRY(hipStreamWaitEvent(st, arena.last, 0));
     if (arena.bytes < L.off) {
-        if (arena.p) HIP_TRY(hipStreamSynchronize(st));   // the stream's previous frame may still use it
+        if (arena.p) HIP_TRY(hipStreamSynchronize(st));   // the previous frames on it may still use it
         (void)hipFree(arena.p);
         arena.p = nullptr;
         arena.bytes = 0;
@@ -637,6 +647,9 @@ int render_chain(rt_scene* s, const rtk::Eye& eye, const rtk::FrameParams& f, bo
         else HIP_TRY(rtc::launch_chain_chunk(s->dev, eye, p, count, st));
     }
     if (p.trace) trace_dump(s, st, 0, (unsigned)cap, (unsigned)p.ogrid, trace_n);   // last chunk only
+    if (!arena.last) HIP_TRY(hipEventCreateWithFlags(&arena.last, hipEventDisableTiming));
+    HIP_TRY(hipEventRecord(arena.last, st));
+    arena.last_stream = st;
     return RT_OK;
 }
 
@@ -1096,6 +1109,20 @@ int rt_walk_timing(rt_scene* s, const float* rays, int n, int lanes, int reps, i
     (void)hipFree(dr);
     (void)hipFree(dout);
     if (e != hipSuccess) return fail(RT_ERR_HIP, std::string("walk timing: ") + hipGetErrorName(e));
+    return RT_OK;
+}
+
+int rt_phong_pow(const float* base, const float* exponent, float* out, int n) {
+    if (!base || !exponent || !out || n < 0) return fail(RT_ERR_ARG, "bad phong_pow arguments");
+    if (n == 0) return RT_OK;
+    float* d = nullptr;
+    HIP_TRY(hipMalloc(reinterpret_cast<void**>(&d), (size_t)n * 3 * sizeof(float)));
+    hipError_t e = hipMemcpy(d, base, (size_t)n * sizeof(float), hipMemcpyHostToDevice);
+    if (e == hipSuccess) e = hipMemcpy(d + n, exponent, (size_t)n * sizeof(float), hipMemcpyHostToDevice);
+    if (e == hipSuccess) e = rtc::launch_phong_pow(d, d + n, d + 2 * (size_t)n, n, nullptr);
+    if (e == hipSuccess) e = hipMemcpy(out, d + 2 * (size_t)n, (size_t)n * sizeof(float), hipMemcpyDeviceToHost);
+    (void)hipFree(d);
+    if (e != hipSuccess) return fail(RT_ERR_HIP, std::string("phong_pow: ") + hipGetErrorName(e));
     return RT_OK;
 }
 

@@ -336,6 +336,26 @@ def test_render_cameras_device_stream(goldens, pkg, scene_dir, torch_cuda):
             assert np.array_equal(o.cpu().numpy(), load_golden_image(cam))
 
 
+def test_render_device_alternating_streams(goldens, pkg, scene_dir, torch_cuda):
+    """Asynchronous renders of one scene issued back to back on two different
+    non-blocking streams share the scene's workspace arena: each use waits for
+    the previous one (its last-use event), so every frame equals its golden."""
+    torch = torch_cuda
+    g = golden_by_name(goldens, "cornellbox_aa1")
+    with pkg.Scene.from_xml(config_path(scene_dir, g["config"]), device=0) as s:
+        cams = [s.cameras()[c["camera"]][0] for c in g["cameras"]]
+        streams = [torch.cuda.Stream(), torch.cuda.Stream()]
+        order = [0, 1, 2, 1, 0, 2, 2, 0]
+        outs = [torch.empty((cams[c].image_height, cams[c].image_width, 3), dtype=torch.uint8, device="cuda")
+                for c in order]
+        for i, c in enumerate(order):
+            s.render_device(cams[c], 1, outs[i].data_ptr(), streams[i % 2].cuda_stream)
+        torch.cuda.synchronize()
+        s.check()
+        for i, c in enumerate(order):
+            assert np.array_equal(outs[i].cpu().numpy(), load_golden_image(g["cameras"][c])), f"render {i}"
+
+
 def test_render_cameras_errors(pkg, scene_dir, torch_cuda):
     with pkg.Scene.from_xml(config_path(scene_dir, "simple.xml"), device=0) as s:
         with pytest.raises(pkg.RtError):
