@@ -117,10 +117,10 @@ typedef struct rt_bvh_info {
     int triangles, spheres;
     double build_ms;         /* whole host build                                  */
     double ref_ms;           /* the reference tree (bvh.h:48-163) alone  (ABI 2) */
-    double wide_ms;          /* the 4-wide SAH tree over the same leaves (ABI 2) */
+    double wide_ms;          /* the SAH occlusion tree + both wide trees (ABI 2) */
     int build_threads;       /* threads the build used                   (ABI 2) */
-    int wide_nodes;          /* 4-wide nodes                             (ABI 2) */
-    uint64_t wide_hash;      /* FNV-1a of the 4-wide nodes + leaf records (ABI 2) */
+    int wide_nodes;          /* wide nodes of both wide trees (occlusion + reference order) */
+    uint64_t wide_hash;      /* FNV-1a of both wide trees + leaf records (ABI 2) */
 } rt_bvh_info;
 
 /* ---- errors / devices ---- */

@@ -65,48 +65,35 @@ struct alignas(16) Pair {
 };
 struct LeafBig { int32_t start, count; };
 
-// Occlusion tree node, 4-wide, 64 B (four dwordx4 loads test four children):
-//   {origin.xyz, exps}  exps = ex | ey << 8 | ez << 16 | slot mask << 24, scale_a = 2^(e_a - 127)
-//   {qlo[3][4] bytes, qhi[3][4] bytes}          axis-major: dword a = axis a's byte of children 0..3
-//       lo = origin_a + qlo[a][c] * scale_a,  hi = origin_a + qhi[a][c] * scale_a  (float, exact
-//       power-of-two scale; the host verifies every decoded box CONTAINS the child's exact box);
-//       a ray picks its near/far plane per axis by swapping whole dwords
-//   {child[4]}  >= 0: quad index; < 0: kLeafBit | offset of a leaf record (16-B units) in LeafRec[]
-//   {order, pad}  reference-order quads (host_scene.cpp build_ref_quads): per octant of the ray
-//       direction (bit a set iff d[a] > 0), one byte of four 2-bit slot indices in the
-//       reference's visiting order; octants 0-3 in `order`, 4-7 in `pad`; 0 in the occlusion tree
-// Leaves are the reference BVH's leaves.  A leaf record is the leaf's header
-// (its EXACT box, tested exactly before the primitives) followed by copies of
-// its primitives, so the box and the first primitive arrive in one round trip:
+// Leaves of the wide trees are the reference BVH's leaves.  A leaf record is
+// the leaf's header (its EXACT box, tested exactly before the primitives)
+// followed by copies of its primitives, so the box and the first primitive
+// arrive in one round trip:
 //   LeafHead {lo.xyz, count} {hi.xyz, slot0}   slot0 = Prim[] index of the first primitive
 //   count x Prim (48 B, same encoding and order as Prim[])
-struct alignas(16) Quad {
-    float ox, oy, oz; uint32_t exps;
-    uint32_t q[6];        // qlo x,y,z dwords (children 0..3 in bytes 0..3), then qhi x,y,z
-    int32_t child[4];
-    uint32_t order;
-    int32_t pad;
-};
-// Reference-order wide node (closest-hit walks, host_scene.cpp build_ref_wide),
-// 128 B = one L2 line, up to kWideSlots children:
-//   dw 0-3    {origin.xyz, exps}  exps = ex | ey << 8 | ez << 16 | slot mask << 24
-//   dw 4-15   quantized child planes, axis-major: lo x (dw 4-5: bytes of slots 0..7), lo y, lo z,
-//             hi x, hi y, hi z (decoded as in Quad: origin + q * 2^(e - 127), containment verified)
-//   dw 16-23  child codes (>= 0 wide-node index, < 0 kLeafBit | leaf-record offset)
-//   dw 24-31  per octant of the ray direction (bit a set iff d[a] > 0): the rank of slot j in the
-//             reference's visiting order at bits 3j..3j+2
-#ifndef RT_WIDE_SLOTS
-#define RT_WIDE_SLOTS 6
-#endif
-constexpr int kWideSlots = RT_WIDE_SLOTS;     // 2..8, even
+// Wide node, 128 B = one L2 line, up to kWideSlots = 6 children.  Two trees
+// use it: the reference BVH collapsed in reference order (closest-hit walks,
+// host_scene.cpp build_ref_wide) and the SAH occlusion tree collapsed
+// (any-hit walks, build_shadow_tree).
+//   dw 0-3    {origin.xyz, exps}  exps = ex | ey << 8 | ez << 16 | slot mask << 24, scale_a = 2^(e_a - 127)
+//   dw 4-21   child planes as fp16 offsets, dword (side * 9 + axis * 3 + pair) holds slots 2*pair (low
+//             half) and 2*pair+1 (high half) of side 0 = lo, 1 = hi; decoded plane = fma(h, scale_a,
+//             origin_a) in f32 (h * scale exact, one rounding; the host verifies with the same fma that
+//             every decoded box CONTAINS the child's exact box); a ray picks its near/far side per axis
+//             by swapping whole dwords
+//   dw 22-27  child codes (>= 0 wide-node index, < 0 kLeafBit | leaf-record offset; INT32_MAX empty)
+//   dw 28-31  reference-order tree: for the octants o = 0..3 of the ray direction (bit a set iff
+//             d[a] > 0; bit 2 clear), the rank of slot j in the reference's visiting order at bits
+//             3j..3j+2; an octant o >= 4 visits in exactly the reverse order of o ^ 7 (every split
+//             flips), rank n-1-r (empty slots hold n-1).  Zero in the occlusion tree.
+constexpr int kWideSlots = 6;
 struct alignas(128) Wide {
     float ox, oy, oz; uint32_t exps;
-    uint32_t q[12];
-    int32_t child[8];
-    uint32_t rank[8];
+    uint32_t h[18];
+    int32_t child[6];
+    uint32_t rank[4];
 };
 static_assert(sizeof(Wide) == 128, "wide node size");
-static_assert(kWideSlots >= 2 && kWideSlots <= 8 && kWideSlots % 2 == 0, "wide node slots");
 
 struct alignas(16) LeafHead {
     float minx, miny, minz; int32_t count;
@@ -122,7 +109,6 @@ constexpr int32_t kLeafStartMask = (1 << kLeafCountShift) - 1;
 constexpr int kLeafMaxCount = 63;
 
 static_assert(sizeof(Pair) == 64, "pair size");
-static_assert(sizeof(Quad) == 64, "quad size");
 static_assert(sizeof(LeafHead) == 32, "leaf head size");
 static_assert(sizeof(Node) == 32, "node size");
 static_assert(sizeof(Prim) == 48, "prim size");

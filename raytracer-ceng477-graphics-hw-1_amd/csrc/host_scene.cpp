@@ -550,69 +550,89 @@ class Builder {
     }
 };
 
+constexpr int kMaxWideSlotsHost = dl::kWideSlots;
 inline int32_t fbits(float f) { int32_t i; std::memcpy(&i, &f, 4); return i; }
 inline float ibits(int32_t i) { float f; std::memcpy(&f, &i, 4); return f; }
 
-// One 4-wide node (dl::Quad): the child boxes of the slots in `mask`,
-// quantized to 8 bits per plane on a power-of-two grid anchored at the union
-// box's low corner.  Every decoded box is checked, with the device's own
-// float arithmetic (one fma, quad_hits), to CONTAIN the child's exact box;
-// false if one does not.  Slots outside `mask` get code INT32_MAX.
-// Quantize the boxes of the slots in `mask` (n slots): origin = union low
-// corner, power-of-two scale per axis, 8-bit plane offsets (ql/qh[slot][axis]);
-// false if a decoded box does not contain its exact box.
-bool quantize_boxes(const float (*lo)[3], const float (*hi)[3], int n, unsigned mask, float* o, int* e,
-                    uint8_t (*ql)[3], uint8_t (*qh)[3]) {
+// fp16 plane offsets of the wide nodes (dl::Wide): a plane decodes as
+// fma(h, 2^e, origin) in f32.  h16_down / h16_up: the largest / smallest
+// fp16 value <= / >= x (x >= 0, finite, < 65504 for up), normal or zero
+// (offsets below the smallest normal go to 0 / 2^-14, so no decode depends on
+// the device's fp16 denormal mode).  Values are returned as floats (exact).
+float h16_value(uint16_t b) {
+    const int ex = (b >> 10) & 31, man = b & 1023;
+    return ex == 0 ? std::ldexp((float)man, -24) : std::ldexp((float)(1024 + man), ex - 25);
+}
+uint16_t h16_down(double x) {
+    if (!(x >= 0x1p-14)) return 0;
+    if (x >= 65504.0) return 0x7bff;
+    int e;
+    std::frexp(x, &e);                                   // x in [2^(e-1), 2^e)
+    const double step = std::ldexp(1.0, e - 11);
+    const int m = (int)std::floor(x / step);             // [1024, 2047]
+    return (uint16_t)(((e - 1 + 15) << 10) | (m - 1024));
+}
+uint16_t h16_up(double x) {
+    if (!(x > 0.0)) return 0;
+    if (x <= 0x1p-14) return (uint16_t)(1 << 10);       // smallest normal
+    int e;
+    std::frexp(x, &e);
+    const double step = std::ldexp(1.0, e - 11);
+    int m = (int)std::ceil(x / step);                    // [1024, 2048]
+    int ex = e - 1 + 15;
+    if (m == 2048) { m = 1024; ++ex; }
+    if (ex >= 31) return 0x7bff;                         // caller keeps offsets far below 65504
+    return (uint16_t)((ex << 10) | (m - 1024));
+}
+
+// One wide node's boxes: the slots in `mask` (n slots) quantized as fp16
+// offsets from the union box's low corner on a power-of-two scale per axis
+// (offsets up to ~2^15, i.e. 11 significant bits of the node's extent).
+// Every decoded box is checked, with the device's arithmetic (the fp16 value
+// is exact in f32, then one fma), to CONTAIN the child's exact box; false if
+// one does not.  Fills origin, exps (with the slot mask) and the plane words.
+bool quantize_wide(const float (*lo)[3], const float (*hi)[3], int n, unsigned mask, dl::Wide& w) {
     auto pow2 = [](int x) { return ibits(x << 23); };                       // 2^(x-127), x in [1, 254]
-    auto dec = [](float org, int v, float sc) { return std::fma((float)v, sc, org); };
-    float top[3] = {-FLT_MAX, -FLT_MAX, -FLT_MAX};
+    auto dec = [](float org, uint16_t h, float sc) { return std::fma(h16_value(h), sc, org); };
+    float o[3], top[3] = {-FLT_MAX, -FLT_MAX, -FLT_MAX};
     for (int a = 0; a < 3; ++a) o[a] = FLT_MAX;
     for (int i = 0; i < n; ++i)
         if (mask >> i & 1u)
             for (int a = 0; a < 3; ++a) { o[a] = std::min(o[a], lo[i][a]); top[a] = std::max(top[a], hi[i][a]); }
+    if (mask == 0)
+        for (int a = 0; a < 3; ++a) o[a] = top[a] = 0.0f;
     bool ok = true;
+    int e[3];
     float sc[3];
     for (int a = 0; a < 3; ++a) {
-        e[a] = 1;
         const double ext = (double)top[a] - o[a];
-        if (ext > 0) e[a] = std::max(1, std::min(254, (int)std::ceil(std::log2(ext / 255.0)) + 127));
-        while (e[a] < 254 && dec(o[a], 255, pow2(e[a])) < top[a]) ++e[a];
+        e[a] = 127;
+        if (ext > 0) e[a] = std::max(1, std::min(254, (int)std::ceil(std::log2(ext)) - 15 + 127));
         sc[a] = pow2(e[a]);
     }
+    uint16_t hl[kMaxWideSlotsHost][3] = {}, hh[kMaxWideSlotsHost][3] = {};
     for (int i = 0; i < n; ++i) {
-        for (int a = 0; a < 3; ++a) { ql[i][a] = 0; qh[i][a] = 0; }
         if (!(mask >> i & 1u)) continue;
         for (int a = 0; a < 3; ++a) {
-            int qlo = (int)std::floor(((double)lo[i][a] - o[a]) / sc[a]);
-            qlo = std::max(0, std::min(255, qlo));
-            while (qlo > 0 && dec(o[a], qlo, sc[a]) > lo[i][a]) --qlo;
-            int qhi = (int)std::ceil(((double)hi[i][a] - o[a]) / sc[a]);
-            qhi = std::max(0, std::min(255, qhi));
-            while (qhi < 255 && dec(o[a], qhi, sc[a]) < hi[i][a]) ++qhi;
-            if (dec(o[a], qlo, sc[a]) > lo[i][a] || dec(o[a], qhi, sc[a]) < hi[i][a]) ok = false;
-            ql[i][a] = (uint8_t)qlo;
-            qh[i][a] = (uint8_t)qhi;
+            uint16_t ql = h16_down(((double)lo[i][a] - o[a]) / sc[a]);
+            while (ql > 0 && dec(o[a], ql, sc[a]) > lo[i][a]) ql = ql == (1 << 10) ? 0 : ql - 1;   // monotone codes
+            uint16_t qh = h16_up(((double)hi[i][a] - o[a]) / sc[a]);
+            while (qh < 0x7bff && dec(o[a], qh, sc[a]) < hi[i][a]) qh = qh == 0 ? (1 << 10) : qh + 1;
+            if (dec(o[a], ql, sc[a]) > lo[i][a] || dec(o[a], qh, sc[a]) < hi[i][a]) ok = false;
+            if (ql != 0 && ql < (1 << 10)) ok = false;                          // never a denormal code
+            if (qh != 0 && qh < (1 << 10)) ok = false;
+            hl[i][a] = ql;
+            hh[i][a] = qh;
         }
     }
-    return ok;
-}
-
-bool make_quad(const float (*lo)[3], const float (*hi)[3], const int32_t* codes, unsigned mask, uint32_t order,
-               dl::Quad& q) {
-    float o[3];
-    int e[3];
-    uint8_t ql[4][3], qh[4][3];
-    const bool ok = quantize_boxes(lo, hi, 4, mask, o, e, ql, qh);
-    uint8_t bytes[24] = {};
-    for (int i = 0; i < 4; ++i)
-        for (int a = 0; a < 3; ++a) { bytes[a * 4 + i] = ql[i][a]; bytes[12 + a * 4 + i] = qh[i][a]; }
-    q = dl::Quad{};
-    q.ox = o[0]; q.oy = o[1]; q.oz = o[2];
-    q.exps = (uint32_t)e[0] | (uint32_t)e[1] << 8 | (uint32_t)e[2] << 16 | (mask & 15u) << 24;
-    std::memcpy(q.q, bytes, 24);
-    for (int i = 0; i < 4; ++i) q.child[i] = (mask >> i & 1u) ? codes[i] : INT32_MAX;
-    q.order = order;
-    q.pad = 0;
+    w.ox = o[0]; w.oy = o[1]; w.oz = o[2];
+    w.exps = (uint32_t)e[0] | (uint32_t)e[1] << 8 | (uint32_t)e[2] << 16 | (mask & 63u) << 24;
+    for (int side = 0; side < 2; ++side)
+        for (int a = 0; a < 3; ++a)
+            for (int pr = 0; pr < 3; ++pr) {
+                const uint16_t (*q)[3] = side ? hh : hl;
+                w.h[side * 9 + a * 3 + pr] = (uint32_t)q[2 * pr][a] | (uint32_t)q[2 * pr + 1][a] << 16;
+            }
     return ok;
 }
 
@@ -997,21 +1017,23 @@ void build_shadow_tree(FlatBVH& out, int threads) {
     for (int a = 0; a < 3; ++a) { out.sroot_lo[a] = tn[root].box.lo[a]; out.sroot_hi[a] = tn[root].box.hi[a]; }
     out.sroot_info = info(root);
 
-    // 4-wide collapse with quantized child boxes (dl::Quad, make_quad: every
-    // decoded box contains the child's box, all the any-hit argument needs).
-    // Leaves are the shared leaf records.
-    out.quads.clear();
-    out.qmax_depth = 0;
+    // Wide collapse (dl::Wide, quantize_wide: every decoded box contains the
+    // child's box, all the any-hit argument needs): a node's slots are a
+    // frontier below an SAH node, grown by replacing the interior slot of
+    // largest box area by its two children.  Leaves are the shared leaf records.
+    out.swnodes.clear();
+    out.swmax_stack = 0;
     bool contain_ok = !out.lrec.empty();
-    std::function<int32_t(int, int)> emit = [&](int n, int depth) -> int32_t {
-        out.qmax_depth = std::max(out.qmax_depth, depth);
+    // returns the node code; *stack = worst-case stack entries of a walk from here down
+    std::function<int32_t(int, int*)> emit = [&](int n, int* stack) -> int32_t {
         const TNode& t = tn[n];
+        *stack = 0;
         if (t.left < 0) {
             if (t.rec < 0) contain_ok = false;
             return dl::kLeafBit | t.rec;
         }
         std::vector<int> ch{t.left, t.right};
-        while (ch.size() < 4) {
+        while ((int)ch.size() < dl::kWideSlots) {
             int best = -1;
             double ba = -1.0;
             for (size_t i = 0; i < ch.size(); ++i)
@@ -1021,21 +1043,27 @@ void build_shadow_tree(FlatBVH& out, int threads) {
             ch[best] = tn[c].left;
             ch.insert(ch.begin() + best + 1, tn[c].right);
         }
-        const int me = (int)out.quads.size();
-        out.quads.emplace_back();
-        int32_t codes[4] = {INT32_MAX, INT32_MAX, INT32_MAX, INT32_MAX};
-        float lo[4][3] = {}, hi[4][3] = {};
+        const int me = (int)out.swnodes.size();
+        out.swnodes.emplace_back();
+        dl::Wide w{};
+        float lo[dl::kWideSlots][3] = {}, hi[dl::kWideSlots][3] = {};
+        int deepest = 0;
+        for (int i = 0; i < dl::kWideSlots; ++i) w.child[i] = INT32_MAX;
         for (size_t i = 0; i < ch.size(); ++i) {
-            codes[i] = emit(ch[i], depth + 1);
+            int st = 0;
+            w.child[i] = emit(ch[i], &st);
+            deepest = std::max(deepest, st);
             for (int a = 0; a < 3; ++a) { lo[i][a] = tn[ch[i]].box.lo[a]; hi[i][a] = tn[ch[i]].box.hi[a]; }
         }
-        dl::Quad q;
-        if (!make_quad(lo, hi, codes, (1u << ch.size()) - 1u, 0u, q)) contain_ok = false;
-        out.quads[me] = q;
+        *stack = (int)ch.size() - 1 + deepest;        // a step pushes at most n - 1, then goes below one
+        if (!quantize_wide(lo, hi, (int)ch.size(), (1u << ch.size()) - 1u, w)) contain_ok = false;
+        out.swnodes[me] = w;
         return me;
     };
-    out.qroot = emit(root, 0);
-    if (!contain_ok || 3 * out.qmax_depth + 4 > dl::kMaxStack) out.quads.clear();   // binary occlusion tree only
+    int stack = 0;
+    out.swroot = emit(root, &stack);
+    out.swmax_stack = stack + 1;
+    if (!contain_ok || out.swmax_stack > dl::kMaxStack) out.swnodes.clear();   // binary occlusion tree only
 }
 
 // Reference-order wide tree for closest-hit walks: the reference BVH collapsed
@@ -1097,10 +1125,11 @@ bool build_ref_wide(FlatBVH& out) {
         }
         const int n = (int)fr.size();
         dl::Wide w{};
+        // ranks for the octants o = 0..3 (d[2] <= 0); an octant o >= 4 visits in the reverse order of o ^ 7
         for (int oct = 0; oct < 8; ++oct) {
-            int order[8], no = 0;
+            int order[dl::kWideSlots], no = 0;
             std::function<void(int, int)> visit = [&](int lo, int hi) {
-                if (hi - lo == 1) { if (no < 8) order[no++] = lo; return; }
+                if (hi - lo == 1) { if (no < dl::kWideSlots) order[no++] = lo; return; }
                 for (const Split& e : sp)
                     if (e.lo == lo && e.hi == hi) {
                         const bool left_first = (oct >> e.axis) & 1;
@@ -1114,14 +1143,20 @@ bool build_ref_wide(FlatBVH& out) {
             if (no != n) ok = false;
             uint32_t rw = 0;
             for (int r = 0; r < no; ++r) rw |= (uint32_t)r << (3 * order[r]);
-            for (int j = n; j < 8; ++j) rw |= 7u << (3 * j);             // empty slots: never valid
-            w.rank[oct] = rw;
+            for (int j = n; j < dl::kWideSlots; ++j) rw |= (uint32_t)(n - 1) << (3 * j);   // empty: never valid
+            if (oct < 4) {
+                w.rank[oct] = rw;
+            } else {                        // check the reversal the device relies on (real slots)
+                const uint32_t all = 01111111u & ((1u << (3 * dl::kWideSlots)) - 1u);   // one per 3-bit field
+                const uint32_t real = (1u << (3 * n)) - 1u;
+                if ((rw & real) != (((uint32_t)(n - 1) * all - w.rank[oct ^ 7]) & real)) ok = false;
+            }
         }
         const int me = (int)out.wnodes.size();
         out.wnodes.emplace_back();
-        float lo[8][3] = {}, hi[8][3] = {};
+        float lo[dl::kWideSlots][3] = {}, hi[dl::kWideSlots][3] = {};
         int deepest = 0;
-        for (int i = 0; i < 8; ++i) w.child[i] = INT32_MAX;
+        for (int i = 0; i < dl::kWideSlots; ++i) w.child[i] = INT32_MAX;
         for (int i = 0; i < n; ++i) {
             std::memcpy(lo[i], fr[i].lo, sizeof(lo[i]));
             std::memcpy(hi[i], fr[i].hi, sizeof(hi[i]));
@@ -1136,17 +1171,7 @@ bool build_ref_wide(FlatBVH& out) {
         }
         // a step pushes at most n - 1 entries, then continues below one of them
         *stack = n - 1 + deepest;
-        float o[3];
-        int e[3];
-        uint8_t ql[8][3], qh[8][3];
-        const unsigned mask = (1u << n) - 1u;
-        if (!quantize_boxes(lo, hi, n, mask, o, e, ql, qh)) ok = false;
-        w.ox = o[0]; w.oy = o[1]; w.oz = o[2];
-        w.exps = (uint32_t)e[0] | (uint32_t)e[1] << 8 | (uint32_t)e[2] << 16 | mask << 24;
-        uint8_t bytes[48] = {};
-        for (int i = 0; i < n; ++i)
-            for (int a = 0; a < 3; ++a) { bytes[a * 8 + i] = ql[i][a]; bytes[24 + a * 8 + i] = qh[i][a]; }
-        std::memcpy(w.q, bytes, 48);
+        if (!quantize_wide(lo, hi, n, (1u << n) - 1u, w)) ok = false;
         out.wnodes[me] = w;
         return me;
     };

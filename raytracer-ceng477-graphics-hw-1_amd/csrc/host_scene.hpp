@@ -63,14 +63,14 @@ struct FlatBVH {
     int32_t sroot_info = 0;
     int smax_depth = 0;
     // leaf records (LeafHead + prims), 16-B units, one per reference leaf in
-    // pre-order, + 3 units of tail pad; shared by both 4-wide trees
+    // pre-order, + 3 units of tail pad; shared by both wide trees
     std::vector<dl::Vec4> lrec;
     std::vector<int32_t> pair_lrec;  // [2 * pair + side]: leaf record offset of a leaf child, else -1
     int32_t root_lrec = -1;          // the root's record when the root is a leaf
-    // the occlusion tree collapsed to 4-wide nodes with quantized child boxes (any-hit walks)
-    std::vector<dl::Quad> quads;
-    int32_t qroot = 0;               // >= 0 quad index, < 0 kLeafBit | leaf-record offset
-    int qmax_depth = 0;
+    // the occlusion tree collapsed to wide nodes (any-hit walks)
+    std::vector<dl::Wide> swnodes;
+    int32_t swroot = 0;              // >= 0 node index, < 0 kLeafBit | leaf-record offset
+    int swmax_stack = 0;             // worst-case stack entries of a walk over them
     // the reference tree collapsed to wide nodes (closest-hit walks, reference order)
     std::vector<dl::Wide> wnodes;
     int32_t wroot = 0;
@@ -78,7 +78,7 @@ struct FlatBVH {
     int leaves = 0, max_leaf = 0, max_depth = 0, max_stack = 0;
     double build_ms = 0;
     double ref_ms = 0, flat_ms = 0, stree_ms = 0;
-    int threads = 1;                 // host threads the build used   // phases of build_ms: reference tree, flatten, 4-wide tree
+    int threads = 1;                 // host threads the build used   // phases of build_ms: reference tree, flatten, wide trees
 };
 
 // parser.cpp:6-218 semantics.  Returns empty string on success, else message.
@@ -88,7 +88,7 @@ std::string load_xml(const char* path, HostScene& out, int threads = 0);
 // raytracer.cpp:342-348: per-triangle normal and centre.
 void prepare_triangles(HostScene& s);
 
-// bvh.h:48-163 + the GPU flatten + the 4-wide tree. Returns empty string or an
+// bvh.h:48-163 + the GPU flatten + the wide trees. Returns empty string or an
 // error message.  threads: host build threads (0: RT_BUILD_THREADS, else the
 // hardware concurrency capped at 16; 1: serial).  The output does not depend
 // on the thread count.

@@ -49,6 +49,38 @@ constexpr int kBlock = 256;
 
 enum LaneState : int { kIdle = 0, kTrav = 1, kDone = 2 };
 
+// Diagnostics build (RT_STEP_STATS=1): per-role wave-step statistics of the
+// walk loops, read by rt_debug_step_stats.  Slot r*8 + {0: wave iterations,
+// 1: walking lanes, 2: lanes at an interior node, 3: lanes stepping a leaf
+// record (not postponed), 4: iterations that step a leaf record, 5: refills,
+// 6: lanes refilled, 7: iterations that step an interior node}; role 0 =
+// phase-A chains, 1 = phase-B chains, 2 = shadow rays, 3 = phase-B queue.
+#ifndef RT_STEP_STATS
+#define RT_STEP_STATS 0
+#endif
+__device__ unsigned long long g_step_stat[32];
+struct StepStat {
+    unsigned long long v[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    __device__ __forceinline__ void step(bool walking, bool interior, bool postponed) {
+        if (!RT_STEP_STATS) return;
+        const unsigned long long wm = __ballot(walking), im = __ballot(walking && interior),
+                                 lm = __ballot(walking && !interior && !postponed);
+        const int nw = __popcll(wm), ni = __popcll(im), nl = __popcll(lm);
+        v[0] += 1; v[1] += nw; v[2] += ni; v[3] += nl; v[4] += nl > 0 ? 1 : 0; v[7] += ni > 0 ? 1 : 0;
+    }
+    __device__ __forceinline__ void refill(unsigned long long mask) {
+        if (!RT_STEP_STATS) return;
+        v[5] += 1; v[6] += __popcll(mask);
+    }
+    __device__ __forceinline__ void flush(int role) {
+        if (!RT_STEP_STATS) return;
+        if ((threadIdx.x & 63) == 0)
+            for (int i = 0; i < 8; ++i) atomicAdd(&g_step_stat[role * 8 + i], v[i]);
+    }
+};
+
+
+
 // LDS, named directly so every access is a ds_read/ds_write (a generic
 // pointer to them would compile to flat loads that wait on vmcnt + lgkmcnt).
 
@@ -412,6 +444,7 @@ __device__ uint32_t bq_consume(const rtk::DevScene& s, const PcParams& p, WalkSt
     unsigned owner = 0;
     Walk wk;
     uint32_t n = 0;
+    StepStat stat;
     while (true) {
         const unsigned long long want = __ballot(!active && !have && !out);
         if (want) {
@@ -450,6 +483,7 @@ __device__ uint32_t bq_consume(const rtk::DevScene& s, const PcParams& p, WalkSt
             if (__any(idle)) __builtin_amdgcn_s_sleep(2);
             continue;
         }
+        stat.step(active, wk.cur >= 0, RT_STEP_STATS && active && wk.tree == nullptr && leaf_postponed(s.leaf_wait_any, wk));
         if (active) {
             const int res = occl_step<COUNT, FetchTop>(s, r, tlim, stk, wk, w);
             if (res || walk_runaway(s, wk)) {
@@ -458,6 +492,7 @@ __device__ uint32_t bq_consume(const rtk::DevScene& s, const PcParams& p, WalkSt
             }
         }
     }
+    stat.flush(3);
     return n;
 }
 
@@ -482,6 +517,7 @@ __device__ void chain_body(const rtk::DevScene& s, const rtk::Eye& e, const PcPa
     Walk wk;
     unsigned t_grab = 0;
     bool fresh = false;      // lane just took an eye ray (packet walk pending)
+    StepStat stat;
     while (true) {
         // (1) epilogue of finished walks: record, queue shadow tasks, reflect or hand on
         if (st == kDone) {
@@ -561,6 +597,7 @@ __device__ void chain_body(const rtk::DevScene& s, const rtk::Eye& e, const PcPa
         if (!exhausted) {
             const unsigned long long idle = __ballot(st == kIdle);
             if (idle) {
+                stat.refill(idle);
                 const unsigned base = wave_grab_lds(&g_head, idle);
                 if (base + (unsigned)__popcll(idle) >= nb) exhausted = true;
                 if (st == kIdle) {
@@ -615,11 +652,13 @@ __device__ void chain_body(const rtk::DevScene& s, const rtk::Eye& e, const PcPa
             if (nt <= thresh ||
                 __popcll(__ballot(st == kDone)) >= (CONT ? (exhausted ? p.btail : p.bservice) : p.service))
                 break;
+            stat.step(st == kTrav, wk.cur >= 0, RT_STEP_STATS && st == kTrav && wk.tree == nullptr && leaf_postponed(s.leaf_wait, wk));
             if (st == kTrav) {
                 if (closest_step<COUNT, FetchTop, WalkStack, CONT>(s, r, stk, wk, w) || walk_runaway(s, wk)) st = kDone;
             }
         }
     }
+    stat.flush(CONT ? 1 : 0);
     uint32_t nshadow = 0;
     if (CONT && kBq > 0) {
         if (lane_id() == 0) atomicSub(&g_bq_prod, 1u);      // this wave produces no more shadow tasks
@@ -655,10 +694,12 @@ __device__ void occlude_body(const rtk::DevScene& s, const PcParams& p, unsigned
     float tlim = 0.0f;
     unsigned owner = 0;
     Walk wk;
+    StepStat stat;
     while (true) {
         if (!exhausted) {
             const unsigned long long idle = __ballot(!active);
             if (idle) {
+                stat.refill(idle);
                 const unsigned base = wave_grab_lds(&g_head, idle);
                 if (base + (unsigned)__popcll(idle) >= n) exhausted = true;
                 if (!active) {
@@ -680,6 +721,7 @@ __device__ void occlude_body(const rtk::DevScene& s, const PcParams& p, unsigned
         }
         const int thresh = exhausted ? 0 : p.orefill;
         while (__popcll(__ballot(active)) > thresh) {
+            stat.step(active, wk.cur >= 0, RT_STEP_STATS && active && wk.tree == nullptr && leaf_postponed(s.leaf_wait_any, wk));
             if (active) {
                 const int res = occl_step<COUNT, FetchTop>(s, r, tlim, stk, wk, w);
                 if (res || walk_runaway(s, wk)) {
@@ -689,6 +731,7 @@ __device__ void occlude_body(const rtk::DevScene& s, const PcParams& p, unsigned
             }
         }
     }
+    stat.flush(2);
     if (p.trace && threadIdx.x == 0 && blk < (unsigned)p.ogrid) {
         p.trace[2 * ((size_t)p.cap + blk)] = t_start;
         p.trace[2 * ((size_t)p.cap + blk) + 1] = (unsigned)wall_clock64();
@@ -1288,7 +1331,7 @@ __global__ __launch_bounds__(kBlock, RT_FINISH_WAVES) void k_finish_any(rtk::Dev
 // Diagnostics (rt_walk_timing): wave 0 of one workgroup walks ray i with
 // lanes [0, lanes) (the same ray in every lane), reps times; lane 0 records
 // the last rep's shader cycles (s_memtime), the steps and the winner.  mode 0:
-// the production closest-hit walk (the reference-order quads), 1: the binary
+// the production closest-hit walk (the reference-order wide tree), 1: the binary
 // reference tree.  Measures the dependent-step latency of one walk.
 template <int MODE>
 __global__ __launch_bounds__(kBlock) void k_walk_timing(rtk::DevScene s, const float* rays, int n, int lanes, int reps,
@@ -1308,29 +1351,33 @@ __global__ __launch_bounds__(kBlock) void k_walk_timing(rtk::DevScene s, const f
         for (int rep = 0; rep < reps; ++rep) {
             t0 = __builtin_amdgcn_s_memtime();
             steps = 0;
-            if (mode == 3) {                     // memory only: dependent quad fetches (first child) from the root
-                if (threadIdx.x == 0) {
-                    int cur = s.qroot;
+            if (mode == 3) {                     // memory only: dependent wide-node fetches (first child) from the root
+                if (threadIdx.x == 0 && s.swnodes) {
+                    int cur = s.swroot;
 #pragma unroll 1
                     for (int hop = 0; hop < 64; ++hop) {
-                        if (cur < 0) cur = s.qroot;
-                        const float4* Q = reinterpret_cast<const float4*>(&s.quads[cur]);
-                        const float4 q2 = Q[2];
-                        cur = __float_as_int(q2.z) ^ (int)(rays[0] * 0.0f);
+                        if (cur < 0) cur = s.swroot;
+                        if (cur < 0) break;
+                        const float4* Q = reinterpret_cast<const float4*>(&s.swnodes[cur]);
+                        const float4 q5 = Q[5];
+                        cur = __float_as_int(q5.z) ^ (int)(rays[0] * 0.0f);
                         ++steps;
                     }
                     h = HitRec{0.0f, cur};
                 }
-            } else if (mode == 4) {              // memory only: the same with all four loads of a quad
-                if (threadIdx.x == 0) {
-                    int cur = s.qroot;
+            } else if (mode == 4) {              // memory only: the same with all seven loads of a node
+                if (threadIdx.x == 0 && s.swnodes) {
+                    int cur = s.swroot;
 #pragma unroll 1
                     for (int hop = 0; hop < 64; ++hop) {
-                        if (cur < 0) cur = s.qroot;
-                        const float4* Q = reinterpret_cast<const float4*>(&s.quads[cur]);
-                        const float4 q0 = Q[0], q1 = Q[1], q2 = Q[2], q3 = Q[3];
-                        const int pick = (__float_as_int(q0.x) ^ __float_as_int(q1.y) ^ __float_as_int(q3.y)) & 0;
-                        cur = __float_as_int(q2.z) + pick;
+                        if (cur < 0) cur = s.swroot;
+                        if (cur < 0) break;
+                        WideNode nd;
+                        wide_load(s.swnodes, cur, nd);
+                        int pick = 0;
+#pragma unroll
+                        for (int j = 0; j < 7; ++j) pick ^= __float_as_int(nd.q[j].x);
+                        cur = wide_code(nd, 0) + (pick & 0);
                         ++steps;
                     }
                     h = HitRec{0.0f, cur};
@@ -1424,6 +1471,16 @@ __global__ __launch_bounds__(kBlock) void k_phong_pow(const float* base, const f
 hipError_t launch_phong_pow(const float* base, const float* expo, float* out, int n, hipStream_t st) {
     hipLaunchKernelGGL(k_phong_pow, dim3((n + kBlock - 1) / kBlock), dim3(kBlock), 0, st, base, expo, out, n);
     return hipGetLastError();
+}
+
+// Diagnostics (RT_STEP_STATS builds): read (and optionally clear) g_step_stat.
+extern "C" int rt_debug_step_stats(unsigned long long* out, int reset) {
+    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_step_stat), sizeof(g_step_stat)) != hipSuccess) return -1;
+    if (reset) {
+        unsigned long long z[32] = {};
+        if (hipMemcpyToSymbol(HIP_SYMBOL(g_step_stat), z, sizeof(z)) != hipSuccess) return -1;
+    }
+    return RT_STEP_STATS;
 }
 
 unsigned chain_block_scap(int n0, int grid, int levels, int nlights) {

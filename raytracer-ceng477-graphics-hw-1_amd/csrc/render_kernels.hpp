@@ -37,12 +37,12 @@ struct DevScene {
     const dl::Pair* spairs;
     float sroot_lo[3], sroot_hi[3];
     int sroot_info;
-    int use_stree;        // NaN-free shadow rays walk: 0 the BVH, 1 the binary occlusion tree, 2 its 4-wide form
+    int use_stree;        // NaN-free shadow rays walk: 0 the BVH, 1 the binary occlusion tree, 2 its wide form
     int count_prod;       // counting passes walk the production trees and count fetched BYTES in the node
                           // counter (bench.py roofline; RT_COUNT_PROD at scene creation)
-    const dl::Quad* quads;
+    const dl::Wide* swnodes;  // the occlusion tree in wide form (any hit)
     const float4* lrec;   // leaf records (dl::LeafHead + prims), indexed in 16-B units
-    int qroot;
+    int swroot;
     const dl::Wide* wnodes;  // the reference tree in wide form (closest hit, reference order)
     int wroot;
     int use_wide;         // NaN-free closest-hit rays walk wnodes (traverse2.hpp wide_closest_step)

@@ -104,7 +104,7 @@ struct rt_scene {
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
     dl::Pair* d_pairs = nullptr;
     dl::Pair* d_spairs = nullptr;
-    dl::Quad* d_quads = nullptr;
+    dl::Wide* d_swnodes = nullptr;
     dl::Wide* d_wnodes = nullptr;
     dl::Vec4* d_lrec = nullptr;
     dl::LeafBig* d_leafbig = nullptr;
@@ -193,7 +193,7 @@ struct rt_scene {
         }
         if (fork_ev) (void)hipEventDestroy(fork_ev);
         (void)hipFree(batch_out);
-        (void)hipFree(d_pairs); (void)hipFree(d_leafbig); (void)hipFree(d_spairs); (void)hipFree(d_quads); (void)hipFree(d_wnodes); (void)hipFree(d_lrec);
+        (void)hipFree(d_pairs); (void)hipFree(d_leafbig); (void)hipFree(d_spairs); (void)hipFree(d_swnodes); (void)hipFree(d_wnodes); (void)hipFree(d_lrec);
         (void)hipFree(d_nodes); (void)hipFree(d_prims); (void)hipFree(d_tri); (void)hipFree(d_mats); (void)hipFree(d_lights);
         (void)hipFree(d_counters); (void)hipFree(d_err); (void)hipFree(d_out); (void)hipFree(d_trace);
         if (ev0) (void)hipEventDestroy(ev0);
@@ -265,7 +265,7 @@ int upload_scene(rt_scene* s, const rt_options* opts) {
     if ((rc = upload(&s->d_pairs, s->bvh.pairs))) return rc;
     if ((rc = upload(&s->d_leafbig, s->bvh.leaf_big))) return rc;
     if ((rc = upload(&s->d_spairs, s->bvh.spairs))) return rc;
-    if ((rc = upload(&s->d_quads, s->bvh.quads))) return rc;
+    if ((rc = upload(&s->d_swnodes, s->bvh.swnodes))) return rc;
     if ((rc = upload(&s->d_wnodes, s->bvh.wnodes))) return rc;
     if ((rc = upload(&s->d_lrec, s->bvh.lrec))) return rc;
     HIP_TRY(hipMalloc(reinterpret_cast<void**>(&s->d_counters), 8 * sizeof(unsigned long long)));
@@ -345,14 +345,14 @@ int upload_scene(rt_scene* s, const rt_options* opts) {
         d.sroot_hi[i] = s->bvh.sroot_hi[i];
     }
     d.sroot_info = s->bvh.sroot_info;
-    d.quads = s->d_quads;
+    d.swnodes = s->d_swnodes;
     d.lrec = reinterpret_cast<const float4*>(s->d_lrec);
-    d.qroot = s->bvh.qroot;
+    d.swroot = s->bvh.swroot;
     // occlusion tree for NaN-free shadow rays: 2 = 4-wide quantized form, 1 = binary, 0 = off (RT_STREE)
-    d.use_stree = !s->bvh.quads.empty() ? 2 : (s->bvh.spairs.empty() ? 0 : 1);
+    d.use_stree = !s->bvh.swnodes.empty() ? 2 : (s->bvh.spairs.empty() ? 0 : 1);
     if (const char* e = std::getenv("RT_STREE")) {
         const int v = std::atoi(e);
-        d.use_stree = v <= 0 ? 0 : (v >= 2 && !s->bvh.quads.empty() ? 2 : (s->bvh.spairs.empty() ? 0 : 1));
+        d.use_stree = v <= 0 ? 0 : (v >= 2 && !s->bvh.swnodes.empty() ? 2 : (s->bvh.spairs.empty() ? 0 : 1));
     }
     // closest-hit walks of NaN-free rays: the reference tree's wide form, reference order (RT_WIDE_WALK=0: the
     // binary form)
@@ -773,15 +773,17 @@ int rt_scene_bvh_info(const rt_scene* s, rt_bvh_info* info) {
     info->ref_ms = s->bvh.ref_ms;
     info->wide_ms = s->bvh.stree_ms;
     info->build_threads = s->bvh.threads;
-    info->wide_nodes = (int)s->bvh.quads.size();
+    info->wide_nodes = (int)(s->bvh.swnodes.size() + s->bvh.wnodes.size());
     uint64_t h = 1469598103934665603ull;           // FNV-1a over the 4-wide tree's bytes
     auto mix = [&h](const void* p, size_t n) {
         const unsigned char* b = static_cast<const unsigned char*>(p);
         for (size_t i = 0; i < n; ++i) { h ^= b[i]; h *= 1099511628211ull; }
     };
-    mix(s->bvh.quads.data(), s->bvh.quads.size() * sizeof(dl::Quad));
+    mix(s->bvh.swnodes.data(), s->bvh.swnodes.size() * sizeof(dl::Wide));
+    mix(s->bvh.wnodes.data(), s->bvh.wnodes.size() * sizeof(dl::Wide));
     mix(s->bvh.lrec.data(), s->bvh.lrec.size() * sizeof(dl::Vec4));
-    mix(&s->bvh.qroot, sizeof(s->bvh.qroot));
+    mix(&s->bvh.swroot, sizeof(s->bvh.swroot));
+    mix(&s->bvh.wroot, sizeof(s->bvh.wroot));
     info->wide_hash = h;
     return RT_OK;
 }

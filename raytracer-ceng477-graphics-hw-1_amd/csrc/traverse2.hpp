@@ -317,8 +317,8 @@ __device__ __forceinline__ bool walk_begin(const rtk::DevScene& s, const Ray& r,
     if (COUNT && !s.count_prod) w.nodes++;    // the reference's root pop (the root box is a kernel argument)
     float bt;
     if ((!COUNT || s.count_prod) && any && k.fast && s.use_stree == 2) {
-        k.tree = nullptr;                    // 4-wide occlusion tree (quad_any_step)
-        k.cur = s.qroot;
+        k.tree = nullptr;                    // the occlusion tree's wide form (wide_any_step)
+        k.cur = s.swroot;
         return true;
     }
     if ((!COUNT || s.count_prod) && any && k.fast && s.use_stree) {
@@ -341,67 +341,66 @@ __device__ __forceinline__ bool walk_begin(const rtk::DevScene& s, const Ray& r,
     return box_hit(r, lo, hi, &bt) && (any || bt <= k.tmax);
 }
 
-// Child boxes of a 4-wide node (dl::Quad), decoded exactly as the host
-// verified them and slab-tested against a NaN-free ray, two children per
-// packed instruction (v_pk_fma_f32 / v_pk_add_f32 / v_pk_mul_f32: IEEE per
-// component, so every value equals the scalar form).  Decode:
-// origin + q * 2^e as one fma, exact because q * 2^e is exact (an 8-bit
-// integer times a power of two); the host checks containment with the same
-// fma.  Slab test: box_hit_fast's, plane by plane (p - o) * inv, except that
-// the near plane of each axis is chosen up front by the sign of inv (the
-// axis's lo and hi dwords swap) instead of by a min/max per child: with o,
-// inv and the planes finite, lo <= hi gives (lo - o) * inv <= (hi - o) * inv
-// for inv > 0 and >= for inv < 0 (rounding is monotone), so the near value is
-// exactly box_hit_fast's min and the far value its max (up to the sign of a
-// zero, which no comparison sees).
+// Child boxes of a wide node (dl::Wide), decoded exactly as the host verified
+// them and slab-tested against a NaN-free ray, two children per packed
+// instruction (v_pk_fma_f32 / v_pk_add_f32 / v_pk_mul_f32: IEEE per component,
+// so every value equals the scalar form).  Decode: the fp16 offset converted
+// to f32 (exact), then origin + h * 2^e as one fma (h * 2^e exact; the host
+// checks containment with the same fma).  Slab test: box_hit_fast's, plane by
+// plane (p - o) * inv, except that the near plane of each axis is chosen up
+// front by the sign of inv (the axis's lo and hi dwords swap) instead of by a
+// min/max per child: with o, inv and the planes finite, lo <= hi gives
+// (lo - o) * inv <= (hi - o) * inv for inv > 0 and >= for inv < 0 (rounding is
+// monotone), so the near value is exactly box_hit_fast's min and the far value
+// its max (up to the sign of a zero, which no comparison sees).
 typedef float f2v __attribute__((ext_vector_type(2)));
 
-struct QuadHits {
-    float t[4];      // entry t of each child box (valid where hit)
-    bool hit[4];     // child exists and its box is hit
-    int code[4];
+__device__ __forceinline__ f2v h2_to_f2(uint32_t w) {
+    return f2v{(float)__builtin_bit_cast(_Float16, (unsigned short)(w & 0xffffu)),
+               (float)__builtin_bit_cast(_Float16, (unsigned short)(w >> 16))};
+}
+
+struct WideNode {
+    float4 q[7];     // dw 0-27: header, planes, child codes
 };
-__device__ __forceinline__ void quad_hits(const dl::Quad* quads, int qi, const Ray& r, QuadHits& c) {
-    const float4* q = reinterpret_cast<const float4*>(&quads[qi]);
-    const float4 q0 = q[0], q1 = q[1], q2 = q[2], q3 = q[3];
-    const uint32_t ex = __float_as_uint(q0.w);
-    const uint32_t mask = ex >> 24;
+__device__ __forceinline__ void wide_load(const dl::Wide* nodes, int i, WideNode& n) {
+    const float4* N = reinterpret_cast<const float4*>(&nodes[i]);
+#pragma unroll
+    for (int j = 0; j < 7; ++j) n.q[j] = N[j];
+}
+__device__ __forceinline__ uint32_t wide_dw(const WideNode& n, int d) {
+    const float4 v = n.q[d >> 2];
+    const int c = d & 3;
+    return __float_as_uint(c == 0 ? v.x : (c == 1 ? v.y : (c == 2 ? v.z : v.w)));
+}
+// entry / exit t of every slot box (slots outside the mask: garbage)
+__device__ __forceinline__ void wide_slabs(const WideNode& n, const Ray& r, float* tmn, float* tmx) {
+    constexpr int W = dl::kWideSlots;
+    const uint32_t ex = wide_dw(n, 3);
     const float sc[3] = {__uint_as_float((ex & 255u) << 23), __uint_as_float(((ex >> 8) & 255u) << 23),
                          __uint_as_float(((ex >> 16) & 255u) << 23)};
-    const float org[3] = {q0.x, q0.y, q0.z};
+    const float org[3] = {n.q[0].x, n.q[0].y, n.q[0].z};
     const float ro[3] = {r.o.x, r.o.y, r.o.z}, ri[3] = {r.inv.x, r.inv.y, r.inv.z};
-    const uint32_t lo_w[3] = {__float_as_uint(q1.x), __float_as_uint(q1.y), __float_as_uint(q1.z)};
-    const uint32_t hi_w[3] = {__float_as_uint(q1.w), __float_as_uint(q2.x), __float_as_uint(q2.y)};
-    c.code[0] = __float_as_int(q2.z);
-    c.code[1] = __float_as_int(q2.w);
-    c.code[2] = __float_as_int(q3.x);
-    c.code[3] = __float_as_int(q3.y);
-    float tmn[4], tmx[4];
 #pragma unroll
     for (int a = 0; a < 3; ++a) {
-        const bool neg = __float_as_int(ri[a]) < 0;
-        const uint32_t nw = neg ? hi_w[a] : lo_w[a], fw = neg ? lo_w[a] : hi_w[a];
+        const bool neg = __float_as_int(ri[a]) < 0;   // near plane: lo for inv > 0, hi for inv < 0
         const f2v s2 = {sc[a], sc[a]}, o2 = {org[a], org[a]}, rr = {ro[a], ro[a]}, iv = {ri[a], ri[a]};
 #pragma unroll
-        for (int pr = 0; pr < 2; ++pr) {            // children 2pr, 2pr+1
-            const f2v qn = {(float)((nw >> (16 * pr)) & 255u), (float)((nw >> (16 * pr + 8)) & 255u)};
-            const f2v qf = {(float)((fw >> (16 * pr)) & 255u), (float)((fw >> (16 * pr + 8)) & 255u)};
-            const f2v tn = (__builtin_elementwise_fma(qn, s2, o2) - rr) * iv;
-            const f2v tf = (__builtin_elementwise_fma(qf, s2, o2) - rr) * iv;
+        for (int pr = 0; pr < W / 2; ++pr) {            // slots 2pr, 2pr+1
+            const uint32_t lw = wide_dw(n, 4 + a * 3 + pr), hw = wide_dw(n, 4 + 9 + a * 3 + pr);
+            const uint32_t nw = neg ? hw : lw, fw = neg ? lw : hw;
+            const f2v tn = (__builtin_elementwise_fma(h2_to_f2(nw), s2, o2) - rr) * iv;
+            const f2v tf = (__builtin_elementwise_fma(h2_to_f2(fw), s2, o2) - rr) * iv;
 #pragma unroll
-            for (int k = 0; k < 2; ++k) {
-                const int ch = 2 * pr + k;
-                tmn[ch] = a == 0 ? tn[k] : __builtin_fmaxf(tmn[ch], tn[k]);
-                tmx[ch] = a == 0 ? tf[k] : __builtin_fminf(tmx[ch], tf[k]);
+            for (int h = 0; h < 2; ++h) {
+                const int c = 2 * pr + h;
+                tmn[c] = a == 0 ? tn[h] : __builtin_fmaxf(tmn[c], tn[h]);
+                tmx[c] = a == 0 ? tf[h] : __builtin_fminf(tmx[c], tf[h]);
             }
         }
     }
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-        c.t[i] = tmn[i];
-        c.hit[i] = ((mask >> i) & 1u) && tmx[i] >= __builtin_fmaxf(0.0f, tmn[i]);
-    }
 }
+__device__ __forceinline__ int wide_code(const WideNode& n, int c) { return (int)wide_dw(n, 22 + c); }
 
 // Primitives of a leaf record (header at L[0..1], prims from L[2]); the first
 // one is passed in already loaded, the next one is in flight while the
@@ -464,46 +463,19 @@ __device__ __forceinline__ bool wide_closest_step(const rtk::DevScene& s, const 
     constexpr int W = dl::kWideSlots;
     if (!COUNT && leaf_postponed(s.leaf_wait, k)) return false;
     if (k.cur >= 0) {
-        if (COUNT) w.nodes += 16 * (W > 4 ? 6 : 5) + 4;   // the node's dwordx4 loads + the octant's rank word
-        const float4* N = reinterpret_cast<const float4*>(&s.wnodes[k.cur]);
-        const float4 q0 = N[0], q1 = N[1], q2 = N[2], q3 = N[3], q4 = N[4];
-        const float4 q5 = W > 4 ? N[5] : q4;
-        const uint32_t rw = reinterpret_cast<const uint32_t*>(&s.wnodes[k.cur])[24 + k.sgn];
-        const uint32_t ex = __float_as_uint(q0.w);
-        const uint32_t mask = ex >> 24;
-        const float sc[3] = {__uint_as_float((ex & 255u) << 23), __uint_as_float(((ex >> 8) & 255u) << 23),
-                             __uint_as_float(((ex >> 16) & 255u) << 23)};
-        const float org[3] = {q0.x, q0.y, q0.z};
-        const float ro[3] = {r.o.x, r.o.y, r.o.z}, ri[3] = {r.inv.x, r.inv.y, r.inv.z};
-        // plane dwords: lo x,y,z then hi x,y,z, two dwords (slots 0-3, 4-7) each
-        const uint32_t pl[12] = {__float_as_uint(q1.x), __float_as_uint(q1.y), __float_as_uint(q1.z),
-                                 __float_as_uint(q1.w), __float_as_uint(q2.x), __float_as_uint(q2.y),
-                                 __float_as_uint(q2.z), __float_as_uint(q2.w), __float_as_uint(q3.x),
-                                 __float_as_uint(q3.y), __float_as_uint(q3.z), __float_as_uint(q3.w)};
-        const int code[8] = {__float_as_int(q4.x), __float_as_int(q4.y), __float_as_int(q4.z), __float_as_int(q4.w),
-                             __float_as_int(q5.x), __float_as_int(q5.y), __float_as_int(q5.z), __float_as_int(q5.w)};
+        if (COUNT) w.nodes += 7 * 16 + 4;                  // the node's seven dwordx4 loads + the octant's rank word
+        WideNode n;
+        wide_load(s.wnodes, k.cur, n);
+        const int ridx = (k.sgn & 4) ? (k.sgn ^ 7) : k.sgn;
+        uint32_t rw = reinterpret_cast<const uint32_t*>(&s.wnodes[k.cur])[28 + ridx];
+        const uint32_t mask = wide_dw(n, 3) >> 24;
+        if (k.sgn & 4)    // the reverse of octant sgn ^ 7: rank n-1-r in every 3-bit field (no borrow: r <= n-1)
+            rw = (uint32_t)(__builtin_popcount(mask) - 1) * 0111111u - rw;
         float tmn[W], tmx[W];
+        wide_slabs(n, r, tmn, tmx);
+        int code[W];
 #pragma unroll
-        for (int a = 0; a < 3; ++a) {
-            const bool neg = __float_as_int(ri[a]) < 0;   // near plane: lo for inv > 0, hi for inv < 0
-            const f2v s2 = {sc[a], sc[a]}, o2 = {org[a], org[a]}, rr = {ro[a], ro[a]}, iv = {ri[a], ri[a]};
-#pragma unroll
-            for (int pr = 0; pr < W / 2; ++pr) {            // slots 2pr, 2pr+1
-                const int dw = pr >> 1, sh = 16 * (pr & 1);
-                const uint32_t lw = pl[2 * a + dw], hw = pl[6 + 2 * a + dw];
-                const uint32_t nw = neg ? hw : lw, fw = neg ? lw : hw;
-                const f2v qn = {(float)((nw >> sh) & 255u), (float)((nw >> (sh + 8)) & 255u)};
-                const f2v qf = {(float)((fw >> sh) & 255u), (float)((fw >> (sh + 8)) & 255u)};
-                const f2v tn = (__builtin_elementwise_fma(qn, s2, o2) - rr) * iv;
-                const f2v tf = (__builtin_elementwise_fma(qf, s2, o2) - rr) * iv;
-#pragma unroll
-                for (int h = 0; h < 2; ++h) {
-                    const int c = 2 * pr + h;
-                    tmn[c] = a == 0 ? tn[h] : __builtin_fmaxf(tmn[c], tn[h]);
-                    tmx[c] = a == 0 ? tf[h] : __builtin_fminf(tmx[c], tf[h]);
-                }
-            }
-        }
+        for (int c = 0; c < W; ++c) code[c] = wide_code(n, c);
         // valid slots as a mask in RANK order (the reference's visiting order for this octant)
         uint32_t vm = 0;
         bool valid[W];
@@ -687,30 +659,34 @@ __device__ __forceinline__ int any_step(const rtk::DevScene& s, const Ray& r, fl
     return 1;
 }
 
-// One any-hit step over the 4-wide occlusion tree (dl::Quad), NaN-free rays
-// only (walk_begin).  Interior: decode and test the (conservative) child
+// One any-hit step over the occlusion tree's wide form (dl::Wide), NaN-free
+// rays only (walk_begin).  Interior: decode and test the (conservative) child
 // boxes, continue with the first hit child, push the others.  Leaf item: test
 // the reference leaf's EXACT box, then its primitives (raytracer.cpp:264-277).
 // Order is free: the any-hit answer does not depend on it.
 // 0 = continue, 1 = finished unoccluded, 2 = finished occluded.
 template <bool COUNT, class STK>
-__device__ __forceinline__ int quad_any_step(const rtk::DevScene& s, const Ray& r, float tlim, STK& stk, Walk& k,
+__device__ __forceinline__ int wide_any_step(const rtk::DevScene& s, const Ray& r, float tlim, STK& stk, Walk& k,
                                              Work& w) {
+    constexpr int W = dl::kWideSlots;
     if (!COUNT && leaf_postponed(s.leaf_wait_any, k)) return 0;
     if (k.cur >= 0) {
-        QuadHits q;
-        quad_hits(s.quads, k.cur, r, q);
-        if (COUNT) w.nodes += 64;
+        if (COUNT) w.nodes += 7 * 16;
+        WideNode n;
+        wide_load(s.swnodes, k.cur, n);
+        float tmn[W], tmx[W];
+        wide_slabs(n, r, tmn, tmx);
+        const uint32_t mask = wide_dw(n, 3) >> 24;
         int next = 0;
         bool have = false;
 #pragma unroll
-        for (int c = 0; c < 4; ++c) {
-            if (q.hit[c]) {
+        for (int c = 0; c < W; ++c) {
+            if (((mask >> c) & 1u) && tmx[c] >= __builtin_fmaxf(0.0f, tmn[c])) {
                 if (!have) {
-                    next = q.code[c];
+                    next = wide_code(n, c);
                     have = true;
                 } else {
-                    stk.put(k.sp, make_int2(q.code[c], 0));
+                    stk.put(k.sp, make_int2(wide_code(n, c), 0));
                     ++k.sp;
                 }
             }
@@ -828,7 +804,7 @@ __device__ __forceinline__ int dual_step(const rtk::DevScene& s, const Ray& r, b
 template <bool COUNT, class FETCH, class STK>
 __device__ __forceinline__ int occl_step(const rtk::DevScene& s, const Ray& r, float tlim, STK& stk, Walk& k,
                                          Work& w) {
-    if (k.tree == nullptr) return quad_any_step<COUNT>(s, r, tlim, stk, k, w);
+    if (k.tree == nullptr) return wide_any_step<COUNT>(s, r, tlim, stk, k, w);
     return any_step<COUNT, FETCH>(s, r, tlim, stk, k, w);
 }
 

@@ -59,7 +59,7 @@ def test_bvh_identical_to_oracle(scene, pkg, oracle, scene_dir):
 @pytest.mark.parametrize("threads", [2, 3, 8, 16])
 def test_parallel_build_equals_serial(scene, threads, pkg, oracle, scene_dir):
     # (f2) the parallel build: the reference tree stays bit-identical to the oracle's (bvh.h:48-163)
-    # and the 4-wide tree is the same bytes whatever the thread count.
+    # and the wide trees are the same bytes whatever the thread count.
     path = config_path(scene_dir, scene)
     ser = pkg.Scene.from_xml(path, host_only=True, build_threads=1)
     par = pkg.Scene.from_xml(path, host_only=True, build_threads=threads)
@@ -69,6 +69,17 @@ def test_parallel_build_equals_serial(scene, threads, pkg, oracle, scene_dir):
     assert (a["build_threads"], b["build_threads"]) == (1, threads)
     assert a["wide_nodes"] == b["wide_nodes"] and a["wide_hash"] == b["wide_hash"]
     assert a["wide_nodes"] > 0
+
+
+@pytest.mark.parametrize("scene", ["cornellbox.xml", "bunny.xml", "car.xml", "dragon_lowres.xml",
+                                   "marbles.xml", "C3_hm_1080p_d6"])
+def test_both_wide_trees_built(scene, pkg, scene_dir):
+    """Both wide trees exist (the kernels otherwise fall back to the binary trees, slower but
+    equally exact, so the GPU parity tests alone would not notice): a 6-wide tree over L leaves
+    has at least (L - 1) / 5 nodes, so both together at least twice that."""
+    info = pkg.Scene.from_xml(config_path(scene_dir, scene), host_only=True).bvh_info()
+    if info["leaves"] >= 2:
+        assert info["wide_nodes"] >= 2 * ((info["leaves"] - 1 + 4) // 5), info
 
 
 def test_parallel_loader_stops_like_serial(pkg, tmp_path):

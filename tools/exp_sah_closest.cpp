@@ -215,75 +215,76 @@ int closest_sah(const Ray& r, Hit* out) {
 }
 
 
-// 4-wide quantized tree (bvh.quads / qleaves): certified closest hit, counting
-// dependent fetch rounds: quads, leaves (exact box + prims in one round).
+// The production trees (bvh.wnodes: reference-order closest hit; bvh.swnodes:
+// occlusion), walked exactly as traverse2.hpp's wide_closest_step /
+// wide_any_step decode and test them, counting dependent fetch rounds: wide
+// nodes and leaf records (exact box + prims in one round).
 long g_qfetch = 0, g_lfetch = 0;
 float pow2f(int e) { uint32_t b = (uint32_t)e << 23; float f; memcpy(&f, &b, 4); return f; }
-void decode_quad(const dl::Quad& q, int c, float* lo, float* hi) {
-    float sc[3] = {pow2f(q.exps & 255u), pow2f((q.exps >> 8) & 255u), pow2f((q.exps >> 16) & 255u)};
-    const uint8_t* b = reinterpret_cast<const uint8_t*>(q.q);
-    const float o[3] = {q.ox, q.oy, q.oz};
-    for (int a = 0; a < 3; ++a) { lo[a] = o[a] + (float)b[a * 4 + c] * sc[a]; hi[a] = o[a] + (float)b[12 + a * 4 + c] * sc[a]; }
+float h16f(uint16_t b) {
+    const int ex = (b >> 10) & 31, man = b & 1023;
+    return ex == 0 ? ldexpf((float)man, -24) : ldexpf((float)(1024 + man), ex - 25);
 }
-int closest_quad(const Ray& r, Hit* out) {
+// entry/exit t of slot c (device arithmetic: fma decode, near plane by the sign of inv)
+void wide_slab(const dl::Wide& w, int c, const Ray& r, float* tmn, float* tmx) {
+    const float sc[3] = {pow2f(w.exps & 255u), pow2f((w.exps >> 8) & 255u), pow2f((w.exps >> 16) & 255u)};
+    const float o[3] = {w.ox, w.oy, w.oz}, ro[3] = {r.o.x, r.o.y, r.o.z}, ri[3] = {r.inv.x, r.inv.y, r.inv.z};
+    for (int a = 0; a < 3; ++a) {
+        const uint32_t lw = w.h[a * 3 + c / 2], hw = w.h[9 + a * 3 + c / 2];
+        const uint16_t hl = (uint16_t)((c & 1) ? lw >> 16 : lw & 0xffff), hh = (uint16_t)((c & 1) ? hw >> 16 : hw & 0xffff);
+        const float pl = fmaf(h16f(hl), sc[a], o[a]), ph = fmaf(h16f(hh), sc[a], o[a]);
+        const bool neg = std::signbit(ri[a]);
+        const float tn = ((neg ? ph : pl) - ro[a]) * ri[a], tf = ((neg ? pl : ph) - ro[a]) * ri[a];
+        *tmn = a == 0 ? tn : fmaxf(*tmn, tn);
+        *tmx = a == 0 ? tf : fminf(*tmx, tf);
+    }
+}
+Hit closest_prod(const Ray& r) {
     Hit h{-1.0f, -1, 0};
-    auto lim = [&](float tb) { return tb < 0 ? FLT_MAX : (float)(tb * (1.0 + g_slack)); };
+    float tmax = FLT_MAX;
     struct E { int32_t code; float t; } st[128];
     int sp = 0;
-    float tb = FLT_MAX, t2 = INFINITY, blt = INFINITY;
-    bool bad = false;
-    int32_t cur = B->qroot;
-    float cur_t = 0;
+    int32_t cur = B->wroot;
+    const int sgn = (r.d.x > 0) | (r.d.y > 0) << 1 | (r.d.z > 0) << 2;
     while (true) {
         if (cur >= 0) {
             g_qfetch++;
-            const dl::Quad& q = B->quads[cur];
-            int n = __builtin_popcount(q.exps >> 24);   // slot mask (contiguous in the occlusion tree)
-            E hits[4]; int nh = 0;
-            for (int c = 0; c < n; ++c) {
-                float lo[3], hi[3], t;
-                decode_quad(q, c, lo, hi);
-                h.visits++;
-                if (box_hit(r, lo, hi, &t) && t <= lim(tb)) {
-                    int j = nh++;
-                    while (j > 0 && hits[j - 1].t > t) { hits[j] = hits[j - 1]; --j; }
-                    hits[j] = {q.child[c], t};
-                }
+            const dl::Wide& w = B->wnodes[cur];
+            const uint32_t mask = w.exps >> 24;
+            uint32_t rw = w.rank[(sgn & 4) ? (sgn ^ 7) : sgn];
+            if (sgn & 4) rw = (uint32_t)(__builtin_popcount(mask) - 1) * 0111111u - rw;
+            E v[8]; int rank_of[8]; uint32_t vm = 0;
+            for (int c = 0; c < dl::kWideSlots; ++c) {
+                float tn, tf;
+                wide_slab(w, c, r, &tn, &tf);
+                const bool ok = ((mask >> c) & 1u) && tf >= fmaxf(0.0f, tn) && tn <= tmax;
+                rank_of[c] = (rw >> (3 * c)) & 7;
+                if (ok) { v[rank_of[c]] = {w.child[c], tn}; vm |= 1u << rank_of[c]; }
             }
-            for (int j = nh - 1; j >= 1; --j) st[sp++] = hits[j];
-            if (nh) { cur = hits[0].code; cur_t = hits[0].t; continue; }
+            if (vm) {
+                int first = __builtin_ctz(vm);
+                for (int k = 7; k > first; --k) if ((vm >> k) & 1u) st[sp++] = v[k];
+                cur = v[first].code;
+                continue;
+            }
         } else {
             g_lfetch++;
             const dl::LeafHead& L = *reinterpret_cast<const dl::LeafHead*>(&B->lrec[cur & ~dl::kLeafBit]);
             float lo[3] = {L.minx, L.miny, L.minz}, hi[3] = {L.maxx, L.maxy, L.maxz}, lt;
-            h.visits++;
-            if (box_hit(r, lo, hi, &lt) && lt <= lim(tb)) {
-                int a = L.slot0, c = L.count;
-                for (int i = a; i < a + c; ++i) {
+            if (box_hit(r, lo, hi, &lt) && lt <= tmax)
+                for (int i = L.slot0; i < L.slot0 + L.count; ++i) {
                     float t;
-                    if (!prim_hit(r, B->prims[i], &t)) continue;
-                    if (!(t >= 0)) bad = true;
-                    if (h.prim < 0 || t < h.t) {
-                        if (h.prim >= 0) t2 = std::min(t2, h.t);
-                        h.t = t; h.prim = i; tb = t; blt = lt;
-                    } else t2 = std::min(t2, t);
+                    if (prim_hit(r, B->prims[i], &t) && (t < h.t || h.t == -1.0f)) { h.t = t; h.prim = i; tmax = t; }
                 }
-            }
-            (void)cur_t;
         }
         bool found = false;
-        while (sp > 0) { --sp; if (st[sp].t <= lim(tb)) { cur = st[sp].code; cur_t = st[sp].t; found = true; break; } }
+        while (sp > 0) { --sp; if (st[sp].t <= tmax) { cur = st[sp].code; found = true; break; } }
         if (!found) break;
     }
-    int status = 0;
-    if (h.prim >= 0) {
-        float tw = h.t;
-        bool ok = !bad && t2 > tw && (blt <= tw || (blt <= tw * (1 + g_slack / 2) && t2 >= blt));
-        status = ok ? 0 : 1;
-    }
-    *out = h;
-    return status;
+    return h;
 }
+int closest_quad(const Ray& r, Hit* out) { *out = closest_prod(r); return 0; }
+
 // Reference-order 4-wide walk (collapse of the reference tree: a quad = node N's
 // children, interior ones replaced by their own children), visiting children in
 // the reference's DFS order (near child first by the sign of d[axis] at N and
@@ -361,6 +362,57 @@ Hit closest_rquad(const Ray& r) {
 // largest box area; the slots keep pre-order and each octant of the ray
 // direction has its own slot permutation (the DFS order below every expanded
 // node depends only on the sign of d[axis]).
+// EXP_QUANT: slot boxes of the greedy wide nodes as the device would decode them
+// (outward-rounded, every decoded box contains the exact one): 0 exact floats,
+// 1 8-bit offsets on a power-of-two grid (the current dl::Quad / dl::Wide),
+// 2 8-bit offsets on a free float scale, 3 fp16 offsets (power-of-two scale,
+// 11 significant bits), 4 16-bit fixed offsets on a free float scale.
+int g_quant = 0;
+float round_down_bits(float x, int bits) {            // x >= 0, keep `bits` significant bits (toward 0)
+    if (!(x > 0)) return 0.0f;
+    int e; const double m = frexp((double)x, &e);
+    return (float)ldexp(floor(ldexp(m, bits)), e - bits);
+}
+float round_up_bits(float x, int bits) {
+    if (!(x > 0)) return 0.0f;
+    int e; const double m = frexp((double)x, &e);
+    return (float)ldexp(ceil(ldexp(m, bits)), e - bits);
+}
+void quantize_node(int n, float (*lo)[3], float (*hi)[3]) {
+    if (g_quant == 0 || n == 0) return;
+    for (int a = 0; a < 3; ++a) {
+        float o = FLT_MAX, top = -FLT_MAX;
+        for (int i = 0; i < n; ++i) { o = std::min(o, lo[i][a]); top = std::max(top, hi[i][a]); }
+        const double ext = (double)top - o;
+        for (int i = 0; i < n; ++i) {
+            float l = lo[i][a], h = hi[i][a];
+            if (!(ext > 0)) continue;
+            if (g_quant == 1 || g_quant == 2 || g_quant == 4) {
+                const int steps = g_quant == 4 ? 65535 : 255;
+                float sc;
+                if (g_quant == 1) sc = (float)ldexp(1.0, (int)ceil(log2(ext / steps)));
+                else sc = (float)(ext / steps) * (1.0f + 1e-6f);
+                while (fmaf((float)steps, sc, o) < top) sc = nextafterf(sc, FLT_MAX);
+                int ql = std::max(0, std::min(steps, (int)floor(((double)l - o) / sc)));
+                while (ql > 0 && fmaf((float)ql, sc, o) > l) --ql;
+                int qh = std::max(0, std::min(steps, (int)ceil(((double)h - o) / sc)));
+                while (qh < steps && fmaf((float)qh, sc, o) < h) ++qh;
+                l = fmaf((float)ql, sc, o);
+                h = fmaf((float)qh, sc, o);
+            } else {                                                   // fp16 offsets
+                const float sc = (float)ldexp(1.0, (int)ceil(log2(ext)) - 15);
+                float hl = round_down_bits((float)(((double)l - o) / sc), 11);
+                float hh = round_up_bits((float)(((double)h - o) / sc), 11);
+                while (fmaf(hl, sc, o) > l) hl = round_down_bits(nextafterf(hl, 0.0f), 11);
+                while (fmaf(hh, sc, o) < h) hh = round_up_bits(nextafterf(hh, FLT_MAX), 11);
+                l = fmaf(hl, sc, o);
+                h = fmaf(hh, sc, o);
+            }
+            lo[i][a] = l;
+            hi[i][a] = h;
+        }
+    }
+}
 int g_width = 4;    // EXP_WIDTH: slots per node
 struct GQuad { int32_t info[8]; float lo[8][3], hi[8][3]; int n; uint8_t perm[8][8]; };
 std::vector<GQuad> g_gq;
@@ -406,6 +458,7 @@ int32_t build_gq(int32_t pair) {
     GQuad q{};
     q.n = (int)fr.size();
     for (int i = 0; i < q.n; ++i) { q.info[i] = fr[i].info; memcpy(q.lo[i], fr[i].lo, 12); memcpy(q.hi[i], fr[i].hi, 12); }
+    quantize_node(q.n, q.lo, q.hi);
     for (int oct = 0; oct < 8; ++oct) {
         // visit order: recursive over the expansion tree (ex[0] is the root)
         std::vector<int> order;
@@ -498,6 +551,7 @@ int32_t build_sn(int32_t pair) {
     SNode q{};
     q.n = (int)fr.size();
     for (int i = 0; i < q.n; ++i) { q.info[i] = fr[i].info; memcpy(q.lo[i], fr[i].lo, 12); memcpy(q.hi[i], fr[i].hi, 12); }
+    quantize_node(q.n, q.lo, q.hi);
     const int me = (int)g_sn.size();
     g_sn.push_back(q);
     for (int i = 0; i < q.n; ++i)
@@ -535,20 +589,27 @@ bool any_wide(const Ray& r, float tlim) {
     }
 }
 
-bool any_quad(const Ray& r, float tlim, long* qf, long* lf) {
-    int32_t st[128]; int sp = 0; int32_t cur = B->qroot;
+bool any_quad(const Ray& r, float tlim, long* qf, long* lf) {     // the production occlusion walk
+    int32_t st[128]; int sp = 0; int32_t cur = B->swroot;
     while (true) {
         if (cur >= 0) {
             (*qf)++;
-            const dl::Quad& q = B->quads[cur];
-            int n = __builtin_popcount(q.exps >> 24);   // slot mask (contiguous in the occlusion tree)
-            bool have = false; int32_t next = 0;
-            for (int c = 0; c < n; ++c) {
-                float lo[3], hi[3], t;
-                decode_quad(q, c, lo, hi);
-                if (box_hit(r, lo, hi, &t)) { if (!have) { next = q.child[c]; have = true; } else st[sp++] = q.child[c]; }
+            const dl::Wide& w = B->swnodes[cur];
+            const uint32_t mask = w.exps >> 24;
+            static const int order_mode = getenv("EXP_ANY_ORDER") ? atoi(getenv("EXP_ANY_ORDER")) : 0;
+            struct V { int32_t code; float t; } v[8]; int nv = 0;
+            for (int c = 0; c < dl::kWideSlots; ++c) {
+                float tn, tf;
+                wide_slab(w, c, r, &tn, &tf);
+                if (((mask >> c) & 1u) && tf >= fmaxf(0.0f, tn)) v[nv++] = {w.child[c], order_mode == 2 ? -tn : tn};
             }
-            if (have) { cur = next; continue; }
+            if (order_mode)        // 1: nearest entry first, 2: farthest first
+                for (int i = 1; i < nv; ++i) for (int j = i; j > 0 && v[j].t < v[j - 1].t; --j) std::swap(v[j], v[j - 1]);
+            if (nv) {
+                for (int j = nv - 1; j >= 1; --j) st[sp++] = v[j].code;
+                cur = v[0].code;
+                continue;
+            }
         } else {
             (*lf)++;
             const dl::LeafHead& L = *reinterpret_cast<const dl::LeafHead*>(&B->lrec[cur & ~dl::kLeafBit]);
@@ -569,6 +630,7 @@ int main(int argc, char** argv) {
     if (argc < 2) { fprintf(stderr, "usage: %s scene.xml [slack]\n", argv[0]); return 2; }
     if (argc > 2) g_slack = atof(argv[2]);
     if (getenv("EXP_WIDTH")) g_width = atoi(getenv("EXP_WIDTH"));
+    if (getenv("EXP_QUANT")) g_quant = atoi(getenv("EXP_QUANT"));
     int dump_row = -1, dump_col = -1;          // --dump ROW COL: print the pixel's chain rays (o, d) as hex floats
     if (argc > 5 && !strcmp(argv[3], "--dump")) { dump_row = atoi(argv[4]); dump_col = atoi(argv[5]); }
     HostScene sc;
@@ -698,9 +760,9 @@ int main(int argc, char** argv) {
            (double)ref_total / walks, (double)sah_total / walks, (double)ref_total / sah_total);
     printf("fallback %ld (%.4f%%) mismatch %ld certified-mismatch %ld\n", fallback, 100.0 * fallback / walks, mismatch,
            cert_mismatch);
-    printf("quad closest: fallback %ld mismatch %ld; per walk: ref pair fetches %.2f leaves %.2f | quad fetches %.2f leaves %.2f\n",
+    printf("production closest: fallback %ld mismatch %ld; per walk: ref pair fetches %.2f leaves %.2f | wide fetches %.2f leaves %.2f\n",
            qfall, qmis, (double)g_rfetch / walks, (double)g_rleaf / walks, (double)g_qfetch / walks, (double)g_lfetch / walks);
-    printf("shadow rays %ld: quad fetches %.2f leaves %.2f per ray\n", nshadow, (double)sq_f / nshadow, (double)sl_f / nshadow);
+    printf("shadow rays %ld (production wide tree): node fetches %.2f leaves %.2f per ray\n", nshadow, (double)sq_f / nshadow, (double)sl_f / nshadow);
     printf("shadow rays, SAH collapsed to %d slots: node fetches %.2f leaves %.2f per ray, mismatch %ld\n", g_width,
            (double)g_snf / nshadow, (double)g_snl / nshadow, aw_mis);
     printf("ref-order quad: mismatch %ld; per walk quad fetches %.2f leaves %.2f; phase-B chain max rounds %ld\n",
