@@ -610,6 +610,10 @@ bool quantize_wide(const float (*lo)[3], const float (*hi)[3], int n, unsigned m
         if (ext > 0) e[a] = std::max(1, std::min(254, (int)std::ceil(std::log2(ext)) - 15 + 127));
         sc[a] = pow2(e[a]);
     }
+    // the device's fused slab arithmetic (traverse2.hpp wide_slabs) needs |origin| <= 2^60 and
+    // scale <= 2^40 to stay free of overflow; a scene beyond that keeps the binary trees
+    for (int a = 0; a < 3; ++a)
+        if (!(std::fabs(o[a]) <= 0x1p60f) || !(sc[a] <= 0x1p40f)) ok = false;
     uint16_t hl[kMaxWideSlotsHost][3] = {}, hh[kMaxWideSlotsHost][3] = {};
     for (int i = 0; i < n; ++i) {
         if (!(mask >> i & 1u)) continue;

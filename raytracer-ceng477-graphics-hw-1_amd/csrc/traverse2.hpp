@@ -296,6 +296,16 @@ struct StackPriv {
     }
 };
 
+// Rays the wide trees' fused slab arithmetic (wide_slabs, RT_SLAB_FMA) takes:
+// NaN-free and |o|, |1/d| <= 2^64 per axis, so with the host's bounds on the
+// nodes (|origin| <= 2^60, scale <= 2^40) no product or margin can overflow.
+// Others walk the binary trees (never seen in practice: |d| < 2^-64).
+__device__ __forceinline__ bool wide_ray_ok(const Ray& r) {
+    constexpr float B = 0x1p64f;
+    return __builtin_fabsf(r.o.x) <= B && __builtin_fabsf(r.o.y) <= B && __builtin_fabsf(r.o.z) <= B &&
+           __builtin_fabsf(r.inv.x) <= B && __builtin_fabsf(r.inv.y) <= B && __builtin_fabsf(r.inv.z) <= B;
+}
+
 // Root test (the reference's first pop).  false: nothing to traverse.
 // Any-hit pops test the box only (raytracer.cpp:268-271); closest-hit also
 // needs bt <= tMax (:184), which prunes a NaN bt.
@@ -313,10 +323,11 @@ __device__ __forceinline__ bool walk_begin(const rtk::DevScene& s, const Ray& r,
     k.sp = 0;
     k.steps = 0;
     k.fast = ray_nan_free(r);
+    const bool wide_ok = k.fast && wide_ray_ok(r);    // the wide trees' slab arithmetic (wide_slabs)
     if (s.nnodes <= 0) return false;
     if (COUNT && !s.count_prod) w.nodes++;    // the reference's root pop (the root box is a kernel argument)
     float bt;
-    if ((!COUNT || s.count_prod) && any && k.fast && s.use_stree == 2) {
+    if ((!COUNT || s.count_prod) && any && wide_ok && s.use_stree == 2) {
         k.tree = nullptr;                    // the occlusion tree's wide form (wide_any_step)
         k.cur = s.swroot;
         return true;
@@ -328,7 +339,7 @@ __device__ __forceinline__ bool walk_begin(const rtk::DevScene& s, const Ray& r,
         const float4 hi = make_float4(s.sroot_hi[0], s.sroot_hi[1], s.sroot_hi[2], 0.0f);
         return box_hit(r, lo, hi, &bt);
     }
-    if ((!COUNT || s.count_prod) && !any && k.fast && s.use_wide) {
+    if ((!COUNT || s.count_prod) && !any && wide_ok && s.use_wide) {
         k.tree = nullptr;                    // the reference tree's wide form, reference order
         k.cur = s.wroot;
         k.sgn = (r.d.x > 0.0f ? 1 : 0) | (r.d.y > 0.0f ? 2 : 0) | (r.d.z > 0.0f ? 4 : 0);
@@ -341,18 +352,7 @@ __device__ __forceinline__ bool walk_begin(const rtk::DevScene& s, const Ray& r,
     return box_hit(r, lo, hi, &bt) && (any || bt <= k.tmax);
 }
 
-// Child boxes of a wide node (dl::Wide), decoded exactly as the host verified
-// them and slab-tested against a NaN-free ray, two children per packed
-// instruction (v_pk_fma_f32 / v_pk_add_f32 / v_pk_mul_f32: IEEE per component,
-// so every value equals the scalar form).  Decode: the fp16 offset converted
-// to f32 (exact), then origin + h * 2^e as one fma (h * 2^e exact; the host
-// checks containment with the same fma).  Slab test: box_hit_fast's, plane by
-// plane (p - o) * inv, except that the near plane of each axis is chosen up
-// front by the sign of inv (the axis's lo and hi dwords swap) instead of by a
-// min/max per child: with o, inv and the planes finite, lo <= hi gives
-// (lo - o) * inv <= (hi - o) * inv for inv > 0 and >= for inv < 0 (rounding is
-// monotone), so the near value is exactly box_hit_fast's min and the far value
-// its max (up to the sign of a zero, which no comparison sees).
+// Child boxes of a wide node (dl::Wide), slab-tested against a NaN-free ray.
 typedef float f2v __attribute__((ext_vector_type(2)));
 
 __device__ __forceinline__ f2v h2_to_f2(uint32_t w) {
@@ -373,7 +373,49 @@ __device__ __forceinline__ uint32_t wide_dw(const WideNode& n, int d) {
     const int c = d & 3;
     return __float_as_uint(c == 0 ? v.x : (c == 1 ? v.y : (c == 2 ? v.z : v.w)));
 }
-// entry / exit t of every slot box (slots outside the mask: garbage)
+// v_fma_mix_f32: fma(f16 half of w (low or high), a, b) in f32, one rounding
+// (the f16 -> f32 conversion is exact).
+template <int HI>
+__device__ __forceinline__ float fma_mix_h(uint32_t w, float a, float b) {
+    float r;
+    if (HI)
+        asm("v_fma_mix_f32 %0, %1, %2, %3 op_sel:[1,0,0] op_sel_hi:[1,0,0]" : "=v"(r) : "v"(w), "v"(a), "v"(b));
+    else
+        asm("v_fma_mix_f32 %0, %1, %2, %3 op_sel_hi:[1,0,0]" : "=v"(r) : "v"(w), "v"(a), "v"(b));
+    return r;
+}
+
+// Entry / exit t of every slot box (slots outside the mask: garbage).
+//
+// RT_SLAB_FMA (default): t = fma(h, 2^e * inv, (origin - o) * inv -/+ M), one
+// v_fma_mix_f32 per plane, where M is a per-node, per-axis margin that makes
+// the result a bound on the exact form below: with u = 2^-24, X = origin + h*2^e
+// - o, the exact form's t_x = RN(RN(RN(origin + h*2^e) - o) * inv) is within
+// |inv| u (|origin| + |h 2^e| + 2.0001 |X|) of X * inv, and the fused form
+// within |inv| (2.0001 u |origin - o| + u |t|) of (X * inv -/+ M); with
+// h * 2^e <= 2^16 * 2^e (fp16 offsets < 2^16) both stay inside
+// M = |inv| 2^-23 (6 |origin - o| + |origin| + 2^18 2^e) + 2^-126
+// (twice the first-order sum, which also absorbs the roundings of M itself).
+// So the fused near value is <= the exact near value and the fused far value
+// >= the exact far value: the test is conservative wherever the exact form's
+// is (its argument is at the top of this block), the boxes only grow, and
+// every leaf is still tested exactly.  No overflow, no NaN: |o|, |inv| <= 2^64
+// (wide_ray_ok) and the host's node bounds (|origin| <= 2^60, 2^e <= 2^40).
+//
+// Otherwise the exact form: the fp16 offset converted to f32 (exact), then
+// origin + h * 2^e as one fma (h * 2^e exact; the host checks containment with
+// the same fma), then box_hit_fast's plane arithmetic (p - o) * inv, two
+// children per packed instruction.
+//
+// Both forms choose the near plane of each axis up front by the sign of inv
+// (the axis's lo and hi dwords swap) instead of by a min/max per child: with o,
+// inv and the planes finite, lo <= hi gives (lo - o) * inv <= (hi - o) * inv for
+// inv > 0 and >= for inv < 0 (rounding is monotone), so the near value is
+// exactly box_hit_fast's min and the far value its max (up to the sign of a
+// zero, which no comparison sees).
+#ifndef RT_SLAB_FMA
+#define RT_SLAB_FMA 1
+#endif
 __device__ __forceinline__ void wide_slabs(const WideNode& n, const Ray& r, float* tmn, float* tmx) {
     constexpr int W = dl::kWideSlots;
     const uint32_t ex = wide_dw(n, 3);
@@ -384,6 +426,28 @@ __device__ __forceinline__ void wide_slabs(const WideNode& n, const Ray& r, floa
 #pragma unroll
     for (int a = 0; a < 3; ++a) {
         const bool neg = __float_as_int(ri[a]) < 0;   // near plane: lo for inv > 0, hi for inv < 0
+#if RT_SLAB_FMA
+        const float si = sc[a] * ri[a];                                   // exact (power of two)
+        const float z = org[a] - ro[a];
+        const float oi = z * ri[a];
+        const float c = __builtin_fmaf(sc[a], 0x1p-5f, __builtin_fabsf(org[a]) * 0x1p-23f);
+        const float m = __builtin_fmaf(__builtin_fabsf(z), 6.0f * 0x1p-23f, c);
+        const float M = __builtin_fmaf(m, __builtin_fabsf(ri[a]), 0x1p-126f);
+        const float on = oi - M, of = oi + M;
+#pragma unroll
+        for (int pr = 0; pr < W / 2; ++pr) {            // slots 2pr, 2pr+1
+            const uint32_t lw = wide_dw(n, 4 + a * 3 + pr), hw = wide_dw(n, 4 + 9 + a * 3 + pr);
+            const uint32_t nw = neg ? hw : lw, fw = neg ? lw : hw;
+            const float tn[2] = {fma_mix_h<0>(nw, si, on), fma_mix_h<1>(nw, si, on)};
+            const float tf[2] = {fma_mix_h<0>(fw, si, of), fma_mix_h<1>(fw, si, of)};
+#pragma unroll
+            for (int h = 0; h < 2; ++h) {
+                const int c2 = 2 * pr + h;
+                tmn[c2] = a == 0 ? tn[h] : __builtin_fmaxf(tmn[c2], tn[h]);
+                tmx[c2] = a == 0 ? tf[h] : __builtin_fminf(tmx[c2], tf[h]);
+            }
+        }
+#else
         const f2v s2 = {sc[a], sc[a]}, o2 = {org[a], org[a]}, rr = {ro[a], ro[a]}, iv = {ri[a], ri[a]};
 #pragma unroll
         for (int pr = 0; pr < W / 2; ++pr) {            // slots 2pr, 2pr+1
@@ -398,6 +462,7 @@ __device__ __forceinline__ void wide_slabs(const WideNode& n, const Ray& r, floa
                 tmx[c] = a == 0 ? tf[h] : __builtin_fminf(tmx[c], tf[h]);
             }
         }
+#endif
     }
 }
 __device__ __forceinline__ int wide_code(const WideNode& n, int c) { return (int)wide_dw(n, 22 + c); }

@@ -221,6 +221,7 @@ int closest_sah(const Ray& r, Hit* out) {
 // nodes and leaf records (exact box + prims in one round).
 long g_qfetch = 0, g_lfetch = 0;
 float pow2f(int e) { uint32_t b = (uint32_t)e << 23; float f; memcpy(&f, &b, 4); return f; }
+int g_slab_fma = 1;   // EXP_SLAB_FMA=0: the exact decode
 float h16f(uint16_t b) {
     const int ex = (b >> 10) & 31, man = b & 1023;
     return ex == 0 ? ldexpf((float)man, -24) : ldexpf((float)(1024 + man), ex - 25);
@@ -232,9 +233,20 @@ void wide_slab(const dl::Wide& w, int c, const Ray& r, float* tmn, float* tmx) {
     for (int a = 0; a < 3; ++a) {
         const uint32_t lw = w.h[a * 3 + c / 2], hw = w.h[9 + a * 3 + c / 2];
         const uint16_t hl = (uint16_t)((c & 1) ? lw >> 16 : lw & 0xffff), hh = (uint16_t)((c & 1) ? hw >> 16 : hw & 0xffff);
-        const float pl = fmaf(h16f(hl), sc[a], o[a]), ph = fmaf(h16f(hh), sc[a], o[a]);
         const bool neg = std::signbit(ri[a]);
-        const float tn = ((neg ? ph : pl) - ro[a]) * ri[a], tf = ((neg ? pl : ph) - ro[a]) * ri[a];
+        float tn, tf;
+        if (g_slab_fma) {                     // traverse2.hpp wide_slabs, RT_SLAB_FMA
+            const float si = sc[a] * ri[a], z = o[a] - ro[a], oi = z * ri[a];
+            const float c = fmaf(sc[a], 0x1p-5f, fabsf(o[a]) * 0x1p-23f);
+            const float m = fmaf(fabsf(z), 6.0f * 0x1p-23f, c);
+            const float M = fmaf(m, fabsf(ri[a]), 0x1p-126f);
+            tn = fmaf(h16f(neg ? hh : hl), si, oi - M);
+            tf = fmaf(h16f(neg ? hl : hh), si, oi + M);
+        } else {
+            const float pl = fmaf(h16f(hl), sc[a], o[a]), ph = fmaf(h16f(hh), sc[a], o[a]);
+            tn = ((neg ? ph : pl) - ro[a]) * ri[a];
+            tf = ((neg ? pl : ph) - ro[a]) * ri[a];
+        }
         *tmn = a == 0 ? tn : fmaxf(*tmn, tn);
         *tmx = a == 0 ? tf : fminf(*tmx, tf);
     }
@@ -631,6 +643,7 @@ int main(int argc, char** argv) {
     if (argc > 2) g_slack = atof(argv[2]);
     if (getenv("EXP_WIDTH")) g_width = atoi(getenv("EXP_WIDTH"));
     if (getenv("EXP_QUANT")) g_quant = atoi(getenv("EXP_QUANT"));
+    if (getenv("EXP_SLAB_FMA")) g_slab_fma = atoi(getenv("EXP_SLAB_FMA"));
     int dump_row = -1, dump_col = -1;          // --dump ROW COL: print the pixel's chain rays (o, d) as hex floats
     if (argc > 5 && !strcmp(argv[3], "--dump")) { dump_row = atoi(argv[4]); dump_col = atoi(argv[5]); }
     HostScene sc;
