@@ -91,7 +91,14 @@ struct StepStat {
 // a wave's lanes hit distinct banks), deeper ones in scratch.  LDS keeps the
 // pushes and pops off the vector-memory (TA) path that the node fetches use.
 constexpr int kLdsStackEntries = RT_LDS_STACK;
+#if RT_LDS_STACK <= 0
+#error "the wide walks push out of order: they need the random-access StackLds (RT_LDS_STACK > 0)"
+#endif
 struct StackLds {
+    // put_lds(i, v): i < kLds (the caller has checked the whole wave has room), or kLds itself, a
+    // per-lane scratch entry that absorbs the writes of slots that push nothing (branch-free pushes)
+    static constexpr int kLds = kLdsStackEntries;
+    __device__ __forceinline__ void put_lds(int i, int2 v);
     // Deep tier as two int arrays: loads shaped unlike the LDS int2 read, so
     // the compiler cannot sink both tiers into one flat load through a
     // selected pointer (which waits on vmcnt and lgkmcnt at every pop).
@@ -101,7 +108,8 @@ struct StackLds {
     __device__ __forceinline__ int2 at(int i);
 };
 #if RT_LDS_STACK > 0
-__shared__ int2 g_lstk[kLdsStackEntries * kBlock];
+__shared__ int2 g_lstk[(kLdsStackEntries + 1) * kBlock];
+__device__ __forceinline__ void StackLds::put_lds(int i, int2 v) { g_lstk[i * kBlock + threadIdx.x] = v; }
 __device__ __forceinline__ void StackLds::put(int i, int2 v) {
     if (i < kLdsStackEntries) {
         g_lstk[i * kBlock + threadIdx.x] = v;

@@ -541,29 +541,39 @@ __device__ __forceinline__ bool wide_closest_step(const rtk::DevScene& s, const 
         int code[W];
 #pragma unroll
         for (int c = 0; c < W; ++c) code[c] = wide_code(n, c);
-        // valid slots as a mask in RANK order (the reference's visiting order for this octant)
-        uint32_t vm = 0;
-        bool valid[W];
+        // valid slots as a mask in RANK order (the reference's visiting order for this octant);
+        // bitwise, not short-circuit, so no slot test becomes a branch
+        uint32_t vm = 0, vs = 0;
         uint32_t rank[W];
 #pragma unroll
         for (int c = 0; c < W; ++c) {
             rank[c] = (rw >> (3 * c)) & 7u;
-            valid[c] = ((mask >> c) & 1u) && tmx[c] >= __builtin_fmaxf(0.0f, tmn[c]) && tmn[c] <= k.tmax;
-            vm |= valid[c] ? 1u << rank[c] : 0u;
+            const uint32_t v = ((mask >> c) & 1u) & (uint32_t)(tmx[c] >= __builtin_fmaxf(0.0f, tmn[c])) &
+                               (uint32_t)(tmn[c] <= k.tmax);
+            vm |= v << rank[c];
+            vs |= v << c;
         }
         if (vm) {
             const uint32_t first = (uint32_t)__builtin_ctz(vm);
             int next = 0;
+            bool push[W];
+            int pos[W];
 #pragma unroll
             for (int c = 0; c < W; ++c) {
-                if (valid[c]) {
-                    if (rank[c] == first) {
-                        next = code[c];
-                    } else {   // deeper on the stack the later it is visited
-                        const int pos = __builtin_popcount(vm >> (rank[c] + 1u));
-                        stk.put(k.sp + pos, make_int2(code[c], __float_as_int(tmn[c])));
-                    }
-                }
+                const bool v = (vs >> c) & 1u;
+                next = (v && rank[c] == first) ? code[c] : next;
+                push[c] = v && rank[c] != first;
+                pos[c] = k.sp + __builtin_popcount(vm >> (rank[c] + 1u));   // deeper the later it is visited
+            }
+            if (__all(k.sp + W - 1 <= STK::kLds)) {
+                // every push of the wave lands in LDS: one unconditional write per slot
+#pragma unroll
+                for (int c = 0; c < W; ++c)
+                    stk.put_lds(push[c] ? pos[c] : STK::kLds, make_int2(code[c], __float_as_int(tmn[c])));
+            } else {
+#pragma unroll
+                for (int c = 0; c < W; ++c)
+                    if (push[c]) stk.put(pos[c], make_int2(code[c], __float_as_int(tmn[c])));
             }
             k.sp += __builtin_popcount(vm) - 1;
             k.cur = next;
@@ -742,21 +752,28 @@ __device__ __forceinline__ int wide_any_step(const rtk::DevScene& s, const Ray& 
         float tmn[W], tmx[W];
         wide_slabs(n, r, tmn, tmx);
         const uint32_t mask = wide_dw(n, 3) >> 24;
-        int next = 0;
-        bool have = false;
+        uint32_t vs = 0;
 #pragma unroll
-        for (int c = 0; c < W; ++c) {
-            if (((mask >> c) & 1u) && tmx[c] >= __builtin_fmaxf(0.0f, tmn[c])) {
-                if (!have) {
-                    next = wide_code(n, c);
-                    have = true;
-                } else {
-                    stk.put(k.sp, make_int2(wide_code(n, c), 0));
-                    ++k.sp;
-                }
+        for (int c = 0; c < W; ++c)
+            vs |= (((mask >> c) & 1u) & (uint32_t)(tmx[c] >= __builtin_fmaxf(0.0f, tmn[c]))) << c;
+        if (vs) {
+            // continue with the first hit slot, push the others in slot order (branch-free when the
+            // whole wave has LDS room for them)
+            const uint32_t first = (uint32_t)__builtin_ctz(vs), pm = vs & (vs - 1u);
+            int next = 0;
+#pragma unroll
+            for (int c = 0; c < W; ++c) next = (uint32_t)c == first ? wide_code(n, c) : next;
+            if (__all(k.sp + W - 1 <= STK::kLds)) {
+#pragma unroll
+                for (int c = 0; c < W; ++c)
+                    stk.put_lds(((pm >> c) & 1u) ? k.sp + __builtin_popcount(pm & ((1u << c) - 1u)) : STK::kLds,
+                                make_int2(wide_code(n, c), 0));
+            } else {
+#pragma unroll
+                for (int c = 0; c < W; ++c)
+                    if ((pm >> c) & 1u) stk.put(k.sp + __builtin_popcount(pm & ((1u << c) - 1u)), make_int2(wide_code(n, c), 0));
             }
-        }
-        if (have) {
+            k.sp += __builtin_popcount(pm);
             k.cur = next;
             return 0;
         }
