@@ -136,7 +136,7 @@ struct rt_scene {
     size_t chunk_samples = size_t(32) << 20;
     int tune_batch = 32;        // RT_BATCH: frames per batched launch (rt_render_frames/cameras; 1 = off)
     int tune_slots = 3;         // RT_SLOTS: frame batches in flight together (workspace slots, <= kSlots)
-    int tune_gb = 0;            // RT_GB: phase-B chain workgroups in k_mix (0 = 1.5625 per CU: 384-416 best of 256-1024 on C3)
+    int tune_gb = 0;            // RT_GB: phase-B chain workgroups in k_mix (0: 1.5625 per CU for a lone frame, 0.5 for batches)
     int tune_bq_cap = 1 << 30;  // RT_BQ_CAP: phase-B shadow queue slots (tests force the k_occlude spill path)
     int tune_bservice = 64;     // RT_BSERVICE: phase-B waves service finished walks once this many lanes are done
     int tune_btail = 64;        // RT_BTAIL: the same once the continuations are exhausted (1: 1.24, 4: 1.18, 16: 1.15, 64: 1.14 ms)
@@ -557,7 +557,11 @@ int render_chain(rt_scene* s, const rtk::Eye& eye, const rtk::FrameParams& f, bo
     // phase split: A walks levels [0, kinline], B the rest (k_mix chain role, gb workgroups)
     const int kinline = std::max(0, s->tune_kinline);
     const bool phase_b = kinline < s->dev.max_depth;
-    const int gb = phase_b ? std::max(1, std::min(s->mix_grid - 1, s->tune_gb > 0 ? s->tune_gb : 25 * s->num_cus / 16)) : 0;
+    // phase-B workgroups: a lone frame's deep chains are its critical path (1.5625 per CU best);
+    // in frame batches other frames hide them and the shadow role wants the CUs (C3: 0.5 per CU
+    // 0.550 ms/frame, 0.75 0.552, 1 0.554, 1.25 0.557, 1.5625 0.568)
+    const int gb_default = f.nframes > 1 ? s->num_cus / 2 : 25 * s->num_cus / 16;
+    const int gb = phase_b ? std::max(1, std::min(s->mix_grid - 1, s->tune_gb > 0 ? s->tune_gb : gb_default)) : 0;
     const int levels_a = std::min(kinline, std::max(s->dev.max_depth, 0)) + 1;
     const unsigned scapA = rtc::chain_block_scap((int)cap, G, levels_a, nl);
     const unsigned ccapA = rtc::chain_block_scap((int)cap, G, 1, 1);
