@@ -287,3 +287,25 @@ def test_phong_pow_matches_glibc_pow(tmp_path):
     assert bad == 0, out.stdout
     assert checked == 2_100_000 and fast > checked // 2
     assert full > 500_000 and exact_mid > 20_000
+
+
+def test_fused_slab_margin_is_conservative(tmp_path):
+    """The wide trees' fused slab test (traverse2.hpp wide_slabs: one fma per fp16 plane with a
+    per-node margin) never puts a near plane after, or a far plane before, the exact
+    decode-then-slab value the containment argument is stated for: 16 M random plane/ray pairs
+    (origins up to 2^40, |1/d| up to 2^64, rays far from and inside the node), and at least half
+    of the margin is left over in every case (it is twice the first-order error bound)."""
+    import shutil
+    import subprocess
+    from pathlib import Path
+    cxx = shutil.which("g++")
+    if cxx is None:
+        pytest.skip("g++ not available")
+    root = Path(__file__).resolve().parent.parent
+    exe = tmp_path / "slab_margin_check"
+    subprocess.run([cxx, "-O2", "-std=c++17", "-ffp-contract=off",
+                    str(root / "tests" / "native" / "slab_margin_check.cpp"), "-o", str(exe)], check=True)
+    out = subprocess.run([str(exe), "2000000"], capture_output=True, text=True, timeout=300)
+    checked, bad, left = out.stdout.split()[-3:]
+    assert int(bad) == 0, out.stdout
+    assert int(checked) > 15_000_000 and float(left) >= 0.5
