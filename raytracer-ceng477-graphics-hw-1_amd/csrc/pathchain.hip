@@ -210,11 +210,23 @@ struct PhaseOut {              // where a chain phase writes its tasks
     int kinline;               // deepest level walked here
 };
 
-// Reflected ray of recorded level lvp = k*cap + sample (raytracer.cpp:430-435).
-__device__ __forceinline__ Ray reflect_from_record(const rtk::DevScene& s, const PcParams& p, size_t lvp) {
-    const float4* rc = p.rec + lvp * 3;
-    const float4 a = rc[0], b = rc[1], c = rc[2];
-    const V hitp{a.x, a.y, a.z}, nn{b.x, b.y, b.z}, d{c.x, c.y, c.z};
+// Hit records (one per recorded level lvp = k*cap + sample), 32 bytes:
+//   rec[2*lvp]     = {hit point xyz, surface code (hit_surface: triangle index or ~sphere slot)}
+//   rec[2*lvp + 1] = {ray direction xyz, material id}
+// The normal is not stored: surface_normal rebuilds it bit-identically from
+// the hit point and the code (a 16-byte face-normal read from the L2-resident
+// scene instead of 16 more bytes per record through HBM, written once and read
+// by every shadow task, the mirror bounce and the shading of the record).
+constexpr int kRecWords = 2;
+__device__ __forceinline__ void rec_write(const PcParams& p, size_t lvp, const V& hitp, int code, const V& d,
+                                          int mat) {
+    float4* rc = p.rec + lvp * kRecWords;
+    rc[0] = make_float4(hitp.x, hitp.y, hitp.z, __int_as_float(code));
+    rc[1] = make_float4(d.x, d.y, d.z, __int_as_float(mat));
+}
+
+// Reflected ray at hit point hitp with normal nn of a ray along d (raytracer.cpp:430-435).
+__device__ __forceinline__ Ray reflect_ray(const rtk::DevScene& s, const V& hitp, const V& nn, const V& d) {
     const V pnt = add(hitp, mul(nn, s.eps));                                            // :397
     const V d2 = nrm(d);
     const V n2 = nrm(nn);
@@ -222,14 +234,22 @@ __device__ __forceinline__ Ray reflect_from_record(const rtk::DevScene& s, const
     return make_ray(pnt, add(d2, mul(mul(n2, 2.0f), rcos)));
 }
 
+// Reflected ray of recorded level lvp.
+__device__ __forceinline__ Ray reflect_from_record(const rtk::DevScene& s, const PcParams& p, size_t lvp) {
+    const float4* rc = p.rec + lvp * kRecWords;
+    const float4 a = rc[0], c = rc[1];
+    const V hitp{a.x, a.y, a.z};
+    return reflect_ray(s, hitp, surface_normal(s, hitp, __float_as_int(a.w)), V{c.x, c.y, c.z});
+}
+
 // Shadow ray of task `owner` (raytracer.cpp:397-404).
 __device__ __forceinline__ Ray shadow_from_record(const rtk::DevScene& s, const PcParams& p, unsigned owner,
                                                   float* tlim) {
     const unsigned lvp = owner / (unsigned)s.nlights;
     const int l = (int)(owner - lvp * (unsigned)s.nlights);
-    const float4* rc = p.rec + (size_t)lvp * 3;
-    const float4 a = rc[0], b = rc[1];
-    const V pnt = add(V{a.x, a.y, a.z}, mul(V{b.x, b.y, b.z}, s.eps));
+    const float4 a = p.rec[(size_t)lvp * kRecWords];
+    const V hitp{a.x, a.y, a.z};
+    const V pnt = add(hitp, mul(surface_normal(s, hitp, __float_as_int(a.w)), s.eps));
     const float4 lp = ld4(&s.lights[l].px);
     const V lpos{lp.x, lp.y, lp.z};
     *tlim = len(sub(lpos, pnt));
@@ -248,9 +268,9 @@ __device__ __forceinline__ Ray shadow_from_record_l2(const rtk::DevScene& s, con
                                                      float* tlim) {
     const unsigned lvp = owner / (unsigned)s.nlights;
     const int l = (int)(owner - lvp * (unsigned)s.nlights);
-    const float4* rc = p.rec + (size_t)lvp * 3;
-    const float4 a = ld4_l2(rc), b = ld4_l2(rc + 1);
-    const V pnt = add(V{a.x, a.y, a.z}, mul(V{b.x, b.y, b.z}, s.eps));
+    const float4 a = ld4_l2(p.rec + (size_t)lvp * kRecWords);
+    const V hitp{a.x, a.y, a.z};
+    const V pnt = add(hitp, mul(surface_normal(s, hitp, __float_as_int(a.w)), s.eps));
     const float4 lp = ld4(&s.lights[l].px);
     const V lpos{lp.x, lp.y, lp.z};
     *tlim = len(sub(lpos, pnt));
@@ -532,14 +552,11 @@ __device__ void chain_body(const rtk::DevScene& s, const rtk::Eye& e, const PcPa
             const HitRec h = wk.best;
             const bool hit = h.prim >= 0;
             V nn{0.0f, 0.0f, 0.0f}, hitp{0.0f, 0.0f, 0.0f};
-            int mat = 0;
+            int mat = 0, code = 0;
             if (hit) {
-                hit_surface(s, r, h, &nn, &mat);
+                hit_surface(s, r, h, &nn, &mat, &code);
                 hitp = add(r.o, mul(r.d, h.t));
-                float4* rc = p.rec + ((size_t)k * p.cap + path) * 3;
-                rc[0] = make_float4(hitp.x, hitp.y, hitp.z, __int_as_float(mat));
-                rc[1] = make_float4(nn.x, nn.y, nn.z, h.t);
-                rc[2] = make_float4(r.d.x, r.d.y, r.d.z, 0.0f);
+                rec_write(p, (size_t)k * p.cap + path, hitp, code, r.d, mat);
             }
             // one shadow task per light (:399-404), light-major within the wave
             const unsigned long long hm = __ballot(hit);
@@ -595,7 +612,7 @@ __device__ void chain_body(const rtk::DevScene& s, const rtk::Eye& e, const PcPa
                 st = kIdle;
                 if (p.trace && !CONT) { p.trace[2 * path] = t_grab; p.trace[2 * path + 1] = (unsigned)wall_clock64(); }
             } else {
-                r = reflect_from_record(s, p, (size_t)k * p.cap + path);
+                r = reflect_ray(s, hitp, nn, r.d);
                 ++k;
                 nrefl++;
                 st = walk_begin<COUNT>(s, r, wk, w) ? kTrav : kDone;
@@ -893,14 +910,11 @@ __global__ __launch_bounds__(kBlock, RT_WAVES_PER_EU) void k_fused(rtk::DevScene
             if (done) {
                 const HitRec h = wk.best;
                 V nn{0.0f, 0.0f, 0.0f}, pnt{0.0f, 0.0f, 0.0f};
-                int mat = 0;
+                int mat = 0, code = 0;
                 if (hit) {
-                    hit_surface(s, r, h, &nn, &mat);
+                    hit_surface(s, r, h, &nn, &mat, &code);
                     const V hitp = add(r.o, mul(r.d, h.t));
-                    float4* rc = p.rec + ((size_t)k * p.cap + path) * 3;
-                    rc[0] = make_float4(hitp.x, hitp.y, hitp.z, __int_as_float(mat));
-                    rc[1] = make_float4(nn.x, nn.y, nn.z, h.t);
-                    rc[2] = make_float4(r.d.x, r.d.y, r.d.z, 0.0f);
+                    rec_write(p, (size_t)k * p.cap + path, hitp, code, r.d, mat);
                     pnt = add(hitp, mul(nn, s.eps));                              // :397
                     const unsigned rank = lane_rank(hm);
                     const unsigned own0 = (unsigned)(((size_t)k * p.cap + path) * nl);
@@ -1004,9 +1018,9 @@ __global__ __launch_bounds__(kBlock, RT_WAVES_PER_EU) void k_fused(rtk::DevScene
                         owner = qbase[(size_t)gq * p.wq_cap + gt + rank];
                         const unsigned lvp = owner / (unsigned)nl;
                         const int l = (int)(owner - lvp * (unsigned)nl);
-                        const float4* rc = p.rec + (size_t)lvp * 3;
-                        const float4 a = rc[0], b = rc[1];
-                        const V pnt = add(V{a.x, a.y, a.z}, mul(V{b.x, b.y, b.z}, s.eps));   // :397
+                        const float4 a = p.rec[(size_t)lvp * kRecWords];
+                        const V hitp{a.x, a.y, a.z};
+                        const V pnt = add(hitp, mul(surface_normal(s, hitp, __float_as_int(a.w)), s.eps));   // :397
                         const float4 lp = ld4(&s.lights[l].px);
                         const V lpos{lp.x, lp.y, lp.z};
                         tlim = len(sub(lpos, pnt));                                          // :400-404
@@ -1052,11 +1066,12 @@ __global__ __launch_bounds__(kBlock, RT_WAVES_PER_EU) void k_fused(rtk::DevScene
 // Blinn-Phong of recorded level k of a path (raytracer.cpp:392-427).
 __device__ __forceinline__ V shade_level(const rtk::DevScene& s, const PcParams& p, unsigned path, int k,
                                          int* mat_out) {
-    const float4* rc = p.rec + ((size_t)k * p.cap + path) * 3;
-    const float4 a = ld_nt(rc), b = ld_nt(rc + 1), c = ld_nt(rc + 2);
-    const int mat = __float_as_int(a.w);
+    const float4* rc = p.rec + ((size_t)k * p.cap + path) * kRecWords;
+    const float4 a = ld_nt(rc), c = ld_nt(rc + 1);
+    const int mat = __float_as_int(c.w);
     *mat_out = mat;
-    const V hitp{a.x, a.y, a.z}, n_{b.x, b.y, b.z}, d{c.x, c.y, c.z};
+    const V hitp{a.x, a.y, a.z}, d{c.x, c.y, c.z};
+    const V n_ = surface_normal(s, hitp, __float_as_int(a.w));
     const dl::Material& M = s.mats[mat - 1];
     const float4 mA = ld4(&M.kax), mD = ld4(&M.kdx);
     V L{0.0f, 0.0f, 0.0f};
@@ -1088,8 +1103,8 @@ __device__ __forceinline__ V shade_level(const rtk::DevScene& s, const PcParams&
 
 // k_shade: Blinn-Phong of every recorded level, one lane per (level, sample)
 // record (the levels of a path are independent here; only the fold below is
-// sequential).  L replaces the record's ray direction (rec[2].xyz), which
-// nothing needs after shading.
+// sequential).  L replaces the record's ray direction (rec[2*lvp+1].xyz),
+// which nothing needs after shading.
 __global__ __launch_bounds__(kBlock) void k_shade(rtk::DevScene s, PcParams p) {
     const size_t n = (size_t)p.levels * (size_t)p.n0;
     for (size_t i = (size_t)blockIdx.x * kBlock + threadIdx.x; i < n; i += (size_t)gridDim.x * kBlock) {
@@ -1099,7 +1114,7 @@ __global__ __launch_bounds__(kBlock) void k_shade(rtk::DevScene s, PcParams p) {
         if (k >= (p.pinfo[path] & 0xff)) continue;
         int mat;
         const V L = shade_level(s, p, path, k, &mat);
-        p.rec[((size_t)k * p.cap + path) * 3 + 2] = make_float4(L.x, L.y, L.z, 0.0f);
+        p.rec[((size_t)k * p.cap + path) * kRecWords + 1] = make_float4(L.x, L.y, L.z, __int_as_float(mat));
     }
 }
 
@@ -1111,14 +1126,13 @@ __device__ __forceinline__ V path_color(const rtk::DevScene& s, const PcParams& 
     V c = kind == kEndBg ? V{s.bgx, s.bgy, s.bgz} : V{0.0f, 0.0f, 0.0f};
     int k = nlev - 1;
     if (kind == kEndLast) {
-        const float4 L = p.rec[((size_t)k * p.cap + path) * 3 + 2];
+        const float4 L = p.rec[((size_t)k * p.cap + path) * kRecWords + 1];
         c = vclamp(V{L.x, L.y, L.z}, 0.0f, FLT_MAX);
         --k;
     }
     for (; k >= 0; --k) {
-        const float4* rc = p.rec + ((size_t)k * p.cap + path) * 3;
-        const float4 L = rc[2];
-        const int mat = __float_as_int(rc[0].w);
+        const float4 L = p.rec[((size_t)k * p.cap + path) * kRecWords + 1];
+        const int mat = __float_as_int(L.w);
         const float4 km = ld4(&s.mats[mat - 1].kmx);
         c = vclamp(add(V{L.x, L.y, L.z}, had(c, V{km.x, km.y, km.z})), 0.0f, FLT_MAX);
     }
@@ -1183,9 +1197,9 @@ __device__ __forceinline__ const dl::Light& fin_light(const rtk::DevScene& s, in
 // occluded (lights >= 32 read their byte directly).
 template <bool LDS>
 __device__ __forceinline__ V shade_words(const rtk::DevScene& s, const PcParams& p, size_t rid, const float4 a,
-                                         const float4 b, const float4 c, const float4 mA, const float4 mD,
+                                         const V n_, const float4 c, const float4 mA, const float4 mD,
                                          const float4 mS, uint32_t occ32) {
-    const V hitp{a.x, a.y, a.z}, n_{b.x, b.y, b.z}, d{c.x, c.y, c.z};
+    const V hitp{a.x, a.y, a.z}, d{c.x, c.y, c.z};
     V L{0.0f, 0.0f, 0.0f};
     L = add(L, V{mA.x, mA.y, mA.z});                                                  // :394-395
     const V pnt = add(hitp, mul(n_, s.eps));                                           // :397
@@ -1267,24 +1281,25 @@ __device__ __forceinline__ V path_shade_fold(const rtk::DevScene& s, const PcPar
     if (nlev == 0) return c;
     const int nl = s.nlights;
     size_t rid = (size_t)(nlev - 1) * p.cap + path;
-    float4 a = p.rec[rid * 3], b = p.rec[rid * 3 + 1], d = p.rec[rid * 3 + 2];
+    float4 a = p.rec[rid * kRecWords], d = p.rec[rid * kRecWords + 1];
     OccRaw oc = occ_load<LDS>(p, rid, nl);
     for (int k = nlev - 1; k >= 0; --k) {
-        const dl::Material& M = fin_mat<LDS>(s, __float_as_int(a.w) - 1);   // before the prefetch (vmcnt order)
+        const dl::Material& M = fin_mat<LDS>(s, __float_as_int(d.w) - 1);   // before the prefetch (vmcnt order)
         const float4 mA = ld4(&M.kax), mD = ld4(&M.kdx), mS = ld4(&M.ksx), km = ld4(&M.kmx);
+        const V n_ = surface_normal(s, V{a.x, a.y, a.z}, __float_as_int(a.w));
         const size_t rn = (size_t)max(k - 1, 0) * p.cap + path;
 #if RT_FINISH_PREFETCH
-        const float4 na = p.rec[rn * 3], nb = p.rec[rn * 3 + 1], nd = p.rec[rn * 3 + 2];
+        const float4 na = p.rec[rn * kRecWords], nd = p.rec[rn * kRecWords + 1];
         const OccRaw noc = occ_load<LDS>(p, rn, nl);
 #endif
-        const V L = shade_words<LDS>(s, p, rid, a, b, d, mA, mD, mS, occ_bits<LDS>(p, oc, nl));
+        const V L = shade_words<LDS>(s, p, rid, a, n_, d, mA, mD, mS, occ_bits<LDS>(p, oc, nl));
         if (kind == kEndLast && k == nlev - 1) c = vclamp(L, 0.0f, FLT_MAX);
         else c = vclamp(add(L, had(c, V{km.x, km.y, km.z})), 0.0f, FLT_MAX);
 #if RT_FINISH_PREFETCH
-        rid = rn; a = na; b = nb; d = nd; oc = noc;
+        rid = rn; a = na; d = nd; oc = noc;
 #else
         if (k > 0) {
-            rid = rn; a = p.rec[rn * 3]; b = p.rec[rn * 3 + 1]; d = p.rec[rn * 3 + 2];
+            rid = rn; a = p.rec[rn * kRecWords]; d = p.rec[rn * kRecWords + 1];
             oc = occ_load<LDS>(p, rn, nl);
         }
 #endif

@@ -530,7 +530,7 @@ int render_chain(rt_scene* s, const rtk::Eye& eye, const rtk::FrameParams& f, bo
     const int unit = 8 * f.aa;
     const size_t unit_samples = (size_t)tiles_x * f.aa * 64;
     const size_t units_total = (size_t)(li + unit - 1) / unit;
-    const size_t per_sample = (size_t)levels * (48 + 8 * nl + nl) + 16;
+    const size_t per_sample = (size_t)levels * (32 + 8 * nl + nl) + 16;   // 32-B hit records (pathchain.hip)
     const size_t id_limit = (size_t)(INT32_MAX - 1) / ((size_t)levels * nl);   // u32 task owner ids (pathchain.hpp)
     const size_t target = std::max<size_t>(
         unit_samples, std::min({s->chunk_samples, kChainBudgetBytes / per_sample, id_limit}));
@@ -569,7 +569,7 @@ int render_chain(rt_scene* s, const rtk::Eye& eye, const rtk::FrameParams& f, bo
     const unsigned wq_cap = fused ? rtc::fused_wave_qcap((int)cap, G, levels, nl) : 0u;
 
     ArenaLayout L;
-    const size_t o_rec = L.take<float4>(3 * cap * levels), o_pinfo = L.take<int>(cap),
+    const size_t o_rec = L.take<float4>(2 * cap * levels), o_pinfo = L.take<int>(cap),
                  o_occ = L.take<uint8_t>(cap * levels * nl + 8);   // + 8: k_finish reads aligned dwords
     size_t o_sqA = 0, o_scntA = 0, o_sflatA = 0, o_cq = 0, o_ccnt = 0, o_cflat = 0, o_sqB = 0, o_scntB = 0,
            o_sflatB = 0, o_totals = 0, o_wq = 0;

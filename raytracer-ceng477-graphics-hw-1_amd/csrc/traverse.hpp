@@ -122,19 +122,39 @@ __device__ __forceinline__ bool any_hit(const rtk::DevScene& s, const Ray& r, fl
     return false;
 }
 
-// Winner's normal and material (Intersection::normal / material_id).
-__device__ __forceinline__ void hit_surface(const rtk::DevScene& s, const Ray& r, const HitRec& h, V* n, int* mat) {
+// Winner's normal and material (Intersection::normal / material_id); *code
+// names the surface for surface_normal: the triangle index (>= 0) or ~slot of
+// the sphere's primitive slot.
+__device__ __forceinline__ void hit_surface(const rtk::DevScene& s, const Ray& r, const HitRec& h, V* n, int* mat,
+                                            int* code = nullptr) {
     const float4* pr = reinterpret_cast<const float4*>(&s.prims[h.prim]);
     const float4 p0 = pr[0];
     if (__float_as_int(p0.w) < 0) {             // sphere
         const float4 p1 = pr[1];
         *n = sphere_normal(r, p0, p1.x, h.t);
         *mat = __float_as_int(pr[2].w);
+        if (code) *code = ~h.prim;
     } else {
         const float4 ts = ld4(&s.tri_shade[__float_as_int(p0.w)]);
         *n = V{ts.x, ts.y, ts.z};
         *mat = __float_as_int(ts.w);
+        if (code) *code = __float_as_int(p0.w);
     }
+}
+
+// The same normal from the hit point and the surface code: a triangle's face
+// normal, or a sphere's (hitp - c) / r normalised -- sphere_normal's own
+// arithmetic on the same hit point (its getPoint is hitp's expression), so
+// bit-identical to what hit_surface returned.
+__device__ __forceinline__ V surface_normal(const rtk::DevScene& s, const V& hitp, int code) {
+    if (code >= 0) {
+        const float4 ts = ld4(&s.tri_shade[code]);
+        return V{ts.x, ts.y, ts.z};
+    }
+    const float4* pr = reinterpret_cast<const float4*>(&s.prims[~code]);
+    const float4 c = pr[0];
+    const float rad = pr[1].x;
+    return nrm(divs(sub(hitp, V{c.x, c.y, c.z}), rad));
 }
 
 // EyeRayGenerator::generate (raytracer.cpp:319-324).  (col+0.5)*su is a double
