@@ -54,13 +54,17 @@ B_NODE, B_TRI, B_SPH, B_PIX = 32, 36, 16, 3
 
 def workspace_bytes(c: dict, nlights: int, out_pixels: int) -> int:
     """Chain-path workspace bytes of one frame from its exact ray counts (pathchain.hip):
-    every hit writes a 48-B record and is shaded from it again in k_finish (48 B + 8 B of occlusion
-    dwords); every sample writes and reads its 4-B path word; every shadow task id is written,
-    packed (read + write) and read (16 B), its ray re-derived from the record's first 32 B and its
-    1-B result written; every reflection re-reads its 48-B record; every output pixel is 3 B."""
+    every hit writes a 32-B record (rec_write) and is shaded from it again in k_finish (32 B, its
+    16-B face normal / sphere and 8 B of occlusion dwords); every sample writes and reads its 4-B
+    path word; every TRACED shadow task id is written, packed (read + write) and read (16 B), its ray
+    re-derived from the record's first 16 B and the surface normal (16 B) and its 1-B result written;
+    a skipped one (light_needed) writes its 1-B result only; every reflection re-reads its 32-B record
+    and normal; every output pixel is 3 B."""
     hits = c["shadow_rays"] // max(1, nlights)
-    return (hits * (48 + 48 + 8) + c["primary_rays"] * 8 + c["shadow_rays"] * (16 + 32 + 1)
-            + c["reflection_rays"] * 48 + out_pixels * 3)
+    skipped = c.get("shadow_rays_skipped", 0)
+    traced = c["shadow_rays"] - skipped
+    return (hits * (32 + 32 + 16 + 8) + c["primary_rays"] * 8 + traced * (16 + 16 + 16 + 1) + skipped
+            + c["reflection_rays"] * (32 + 16) + out_pixels * 3)
 
 # kernels one frame launches, per render path (the roofline covers all of them)
 PATH_KERNELS = {
@@ -251,10 +255,10 @@ def main() -> int:
     alg_bytes = traversal_bytes + ws_bytes
     note("counting passes done")
     ps_local = cnt["primary_rays"] + cnt["shadow_rays"]
-    tot = torch.tensor([ps_local, cnt["primary_rays"], cnt["shadow_rays"], cnt["reflection_rays"]],
-                       dtype=torch.float64, device=dev)
+    tot = torch.tensor([ps_local, cnt["primary_rays"], cnt["shadow_rays"], cnt["reflection_rays"],
+                        cnt["shadow_rays_skipped"]], dtype=torch.float64, device=dev)
     tot = all_reduce(tot)
-    ps_frame, prim_frame, shadow_frame, refl_frame = (int(x) for x in tot.tolist())
+    ps_frame, prim_frame, shadow_frame, refl_frame, skip_frame = (int(x) for x in tot.tolist())
 
     def step(n, ev_pair=None):
         """n frames (steps) submitted together: this rank's stripes of each, then (N>1) one gather."""
@@ -374,12 +378,18 @@ def main() -> int:
                        "trace_frames": max(a.warmup, F) + a.steps if a.trace else None,
                        "assembled_frames_equal_single_gpu": frames_ok,
                        "primary_rays": prim_frame, "shadow_rays": shadow_frame, "reflection_rays": refl_frame,
+                       # of shadow_rays: rays the timed kernels do not trace because their result cannot
+                       # change the pixel (light behind the surface, pathchain.hip light_needed); the
+                       # image is the reference's either way (parity tests)
+                       "shadow_rays_skipped": skip_frame,
+                       "mray_s_traced": round((ps_frame - skip_frame) * a.steps / elapsed / 1e6, 3),
                        "mray_s_all": round((ps_frame + refl_frame) * a.steps / elapsed / 1e6, 3),
                        "scene_load_s": round(load_s, 4),
                        "host_build": {"bvh_build_ms": round(binfo["build_ms"], 2), "ref_tree_ms": round(binfo["ref_ms"], 2),
                                       "wide_tree_ms": round(binfo["wide_ms"], 2), "threads": binfo["build_threads"]},
-                       "value_definition": f"frames submitted {F} at a time as frame batches, scene and frames "
-                                           "resident in HBM, max-over-ranks wall time"},
+                       "value_definition": f"the reference's primary+shadow rays of a frame (its own counters) x "
+                                           f"frames / wall time; frames submitted {F} at a time as frame batches, "
+                                           "scene and frames resident in HBM, max-over-ranks wall time"},
             "single_frame": ({"ms": round(lat_ms, 4), "mray_s": round(ps_frame / lat_ms / 1e3, 3),
                               "definition": "one frame alone on the GPU (rt_render_device), device time"}
                              if lat else None),

@@ -33,7 +33,7 @@
 extern "C" {
 #endif
 
-#define RT_ABI_VERSION 5
+#define RT_ABI_VERSION 6
 
 typedef enum rt_status {
     RT_OK = 0,
@@ -110,6 +110,9 @@ typedef struct rt_stats {
     uint64_t sphere_tests;      /* analytic sphere tests                     */
     double   kernel_ms;         /* device time of the render kernel(s)       */
     double   wall_ms;           /* host wall time of the call                */
+    uint64_t shadow_rays_skipped;  /* of shadow_rays: not traced by the chain path's
+                                      timed kernels because they cannot change the
+                                      pixel (light behind the surface; ABI 6)   */
 } rt_stats;
 
 typedef struct rt_bvh_info {

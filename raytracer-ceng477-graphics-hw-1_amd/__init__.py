@@ -59,7 +59,8 @@ class Stats(ctypes.Structure):
     _fields_ = [("primary_rays", ctypes.c_uint64), ("shadow_rays", ctypes.c_uint64),
                 ("reflection_rays", ctypes.c_uint64), ("node_visits", ctypes.c_uint64),
                 ("tri_tests", ctypes.c_uint64), ("sphere_tests", ctypes.c_uint64),
-                ("kernel_ms", ctypes.c_double), ("wall_ms", ctypes.c_double)]
+                ("kernel_ms", ctypes.c_double), ("wall_ms", ctypes.c_double),
+                ("shadow_rays_skipped", ctypes.c_uint64)]
 
     def as_dict(self) -> dict:
         return {k: getattr(self, k) for k, _ in self._fields_}

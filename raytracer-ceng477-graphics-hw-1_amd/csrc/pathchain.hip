@@ -127,7 +127,7 @@ using WalkStack = StackLds;
 using WalkStack = StackPriv;
 #endif
 __shared__ unsigned g_head;                    // block-local work queue head
-__shared__ unsigned g_scnt;                    // block-local shadow-ray count (hit lanes)
+__shared__ unsigned g_scnt;                    // block-local shadow-task count
 
 // Pair fetches go to global memory: caching the top BVH levels in LDS showed
 // no gain (their loads are wave-coherent and hit the L1).
@@ -223,6 +223,24 @@ __device__ __forceinline__ void rec_write(const PcParams& p, size_t lvp, const V
     float4* rc = p.rec + lvp * kRecWords;
     rc[0] = make_float4(hitp.x, hitp.y, hitp.z, __int_as_float(code));
     rc[1] = make_float4(d.x, d.y, d.z, __int_as_float(mat));
+}
+
+// Can light l's shadow ray from this hit change the pixel?  The shading
+// (shade_words, raytracer.cpp:405-425) adds nothing for an occluded light; for
+// a visible one with cos < cos_thr it adds no specular term (its test fails)
+// and the diffuse term kd * 0 * E = +-0 (the clamp gives 0).  With kd (host:
+// s.cull_shadows) and E finite the sum is the same either way, so the ray is
+// not traced and the light is recorded as occluded.  The same arithmetic as
+// shade_words on the same record values, so the decision is exact.
+__device__ __forceinline__ bool light_needed(const rtk::DevScene& s, const V& hitp, const V& nn, int l) {
+    const float4 lp = ld4(&s.lights[l].px), li4 = ld4(&s.lights[l].ix);
+    const V lpos{lp.x, lp.y, lp.z};
+    const V pnt = add(hitp, mul(nn, s.eps));
+    const float dist = len(sub(lpos, pnt));
+    const float cos_t = dot(nrm(sub(lpos, hitp)), nn);
+    if (!(cos_t < s.cos_thr)) return true;
+    const V E = divs(V{li4.x, li4.y, li4.z}, dist * dist);
+    return !(__builtin_isfinite(E.x) && __builtin_isfinite(E.y) && __builtin_isfinite(E.z));
 }
 
 // Reflected ray at hit point hitp with normal nn of a ray along d (raytracer.cpp:430-435).
@@ -531,7 +549,7 @@ __device__ void chain_body(const rtk::DevScene& s, const rtk::Eye& e, const PcPa
                            const PhaseOut& o) {
     WalkStack stk;
     Work w;
-    uint32_t nprim = 0, nrefl = 0;
+    uint32_t nprim = 0, nrefl = 0, nskip = 0;
     const int nl = s.nlights;
     unsigned nb;
     if (CONT) nb = chunk_count(p.totals[1], G, blk, (unsigned)p.tchunk);
@@ -558,39 +576,44 @@ __device__ void chain_body(const rtk::DevScene& s, const rtk::Eye& e, const PcPa
                 hitp = add(r.o, mul(r.d, h.t));
                 rec_write(p, (size_t)k * p.cap + path, hitp, code, r.d, mat);
             }
-            // one shadow task per light (:399-404), light-major within the wave
-            const unsigned long long hm = __ballot(hit);
-            bool queued = false;
-            if (CONT && kBq > 0 && hm) {
-                // phase B: into the workgroup queue (walked by its finished waves); the records
-                // written above must be visible to the workgroup before the owner ids are
-                __builtin_amdgcn_s_waitcnt(0);     // the record stores have completed (a workgroup fence
-                                                   // alone does not wait for them on gfx950)
-                const unsigned cnt = (unsigned)__popcll(hm), need = cnt * (unsigned)nl;
-                const int leader = __ffsll((unsigned long long)hm) - 1;
-                unsigned base = 0;
-                if (lane_id() == leader) base = atomicAdd(&g_bq_tail, need);
-                base = __shfl(base, leader, 64);
-                const unsigned rank = lane_rank(hm);
-                const unsigned own0 = (unsigned)(((size_t)k * p.cap + path) * nl);
-                if (base + need <= (unsigned)p.bq_cap) {
-                    if (hit)
-                        for (int l = 0; l < nl; ++l)
-                            __atomic_store_n(&g_bq[base + l * cnt + rank], own0 + (unsigned)l, __ATOMIC_RELAXED);
-                    queued = true;
-                } else if (hit) {
-                    for (int l = 0; l < nl; ++l) {       // spilled: mark the reserved slots that exist
-                        const unsigned q = base + l * cnt + rank;
-                        if (q < (unsigned)p.bq_cap) __atomic_store_n(&g_bq[q], kBqSkip, __ATOMIC_RELAXED);
+            // one shadow task per light (:399-404) whose ray can change the pixel (light_needed; the
+            // counting passes trace every one, as the reference does); light-major within the wave
+            const size_t lvp = (size_t)k * p.cap + path;
+            const unsigned own0 = (unsigned)(lvp * nl);
+            if (CONT && kBq > 0 && __ballot(hit))
+                __builtin_amdgcn_s_waitcnt(0);     // phase B: the record stores have completed before the
+                                                   // owner ids are published to the workgroup (a workgroup
+                                                   // fence alone does not wait for them on gfx950)
+            for (int l = 0; l < nl; ++l) {
+                bool want = hit;
+                if (hit && s.cull_shadows && !light_needed(s, hitp, nn, l)) {
+                    if (COUNT) nskip++;            // the reference traces it: counted as its shadow ray
+                    if (!COUNT || s.count_prod) {
+                        want = false;
+                        p.occ[lvp * nl + l] = 1;   // shaded as occluded: the same sum (light_needed)
                     }
                 }
-            }
-            if (hit && !queued) {
-                const unsigned cnt = (unsigned)__popcll(hm);
-                const unsigned base = wave_grab_lds(&g_scnt, hm);
-                const unsigned rank = lane_rank(hm);
-                const unsigned own0 = (unsigned)(((size_t)k * p.cap + path) * nl);
-                for (int l = 0; l < nl; ++l) sq[base * nl + l * cnt + rank] = own0 + (unsigned)l;
+                const unsigned long long m = __ballot(want);
+                if (!m) continue;
+                const unsigned cnt = (unsigned)__popcll(m), rank = lane_rank(m);
+                bool queued = false;
+                if (CONT && kBq > 0) {
+                    // phase B: into the workgroup queue (walked by its finished waves)
+                    const int leader = __ffsll((unsigned long long)m) - 1;
+                    unsigned base = 0;
+                    if (lane_id() == leader) base = atomicAdd(&g_bq_tail, cnt);
+                    base = __shfl(base, leader, 64);
+                    if (base + cnt <= (unsigned)p.bq_cap) {
+                        if (want) __atomic_store_n(&g_bq[base + rank], own0 + (unsigned)l, __ATOMIC_RELAXED);
+                        queued = true;
+                    } else if (want && base + rank < (unsigned)p.bq_cap) {
+                        __atomic_store_n(&g_bq[base + rank], kBqSkip, __ATOMIC_RELAXED);   // spilled: mark the slot
+                    }
+                }
+                if (!queued) {
+                    const unsigned base = wave_grab_lds(&g_scnt, m);
+                    if (want) sq[base + rank] = own0 + (unsigned)l;
+                }
             }
             bool ends = true;
             if (!hit) {                                                          // :442-449
@@ -691,11 +714,14 @@ __device__ void chain_body(const rtk::DevScene& s, const rtk::Eye& e, const PcPa
     }
     __syncthreads();
     if (threadIdx.x == 0) {
-        o.scount[blk] = g_scnt * (unsigned)nl;
+        o.scount[blk] = g_scnt;
         if (!CONT) o.ccount[blk] = g_ccnt;
     }
     if (COUNT) {
-        if (CONT) wave_add_counter(&p.counters[1], nshadow);
+        // shadow rays not traced (light_needed): counter 6; a production counting pass (count_prod)
+        // skips them, and counts them among the shadow rays here so counter 1 stays the reference's
+        wave_add_counter(&p.counters[1], (CONT ? nshadow : 0u) + (s.count_prod ? nskip : 0u));
+        wave_add_counter(&p.counters[6], nskip);
         wave_add_counter(&p.counters[0], nprim);
         wave_add_counter(&p.counters[2], nrefl);
         wave_add_counter(&p.counters[3], w.nodes);

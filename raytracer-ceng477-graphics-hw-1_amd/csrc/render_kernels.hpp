@@ -51,6 +51,8 @@ struct DevScene {
     int walk_cap;         // always-on bound on one walk's step calls (traverse2.hpp walk_runaway)
     int leaf_wait;        // 4-wide walks: a lane at a leaf record waits while fewer than leaf_wait/64 of the
                           // wave's walking lanes are at one (0: never waits; RT_LEAF_WAIT)
+    int cull_shadows;     // chain path: shadow rays that cannot change the pixel are not traced
+                          // (pathchain.hip light_needed; every material's kd finite; RT_CULL=0 disables)
 
     // Sphere prims carry ~sphere_index in p0.w (negative), triangles their id.
     __device__ __forceinline__ bool prim_is_sphere(int, const float4 p0) const {

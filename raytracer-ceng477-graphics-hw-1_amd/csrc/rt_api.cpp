@@ -371,6 +371,11 @@ int upload_scene(rt_scene* s, const rt_options* opts) {
     if (const char* e = std::getenv("RT_LEAF_WAIT")) d.leaf_wait = std::max(0, std::min(64, std::atoi(e)));
     d.leaf_wait_any = d.leaf_wait;
     if (const char* e = std::getenv("RT_LEAF_WAIT_ANY")) d.leaf_wait_any = std::max(0, std::min(64, std::atoi(e)));
+    // shadow rays of lights behind the surface add +-0 when kd is finite (pathchain.hip light_needed)
+    d.cull_shadows = 1;
+    for (const auto& m : mats)
+        if (!std::isfinite(m.kdx) || !std::isfinite(m.kdy) || !std::isfinite(m.kdz)) d.cull_shadows = 0;
+    if (const char* e = std::getenv("RT_CULL")) d.cull_shadows = d.cull_shadows && std::atoi(e) != 0;
     // measurement: counting passes walk the production trees and count fetched bytes (bench.py)
     d.count_prod = std::getenv("RT_COUNT_PROD") ? 1 : 0;
     if (const char* e = std::getenv("RT_PRIO")) d.prio = std::atoi(e) != 0;
@@ -1055,6 +1060,7 @@ int rt_render_cameras(rt_scene* s, const rt_camera* cams, int n, int aa, uint8_t
             sum.primary_rays += one.primary_rays; sum.shadow_rays += one.shadow_rays;
             sum.reflection_rays += one.reflection_rays; sum.node_visits += one.node_visits;
             sum.tri_tests += one.tri_tests; sum.sphere_tests += one.sphere_tests; sum.kernel_ms += one.kernel_ms;
+            sum.shadow_rays_skipped += one.shadow_rays_skipped;
         }
         if (stats) {
             *stats = sum;
@@ -1156,7 +1162,7 @@ int rt_counters_read(rt_scene* s, rt_stats* st) {
     unsigned long long c[8];
     HIP_TRY(hipMemcpy(c, s->d_counters, sizeof(c), hipMemcpyDeviceToHost));
     st->primary_rays = c[0]; st->shadow_rays = c[1]; st->reflection_rays = c[2];
-    st->node_visits = c[3]; st->tri_tests = c[4]; st->sphere_tests = c[5];
+    st->node_visits = c[3]; st->tri_tests = c[4]; st->sphere_tests = c[5]; st->shadow_rays_skipped = c[6];
     return check_device_error(s);
 }
 

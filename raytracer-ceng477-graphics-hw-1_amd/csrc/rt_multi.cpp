@@ -232,6 +232,7 @@ int rt_internal_group_render(rt_group* g, const rt_camera* cam, int aa, uint8_t*
             sum.primary_rays += one.primary_rays; sum.shadow_rays += one.shadow_rays;
             sum.reflection_rays += one.reflection_rays; sum.node_visits += one.node_visits;
             sum.tri_tests += one.tri_tests; sum.sphere_tests += one.sphere_tests;
+            sum.shadow_rays_skipped += one.shadow_rays_skipped;
         } else if ((rc = rt_scene_check(g->rep[d]))) {
             return rc;
         }

@@ -118,6 +118,41 @@ def test_device_counters_accumulate(path, goldens, pkg, scene_dir, torch_cuda):
         assert np.array_equal(out.cpu().numpy(), load_golden_image(cam_g))
 
 
+@pytest.mark.parametrize("gname", ["C3_hm_1080p_d6_aa1", "cornellbox_aa1", "C1_simple_aa1"])
+def test_skipped_shadow_rays(gname, goldens, pkg, scene_dir, torch_cuda, monkeypatch):
+    """Shadow rays whose light is behind the surface are not traced by the chain path
+    (pathchain.hip light_needed): the image is the golden with and without the skip (RT_CULL=0), the
+    counting pass still reports the reference's shadow rays, and a production counting pass
+    (RT_COUNT_PROD, which skips them) reports the same totals and the same number skipped."""
+    g = golden_by_name(goldens, gname)
+    cam_g = g["cameras"][0]
+    ref = load_golden_image(cam_g)
+    st = {}
+    for cull in ("1", "0"):
+        for prod in ("0", "1"):
+            monkeypatch.setenv("RT_CULL", cull)
+            if prod == "1":
+                monkeypatch.setenv("RT_COUNT_PROD", "1")
+            else:
+                monkeypatch.delenv("RT_COUNT_PROD", raising=False)
+            with pkg.Scene.from_xml(config_path(scene_dir, g["config"]), device=0, render_path="chain") as s:
+                c, _ = s.cameras()[cam_g["camera"]]
+                img, st[cull, prod] = s.render(c, aa=g["aa"], stats=True)
+                assert np.array_equal(img, ref), f"RT_CULL={cull} RT_COUNT_PROD={prod} (counting pass)"
+                img2, _ = s.render(c, aa=g["aa"], stats=False)
+                assert np.array_equal(img2, ref), f"RT_CULL={cull} (timed kernels)"
+    ref_counts = _counters(cam_g["counters"])
+    assert _stats(st["1", "0"]) == ref_counts
+    assert _stats(st["0", "0"]) == ref_counts
+    for cull in ("1", "0"):
+        assert st[cull, "1"]["primary_rays"] == ref_counts[0]
+        assert st[cull, "1"]["shadow_rays"] == ref_counts[1]
+    assert st["0", "0"]["shadow_rays_skipped"] == 0 and st["0", "1"]["shadow_rays_skipped"] == 0
+    assert st["1", "1"]["shadow_rays_skipped"] == st["1", "0"]["shadow_rays_skipped"]
+    if gname.startswith("C3"):
+        assert st["1", "0"]["shadow_rays_skipped"] > 0.05 * ref_counts[1]
+
+
 def test_max_depth_override_matches_derived_scene(goldens, pkg, scene_dir, torch_cuda):
     """cornellbox.xml camera 2 with MaxRecursionDepth forced to 0 == the C2 golden."""
     g = golden_by_name(goldens, "C2_cornellbox_800_d0_aa1")
