@@ -561,7 +561,7 @@ __device__ void chain_body(const rtk::DevScene& s, const rtk::Eye& e, const PcPa
     int k = 0;
     Ray r;
     Walk wk;
-    unsigned t_grab = 0;
+    unsigned t_grab = 0, tsteps = 0;
     bool fresh = false;      // lane just took an eye ray (packet walk pending)
     StepStat stat;
     while (true) {
@@ -634,6 +634,10 @@ __device__ void chain_body(const rtk::DevScene& s, const rtk::Eye& e, const PcPa
             if (ends || handoff) {
                 st = kIdle;
                 if (p.trace && !CONT) { p.trace[2 * path] = t_grab; p.trace[2 * path + 1] = (unsigned)wall_clock64(); }
+                if (p.trace && CONT) {       // phase B: {grab, end, last level, walk steps} after A's entries
+                    unsigned* tb = p.trace + 2 * ((size_t)p.cap + p.trace_blocks) + 4 * (size_t)path;
+                    tb[0] = t_grab; tb[1] = (unsigned)wall_clock64(); tb[2] = (unsigned)k; tb[3] = tsteps;
+                }
             } else {
                 r = reflect_ray(s, hitp, nn, r.d);
                 ++k;
@@ -656,6 +660,7 @@ __device__ void chain_body(const rtk::DevScene& s, const rtk::Eye& e, const PcPa
                             const unsigned lvp = p.cflat[j];
                             path = lvp % (unsigned)p.cap;
                             k = (int)(lvp / (unsigned)p.cap) + 1;
+                            if (p.trace) { t_grab = (unsigned)wall_clock64(); tsteps = 0; }
                             r = reflect_from_record(s, p, lvp);
                             nrefl++;
                             st = walk_begin<COUNT>(s, r, wk, w) ? kTrav : kDone;
@@ -702,6 +707,7 @@ __device__ void chain_body(const rtk::DevScene& s, const rtk::Eye& e, const PcPa
                 break;
             stat.step(st == kTrav, wk.cur >= 0, RT_STEP_STATS && st == kTrav && wk.tree == nullptr && leaf_postponed(s.leaf_wait, wk));
             if (st == kTrav) {
+                if (CONT && p.trace) ++tsteps;
                 if (closest_step<COUNT, FetchTop, WalkStack, CONT>(s, r, stk, wk, w) || walk_runaway(s, wk)) st = kDone;
             }
         }

@@ -92,8 +92,10 @@ struct PcParams {
     unsigned wq_cap;
     int producers;    // k_fused: chain-producing waves per workgroup (1..4), the rest consume
     int crefill;      // k_fused consumers refill once <= crefill lanes are still walking
-    unsigned* trace;  // diagnostics (RT_TRACE): [cap][2] sample {grab, chain end}, then [ogrid][2] k_occlude
-                      // workgroup {start, end}; wall clock; or null
+    unsigned* trace;  // diagnostics (RT_TRACE): [cap][2] sample {grab, chain end}, then [trace_blocks][2]
+                      // k_occlude workgroup {start, end}, then [cap][4] phase-B continuation {grab, end,
+                      // last level, walk steps}; wall clock; or null
+    int trace_blocks;
 };
 
 // Worst-case task-queue slots per workgroup: every sample of the workgroup

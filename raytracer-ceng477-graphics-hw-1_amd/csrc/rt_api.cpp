@@ -644,7 +644,8 @@ int render_chain(rt_scene* s, const rtk::Eye& eye, const rtk::FrameParams& f, bo
         p.eyes[i] = i < p.nframes && p.nframes > 1 ? f.eyes[i] : eye;
         p.fouts[i] = i < p.nframes && p.nframes > 1 ? f.outs[i] : f.out;
     }
-    const size_t trace_n = 2 * (cap + (size_t)std::max(s->mix_grid, s->occl_grid));
+    p.trace_blocks = std::max(s->mix_grid, s->occl_grid);
+    const size_t trace_n = 2 * (cap + (size_t)p.trace_blocks) + 4 * cap;
     p.trace = trace_buffer(s, trace_n);
     for (int r0 = 0; r0 < li; r0 += chunk_rows) {
         p.chunk_row0 = r0;
@@ -655,7 +656,7 @@ int render_chain(rt_scene* s, const rtk::Eye& eye, const rtk::FrameParams& f, bo
         if (fused) HIP_TRY(rtc::launch_fused_chunk(s->dev, eye, p, count, st));
         else HIP_TRY(rtc::launch_chain_chunk(s->dev, eye, p, count, st));
     }
-    if (p.trace) trace_dump(s, st, 0, (unsigned)cap, (unsigned)p.ogrid, trace_n);   // last chunk only
+    if (p.trace) trace_dump(s, st, 0, (unsigned)cap, (unsigned)p.trace_blocks, trace_n);   // last chunk only
     if (!arena.last) HIP_TRY(hipEventCreateWithFlags(&arena.last, hipEventDisableTiming));
     HIP_TRY(hipEventRecord(arena.last, st));
     arena.last_stream = st;

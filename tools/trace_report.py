@@ -94,6 +94,24 @@ def main():
             os_, oe = rel(ob[0::2][okb], t0), rel(ob[1::2][okb], t0)
             r["k_occlude_blocks"] = {"start_min": round(float(os_.min()), 1), "start_max": round(float(os_.max()), 1),
                                      "end_pct_us": {p: round(float(np.percentile(oe, p)), 1) for p in (0, 50, 90, 99, 100)}}
+            pb = tr[2 * (cap + og):2 * (cap + og) + 4 * cap].reshape(-1, 4)
+            okp = pb[:, 1] != 0
+            if okp.any():        # phase-B continuations (k_mix chain role): grab, end, last level, walk steps
+                q = np.nonzero(okp)[0]
+                bs, be = rel(pb[okp, 0], t0), rel(pb[okp, 1], t0)
+                bd = be - bs
+                lv, stp = pb[okp, 2].astype(np.int64), pb[okp, 3].astype(np.int64)
+                top = np.argsort(bd)[::-1][:8]
+                r["phase_b"] = {
+                    "chains": int(okp.sum()),
+                    "start_pct_us": {p: round(float(np.percentile(bs, p)), 1) for p in (0, 50, 100)},
+                    "end_pct_us": {p: round(float(np.percentile(be, p)), 1) for p in (50, 90, 99, 99.9, 100)},
+                    "dur_pct_us": {p: round(float(np.percentile(bd, p)), 1) for p in (50, 90, 99, 100)},
+                    "steps_pct": {p: int(np.percentile(stp, p)) for p in (50, 90, 99, 100)},
+                    "last_level_hist": np.bincount(lv).tolist(),
+                    "slowest": [{"q": int(q[j]), "start": round(float(bs[j]), 1), "dur": round(float(bd[j]), 1),
+                                 "level": int(lv[j]), "steps": int(stp[j]),
+                                 "us_per_step": round(float(bd[j]) / max(1, int(stp[j])), 2)} for j in top]}
             res.append(r)
         sc.close()
         del os.environ["RT_TRACE"]
