@@ -42,6 +42,13 @@ import time
 from pathlib import Path
 
 ROOT = Path(__file__).resolve().parent
+
+# Hardware queues per process (read by the HIP runtime at its first use, so set before torch touches
+# the GPU): each workspace slot renders on its own stream beside the caller's, and HIP multiplexes
+# streams beyond GPU_MAX_HW_QUEUES (4 by default) onto the same queues, which serialises the slots.
+# With 8 queues the library runs 6 frame batches in flight (rt_api.cpp tune_slots); RT_HW_QUEUES
+# overrides (the box refuses more than 32).
+os.environ["GPU_MAX_HW_QUEUES"] = os.environ.get("RT_HW_QUEUES", "8")
 sys.path.insert(0, str(ROOT))
 
 import __graft_entry__ as graft  # noqa: E402
@@ -369,7 +376,8 @@ def main() -> int:
                        "max_recursion_depth": 6 if config != "C2_cornellbox_800_d0" else 0,
                        "parallelism": f"stripes{S}x{world}" + ("+rccl_gather" if world > 1 else ""),
                        "frames_in_flight": F, "frame_latency_ms": round(lat_ms, 4) if lat else None,
-                       "workspace_slots": int(os.environ.get("RT_SLOTS", "3")),
+                       "workspace_slots": int(os.environ.get("RT_SLOTS", max(1, min(6, int(os.environ["GPU_MAX_HW_QUEUES"]) - 1)))),
+                       "hw_queues": int(os.environ["GPU_MAX_HW_QUEUES"]),
                        # every frame this process rendered on the GPU (counting pass, warmup, timed, latency,
                        # host-buffer runs): the divisor for whole-run PMC totals (tools/summarize_profile.py)
                        "frames_rendered_total": 2 + max(a.warmup, F) + a.steps

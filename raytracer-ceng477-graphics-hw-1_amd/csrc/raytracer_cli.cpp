@@ -33,6 +33,9 @@ int die(const char* what) {
 }  // namespace
 
 int main(int argc, char** argv) {
+    // several cameras render as concurrent frame batches, one stream each: give HIP enough hardware
+    // queues that they do not share (read at the runtime's first use; RT_HW_QUEUES overrides)
+    setenv("GPU_MAX_HW_QUEUES", std::getenv("RT_HW_QUEUES") ? std::getenv("RT_HW_QUEUES") : "8", 1);
     const char* scene_path = nullptr;
     int aa = 2, max_depth = -1000, device = -1, gpus = 0;
     bool write = true;

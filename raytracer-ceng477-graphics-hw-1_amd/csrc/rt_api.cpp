@@ -135,7 +135,8 @@ struct rt_scene {
     // 159.6, 16 M 147.4, 32 M 140.6 ms/frame.  32 M samples = 15 GB of workspace per slot (C3).
     size_t chunk_samples = size_t(32) << 20;
     int tune_batch = 32;        // RT_BATCH: frames per batched launch (rt_render_frames/cameras; 1 = off)
-    int tune_slots = 3;         // RT_SLOTS: frame batches in flight together (workspace slots, <= kSlots)
+    int tune_slots = 3;         // RT_SLOTS: frame batches in flight together (workspace slots, <= kSlots;
+                                // default GPU_MAX_HW_QUEUES - 1)
     int tune_gb = 0;            // RT_GB: phase-B chain workgroups in k_mix (0: 1.5625 per CU for a lone frame, 0.5 for batches)
     int tune_bq_cap = 1 << 30;  // RT_BQ_CAP: phase-B shadow queue slots (tests force the k_occlude spill path)
     int tune_bservice = 64;     // RT_BSERVICE: phase-B waves service finished walks once this many lanes are done
@@ -147,7 +148,7 @@ struct rt_scene {
     // chain-path workspaces: one device arena per concurrent-frame slot (grown
     // on demand, carved per frame); slot 0 serves single renders, slots
     // [0, kSlots) the concurrent frames of rt_render_cameras*.
-    static constexpr int kSlots = 4;
+    static constexpr int kSlots = 6;
     // An arena may be used from any caller stream: `last` is recorded after each
     // use on `last_stream`, and a use from another stream first waits on it.
     struct Arena {
@@ -306,6 +307,14 @@ int upload_scene(rt_scene* s, const rt_options* opts) {
     if (const char* e = std::getenv("RT_BREFILL")) s->tune_brefill = std::max(0, std::min(63, std::atoi(e)));
     if (const char* e = std::getenv("RT_OREFILL")) s->tune_orefill = std::max(0, std::min(63, std::atoi(e)));
     if (const char* e = std::getenv("RT_BATCH")) s->tune_batch = std::max(1, std::atoi(e));
+    // frame batches in flight: one HIP stream each beside the caller's; HIP multiplexes streams beyond
+    // GPU_MAX_HW_QUEUES hardware queues (4 by default) onto the same queues, which serialises them
+    // (C3: 4 slots on 4 queues 0.60 ms/frame, on 8 queues 0.51)
+    {
+        const char* q = std::getenv("GPU_MAX_HW_QUEUES");
+        const int hwq = q ? std::atoi(q) : 4;
+        s->tune_slots = std::max(1, std::min(rt_scene::kSlots, (hwq > 0 ? hwq : 4) - 1));
+    }
     if (const char* e = std::getenv("RT_SLOTS")) s->tune_slots = std::max(1, std::atoi(e));
     if (const char* e = std::getenv("RT_CHUNK_SAMPLES"))
         s->chunk_samples = std::max<size_t>(4096, std::min<size_t>(size_t(1) << 26, std::strtoull(e, nullptr, 10)));
@@ -997,14 +1006,15 @@ int render_cameras(rt_scene* s, const rt_camera* cams, int n, int aa, void* cons
     }
     if (!s->fork_ev) HIP_TRY(hipEventCreateWithFlags(&s->fork_ev, hipEventDisableTiming));
     HIP_TRY(hipEventRecord(s->fork_ev, stream));
-    const int used = std::min(n, rt_scene::kSlots);
+    const int nslot = std::max(1, std::min(s->tune_slots, rt_scene::kSlots));
+    const int used = std::min(n, nslot);
     for (int k = 0; k < used; ++k) {
         if (!s->slot_stream[k]) HIP_TRY(hipStreamCreateWithFlags(&s->slot_stream[k], hipStreamNonBlocking));
         if (!s->slot_done[k]) HIP_TRY(hipEventCreateWithFlags(&s->slot_done[k], hipEventDisableTiming));
         HIP_TRY(hipStreamWaitEvent(s->slot_stream[k], s->fork_ev, 0));
     }
     for (int i = 0; i < n; ++i) {
-        const int k = i % rt_scene::kSlots;
+        const int k = i % nslot;
         const int rc = render_frame(s, &cams[i], aa, rows_of(i), rank, nranks, outs_dev[i], s->slot_stream[k],
                                     flags, k);
         if (rc) return rc;
