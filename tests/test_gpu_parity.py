@@ -281,7 +281,7 @@ def test_render_frames_device_batch(nranks, nframes, gname, path, batch, goldens
         assert _stats(cnt) == tuple(nframes * x for x in _counters(c))
 
 
-@pytest.mark.parametrize("slots", ["3", "4"])
+@pytest.mark.parametrize("slots", ["3", "4", "6"])
 def test_render_frames_device_many_batches(slots, goldens, pkg, scene_dir, torch_cuda, monkeypatch):
     """70 frames of 8-rank shards: more frames than kMaxFrames (32) per batch and more batches than
     slots, so batches reuse slot workspaces while others run; every frame equals the golden."""
