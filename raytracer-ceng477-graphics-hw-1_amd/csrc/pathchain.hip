@@ -872,11 +872,12 @@ __global__ __launch_bounds__(kBlock, RT_MIX_WAVES) void k_mix(rtk::DevScene s, r
     else if (!p.exp_skip_occ) occlude_body<COUNT>(s, p, blockIdx.x - p.gb, gridDim.x - p.gb, p.sflatA, p.totals[0]);
 }
 
-// Phase B's shadow tasks.
+// Phase B's shadow tasks (which = 1), or phase A's (which = 0: p.split_occ, frame batches).
 template <bool COUNT>
-__global__ __launch_bounds__(kBlock, RT_OCC_WAVES_PER_EU) void k_occlude(rtk::DevScene s, PcParams p) {
+__global__ __launch_bounds__(kBlock, RT_OCC_WAVES_PER_EU) void k_occlude(rtk::DevScene s, PcParams p, int which) {
     block_init(s);
-    occlude_body<COUNT>(s, p, blockIdx.x, gridDim.x, p.sflatB, p.totals[2]);
+    if (which) occlude_body<COUNT>(s, p, blockIdx.x, gridDim.x, p.sflatB, p.totals[2]);
+    else occlude_body<COUNT>(s, p, blockIdx.x, gridDim.x, p.sflatA, p.totals[0]);
 }
 
 // ---------------------------------------------------------------------------
@@ -1553,12 +1554,21 @@ hipError_t launch_chain_chunk(const rtk::DevScene& s, const rtk::Eye& e, const P
     hipLaunchKernelGGL(k_pack_a, dim3(p.grid), blk, 0, st, p);
     PcParams q = p;
     if (!phase_b) q.gb = 0;
-    if (count) hipLaunchKernelGGL(k_mix<true>, dim3(q.gb + p.ogrid), blk, 0, st, s, e, q);
-    else hipLaunchKernelGGL(k_mix<false>, dim3(q.gb + p.ogrid), blk, 0, st, s, e, q);
+    // p.split_occ (frame batches): k_mix only walks the chains, A's shadow tasks go to k_occlude (5 waves
+    // per SIMD); otherwise k_mix's other workgroups walk them beside the chains
+    const bool split = p.split_occ && phase_b;
+    const int mgrid = split ? q.gb : q.gb + p.ogrid;
+    if (count) hipLaunchKernelGGL(k_mix<true>, dim3(mgrid), blk, 0, st, s, e, q);
+    else hipLaunchKernelGGL(k_mix<false>, dim3(mgrid), blk, 0, st, s, e, q);
+    if (split) {
+        if (count) hipLaunchKernelGGL(k_occlude<true>, dim3(p.occ_grid), blk, 0, st, s, p, 0);
+        else hipLaunchKernelGGL(k_occlude<false>, dim3(p.occ_grid), blk, 0, st, s, p, 0);
+    }
     if (phase_b) {
         hipLaunchKernelGGL(k_pack_b, dim3(p.gb), blk, 0, st, p);
-        if (count) hipLaunchKernelGGL(k_occlude<true>, dim3(p.ogrid), blk, 0, st, s, p);
-        else hipLaunchKernelGGL(k_occlude<false>, dim3(p.ogrid), blk, 0, st, s, p);
+        const int og = split ? p.occ_grid : p.ogrid;
+        if (count) hipLaunchKernelGGL(k_occlude<true>, dim3(og), blk, 0, st, s, p, 1);
+        else hipLaunchKernelGGL(k_occlude<false>, dim3(og), blk, 0, st, s, p, 1);
     }
     launch_finish(s, p, st);
     return hipGetLastError();

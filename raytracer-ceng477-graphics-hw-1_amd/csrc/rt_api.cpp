@@ -574,7 +574,10 @@ int render_chain(rt_scene* s, const rtk::Eye& eye, const rtk::FrameParams& f, bo
     // phase-B workgroups: a lone frame's deep chains are its critical path (1.5625 per CU best);
     // in frame batches other frames hide them and the shadow role wants the CUs (C3: 0.5 per CU
     // 0.550 ms/frame, 0.75 0.552, 1 0.554, 1.25 0.557, 1.5625 0.568)
-    const int gb_default = f.nframes > 1 ? s->num_cus / 2 : 25 * s->num_cus / 16;
+    // frame batches: A's shadow rays in their own 5-wave k_occlude launch (split_occ) and 1 phase-B
+    // workgroup per CU (6 slots in flight: 0.504-0.512 -> 0.495 ms/frame; 0.5 per CU 0.500, 2 0.4995)
+    const bool split_occ = f.nframes > 1 && (!std::getenv("RT_SPLIT_OCC") || std::atoi(std::getenv("RT_SPLIT_OCC")));
+    const int gb_default = f.nframes > 1 ? (split_occ ? s->num_cus : s->num_cus / 2) : 25 * s->num_cus / 16;
     const int gb = phase_b ? std::max(1, std::min(s->mix_grid - 1, s->tune_gb > 0 ? s->tune_gb : gb_default)) : 0;
     const int levels_a = std::min(kinline, std::max(s->dev.max_depth, 0)) + 1;
     const unsigned scapA = rtc::chain_block_scap((int)cap, G, levels_a, nl);
@@ -624,6 +627,8 @@ int render_chain(rt_scene* s, const rtk::Eye& eye, const rtk::FrameParams& f, bo
     p.kinline = phase_b ? kinline : 1 << 30;
     p.gb = gb;
     p.ogrid = phase_b ? std::max(1, s->mix_grid - gb) : s->mix_grid;
+    p.occ_grid = s->occl_grid;
+    p.split_occ = split_occ ? 1 : 0;
     p.refill = s->tune_refill >= 0 ? s->tune_refill : 0;
     p.service = s->tune_service >= 0 ? s->tune_service : 64;
     p.bservice = s->tune_bservice;
