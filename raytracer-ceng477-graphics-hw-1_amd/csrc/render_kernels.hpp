@@ -74,6 +74,7 @@ struct FrameParams {
     int slab_rows;        // rows in this rank's slab
     uint8_t* out;         // slab_rows * width * 3
     int out_k = 1, out_j = 0;   // chain path: sub-frame j of out_k interleaved sub-frames (pathchain.hip out_row)
+    int chunk_k = 1, chunk_j = 0;   // chain path: this call renders sample chunks j, j+k, ... of the frame
     unsigned long long* counters;  // 6 x u64 (RT_RENDER_COUNT)
     unsigned* trace;      // diagnostics (RT_TRACE): per output pixel {wave start, pixel end} wall clock, or null
     // chain path, frame batches (rt_render_frames_device): slab_rows = nframes * frame_rows virtual

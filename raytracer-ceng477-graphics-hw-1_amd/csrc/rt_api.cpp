@@ -509,7 +509,7 @@ int render_wavefront(rt_scene* s, const rtk::Eye& eye, const rtk::FrameParams& f
     p.R = s->ws.R; p.child = s->ws.child;
     p.qcount = s->ws.counts; p.scount = s->ws.counts + levels + 1;
     p.out = f.out; p.counters = f.counters;
-    for (int r0 = 0; r0 < li; r0 += chunk_rows) {
+    for (int r0 = f.chunk_j * chunk_rows; r0 < li; r0 += f.chunk_k * chunk_rows) {
         p.chunk_row0 = r0;
         p.chunk_rows = std::min(chunk_rows, li - r0);
         p.n0 = tiles_x * ((p.chunk_rows + 7) / 8) * 64;
@@ -553,6 +553,28 @@ int render_chain(rt_scene* s, const rtk::Eye& eye, const rtk::FrameParams& f, bo
     const size_t cap = units * unit_samples;
     if (cap * levels * nl >= (size_t)INT32_MAX) return fail(RT_ERR_LIMIT, "frame chunk too large for the chain path");
     const bool fused = s->path == rt_scene::kFused;
+    // A frame of several chunks (C5: 17 of 32 M samples): chunks on the workspace slots' streams
+    // (chunk j on slot j mod K), so one chunk's tail overlaps the next chunks' bulk.  Chunks write
+    // disjoint output rows.
+    const int nchunks = (li + chunk_rows - 1) / chunk_rows;
+    const int K = std::min({nchunks, s->tune_slots, rt_scene::kSlots});
+    if (f.chunk_k == 1 && K > 1 && !s->trace_file.size()) {
+        if (!s->fork_ev) HIP_TRY(hipEventCreateWithFlags(&s->fork_ev, hipEventDisableTiming));
+        HIP_TRY(hipEventRecord(s->fork_ev, st));
+        for (int j = 0; j < K; ++j) {
+            if (!s->slot_stream[j]) HIP_TRY(hipStreamCreateWithFlags(&s->slot_stream[j], hipStreamNonBlocking));
+            if (!s->slot_done[j]) HIP_TRY(hipEventCreateWithFlags(&s->slot_done[j], hipEventDisableTiming));
+            HIP_TRY(hipStreamWaitEvent(s->slot_stream[j], s->fork_ev, 0));
+            rtk::FrameParams g = f;
+            g.chunk_k = K;
+            g.chunk_j = j;
+            const int rc = render_chain(s, eye, g, count, s->slot_stream[j], j);
+            if (rc) return rc;
+            HIP_TRY(hipEventRecord(s->slot_done[j], s->slot_stream[j]));
+            HIP_TRY(hipStreamWaitEvent(st, s->slot_done[j], 0));
+        }
+        return RT_OK;
+    }
     if (s->chain_grid == 0) {
         int cb = 0, mb = 0, ob = 0, fb = 0;
         HIP_TRY(rtc::chain_occupancy(&cb, &mb, &ob));
@@ -661,7 +683,7 @@ int render_chain(rt_scene* s, const rtk::Eye& eye, const rtk::FrameParams& f, bo
     p.trace_blocks = std::max(s->mix_grid, s->occl_grid);
     const size_t trace_n = 2 * (cap + (size_t)p.trace_blocks) + 4 * cap;
     p.trace = trace_buffer(s, trace_n);
-    for (int r0 = 0; r0 < li; r0 += chunk_rows) {
+    for (int r0 = f.chunk_j * chunk_rows; r0 < li; r0 += f.chunk_k * chunk_rows) {
         p.chunk_row0 = r0;
         p.chunk_rows = std::min(chunk_rows, li - r0);
         p.n0 = tiles_x * ((p.chunk_rows + 7) / 8) * 64;
