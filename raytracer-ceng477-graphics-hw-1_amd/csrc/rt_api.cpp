@@ -126,7 +126,7 @@ struct rt_scene {
     // at 128, single-frame 1.18 -> 1.11-1.15 ms.  Continuations (the mug's clustered mirror chains)
     // gain from chunks only when other frames hide the tail: 128 gives batches 0.685 -> 0.650 ms/frame
     // but a lone frame 1.15 -> 1.36 ms, so a lone frame keeps fine interleaving.
-    int tune_tchunk = 0;        // RT_TCHUNK (0: 128 for frame batches, 8 for one frame)
+    int tune_tchunk = 0;        // RT_TCHUNK (0: 128 for frame batches, 1 for one frame)
     int tune_ochunk = 256;      // RT_OCHUNK
     int tune_packet = 1;        // RT_PACKET
     int tune_kinline = 1;       // RT_KINLINE: deepest level of phase A
@@ -660,7 +660,9 @@ int render_chain(rt_scene* s, const rtk::Eye& eye, const rtk::FrameParams& f, bo
     p.orefill = s->tune_orefill;
     p.brefill = s->tune_brefill;
     p.bprio = s->tune_bprio;
-    p.tchunk = s->tune_tchunk > 0 ? s->tune_tchunk : (f.nframes > 1 ? 128 : 8);
+    // continuations dealt one at a time round-robin for a lone frame (its deep chains spread over
+    // the phase-B workgroups: 1.12 -> 1.10 ms; 2: 1.11-1.14, 4: 1.12-1.13), in chunks of 128 in batches
+    p.tchunk = s->tune_tchunk > 0 ? s->tune_tchunk : (f.nframes > 1 ? 128 : 1);
     p.ochunk = s->tune_ochunk;
     p.packet = s->tune_packet && s->bvh.max_stack <= dl::kMaxStack;
     p.exp_skip_occ = std::getenv("RT_EXP_SKIP_OCC") ? 1 : 0;
