@@ -199,6 +199,8 @@ __device__ __forceinline__ unsigned block_sample(unsigned v, unsigned G, unsigne
 // 256-sample units, continuation and shadow tasks by index j -> j mod G.
 // ---------------------------------------------------------------------------
 __shared__ unsigned g_ccnt;    // block-local continuation count
+__shared__ unsigned g_uid[kDynUnits];   // dynamic phase-A units: the workgroup's k-th unit (kUidUnset: not yet taken)
+constexpr unsigned kUidUnset = ~0u, kUidNone = ~0u - 1u;
 
 struct PhaseOut {              // where a chain phase writes its tasks
     unsigned* sq;              // shadow tasks, region blk at sq + blk * scap
@@ -554,6 +556,14 @@ __device__ void chain_body(const rtk::DevScene& s, const rtk::Eye& e, const PcPa
     unsigned nb;
     if (CONT) nb = chunk_count(p.totals[1], G, blk, (unsigned)p.tchunk);
     else nb = group_samples((unsigned)p.n0, G, blk);
+    // dynamic units (phase A, p.dyn_units > 0): the workgroup's k-th 256-sample unit is not
+    // blk + k*G but the next one of a launch-wide counter (p.totals[3], zeroed before the launch),
+    // taken when the workgroup reaches it, so a workgroup whose samples were cheap takes more of
+    // them and no workgroup waits out a fixed share.  At most p.dyn_units units per workgroup
+    // (its shadow and continuation queues are sized for that many).
+    const bool dyn = !CONT && p.dyn_units > 0;
+    const unsigned units = ((unsigned)p.n0 + 255u) / 256u;
+    if (dyn) nb = (unsigned)p.dyn_units * 256u;
     unsigned* const sq = o.sq + (size_t)blk * o.scap;
     int st = kIdle;
     bool exhausted = nb == 0;
@@ -652,9 +662,26 @@ __device__ void chain_body(const rtk::DevScene& s, const rtk::Eye& e, const PcPa
                 stat.refill(idle);
                 const unsigned base = wave_grab_lds(&g_head, idle);
                 if (base + (unsigned)__popcll(idle) >= nb) exhausted = true;
+                unsigned uid = 0;           // dyn: the unit of this lane's sample
+                if (dyn) {
+                    // the wave whose grab holds a unit's first sample takes that unit from the counter,
+                    // once the previous unit is taken: a workgroup's units come in order, so a unit
+                    // beyond the counter's end means no later one either
+                    const unsigned jf = (base + 255u) >> 8;
+                    if (lane_id() == 0 && jf * 256u < base + (unsigned)__popcll(idle) && jf < (unsigned)p.dyn_units) {
+                        if (jf > 0)
+                            while (*(volatile unsigned*)&g_uid[jf - 1] == kUidUnset) __builtin_amdgcn_s_sleep(1);
+                        const unsigned u = atomicAdd(&p.totals[3], 1u);
+                        *(volatile unsigned*)&g_uid[jf] = u < units ? u : kUidNone;
+                    }
+                    const unsigned v = base + lane_rank(idle);
+                    if (st == kIdle && v < nb)
+                        while ((uid = *(volatile unsigned*)&g_uid[v >> 8]) == kUidUnset) __builtin_amdgcn_s_sleep(1);
+                    if (__any(st == kIdle && v < nb && uid == kUidNone)) exhausted = true;
+                }
                 if (st == kIdle) {
                     const unsigned v = base + lane_rank(idle);
-                    if (v < nb) {
+                    if (v < nb && uid != kUidNone) {
                         if (CONT) {
                             const unsigned j = chunk_task(v, G, blk, (unsigned)p.tchunk);
                             const unsigned lvp = p.cflat[j];
@@ -665,7 +692,7 @@ __device__ void chain_body(const rtk::DevScene& s, const rtk::Eye& e, const PcPa
                             nrefl++;
                             st = walk_begin<COUNT>(s, r, wk, w) ? kTrav : kDone;
                         } else {
-                            const unsigned idx = (blk + (v >> 8) * G) * 256u + (v & 255u);
+                            const unsigned idx = (dyn ? uid : blk + (v >> 8) * G) * 256u + (v & 255u);
                             if (slab_sample_ray(e, p, idx, &r)) {
                                 path = idx;
                                 k = 0;
@@ -812,6 +839,7 @@ __device__ __forceinline__ PhaseOut phase_b(const PcParams& p) {
 template <bool COUNT>
 __global__ __launch_bounds__(kBlock, RT_WAVES_PER_EU) void k_chain(rtk::DevScene s, rtk::Eye e, PcParams p) {
     if (threadIdx.x == 0) g_ccnt = 0;
+    if (threadIdx.x < kDynUnits) g_uid[threadIdx.x] = kUidUnset;
     block_init(s);
     chain_body<COUNT, false>(s, e, p, blockIdx.x, gridDim.x, phase_a(p));
 }
@@ -1539,16 +1567,23 @@ extern "C" int rt_debug_step_stats(unsigned long long* out, int reset) {
     return RT_STEP_STATS;
 }
 
-unsigned chain_block_scap(int n0, int grid, int levels, int nlights) {
+unsigned chain_block_units(int n0, int grid) {
     const unsigned units = ((unsigned)n0 + 255u) / 256u;
-    const unsigned per_block = (units + (unsigned)grid - 1u) / (unsigned)grid;
-    return per_block * 256u * (unsigned)levels * (unsigned)nlights;
+    return (units + (unsigned)grid - 1u) / (unsigned)grid;
+}
+
+unsigned chain_block_scap(int n0, int grid, int levels, int nlights) {
+    return chain_block_units(n0, grid) * 256u * (unsigned)levels * (unsigned)nlights;
 }
 
 hipError_t launch_chain_chunk(const rtk::DevScene& s, const rtk::Eye& e, const PcParams& p, bool count,
                               hipStream_t st) {
     const dim3 blk(kBlock);
     const bool phase_b = p.kinline < s.max_depth;     // any continuation possible
+    if (p.dyn_units) {
+        const hipError_t me = hipMemsetAsync(p.totals + 3, 0, sizeof(unsigned), st);   // dynamic unit counter
+        if (me != hipSuccess) return me;
+    }
     if (count) hipLaunchKernelGGL(k_chain<true>, dim3(p.grid), blk, 0, st, s, e, p);
     else hipLaunchKernelGGL(k_chain<false>, dim3(p.grid), blk, 0, st, s, e, p);
     hipLaunchKernelGGL(k_pack_a, dim3(p.grid), blk, 0, st, p);

@@ -61,7 +61,7 @@ struct PcParams {
     unsigned scapB;
     unsigned* scntB;  // [gb]
     unsigned* sflatB; // B's shadow tasks packed (k_pack_b), totals[2] of them
-    unsigned* totals; // [3]
+    unsigned* totals; // [4]: packed task counts (3), phase-A unit counter
     int kinline;      // deepest level phase A walks (>= max_depth: no phase B)
     int gb;           // k_mix workgroups in the chain role (the other p.ogrid ones occlude A's tasks)
     int tchunk;       // continuation tasks (phase B) are dealt to workgroups in chunks of this many
@@ -82,6 +82,8 @@ struct PcParams {
     int btail;        // phase-B chains once no continuation is left to take: service at this many done lanes
     int bq_cap;       // phase-B workgroup shadow queue slots in use (<= kBq; 0: every task to k_occlude)
     int spread;       // tiles interleaved per wave within a 256-sample unit (1, 2 or 4)
+    int dyn_units;    // > 0: phase-A waves take 256-sample units from a launch-wide counter (totals[3]),
+                      // at most this many per workgroup; 0: static per-workgroup interleave
     uint8_t* out;
     // Frame batch: the slab's rows are nframes frames of frame_rows rows each (slab_rows = nframes *
     // frame_rows); frame f's samples use eyes[f] and its pixels go to fouts[f] (nframes > 1 only).
@@ -103,6 +105,10 @@ struct PcParams {
 // Worst-case task-queue slots per workgroup: every sample of the workgroup
 // recording `levels` levels, one task per light.
 unsigned chain_block_scap(int n0, int grid, int levels, int nlights);
+// A workgroup's static share of 256-sample units (k_chain with PcParams::dyn_units = 0).
+unsigned chain_block_units(int n0, int grid);
+// Dynamic phase-A units: most units one k_chain workgroup may take (its LDS unit table).
+constexpr int kDynUnits = 128;
 
 // Resident workgroups per CU of the (non-counting) k_chain / k_mix / k_occlude:
 // the persistent grids are sized so every workgroup starts at t = 0 (a late-

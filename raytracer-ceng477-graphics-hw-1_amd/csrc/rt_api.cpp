@@ -141,6 +141,7 @@ struct rt_scene {
     int tune_bq_cap = 1 << 30;  // RT_BQ_CAP: phase-B shadow queue slots (tests force the k_occlude spill path)
     int tune_bservice = 64;     // RT_BSERVICE: phase-B waves service finished walks once this many lanes are done
     int tune_btail = 64;        // RT_BTAIL: the same once the continuations are exhausted (1: 1.24, 4: 1.18, 16: 1.15, 64: 1.14 ms)
+    int tune_dyn = 1;           // RT_DYN_UNITS: phase-A waves take sample units from a launch-wide counter
     int tune_split = 1;         // RT_SPLIT: a frame runs as this many concurrent interleaved sub-frames (2: +8%, 3: +18% on C3)
     std::string trace_file;     // RT_TRACE: dump per-sample wall-clock timings after each render (diagnostics)
     unsigned* d_trace = nullptr;
@@ -324,6 +325,7 @@ int upload_scene(rt_scene* s, const rt_options* opts) {
     if (const char* e = std::getenv("RT_BSERVICE")) s->tune_bservice = std::max(1, std::min(64, std::atoi(e)));
     if (const char* e = std::getenv("RT_BTAIL")) s->tune_btail = std::max(1, std::min(64, std::atoi(e)));
     if (const char* e = std::getenv("RT_SPLIT")) s->tune_split = std::max(1, std::atoi(e));
+    if (const char* e = std::getenv("RT_DYN_UNITS")) s->tune_dyn = std::atoi(e) != 0;
     if (const char* e = std::getenv("RT_PROD")) s->tune_producers = std::max(1, std::min(4, std::atoi(e)));
     if (const char* e = std::getenv("RT_CREFILL")) s->tune_crefill = std::max(0, std::min(63, std::atoi(e)));
     if (const char* e = std::getenv("RT_TRACE")) s->trace_file = e;
@@ -602,8 +604,14 @@ int render_chain(rt_scene* s, const rtk::Eye& eye, const rtk::FrameParams& f, bo
     const int gb_default = f.nframes > 1 ? (split_occ ? s->num_cus : s->num_cus / 2) : 25 * s->num_cus / 16;
     const int gb = phase_b ? std::max(1, std::min(s->mix_grid - 1, s->tune_gb > 0 ? s->tune_gb : gb_default)) : 0;
     const int levels_a = std::min(kinline, std::max(s->dev.max_depth, 0)) + 1;
-    const unsigned scapA = rtc::chain_block_scap((int)cap, G, levels_a, nl);
-    const unsigned ccapA = rtc::chain_block_scap((int)cap, G, 1, 1);
+    // dynamic phase-A units: a workgroup may take up to twice its static share (at most
+    // rtc::kDynUnits), and its queues are sized for that
+    const unsigned share = rtc::chain_block_units((int)cap, G);
+    const unsigned dyn_units = s->tune_dyn && share <= (unsigned)rtc::kDynUnits
+                                   ? std::min(2u * share, (unsigned)rtc::kDynUnits) : 0u;
+    const unsigned units_a = dyn_units ? dyn_units : share;
+    const unsigned scapA = units_a * 256u * (unsigned)(levels_a * nl);
+    const unsigned ccapA = units_a * 256u;
     const unsigned scapB = phase_b ? (unsigned)(((cap + gb - 1) / gb) * (size_t)(levels - levels_a) * nl) : 0u;
     const unsigned wq_cap = fused ? rtc::fused_wave_qcap((int)cap, G, levels, nl) : 0u;
 
@@ -668,6 +676,7 @@ int render_chain(rt_scene* s, const rtk::Eye& eye, const rtk::FrameParams& f, bo
     p.exp_skip_occ = std::getenv("RT_EXP_SKIP_OCC") ? 1 : 0;
     p.shade_split = std::getenv("RT_SHADE_SPLIT") ? std::atoi(std::getenv("RT_SHADE_SPLIT")) : 0;
     p.spread = s->tune_spread;
+    p.dyn_units = (int)dyn_units;
     p.crefill = s->tune_crefill;
     p.wq = static_cast<unsigned*>(at(o_wq));
     p.wq_cap = wq_cap;
