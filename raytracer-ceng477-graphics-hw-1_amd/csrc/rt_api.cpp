@@ -99,6 +99,7 @@ struct rt_scene {
     dl::Light* d_lights = nullptr;
     unsigned long long* d_counters = nullptr;
     unsigned* d_err = nullptr;                 // device error word (DevScene.err)
+    unsigned* h_err = nullptr;                 // pinned host copy of it (rt_render reads it with the frame)
     uint8_t* d_out = nullptr;
     size_t out_cap = 0;
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
@@ -198,6 +199,7 @@ struct rt_scene {
         (void)hipFree(d_pairs); (void)hipFree(d_leafbig); (void)hipFree(d_spairs); (void)hipFree(d_swnodes); (void)hipFree(d_wnodes); (void)hipFree(d_lrec);
         (void)hipFree(d_nodes); (void)hipFree(d_prims); (void)hipFree(d_tri); (void)hipFree(d_mats); (void)hipFree(d_lights);
         (void)hipFree(d_counters); (void)hipFree(d_err); (void)hipFree(d_out); (void)hipFree(d_trace);
+        if (h_err) (void)hipHostFree(h_err);
         if (ev0) (void)hipEventDestroy(ev0);
         if (ev1) (void)hipEventDestroy(ev1);
     }
@@ -1264,9 +1266,16 @@ int rt_render(rt_scene* s, const rt_camera* cam, int aa, uint8_t* out_rgb, rt_st
     rc = rt_render_device(s, cam, aa, cam->image_height, 0, 1, s->d_out, nullptr, count ? RT_RENDER_COUNT : 0);
     if (rc) return rc;
     HIP_TRY(hipEventRecord(s->ev1, nullptr));
+    // the error word travels with the frame (one synchronisation instead of two)
+    if (!s->h_err) HIP_TRY(hipHostMalloc(reinterpret_cast<void**>(&s->h_err), sizeof(unsigned)));
+    HIP_TRY(hipMemcpyAsync(s->h_err, s->d_err, sizeof(unsigned), hipMemcpyDeviceToHost, nullptr));
     HIP_TRY(hipMemcpy(out_rgb, s->d_out, bytes, hipMemcpyDeviceToHost));
     HIP_TRY(hipEventSynchronize(s->ev1));
-    if ((rc = check_device_error(s))) return rc;
+    if (*s->h_err) {
+        *s->h_err = 0;
+        HIP_TRY(hipMemset(s->d_err, 0, sizeof(unsigned)));
+        return fail(RT_ERR_LIMIT, "a BVH walk exceeded its step bound (walk_cap) and was cut off; the frame is invalid");
+    }
     if (stats) {
         rc = rt_counters_read(s, stats);
         if (rc) return rc;
