@@ -524,7 +524,7 @@ int render_wavefront(rt_scene* s, const rtk::Eye& eye, const rtk::FrameParams& f
 
 // Chain path: chunks of whole 8*aa-row groups, workspace sized for the worst
 // case (every sample recording every level) so no queue can overflow.
-constexpr size_t kChainBudgetBytes = size_t(24) << 30;   // per workspace slot (4 slots: 96 of 288 GB HBM)
+constexpr size_t kChainBudgetBytes = size_t(24) << 30;   // per workspace slot (6 slots: at most 144 of 288 GB HBM)
 
 // Bump layout of the chain-path workspace (one device arena, grown on demand).
 struct ArenaLayout {
