@@ -1496,7 +1496,7 @@ __global__ __launch_bounds__(kBlock) void k_walk_timing(rtk::DevScene s, const f
 // lane per record) then k_compose (p.shade_split).
 void launch_finish(const rtk::DevScene& s, const PcParams& p, hipStream_t st) {
     const int npix = (p.chunk_rows / p.aa) * p.width;
-    const dim3 pgrid(std::max(1, (npix + kBlock - 1) / kBlock));
+    const dim3 pgrid(std::max(1, std::min((npix + kBlock - 1) / kBlock, p.fin_grid > 0 ? p.fin_grid : INT32_MAX)));
     if (!p.shade_split) {
         if (s.nmats <= kFinishMats && s.nlights <= kFinishLights)
             hipLaunchKernelGGL(k_finish, pgrid, dim3(kBlock), 0, st, s, p);

@@ -73,6 +73,7 @@ struct PcParams {
     int ogrid;        // k_occlude persistent grid
     int split_occ;    // 1: A's shadow tasks in their own k_occlude launch (occ_grid workgroups), not in k_mix
     int occ_grid;     // resident k_occlude workgroups
+    int fin_grid;     // k_finish workgroups at most (0: a lane per output pixel), a grid-stride loop beyond
     int refill;       // a wave refills once <= refill of its lanes are still walking
     int orefill;      // the same for the shadow (any-hit) walks
     int brefill;      // the same for phase-B chains

@@ -138,6 +138,8 @@ struct rt_scene {
     int tune_batch = 32;        // RT_BATCH: frames per batched launch (rt_render_frames/cameras; 1 = off)
     int tune_slots = 3;         // RT_SLOTS: frame batches in flight together (workspace slots, <= kSlots;
                                 // default GPU_MAX_HW_QUEUES - 1)
+    int tune_fgrid = 0;         // RT_FGRID: k_finish workgroups at most (0: 8 per CU; its waves are dispatch-bound
+                                // at a lane per pixel: 0.515 -> 0.49 ms per batched frame)
     int tune_gb = 0;            // RT_GB: phase-B chain workgroups in k_mix (0: 1.5625 per CU for a lone frame, 0.5 for batches)
     int tune_bq_cap = 1 << 30;  // RT_BQ_CAP: phase-B shadow queue slots (tests force the k_occlude spill path)
     int tune_bservice = 64;     // RT_BSERVICE: phase-B waves service finished walks once this many lanes are done
@@ -323,6 +325,7 @@ int upload_scene(rt_scene* s, const rt_options* opts) {
         s->chunk_samples = std::max<size_t>(4096, std::min<size_t>(size_t(1) << 26, std::strtoull(e, nullptr, 10)));
     if (const char* e = std::getenv("RT_KINLINE")) s->tune_kinline = std::max(0, std::atoi(e));
     if (const char* e = std::getenv("RT_GB")) s->tune_gb = std::max(0, std::atoi(e));
+    if (const char* e = std::getenv("RT_FGRID")) s->tune_fgrid = std::max(0, std::atoi(e));
     if (const char* e = std::getenv("RT_BQ_CAP")) s->tune_bq_cap = std::max(0, std::atoi(e));
     if (const char* e = std::getenv("RT_BSERVICE")) s->tune_bservice = std::max(1, std::min(64, std::atoi(e)));
     if (const char* e = std::getenv("RT_BTAIL")) s->tune_btail = std::max(1, std::min(64, std::atoi(e)));
@@ -642,7 +645,7 @@ int render_chain(rt_scene* s, const rtk::Eye& eye, const rtk::FrameParams& f, bo
         arena.bytes = L.off;
     }
     auto at = [&](size_t o) { return static_cast<void*>(arena.p + o); };
-    rtc::PcParams p;
+    rtc::PcParams p{};
     p.width = f.width; p.height = f.height; p.aa = f.aa; p.stripe_rows = f.stripe_rows;
     p.rank = f.rank; p.nranks = f.nranks; p.slab_rows = f.slab_rows;
     p.wi = wi; p.tiles_x = tiles_x; p.cap = (int)cap; p.levels = levels; p.nlights = s->dev.nlights;
@@ -660,6 +663,7 @@ int render_chain(rt_scene* s, const rtk::Eye& eye, const rtk::FrameParams& f, bo
     p.gb = gb;
     p.ogrid = phase_b ? std::max(1, s->mix_grid - gb) : s->mix_grid;
     p.occ_grid = s->occl_grid;
+    p.fin_grid = s->tune_fgrid > 0 ? s->tune_fgrid : 8 * s->num_cus;
     p.split_occ = split_occ ? 1 : 0;
     p.refill = s->tune_refill >= 0 ? s->tune_refill : 0;
     p.service = s->tune_service >= 0 ? s->tune_service : 64;
