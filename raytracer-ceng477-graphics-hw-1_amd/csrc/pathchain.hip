@@ -626,12 +626,13 @@ __device__ void chain_body(const rtk::DevScene& s, const rtk::Eye& e, const PcPa
                 }
             }
             bool ends = true;
+            const int cbit = CONT ? kPathCont : 0;
             if (!hit) {                                                          // :442-449
-                p.pinfo[path] = k | ((k == 0 ? kEndBg : kEndZero) << 8);
+                p.pinfo[path] = k | ((k == 0 ? kEndBg : kEndZero) << 8) | cbit;
             } else if (!s.mats[mat - 1].is_mirror) {
-                p.pinfo[path] = (k + 1) | (kEndLast << 8);
+                p.pinfo[path] = (k + 1) | (kEndLast << 8) | cbit;
             } else if (k >= s.max_depth) {        // child beyond MaxRecursionDepth: 0 (:387-389)
-                p.pinfo[path] = (k + 1) | (kEndZero << 8);
+                p.pinfo[path] = (k + 1) | (kEndZero << 8) | cbit;
             } else {
                 ends = false;
             }
@@ -640,6 +641,7 @@ __device__ void chain_body(const rtk::DevScene& s, const rtk::Eye& e, const PcPa
             if (handoff) {
                 const unsigned base = wave_grab_lds(&g_ccnt, cm);
                 o.cq[(size_t)blk * o.ccap + base + lane_rank(cm)] = (unsigned)((size_t)k * p.cap + path);
+                p.pinfo[path] = kPathCont;        // continued in phase B (finish_pixels' order)
             }
             if (ends || handoff) {
                 st = kIdle;
@@ -1183,7 +1185,7 @@ __global__ __launch_bounds__(kBlock) void k_shade(rtk::DevScene s, PcParams p) {
 // over the shaded records.
 __device__ __forceinline__ V path_color(const rtk::DevScene& s, const PcParams& p, unsigned path) {
     const int info = p.pinfo[path];
-    const int nlev = info & 0xff, kind = info >> 8;
+    const int nlev = info & 0xff, kind = (info >> 8) & 0xff;
     V c = kind == kEndBg ? V{s.bgx, s.bgy, s.bgz} : V{0.0f, 0.0f, 0.0f};
     int k = nlev - 1;
     if (kind == kEndLast) {
@@ -1337,7 +1339,7 @@ __device__ __forceinline__ uint32_t occ_bits(const PcParams& p, const OccRaw& o,
 template <bool LDS>
 __device__ __forceinline__ V path_shade_fold(const rtk::DevScene& s, const PcParams& p, unsigned path) {
     const int info = p.pinfo[path];
-    const int nlev = info & 0xff, kind = info >> 8;
+    const int nlev = info & 0xff, kind = (info >> 8) & 0xff;
     V c = kind == kEndBg ? V{s.bgx, s.bgy, s.bgz} : V{0.0f, 0.0f, 0.0f};
     if (nlev == 0) return c;
     const int nl = s.nlights;
@@ -1368,30 +1370,63 @@ __device__ __forceinline__ V path_shade_fold(const rtk::DevScene& s, const PcPar
     return c;
 }
 
+// One output pixel (rr, ocol) of the chunk: its F x F samples shaded, folded, quantised and averaged.
+template <bool LDS>
+__device__ __forceinline__ void finish_pixel(const rtk::DevScene& s, const PcParams& p, int rr, int ocol) {
+    const int F = p.aa;
+    const int lr = p.chunk_row0 / p.aa + rr;
+    if (lr >= p.slab_rows) return;
+    int lf = lr;
+    const int fr = batch_frame(p, &lf);
+    const int stripe = lf / p.stripe_rows;
+    const int g = (stripe * p.nranks + p.rank) * p.stripe_rows + (lf - stripe * p.stripe_rows);
+    if (g >= p.height) return;
+    uint32_t sr = 0, sg = 0, sb = 0;
+    for (int k = 0; k < F; ++k)
+        for (int l = 0; l < F; ++l) {
+            const V c = path_shade_fold<LDS>(s, p, slab_slot(p.tiles_x, ocol * F + l, rr * F + k));
+            sr += quantise(c.x); sg += quantise(c.y); sb += quantise(c.z);
+        }
+    const uint32_t ff = (uint32_t)(F * F);
+    uint8_t* o = (p.nframes > 1 ? p.fouts[fr] : p.out) + ((size_t)out_row(p, lf) * p.width + ocol) * 3;
+    o[0] = (uint8_t)(sr / ff); o[1] = (uint8_t)(sg / ff); o[2] = (uint8_t)(sb / ff);
+}
+
+// p.fin_cont (chain path): the pixels of the paths continued in phase B first (cflat, totals[1] of
+// them; each pixel once, by the lane holding its first continued sample), so their long folds
+// overlap the rest; then every pixel without a continued sample (pinfo's kPathCont bit)
 template <bool LDS>
 __device__ __forceinline__ void finish_pixels(const rtk::DevScene& s, const PcParams& p) {
-    const int lr0 = p.chunk_row0 / p.aa;
-    const int nrows = p.chunk_rows / p.aa;
-    const int npix = nrows * p.width;
     const int F = p.aa;
-    for (int q = blockIdx.x * kBlock + threadIdx.x; q < npix; q += gridDim.x * kBlock) {
+    const unsigned gtid = blockIdx.x * kBlock + threadIdx.x, gstride = gridDim.x * kBlock;
+    if (p.fin_cont) {
+        const unsigned n = p.totals[1];
+        for (unsigned j = gtid; j < n; j += gstride) {
+            const unsigned path = p.cflat[j] % (unsigned)p.cap;
+            const unsigned tile = path >> 6, lane = path & 63u;
+            const int ix = (int)(tile % (unsigned)p.tiles_x) * 8 + (int)(lane & 7u);
+            const int iyc = (int)(tile / (unsigned)p.tiles_x) * 8 + (int)(lane >> 3);
+            const int ocol = ix / F, rr = iyc / F;
+            unsigned first = path;
+            for (int k = F - 1; k >= 0; --k)
+                for (int l = F - 1; l >= 0; --l) {
+                    const unsigned sl = slab_slot(p.tiles_x, ocol * F + l, rr * F + k);
+                    if (p.pinfo[sl] & kPathCont) first = sl;
+                }
+            if (first == path) finish_pixel<LDS>(s, p, rr, ocol);
+        }
+    }
+    const int npix = (p.chunk_rows / p.aa) * p.width;
+    for (int q = (int)gtid; q < npix; q += (int)gstride) {
         const int rr = q / p.width, ocol = q - rr * p.width;
-        const int lr = lr0 + rr;
-        if (lr >= p.slab_rows) continue;
-        int lf = lr;
-        const int fr = batch_frame(p, &lf);
-        const int stripe = lf / p.stripe_rows;
-        const int g = (stripe * p.nranks + p.rank) * p.stripe_rows + (lf - stripe * p.stripe_rows);
-        if (g >= p.height) continue;
-        uint32_t sr = 0, sg = 0, sb = 0;
-        for (int k = 0; k < F; ++k)
-            for (int l = 0; l < F; ++l) {
-                const V c = path_shade_fold<LDS>(s, p, slab_slot(p.tiles_x, ocol * F + l, rr * F + k));
-                sr += quantise(c.x); sg += quantise(c.y); sb += quantise(c.z);
-            }
-        const uint32_t ff = (uint32_t)(F * F);
-        uint8_t* o = (p.nframes > 1 ? p.fouts[fr] : p.out) + ((size_t)out_row(p, lf) * p.width + ocol) * 3;
-        o[0] = (uint8_t)(sr / ff); o[1] = (uint8_t)(sg / ff); o[2] = (uint8_t)(sb / ff);
+        if (p.fin_cont) {
+            bool cont = false;
+            for (int k = 0; k < F; ++k)
+                for (int l = 0; l < F; ++l)
+                    cont |= (p.pinfo[slab_slot(p.tiles_x, ocol * F + l, rr * F + k)] & kPathCont) != 0;
+            if (cont) continue;
+        }
+        finish_pixel<LDS>(s, p, rr, ocol);
     }
 }
 
@@ -1605,7 +1640,11 @@ hipError_t launch_chain_chunk(const rtk::DevScene& s, const rtk::Eye& e, const P
         if (count) hipLaunchKernelGGL(k_occlude<true>, dim3(og), blk, 0, st, s, p, 1);
         else hipLaunchKernelGGL(k_occlude<false>, dim3(og), blk, 0, st, s, p, 1);
     }
-    launch_finish(s, p, st);
+    // continued pixels first only where they are few and deep (one sample per pixel): with 16 samples
+    // a pixel (C5: 130 vs 106 ms) and without phase B (C2: +5 %) the extra pinfo reads cost more
+    PcParams f = p;
+    f.fin_cont = phase_b && p.aa == 1;
+    launch_finish(s, f, st);
     return hipGetLastError();
 }
 

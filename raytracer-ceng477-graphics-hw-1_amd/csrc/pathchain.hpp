@@ -37,6 +37,8 @@ enum PathKind : int {
     kEndZero = 1,   // deepest ray missed at depth > 0, or beyond MaxRecursionDepth: black
     kEndLast = 2,   // last recorded hit is not a mirror: its own clamp(L)
 };
+// pinfo bit of a path continued in phase B (set by phase A's hand-off, kept by phase B's end)
+constexpr int kPathCont = 1 << 16;
 
 struct PcParams {
     int width, height, aa, stripe_rows, rank, nranks, slab_rows;
@@ -74,6 +76,7 @@ struct PcParams {
     int split_occ;    // 1: A's shadow tasks in their own k_occlude launch (occ_grid workgroups), not in k_mix
     int occ_grid;     // resident k_occlude workgroups
     int fin_grid;     // k_finish workgroups at most (0: a lane per output pixel), a grid-stride loop beyond
+    int fin_cont;     // k_finish: the continued paths' pixels first (chain path: cflat, totals[1], kPathCont)
     int refill;       // a wave refills once <= refill of its lanes are still walking
     int orefill;      // the same for the shadow (any-hit) walks
     int brefill;      // the same for phase-B chains
