@@ -41,7 +41,11 @@ constexpr int kBlock = 256;
 #define RT_FINISH_PREFETCH 1   // k_finish: next level's record in flight while shading
 #endif
 #ifndef RT_FINISH_WAVES
-#define RT_FINISH_WAVES 1
+#define RT_FINISH_WAVES 4     // k_finish: 128 VGPRs, 4 waves/SIMD, no spills (unbounded: 129, 3 waves): C3 batches
+                              // 0.507-0.508 -> 0.502-0.504 ms/frame; 5 (spills) 0.532, 6 0.559
+#endif
+#ifndef RT_FINISH_ANY_WAVES
+#define RT_FINISH_ANY_WAVES 1 // k_finish_any (large scenes): at 4 waves it spills a VGPR
 #endif
 #ifndef RT_OCC_WAVES_PER_EU
 #define RT_OCC_WAVES_PER_EU 5     // k_mix / k_occlude (the any-hit bulk); 5/5 measured best of 4..6
@@ -1443,7 +1447,7 @@ __global__ __launch_bounds__(kBlock, RT_FINISH_WAVES) void k_finish(rtk::DevScen
     __syncthreads();
     finish_pixels<true>(s, p);
 }
-__global__ __launch_bounds__(kBlock, RT_FINISH_WAVES) void k_finish_any(rtk::DevScene s, PcParams p) {
+__global__ __launch_bounds__(kBlock, RT_FINISH_ANY_WAVES) void k_finish_any(rtk::DevScene s, PcParams p) {
     finish_pixels<false>(s, p);
 }
 
