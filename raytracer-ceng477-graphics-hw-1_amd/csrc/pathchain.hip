@@ -548,6 +548,23 @@ __device__ uint32_t bq_consume(const rtk::DevScene& s, const PcParams& p, WalkSt
     return n;
 }
 
+// The u-th unit taken -> the unit id.  The slab's rows of units (tiles_x / 4 units each) are cut
+// into super-rows of ublk_h tile rows (< 0: one frame of the batch), each walked in column blocks
+// ublk_w units wide, so the units in flight (a launch-wide counter: the whole GPU on them at once)
+// cover a column of the image instead of a full-width band (C3, 256-px columns a frame high: ~1 %
+// per batched frame, ~2 % one frame).  Identity when ublk_h == 0 or the units do not tile the rows.
+__device__ __forceinline__ unsigned unit_order(const PcParams& p, unsigned u, unsigned units) {
+    const unsigned upr = (unsigned)p.tiles_x / 4u;
+    if (p.ublk_h == 0 || (p.tiles_x & 3) || units % upr) return u;
+    const unsigned rows = units / upr, bw = (unsigned)p.ublk_w;
+    const unsigned bh = p.ublk_h > 0 ? (unsigned)p.ublk_h : (rows % (unsigned)p.nframes ? rows : rows / (unsigned)p.nframes);
+    const unsigned r0 = u / (bh * upr) * bh, h = min(bh, rows - r0);
+    const unsigned i = u - r0 * upr;            // index within the super-row (h rows x upr units)
+    const unsigned c0 = i / (h * bw) * bw, w = min(bw, upr - c0);
+    const unsigned l = i - c0 * h;
+    return (r0 + l / w) * upr + c0 + l % w;
+}
+
 // closest-hit chains of one phase (raytracer.cpp:385-439 minus the shading):
 // record each hit, queue its shadow tasks, follow (or hand on) mirrors.
 template <bool COUNT, bool CONT>
@@ -678,7 +695,7 @@ __device__ void chain_body(const rtk::DevScene& s, const rtk::Eye& e, const PcPa
                         if (jf > 0)
                             while (*(volatile unsigned*)&g_uid[jf - 1] == kUidUnset) __builtin_amdgcn_s_sleep(1);
                         const unsigned u = atomicAdd(&p.totals[3], 1u);
-                        *(volatile unsigned*)&g_uid[jf] = u < units ? u : kUidNone;
+                        *(volatile unsigned*)&g_uid[jf] = u < units ? unit_order(p, u, units) : kUidNone;
                     }
                     const unsigned v = base + lane_rank(idle);
                     if (st == kIdle && v < nb)

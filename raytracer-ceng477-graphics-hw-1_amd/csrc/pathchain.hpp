@@ -88,6 +88,8 @@ struct PcParams {
     int spread;       // tiles interleaved per wave within a 256-sample unit (1, 2 or 4)
     int dyn_units;    // > 0: phase-A waves take 256-sample units from a launch-wide counter (totals[3]),
                       // at most this many per workgroup; 0: static per-workgroup interleave
+    int ublk_h, ublk_w; // dynamic units taken in column blocks of ublk_h tile rows (< 0: a frame; 0: off)
+                        // x ublk_w units (unit_order)
     uint8_t* out;
     // Frame batch: the slab's rows are nframes frames of frame_rows rows each (slab_rows = nframes *
     // frame_rows); frame f's samples use eyes[f] and its pixels go to fouts[f] (nframes > 1 only).

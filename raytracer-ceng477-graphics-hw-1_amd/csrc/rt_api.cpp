@@ -145,6 +145,8 @@ struct rt_scene {
     int tune_bservice = 64;     // RT_BSERVICE: phase-B waves service finished walks once this many lanes are done
     int tune_btail = 64;        // RT_BTAIL: the same once the continuations are exhausted (1: 1.24, 4: 1.18, 16: 1.15, 64: 1.14 ms)
     int tune_dyn = 1;           // RT_DYN_UNITS: phase-A waves take sample units from a launch-wide counter
+    int tune_ublk_h = -1, tune_ublk_w = 8;  // RT_UBLK_H / RT_UBLK_W: phase-A unit column blocks (unit_order;
+                                            // H -1: a frame high, 0: row-major units)
     int tune_split = 1;         // RT_SPLIT: a frame runs as this many concurrent interleaved sub-frames (2: +8%, 3: +18% on C3)
     std::string trace_file;     // RT_TRACE: dump per-sample wall-clock timings after each render (diagnostics)
     unsigned* d_trace = nullptr;
@@ -331,6 +333,8 @@ int upload_scene(rt_scene* s, const rt_options* opts) {
     if (const char* e = std::getenv("RT_BTAIL")) s->tune_btail = std::max(1, std::min(64, std::atoi(e)));
     if (const char* e = std::getenv("RT_SPLIT")) s->tune_split = std::max(1, std::atoi(e));
     if (const char* e = std::getenv("RT_DYN_UNITS")) s->tune_dyn = std::atoi(e) != 0;
+    if (const char* e = std::getenv("RT_UBLK_H")) s->tune_ublk_h = std::max(-1, std::atoi(e));
+    if (const char* e = std::getenv("RT_UBLK_W")) s->tune_ublk_w = std::max(1, std::atoi(e));
     if (const char* e = std::getenv("RT_PROD")) s->tune_producers = std::max(1, std::min(4, std::atoi(e)));
     if (const char* e = std::getenv("RT_CREFILL")) s->tune_crefill = std::max(0, std::min(63, std::atoi(e)));
     if (const char* e = std::getenv("RT_TRACE")) s->trace_file = e;
@@ -683,6 +687,8 @@ int render_chain(rt_scene* s, const rtk::Eye& eye, const rtk::FrameParams& f, bo
     p.shade_split = std::getenv("RT_SHADE_SPLIT") ? std::atoi(std::getenv("RT_SHADE_SPLIT")) : 0;
     p.spread = s->tune_spread;
     p.dyn_units = (int)dyn_units;
+    p.ublk_h = s->tune_ublk_h;
+    p.ublk_w = std::max(1, s->tune_ublk_w);
     p.crefill = s->tune_crefill;
     p.wq = static_cast<unsigned*>(at(o_wq));
     p.wq_cap = wq_cap;
