@@ -53,25 +53,46 @@ sys.path.insert(0, str(ROOT))
 
 import __graft_entry__ as graft  # noqa: E402
 
-HBM_PEAK_GBPS = 8000.0     # MI355X spec (MI355X_MICROARCH.md §HBM; 6.29 TB/s measured float4 copy)
-L2_PEAK_GBPS = 34500.0     # MI355X_MICROARCH.md §L2: ~34.5 TB/s aggregate over the 8 XCDs
+HBM_SPEC_GBPS = 8000.0     # MI355X spec (MI355X_MICROARCH.md §HBM); the line prices against MEASURED peaks
+                           # (rt_measure_peaks: HBM streaming copy, walk-shaped L2 gather) and shows the spec
 # The reference's algorithmic bytes per unit of work, reported for comparison
 B_NODE, B_TRI, B_SPH, B_PIX = 32, 36, 16, 3
 
 
-def workspace_bytes(c: dict, nlights: int, out_pixels: int) -> int:
-    """Chain-path workspace bytes of one frame from its exact ray counts (pathchain.hip):
-    every hit writes a 32-B record (rec_write) and is shaded from it again in k_finish (32 B, its
-    16-B face normal / sphere and 8 B of occlusion dwords); every sample writes and reads its 4-B
-    path word; every TRACED shadow task id is written, packed (read + write) and read (16 B), its ray
-    re-derived from the record's first 16 B and the surface normal (16 B) and its 1-B result written;
-    a skipped one (light_needed) writes its 1-B result only; every reflection re-reads its 32-B record
-    and normal; every output pixel is 3 B."""
-    hits = c["shadow_rays"] // max(1, nlights)
-    skipped = c.get("shadow_rays_skipped", 0)
-    traced = c["shadow_rays"] - skipped
-    return (hits * (32 + 32 + 16 + 8) + c["primary_rays"] * 8 + traced * (16 + 16 + 16 + 1) + skipped
-            + c["reflection_rays"] * (32 + 16) + out_pixels * 3)
+def kernel_bytes(r: dict, c: dict, out_pixels: int, batched: bool) -> dict:
+    """Algorithmic bytes of one frame per kernel of the chain path (pathchain.hip), from a
+    production-fetch counting pass: `r` = its per-role counter slots (Scene.counters_raw: the bytes
+    each role's walks fetch -- wide-node lines, leaf records, primitives -- and its ray / hit counts),
+    `c` = the reference's counters.  Workspace traffic per item: a hit writes its 32-B record and reads
+    its 16-B face normal (TriShade); a traced shadow task id is written (4 B), read by its walker with
+    the record's first 16 B and the normal, and its 1-B result written; a skipped one (light_needed)
+    writes its 1-B result; a continuation id is written in phase A and read in phase B with its
+    record and normal; packing reads and writes each task id; k_finish reads every sample's path
+    word (4 B) and every hit's record, normal and occlusion dwords (8 B), and writes 3 B per pixel.
+    One frame alone, A's shadow rays run in k_mix's shadow role; in frame batches in k_occlude."""
+    REC, NRM, TASK, OCC = 32, 16, 4, 1
+    samples, skipped = c["primary_rays"], c["shadow_rays_skipped"]
+    a_sh, bq, bo, conts = r["a_shadow_rays"], r["bq_shadow_rays"], r["bo_shadow_rays"], r["continuations"]
+    shadow_ws = TASK + 16 + NRM + OCC
+    k = {
+        "k_chain": r["a_walk_bytes"] + samples * 4 + r["a_hits"] * (REC + NRM) + a_sh * TASK + skipped * OCC
+                   + conts * TASK,
+        "k_pack_a": (a_sh + conts) * 2 * TASK,
+        "k_mix": r["b_walk_bytes"] + r["bq_shadow_bytes"] + conts * (TASK + REC + NRM) + r["b_hits"] * (REC + NRM)
+                 + bq * (16 + NRM + OCC) + bo * TASK,
+        "k_occlude_a": r["a_shadow_bytes"] + a_sh * shadow_ws,
+        "k_pack_b": bo * 2 * TASK,
+        "k_occlude_b": r["bo_shadow_bytes"] + bo * shadow_ws,
+        "k_finish": samples * 4 + (r["a_hits"] + r["b_hits"]) * (REC + NRM + 8) + out_pixels * 3,
+    }
+    if not batched:                       # one frame: A's shadow rays are k_mix's shadow role
+        k["k_mix"] += k.pop("k_occlude_a")
+    return k
+
+
+def traversal_bytes(r: dict) -> int:
+    return r["a_walk_bytes"] + r["b_walk_bytes"] + r["a_shadow_bytes"] + r["bq_shadow_bytes"] + r["bo_shadow_bytes"]
+
 
 # kernels one frame launches, per render path (the roofline covers all of them)
 PATH_KERNELS = {
@@ -238,6 +259,12 @@ def main() -> int:
         print(f"[bench rank {rank}] {msg} t={time.perf_counter() - t0:.1f}s", file=sys.stderr, flush=True)
 
     note(f"scene loaded {W}x{H} aa{aa}")
+    # measured roofline denominators on this device (rt_measure_peaks, ~1 s): HBM streaming copy and
+    # the walks' access shape (random whole 128-B lines shared by every workgroup) from a table inside
+    # one XCD's L2 and from a table the size of the scene's walk hot set
+    hot_bytes = {k: binfo[k] for k in ("ref_wide_bytes", "occ_wide_bytes", "leaf_record_bytes", "tri_shade_bytes")}
+    peaks = pkg.measure_peaks(local, sum(hot_bytes.values()))
+    note(f"peaks {({k: round(v) for k, v in peaks.items()})}")
     # Counting passes (not timed).  (1) the reference's exact work (rays, node visits, tests): the
     # metric's ray counts, equal to the reference's counters (parity tests); (2) the production walks'
     # own fetched bytes (RT_COUNT_PROD: a scene whose counting kernels walk the timed kernels' trees).
@@ -254,12 +281,16 @@ def main() -> int:
     pscene.counters_reset(sp)
     pscene.render_device(cam, aa, slab.data_ptr(), sp, S, rank, world, count=True)
     pcnt = pscene.counters_read()
+    roles = pscene.counters_raw()
     pscene.close()
     if any(pcnt[k] != cnt[k] for k in ("primary_rays", "shadow_rays", "reflection_rays")):
         raise RuntimeError(f"production counting pass disagrees on ray counts: {pcnt} vs {cnt}")
-    traversal_bytes = pcnt["node_visits"]
-    ws_bytes = workspace_bytes(cnt, Path(xml).read_text().count("<PointLight"), rows * W)
-    alg_bytes = traversal_bytes + ws_bytes
+    if traversal_bytes(roles) != pcnt["node_visits"]:
+        raise RuntimeError(f"per-role fetch bytes do not add up: {roles} vs {pcnt['node_visits']}")
+    kbytes = kernel_bytes(roles, cnt, rows * W, batched=F > 1)
+    alg_bytes = sum(kbytes.values())
+    trav_bytes = traversal_bytes(roles)
+    ws_bytes = alg_bytes - trav_bytes
     note("counting passes done")
     ps_local = cnt["primary_rays"] + cnt["shadow_rays"]
     tot = torch.tensor([ps_local, cnt["primary_rays"], cnt["shadow_rays"], cnt["reflection_rays"],
@@ -352,6 +383,44 @@ def main() -> int:
             ts.append(time.perf_counter() - t1)
         host_ms = sorted(ts)[len(ts) // 2] * 1e3
 
+    footprint = scene.memory()
+    footprint["total_bytes"] = footprint["scene_bytes"] + footprint["workspace_bytes"]
+
+    # per-kernel device time (rank 0): a scene with RT_KTIME=1 times the kernels of each chain launch
+    # with events between them on ONE workspace slot (kernels back to back) -- the frame batches of the
+    # timed configuration (same batch size: the slot gets the same workspace share) and one frame alone
+    ktimes = None
+    if rank == 0 and a.path == "chain" and not a.trace:
+        nslots = int(os.environ.get("RT_SLOTS", max(1, min(6, int(os.environ["GPU_MAX_HW_QUEUES"]) - 1))))
+        budget_mb = int(os.environ.get("RT_WS_BUDGET_MB", "16384"))
+        saved = {k: os.environ.get(k) for k in ("RT_KTIME", "RT_SLOTS", "RT_WS_BUDGET_MB")}
+        os.environ.update(RT_KTIME="1", RT_SLOTS="1", RT_WS_BUDGET_MB=str(max(64, budget_mb // nslots)))
+        try:
+            kscene = pkg.Scene.from_xml(xml, device=local, render_path=a.path)
+        finally:
+            for k, v in saved.items():
+                if v is None:
+                    os.environ.pop(k, None)
+                else:
+                    os.environ[k] = v
+        ktimes = {}
+        for mode, n in (("batched", F), ("one_frame", 1)):
+            reps = 2 if n > 1 else 5
+            for rep in range(reps + 1):
+                if n > 1:
+                    kscene.render_frames_device([cam] * n, aa, [slab_bufs[0][f].data_ptr() for f in range(n)], sp,
+                                                S, rank, world)
+                else:
+                    kscene.render_device(cam, aa, slab.data_ptr(), sp, S, rank, world)
+                torch.cuda.synchronize(dev)
+                if rep == 0:
+                    kscene.kernel_times(reset=True)       # the first round allocates the workspace
+            ms, launches = kscene.kernel_times(reset=True)
+            frames = reps * n
+            ktimes[mode] = {k: round(v / frames, 5) for k, v in ms.items() if v > 0}
+            ktimes[mode]["launches_per_frame"] = round(launches / frames, 4)
+        kscene.close()
+
     traffic, traffic_src = None, None
     tfile = ROOT / "profiles" / "traffic.json"
     if tfile.exists():       # HBM bytes per frame from the committed rocprofv3 FETCH/WRITE passes
@@ -363,6 +432,20 @@ def main() -> int:
         ms = elapsed / a.steps * 1e3
         value = ps_frame * a.steps / elapsed / 1e6
         achieved = alg_bytes / (kern_ms / 1e3) / 1e9
+        # each kernel's own fraction: its alg bytes per frame / its one-slot time per frame (RT_KTIME),
+        # against the measured L2 gather peak
+        per_kernel, dominant = None, None
+        if ktimes:
+            kt = ktimes["batched" if F > 1 else "one_frame"]
+            per_kernel = {}
+            for k, b in kbytes.items():
+                t = kt.get(k)
+                gbps = b / (t / 1e3) / 1e9 if t else None
+                per_kernel[k] = {"alg_bytes": int(b), "ms_one_slot": t,
+                                 "achieved": round(gbps, 1) if gbps else None,
+                                 "frac": round(gbps / peaks["l2_gather_gbps"], 4) if gbps else None}
+            dk = max((k for k in per_kernel if per_kernel[k]["ms_one_slot"]), key=lambda k: per_kernel[k]["ms_one_slot"])
+            dominant = {"kernel": dk, **per_kernel[dk]}
         traffic_gbps = traffic / (kern_ms / 1e3) / 1e9 if traffic else None
         if backend != "nccl":
             desc += f" [REHEARSAL: {backend} host-staged gather, all ranks on one GPU; not a measurement]"
@@ -395,25 +478,35 @@ def main() -> int:
                        "scene_load_s": round(load_s, 4),
                        "host_build": {"bvh_build_ms": round(binfo["build_ms"], 2), "ref_tree_ms": round(binfo["ref_ms"], 2),
                                       "wide_tree_ms": round(binfo["wide_ms"], 2), "threads": binfo["build_threads"]},
-                       "value_definition": f"the reference's primary+shadow rays of a frame (its own counters) x "
+                       "value_definition": f"REFERENCE-EQUIVALENT primary+shadow rays: the reference's own "
+                                           f"counters for a frame (incl. the shadow_rays_skipped that the timed "
+                                           f"kernels provably need not trace; mray_s_traced excludes them) x "
                                            f"frames / wall time; frames submitted {F} at a time as frame batches, "
                                            "scene and frames resident in HBM, max-over-ranks wall time"},
             "single_frame": ({"ms": round(lat_ms, 4), "mray_s": round(ps_frame / lat_ms / 1e3, 3),
                               "definition": "one frame alone on the GPU (rt_render_device), device time"}
                              if lat else None),
+            "hbm_footprint": footprint,
+            "kernel_ms_one_slot": ktimes,
             "drop_in": ({"ms_per_frame": round(host_ms, 4), "mray_s": round(ps_frame / host_ms / 1e3, 3),
                          "definition": "SURVEY §8(d): rt_render wall time, camera upload to the uint8 frame in "
                                        "host memory (PCIe included), one frame at a time"} if host_ms else None),
-            "roofline": {"bound": "l2", "achieved": round(achieved, 2), "peak": L2_PEAK_GBPS, "unit": "GB/s",
-                         "frac": round(achieved / L2_PEAK_GBPS, 4), "traffic": traffic,
-                         "bound_note": "the walks read a ~6 MB cache-resident scene (L2/MALL); the bytes the timed "
-                                       "kernels fetch and move are priced against the L2's aggregate bandwidth; "
-                                       "the HBM bytes they actually move (PMC) are `hbm`",
+            "roofline": {"bound": "l2", "achieved": round(achieved, 2), "peak": round(peaks["l2_gather_gbps"], 1),
+                         "unit": "GB/s", "frac": round(achieved / peaks["l2_gather_gbps"], 4), "traffic": traffic,
+                         "bound_note": "the walks gather random 128-B lines of a ~5 MB cache-resident scene; the bytes "
+                                       "the timed kernels fetch and move are priced against the MEASURED L2 gather "
+                                       "peak (rt_measure_peaks: the walks' access shape from a table inside one "
+                                       "XCD's L2); the HBM bytes they actually move (PMC) are `hbm`, priced against "
+                                       "the measured HBM streaming copy",
+                         "peak_measured": {k: round(v, 1) for k, v in peaks.items()},
+                         "walk_hot_set_bytes": hot_bytes,
                          "alg_bytes_per_launch": int(alg_bytes), "launch_unit": "one frame (this rank's stripes)",
-                         "alg_bytes_split": {"traversal": int(traversal_bytes), "workspace": int(ws_bytes)},
+                         "alg_bytes_split": {"traversal": int(trav_bytes), "workspace": int(ws_bytes)},
+                         "per_kernel": per_kernel,
+                         "dominant": dominant,
                          "hbm": {"bytes_per_frame": traffic, "gbps": round(traffic_gbps, 2) if traffic else None,
-                                 "peak": HBM_PEAK_GBPS,
-                                 "frac": round(traffic_gbps / HBM_PEAK_GBPS, 4) if traffic else None,
+                                 "peak": round(peaks["hbm_copy_gbps"], 1), "spec": HBM_SPEC_GBPS,
+                                 "frac": round(traffic_gbps / peaks["hbm_copy_gbps"], 4) if traffic else None,
                                  "source": traffic_src},
                          "reference_model": {"bytes_per_frame": int(ref_alg_bytes),
                                              "note": "SURVEY §8(d) per-operation model of the reference's own walk "

@@ -33,7 +33,7 @@
 extern "C" {
 #endif
 
-#define RT_ABI_VERSION 6
+#define RT_ABI_VERSION 7
 
 typedef enum rt_status {
     RT_OK = 0,
@@ -124,6 +124,11 @@ typedef struct rt_bvh_info {
     int build_threads;       /* threads the build used                   (ABI 2) */
     int wide_nodes;          /* wide nodes of both wide trees (occlusion + reference order) */
     uint64_t wide_hash;      /* FNV-1a of both wide trees + leaf records (ABI 2) */
+    /* device bytes of the structures the production walks read (ABI 7) */
+    uint64_t ref_wide_bytes;     /* reference-order wide tree (closest hit)           */
+    uint64_t occ_wide_bytes;     /* occlusion wide tree (any hit)                      */
+    uint64_t leaf_record_bytes;  /* leaf records: exact leaf box + primitive copies    */
+    uint64_t tri_shade_bytes;    /* per-triangle normal + material (hit epilogues)     */
 } rt_bvh_info;
 
 /* ---- errors / devices ---- */
@@ -141,7 +146,12 @@ int rt_device_count(int* count);
  * round-robin over the devices (env RT_GROUP_STRIPE, default 8), render them
  * concurrently (one HIP stream per device), gather the uint8 slabs to device 0
  * with ONE ncclGather over xGMI, un-interleave them there and copy the frame
- * to the caller's buffer -- the same bytes as one GPU.  The asynchronous
+ * to the caller's buffer -- designed to give the same bytes as one GPU; the
+ * RCCL gather at n > 1 has not run on hardware yet (a group of one, and the
+ * RT_GROUP_VIRTUAL=1 rehearsal -- n ranks on device 0, device copies in place
+ * of RCCL -- are tested bit-exact).  rt_render_cameras on a group renders each
+ * run of consecutive same-size cameras as one frame batch on every device
+ * (frames in flight together) with one grouped gather.  The asynchronous
  * device-buffer entry points (rt_render_device, rt_render_frames_device,
  * rt_render_cameras_device) keep using device 0 only: a one-process-per-GPU
  * caller shards with their stripe/rank arguments instead.  n = 1 runs the
@@ -229,6 +239,28 @@ int rt_walk_timing(rt_scene* scene, const float* rays, int n, int lanes, int rep
  * (raytracer.cpp:414) -- on the current device (host arrays, synchronous;
  * ABI 5). */
 int rt_phong_pow(const float* base, const float* exponent, float* out, int n);
+/* HBM held by a scene on its (first) device (ABI 7): the uploaded scene (trees,
+ * primitives, tables) and the render workspaces allocated so far (chain-path
+ * arenas of every slot, output staging).  The workspaces grow on demand up to
+ * the scene's budget, env RT_WS_BUDGET_MB at scene creation (default 16384 MB
+ * for all slots together); a frame batch or chunk is sized to fit it. */
+int rt_scene_memory(const rt_scene* scene, uint64_t* scene_bytes, uint64_t* workspace_bytes);
+/* Measured roofline denominators (ABI 7), on `device` (-1: the
+ * current one), ~1 s, allocates 4 GiB + the tables temporarily:
+ *   hbm_copy_gbps      streaming float4 copy of 2 GiB (read + write bytes / time)
+ *   hbm_read_gbps      the same buffer read only
+ *   l2_gather_gbps     the BVH walks' access shape: every lane reads whole random
+ *                      128-B lines (eight dwordx4) of a table every workgroup shares,
+ *                      4 lines in flight per lane; table of l2_table_bytes (2 MiB,
+ *                      inside one XCD's 4 MiB L2)
+ *   scene_gather_gbps  the same over a table of scene_table_bytes (the caller's
+ *                      walk hot set; lines beyond L2 come from the Infinity Cache) */
+typedef struct rt_peaks {
+    double hbm_copy_gbps, hbm_read_gbps;
+    double l2_gather_gbps, l2_table_bytes;
+    double scene_gather_gbps, scene_table_bytes;
+} rt_peaks;
+int rt_measure_peaks(int device, uint64_t scene_table_bytes, rt_peaks* out);
 /* Rows in one rank's slab (max over ranks, so all slabs have equal size). */
 int rt_slab_rows(int height, int stripe_rows, int nranks);
 /* Rank-0 reassembly: slabs[nranks][slab_rows][W][3] (gathered) -> image[H][W][3]. */
@@ -236,13 +268,30 @@ int rt_unshuffle_stripes(const void* slabs_dev, void* image_dev, int width, int 
                          int stripe_rows, int nranks, void* stream);
 int rt_counters_reset(rt_scene* scene, void* stream);
 int rt_counters_read(rt_scene* scene, rt_stats* stats);   /* synchronises the device */
+/* Diagnostics (ABI 7): the raw u64 counter block, n slots (returns the slots
+ * copied).  0-6 as rt_stats; 8.. per kernel role of the chain path (pathchain.hpp
+ * CounterSlot): phase-A / phase-B closest-hit walk bytes (or node visits), walks
+ * and hits, continuations, and the shadow rays of A, of B's workgroup queue and
+ * of B's overflow -- bytes and rays each.  Bytes when the scene was created with
+ * RT_COUNT_PROD=1 (the production walks' fetched bytes). */
+int rt_counters_read_raw(rt_scene* scene, uint64_t* out, int n);
+/* Diagnostics (ABI 7): per-kernel device time of the chain path's launches
+ * since the last reset, for a scene created with env RT_KTIME=1 (events between
+ * the kernels of each launch; each launch then synchronises).  ms[k] for k =
+ * k_chain, k_pack_a, k_mix, k_occlude (A's shadows, frame batches), k_pack_b,
+ * k_occlude (B's overflow), k_finish.  Returns the launches timed. */
+int rt_kernel_times(rt_scene* scene, double* ms, int n, int reset);
 /* Synchronises the scene's device and reports a walk that was cut off since
  * the last check: every BVH walk has an always-on step bound (64 x the tree's
  * nodes; a DFS pops each node at most once), and a walk exceeding it ends
  * early and sets the scene's device error word -> RT_ERR_LIMIT (the frames
  * rendered since the last check are then invalid).  rt_render,
  * rt_render_cameras and rt_counters_read check it themselves; asynchronous
- * callers (rt_render_device, rt_render_frames_device) call this.  (ABI 4) */
+ * callers (rt_render_device, rt_render_frames_device) call this.  The word is
+ * SCENE-WIDE, not per stream: a check reports (and clears) a walk cut off in
+ * any render of the scene on any stream since the previous check, so callers
+ * that render one scene on several streams should check after joining them.
+ * (ABI 4) */
 int rt_scene_check(rt_scene* scene);
 
 /* Primary closest-hit per internal pixel ((W*aa) x (H*aa)): t (tSmall, -1 on

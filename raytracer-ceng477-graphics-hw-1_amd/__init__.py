@@ -71,10 +71,66 @@ class BvhInfo(ctypes.Structure):
                 ("max_depth", ctypes.c_int), ("max_stack", ctypes.c_int), ("triangles", ctypes.c_int),
                 ("spheres", ctypes.c_int), ("build_ms", ctypes.c_double),
                 ("ref_ms", ctypes.c_double), ("wide_ms", ctypes.c_double), ("build_threads", ctypes.c_int),
-                ("wide_nodes", ctypes.c_int), ("wide_hash", ctypes.c_uint64)]
+                ("wide_nodes", ctypes.c_int), ("wide_hash", ctypes.c_uint64),
+                ("ref_wide_bytes", ctypes.c_uint64), ("occ_wide_bytes", ctypes.c_uint64),
+                ("leaf_record_bytes", ctypes.c_uint64), ("tri_shade_bytes", ctypes.c_uint64)]
 
     def as_dict(self) -> dict:
         return {k: getattr(self, k) for k, _ in self._fields_}
+
+
+class PointLight(ctypes.Structure):     # rt_point_light (parser.h:180-183)
+    _fields_ = [("position", Vec3f), ("intensity", Vec3f)]
+
+
+class Material(ctypes.Structure):       # rt_material (parser.h:185-192)
+    _fields_ = [("is_mirror", ctypes.c_int), ("ambient", Vec3f), ("diffuse", Vec3f), ("specular", Vec3f),
+                ("mirror", Vec3f), ("phong_exponent", ctypes.c_float)]
+
+
+class Triangle(ctypes.Structure):       # rt_triangle: material id, 1-based vertex ids
+    _fields_ = [("material_id", ctypes.c_int), ("v0_id", ctypes.c_int), ("v1_id", ctypes.c_int),
+                ("v2_id", ctypes.c_int)]
+
+
+class Sphere(ctypes.Structure):         # rt_sphere
+    _fields_ = [("material_id", ctypes.c_int), ("center_vertex_id", ctypes.c_int), ("radius", ctypes.c_float)]
+
+
+class SceneDesc(ctypes.Structure):      # rt_scene_desc: borrowed host arrays
+    _fields_ = [("background_color", ctypes.c_int * 3), ("shadow_ray_epsilon", ctypes.c_float),
+                ("max_recursion_depth", ctypes.c_int), ("ambient_light", Vec3f),
+                ("lights", ctypes.POINTER(PointLight)), ("num_lights", ctypes.c_int),
+                ("materials", ctypes.POINTER(Material)), ("num_materials", ctypes.c_int),
+                ("vertices", ctypes.POINTER(Vec3f)), ("num_vertices", ctypes.c_int),
+                ("triangles", ctypes.POINTER(Triangle)), ("num_triangles", ctypes.c_int),
+                ("spheres", ctypes.POINTER(Sphere)), ("num_spheres", ctypes.c_int)]
+
+
+def make_desc(a: dict) -> tuple[SceneDesc, list]:
+    """rt_scene_desc over ctypes arrays built from scenes.scene_arrays(); returns (desc, keepalive)."""
+    def v3(x):
+        return Vec3f(*x)
+
+    def arr(T, xs):
+        return (T * max(1, len(xs)))(*xs)
+
+    lights = arr(PointLight, [PointLight(v3(p), v3(i)) for p, i in a["lights"]])
+    mats = arr(Material, [Material(m["is_mirror"], v3(m["ambient"]), v3(m["diffuse"]), v3(m["specular"]),
+                                   v3(m["mirror"]), m["phong_exponent"]) for m in a["materials"]])
+    verts = arr(Vec3f, [v3(v) for v in a["vertices"]])
+    tris = arr(Triangle, [Triangle(*t) for t in a["triangles"]])
+    sph = arr(Sphere, [Sphere(*s) for s in a["spheres"]])
+    d = SceneDesc((ctypes.c_int * 3)(*a["background_color"]), a["shadow_ray_epsilon"], a["max_recursion_depth"],
+                  v3(a["ambient_light"]), lights, len(a["lights"]), mats, len(a["materials"]), verts,
+                  len(a["vertices"]), tris, len(a["triangles"]), sph, len(a["spheres"]))
+    return d, [lights, mats, verts, tris, sph]
+
+
+def camera_from(c: dict) -> "Camera":
+    """rt_camera from a scenes.scene_arrays() camera entry."""
+    return Camera(Vec3f(*c["position"]), Vec3f(*c["gaze"]), Vec3f(*c["up"]), (ctypes.c_float * 4)(*c["near_plane"]),
+                  c["near_distance"], c["image_width"], c["image_height"])
 
 
 # device_layout.hpp dl::Node (32 B)
@@ -108,10 +164,14 @@ _SIGS = [
                                                ctypes.c_int, ctypes.c_int, _P, _P, ctypes.c_int]),
     ("rt_walk_timing", ctypes.c_int, [_P, _P, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int, _P]),
     ("rt_phong_pow", ctypes.c_int, [_P, _P, _P, ctypes.c_int]),
+    ("rt_measure_peaks", ctypes.c_int, [ctypes.c_int, ctypes.c_uint64, _P]),
+    ("rt_scene_memory", ctypes.c_int, [_P, ctypes.POINTER(ctypes.c_uint64), ctypes.POINTER(ctypes.c_uint64)]),
     ("rt_slab_rows", ctypes.c_int, [ctypes.c_int, ctypes.c_int, ctypes.c_int]),
     ("rt_unshuffle_stripes", ctypes.c_int, [_P, _P, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int, _P]),
     ("rt_counters_reset", ctypes.c_int, [_P, _P]),
     ("rt_counters_read", ctypes.c_int, [_P, ctypes.POINTER(Stats)]),
+    ("rt_counters_read_raw", ctypes.c_int, [_P, _P, ctypes.c_int]),
+    ("rt_kernel_times", ctypes.c_int, [_P, _P, ctypes.c_int, ctypes.c_int]),
     ("rt_scene_check", ctypes.c_int, [_P]),
     ("rt_primary_hits", ctypes.c_int, [_P, ctypes.POINTER(Camera), ctypes.c_int, _P, _P]),
     ("rt_downsample_host", ctypes.c_int, [_P, ctypes.c_int, ctypes.c_int, ctypes.c_int, _P]),
@@ -168,6 +228,19 @@ def phong_pow(base, exponent) -> np.ndarray:
     return out
 
 
+class Peaks(ctypes.Structure):
+    _fields_ = [("hbm_copy_gbps", ctypes.c_double), ("hbm_read_gbps", ctypes.c_double),
+                ("l2_gather_gbps", ctypes.c_double), ("l2_table_bytes", ctypes.c_double),
+                ("scene_gather_gbps", ctypes.c_double), ("scene_table_bytes", ctypes.c_double)]
+
+
+def measure_peaks(device: int = -1, scene_table_bytes: int = 6 << 20) -> dict:
+    """rt_measure_peaks: measured HBM copy/read and walk-shaped L2 gather bandwidths (GB/s)."""
+    p = Peaks()
+    _check(lib().rt_measure_peaks(device, scene_table_bytes, ctypes.byref(p)))
+    return {k: getattr(p, k) for k, _ in p._fields_}
+
+
 def slab_rows(height: int, stripe_rows: int, nranks: int) -> int:
     return lib().rt_slab_rows(height, stripe_rows, nranks)
 
@@ -190,6 +263,21 @@ class Scene:
                   "fused": RT_OPT_FUSED, "default": 0}[render_path]
         opts = Options(device, flags, build_threads)
         _check(lib().rt_scene_load_xml(str(path).encode(), ctypes.byref(opts), ctypes.byref(h)))
+        return cls(h.value)
+
+    @classmethod
+    def from_desc(cls, arrays: dict, device: int = -1, host_only: bool = False,
+                  render_path: str = "chain") -> "Scene":
+        """rt_scene_create from borrowed host arrays (the reference's RayTracer(parser::Scene&) ctor,
+        raytracer.cpp:335-350); `arrays` as returned by scenes.scene_arrays()."""
+        desc, keep = make_desc(arrays)
+        h = ctypes.c_void_p()
+        flags = RT_OPT_HOST_ONLY if host_only else 0
+        flags |= {"chain": RT_OPT_CHAIN, "wavefront": RT_OPT_WAVEFRONT, "megakernel": RT_OPT_MEGAKERNEL,
+                  "fused": RT_OPT_FUSED, "default": 0}[render_path]
+        opts = Options(device, flags, 0)
+        _check(lib().rt_scene_create(ctypes.byref(desc), ctypes.byref(opts), ctypes.byref(h)))
+        del keep
         return cls(h.value)
 
     def close(self) -> None:
@@ -300,6 +388,34 @@ class Scene:
         st = Stats()
         _check(lib().rt_counters_read(self._h, ctypes.byref(st)))
         return st.as_dict()
+
+    def memory(self) -> dict:
+        """HBM the scene holds (rt_scene_memory): uploaded scene and render workspaces, bytes."""
+        a, b = ctypes.c_uint64(), ctypes.c_uint64()
+        _check(lib().rt_scene_memory(self._h, ctypes.byref(a), ctypes.byref(b)))
+        return {"scene_bytes": a.value, "workspace_bytes": b.value}
+
+    COUNTER_SLOTS = ("a_walk_bytes", "a_walks", "a_hits", "b_walk_bytes", "b_walks", "b_hits", "continuations",
+                     "a_shadow_bytes", "a_shadow_rays", "bq_shadow_bytes", "bq_shadow_rays", "bo_shadow_bytes",
+                     "bo_shadow_rays")
+
+    def counters_raw(self) -> dict:
+        """rt_counters_read_raw: the per-role counter slots (pathchain.hpp CounterSlot) by name."""
+        out = np.zeros(32, dtype=np.uint64)
+        n = lib().rt_counters_read_raw(self._h, out.ctypes.data_as(ctypes.c_void_p), 32)
+        if n < 0:
+            _check(n)
+        return {k: int(out[8 + i]) for i, k in enumerate(self.COUNTER_SLOTS)}
+
+    KERNEL_KINDS = ("k_chain", "k_pack_a", "k_mix", "k_occlude_a", "k_pack_b", "k_occlude_b", "k_finish")
+
+    def kernel_times(self, reset: bool = True) -> tuple[dict, int]:
+        """rt_kernel_times (RT_KTIME=1 scenes): ms per kernel of the chain launches, and the launch count."""
+        ms = np.zeros(8, dtype=np.float64)
+        n = lib().rt_kernel_times(self._h, ms.ctypes.data_as(ctypes.c_void_p), 8, int(reset))
+        if n < 0:
+            _check(n)
+        return {k: float(ms[i]) for i, k in enumerate(self.KERNEL_KINDS)}, n
 
     def num_devices(self) -> int:
         return lib().rt_scene_num_devices(self._h)

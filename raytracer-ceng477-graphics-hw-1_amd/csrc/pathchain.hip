@@ -545,6 +545,10 @@ __device__ uint32_t bq_consume(const rtk::DevScene& s, const PcParams& p, WalkSt
         }
     }
     stat.flush(3);
+    if (COUNT) {
+        wave_add_counter(&p.counters[kCntBQBytes], w.nodes);
+        wave_add_counter(&p.counters[kCntBQRays], n);
+    }
     return n;
 }
 
@@ -572,7 +576,7 @@ __device__ void chain_body(const rtk::DevScene& s, const rtk::Eye& e, const PcPa
                            const PhaseOut& o) {
     WalkStack stk;
     Work w;
-    uint32_t nprim = 0, nrefl = 0, nskip = 0;
+    uint32_t nprim = 0, nrefl = 0, nskip = 0, nhit = 0, ncont = 0;
     const int nl = s.nlights;
     unsigned nb;
     if (CONT) nb = chunk_count(p.totals[1], G, blk, (unsigned)p.tchunk);
@@ -606,6 +610,7 @@ __device__ void chain_body(const rtk::DevScene& s, const rtk::Eye& e, const PcPa
                 hit_surface(s, r, h, &nn, &mat, &code);
                 hitp = add(r.o, mul(r.d, h.t));
                 rec_write(p, (size_t)k * p.cap + path, hitp, code, r.d, mat);
+                if (COUNT) nhit++;
             }
             // one shadow task per light (:399-404) whose ray can change the pixel (light_needed; the
             // counting passes trace every one, as the reference does); light-major within the wave
@@ -660,6 +665,7 @@ __device__ void chain_body(const rtk::DevScene& s, const rtk::Eye& e, const PcPa
             const bool handoff = !ends && k >= o.kinline;                      // deeper levels: next phase
             const unsigned long long cm = __ballot(handoff);
             if (handoff) {
+                if (COUNT) ncont++;
                 const unsigned base = wave_grab_lds(&g_ccnt, cm);
                 o.cq[(size_t)blk * o.ccap + base + lane_rank(cm)] = (unsigned)((size_t)k * p.cap + path);
                 p.pinfo[path] = kPathCont;        // continued in phase B (finish_pixels' order)
@@ -764,9 +770,19 @@ __device__ void chain_body(const rtk::DevScene& s, const rtk::Eye& e, const PcPa
     }
     stat.flush(CONT ? 1 : 0);
     uint32_t nshadow = 0;
+    if (COUNT) {
+        wave_add_counter(&p.counters[CONT ? kCntBWalkBytes : kCntAWalkBytes], w.nodes);
+        wave_add_counter(&p.counters[CONT ? kCntBWalks : kCntAWalks], nprim + nrefl);
+        wave_add_counter(&p.counters[CONT ? kCntBHits : kCntAHits], nhit);
+        if (!CONT) wave_add_counter(&p.counters[kCntConts], ncont);
+    }
     if (CONT && kBq > 0) {
         if (lane_id() == 0) atomicSub(&g_bq_prod, 1u);      // this wave produces no more shadow tasks
-        nshadow = bq_consume<COUNT>(s, p, stk, w);
+        Work wq;                                            // the queue's walks, counted apart (kCntBQ*)
+        nshadow = bq_consume<COUNT>(s, p, stk, wq);
+        w.nodes += wq.nodes;
+        w.tris += wq.tris;
+        w.spheres += wq.spheres;
     }
     __syncthreads();
     if (threadIdx.x == 0) {
@@ -790,7 +806,7 @@ __device__ void chain_body(const rtk::DevScene& s, const rtk::Eye& e, const PcPa
 // (raytracer.cpp:227-280).
 template <bool COUNT>
 __device__ void occlude_body(const rtk::DevScene& s, const PcParams& p, unsigned blk, unsigned G,
-                             const unsigned* tasks, unsigned total) {
+                             const unsigned* tasks, unsigned total, int role) {   // role 0: A's tasks, 1: B's overflow
     WalkStack stk;
     Work w;
     uint32_t nrays = 0;
@@ -844,6 +860,8 @@ __device__ void occlude_body(const rtk::DevScene& s, const PcParams& p, unsigned
         p.trace[2 * ((size_t)p.cap + blk) + 1] = (unsigned)wall_clock64();
     }
     if (COUNT) {
+        wave_add_counter(&p.counters[role ? kCntBOBytes : kCntASBytes], w.nodes);
+        wave_add_counter(&p.counters[role ? kCntBORays : kCntASRays], nrays);
         wave_add_counter(&p.counters[1], nrays);
         wave_add_counter(&p.counters[3], w.nodes);
         wave_add_counter(&p.counters[4], w.tris);
@@ -920,15 +938,15 @@ __global__ __launch_bounds__(kBlock, RT_MIX_WAVES) void k_mix(rtk::DevScene s, r
         if (p.bprio) __builtin_amdgcn_s_setprio(3);    // the deep chains are the frame's critical path
         chain_body<COUNT, true>(s, e, p, blockIdx.x, (unsigned)p.gb, phase_b(p));
     }
-    else if (!p.exp_skip_occ) occlude_body<COUNT>(s, p, blockIdx.x - p.gb, gridDim.x - p.gb, p.sflatA, p.totals[0]);
+    else if (!p.exp_skip_occ) occlude_body<COUNT>(s, p, blockIdx.x - p.gb, gridDim.x - p.gb, p.sflatA, p.totals[0], 0);
 }
 
 // Phase B's shadow tasks (which = 1), or phase A's (which = 0: p.split_occ, frame batches).
 template <bool COUNT>
 __global__ __launch_bounds__(kBlock, RT_OCC_WAVES_PER_EU) void k_occlude(rtk::DevScene s, PcParams p, int which) {
     block_init(s);
-    if (which) occlude_body<COUNT>(s, p, blockIdx.x, gridDim.x, p.sflatB, p.totals[2]);
-    else occlude_body<COUNT>(s, p, blockIdx.x, gridDim.x, p.sflatA, p.totals[0]);
+    if (which) occlude_body<COUNT>(s, p, blockIdx.x, gridDim.x, p.sflatB, p.totals[2], 1);
+    else occlude_body<COUNT>(s, p, blockIdx.x, gridDim.x, p.sflatA, p.totals[0], 0);
 }
 
 // ---------------------------------------------------------------------------
@@ -1633,15 +1651,18 @@ unsigned chain_block_scap(int n0, int grid, int levels, int nlights) {
 }
 
 hipError_t launch_chain_chunk(const rtk::DevScene& s, const rtk::Eye& e, const PcParams& p, bool count,
-                              hipStream_t st) {
+                              hipStream_t st, KTimer* kt) {
     const dim3 blk(kBlock);
+    auto mark = [&](int k) { if (kt) kt->mark(k, st); };
     const bool phase_b = p.kinline < s.max_depth;     // any continuation possible
     if (p.dyn_units) {
         const hipError_t me = hipMemsetAsync(p.totals + 3, 0, sizeof(unsigned), st);   // dynamic unit counter
         if (me != hipSuccess) return me;
     }
+    mark(kKChain);
     if (count) hipLaunchKernelGGL(k_chain<true>, dim3(p.grid), blk, 0, st, s, e, p);
     else hipLaunchKernelGGL(k_chain<false>, dim3(p.grid), blk, 0, st, s, e, p);
+    mark(kKPackA);
     hipLaunchKernelGGL(k_pack_a, dim3(p.grid), blk, 0, st, p);
     PcParams q = p;
     if (!phase_b) q.gb = 0;
@@ -1649,15 +1670,19 @@ hipError_t launch_chain_chunk(const rtk::DevScene& s, const rtk::Eye& e, const P
     // per SIMD); otherwise k_mix's other workgroups walk them beside the chains
     const bool split = p.split_occ && phase_b;
     const int mgrid = split ? q.gb : q.gb + p.ogrid;
+    mark(kKMix);
     if (count) hipLaunchKernelGGL(k_mix<true>, dim3(mgrid), blk, 0, st, s, e, q);
     else hipLaunchKernelGGL(k_mix<false>, dim3(mgrid), blk, 0, st, s, e, q);
     if (split) {
+        mark(kKOccA);
         if (count) hipLaunchKernelGGL(k_occlude<true>, dim3(p.occ_grid), blk, 0, st, s, p, 0);
         else hipLaunchKernelGGL(k_occlude<false>, dim3(p.occ_grid), blk, 0, st, s, p, 0);
     }
     if (phase_b) {
+        mark(kKPackB);
         hipLaunchKernelGGL(k_pack_b, dim3(p.gb), blk, 0, st, p);
         const int og = split ? p.occ_grid : p.ogrid;
+        mark(kKOccB);
         if (count) hipLaunchKernelGGL(k_occlude<true>, dim3(og), blk, 0, st, s, p, 1);
         else hipLaunchKernelGGL(k_occlude<false>, dim3(og), blk, 0, st, s, p, 1);
     }
@@ -1665,7 +1690,9 @@ hipError_t launch_chain_chunk(const rtk::DevScene& s, const rtk::Eye& e, const P
     // a pixel (C5: 130 vs 106 ms) and without phase B (C2: +5 %) the extra pinfo reads cost more
     PcParams f = p;
     f.fin_cont = phase_b && p.aa == 1;
+    mark(kKFinish);
     launch_finish(s, f, st);
+    mark(kKEnd);
     return hipGetLastError();
 }
 

@@ -40,6 +40,27 @@ enum PathKind : int {
 // pinfo bit of a path continued in phase B (set by phase A's hand-off, kept by phase B's end)
 constexpr int kPathCont = 1 << 16;
 
+// Device counter block (u64 slots, RT_RENDER_COUNT launches).  0-6 are rt_stats' (primary, shadow,
+// reflection, node visits, triangle tests, sphere tests, skipped shadow rays); the per-role slots
+// split the walks by the kernel role that runs them in the timed path, so a production-fetch
+// counting pass (RT_COUNT_PROD: "node visits" = fetched bytes) gives each kernel its own bytes.
+constexpr int kCounters = 32;
+enum CounterSlot : int {
+    kCntAWalkBytes = 8,   // phase A closest-hit walks (k_chain)
+    kCntAWalks,           //   walks started in phase A (primary + level-1 reflections)
+    kCntAHits,            //   their hits (records written)
+    kCntBWalkBytes,       // phase B closest-hit walks (k_mix chain role)
+    kCntBWalks,
+    kCntBHits,
+    kCntConts,            // continuations handed from A to B
+    kCntASBytes,          // A's shadow rays (k_mix shadow role for one frame; k_occlude in frame batches)
+    kCntASRays,
+    kCntBQBytes,          // B's shadow rays walked from the workgroup LDS queue (k_mix chain role)
+    kCntBQRays,
+    kCntBOBytes,          // B's shadow rays that overflowed to k_occlude
+    kCntBORays,
+};
+
 struct PcParams {
     int width, height, aa, stripe_rows, rank, nranks, slab_rows;
     int wi, tiles_x, chunk_row0, chunk_rows, n0;
@@ -133,7 +154,24 @@ hipError_t launch_phong_pow(const float* base, const float* expo, float* out, in
 hipError_t launch_walk_timing(const rtk::DevScene& s, const float* rays, int n, int lanes, int reps, int mode,
                               unsigned long long* out, hipStream_t st);
 
+// Diagnostics (RT_KTIME=1 scenes, rt_kernel_times): HIP events recorded between the kernels of a
+// chain launch on its stream, so the host can split the launch's time per kernel (one slot: the
+// kernels run back to back).
+enum KernelKind : int { kKChain = 0, kKPackA, kKMix, kKOccA, kKPackB, kKOccB, kKFinish, kKEnd, kKKinds };
+struct KTimer {
+    static constexpr int kMax = 16;
+    hipEvent_t ev[kMax] = {};
+    int kind[kMax] = {};
+    int n = 0;
+    void mark(int k, hipStream_t st) {
+        if (n < kMax && ev[n]) {
+            kind[n] = k;
+            (void)hipEventRecord(ev[n++], st);
+        }
+    }
+};
+
 hipError_t launch_chain_chunk(const rtk::DevScene& s, const rtk::Eye& e, const PcParams& p, bool count,
-                              hipStream_t stream);
+                              hipStream_t stream, KTimer* kt = nullptr);
 
 }  // namespace rtc

@@ -1,0 +1,167 @@
+// Measured roofline denominators on the device the renderer runs on
+// (rt_measure_peaks, include/rt/rt.h; SURVEY.md §8(d): "Fraction = that /
+// measured HBM peak, where the peak comes from a streaming-copy kernel on the
+// box").  Three kernels:
+//   * k_copy: streaming float4 copy of a buffer far larger than the Infinity
+//     Cache (read + write bytes over time) -- the HBM peak;
+//   * k_read: the same buffer read only (a running XOR) -- the HBM read peak;
+//   * k_gather: the BVH walks' access shape -- every lane reads whole random
+//     128-B lines (eight dwordx4, one wide node's line) of a table that every
+//     workgroup shares, many lines in flight per lane.  With a table that fits
+//     one XCD's 4 MiB L2 it is the L2 gather peak the walks are priced
+//     against; with the scene's own walk hot set it shows what that set's size
+//     costs (lines beyond L2 come from the Infinity Cache).
+// Times are best-of-N HIP event intervals on a private stream.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <string>
+#include <vector>
+
+#include "rt/rt.h"
+#include "rt_internal.hpp"
+
+namespace {
+
+constexpr int kBlk = 256;
+
+__global__ __launch_bounds__(kBlk) void k_copy(const float4* __restrict__ src, float4* __restrict__ dst, size_t n) {
+    const size_t stride = (size_t)gridDim.x * kBlk;
+    for (size_t i = (size_t)blockIdx.x * kBlk + threadIdx.x; i < n; i += stride) dst[i] = src[i];
+}
+
+__global__ __launch_bounds__(kBlk) void k_read(const float4* __restrict__ src, size_t n, unsigned* sink) {
+    const size_t stride = (size_t)gridDim.x * kBlk;
+    unsigned acc = 0;
+    size_t i = (size_t)blockIdx.x * kBlk + threadIdx.x;
+    for (; i + 3 * stride < n; i += 4 * stride) {      // four loads in flight per lane
+        const float4 a = src[i], b = src[i + stride], c = src[i + 2 * stride], d = src[i + 3 * stride];
+        acc ^= __float_as_uint(a.x) ^ __float_as_uint(a.y) ^ __float_as_uint(a.z) ^ __float_as_uint(a.w) ^
+               __float_as_uint(b.x) ^ __float_as_uint(b.y) ^ __float_as_uint(b.z) ^ __float_as_uint(b.w) ^
+               __float_as_uint(c.x) ^ __float_as_uint(c.y) ^ __float_as_uint(c.z) ^ __float_as_uint(c.w) ^
+               __float_as_uint(d.x) ^ __float_as_uint(d.y) ^ __float_as_uint(d.z) ^ __float_as_uint(d.w);
+    }
+    for (; i < n; i += stride) {
+        const float4 a = src[i];
+        acc ^= __float_as_uint(a.x) ^ __float_as_uint(a.y) ^ __float_as_uint(a.z) ^ __float_as_uint(a.w);
+    }
+    if (acc == 0x9e3779b9u) sink[0] = acc;            // never true in practice; keeps the loads
+}
+
+__device__ __forceinline__ unsigned mix32(unsigned x) {
+    x ^= x >> 16; x *= 0x7feb352du; x ^= x >> 15; x *= 0x846ca68bu; x ^= x >> 16;
+    return x;
+}
+
+// ITER iterations per lane, UNROLL independent random lines in flight per lane.
+template <int UNROLL>
+__global__ __launch_bounds__(kBlk) void k_gather(const float4* __restrict__ tab, unsigned nlines, int iters,
+                                                 unsigned seed, unsigned* sink) {
+    const unsigned gtid = blockIdx.x * kBlk + threadIdx.x;
+    unsigned acc = 0;
+    for (int it = 0; it < iters; it += UNROLL) {
+        float4 v[UNROLL][8];
+#pragma unroll
+        for (int u = 0; u < UNROLL; ++u) {
+            const unsigned line = mix32(gtid * 0x9e3779b1u + (unsigned)(it + u) * 0x85ebca6bu + seed) % nlines;
+            const float4* q = tab + (size_t)line * 8;
+#pragma unroll
+            for (int j = 0; j < 8; ++j) v[u][j] = q[j];
+        }
+#pragma unroll
+        for (int u = 0; u < UNROLL; ++u)
+#pragma unroll
+            for (int j = 0; j < 8; ++j)
+                acc ^= __float_as_uint(v[u][j].x) ^ __float_as_uint(v[u][j].y) ^ __float_as_uint(v[u][j].z) ^
+                       __float_as_uint(v[u][j].w);
+    }
+    if (acc == 0x9e3779b9u) sink[0] = acc;
+}
+
+#define PK_TRY(expr)                                                                                 \
+    do {                                                                                             \
+        hipError_t e_ = (expr);                                                                      \
+        if (e_ != hipSuccess) {                                                                      \
+            err = std::string(#expr) + ": " + hipGetErrorName(e_);                                   \
+            goto done;                                                                               \
+        }                                                                                            \
+    } while (0)
+
+}  // namespace
+
+extern "C" int rt_measure_peaks(int device, uint64_t scene_table_bytes, rt_peaks* out) {
+    if (!out) return rt_internal_set_error(RT_ERR_ARG, "peaks: out is NULL");
+    *out = rt_peaks{};
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0) return rt_internal_set_error(RT_ERR_NO_DEVICE, "no HIP device visible");
+    if (device >= ndev) return rt_internal_set_error(RT_ERR_ARG, "peaks: device ordinal out of range");
+    std::string err;
+    float4 *big = nullptr, *big2 = nullptr, *tab = nullptr;
+    unsigned* sink = nullptr;
+    hipStream_t st = nullptr;
+    hipEvent_t e0 = nullptr, e1 = nullptr;
+    const size_t big_bytes = size_t(2) << 30;                    // 2 GiB: 8x the 256 MiB Infinity Cache
+    const size_t nbig = big_bytes / sizeof(float4);
+    const size_t small_table = size_t(2) << 20;                   // 2 MiB: inside one XCD's 4 MiB L2
+    const size_t scene_table = std::max<size_t>(128, std::min<size_t>(scene_table_bytes, size_t(64) << 20)) & ~size_t(127);
+    const size_t tab_bytes = std::max(small_table, scene_table);
+    int cus = 256;
+    {
+        if (device >= 0) PK_TRY(hipSetDevice(device));
+        hipDeviceProp_t prop;
+        int cur = 0;
+        PK_TRY(hipGetDevice(&cur));
+        PK_TRY(hipGetDeviceProperties(&prop, cur));
+        cus = std::max(1, prop.multiProcessorCount);
+        PK_TRY(hipStreamCreateWithFlags(&st, hipStreamNonBlocking));
+        PK_TRY(hipEventCreate(&e0));
+        PK_TRY(hipEventCreate(&e1));
+        PK_TRY(hipMalloc(reinterpret_cast<void**>(&big), big_bytes));
+        PK_TRY(hipMalloc(reinterpret_cast<void**>(&big2), big_bytes));
+        PK_TRY(hipMalloc(reinterpret_cast<void**>(&tab), tab_bytes));
+        PK_TRY(hipMalloc(reinterpret_cast<void**>(&sink), 64));
+        PK_TRY(hipMemsetAsync(big, 0x3c, big_bytes, st));
+        PK_TRY(hipMemsetAsync(big2, 0, big_bytes, st));
+        PK_TRY(hipMemsetAsync(tab, 0x41, tab_bytes, st));
+        auto best_ms = [&](auto launch, int reps) -> float {
+            float best = 1e30f;
+            launch();                                           // warm (and the caches, for the gather)
+            for (int r = 0; r < reps; ++r) {
+                if (hipEventRecord(e0, st) != hipSuccess) return -1.0f;
+                launch();
+                if (hipEventRecord(e1, st) != hipSuccess || hipEventSynchronize(e1) != hipSuccess) return -1.0f;
+                float ms = 0;
+                if (hipEventElapsedTime(&ms, e0, e1) != hipSuccess) return -1.0f;
+                best = std::min(best, ms);
+            }
+            return best;
+        };
+        const dim3 grid(cus * 8), blk(kBlk);
+        float ms = best_ms([&] { hipLaunchKernelGGL(k_copy, grid, blk, 0, st, big, big2, nbig); }, 5);
+        if (ms <= 0) { err = "peaks: copy timing failed"; goto done; }
+        out->hbm_copy_gbps = 2.0 * (double)big_bytes / (ms * 1e-3) / 1e9;
+        ms = best_ms([&] { hipLaunchKernelGGL(k_read, grid, blk, 0, st, big, nbig, sink); }, 5);
+        if (ms <= 0) { err = "peaks: read timing failed"; goto done; }
+        out->hbm_read_gbps = (double)big_bytes / (ms * 1e-3) / 1e9;
+        const int iters = 64;
+        const double gbytes = (double)grid.x * kBlk * iters * 128.0;
+        for (int which = 0; which < 2; ++which) {
+            const size_t tb = which == 0 ? small_table : scene_table;
+            const unsigned nlines = (unsigned)(tb / 128);
+            ms = best_ms([&] { hipLaunchKernelGGL(k_gather<4>, grid, blk, 0, st, tab, nlines, iters, 17u + which, sink); }, 5);
+            if (ms <= 0) { err = "peaks: gather timing failed"; goto done; }
+            const double gbps = gbytes / (ms * 1e-3) / 1e9;
+            if (which == 0) { out->l2_gather_gbps = gbps; out->l2_table_bytes = (double)tb; }
+            else { out->scene_gather_gbps = gbps; out->scene_table_bytes = (double)tb; }
+        }
+        PK_TRY(hipGetLastError());
+    }
+done:
+    if (st) (void)hipStreamSynchronize(st);
+    (void)hipFree(big); (void)hipFree(big2); (void)hipFree(tab); (void)hipFree(sink);
+    if (e0) (void)hipEventDestroy(e0);
+    if (e1) (void)hipEventDestroy(e1);
+    if (st) (void)hipStreamDestroy(st);
+    if (!err.empty()) return rt_internal_set_error(RT_ERR_HIP, err.c_str());
+    return RT_OK;
+}

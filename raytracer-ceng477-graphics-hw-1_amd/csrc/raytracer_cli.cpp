@@ -34,8 +34,10 @@ int die(const char* what) {
 
 int main(int argc, char** argv) {
     // several cameras render as concurrent frame batches, one stream each: give HIP enough hardware
-    // queues that they do not share (read at the runtime's first use; RT_HW_QUEUES overrides)
-    setenv("GPU_MAX_HW_QUEUES", std::getenv("RT_HW_QUEUES") ? std::getenv("RT_HW_QUEUES") : "8", 1);
+    // queues that they do not share (read at the runtime's first use).  RT_HW_QUEUES overrides; a
+    // GPU_MAX_HW_QUEUES the user already set is kept; otherwise 8.
+    if (const char* q = std::getenv("RT_HW_QUEUES")) setenv("GPU_MAX_HW_QUEUES", q, 1);
+    else setenv("GPU_MAX_HW_QUEUES", "8", 0);
     const char* scene_path = nullptr;
     int aa = 2, max_depth = -1000, device = -1, gpus = 0;
     bool write = true;

@@ -148,6 +148,24 @@ struct rt_scene {
     int tune_ublk_h = -1, tune_ublk_w = 8;  // RT_UBLK_H / RT_UBLK_W: phase-A unit column blocks (unit_order;
                                             // H -1: a frame high, 0: row-major units)
     int tune_split = 1;         // RT_SPLIT: a frame runs as this many concurrent interleaved sub-frames (2: +8%, 3: +18% on C3)
+    // RT_WS_BUDGET_MB: HBM for the chain-path workspace arenas of all slots together.  A launch's arena
+    // is sized for the worst case (every sample recording every level), so the budget bounds the
+    // samples per launch (and the frames per frame batch); it is split evenly over the slots.
+    size_t ws_budget = size_t(16) << 30;
+    size_t scene_bytes = 0;     // device bytes of the uploaded scene (trees, primitives, tables)
+    bool ktime = false;         // RT_KTIME: per-kernel times of chain launches (rt_kernel_times; syncs each launch)
+    double kt_ms[rtc::kKKinds] = {};
+    long long kt_launches = 0;
+    rtc::KTimer kt;
+    size_t slot_budget() const { return ws_budget / (size_t)std::max(1, std::min(tune_slots, kSlots)); }
+    // samples whose worst-case chain arena fits one slot's budget (pathchain.hip layout: records, path
+    // word, occlusion bytes, phase-A/B shadow queues and packed lists, continuation queues)
+    size_t slot_samples() const {
+        const size_t levels = (size_t)std::max(dev.max_depth, 0) + 1, nl = (size_t)std::max(dev.nlights, 1);
+        const size_t la = std::min((size_t)std::max(tune_kinline, 0), levels - 1) + 1;
+        const size_t per = levels * (32 + nl) + 4 + la * nl * 12 + 12 + (levels - la) * nl * 8;
+        return std::max<size_t>(4096, slot_budget() / per / 32 * 31);
+    }
     std::string trace_file;     // RT_TRACE: dump per-sample wall-clock timings after each render (diagnostics)
     unsigned* d_trace = nullptr;
     size_t trace_cap = 0;
@@ -199,6 +217,8 @@ struct rt_scene {
             if (slot_done[i]) (void)hipEventDestroy(slot_done[i]);
         }
         if (fork_ev) (void)hipEventDestroy(fork_ev);
+        for (auto& e : kt.ev)
+            if (e) (void)hipEventDestroy(e);
         (void)hipFree(batch_out);
         (void)hipFree(d_pairs); (void)hipFree(d_leafbig); (void)hipFree(d_spairs); (void)hipFree(d_swnodes); (void)hipFree(d_wnodes); (void)hipFree(d_lrec);
         (void)hipFree(d_nodes); (void)hipFree(d_prims); (void)hipFree(d_tri); (void)hipFree(d_mats); (void)hipFree(d_lights);
@@ -276,8 +296,14 @@ int upload_scene(rt_scene* s, const rt_options* opts) {
     if ((rc = upload(&s->d_swnodes, s->bvh.swnodes))) return rc;
     if ((rc = upload(&s->d_wnodes, s->bvh.wnodes))) return rc;
     if ((rc = upload(&s->d_lrec, s->bvh.lrec))) return rc;
-    HIP_TRY(hipMalloc(reinterpret_cast<void**>(&s->d_counters), 8 * sizeof(unsigned long long)));
-    HIP_TRY(hipMemset(s->d_counters, 0, 8 * sizeof(unsigned long long)));
+    {
+        auto vb = [](const auto& v) { return v.size() * sizeof(v[0]); };
+        s->scene_bytes = vb(s->bvh.nodes) + vb(s->bvh.prims) + vb(s->bvh.tri_shade) + vb(mats) + vb(lights) +
+                         vb(s->bvh.pairs) + vb(s->bvh.leaf_big) + vb(s->bvh.spairs) + vb(s->bvh.swnodes) +
+                         vb(s->bvh.wnodes) + vb(s->bvh.lrec);
+    }
+    HIP_TRY(hipMalloc(reinterpret_cast<void**>(&s->d_counters), rtc::kCounters * sizeof(unsigned long long)));
+    HIP_TRY(hipMemset(s->d_counters, 0, rtc::kCounters * sizeof(unsigned long long)));
     HIP_TRY(hipMalloc(reinterpret_cast<void**>(&s->d_err), sizeof(unsigned)));
     HIP_TRY(hipMemset(s->d_err, 0, sizeof(unsigned)));
     HIP_TRY(hipEventCreate(&s->ev0));
@@ -338,6 +364,9 @@ int upload_scene(rt_scene* s, const rt_options* opts) {
     if (const char* e = std::getenv("RT_PROD")) s->tune_producers = std::max(1, std::min(4, std::atoi(e)));
     if (const char* e = std::getenv("RT_CREFILL")) s->tune_crefill = std::max(0, std::min(63, std::atoi(e)));
     if (const char* e = std::getenv("RT_TRACE")) s->trace_file = e;
+    s->ktime = std::getenv("RT_KTIME") && std::atoi(std::getenv("RT_KTIME")) != 0;
+    if (const char* e = std::getenv("RT_WS_BUDGET_MB"))
+        s->ws_budget = std::max<size_t>(64, std::strtoull(e, nullptr, 10)) << 20;
 
     rtk::DevScene& d = s->dev;
     d.nodes = s->d_nodes; d.prims = s->d_prims; d.tri_shade = s->d_tri; d.mats = s->d_mats; d.lights = s->d_lights;
@@ -381,6 +410,14 @@ int upload_scene(rt_scene* s, const rt_options* opts) {
     d.use_wide = !s->bvh.nodes.empty() && !s->bvh.lrec.empty() &&
                  (!s->bvh.wnodes.empty() || (s->bvh.root_info < 0 && s->bvh.root_lrec >= 0));
     if (const char* e = std::getenv("RT_WIDE_WALK")) d.use_wide = d.use_wide && std::atoi(e) != 0;
+    // experiment (RT_SHADOW_ON_REF=1): any-hit walks on the reference-order wide tree instead of the SAH
+    // occlusion tree (exact either way: any hit is order-free and both trees hold the same leaf records);
+    // one tree means a smaller walk hot set
+    if (std::getenv("RT_SHADOW_ON_REF") && std::atoi(std::getenv("RT_SHADOW_ON_REF")) && !s->bvh.wnodes.empty() &&
+        d.use_stree == 2) {
+        d.swnodes = s->d_wnodes;
+        d.swroot = s->bvh.wroot;
+    }
     d.err = s->d_err;
     {   // walk_runaway: 64 x (every node of the largest tree + leaves); RT_WALK_CAP overrides (tests)
         const long long nodes = (long long)s->bvh.pairs.size() + s->bvh.leaves + 64;   // the largest tree
@@ -530,8 +567,9 @@ int render_wavefront(rt_scene* s, const rtk::Eye& eye, const rtk::FrameParams& f
 }
 
 // Chain path: chunks of whole 8*aa-row groups, workspace sized for the worst
-// case (every sample recording every level) so no queue can overflow.
-constexpr size_t kChainBudgetBytes = size_t(24) << 30;   // per workspace slot (6 slots: at most 144 of 288 GB HBM)
+// case (every sample recording every level) so no queue can overflow; the
+// arenas of all slots together stay within the scene's workspace budget
+// (rt_scene::ws_budget, RT_WS_BUDGET_MB).
 
 // Bump layout of the chain-path workspace (one device arena, grown on demand).
 struct ArenaLayout {
@@ -542,6 +580,17 @@ struct ArenaLayout {
         off += (std::max<size_t>(n, 1) * sizeof(T) + 255) & ~size_t(255);
         return o;
     }
+};
+
+// Sizes of one chain-path launch of `units` row units (phase split, queue capacities, grids).
+struct ChainPlan {
+    size_t cap = 0;                 // samples of the launch
+    int G = 1, gb = 0, levels_a = 1, kinline = 0;
+    bool phase_b = false, split_occ = false;
+    unsigned dyn_units = 0, scapA = 0, ccapA = 0, scapB = 0, wq_cap = 0;
+    // arena offsets
+    size_t o_rec = 0, o_pinfo = 0, o_occ = 0, o_sqA = 0, o_scntA = 0, o_sflatA = 0, o_cq = 0, o_ccnt = 0,
+           o_cflat = 0, o_sqB = 0, o_scntB = 0, o_sflatB = 0, o_totals = 0, o_wq = 0, bytes = 0;
 };
 
 int render_chain(rt_scene* s, const rtk::Eye& eye, const rtk::FrameParams& f, bool count, hipStream_t st,
@@ -555,15 +604,83 @@ int render_chain(rt_scene* s, const rtk::Eye& eye, const rtk::FrameParams& f, bo
     const int unit = 8 * f.aa;
     const size_t unit_samples = (size_t)tiles_x * f.aa * 64;
     const size_t units_total = (size_t)(li + unit - 1) / unit;
-    const size_t per_sample = (size_t)levels * (32 + 8 * nl + nl) + 16;   // 32-B hit records (pathchain.hip)
-    const size_t id_limit = (size_t)(INT32_MAX - 1) / ((size_t)levels * nl);   // u32 task owner ids (pathchain.hpp)
-    const size_t target = std::max<size_t>(
-        unit_samples, std::min({s->chunk_samples, kChainBudgetBytes / per_sample, id_limit}));
-    const size_t units = std::min(units_total, std::max<size_t>(1, target / unit_samples));
-    const int chunk_rows = (int)units * unit;
-    const size_t cap = units * unit_samples;
-    if (cap * levels * nl >= (size_t)INT32_MAX) return fail(RT_ERR_LIMIT, "frame chunk too large for the chain path");
     const bool fused = s->path == rt_scene::kFused;
+    if (s->chain_grid == 0) {
+        int cb = 0, mb = 0, ob = 0, fb = 0;
+        HIP_TRY(rtc::chain_occupancy(&cb, &mb, &ob));
+        HIP_TRY(rtc::fused_occupancy(&fb));
+        s->chain_grid = std::min(rtc::kMaxChainGrid, std::max(1, cb) * s->num_cus);
+        s->mix_grid = std::max(1, mb) * s->num_cus;
+        s->occl_grid = std::max(1, ob) * s->num_cus;
+        s->fused_grid = std::max(1, fb) * s->num_cus;
+        if (const char* e = std::getenv("RT_CGRID")) s->chain_grid = std::max(1, std::min(rtc::kMaxChainGrid, std::atoi(e)));
+        if (const char* e = std::getenv("RT_OGRID")) s->occl_grid = std::max(1, std::atoi(e));
+        if (const char* e = std::getenv("RT_MGRID")) s->mix_grid = std::max(2, std::atoi(e));
+    }
+    const int max_grid = fused ? s->fused_grid : s->chain_grid;
+    auto grid_for = [&](int n0) { return std::max(1, std::min(max_grid, (n0 + 255) / 256)); };
+    // Every size of a launch of `units` row units, and its arena layout: worst-case queue sizing (every
+    // sample recording every level), so no queue can overflow.
+    auto plan = [&](size_t nunits) {
+        ChainPlan P;
+        P.cap = nunits * unit_samples;
+        const size_t cap = P.cap;
+        P.G = grid_for((int)std::min<size_t>(cap, INT32_MAX));
+        // phase split: A walks levels [0, kinline], B the rest (k_mix chain role, gb workgroups)
+        P.kinline = std::max(0, s->tune_kinline);
+        P.phase_b = P.kinline < s->dev.max_depth;
+        // phase-B workgroups: a lone frame's deep chains are its critical path (1.5625 per CU best);
+        // in frame batches other frames hide them and the shadow role wants the CUs (C3: 0.5 per CU
+        // 0.550 ms/frame, 0.75 0.552, 1 0.554, 1.25 0.557, 1.5625 0.568)
+        // frame batches: A's shadow rays in their own 5-wave k_occlude launch (split_occ) and 1 phase-B
+        // workgroup per CU (6 slots in flight: 0.504-0.512 -> 0.495 ms/frame; 0.5 per CU 0.500, 2 0.4995)
+        P.split_occ = f.nframes > 1 && (!std::getenv("RT_SPLIT_OCC") || std::atoi(std::getenv("RT_SPLIT_OCC")));
+        const int gb_default = f.nframes > 1 ? (P.split_occ ? s->num_cus : s->num_cus / 2) : 25 * s->num_cus / 16;
+        P.gb = P.phase_b ? std::max(1, std::min(s->mix_grid - 1, s->tune_gb > 0 ? s->tune_gb : gb_default)) : 0;
+        P.levels_a = std::min(P.kinline, std::max(s->dev.max_depth, 0)) + 1;
+        // dynamic phase-A units: a workgroup may take up to twice its static share (at most
+        // rtc::kDynUnits), and its queues are sized for that
+        const unsigned share = rtc::chain_block_units((int)std::min<size_t>(cap, INT32_MAX), P.G);
+        P.dyn_units = s->tune_dyn && share <= (unsigned)rtc::kDynUnits ? std::min(2u * share, (unsigned)rtc::kDynUnits) : 0u;
+        const unsigned units_a = P.dyn_units ? P.dyn_units : share;
+        P.scapA = units_a * 256u * (unsigned)(P.levels_a * nl);
+        P.ccapA = units_a * 256u;
+        P.scapB = P.phase_b ? (unsigned)(((cap + P.gb - 1) / P.gb) * (size_t)(levels - P.levels_a) * nl) : 0u;
+        P.wq_cap = fused ? rtc::fused_wave_qcap((int)std::min<size_t>(cap, INT32_MAX), P.G, levels, nl) : 0u;
+        ArenaLayout L;
+        P.o_rec = L.take<float4>(2 * cap * levels);
+        P.o_pinfo = L.take<int>(cap);
+        P.o_occ = L.take<uint8_t>(cap * levels * nl + 8);   // + 8: k_finish reads aligned dwords
+        if (fused) {
+            P.o_wq = L.take<unsigned>((size_t)P.G * 4 * P.wq_cap);
+        } else {
+            P.o_sqA = L.take<unsigned>((size_t)P.G * P.scapA); P.o_scntA = L.take<unsigned>(P.G);
+            P.o_sflatA = L.take<unsigned>(cap * P.levels_a * nl);
+            P.o_cq = L.take<unsigned>((size_t)P.G * P.ccapA); P.o_ccnt = L.take<unsigned>(P.G);
+            P.o_cflat = L.take<unsigned>(cap);
+            P.o_sqB = L.take<unsigned>((size_t)P.gb * P.scapB); P.o_scntB = L.take<unsigned>(P.gb + 1);
+            P.o_sflatB = L.take<unsigned>(cap * (levels - P.levels_a) * nl); P.o_totals = L.take<unsigned>(4);
+        }
+        P.bytes = L.off;
+        return P;
+    };
+    // Launch size: as many row units as the chunk target (RT_CHUNK_SAMPLES), the u32 task ids and the
+    // slot's share of the workspace budget (RT_WS_BUDGET_MB over the slots) allow.
+    const size_t id_limit = (size_t)(INT32_MAX - 1) / ((size_t)levels * nl);   // u32 task owner ids (pathchain.hpp)
+    size_t units = std::min(units_total, std::max<size_t>(1, std::min(s->chunk_samples, id_limit) / unit_samples));
+    const size_t budget = s->slot_budget();
+    if (plan(units).bytes > budget) {
+        size_t lo = 1, hi = units;                 // largest units in [1, units] whose arena fits the budget
+        while (lo < hi) {
+            const size_t mid = lo + (hi - lo + 1) / 2;
+            if (plan(mid).bytes <= budget) lo = mid; else hi = mid - 1;
+        }
+        units = lo;
+    }
+    const ChainPlan P = plan(units);
+    const int chunk_rows = (int)units * unit;
+    const size_t cap = P.cap;
+    if (cap * levels * nl >= (size_t)INT32_MAX) return fail(RT_ERR_LIMIT, "frame chunk too large for the chain path");
     // A frame of several chunks (C5: 17 of 32 M samples): chunks on the workspace slots' streams
     // (chunk j on slot j mod K), so one chunk's tail overlaps the next chunks' bulk.  Chunks write
     // disjoint output rows.
@@ -586,89 +703,37 @@ int render_chain(rt_scene* s, const rtk::Eye& eye, const rtk::FrameParams& f, bo
         }
         return RT_OK;
     }
-    if (s->chain_grid == 0) {
-        int cb = 0, mb = 0, ob = 0, fb = 0;
-        HIP_TRY(rtc::chain_occupancy(&cb, &mb, &ob));
-        HIP_TRY(rtc::fused_occupancy(&fb));
-        s->chain_grid = std::min(rtc::kMaxChainGrid, std::max(1, cb) * s->num_cus);
-        s->mix_grid = std::max(1, mb) * s->num_cus;
-        s->occl_grid = std::max(1, ob) * s->num_cus;
-        s->fused_grid = std::max(1, fb) * s->num_cus;
-        if (const char* e = std::getenv("RT_CGRID")) s->chain_grid = std::max(1, std::min(rtc::kMaxChainGrid, std::atoi(e)));
-        if (const char* e = std::getenv("RT_OGRID")) s->occl_grid = std::max(1, std::atoi(e));
-        if (const char* e = std::getenv("RT_MGRID")) s->mix_grid = std::max(2, std::atoi(e));
-    }
-    const int max_grid = fused ? s->fused_grid : s->chain_grid;
-    auto grid_for = [&](int n0) { return std::max(1, std::min(max_grid, (n0 + 255) / 256)); };
-    const int G = grid_for((int)cap);
-    // phase split: A walks levels [0, kinline], B the rest (k_mix chain role, gb workgroups)
-    const int kinline = std::max(0, s->tune_kinline);
-    const bool phase_b = kinline < s->dev.max_depth;
-    // phase-B workgroups: a lone frame's deep chains are its critical path (1.5625 per CU best);
-    // in frame batches other frames hide them and the shadow role wants the CUs (C3: 0.5 per CU
-    // 0.550 ms/frame, 0.75 0.552, 1 0.554, 1.25 0.557, 1.5625 0.568)
-    // frame batches: A's shadow rays in their own 5-wave k_occlude launch (split_occ) and 1 phase-B
-    // workgroup per CU (6 slots in flight: 0.504-0.512 -> 0.495 ms/frame; 0.5 per CU 0.500, 2 0.4995)
-    const bool split_occ = f.nframes > 1 && (!std::getenv("RT_SPLIT_OCC") || std::atoi(std::getenv("RT_SPLIT_OCC")));
-    const int gb_default = f.nframes > 1 ? (split_occ ? s->num_cus : s->num_cus / 2) : 25 * s->num_cus / 16;
-    const int gb = phase_b ? std::max(1, std::min(s->mix_grid - 1, s->tune_gb > 0 ? s->tune_gb : gb_default)) : 0;
-    const int levels_a = std::min(kinline, std::max(s->dev.max_depth, 0)) + 1;
-    // dynamic phase-A units: a workgroup may take up to twice its static share (at most
-    // rtc::kDynUnits), and its queues are sized for that
-    const unsigned share = rtc::chain_block_units((int)cap, G);
-    const unsigned dyn_units = s->tune_dyn && share <= (unsigned)rtc::kDynUnits
-                                   ? std::min(2u * share, (unsigned)rtc::kDynUnits) : 0u;
-    const unsigned units_a = dyn_units ? dyn_units : share;
-    const unsigned scapA = units_a * 256u * (unsigned)(levels_a * nl);
-    const unsigned ccapA = units_a * 256u;
-    const unsigned scapB = phase_b ? (unsigned)(((cap + gb - 1) / gb) * (size_t)(levels - levels_a) * nl) : 0u;
-    const unsigned wq_cap = fused ? rtc::fused_wave_qcap((int)cap, G, levels, nl) : 0u;
-
-    ArenaLayout L;
-    const size_t o_rec = L.take<float4>(2 * cap * levels), o_pinfo = L.take<int>(cap),
-                 o_occ = L.take<uint8_t>(cap * levels * nl + 8);   // + 8: k_finish reads aligned dwords
-    size_t o_sqA = 0, o_scntA = 0, o_sflatA = 0, o_cq = 0, o_ccnt = 0, o_cflat = 0, o_sqB = 0, o_scntB = 0,
-           o_sflatB = 0, o_totals = 0, o_wq = 0;
-    if (fused) {
-        o_wq = L.take<unsigned>((size_t)G * 4 * wq_cap);
-    } else {
-        o_sqA = L.take<unsigned>((size_t)G * scapA); o_scntA = L.take<unsigned>(G);
-        o_sflatA = L.take<unsigned>(cap * levels_a * nl);
-        o_cq = L.take<unsigned>((size_t)G * ccapA); o_ccnt = L.take<unsigned>(G); o_cflat = L.take<unsigned>(cap);
-        o_sqB = L.take<unsigned>((size_t)gb * scapB); o_scntB = L.take<unsigned>(gb + 1);
-        o_sflatB = L.take<unsigned>(cap * (levels - levels_a) * nl); o_totals = L.take<unsigned>(4);
-    }
     // order this use after the arena's previous one (possibly on another stream)
     if (arena.last && arena.last_stream != st) HIP_TRY(hipStreamWaitEvent(st, arena.last, 0));
-    if (arena.bytes < L.off) {
+    if (arena.bytes < P.bytes) {
         if (arena.p) HIP_TRY(hipStreamSynchronize(st));   // the previous frames on it may still use it
         (void)hipFree(arena.p);
         arena.p = nullptr;
         arena.bytes = 0;
-        HIP_TRY(hipMalloc(reinterpret_cast<void**>(&arena.p), L.off));
-        arena.bytes = L.off;
+        HIP_TRY(hipMalloc(reinterpret_cast<void**>(&arena.p), P.bytes));
+        arena.bytes = P.bytes;
     }
     auto at = [&](size_t o) { return static_cast<void*>(arena.p + o); };
     rtc::PcParams p{};
     p.width = f.width; p.height = f.height; p.aa = f.aa; p.stripe_rows = f.stripe_rows;
     p.rank = f.rank; p.nranks = f.nranks; p.slab_rows = f.slab_rows;
     p.wi = wi; p.tiles_x = tiles_x; p.cap = (int)cap; p.levels = levels; p.nlights = s->dev.nlights;
-    p.rec = static_cast<float4*>(at(o_rec));
-    p.pinfo = static_cast<int*>(at(o_pinfo));
-    p.occ = static_cast<uint8_t*>(at(o_occ));
-    p.sqA = static_cast<unsigned*>(at(o_sqA)); p.scapA = scapA;
-    p.scntA = static_cast<unsigned*>(at(o_scntA)); p.sflatA = static_cast<unsigned*>(at(o_sflatA));
-    p.cq = static_cast<unsigned*>(at(o_cq)); p.ccapA = ccapA;
-    p.ccnt = static_cast<unsigned*>(at(o_ccnt)); p.cflat = static_cast<unsigned*>(at(o_cflat));
-    p.sqB = static_cast<unsigned*>(at(o_sqB)); p.scapB = scapB;
-    p.scntB = static_cast<unsigned*>(at(o_scntB)); p.sflatB = static_cast<unsigned*>(at(o_sflatB));
-    p.totals = static_cast<unsigned*>(at(o_totals));
-    p.kinline = phase_b ? kinline : 1 << 30;
-    p.gb = gb;
-    p.ogrid = phase_b ? std::max(1, s->mix_grid - gb) : s->mix_grid;
+    p.rec = static_cast<float4*>(at(P.o_rec));
+    p.pinfo = static_cast<int*>(at(P.o_pinfo));
+    p.occ = static_cast<uint8_t*>(at(P.o_occ));
+    p.sqA = static_cast<unsigned*>(at(P.o_sqA)); p.scapA = P.scapA;
+    p.scntA = static_cast<unsigned*>(at(P.o_scntA)); p.sflatA = static_cast<unsigned*>(at(P.o_sflatA));
+    p.cq = static_cast<unsigned*>(at(P.o_cq)); p.ccapA = P.ccapA;
+    p.ccnt = static_cast<unsigned*>(at(P.o_ccnt)); p.cflat = static_cast<unsigned*>(at(P.o_cflat));
+    p.sqB = static_cast<unsigned*>(at(P.o_sqB)); p.scapB = P.scapB;
+    p.scntB = static_cast<unsigned*>(at(P.o_scntB)); p.sflatB = static_cast<unsigned*>(at(P.o_sflatB));
+    p.totals = static_cast<unsigned*>(at(P.o_totals));
+    p.kinline = P.phase_b ? P.kinline : 1 << 30;
+    p.gb = P.gb;
+    p.ogrid = P.phase_b ? std::max(1, s->mix_grid - P.gb) : s->mix_grid;
     p.occ_grid = s->occl_grid;
     p.fin_grid = s->tune_fgrid > 0 ? s->tune_fgrid : 8 * s->num_cus;
-    p.split_occ = split_occ ? 1 : 0;
+    p.split_occ = P.split_occ ? 1 : 0;
     p.refill = s->tune_refill >= 0 ? s->tune_refill : 0;
     p.service = s->tune_service >= 0 ? s->tune_service : 64;
     p.bservice = s->tune_bservice;
@@ -686,12 +751,12 @@ int render_chain(rt_scene* s, const rtk::Eye& eye, const rtk::FrameParams& f, bo
     p.exp_skip_occ = std::getenv("RT_EXP_SKIP_OCC") ? 1 : 0;
     p.shade_split = std::getenv("RT_SHADE_SPLIT") ? std::atoi(std::getenv("RT_SHADE_SPLIT")) : 0;
     p.spread = s->tune_spread;
-    p.dyn_units = (int)dyn_units;
+    p.dyn_units = (int)P.dyn_units;
     p.ublk_h = s->tune_ublk_h;
     p.ublk_w = std::max(1, s->tune_ublk_w);
     p.crefill = s->tune_crefill;
-    p.wq = static_cast<unsigned*>(at(o_wq));
-    p.wq_cap = wq_cap;
+    p.wq = static_cast<unsigned*>(at(P.o_wq));
+    p.wq_cap = P.wq_cap;
     p.out = f.out; p.counters = f.counters;
     p.out_k = f.out_k; p.out_j = f.out_j;
     p.nframes = std::max(1, f.nframes);
@@ -711,9 +776,25 @@ int render_chain(rt_scene* s, const rtk::Eye& eye, const rtk::FrameParams& f, bo
         p.chunk_rows = std::min(chunk_rows, li - r0);
         p.n0 = tiles_x * ((p.chunk_rows + 7) / 8) * 64;
         p.grid = grid_for(p.n0);
-        if (p.grid > G) return fail(RT_ERR_LIMIT, "internal: chain grid exceeds the workspace");
-        if (fused) HIP_TRY(rtc::launch_fused_chunk(s->dev, eye, p, count, st));
-        else HIP_TRY(rtc::launch_chain_chunk(s->dev, eye, p, count, st));
+        if (p.grid > P.G) return fail(RT_ERR_LIMIT, "internal: chain grid exceeds the workspace");
+        if (fused) {
+            HIP_TRY(rtc::launch_fused_chunk(s->dev, eye, p, count, st));
+        } else if (s->ktime) {
+            // diagnostics: events between the kernels, then the launch's per-kernel split (synchronous)
+            for (int i = 0; i < rtc::KTimer::kMax; ++i)
+                if (!s->kt.ev[i]) HIP_TRY(hipEventCreate(&s->kt.ev[i]));
+            s->kt.n = 0;
+            HIP_TRY(rtc::launch_chain_chunk(s->dev, eye, p, count, st, &s->kt));
+            HIP_TRY(hipEventSynchronize(s->kt.ev[s->kt.n - 1]));
+            for (int i = 0; i + 1 < s->kt.n; ++i) {
+                float ms = 0;
+                HIP_TRY(hipEventElapsedTime(&ms, s->kt.ev[i], s->kt.ev[i + 1]));
+                s->kt_ms[s->kt.kind[i]] += ms;
+            }
+            s->kt_launches++;
+        } else {
+            HIP_TRY(rtc::launch_chain_chunk(s->dev, eye, p, count, st));
+        }
     }
     if (p.trace) trace_dump(s, st, 0, (unsigned)cap, (unsigned)p.trace_blocks, trace_n);   // last chunk only
     if (!arena.last) HIP_TRY(hipEventCreateWithFlags(&arena.last, hipEventDisableTiming));
@@ -854,6 +935,10 @@ int rt_scene_bvh_info(const rt_scene* s, rt_bvh_info* info) {
     mix(&s->bvh.swroot, sizeof(s->bvh.swroot));
     mix(&s->bvh.wroot, sizeof(s->bvh.wroot));
     info->wide_hash = h;
+    info->ref_wide_bytes = s->bvh.wnodes.size() * sizeof(dl::Wide);
+    info->occ_wide_bytes = s->bvh.swnodes.size() * sizeof(dl::Wide);
+    info->leaf_record_bytes = s->bvh.lrec.size() * sizeof(dl::Vec4);
+    info->tri_shade_bytes = s->bvh.tri_shade.size() * sizeof(dl::TriShade);
     return RT_OK;
 }
 
@@ -871,6 +956,15 @@ int rt_scene_export_nodes(const rt_scene* s, void* out, int capacity) {
     const int n = (int)s->bvh.nodes.size();
     if (out && capacity > 0) std::memcpy(out, s->bvh.nodes.data(), (size_t)std::min(n, capacity) * sizeof(dl::Node));
     return n;
+}
+
+int rt_scene_memory(const rt_scene* s, uint64_t* scene_bytes, uint64_t* workspace_bytes) {
+    if (!s) return fail(RT_ERR_ARG, "scene is NULL");
+    size_t ws = s->ws.bytes + s->out_cap + s->batch_out_cap + s->trace_cap * sizeof(unsigned);
+    for (const auto& a : s->arenas) ws += a.bytes;
+    if (scene_bytes) *scene_bytes = s->host_only ? 0 : s->scene_bytes;
+    if (workspace_bytes) *workspace_bytes = ws;
+    return RT_OK;
 }
 
 int rt_slab_rows(int height, int stripe_rows, int nranks) {
@@ -1018,7 +1112,7 @@ int render_cameras(rt_scene* s, const rt_camera* cams, int n, int aa, void* cons
             int j = i + 1;
             while (j < n && j - i < bmax &&
                    cams[j].image_width == c.image_width && cams[j].image_height == c.image_height &&
-                   (long long)(j - i + 1) * per <= (long long)s->chunk_samples)
+                   (long long)(j - i + 1) * per <= (long long)std::min(s->chunk_samples, s->slot_samples()))
                 ++j;
             starts.push_back(i);
             i = j;
@@ -1113,15 +1207,23 @@ int rt_render_cameras(rt_scene* s, const rt_camera* cams, int n, int aa, uint8_t
         if (!outs[i]) return fail(RT_ERR_ARG, "output buffer is NULL");
     }
     const auto t0 = std::chrono::steady_clock::now();
-    if (s->group) {                  // device group: the cameras one after another, each frame on every device
+    if (s->group) {
+        // device group: runs of consecutive same-size cameras as frame batches (every device renders its
+        // stripes of all of them in flight together, one grouped gather per run)
         rt_stats sum{}, one{};
-        for (int i = 0; i < n; ++i) {
-            const int rc = rt_internal_group_render(s->group, &cams[i], aa, outs[i], stats ? &one : nullptr);
+        for (int i = 0; i < n;) {
+            int j = i + 1;
+            while (j < n && j - i < rtc::kMaxFrames && cams[j].image_width == cams[i].image_width &&
+                   cams[j].image_height == cams[i].image_height)
+                ++j;
+            const int rc = rt_internal_group_render_frames(s->group, cams + i, j - i, aa, outs + i,
+                                                           stats ? &one : nullptr);
             if (rc) return rc;
             sum.primary_rays += one.primary_rays; sum.shadow_rays += one.shadow_rays;
             sum.reflection_rays += one.reflection_rays; sum.node_visits += one.node_visits;
             sum.tri_tests += one.tri_tests; sum.sphere_tests += one.sphere_tests; sum.kernel_ms += one.kernel_ms;
             sum.shadow_rays_skipped += one.shadow_rays_skipped;
+            i = j;
         }
         if (stats) {
             *stats = sum;
@@ -1145,7 +1247,7 @@ int rt_render_cameras(rt_scene* s, const rt_camera* cams, int n, int aa, uint8_t
     std::vector<void*> dev(n);
     for (int i = 0; i < n; ++i) dev[i] = s->batch_out + off[i];
     const bool count = stats != nullptr;
-    if (count) HIP_TRY(hipMemset(s->d_counters, 0, 8 * sizeof(unsigned long long)));
+    if (count) HIP_TRY(hipMemset(s->d_counters, 0, rtc::kCounters * sizeof(unsigned long long)));
     int rc = render_cameras(s, cams, n, aa, dev.data(), nullptr, count ? RT_RENDER_COUNT : 0);
     if (rc == RT_OK) {
         HIP_TRY(hipDeviceSynchronize());
@@ -1212,8 +1314,30 @@ int rt_unshuffle_stripes(const void* slabs, void* image, int width, int height, 
 int rt_counters_reset(rt_scene* s, void* stream) {
     if (!s) return fail(RT_ERR_ARG, "scene is NULL");
     HIP_TRY(hipSetDevice(s->device));
-    HIP_TRY(hipMemsetAsync(s->d_counters, 0, 8 * sizeof(unsigned long long), static_cast<hipStream_t>(stream)));
+    HIP_TRY(hipMemsetAsync(s->d_counters, 0, rtc::kCounters * sizeof(unsigned long long), static_cast<hipStream_t>(stream)));
     return RT_OK;
+}
+
+int rt_kernel_times(rt_scene* s, double* ms, int n, int reset) {
+    if (!s || !ms || n < 1) return fail(RT_ERR_ARG, "scene/ms is NULL or n < 1");
+    for (int i = 0; i < n; ++i) ms[i] = i < rtc::kKKinds ? s->kt_ms[i] : 0.0;
+    const int launches = (int)std::min<long long>(INT32_MAX, s->kt_launches);
+    if (reset) {
+        for (double& v : s->kt_ms) v = 0;
+        s->kt_launches = 0;
+    }
+    return s->ktime ? launches : fail(RT_ERR_ARG, "kernel timing is off (create the scene with RT_KTIME=1)");
+}
+
+int rt_counters_read_raw(rt_scene* s, uint64_t* out, int n) {
+    if (!s || !out || n < 1) return fail(RT_ERR_ARG, "scene/out is NULL or n < 1");
+    if (s->host_only) return fail(RT_ERR_NO_DEVICE, "scene was created with RT_OPT_HOST_ONLY");
+    HIP_TRY(hipSetDevice(s->device));
+    HIP_TRY(hipDeviceSynchronize());
+    unsigned long long c[rtc::kCounters];
+    HIP_TRY(hipMemcpy(c, s->d_counters, sizeof(c), hipMemcpyDeviceToHost));
+    for (int i = 0; i < n; ++i) out[i] = i < rtc::kCounters ? c[i] : 0;
+    return std::min(n, (int)rtc::kCounters);
 }
 
 int rt_counters_read(rt_scene* s, rt_stats* st) {
@@ -1232,7 +1356,7 @@ int rt_set_devices(int n) {
     if (n >= 1) {
         int count = 0;
         if (hipGetDeviceCount(&count) != hipSuccess || count == 0) return fail(RT_ERR_NO_DEVICE, "no HIP device visible");
-        if (n > count)
+        if (n > count && !(rt_internal_group_virtual() && n <= 16))
             return fail(RT_ERR_ARG, "rt_set_devices(" + std::to_string(n) + "): only " + std::to_string(count) +
                                         " devices visible");
     }
@@ -1271,7 +1395,7 @@ int rt_render(rt_scene* s, const rt_camera* cam, int aa, uint8_t* out_rgb, rt_st
         s->out_cap = bytes;
     }
     const bool count = stats != nullptr;
-    if (count) HIP_TRY(hipMemset(s->d_counters, 0, 8 * sizeof(unsigned long long)));
+    if (count) HIP_TRY(hipMemset(s->d_counters, 0, rtc::kCounters * sizeof(unsigned long long)));
     HIP_TRY(hipEventRecord(s->ev0, nullptr));
     rc = rt_render_device(s, cam, aa, cam->image_height, 0, 1, s->d_out, nullptr, count ? RT_RENDER_COUNT : 0);
     if (rc) return rc;

@@ -94,25 +94,30 @@ int grow(uint8_t** p, size_t* cap, size_t bytes) {
 
 struct rt_group {
     int n = 0;
-    std::vector<rt_scene*> rep;          // rep[0]: the primary scene (not owned); rep[d]: replica on device d
+    bool virt = false;                   // RT_GROUP_VIRTUAL rehearsal: every rank on device 0, copies for the gather
+    std::vector<rt_scene*> rep;          // rep[0]: the primary scene (not owned); rep[d]: replica of rank d
     std::vector<ncclComm_t> comms;       // one communicator over the n devices, rank d on device d
-    std::vector<hipStream_t> streams;    // one render + gather stream per device
-    std::vector<uint8_t*> slabs;         // device d: its stripes, slab_rows * W * 3
+    std::vector<hipStream_t> streams;    // one render + gather stream per rank
+    std::vector<hipEvent_t> joined;      // rank d's gather issued (device 0's stream waits on it)
+    std::vector<uint8_t*> slabs;         // rank d: its stripes of every frame of a batch, frame-major
     std::vector<size_t> slab_cap;
-    uint8_t* gathered = nullptr;         // device 0: n slabs
+    uint8_t* gathered = nullptr;         // device 0: [frame][rank] slabs
     size_t gathered_cap = 0;
-    uint8_t* image = nullptr;            // device 0: the assembled frame
+    uint8_t* image = nullptr;            // device 0: the assembled frames
     size_t image_cap = 0;
-    hipEvent_t ev0 = nullptr, ev1 = nullptr;   // device 0: kernel time of a group frame
+    hipEvent_t ev0 = nullptr, ev1 = nullptr;   // device 0: kernel time of a group call
     int stripe_rows = 8;                 // RT_GROUP_STRIPE
+
+    int dev(int d) const { return virt ? 0 : d; }
 
     ~rt_group() {
         for (int d = 0; d < n; ++d) {
-            (void)hipSetDevice(d);
+            (void)hipSetDevice(dev(d));
             if (d < (int)streams.size() && streams[d]) (void)hipStreamSynchronize(streams[d]);
             if (d < (int)slabs.size()) (void)hipFree(slabs[d]);
             if (d < (int)comms.size() && comms[d] && rccl().comm_destroy) rccl().comm_destroy(comms[d]);
             if (d < (int)streams.size() && streams[d]) (void)hipStreamDestroy(streams[d]);
+            if (d < (int)joined.size() && joined[d]) (void)hipEventDestroy(joined[d]);
         }
         (void)hipSetDevice(0);
         (void)hipFree(gathered);
@@ -126,16 +131,24 @@ struct rt_group {
 
 int rt_internal_group_size(const rt_group* g) { return g ? g->n : 1; }
 
+bool rt_internal_group_virtual() {
+    const char* e = std::getenv("RT_GROUP_VIRTUAL");
+    return e && std::atoi(e) != 0;
+}
+
 int rt_internal_group_create(rt_scene* primary, int n, rt_group** out) {
     *out = nullptr;
+    const bool virt = rt_internal_group_virtual();
     const Rccl& r = rccl();
-    if (!r.error.empty()) return fail(RT_ERR_NO_DEVICE, "multi-GPU group: " + r.error);
+    if (!virt && !r.error.empty()) return fail(RT_ERR_NO_DEVICE, "multi-GPU group: " + r.error);
     rt_group* g = new rt_group();
     g->n = n;
+    g->virt = virt;
     g->rep.assign(n, nullptr);
     g->rep[0] = primary;
     g->comms.assign(n, nullptr);
     g->streams.assign(n, nullptr);
+    g->joined.assign(n, nullptr);
     g->slabs.assign(n, nullptr);
     g->slab_cap.assign(n, 0);
     if (const char* e = std::getenv("RT_GROUP_STRIPE")) g->stripe_rows = std::max(1, std::atoi(e));
@@ -145,22 +158,26 @@ int rt_internal_group_create(rt_scene* primary, int n, rt_group** out) {
         return rc;
     };
     for (int d = 1; d < n; ++d) {
-        const int rc = rt_internal_replicate(primary, d, &g->rep[d]);
+        const int rc = rt_internal_replicate(primary, g->dev(d), &g->rep[d]);
         if (rc) return bail(rc);
     }
     for (int d = 0; d < n; ++d) {
-        if (hipSetDevice(d) != hipSuccess || hipStreamCreateWithFlags(&g->streams[d], hipStreamNonBlocking) != hipSuccess)
-            return bail(fail(RT_ERR_HIP, "multi-GPU group: stream creation failed on device " + std::to_string(d)));
+        if (hipSetDevice(g->dev(d)) != hipSuccess ||
+            hipStreamCreateWithFlags(&g->streams[d], hipStreamNonBlocking) != hipSuccess ||
+            hipEventCreateWithFlags(&g->joined[d], hipEventDisableTiming) != hipSuccess)
+            return bail(fail(RT_ERR_HIP, "multi-GPU group: stream creation failed for rank " + std::to_string(d)));
     }
     (void)hipSetDevice(0);
     if (hipEventCreate(&g->ev0) != hipSuccess || hipEventCreate(&g->ev1) != hipSuccess)
         return bail(fail(RT_ERR_HIP, "multi-GPU group: event creation failed"));
-    std::vector<int> devs(n);
-    for (int d = 0; d < n; ++d) devs[d] = d;
-    const ncclResult_t e = r.comm_init_all(g->comms.data(), n, devs.data());
-    if (e != ncclSuccess) {
-        g->comms.assign(n, nullptr);
-        return bail(nccl_fail("ncclCommInitAll", e));
+    if (!virt) {
+        std::vector<int> devs(n);
+        for (int d = 0; d < n; ++d) devs[d] = d;
+        const ncclResult_t e = r.comm_init_all(g->comms.data(), n, devs.data());
+        if (e != ncclSuccess) {
+            g->comms.assign(n, nullptr);
+            return bail(nccl_fail("ncclCommInitAll", e));
+        }
     }
     (void)hipSetDevice(0);
     *out = g;
@@ -181,49 +198,80 @@ int rt_internal_group_set_max_depth(rt_group* g, int depth) {
     return RT_OK;
 }
 
-int rt_internal_group_render(rt_group* g, const rt_camera* cam, int aa, uint8_t* out_rgb, rt_stats* stats) {
+// nf frames of one size on the group, in flight together: every rank renders its row stripes of all
+// of them as one frame batch (rt_render_frames_device: one persistent grid walks the frames, so one
+// frame's mirror-chain tail overlaps the others' bulk), ONE grouped RCCL call gathers every frame's
+// slabs to device 0 (one ncclGather per frame inside ncclGroupStart/End), device 0 un-interleaves
+// each frame and copies it to outs[f].  nf = 1 is rt_render's frame.
+int rt_internal_group_render_frames(rt_group* g, const rt_camera* cams, int nf, int aa, uint8_t* const* outs,
+                                    rt_stats* stats) {
     const auto t0 = std::chrono::steady_clock::now();
-    const int n = g->n, W = cam->image_width, H = cam->image_height, S = g->stripe_rows;
+    const int n = g->n, W = cams[0].image_width, H = cams[0].image_height, S = g->stripe_rows;
+    for (int f = 1; f < nf; ++f)
+        if (cams[f].image_width != W || cams[f].image_height != H)
+            return fail(RT_ERR_ARG, "internal: a group frame batch mixes image sizes");
     const int rows = rt_slab_rows(H, S, n);
     const size_t slab_bytes = (size_t)rows * W * 3, frame_bytes = (size_t)W * H * 3;
     const int flags = stats ? RT_RENDER_COUNT : 0;
-    // buffers (every stream idle between group frames: each call ends synchronised)
+    // buffers (every stream idle between group calls: each call ends synchronised)
     for (int d = 0; d < n; ++d) {
-        HIP_OK(hipSetDevice(d));
-        int rc = grow(&g->slabs[d], &g->slab_cap[d], slab_bytes);
+        HIP_OK(hipSetDevice(g->dev(d)));
+        int rc = grow(&g->slabs[d], &g->slab_cap[d], slab_bytes * nf);
         if (rc) return rc;
         if (stats && (rc = rt_counters_reset(g->rep[d], g->streams[d]))) return rc;
     }
     HIP_OK(hipSetDevice(0));
-    int rc = grow(&g->gathered, &g->gathered_cap, slab_bytes * n);
-    if (!rc) rc = grow(&g->image, &g->image_cap, frame_bytes);
+    int rc = grow(&g->gathered, &g->gathered_cap, slab_bytes * n * nf);
+    if (!rc) rc = grow(&g->image, &g->image_cap, frame_bytes * nf);
     if (rc) return rc;
     HIP_OK(hipEventRecord(g->ev0, g->streams[0]));
-    // every device renders its stripes (rank d of n), each on its own stream
+    // every rank renders its stripes of every frame (rank d of n), each on its own stream
+    std::vector<void*> ptrs(nf);
     for (int d = 0; d < n; ++d) {
-        rc = rt_render_device(g->rep[d], cam, aa, S, d, n, g->slabs[d], g->streams[d], flags);
+        for (int f = 0; f < nf; ++f) ptrs[f] = g->slabs[d] + f * slab_bytes;
+        rc = nf == 1 ? rt_render_device(g->rep[d], cams, aa, S, d, n, ptrs[0], g->streams[d], flags)
+                     : rt_render_frames_device(g->rep[d], cams, nf, aa, S, d, n, ptrs.data(), g->streams[d], flags);
         if (rc) return rc;
     }
-    // one gather of the uint8 slabs to device 0 over xGMI
-    const Rccl& r = rccl();
-    ncclResult_t e = r.group_start();
-    for (int d = 0; d < n && e == ncclSuccess; ++d)
-        e = r.gather(g->slabs[d], d == 0 ? g->gathered : nullptr, slab_bytes, ncclUint8, 0, g->comms[d], g->streams[d]);
-    const ncclResult_t e2 = r.group_end();
-    if (e != ncclSuccess) return nccl_fail("ncclGather", e);
-    if (e2 != ncclSuccess) return nccl_fail("ncclGroupEnd", e2);
-    // device 0: slabs -> row order, then to the caller's buffer
+    // the uint8 slabs of every frame to device 0 over xGMI: one grouped RCCL call
+    if (g->virt) {               // rehearsal: the ranks share device 0, plain copies stand in for RCCL
+        for (int d = 0; d < n; ++d)
+            for (int f = 0; f < nf; ++f)
+                HIP_OK(hipMemcpyAsync(g->gathered + ((size_t)f * n + d) * slab_bytes, g->slabs[d] + f * slab_bytes,
+                                      slab_bytes, hipMemcpyDeviceToDevice, g->streams[d]));
+    } else {
+        const Rccl& r = rccl();
+        ncclResult_t e = r.group_start();
+        for (int f = 0; f < nf && e == ncclSuccess; ++f)
+            for (int d = 0; d < n && e == ncclSuccess; ++d)
+                e = r.gather(g->slabs[d] + f * slab_bytes, d == 0 ? g->gathered + (size_t)f * n * slab_bytes : nullptr,
+                             slab_bytes, ncclUint8, 0, g->comms[d], g->streams[d]);
+        const ncclResult_t e2 = r.group_end();
+        if (e != ncclSuccess) return nccl_fail("ncclGather", e);
+        if (e2 != ncclSuccess) return nccl_fail("ncclGroupEnd", e2);
+    }
+    for (int d = 1; d < n; ++d) {
+        HIP_OK(hipSetDevice(g->dev(d)));
+        HIP_OK(hipEventRecord(g->joined[d], g->streams[d]));
+        HIP_OK(hipSetDevice(0));
+        HIP_OK(hipStreamWaitEvent(g->streams[0], g->joined[d], 0));
+    }
+    // device 0: slabs -> row order, then to the caller's buffers
     HIP_OK(hipSetDevice(0));
-    rc = rt_unshuffle_stripes(g->gathered, g->image, W, H, S, n, g->streams[0]);
-    if (rc) return rc;
+    for (int f = 0; f < nf; ++f) {
+        rc = rt_unshuffle_stripes(g->gathered + (size_t)f * n * slab_bytes, g->image + f * frame_bytes, W, H, S, n,
+                                  g->streams[0]);
+        if (rc) return rc;
+    }
     HIP_OK(hipEventRecord(g->ev1, g->streams[0]));
-    HIP_OK(hipMemcpyAsync(out_rgb, g->image, frame_bytes, hipMemcpyDeviceToHost, g->streams[0]));
+    for (int f = 0; f < nf; ++f)
+        HIP_OK(hipMemcpyAsync(outs[f], g->image + f * frame_bytes, frame_bytes, hipMemcpyDeviceToHost, g->streams[0]));
     for (int d = 0; d < n; ++d) {
-        HIP_OK(hipSetDevice(d));
+        HIP_OK(hipSetDevice(g->dev(d)));
         HIP_OK(hipStreamSynchronize(g->streams[d]));
     }
     HIP_OK(hipSetDevice(0));
-    // walks cut off by their step bound on any device (rt_scene_check), then the counters
+    // walks cut off by their step bound on any rank (rt_scene_check), then the counters
     rt_stats sum{};
     for (int d = 0; d < n; ++d) {
         if (stats) {
@@ -246,4 +294,9 @@ int rt_internal_group_render(rt_group* g, const rt_camera* cam, int aa, uint8_t*
         stats->wall_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
     }
     return RT_OK;
+}
+
+int rt_internal_group_render(rt_group* g, const rt_camera* cam, int aa, uint8_t* out_rgb, rt_stats* stats) {
+    uint8_t* outs[1] = {out_rgb};
+    return rt_internal_group_render_frames(g, cam, 1, aa, outs, stats);
 }

@@ -80,6 +80,75 @@ def config_xml(name: str) -> str:
     return scene_text(name if name.endswith(".xml") else name + ".xml")
 
 
+def _strtof():
+    """libc strtof: the reference reads its floats with `istream >> float` (parser.cpp), i.e. strtof
+    semantics; a Python float rounded to f32 would round twice."""
+    import ctypes
+    libc = ctypes.CDLL(None)
+    f = libc.strtof
+    f.restype = ctypes.c_float
+    f.argtypes = [ctypes.c_char_p, ctypes.c_void_p]
+    return lambda tok: f(tok.encode(), None)
+
+
+def scene_arrays(text: str) -> dict:
+    """A scene's XML as the plain arrays of rt_scene_desc (include/rt/rt.h), read the way
+    Scene::loadFromXml reads them (parser.cpp:6-218: defaults bg 0 0 0, eps 0.001, depth 0; ids are
+    1-based and implicit by order; `type="mirror"` sets is_mirror), with the triangles in the
+    RayTracer ctor's flattening order (raytracer.cpp:336-341): the standalone <Triangle>s, then each
+    <Mesh>'s faces with the mesh's material.  Cameras are returned beside them (rt_camera fields)."""
+    import xml.etree.ElementTree as ET
+    sf = _strtof()
+    root = ET.fromstring(text)
+
+    def floats(t):
+        return [sf(v) for v in t.split()]
+
+    def ints(t):
+        return [int(v) for v in t.split()]
+
+    def opt(tag, default):
+        e = root.find(tag)
+        return e.text if e is not None else default
+
+    lights_el = root.find("Lights")
+    out = {
+        "background_color": ints(opt("BackgroundColor", "0 0 0"))[:3],
+        "shadow_ray_epsilon": floats(opt("ShadowRayEpsilon", "0.001"))[0],
+        "max_recursion_depth": ints(opt("MaxRecursionDepth", "0"))[0],
+        "ambient_light": floats(lights_el.find("AmbientLight").text)[:3],
+        "lights": [(floats(pl.find("Position").text)[:3], floats(pl.find("Intensity").text)[:3])
+                   for pl in lights_el.findall("PointLight")],
+        "materials": [dict(is_mirror=1 if m.get("type") == "mirror" else 0,
+                           ambient=floats(m.find("AmbientReflectance").text)[:3],
+                           diffuse=floats(m.find("DiffuseReflectance").text)[:3],
+                           specular=floats(m.find("SpecularReflectance").text)[:3],
+                           mirror=floats(m.find("MirrorReflectance").text)[:3],
+                           phong_exponent=floats(m.find("PhongExponent").text)[0])
+                      for m in root.find("Materials").findall("Material")],
+    }
+    vd = floats(root.find("VertexData").text)
+    out["vertices"] = [vd[i:i + 3] for i in range(0, len(vd) - len(vd) % 3, 3)]
+    objs = root.find("Objects")
+    tris = [(int(t.find("Material").text), *ints(t.find("Indices").text)[:3]) for t in objs.findall("Triangle")]
+    for m in objs.findall("Mesh"):
+        mid = int(m.find("Material").text)
+        f = ints(m.find("Faces").text)
+        tris += [(mid, f[i], f[i + 1], f[i + 2]) for i in range(0, len(f) - len(f) % 3, 3)]
+    out["triangles"] = tris
+    out["spheres"] = [(int(s.find("Material").text), int(s.find("Center").text), sf(s.find("Radius").text.strip()))
+                      for s in objs.findall("Sphere")]
+    cams = []
+    for c in root.find("Cameras").findall("Camera"):
+        res = ints(c.find("ImageResolution").text)
+        cams.append(dict(position=floats(c.find("Position").text)[:3], gaze=floats(c.find("Gaze").text)[:3],
+                         up=floats(c.find("Up").text)[:3], near_plane=floats(c.find("NearPlane").text)[:4],
+                         near_distance=floats(c.find("NearDistance").text)[0], image_width=res[0],
+                         image_height=res[1], image_name=c.find("ImageName").text.strip()))
+    out["cameras"] = cams
+    return out
+
+
 def write_config(name: str, directory: str | os.PathLike) -> str:
     """Write the config's XML into `directory`; return its path."""
     d = Path(directory)

@@ -9,8 +9,12 @@ from pathlib import Path
 
 # The production configuration (bench.py, the CLI): 8 HIP hardware queues, so the library runs six
 # workspace slots on streams that do not share queues.  Read when HIP starts, so set before any test
-# touches the GPU; RT_HW_QUEUES overrides.
-os.environ["GPU_MAX_HW_QUEUES"] = os.environ.get("RT_HW_QUEUES", "8")
+# touches the GPU.  RT_HW_QUEUES overrides; a GPU_MAX_HW_QUEUES already in the environment is kept
+# (test_gpu_slots.py runs the slot/arena tests at HIP's default of 4 queues in a child process).
+if os.environ.get("RT_HW_QUEUES"):
+    os.environ["GPU_MAX_HW_QUEUES"] = os.environ["RT_HW_QUEUES"]
+else:
+    os.environ.setdefault("GPU_MAX_HW_QUEUES", "8")
 
 import numpy as np
 import pytest

@@ -1,9 +1,15 @@
 """GPU: the C-ABI's multi-GPU device group (rt_set_devices, rt_multi.cpp) --
-row stripes rendered per device, ONE ncclGather of the uint8 slabs to device 0,
-un-interleave, D2H.  On a one-GPU box the group of one device runs the whole
-path (replica set-up, RCCL communicator, gather, unshuffle, counters); larger
-groups are exercised by the driver's 8-GPU node.  Every image must equal the
-reference golden (raytracer.cpp:487-525 renders, ppm.cpp:4-39 bytes).
+row stripes rendered per device, ONE (grouped) ncclGather of the uint8 slabs to
+device 0, un-interleave, D2H.  On a one-GPU box:
+  * the group of one device runs the whole path with RCCL (replica set-up,
+    communicator, gather, unshuffle, counters);
+  * RT_GROUP_VIRTUAL=1 groups of 2 and 3 ranks, all on device 0, run every part
+    of the N > 1 path (replicas, per-rank streams and slabs, rank-major stripe
+    mapping, frame batches, unshuffle of n slabs, summed counters) except the
+    RCCL call itself, which device copies replace.
+The RCCL gather at N > 1 is UNVERIFIED on hardware here (no multi-GPU box is
+available to this suite).  Every image must equal the reference golden
+(raytracer.cpp:487-525 renders, ppm.cpp:4-39 bytes).
 """
 from __future__ import annotations
 
@@ -70,14 +76,54 @@ def test_group_render_cameras_and_depth_override(group, goldens, pkg, scene_dir)
         for cam in g["cameras"]:
             assert np.array_equal(imgs[cam["camera"]], load_golden_image(cam))
         assert st["primary_rays"] == sum(c["counters"]["primary"] for c in g["cameras"])
-    # MaxRecursionDepth override reaches every replica: C3 scene at depth 2 = the verbatim depth
-    with pkg.Scene.from_xml(config_path(scene_dir, "C3_hm_1080p_d6")) as s, \
-            pkg.Scene.from_xml(config_path(scene_dir, "C3_hm_1080p_d6"), device=0, render_path="chain") as one:
+    # MaxRecursionDepth override reaches every replica: C3 scene at depth 2 on the group = the same
+    # scene at depth 2 on one device without a group
+    with pkg.Scene.from_xml(config_path(scene_dir, "C3_hm_1080p_d6")) as s:
         s.set_max_depth(2)
-        one.set_max_depth(2)
         a, _ = s.render(s.camera(0), aa=1)
+    pkg.set_devices(0)
+    with pkg.Scene.from_xml(config_path(scene_dir, "C3_hm_1080p_d6"), device=0, render_path="chain") as one:
+        assert one.num_devices() == 1
+        one.set_max_depth(2)
         b, _ = one.render(one.camera(0), aa=1)
-        assert np.array_equal(a, b)
+    assert np.array_equal(a, b)
+
+
+@pytest.fixture(params=[2, 3])
+def virtual_group(request, pkg, torch_cuda, monkeypatch):
+    """A rehearsal group of 2 or 3 ranks on device 0 (RT_GROUP_VIRTUAL: copies instead of RCCL)."""
+    monkeypatch.setenv("RT_GROUP_VIRTUAL", "1")
+    pkg.set_devices(request.param)
+    yield request.param
+    pkg.set_devices(0)
+
+
+@pytest.mark.parametrize("stripe", ["8", "5"])
+def test_virtual_group_frames_equal_golden(virtual_group, stripe, goldens, pkg, scene_dir, monkeypatch):
+    """N > 1 group path on one GPU: single frames (rt_render) and frame batches (rt_render_cameras:
+    every rank renders its stripes of a run of same-size cameras in flight together, one grouped
+    gather, per-frame unshuffle) equal the goldens; counters are summed over the ranks."""
+    monkeypatch.setenv("RT_GROUP_STRIPE", stripe)
+    g = golden_by_name(goldens, "C3_hm_1080p_d6_aa1")
+    cam_g = g["cameras"][0]
+    ref = load_golden_image(cam_g)
+    with pkg.Scene.from_xml(config_path(scene_dir, g["config"])) as s:
+        assert s.num_devices() == virtual_group
+        img, st = s.render(s.camera(0), aa=1, stats=True)
+        assert np.array_equal(img, ref)
+        assert _stats(st) == _counters(cam_g["counters"])
+        imgs, st = s.render_cameras([s.camera(0)] * 3, aa=1, stats=True)
+        for im in imgs:
+            assert np.array_equal(im, ref)
+        assert _stats(st) == tuple(3 * v for v in _counters(cam_g["counters"]))
+    g = golden_by_name(goldens, "cornellbox_aa1")
+    with pkg.Scene.from_xml(config_path(scene_dir, g["config"])) as s:
+        cams = [c for c, _ in s.cameras()]
+        order = [1, 2, 0, 2, 1]             # mixed sizes (480^2, 800^2): runs of same-size frames
+        imgs, _ = s.render_cameras([cams[i] for i in order], aa=1)
+        for i, im in zip(order, imgs):
+            cam = next(c for c in g["cameras"] if c["camera"] == i)
+            assert np.array_equal(im, load_golden_image(cam))
 
 
 @pytest.mark.parametrize("name", ["cornellbox_aa1", "car_aa1"])

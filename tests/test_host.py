@@ -32,7 +32,7 @@ def test_library_exports_every_declared_symbol(pkg):
         assert hasattr(L, n), n
     bound = {s[0] for s in pkg._SIGS}
     assert set(names) == bound, "ctypes bindings out of sync with rt.h"
-    assert L.rt_abi_version() == 6
+    assert L.rt_abi_version() == 7
 
 
 def test_cli_binary_built(pkg):
@@ -199,70 +199,25 @@ def test_host_only_scene_cannot_render(pkg, scene_dir):
     assert e.value.code == -5
 
 
-def test_scene_create_from_desc_matches_xml(pkg, oracle, scene_dir):
-    """rt_scene_create with borrowed host arrays builds the same BVH as the XML path."""
-    import xml.etree.ElementTree as ET
-    root = ET.fromstring(pkg.scenes.scene_text("simple.xml"))
-    L = pkg.lib()
-
-    def v3(t):
-        x, y, z = (float(v) for v in t.split())
-        return pkg.Vec3f(x, y, z)
-
-    class Light(ctypes.Structure):
-        _fields_ = [("position", pkg.Vec3f), ("intensity", pkg.Vec3f)]
-
-    class Mat(ctypes.Structure):
-        _fields_ = [("is_mirror", ctypes.c_int), ("ambient", pkg.Vec3f), ("diffuse", pkg.Vec3f),
-                    ("specular", pkg.Vec3f), ("mirror", pkg.Vec3f), ("phong_exponent", ctypes.c_float)]
-
-    class Tri(ctypes.Structure):
-        _fields_ = [("material_id", ctypes.c_int), ("v0_id", ctypes.c_int), ("v1_id", ctypes.c_int),
-                    ("v2_id", ctypes.c_int)]
-
-    class Sph(ctypes.Structure):
-        _fields_ = [("material_id", ctypes.c_int), ("center_vertex_id", ctypes.c_int), ("radius", ctypes.c_float)]
-
-    class Desc(ctypes.Structure):
-        _fields_ = [("background_color", ctypes.c_int * 3), ("shadow_ray_epsilon", ctypes.c_float),
-                    ("max_recursion_depth", ctypes.c_int), ("ambient_light", pkg.Vec3f),
-                    ("lights", ctypes.POINTER(Light)), ("num_lights", ctypes.c_int),
-                    ("materials", ctypes.POINTER(Mat)), ("num_materials", ctypes.c_int),
-                    ("vertices", ctypes.POINTER(pkg.Vec3f)), ("num_vertices", ctypes.c_int),
-                    ("triangles", ctypes.POINTER(Tri)), ("num_triangles", ctypes.c_int),
-                    ("spheres", ctypes.POINTER(Sph)), ("num_spheres", ctypes.c_int)]
-
-    lights = [Light(v3(pl.find("Position").text), v3(pl.find("Intensity").text))
-              for pl in root.find("Lights").findall("PointLight")]
-    mats = [Mat(1 if m.get("type") == "mirror" else 0, v3(m.find("AmbientReflectance").text),
-                v3(m.find("DiffuseReflectance").text), v3(m.find("SpecularReflectance").text),
-                v3(m.find("MirrorReflectance").text), float(m.find("PhongExponent").text))
-            for m in root.find("Materials").findall("Material")]
-    nums = root.find("VertexData").text.split()
-    verts = [pkg.Vec3f(float(nums[i]), float(nums[i + 1]), float(nums[i + 2])) for i in range(0, len(nums), 3)]
-    objs = root.find("Objects")
-    tris = [Tri(int(t.find("Material").text), *[int(v) for v in t.find("Indices").text.split()])
-            for t in objs.findall("Triangle")]
-    for m in objs.findall("Mesh"):
-        f = [int(v) for v in m.find("Faces").text.split()]
-        tris += [Tri(int(m.find("Material").text), f[i], f[i + 1], f[i + 2]) for i in range(0, len(f), 3)]
-    sph = [Sph(int(s.find("Material").text), int(s.find("Center").text), float(s.find("Radius").text))
-           for s in objs.findall("Sphere")]
-    arr = lambda T, xs: (T * len(xs))(*xs)  # noqa: E731
-    d = Desc((ctypes.c_int * 3)(0, 0, 0), 1e-3, 6, v3(root.find("Lights").find("AmbientLight").text),
-             arr(Light, lights), len(lights), arr(Mat, mats), len(mats), arr(pkg.Vec3f, verts), len(verts),
-             arr(Tri, tris), len(tris), arr(Sph, sph), len(sph))
-    h = ctypes.c_void_p()
-    opts = pkg.Options(-1, pkg.RT_OPT_HOST_ONLY)
-    assert L.rt_scene_create(ctypes.byref(d), ctypes.byref(opts), ctypes.byref(h)) == 0, L.rt_last_error()
-    s = pkg.Scene(h.value)
-    ref = oracle.OracleScene(config_path(scene_dir, "simple.xml")).export_nodes()
+@pytest.mark.parametrize("config", ["simple.xml", "C2_cornellbox_800_d0", "C3_hm_1080p_d6"])
+def test_scene_create_from_desc_matches_xml(pkg, oracle, scene_dir, config):
+    """rt_scene_create with borrowed host arrays (the reference's flattening order,
+    raytracer.cpp:336-341) builds the same BVH as the XML path and the oracle."""
+    arrays = pkg.scenes.scene_arrays(pkg.scenes.config_xml(config))
+    s = pkg.Scene.from_desc(arrays, host_only=True)
+    x = pkg.Scene.from_xml(config_path(scene_dir, config), host_only=True)
+    ref = oracle.OracleScene(config_path(scene_dir, config)).export_nodes()
     assert s.export_nodes().tobytes() == ref.tobytes()
+    assert s.bvh_info()["wide_hash"] == x.bvh_info()["wide_hash"]
+    cams = x.cameras()
+    assert len(cams) == len(arrays["cameras"])
+    for (c, name), a in zip(cams, arrays["cameras"]):
+        assert bytes(c) == bytes(pkg.camera_from(a)) and name == a["image_name"]
     # an out-of-range vertex id is rejected with RT_ERR_ARG
-    tris[0].v0_id = 999
-    d.triangles = arr(Tri, tris)
-    h2 = ctypes.c_void_p()
-    assert L.rt_scene_create(ctypes.byref(d), ctypes.byref(opts), ctypes.byref(h2)) == -1
+    arrays["triangles"][0] = (arrays["triangles"][0][0], 999999, 1, 2)
+    with pytest.raises(pkg.RtError) as e:
+        pkg.Scene.from_desc(arrays, host_only=True)
+    assert e.value.code == -1
 
 
 def test_phong_pow_matches_glibc_pow(tmp_path):
