@@ -249,16 +249,19 @@ int rt_scene_memory(const rt_scene* scene, uint64_t* scene_bytes, uint64_t* work
  * current one), ~1 s, allocates 4 GiB + the tables temporarily:
  *   hbm_copy_gbps      streaming float4 copy of 2 GiB (read + write bytes / time)
  *   hbm_read_gbps      the same buffer read only
- *   l2_gather_gbps     the BVH walks' access shape: every lane reads whole random
+ *   l2_gather_gbps     the BVH walks' divergent fetch: every lane reads whole random
  *                      128-B lines (eight dwordx4) of a table every workgroup shares,
- *                      4 lines in flight per lane; table of l2_table_bytes (2 MiB,
+ *                      2 lines in flight per lane; table of l2_table_bytes (2 MiB,
  *                      inside one XCD's 4 MiB L2)
  *   scene_gather_gbps  the same over a table of scene_table_bytes (the caller's
- *                      walk hot set; lines beyond L2 come from the Infinity Cache) */
+ *                      walk hot set; lines beyond L2 come from the Infinity Cache)
+ *   l2_line_gbps,      the same bytes with 8 lanes reading the 8 pieces of one line
+ *   scene_line_gbps    (full-line fetches: the L2's deliverable bandwidth) */
 typedef struct rt_peaks {
     double hbm_copy_gbps, hbm_read_gbps;
     double l2_gather_gbps, l2_table_bytes;
     double scene_gather_gbps, scene_table_bytes;
+    double l2_line_gbps, scene_line_gbps;
 } rt_peaks;
 int rt_measure_peaks(int device, uint64_t scene_table_bytes, rt_peaks* out);
 /* Rows in one rank's slab (max over ranks, so all slabs have equal size). */
@@ -279,7 +282,7 @@ int rt_counters_read_raw(rt_scene* scene, uint64_t* out, int n);
  * since the last reset, for a scene created with env RT_KTIME=1 (events between
  * the kernels of each launch; each launch then synchronises).  ms[k] for k =
  * k_chain, k_pack_a, k_mix, k_occlude (A's shadows, frame batches), k_pack_b,
- * k_occlude (B's overflow), k_finish.  Returns the launches timed. */
+ * k_occlude (B's overflow), k_finish, k_fallback.  Returns the launches timed. */
 int rt_kernel_times(rt_scene* scene, double* ms, int n, int reset);
 /* Synchronises the scene's device and reports a walk that was cut off since
  * the last check: every BVH walk has an always-on step bound (64 x the tree's

@@ -231,7 +231,8 @@ def phong_pow(base, exponent) -> np.ndarray:
 class Peaks(ctypes.Structure):
     _fields_ = [("hbm_copy_gbps", ctypes.c_double), ("hbm_read_gbps", ctypes.c_double),
                 ("l2_gather_gbps", ctypes.c_double), ("l2_table_bytes", ctypes.c_double),
-                ("scene_gather_gbps", ctypes.c_double), ("scene_table_bytes", ctypes.c_double)]
+                ("scene_gather_gbps", ctypes.c_double), ("scene_table_bytes", ctypes.c_double),
+                ("l2_line_gbps", ctypes.c_double), ("scene_line_gbps", ctypes.c_double)]
 
 
 def measure_peaks(device: int = -1, scene_table_bytes: int = 6 << 20) -> dict:
@@ -407,12 +408,12 @@ class Scene:
             _check(n)
         return {k: int(out[8 + i]) for i, k in enumerate(self.COUNTER_SLOTS)}
 
-    KERNEL_KINDS = ("k_chain", "k_pack_a", "k_mix", "k_occlude_a", "k_pack_b", "k_occlude_b", "k_finish")
+    KERNEL_KINDS = ("k_chain", "k_pack_a", "k_mix", "k_occlude_a", "k_pack_b", "k_occlude_b", "k_finish", "k_fallback")
 
     def kernel_times(self, reset: bool = True) -> tuple[dict, int]:
         """rt_kernel_times (RT_KTIME=1 scenes): ms per kernel of the chain launches, and the launch count."""
-        ms = np.zeros(8, dtype=np.float64)
-        n = lib().rt_kernel_times(self._h, ms.ctypes.data_as(ctypes.c_void_p), 8, int(reset))
+        ms = np.zeros(16, dtype=np.float64)
+        n = lib().rt_kernel_times(self._h, ms.ctypes.data_as(ctypes.c_void_p), 16, int(reset))
         if n < 0:
             _check(n)
         return {k: float(ms[i]) for i, k in enumerate(self.KERNEL_KINDS)}, n

@@ -161,12 +161,6 @@ __device__ __forceinline__ unsigned wave_grab_lds(unsigned* ctr, unsigned long l
     return __shfl(base, leader, 64);
 }
 
-typedef float nt4 __attribute__((ext_vector_type(4)));
-__device__ __forceinline__ float4 ld_nt(const float4* p) {
-    const nt4 x = __builtin_nontemporal_load(reinterpret_cast<const nt4*>(p));
-    return make_float4(x.x, x.y, x.z, x.w);
-}
-
 // Block b's samples: units b, b+G, b+2G, ... of 256 consecutive slots.
 __device__ __forceinline__ unsigned block_samples(unsigned n0, unsigned G) {
     const unsigned units = (n0 + 255u) / 256u;
@@ -224,6 +218,13 @@ struct PhaseOut {              // where a chain phase writes its tasks
 // scene instead of 16 more bytes per record through HBM, written once and read
 // by every shadow task, the mirror bounce and the shading of the record).
 constexpr int kRecWords = 2;
+// Record id of level k of sample `path` (continuation index c when k >= p.la): levels below la at
+// k * cap + path, deeper ones (phase B) only for the first cb continuations, after them.
+// (Record ids, and owner ids rid * nl + l, stay below 2^31: rt_api.cpp checks cap * levels * nl.)
+__device__ __forceinline__ unsigned rec_id(const PcParams& p, int k, unsigned path, unsigned c) {
+    return k < p.la ? (unsigned)k * (unsigned)p.cap + path
+                    : (unsigned)p.la * (unsigned)p.cap + (unsigned)(k - p.la) * p.cb + c;
+}
 __device__ __forceinline__ void rec_write(const PcParams& p, size_t lvp, const V& hitp, int code, const V& d,
                                           int mat) {
     float4* rc = p.rec + lvp * kRecWords;
@@ -266,6 +267,16 @@ __device__ __forceinline__ Ray reflect_from_record(const rtk::DevScene& s, const
     return reflect_ray(s, hitp, surface_normal(s, hitp, __float_as_int(a.w)), V{c.x, c.y, c.z});
 }
 
+// Shadow ray toward light l from a hit (raytracer.cpp:397-404): origin hitp + n * eps, direction
+// normalize(L - origin), length |L - origin|.
+__device__ __forceinline__ Ray shadow_ray(const rtk::DevScene& s, const V& hitp, const V& nn, int l, float* tlim) {
+    const V pnt = add(hitp, mul(nn, s.eps));
+    const float4 lp = ld4(&s.lights[l].px);
+    const V lpos{lp.x, lp.y, lp.z};
+    *tlim = len(sub(lpos, pnt));
+    return make_ray(pnt, nrm(sub(lpos, pnt)));
+}
+
 // Shadow ray of task `owner` (raytracer.cpp:397-404).
 __device__ __forceinline__ Ray shadow_from_record(const rtk::DevScene& s, const PcParams& p, unsigned owner,
                                                   float* tlim) {
@@ -273,11 +284,30 @@ __device__ __forceinline__ Ray shadow_from_record(const rtk::DevScene& s, const 
     const int l = (int)(owner - lvp * (unsigned)s.nlights);
     const float4 a = p.rec[(size_t)lvp * kRecWords];
     const V hitp{a.x, a.y, a.z};
-    const V pnt = add(hitp, mul(surface_normal(s, hitp, __float_as_int(a.w)), s.eps));
-    const float4 lp = ld4(&s.lights[l].px);
-    const V lpos{lp.x, lp.y, lp.z};
-    *tlim = len(sub(lpos, pnt));
-    return make_ray(pnt, nrm(sub(lpos, pnt)));
+    return shadow_ray(s, hitp, surface_normal(s, hitp, __float_as_int(a.w)), l, tlim);
+}
+
+// Rays the timed walks leave to k_fallback: not NaN-free, or beyond the range of the wide trees' fused
+// slab test (wide_ray_ok; in practice a direction component of exactly 0, whose 1/d is infinite).
+// The production kernels then carry only the wide-tree walks (fewer registers: no VGPR spills).
+__device__ __forceinline__ bool defer_closest(const rtk::DevScene& s, const Ray& r) {
+    return s.nnodes > 0 && ((s.force_fb & 1) || !(s.use_wide && ray_nan_free(r) && wide_ray_ok(r)));
+}
+__device__ __forceinline__ bool defer_any(const rtk::DevScene& s, const Ray& r) {
+    return s.nnodes > 0 && ((s.force_fb & 2) || !(s.use_stree == 2 && ray_nan_free(r) && wide_ray_ok(r)));
+}
+__device__ __forceinline__ void fb_chain(const PcParams& p, unsigned entry) {
+    const unsigned i = atomicAdd(&p.totals[4], 1u);
+    if (i < p.fbc_cap) p.fbc[i] = entry;       // fbc_cap = cap: a sample defers at most one ray per launch
+}
+__device__ __forceinline__ void fb_shadow(const PcParams& p, unsigned owner) {
+    const unsigned i = atomicAdd(&p.totals[5], 1u);
+    if (i < p.fbs_cap) {
+        p.fbs[i] = owner;
+    } else {                                   // queue full: mark the byte, k_fallback scans for it
+        p.occ[owner] = kOccDeferred;
+        __hip_atomic_store(&p.totals[6], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
 }
 
 // The same shadow ray for a task produced by another wave of the workgroup
@@ -294,11 +324,7 @@ __device__ __forceinline__ Ray shadow_from_record_l2(const rtk::DevScene& s, con
     const int l = (int)(owner - lvp * (unsigned)s.nlights);
     const float4 a = ld4_l2(p.rec + (size_t)lvp * kRecWords);
     const V hitp{a.x, a.y, a.z};
-    const V pnt = add(hitp, mul(surface_normal(s, hitp, __float_as_int(a.w)), s.eps));
-    const float4 lp = ld4(&s.lights[l].px);
-    const V lpos{lp.x, lp.y, lp.z};
-    *tlim = len(sub(lpos, pnt));
-    return make_ray(pnt, nrm(sub(lpos, pnt)));
+    return shadow_ray(s, hitp, surface_normal(s, hitp, __float_as_int(a.w)), l, tlim);
 }
 
 // Samples of workgroup blk (of G): units blk, blk+G, ... of 256 slots.
@@ -525,7 +551,8 @@ __device__ uint32_t bq_consume(const rtk::DevScene& s, const PcParams& p, WalkSt
                     owner = v;
                     r = shadow_from_record_l2(s, p, owner, &tlim);
                     ++n;
-                    if (walk_begin<COUNT>(s, r, wk, w, true)) active = true;
+                    if (!COUNT && defer_any(s, r)) fb_shadow(p, owner);
+                    else if (walk_begin<COUNT>(s, r, wk, w, true)) active = true;
                     else p.occ[owner] = 0;
                 }
             }
@@ -537,7 +564,7 @@ __device__ uint32_t bq_consume(const rtk::DevScene& s, const PcParams& p, WalkSt
         }
         stat.step(active, wk.cur >= 0, RT_STEP_STATS && active && wk.tree == nullptr && leaf_postponed(s.leaf_wait_any, wk));
         if (active) {
-            const int res = occl_step<COUNT, FetchTop>(s, r, tlim, stk, wk, w);
+            const int res = occl_step_timed<COUNT>(s, r, tlim, stk, wk, w);
             if (res || walk_runaway(s, wk)) {
                 p.occ[owner] = res == 2 ? 1 : 0;
                 active = false;
@@ -579,7 +606,7 @@ __device__ void chain_body(const rtk::DevScene& s, const rtk::Eye& e, const PcPa
     uint32_t nprim = 0, nrefl = 0, nskip = 0, nhit = 0, ncont = 0;
     const int nl = s.nlights;
     unsigned nb;
-    if (CONT) nb = chunk_count(p.totals[1], G, blk, (unsigned)p.tchunk);
+    if (CONT) nb = chunk_count(min(p.totals[1], p.cb), G, blk, (unsigned)p.tchunk);   // the rest: k_fallback
     else nb = group_samples((unsigned)p.n0, G, blk);
     // dynamic units (phase A, p.dyn_units > 0): the workgroup's k-th 256-sample unit is not
     // blk + k*G but the next one of a launch-wide counter (p.totals[3], zeroed before the launch),
@@ -592,7 +619,7 @@ __device__ void chain_body(const rtk::DevScene& s, const rtk::Eye& e, const PcPa
     unsigned* const sq = o.sq + (size_t)blk * o.scap;
     int st = kIdle;
     bool exhausted = nb == 0;
-    unsigned path = 0;
+    unsigned path = 0, cix = 0;   // sample slot; continuation index (phase B: its deeper records)
     int k = 0;
     Ray r;
     Walk wk;
@@ -606,15 +633,15 @@ __device__ void chain_body(const rtk::DevScene& s, const rtk::Eye& e, const PcPa
             const bool hit = h.prim >= 0;
             V nn{0.0f, 0.0f, 0.0f}, hitp{0.0f, 0.0f, 0.0f};
             int mat = 0, code = 0;
+            const size_t lvp = rec_id(p, k, path, cix);
             if (hit) {
                 hit_surface(s, r, h, &nn, &mat, &code);
                 hitp = add(r.o, mul(r.d, h.t));
-                rec_write(p, (size_t)k * p.cap + path, hitp, code, r.d, mat);
+                rec_write(p, lvp, hitp, code, r.d, mat);
                 if (COUNT) nhit++;
             }
             // one shadow task per light (:399-404) whose ray can change the pixel (light_needed; the
             // counting passes trace every one, as the reference does); light-major within the wave
-            const size_t lvp = (size_t)k * p.cap + path;
             const unsigned own0 = (unsigned)(lvp * nl);
             if (CONT && kBq > 0 && __ballot(hit))
                 __builtin_amdgcn_s_waitcnt(0);     // phase B: the record stores have completed before the
@@ -681,7 +708,12 @@ __device__ void chain_body(const rtk::DevScene& s, const rtk::Eye& e, const PcPa
                 r = reflect_ray(s, hitp, nn, r.d);
                 ++k;
                 nrefl++;
-                st = walk_begin<COUNT>(s, r, wk, w) ? kTrav : kDone;
+                if (!COUNT && defer_closest(s, r)) {     // the rest of this path: k_fallback
+                    fb_chain(p, (unsigned)lvp);
+                    st = kIdle;
+                } else {
+                    st = walk_begin<COUNT>(s, r, wk, w) ? kTrav : kDone;
+                }
             }
         }
         // (2) refill idle lanes with this workgroup's next samples / continuations
@@ -716,10 +748,12 @@ __device__ void chain_body(const rtk::DevScene& s, const rtk::Eye& e, const PcPa
                             const unsigned lvp = p.cflat[j];
                             path = lvp % (unsigned)p.cap;
                             k = (int)(lvp / (unsigned)p.cap) + 1;
+                            cix = j;
                             if (p.trace) { t_grab = (unsigned)wall_clock64(); tsteps = 0; }
                             r = reflect_from_record(s, p, lvp);
                             nrefl++;
-                            st = walk_begin<COUNT>(s, r, wk, w) ? kTrav : kDone;
+                            if (!COUNT && defer_closest(s, r)) fb_chain(p, lvp);
+                            else st = walk_begin<COUNT>(s, r, wk, w) ? kTrav : kDone;
                         } else {
                             const unsigned idx = (dyn ? uid : blk + (v >> 8) * G) * 256u + (v & 255u);
                             if (slab_sample_ray(e, p, idx, &r)) {
@@ -728,6 +762,7 @@ __device__ void chain_body(const rtk::DevScene& s, const rtk::Eye& e, const PcPa
                                 if (p.trace) t_grab = (unsigned)wall_clock64();
                                 nprim++;
                                 if (s.max_depth < 0) p.pinfo[path] = 0 | (kEndZero << 8);   // depth 0 > max: black
+                                else if (!COUNT && defer_closest(s, r)) fb_chain(p, kFbEye | path);
                                 else if (RT_PACKET_WALK && p.packet) fresh = true;
                                 else st = walk_begin<COUNT>(s, r, wk, w) ? kTrav : kDone;
                             }
@@ -764,7 +799,7 @@ __device__ void chain_body(const rtk::DevScene& s, const rtk::Eye& e, const PcPa
             stat.step(st == kTrav, wk.cur >= 0, RT_STEP_STATS && st == kTrav && wk.tree == nullptr && leaf_postponed(s.leaf_wait, wk));
             if (st == kTrav) {
                 if (CONT && p.trace) ++tsteps;
-                if (closest_step<COUNT, FetchTop, WalkStack, CONT>(s, r, stk, wk, w) || walk_runaway(s, wk)) st = kDone;
+                if (closest_step_timed<COUNT, CONT>(s, r, stk, wk, w) || walk_runaway(s, wk)) st = kDone;
             }
         }
     }
@@ -832,7 +867,8 @@ __device__ void occlude_body(const rtk::DevScene& s, const PcParams& p, unsigned
                         owner = tasks[j];
                         r = shadow_from_record(s, p, owner, &tlim);
                         nrays++;
-                        if (walk_begin<COUNT>(s, r, wk, w, true)) active = true;
+                        if (!COUNT && defer_any(s, r)) fb_shadow(p, owner);
+                        else if (walk_begin<COUNT>(s, r, wk, w, true)) active = true;
                         else p.occ[owner] = 0;
                     }
                 }
@@ -846,7 +882,7 @@ __device__ void occlude_body(const rtk::DevScene& s, const PcParams& p, unsigned
         while (__popcll(__ballot(active)) > thresh) {
             stat.step(active, wk.cur >= 0, RT_STEP_STATS && active && wk.tree == nullptr && leaf_postponed(s.leaf_wait_any, wk));
             if (active) {
-                const int res = occl_step<COUNT, FetchTop>(s, r, tlim, stk, wk, w);
+                const int res = occl_step_timed<COUNT>(s, r, tlim, stk, wk, w);
                 if (res || walk_runaway(s, wk)) {
                     p.occ[owner] = res == 2 ? 1 : 0;
                     active = false;
@@ -888,8 +924,9 @@ __global__ __launch_bounds__(kBlock, RT_WAVES_PER_EU) void k_chain(rtk::DevScene
 // Region b of a per-workgroup queue (q[b*cap ..], cnt[b] entries) copied to
 // its place in the packed array: the consumers then index tasks directly.
 // Workgroup 0 stores the total.
+// cid (continuations): cid[sample] = the packed index of its continuation (its phase-B records).
 __device__ void pack_region(const unsigned* q, unsigned cap, const unsigned* cnt, int nreg, unsigned* flat,
-                            unsigned* total, unsigned b) {
+                            unsigned* total, unsigned b, unsigned* cid = nullptr, unsigned ncap = 1) {
     __shared__ unsigned s_before, s_all;
     if (threadIdx.x == 0) { s_before = 0; s_all = 0; }
     __syncthreads();
@@ -909,8 +946,16 @@ __device__ void pack_region(const unsigned* q, unsigned cap, const unsigned* cnt
     for (; k + 3 * kBlock < n; k += 4 * kBlock) {          // four loads in flight per lane
         const unsigned v0 = src[k], v1 = src[k + kBlock], v2 = src[k + 2 * kBlock], v3 = src[k + 3 * kBlock];
         flat[off + k] = v0; flat[off + k + kBlock] = v1; flat[off + k + 2 * kBlock] = v2; flat[off + k + 3 * kBlock] = v3;
+        if (cid) {
+            cid[v0 % ncap] = off + k; cid[v1 % ncap] = off + k + kBlock;
+            cid[v2 % ncap] = off + k + 2 * kBlock; cid[v3 % ncap] = off + k + 3 * kBlock;
+        }
     }
-    for (; k < n; k += kBlock) flat[off + k] = src[k];
+    for (; k < n; k += kBlock) {
+        const unsigned v = src[k];
+        flat[off + k] = v;
+        if (cid) cid[v % ncap] = off + k;
+    }
     if (b == 0 && threadIdx.x == 0) *total = s_all;
     __syncthreads();
 }
@@ -918,7 +963,7 @@ __device__ void pack_region(const unsigned* q, unsigned cap, const unsigned* cnt
 // After phase A: pack its shadow tasks and continuations (one workgroup per region).
 __global__ __launch_bounds__(kBlock) void k_pack_a(PcParams p) {
     pack_region(p.sqA, p.scapA, p.scntA, p.grid, p.sflatA, &p.totals[0], blockIdx.x);
-    pack_region(p.cq, p.ccapA, p.ccnt, p.grid, p.cflat, &p.totals[1], blockIdx.x);
+    pack_region(p.cq, p.ccapA, p.ccnt, p.grid, p.cflat, &p.totals[1], blockIdx.x, p.cid, (unsigned)p.cap);
 }
 __global__ __launch_bounds__(kBlock) void k_pack_b(PcParams p) {
     pack_region(p.sqB, p.scapB, p.scntB, p.gb, p.sflatB, &p.totals[2], blockIdx.x);
@@ -1165,115 +1210,12 @@ __global__ __launch_bounds__(kBlock, RT_WAVES_PER_EU) void k_fused(rtk::DevScene
     }
 }
 
-// Blinn-Phong of recorded level k of a path (raytracer.cpp:392-427).
-__device__ __forceinline__ V shade_level(const rtk::DevScene& s, const PcParams& p, unsigned path, int k,
-                                         int* mat_out) {
-    const float4* rc = p.rec + ((size_t)k * p.cap + path) * kRecWords;
-    const float4 a = ld_nt(rc), c = ld_nt(rc + 1);
-    const int mat = __float_as_int(c.w);
-    *mat_out = mat;
-    const V hitp{a.x, a.y, a.z}, d{c.x, c.y, c.z};
-    const V n_ = surface_normal(s, hitp, __float_as_int(a.w));
-    const dl::Material& M = s.mats[mat - 1];
-    const float4 mA = ld4(&M.kax), mD = ld4(&M.kdx);
-    V L{0.0f, 0.0f, 0.0f};
-    L = add(L, V{mA.x, mA.y, mA.z});                                                  // :394-395
-    const V pnt = add(hitp, mul(n_, s.eps));                                           // :397
-    const uint8_t* occ = p.occ + ((size_t)k * p.cap + path) * s.nlights;
-    for (int l = 0; l < s.nlights; ++l) {
-        if (occ[l]) continue;
-        const float4 lp = ld4(&s.lights[l].px), li4 = ld4(&s.lights[l].ix);
-        const V lpos{lp.x, lp.y, lp.z};
-        const float dist = len(sub(lpos, pnt));
-        const V ldir = nrm(sub(lpos, pnt));
-        const V ldir_real = nrm(sub(lpos, hitp));
-        const float cos_t = dot(ldir_real, n_);
-        const V E = divs(V{li4.x, li4.y, li4.z}, dist * dist);
-        // theta = acos(cos)*180/3.1415 <= 90.01  <=>  cos in [cos_thr, 1]
-        if (cos_t >= s.cos_thr && cos_t <= 1.0f) {
-            const V hh = nrm(add(ldir, neg(nrm(d))));
-            const float base = smax(0.0f, dot(nrm(n_), hh));
-            const float ca = phong_pow(base, mA.w);
-            const float4 mS = ld4(&M.ksx);
-            L = add(L, had(mul(V{mS.x, mS.y, mS.z}, ca), E));
-        }
-        const float cl = smax(0.0f, smin(1.0f, cos_t));                               // clampFloat(cos, 0, 1)
-        L = add(L, had(mul(V{mD.x, mD.y, mD.z}, cl), E));
-    }
-    return L;
-}
-
-// k_shade: Blinn-Phong of every recorded level, one lane per (level, sample)
-// record (the levels of a path are independent here; only the fold below is
-// sequential).  L replaces the record's ray direction (rec[2*lvp+1].xyz),
-// which nothing needs after shading.
-__global__ __launch_bounds__(kBlock) void k_shade(rtk::DevScene s, PcParams p) {
-    const size_t n = (size_t)p.levels * (size_t)p.n0;
-    for (size_t i = (size_t)blockIdx.x * kBlock + threadIdx.x; i < n; i += (size_t)gridDim.x * kBlock) {
-        const int k = (int)(i / (size_t)p.n0);
-        const unsigned path = (unsigned)(i - (size_t)k * p.n0);
-        if (!slab_slot_valid(p, path)) continue;
-        if (k >= (p.pinfo[path] & 0xff)) continue;
-        int mat;
-        const V L = shade_level(s, p, path, k, &mat);
-        p.rec[((size_t)k * p.cap + path) * kRecWords + 1] = make_float4(L.x, L.y, L.z, __int_as_float(mat));
-    }
-}
-
-// Recursive clamp-and-add evaluated deepest-first (raytracer.cpp:436-451)
-// over the shaded records.
-__device__ __forceinline__ V path_color(const rtk::DevScene& s, const PcParams& p, unsigned path) {
-    const int info = p.pinfo[path];
-    const int nlev = info & 0xff, kind = (info >> 8) & 0xff;
-    V c = kind == kEndBg ? V{s.bgx, s.bgy, s.bgz} : V{0.0f, 0.0f, 0.0f};
-    int k = nlev - 1;
-    if (kind == kEndLast) {
-        const float4 L = p.rec[((size_t)k * p.cap + path) * kRecWords + 1];
-        c = vclamp(V{L.x, L.y, L.z}, 0.0f, FLT_MAX);
-        --k;
-    }
-    for (; k >= 0; --k) {
-        const float4 L = p.rec[((size_t)k * p.cap + path) * kRecWords + 1];
-        const int mat = __float_as_int(L.w);
-        const float4 km = ld4(&s.mats[mat - 1].kmx);
-        c = vclamp(add(V{L.x, L.y, L.z}, had(c, V{km.x, km.y, km.z})), 0.0f, FLT_MAX);
-    }
-    return c;
-}
-
 // Output row of slab row lr.  A frame split into out_k interleaved sub-frames
 // (rt_api.cpp render_frame) renders sub-frame out_j's stripes; its stripe m is
 // stripe m*out_k + out_j of the caller's slab.
 __device__ __forceinline__ int out_row(const PcParams& p, int lr) {
     const int m = lr / p.stripe_rows;
     return (m * p.out_k + p.out_j) * p.stripe_rows + (lr - m * p.stripe_rows);
-}
-
-// k_compose: fold + toPixel + ImageProcessor::downSample per output pixel
-__global__ __launch_bounds__(kBlock) void k_compose(rtk::DevScene s, PcParams p) {
-    const int lr0 = p.chunk_row0 / p.aa;
-    const int nrows = p.chunk_rows / p.aa;
-    const int npix = nrows * p.width;
-    const int F = p.aa;
-    for (int q = blockIdx.x * kBlock + threadIdx.x; q < npix; q += gridDim.x * kBlock) {
-        const int rr = q / p.width, ocol = q - rr * p.width;
-        const int lr = lr0 + rr;
-        if (lr >= p.slab_rows) continue;
-        int lf = lr;
-        const int fr = batch_frame(p, &lf);
-        const int stripe = lf / p.stripe_rows;
-        const int g = (stripe * p.nranks + p.rank) * p.stripe_rows + (lf - stripe * p.stripe_rows);
-        if (g >= p.height) continue;
-        uint32_t sr = 0, sg = 0, sb = 0;
-        for (int k = 0; k < F; ++k)
-            for (int l = 0; l < F; ++l) {
-                const V c = path_color(s, p, slab_slot(p.tiles_x, ocol * F + l, rr * F + k));
-                sr += quantise(c.x); sg += quantise(c.y); sb += quantise(c.z);
-            }
-        const uint32_t ff = (uint32_t)(F * F);
-        uint8_t* o = (p.nframes > 1 ? p.fouts[fr] : p.out) + ((size_t)out_row(p, lf) * p.width + ocol) * 3;
-        o[0] = (uint8_t)(sr / ff); o[1] = (uint8_t)(sg / ff); o[2] = (uint8_t)(sb / ff);
-    }
 }
 
 // Small scenes (<= kFinishMats materials, <= kFinishLights lights): k_finish
@@ -1294,14 +1236,12 @@ __device__ __forceinline__ const dl::Light& fin_light(const rtk::DevScene& s, in
     return s.lights[i];
 }
 
-// Blinn-Phong of one record from its already-loaded words and material
-// (shade_level's arithmetic, raytracer.cpp:391-425); occ bit l set = light l
-// occluded (lights >= 32 read their byte directly).
-template <bool LDS>
-__device__ __forceinline__ V shade_words(const rtk::DevScene& s, const PcParams& p, size_t rid, const float4 a,
-                                         const V n_, const float4 c, const float4 mA, const float4 mD,
-                                         const float4 mS, uint32_t occ32) {
-    const V hitp{a.x, a.y, a.z}, d{c.x, c.y, c.z};
+// Blinn-Phong of one hit (raytracer.cpp:391-425): hit point, ray direction, normal, material words;
+// occluded(l): light l's shadow ray found an occluder.  The one shading arithmetic of the chain path
+// (k_finish from records, k_fallback inline).
+template <bool LDS, class OCC>
+__device__ __forceinline__ V shade_core(const rtk::DevScene& s, const V hitp, const V d, const V n_, const float4 mA,
+                                        const float4 mD, const float4 mS, OCC&& occluded_fn) {
     V L{0.0f, 0.0f, 0.0f};
     L = add(L, V{mA.x, mA.y, mA.z});                                                  // :394-395
     const V pnt = add(hitp, mul(n_, s.eps));                                           // :397
@@ -1310,8 +1250,7 @@ __device__ __forceinline__ V shade_words(const rtk::DevScene& s, const PcParams&
 #pragma unroll 1
     for (int l = 0; l < nl; ++l) {
         if (LDS && l >= s.nlights) break;
-        const bool occluded = (LDS || l < 32) ? ((occ32 >> l) & 1u) != 0 : p.occ[rid * s.nlights + l] != 0;
-        if (occluded) continue;
+        if (occluded_fn(l)) continue;
         const dl::Light& Lt = fin_light<LDS>(s, l);
         const float4 lp = ld4(&Lt.px), li4 = ld4(&Lt.ix);
         const V lpos{lp.x, lp.y, lp.z};
@@ -1336,6 +1275,17 @@ __device__ __forceinline__ V shade_words(const rtk::DevScene& s, const PcParams&
     return L;
 }
 
+// The same for record rid from its already-loaded words: occ bit l set = light l occluded (lights >= 32
+// read their byte directly).
+template <bool LDS>
+__device__ __forceinline__ V shade_words(const rtk::DevScene& s, const PcParams& p, unsigned rid, const float4 a,
+                                         const V n_, const float4 c, const float4 mA, const float4 mD,
+                                         const float4 mS, uint32_t occ32) {
+    return shade_core<LDS>(s, V{a.x, a.y, a.z}, V{c.x, c.y, c.z}, n_, mA, mD, mS, [&](int l) {
+        return (LDS || l < 32) ? ((occ32 >> l) & 1u) != 0 : p.occ[(size_t)rid * s.nlights + l] != 0;
+    });
+}
+
 // Occlusion bytes of record rid.  Up to four lights: the two aligned dwords
 // covering them, loaded together and decoded only where the bits are used, so
 // the loads stay in flight with the prefetched record (a byte loop waits for
@@ -1343,12 +1293,12 @@ __device__ __forceinline__ V shade_words(const rtk::DevScene& s, const PcParams&
 // second dword.  More lights: decoded from the bytes at use.
 struct OccRaw {
     uint32_t w0, w1;
-    size_t off;       // byte offset of the record's first light
+    unsigned off;     // byte offset of the record's first light (owner id of light 0, < 2^31)
 };
 template <bool SMALL>
-__device__ __forceinline__ OccRaw occ_load(const PcParams& p, size_t rid, int nl) {
+__device__ __forceinline__ OccRaw occ_load(const PcParams& p, unsigned rid, int nl) {
     OccRaw o;
-    o.off = rid * (size_t)nl;
+    o.off = rid * (unsigned)nl;
     if (SMALL) {
         const uint32_t* wd = reinterpret_cast<const uint32_t*>(p.occ) + (o.off >> 2);
         o.w0 = wd[0];
@@ -1380,18 +1330,24 @@ __device__ __forceinline__ V path_shade_fold(const rtk::DevScene& s, const PcPar
     const int info = p.pinfo[path];
     const int nlev = info & 0xff, kind = (info >> 8) & 0xff;
     V c = kind == kEndBg ? V{s.bgx, s.bgy, s.bgz} : V{0.0f, 0.0f, 0.0f};
+    if (kind == kEndTail) {                    // levels >= nlev: k_fallback's folded colour
+        const float4 t = p.tail[path];
+        c = V{t.x, t.y, t.z};
+    }
     if (nlev == 0) return c;
     const int nl = s.nlights;
-    size_t rid = (size_t)(nlev - 1) * p.cap + path;
-    float4 a = p.rec[rid * kRecWords], d = p.rec[rid * kRecWords + 1];
+    const unsigned cx = nlev > p.la ? p.cid[path] : 0u;   // continued paths: their phase-B records
+    unsigned rid = rec_id(p, nlev - 1, path, cx);
+    float4 a = p.rec[(size_t)rid * kRecWords], d = p.rec[(size_t)rid * kRecWords + 1];
     OccRaw oc = occ_load<LDS>(p, rid, nl);
     for (int k = nlev - 1; k >= 0; --k) {
         const dl::Material& M = fin_mat<LDS>(s, __float_as_int(d.w) - 1);   // before the prefetch (vmcnt order)
         const float4 mA = ld4(&M.kax), mD = ld4(&M.kdx), mS = ld4(&M.ksx), km = ld4(&M.kmx);
         const V n_ = surface_normal(s, V{a.x, a.y, a.z}, __float_as_int(a.w));
-        const size_t rn = (size_t)max(k - 1, 0) * p.cap + path;
+        // the next (shallower) record: phase-B ids step down by cb, phase-A ids are (k-1) * cap + path
+        const unsigned rn = k - 1 >= p.la ? rid - p.cb : (unsigned)max(k - 1, 0) * (unsigned)p.cap + path;
 #if RT_FINISH_PREFETCH
-        const float4 na = p.rec[rn * kRecWords], nd = p.rec[rn * kRecWords + 1];
+        const float4 na = p.rec[(size_t)rn * kRecWords], nd = p.rec[(size_t)rn * kRecWords + 1];
         const OccRaw noc = occ_load<LDS>(p, rn, nl);
 #endif
         const V L = shade_words<LDS>(s, p, rid, a, n_, d, mA, mD, mS, occ_bits<LDS>(p, oc, nl));
@@ -1401,7 +1357,7 @@ __device__ __forceinline__ V path_shade_fold(const rtk::DevScene& s, const PcPar
         rid = rn; a = na; d = nd; oc = noc;
 #else
         if (k > 0) {
-            rid = rn; a = p.rec[rn * kRecWords]; d = p.rec[rn * kRecWords + 1];
+            rid = rn; a = p.rec[(size_t)rn * kRecWords]; d = p.rec[(size_t)rn * kRecWords + 1];
             oc = occ_load<LDS>(p, rn, nl);
         }
 #endif
@@ -1486,6 +1442,128 @@ __global__ __launch_bounds__(kBlock, RT_FINISH_ANY_WAVES) void k_finish_any(rtk:
     finish_pixels<false>(s, p);
 }
 
+// ---------------------------------------------------------------------------
+// k_fallback: what the timed walks leave (rare): rays the wide trees' fused
+// slab test does not take (defer_closest / defer_any: NaN, or a direction
+// component of 0) and continuations beyond the phase-B record capacity.  Each
+// lane runs the general walks (wide or binary trees, the reference's NaN
+// semantics) one item at a time:
+//   * a chain entry: the path from the deferred ray to its end, closest hit,
+//     shadow rays inline, shading (shade_core) and the deepest-first fold
+//     (raytracer.cpp:385-452) -> tail[path], pinfo = nlev | kEndTail;
+//   * a shadow task: its any-hit walk -> occ[owner];
+//   * after a full shadow queue: every occlusion byte marked kOccDeferred.
+// Launched after the shadow kernels and before k_finish; with nothing to do it
+// exits at once.
+// ---------------------------------------------------------------------------
+constexpr int kFbMaxLevels = 66;      // max_recursion_depth <= 64 (rt_scene_set_max_depth) + 1
+
+__device__ __forceinline__ bool fallback_any(const rtk::DevScene& s, const Ray& r, float tlim, WalkStack& stk,
+                                             Work& w) {
+    Walk wk;
+    if (!walk_begin<false>(s, r, wk, w, true)) return false;
+    while (true) {
+        const int res = occl_step<false, FetchTop>(s, r, tlim, stk, wk, w);
+        if (res) return res == 2;
+        if (walk_runaway(s, wk)) return false;
+    }
+}
+
+__device__ void fallback_chain(const rtk::DevScene& s, const rtk::Eye& e, const PcParams& p, unsigned entry,
+                               WalkStack& stk, Work& w) {
+    const unsigned cap = (unsigned)p.cap;
+    unsigned path;
+    int k;
+    Ray r;
+    if (entry & kFbEye) {                          // a deferred eye ray
+        path = entry & ~kFbEye;
+        k = 0;
+        if (!slab_sample_ray(e, p, path, &r)) return;
+    } else {                                       // the reflection of record `entry`
+        const size_t aspace = (size_t)p.la * cap;
+        int kprev;
+        if (entry < aspace) {
+            kprev = (int)(entry / cap);
+            path = entry % cap;
+        } else {
+            const size_t q = entry - aspace;
+            kprev = p.la + (int)(q / p.cb);
+            path = p.cflat[q % p.cb] % cap;
+        }
+        k = kprev + 1;
+        r = reflect_from_record(s, p, entry);
+    }
+    const int k0 = k;
+    V Ls[kFbMaxLevels], Km[kFbMaxLevels];          // the mirror levels' shading and km, k0 onward
+    int n = 0;
+    V c{0.0f, 0.0f, 0.0f};                         // the deepest level's value (before the fold)
+    while (true) {
+        if (k > s.max_depth) break;                // beyond MaxRecursionDepth: 0 (:387-389)
+        Walk wk;
+        if (walk_begin<false>(s, r, wk, w)) {
+            while (!closest_step<false, FetchTop, WalkStack>(s, r, stk, wk, w) && !walk_runaway(s, wk)) {
+            }
+        }
+        const HitRec h = wk.best;
+        if (h.prim < 0) {                          // miss: background at depth 0, else 0 (:442-449)
+            if (k == 0) c = V{s.bgx, s.bgy, s.bgz};
+            break;
+        }
+        V nn;
+        int mat, code;
+        hit_surface(s, r, h, &nn, &mat, &code);
+        const V hitp = add(r.o, mul(r.d, h.t));
+        const dl::Material& M = s.mats[mat - 1];
+        const float4 mA = ld4(&M.kax), mD = ld4(&M.kdx), mS = ld4(&M.ksx), km = ld4(&M.kmx);
+        const V L = shade_core<false>(s, hitp, r.d, nn, mA, mD, mS, [&](int l) {
+            if (s.cull_shadows && !light_needed(s, hitp, nn, l)) return true;   // the same sum (light_needed)
+            float tlim;
+            const Ray sr = shadow_ray(s, hitp, nn, l, &tlim);
+            return fallback_any(s, sr, tlim, stk, w);
+        });
+        if (!M.is_mirror) {                        // the last level: its own clamp (:451)
+            c = vclamp(L, 0.0f, FLT_MAX);
+            break;
+        }
+        Ls[n] = L;
+        Km[n] = V{km.x, km.y, km.z};
+        ++n;
+        if (k >= s.max_depth || n >= kFbMaxLevels) break;   // the child beyond the depth returns 0
+        r = reflect_ray(s, hitp, nn, r.d);
+        ++k;
+    }
+    for (int i = n - 1; i >= 0; --i) c = vclamp(add(Ls[i], had(c, Km[i])), 0.0f, FLT_MAX);   // :436-451
+    p.tail[path] = make_float4(c.x, c.y, c.z, 0.0f);
+    p.pinfo[path] = k0 | (kEndTail << 8) | (k0 >= p.la ? kPathCont : 0);
+}
+
+__global__ __launch_bounds__(kBlock) void k_fallback(rtk::DevScene s, rtk::Eye e, PcParams p) {
+    block_init(s);
+    WalkStack stk;
+    Work w;
+    const unsigned gt = blockIdx.x * kBlock + threadIdx.x, gs = gridDim.x * kBlock;
+    const unsigned nfc = min(p.totals[4], p.fbc_cap);
+    const unsigned ncont = p.totals[1], novf = ncont > p.cb ? ncont - p.cb : 0u;
+    for (unsigned i = gt; i < nfc + novf; i += gs)
+        fallback_chain(s, e, p, i < nfc ? p.fbc[i] : p.cflat[p.cb + (i - nfc)], stk, w);
+    const unsigned nfs = min(p.totals[5], p.fbs_cap);
+    for (unsigned i = gt; i < nfs; i += gs) {
+        const unsigned owner = p.fbs[i];
+        float tlim;
+        const Ray r = shadow_from_record(s, p, owner, &tlim);
+        p.occ[owner] = fallback_any(s, r, tlim, stk, w) ? 1 : 0;
+    }
+    if (p.totals[6]) {                             // the shadow queue overflowed: the marked bytes
+        const size_t nocc = ((size_t)p.la * (unsigned)p.cap + (size_t)(p.levels - p.la) * p.cb) * s.nlights;
+        for (size_t i = gt; i < nocc; i += gs)
+            if (p.occ[i] == kOccDeferred) {
+                float tlim;
+                const Ray r = shadow_from_record(s, p, (unsigned)i, &tlim);
+                p.occ[i] = fallback_any(s, r, tlim, stk, w) ? 1 : 0;
+            }
+    }
+}
+
 // Diagnostics (rt_walk_timing): wave 0 of one workgroup walks ray i with
 // lanes [0, lanes) (the same ray in every lane), reps times; lane 0 records
 // the last rep's shader cycles (s_memtime), the steps and the winner.  mode 0:
@@ -1566,22 +1644,15 @@ __global__ __launch_bounds__(kBlock) void k_walk_timing(rtk::DevScene s, const f
 
 }  // namespace
 
-// Shading + fold + SSAA: k_finish (a lane per pixel, default) or k_shade (a
-// lane per record) then k_compose (p.shade_split).
+// Shading + fold + SSAA: k_finish (a lane per pixel; materials and lights in LDS), or k_finish_any for
+// larger scenes.
 void launch_finish(const rtk::DevScene& s, const PcParams& p, hipStream_t st) {
     const int npix = (p.chunk_rows / p.aa) * p.width;
     const dim3 pgrid(std::max(1, std::min((npix + kBlock - 1) / kBlock, p.fin_grid > 0 ? p.fin_grid : INT32_MAX)));
-    if (!p.shade_split) {
-        if (s.nmats <= kFinishMats && s.nlights <= kFinishLights)
-            hipLaunchKernelGGL(k_finish, pgrid, dim3(kBlock), 0, st, s, p);
-        else
-            hipLaunchKernelGGL(k_finish_any, pgrid, dim3(kBlock), 0, st, s, p);
-        return;
-    }
-    const size_t nrec = (size_t)p.levels * (size_t)p.n0;
-    hipLaunchKernelGGL(k_shade, dim3((unsigned)std::max<size_t>(1, std::min<size_t>(65535, (nrec + kBlock - 1) / kBlock))),
-                       dim3(kBlock), 0, st, s, p);
-    hipLaunchKernelGGL(k_compose, pgrid, dim3(kBlock), 0, st, s, p);
+    if (s.nmats <= kFinishMats && s.nlights <= kFinishLights)
+        hipLaunchKernelGGL(k_finish, pgrid, dim3(kBlock), 0, st, s, p);
+    else
+        hipLaunchKernelGGL(k_finish_any, pgrid, dim3(kBlock), 0, st, s, p);
 }
 
 hipError_t chain_occupancy(int* chain_blocks_per_cu, int* mix_blocks_per_cu, int* occlude_blocks_per_cu) {
@@ -1655,8 +1726,8 @@ hipError_t launch_chain_chunk(const rtk::DevScene& s, const rtk::Eye& e, const P
     const dim3 blk(kBlock);
     auto mark = [&](int k) { if (kt) kt->mark(k, st); };
     const bool phase_b = p.kinline < s.max_depth;     // any continuation possible
-    if (p.dyn_units) {
-        const hipError_t me = hipMemsetAsync(p.totals + 3, 0, sizeof(unsigned), st);   // dynamic unit counter
+    {   // the dynamic unit counter and k_fallback's counts
+        const hipError_t me = hipMemsetAsync(p.totals + 3, 0, 4 * sizeof(unsigned), st);
         if (me != hipSuccess) return me;
     }
     mark(kKChain);
@@ -1688,6 +1759,8 @@ hipError_t launch_chain_chunk(const rtk::DevScene& s, const rtk::Eye& e, const P
     }
     // continued pixels first only where they are few and deep (one sample per pixel): with 16 samples
     // a pixel (C5: 130 vs 106 ms) and without phase B (C2: +5 %) the extra pinfo reads cost more
+    mark(kKFallback);
+    hipLaunchKernelGGL(k_fallback, dim3(p.fb_grid), blk, 0, st, s, e, p);
     PcParams f = p;
     f.fin_cont = phase_b && p.aa == 1;
     mark(kKFinish);

@@ -10,7 +10,7 @@
 //              -> append one shadow ray per light to a queue -> reflect ->
 //              closest hit ... (no shading, no shadow traversal on the chain)
 //   k_occlude  any-hit over the shadow queue, fully parallel
-//   k_compose  per output pixel: per sample, shade every recorded level with
+//   k_finish   per output pixel: per sample, shade every recorded level with
 //              the occlusion bytes and fold deepest-first
 //              c_k = clamp(L_k + c_{k+1} (x) km_k) (raytracer.cpp:385-452),
 //              toPixel, SSAA integer box filter
@@ -36,7 +36,13 @@ enum PathKind : int {
     kEndBg = 0,     // deepest ray missed at depth 0: background
     kEndZero = 1,   // deepest ray missed at depth > 0, or beyond MaxRecursionDepth: black
     kEndLast = 2,   // last recorded hit is not a mirror: its own clamp(L)
+    kEndTail = 3,   // levels >= nlev were finished by k_fallback: their folded colour is tail[path]
 };
+// k_fallback chain entries: the record id whose reflected ray was deferred, or kFbEye | sample for a
+// deferred eye ray
+constexpr unsigned kFbEye = 0x80000000u;
+// occlusion byte of a deferred shadow task whose fallback-queue slot overflowed (k_fallback scans for it)
+constexpr uint8_t kOccDeferred = 2;
 // pinfo bit of a path continued in phase B (set by phase A's hand-off, kept by phase B's end)
 constexpr int kPathCont = 1 << 16;
 
@@ -67,9 +73,25 @@ struct PcParams {
     int cap;          // path slots per chunk (>= n0)
     int levels;       // max_depth + 1 (>= 1)
     int nlights;
-    float4* rec;      // [levels][cap][3]: {hitp.xyz, mat}, {n.xyz, t}, {d.xyz, 0}
-    int* pinfo;       // [cap]: nlev | kind << 8
-    uint8_t* occ;     // [levels][cap][nl]
+    // Hit records, 32 B (pathchain.hip rec_write), by record id (rec_id): levels [0, la) of every sample
+    // at k * cap + sample (phase A), deeper levels only for the first cb continuations, at
+    // la * cap + (k - la) * cb + c for continuation c (phase B); occlusion bytes by record id * nl.
+    float4* rec;
+    int* pinfo;       // [cap]: nlev | kind << 8 | kPathCont
+    uint8_t* occ;
+    int la;           // levels stored for every sample (phase A's; all levels on the fused path)
+    unsigned cb;      // continuations with records (the rest finish in k_fallback)
+    unsigned* cid;    // [cap]: continuation index of a continued sample (k_pack_a)
+    float4* tail;     // [cap]: folded colour of the levels k_fallback finished (kEndTail)
+    // k_fallback's work: rays the timed walks do not take (NaN-free and in range for the wide trees'
+    // fused slab test, wide_walk_ok) and continuations beyond cb.  fbc: chain entries (kFbEye | sample
+    // or the record id whose reflection was deferred), totals[4] of them; fbs: shadow task owner ids,
+    // totals[5] of them, overflow flagged in totals[6] (the task's occlusion byte then kOccDeferred)
+    unsigned* fbc;
+    unsigned fbc_cap;
+    unsigned* fbs;
+    unsigned fbs_cap;
+    int fb_grid;      // k_fallback workgroups
     // phase A (k_chain: levels [0, kinline]) and phase B (k_mix chain role: deeper levels).
     // Task queues hold u32 owner ids; per-workgroup regions, counts, exclusive prefixes.
     unsigned* sqA;    // shadow tasks of A: [grid][scapA], owner = (level*cap + sample)*nl + light
@@ -84,13 +106,12 @@ struct PcParams {
     unsigned scapB;
     unsigned* scntB;  // [gb]
     unsigned* sflatB; // B's shadow tasks packed (k_pack_b), totals[2] of them
-    unsigned* totals; // [4]: packed task counts (3), phase-A unit counter
+    unsigned* totals; // [8]: packed task counts (3), phase-A unit counter, k_fallback chains / shadows / overflow
     int kinline;      // deepest level phase A walks (>= max_depth: no phase B)
     int gb;           // k_mix workgroups in the chain role (the other p.ogrid ones occlude A's tasks)
     int tchunk;       // continuation tasks (phase B) are dealt to workgroups in chunks of this many
     int ochunk;       // ... and shadow tasks (k_mix occlusion role, k_occlude) in chunks of this many
     int packet;       // 1: eye rays of a wave walk as one packet when exact (packet_closest)
-    int shade_split;  // 1: k_shade (a lane per record) + k_compose instead of k_finish
     int exp_skip_occ; // experiments only (RT_EXP_SKIP_OCC): k_mix's occlusion role does nothing (wrong images)
     int grid;         // k_chain persistent grid (= number of shadow-queue regions)
     int ogrid;        // k_occlude persistent grid
@@ -142,7 +163,7 @@ constexpr int kDynUnits = 128;
 // starting workgroup that owns slow pixels would stretch the frame).
 hipError_t chain_occupancy(int* chain_blocks_per_cu, int* mix_blocks_per_cu, int* occlude_blocks_per_cu);
 
-// Fused path: k_fused (chains + shadow rays, per-wave task queues) + k_compose.
+// Fused path: k_fused (chains + shadow rays, per-wave task queues) + k_finish.
 hipError_t fused_occupancy(int* blocks_per_cu);
 unsigned fused_wave_qcap(int n0, int grid, int levels, int nlights);
 hipError_t launch_fused_chunk(const rtk::DevScene& s, const rtk::Eye& e, const PcParams& p, bool count,
@@ -157,7 +178,7 @@ hipError_t launch_walk_timing(const rtk::DevScene& s, const float* rays, int n, 
 // Diagnostics (RT_KTIME=1 scenes, rt_kernel_times): HIP events recorded between the kernels of a
 // chain launch on its stream, so the host can split the launch's time per kernel (one slot: the
 // kernels run back to back).
-enum KernelKind : int { kKChain = 0, kKPackA, kKMix, kKOccA, kKPackB, kKOccB, kKFinish, kKEnd, kKKinds };
+enum KernelKind : int { kKChain = 0, kKPackA, kKMix, kKOccA, kKPackB, kKOccB, kKFinish, kKFallback, kKEnd, kKKinds };
 struct KTimer {
     static constexpr int kMax = 16;
     hipEvent_t ev[kMax] = {};

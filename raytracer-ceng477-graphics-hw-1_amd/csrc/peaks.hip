@@ -5,12 +5,14 @@
 //   * k_copy: streaming float4 copy of a buffer far larger than the Infinity
 //     Cache (read + write bytes over time) -- the HBM peak;
 //   * k_read: the same buffer read only (a running XOR) -- the HBM read peak;
-//   * k_gather: the BVH walks' access shape -- every lane reads whole random
-//     128-B lines (eight dwordx4, one wide node's line) of a table that every
-//     workgroup shares, many lines in flight per lane.  With a table that fits
-//     one XCD's 4 MiB L2 it is the L2 gather peak the walks are priced
-//     against; with the scene's own walk hot set it shows what that set's size
-//     costs (lines beyond L2 come from the Infinity Cache).
+//   * k_gather: random 128-B lines of a table every workgroup shares, many in
+//     flight per lane, in two shapes: each lane its own line (eight dwordx4:
+//     the walks' divergent node fetch, 64 distinct lines per wave
+//     instruction -- bound by the texture-address path, ~6 TB/s) and eight
+//     lanes per line (the same bytes, 8 distinct lines per instruction: what
+//     the L2 delivers to full-line fetches, ~25 TB/s).  With a table that fits
+//     one XCD's 4 MiB L2, and with the scene's own walk hot set (lines beyond
+//     L2 come from the Infinity Cache).
 // Times are best-of-N HIP event intervals on a private stream.
 #include <hip/hip_runtime.h>
 
@@ -53,20 +55,35 @@ __device__ __forceinline__ unsigned mix32(unsigned x) {
     return x;
 }
 
-// ITER iterations per lane, UNROLL independent random lines in flight per lane.
-template <int UNROLL>
+__device__ __forceinline__ unsigned pick(unsigned h, unsigned n) { return (unsigned)(((unsigned long long)h * n) >> 32); }
+
+// ITER iterations per lane, UNROLL independent random lines in flight per lane.  COOP = false: every
+// lane reads its own line (eight dwordx4, 64 distinct lines per wave instruction: the walks'
+// divergent fetch); COOP = true: the same bytes with the 8 lanes of each group reading the 8 pieces
+// of one line (8 distinct lines per wave instruction: what the L2 delivers to full-line fetches).
+template <int UNROLL, bool COOP>
 __global__ __launch_bounds__(kBlk) void k_gather(const float4* __restrict__ tab, unsigned nlines, int iters,
                                                  unsigned seed, unsigned* sink) {
     const unsigned gtid = blockIdx.x * kBlk + threadIdx.x;
+    const unsigned lane = threadIdx.x & 63;
     unsigned acc = 0;
     for (int it = 0; it < iters; it += UNROLL) {
         float4 v[UNROLL][8];
 #pragma unroll
         for (int u = 0; u < UNROLL; ++u) {
-            const unsigned line = mix32(gtid * 0x9e3779b1u + (unsigned)(it + u) * 0x85ebca6bu + seed) % nlines;
-            const float4* q = tab + (size_t)line * 8;
+            if (!COOP) {
+                const unsigned line = pick(mix32(gtid * 0x9e3779b1u + (unsigned)(it + u) * 0x85ebca6bu + seed), nlines);
+                const float4* q = tab + (size_t)line * 8;
 #pragma unroll
-            for (int j = 0; j < 8; ++j) v[u][j] = q[j];
+                for (int j = 0; j < 8; ++j) v[u][j] = q[j];
+            } else {
+#pragma unroll
+                for (int j = 0; j < 8; ++j) {
+                    const unsigned owner = (gtid & ~63u) + (lane >> 3) + 8u * (unsigned)j;
+                    const unsigned line = pick(mix32(owner * 0x9e3779b1u + (unsigned)(it + u) * 0x85ebca6bu + seed), nlines);
+                    v[u][j] = tab[(size_t)line * 8 + (lane & 7)];
+                }
+            }
         }
 #pragma unroll
         for (int u = 0; u < UNROLL; ++u)
@@ -145,14 +162,20 @@ extern "C" int rt_measure_peaks(int device, uint64_t scene_table_bytes, rt_peaks
         out->hbm_read_gbps = (double)big_bytes / (ms * 1e-3) / 1e9;
         const int iters = 64;
         const double gbytes = (double)grid.x * kBlk * iters * 128.0;
-        for (int which = 0; which < 2; ++which) {
-            const size_t tb = which == 0 ? small_table : scene_table;
+        for (int which = 0; which < 4; ++which) {
+            const size_t tb = (which & 1) == 0 ? small_table : scene_table;
             const unsigned nlines = (unsigned)(tb / 128);
-            ms = best_ms([&] { hipLaunchKernelGGL(k_gather<4>, grid, blk, 0, st, tab, nlines, iters, 17u + which, sink); }, 5);
+            const bool coop = which >= 2;
+            ms = best_ms([&] {
+                if (coop) hipLaunchKernelGGL((k_gather<2, true>), grid, blk, 0, st, tab, nlines, iters, 17u + which, sink);
+                else hipLaunchKernelGGL((k_gather<2, false>), grid, blk, 0, st, tab, nlines, iters, 17u + which, sink);
+            }, 5);
             if (ms <= 0) { err = "peaks: gather timing failed"; goto done; }
             const double gbps = gbytes / (ms * 1e-3) / 1e9;
             if (which == 0) { out->l2_gather_gbps = gbps; out->l2_table_bytes = (double)tb; }
-            else { out->scene_gather_gbps = gbps; out->scene_table_bytes = (double)tb; }
+            else if (which == 1) { out->scene_gather_gbps = gbps; out->scene_table_bytes = (double)tb; }
+            else if (which == 2) out->l2_line_gbps = gbps;
+            else out->scene_line_gbps = gbps;
         }
         PK_TRY(hipGetLastError());
     }

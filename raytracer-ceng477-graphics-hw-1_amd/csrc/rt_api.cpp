@@ -152,6 +152,11 @@ struct rt_scene {
     // is sized for the worst case (every sample recording every level), so the budget bounds the
     // samples per launch (and the frames per frame batch); it is split evenly over the slots.
     size_t ws_budget = size_t(16) << 30;
+    // RT_CONT_DEN: phase-B records for cap / den continuations per launch (C3: ~9 % of the samples
+    // continue; the rest, if any, finish in k_fallback); 1 = every sample
+    int tune_cont_den = 6;
+    int tune_cont_cb = 0;       // RT_CONT_CB (tests): exactly this many (k_fallback finishes the rest)
+    int tune_fbs_cap = 0;       // RT_FBS_CAP (tests): k_fallback shadow-queue slots (0: one per sample)
     size_t scene_bytes = 0;     // device bytes of the uploaded scene (trees, primitives, tables)
     bool ktime = false;         // RT_KTIME: per-kernel times of chain launches (rt_kernel_times; syncs each launch)
     double kt_ms[rtc::kKKinds] = {};
@@ -163,7 +168,8 @@ struct rt_scene {
     size_t slot_samples() const {
         const size_t levels = (size_t)std::max(dev.max_depth, 0) + 1, nl = (size_t)std::max(dev.nlights, 1);
         const size_t la = std::min((size_t)std::max(tune_kinline, 0), levels - 1) + 1;
-        const size_t per = levels * (32 + nl) + 4 + la * nl * 12 + 12 + (levels - la) * nl * 8;
+        const size_t per = la * (32 + nl) + 4 + 4 + 16 + 8 + la * nl * 12 + 12 +
+                           (levels - la) * (32 + nl + 8 * nl) / (size_t)std::max(1, tune_cont_den);
         return std::max<size_t>(4096, slot_budget() / per / 32 * 31);
     }
     std::string trace_file;     // RT_TRACE: dump per-sample wall-clock timings after each render (diagnostics)
@@ -365,6 +371,9 @@ int upload_scene(rt_scene* s, const rt_options* opts) {
     if (const char* e = std::getenv("RT_CREFILL")) s->tune_crefill = std::max(0, std::min(63, std::atoi(e)));
     if (const char* e = std::getenv("RT_TRACE")) s->trace_file = e;
     s->ktime = std::getenv("RT_KTIME") && std::atoi(std::getenv("RT_KTIME")) != 0;
+    if (const char* e = std::getenv("RT_CONT_DEN")) s->tune_cont_den = std::max(1, std::atoi(e));
+    if (const char* e = std::getenv("RT_CONT_CB")) s->tune_cont_cb = std::max(0, std::atoi(e));
+    if (const char* e = std::getenv("RT_FBS_CAP")) s->tune_fbs_cap = std::max(0, std::atoi(e));
     if (const char* e = std::getenv("RT_WS_BUDGET_MB"))
         s->ws_budget = std::max<size_t>(64, std::strtoull(e, nullptr, 10)) << 20;
 
@@ -433,6 +442,7 @@ int upload_scene(rt_scene* s, const rt_options* opts) {
     for (const auto& m : mats)
         if (!std::isfinite(m.kdx) || !std::isfinite(m.kdy) || !std::isfinite(m.kdz)) d.cull_shadows = 0;
     if (const char* e = std::getenv("RT_CULL")) d.cull_shadows = d.cull_shadows && std::atoi(e) != 0;
+    d.force_fb = std::getenv("RT_FORCE_FALLBACK") ? std::atoi(std::getenv("RT_FORCE_FALLBACK")) : 0;
     // measurement: counting passes walk the production trees and count fetched bytes (bench.py)
     d.count_prod = std::getenv("RT_COUNT_PROD") ? 1 : 0;
     if (const char* e = std::getenv("RT_PRIO")) d.prio = std::atoi(e) != 0;
@@ -588,9 +598,12 @@ struct ChainPlan {
     int G = 1, gb = 0, levels_a = 1, kinline = 0;
     bool phase_b = false, split_occ = false;
     unsigned dyn_units = 0, scapA = 0, ccapA = 0, scapB = 0, wq_cap = 0;
+    int la = 1, tchunk = 1;         // levels stored per sample; phase-B continuation chunk
+    size_t cb = 0;                  // continuations with phase-B records
     // arena offsets
     size_t o_rec = 0, o_pinfo = 0, o_occ = 0, o_sqA = 0, o_scntA = 0, o_sflatA = 0, o_cq = 0, o_ccnt = 0,
-           o_cflat = 0, o_sqB = 0, o_scntB = 0, o_sflatB = 0, o_totals = 0, o_wq = 0, bytes = 0;
+           o_cflat = 0, o_sqB = 0, o_scntB = 0, o_sflatB = 0, o_totals = 0, o_wq = 0, o_cid = 0, o_tail = 0,
+           o_fbc = 0, o_fbs = 0, bytes = 0;
 };
 
 int render_chain(rt_scene* s, const rtk::Eye& eye, const rtk::FrameParams& f, bool count, hipStream_t st,
@@ -645,12 +658,28 @@ int render_chain(rt_scene* s, const rtk::Eye& eye, const rtk::FrameParams& f, bo
         const unsigned units_a = P.dyn_units ? P.dyn_units : share;
         P.scapA = units_a * 256u * (unsigned)(P.levels_a * nl);
         P.ccapA = units_a * 256u;
-        P.scapB = P.phase_b ? (unsigned)(((cap + P.gb - 1) / P.gb) * (size_t)(levels - P.levels_a) * nl) : 0u;
+        // records: levels [0, la) for every sample; deeper ones (phase B) for the first cb continuations
+        // (the rest finish in k_fallback; counting passes keep every one: cb = cap)
+        P.la = fused || !P.phase_b ? levels : P.levels_a;
+        P.cb = P.la >= levels ? 0 : (count ? cap : std::min(cap, std::max(cap / (size_t)std::max(1, s->tune_cont_den),
+                                                                            std::min<size_t>(cap, 65536))));
+        if (s->tune_cont_cb > 0 && !count && P.la < levels) P.cb = std::min(cap, (size_t)s->tune_cont_cb);
+        P.tchunk = s->tune_tchunk > 0 ? s->tune_tchunk : (f.nframes > 1 ? 128 : 1);
+        {   // a phase-B workgroup's continuations: at most ceil(chunks / gb) chunks of tchunk (chunk_count)
+            const size_t ch = (size_t)P.tchunk, nch = (P.cb + ch - 1) / ch;
+            const size_t per_wg = P.gb > 0 ? (nch + P.gb - 1) / P.gb * ch : 0;
+            P.scapB = P.phase_b ? (unsigned)(per_wg * (size_t)(levels - P.la) * nl) : 0u;
+        }
         P.wq_cap = fused ? rtc::fused_wave_qcap((int)std::min<size_t>(cap, INT32_MAX), P.G, levels, nl) : 0u;
+        const size_t nrec = cap * P.la + P.cb * (levels - P.la);
         ArenaLayout L;
-        P.o_rec = L.take<float4>(2 * cap * levels);
+        P.o_rec = L.take<float4>(2 * nrec);
         P.o_pinfo = L.take<int>(cap);
-        P.o_occ = L.take<uint8_t>(cap * levels * nl + 8);   // + 8: k_finish reads aligned dwords
+        P.o_occ = L.take<uint8_t>(nrec * nl + 8);   // + 8: k_finish reads aligned dwords
+        P.o_cid = L.take<unsigned>(cap);
+        P.o_tail = L.take<float4>(cap);
+        P.o_fbc = L.take<unsigned>(cap);
+        P.o_fbs = L.take<unsigned>(cap);
         if (fused) {
             P.o_wq = L.take<unsigned>((size_t)P.G * 4 * P.wq_cap);
         } else {
@@ -659,8 +688,9 @@ int render_chain(rt_scene* s, const rtk::Eye& eye, const rtk::FrameParams& f, bo
             P.o_cq = L.take<unsigned>((size_t)P.G * P.ccapA); P.o_ccnt = L.take<unsigned>(P.G);
             P.o_cflat = L.take<unsigned>(cap);
             P.o_sqB = L.take<unsigned>((size_t)P.gb * P.scapB); P.o_scntB = L.take<unsigned>(P.gb + 1);
-            P.o_sflatB = L.take<unsigned>(cap * (levels - P.levels_a) * nl); P.o_totals = L.take<unsigned>(4);
+            P.o_sflatB = L.take<unsigned>(P.cb * (levels - P.la) * nl);
         }
+        P.o_totals = L.take<unsigned>(8);
         P.bytes = L.off;
         return P;
     };
@@ -728,6 +758,15 @@ int render_chain(rt_scene* s, const rtk::Eye& eye, const rtk::FrameParams& f, bo
     p.sqB = static_cast<unsigned*>(at(P.o_sqB)); p.scapB = P.scapB;
     p.scntB = static_cast<unsigned*>(at(P.o_scntB)); p.sflatB = static_cast<unsigned*>(at(P.o_sflatB));
     p.totals = static_cast<unsigned*>(at(P.o_totals));
+    p.la = P.la;
+    p.cb = (unsigned)P.cb;
+    p.cid = static_cast<unsigned*>(at(P.o_cid));
+    p.tail = static_cast<float4*>(at(P.o_tail));
+    p.fbc = static_cast<unsigned*>(at(P.o_fbc));
+    p.fbc_cap = (unsigned)cap;
+    p.fbs = static_cast<unsigned*>(at(P.o_fbs));
+    p.fbs_cap = s->tune_fbs_cap > 0 ? (unsigned)std::min<size_t>(cap, s->tune_fbs_cap) : (unsigned)cap;
+    p.fb_grid = s->num_cus;
     p.kinline = P.phase_b ? P.kinline : 1 << 30;
     p.gb = P.gb;
     p.ogrid = P.phase_b ? std::max(1, s->mix_grid - P.gb) : s->mix_grid;
@@ -745,11 +784,10 @@ int render_chain(rt_scene* s, const rtk::Eye& eye, const rtk::FrameParams& f, bo
     p.bprio = s->tune_bprio;
     // continuations dealt one at a time round-robin for a lone frame (its deep chains spread over
     // the phase-B workgroups: 1.12 -> 1.10 ms; 2: 1.11-1.14, 4: 1.12-1.13), in chunks of 128 in batches
-    p.tchunk = s->tune_tchunk > 0 ? s->tune_tchunk : (f.nframes > 1 ? 128 : 1);
+    p.tchunk = P.tchunk;
     p.ochunk = s->tune_ochunk;
     p.packet = s->tune_packet && s->bvh.max_stack <= dl::kMaxStack;
     p.exp_skip_occ = std::getenv("RT_EXP_SKIP_OCC") ? 1 : 0;
-    p.shade_split = std::getenv("RT_SHADE_SPLIT") ? std::atoi(std::getenv("RT_SHADE_SPLIT")) : 0;
     p.spread = s->tune_spread;
     p.dyn_units = (int)P.dyn_units;
     p.ublk_h = s->tune_ublk_h;

@@ -890,4 +890,20 @@ __device__ __forceinline__ int occl_step(const rtk::DevScene& s, const Ray& r, f
     return any_step<COUNT, FETCH>(s, r, tlim, stk, k, w);
 }
 
+// The timed (non-counting) kernels walk only the wide trees: a ray the wide trees' slab test does
+// not take is deferred to k_fallback before its walk begins (pathchain.hip defer_closest /
+// defer_any), so these kernels carry no binary-tree walk code and fit their register budgets without
+// spills.  Counting kernels keep the general steps (the reference tree, the production-fetch pass).
+template <bool COUNT, bool PIPE, class STK>
+__device__ __forceinline__ bool closest_step_timed(const rtk::DevScene& s, const Ray& r, STK& stk, Walk& k, Work& w) {
+    if constexpr (COUNT) return closest_step<COUNT, FetchGlobal, STK, PIPE>(s, r, stk, k, w);
+    else return wide_closest_step<false>(s, r, stk, k, w);
+}
+template <bool COUNT, class STK>
+__device__ __forceinline__ int occl_step_timed(const rtk::DevScene& s, const Ray& r, float tlim, STK& stk, Walk& k,
+                                               Work& w) {
+    if constexpr (COUNT) return occl_step<COUNT, FetchGlobal>(s, r, tlim, stk, k, w);
+    else return wide_any_step<false>(s, r, tlim, stk, k, w);
+}
+
 }  // namespace rtd
