@@ -249,10 +249,10 @@ int rt_scene_memory(const rt_scene* scene, uint64_t* scene_bytes, uint64_t* work
  * current one), ~1 s, allocates 4 GiB + the tables temporarily:
  *   hbm_copy_gbps      streaming float4 copy of 2 GiB (read + write bytes / time)
  *   hbm_read_gbps      the same buffer read only
- *   l2_gather_gbps     the BVH walks' divergent fetch: every lane reads whole random
- *                      128-B lines (eight dwordx4) of a table every workgroup shares,
- *                      2 lines in flight per lane; table of l2_table_bytes (2 MiB,
- *                      inside one XCD's 4 MiB L2)
+ *   l2_gather_gbps     the BVH walks' divergent fetch: every lane reads one random
+ *                      128-B line (eight dwordx4) per dependent step from a table every
+ *                      workgroup shares, best of 8..20 waves per CU; table of
+ *                      l2_table_bytes (2 MiB, inside one XCD's 4 MiB L2)
  *   scene_gather_gbps  the same over a table of scene_table_bytes (the caller's
  *                      walk hot set; lines beyond L2 come from the Infinity Cache)
  *   l2_line_gbps,      the same bytes with 8 lanes reading the 8 pieces of one line

@@ -34,8 +34,8 @@ namespace {
 
 constexpr int kBlock = 256;
 #ifndef RT_WAVES_PER_EU
-#define RT_WAVES_PER_EU 4     // k_chain: 4 waves/SIMD (118 VGPRs).  One frame at a time 5 waves (96 VGPRs)
-                              // won (1.36 -> 1.32 ms); with frame batches 4 wins (0.81-0.82 -> 0.79-0.80 ms/frame)
+#define RT_WAVES_PER_EU 5     // k_chain: 5 waves/SIMD (96 VGPRs, no spills since the binary-tree walks moved to
+                              // k_fallback; 4 waves: 100 VGPRs): C3 batches 0.480-0.486 -> 0.468-0.472 ms/frame
 #endif
 #ifndef RT_FINISH_PREFETCH
 #define RT_FINISH_PREFETCH 1   // k_finish: next level's record in flight while shading
@@ -914,7 +914,7 @@ __device__ __forceinline__ PhaseOut phase_b(const PcParams& p) {
 
 // Phase A: every sample, levels [0, kinline].
 template <bool COUNT>
-__global__ __launch_bounds__(kBlock, RT_WAVES_PER_EU) void k_chain(rtk::DevScene s, rtk::Eye e, PcParams p) {
+__global__ __launch_bounds__(kBlock, COUNT ? 4 : RT_WAVES_PER_EU) void k_chain(rtk::DevScene s, rtk::Eye e, PcParams p) {
     if (threadIdx.x == 0) g_ccnt = 0;
     if (threadIdx.x < kDynUnits) g_uid[threadIdx.x] = kUidUnset;
     block_init(s);

@@ -5,14 +5,14 @@
 //   * k_copy: streaming float4 copy of a buffer far larger than the Infinity
 //     Cache (read + write bytes over time) -- the HBM peak;
 //   * k_read: the same buffer read only (a running XOR) -- the HBM read peak;
-//   * k_gather: random 128-B lines of a table every workgroup shares, many in
-//     flight per lane, in two shapes: each lane its own line (eight dwordx4:
-//     the walks' divergent node fetch, 64 distinct lines per wave
-//     instruction -- bound by the texture-address path, ~6 TB/s) and eight
-//     lanes per line (the same bytes, 8 distinct lines per instruction: what
-//     the L2 delivers to full-line fetches, ~25 TB/s).  With a table that fits
-//     one XCD's 4 MiB L2, and with the scene's own walk hot set (lines beyond
-//     L2 come from the Infinity Cache).
+//   * k_walk: the walks' own fetch shape -- one dependent 128-B line per lane
+//     per step (eight dwordx4, each lane its own line: 64 distinct lines per
+//     wave instruction), best of 8..20 waves per CU (~10 TB/s);
+//   * k_gather (8 lanes per line): the same bytes as full-line fetches, 8
+//     distinct lines per wave instruction, many in flight -- what the L2
+//     delivers (~25 TB/s).
+//   Both over a table that fits one XCD's 4 MiB L2 and over a table the size
+//   of the scene's walk hot set (lines beyond L2 come from the Infinity Cache).
 // Times are best-of-N HIP event intervals on a private stream.
 #include <hip/hip_runtime.h>
 
@@ -27,9 +27,20 @@ namespace {
 
 constexpr int kBlk = 256;
 
-__global__ __launch_bounds__(kBlk) void k_copy(const float4* __restrict__ src, float4* __restrict__ dst, size_t n) {
+// four 16-B loads in flight per lane before their (nontemporal) stores (n: a multiple of 4 x the grid's
+// threads)
+typedef float f4v __attribute__((ext_vector_type(4)));
+__global__ __launch_bounds__(kBlk) void k_copy(const float4* __restrict__ src_, float4* __restrict__ dst_, size_t n) {
+    const f4v* src = reinterpret_cast<const f4v*>(src_);
+    f4v* dst = reinterpret_cast<f4v*>(dst_);
     const size_t stride = (size_t)gridDim.x * kBlk;
-    for (size_t i = (size_t)blockIdx.x * kBlk + threadIdx.x; i < n; i += stride) dst[i] = src[i];
+    for (size_t i = (size_t)blockIdx.x * kBlk + threadIdx.x; i + 3 * stride < n; i += 4 * stride) {
+        const f4v a = src[i], b = src[i + stride], c = src[i + 2 * stride], d = src[i + 3 * stride];
+        __builtin_nontemporal_store(a, dst + i);
+        __builtin_nontemporal_store(b, dst + i + stride);
+        __builtin_nontemporal_store(c, dst + i + 2 * stride);
+        __builtin_nontemporal_store(d, dst + i + 3 * stride);
+    }
 }
 
 __global__ __launch_bounds__(kBlk) void k_read(const float4* __restrict__ src, size_t n, unsigned* sink) {
@@ -95,6 +106,27 @@ __global__ __launch_bounds__(kBlk) void k_gather(const float4* __restrict__ tab,
     if (acc == 0x9e3779b9u) sink[0] = acc;
 }
 
+// The walks' own shape: one dependent 128-B line per lane per step (the next line from the data), each
+// lane its own line (eight dwordx4: 64 distinct lines per wave instruction), STEPS steps.
+__global__ __launch_bounds__(kBlk) void k_walk(const float4* __restrict__ tab, unsigned nlines, int steps,
+                                              unsigned* sink) {
+    unsigned line = pick(mix32(blockIdx.x * kBlk + threadIdx.x), nlines);
+    unsigned acc = 0;
+    for (int st = 0; st < steps; ++st) {
+        const float4* q = tab + (size_t)line * 8;
+        float4 v[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) v[j] = q[j];
+        unsigned h = 0;
+#pragma unroll
+        for (int j = 0; j < 8; ++j)
+            h ^= __float_as_uint(v[j].x) ^ __float_as_uint(v[j].y) ^ __float_as_uint(v[j].z) ^ __float_as_uint(v[j].w);
+        acc ^= h;
+        line = pick(mix32(h ^ (unsigned)st ^ ((blockIdx.x * kBlk + threadIdx.x) * 0x9e3779b1u)), nlines);
+    }
+    if (acc == 0x9e3779b9u) sink[0] = acc;
+}
+
 #define PK_TRY(expr)                                                                                 \
     do {                                                                                             \
         hipError_t e_ = (expr);                                                                      \
@@ -154,24 +186,36 @@ extern "C" int rt_measure_peaks(int device, uint64_t scene_table_bytes, rt_peaks
             return best;
         };
         const dim3 grid(cus * 8), blk(kBlk);
-        float ms = best_ms([&] { hipLaunchKernelGGL(k_copy, grid, blk, 0, st, big, big2, nbig); }, 5);
-        if (ms <= 0) { err = "peaks: copy timing failed"; goto done; }
-        out->hbm_copy_gbps = 2.0 * (double)big_bytes / (ms * 1e-3) / 1e9;
+        float ms = 0;
+        for (int wpc : {8, 16, 32}) {              // best over the grid size (2 GiB divides every grid's 4 x threads)
+            const dim3 cg(cus * wpc / 4);
+            ms = best_ms([&] { hipLaunchKernelGGL(k_copy, cg, blk, 0, st, big, big2, nbig); }, 5);
+            if (ms <= 0) { err = "peaks: copy timing failed"; goto done; }
+            out->hbm_copy_gbps = std::max(out->hbm_copy_gbps, 2.0 * (double)big_bytes / (ms * 1e-3) / 1e9);
+        }
         ms = best_ms([&] { hipLaunchKernelGGL(k_read, grid, blk, 0, st, big, nbig, sink); }, 5);
         if (ms <= 0) { err = "peaks: read timing failed"; goto done; }
         out->hbm_read_gbps = (double)big_bytes / (ms * 1e-3) / 1e9;
         const int iters = 64;
         const double gbytes = (double)grid.x * kBlk * iters * 128.0;
+        PK_TRY(hipMemcpyAsync(tab, big, tab_bytes, hipMemcpyDeviceToDevice, st));   // varied words (the walk's hash)
         for (int which = 0; which < 4; ++which) {
             const size_t tb = (which & 1) == 0 ? small_table : scene_table;
             const unsigned nlines = (unsigned)(tb / 128);
-            const bool coop = which >= 2;
-            ms = best_ms([&] {
-                if (coop) hipLaunchKernelGGL((k_gather<2, true>), grid, blk, 0, st, tab, nlines, iters, 17u + which, sink);
-                else hipLaunchKernelGGL((k_gather<2, false>), grid, blk, 0, st, tab, nlines, iters, 17u + which, sink);
-            }, 5);
-            if (ms <= 0) { err = "peaks: gather timing failed"; goto done; }
-            const double gbps = gbytes / (ms * 1e-3) / 1e9;
+            double gbps = 0;
+            if (which < 2) {           // the divergent walk shape, best of 8..20 waves per CU
+                const int wsteps = 128;
+                for (int wpc : {8, 12, 16, 20}) {
+                    const dim3 wg(cus * wpc / 4);
+                    ms = best_ms([&] { hipLaunchKernelGGL(k_walk, wg, blk, 0, st, tab, nlines, wsteps, sink); }, 3);
+                    if (ms <= 0) { err = "peaks: walk timing failed"; goto done; }
+                    gbps = std::max(gbps, (double)wg.x * kBlk * wsteps * 128.0 / (ms * 1e-3) / 1e9);
+                }
+            } else {                   // full-line fetches: 8 lanes per line
+                ms = best_ms([&] { hipLaunchKernelGGL((k_gather<2, true>), grid, blk, 0, st, tab, nlines, iters, 17u + which, sink); }, 5);
+                if (ms <= 0) { err = "peaks: gather timing failed"; goto done; }
+                gbps = gbytes / (ms * 1e-3) / 1e9;
+            }
             if (which == 0) { out->l2_gather_gbps = gbps; out->l2_table_bytes = (double)tb; }
             else if (which == 1) { out->scene_gather_gbps = gbps; out->scene_table_bytes = (double)tb; }
             else if (which == 2) out->l2_line_gbps = gbps;
