@@ -59,7 +59,7 @@ if stats:
         if k not in frame_kernels:
             continue
         calls, tot = int(r["Calls"]), float(r["TotalDurationNs"])
-        if k in ("k_pack_a", "k_pack_b", "k_finish", "k_finish_any", "k_occlude"):
+        if k in ("k_pack_a", "k_pack_b", "k_finish", "k_finish_any", "k_occlude", "k_fallback"):
             tot -= min(calls, counting_calls) * float(r["AverageNs"])     # the counting passes' launches
         per_kernel_ms[k] = tot / frames / 1e6
 kernel_ms_sum = sum(per_kernel_ms.values())
