@@ -80,7 +80,7 @@ struct LeafBig { int32_t start, count; };
 //             half) and 2*pair+1 (high half) of side 0 = lo, 1 = hi; decoded plane = fma(h, scale_a,
 //             origin_a) in f32 (h * scale exact, one rounding; the host verifies with the same fma that
 //             every decoded box CONTAINS the child's exact box); a ray picks its near/far side per axis
-//             by swapping whole dwords
+//             by swapping whole dwords; an empty slot holds lo = +inf, hi = -inf (never hit)
 //   dw 22-27  child codes (>= 0 wide-node index, < 0 kLeafBit | leaf-record offset; INT32_MAX empty)
 //   dw 28-31  reference-order tree: for the octants o = 0..3 of the ray direction (bit a set iff
 //             d[a] > 0; bit 2 clear), the rank of slot j in the reference's visiting order at bits

@@ -614,7 +614,12 @@ bool quantize_wide(const float (*lo)[3], const float (*hi)[3], int n, unsigned m
     // scale <= 2^40 to stay free of overflow; a scene beyond that keeps the binary trees
     for (int a = 0; a < 3; ++a)
         if (!(std::fabs(o[a]) <= 0x1p60f) || !(sc[a] <= 0x1p40f)) ok = false;
-    uint16_t hl[kMaxWideSlotsHost][3] = {}, hh[kMaxWideSlotsHost][3] = {};
+    // empty slots: lo = +inf, hi = -inf on every axis, so the device's slab test rejects them by
+    // itself (entry +inf, exit -inf, or NaN when a plane product underflows to 0: every comparison
+    // false) and needs no slot-mask test
+    uint16_t hl[kMaxWideSlotsHost][3], hh[kMaxWideSlotsHost][3];
+    for (int i = 0; i < kMaxWideSlotsHost; ++i)
+        for (int a = 0; a < 3; ++a) { hl[i][a] = 0x7c00; hh[i][a] = 0xfc00; }
     for (int i = 0; i < n; ++i) {
         if (!(mask >> i & 1u)) continue;
         for (int a = 0; a < 3; ++a) {

@@ -103,6 +103,7 @@ struct StackLds {
     // per-lane scratch entry that absorbs the writes of slots that push nothing (branch-free pushes)
     static constexpr int kLds = kLdsStackEntries;
     __device__ __forceinline__ void put_lds(int i, int2 v);
+    __device__ __forceinline__ int code_lds(int i);      // entry i (< kLds) .x
     // Deep tier as two int arrays: loads shaped unlike the LDS int2 read, so
     // the compiler cannot sink both tiers into one flat load through a
     // selected pointer (which waits on vmcnt and lgkmcnt at every pop).
@@ -114,6 +115,7 @@ struct StackLds {
 #if RT_LDS_STACK > 0
 __shared__ int2 g_lstk[(kLdsStackEntries + 1) * kBlock];
 __device__ __forceinline__ void StackLds::put_lds(int i, int2 v) { g_lstk[i * kBlock + threadIdx.x] = v; }
+__device__ __forceinline__ int StackLds::code_lds(int i) { return g_lstk[i * kBlock + threadIdx.x].x; }
 __device__ __forceinline__ void StackLds::put(int i, int2 v) {
     if (i < kLdsStackEntries) {
         g_lstk[i * kBlock + threadIdx.x] = v;
@@ -623,7 +625,7 @@ __device__ void chain_body(const rtk::DevScene& s, const rtk::Eye& e, const PcPa
     int k = 0;
     Ray r;
     Walk wk;
-    unsigned t_grab = 0, tsteps = 0;
+    unsigned t_grab = 0, tsteps = 0, twit = 0, wit = 0;   // trace: grab time, own steps, wave steps
     bool fresh = false;      // lane just took an eye ray (packet walk pending)
     StepStat stat;
     while (true) {
@@ -702,7 +704,7 @@ __device__ void chain_body(const rtk::DevScene& s, const rtk::Eye& e, const PcPa
                 if (p.trace && !CONT) { p.trace[2 * path] = t_grab; p.trace[2 * path + 1] = (unsigned)wall_clock64(); }
                 if (p.trace && CONT) {       // phase B: {grab, end, last level, walk steps} after A's entries
                     unsigned* tb = p.trace + 2 * ((size_t)p.cap + p.trace_blocks) + 4 * (size_t)path;
-                    tb[0] = t_grab; tb[1] = (unsigned)wall_clock64(); tb[2] = (unsigned)k; tb[3] = tsteps;
+                    tb[0] = t_grab; tb[1] = (unsigned)wall_clock64(); tb[2] = (unsigned)k | ((wit - twit) << 8); tb[3] = tsteps;
                 }
             } else {
                 r = reflect_ray(s, hitp, nn, r.d);
@@ -749,7 +751,7 @@ __device__ void chain_body(const rtk::DevScene& s, const rtk::Eye& e, const PcPa
                             path = lvp % (unsigned)p.cap;
                             k = (int)(lvp / (unsigned)p.cap) + 1;
                             cix = j;
-                            if (p.trace) { t_grab = (unsigned)wall_clock64(); tsteps = 0; }
+                            if (p.trace) { t_grab = (unsigned)wall_clock64(); tsteps = 0; twit = wit; }
                             r = reflect_from_record(s, p, lvp);
                             nrefl++;
                             if (!COUNT && defer_closest(s, r)) fb_chain(p, lvp);
@@ -797,6 +799,7 @@ __device__ void chain_body(const rtk::DevScene& s, const rtk::Eye& e, const PcPa
                 __popcll(__ballot(st == kDone)) >= (CONT ? (exhausted ? p.btail : p.bservice) : p.service))
                 break;
             stat.step(st == kTrav, wk.cur >= 0, RT_STEP_STATS && st == kTrav && wk.tree == nullptr && leaf_postponed(s.leaf_wait, wk));
+            if (CONT && p.trace) ++wit;
             if (st == kTrav) {
                 if (CONT && p.trace) ++tsteps;
                 if (closest_step_timed<COUNT, CONT>(s, r, stk, wk, w) || walk_runaway(s, wk)) st = kDone;

@@ -548,29 +548,37 @@ __device__ __forceinline__ bool wide_closest_step(const rtk::DevScene& s, const 
 #pragma unroll
         for (int c = 0; c < W; ++c) {
             rank[c] = (rw >> (3 * c)) & 7u;
-            const uint32_t v = ((mask >> c) & 1u) & (uint32_t)(tmx[c] >= __builtin_fmaxf(0.0f, tmn[c])) &
-                               (uint32_t)(tmn[c] <= k.tmax);
+            // empty slots hold +inf / -inf planes (quantize_wide): never valid, no mask test
+            const uint32_t v = (uint32_t)(tmx[c] >= __builtin_fmaxf(0.0f, tmn[c])) & (uint32_t)(tmn[c] <= k.tmax);
             vm |= v << rank[c];
             vs |= v << c;
         }
         if (vm) {
+            int pos[W];
+#pragma unroll
+            for (int c = 0; c < W; ++c)
+                pos[c] = k.sp + __builtin_popcount(vm >> (rank[c] + 1u));   // deeper the later it is visited
+            if (__all(k.sp + W <= STK::kLds)) {
+                // every valid slot of the wave lands in LDS, the first one (rank order) on top: one
+                // unconditional write per slot, then the next node is read back from the top (cheaper
+                // than selecting it and the pushes apart)
+#pragma unroll
+                for (int c = 0; c < W; ++c)
+                    stk.put_lds(((vs >> c) & 1u) ? pos[c] : STK::kLds, make_int2(code[c], __float_as_int(tmn[c])));
+                k.sp += __builtin_popcount(vm) - 1;
+                k.cur = stk.code_lds(k.sp);
+                return false;
+            }
             const uint32_t first = (uint32_t)__builtin_ctz(vm);
             int next = 0;
             bool push[W];
-            int pos[W];
 #pragma unroll
             for (int c = 0; c < W; ++c) {
                 const bool v = (vs >> c) & 1u;
                 next = (v && rank[c] == first) ? code[c] : next;
                 push[c] = v && rank[c] != first;
-                pos[c] = k.sp + __builtin_popcount(vm >> (rank[c] + 1u));   // deeper the later it is visited
             }
-            if (__all(k.sp + W - 1 <= STK::kLds)) {
-                // every push of the wave lands in LDS: one unconditional write per slot
-#pragma unroll
-                for (int c = 0; c < W; ++c)
-                    stk.put_lds(push[c] ? pos[c] : STK::kLds, make_int2(code[c], __float_as_int(tmn[c])));
-            } else {
+            {
 #pragma unroll
                 for (int c = 0; c < W; ++c)
                     if (push[c]) stk.put(pos[c], make_int2(code[c], __float_as_int(tmn[c])));
@@ -751,24 +759,27 @@ __device__ __forceinline__ int wide_any_step(const rtk::DevScene& s, const Ray& 
         wide_load(s.swnodes, k.cur, n);
         float tmn[W], tmx[W];
         wide_slabs(n, r, tmn, tmx);
-        const uint32_t mask = wide_dw(n, 3) >> 24;
-        uint32_t vs = 0;
+        uint32_t vs = 0;                  // empty slots: +inf / -inf planes, never valid (quantize_wide)
 #pragma unroll
-        for (int c = 0; c < W; ++c)
-            vs |= (((mask >> c) & 1u) & (uint32_t)(tmx[c] >= __builtin_fmaxf(0.0f, tmn[c]))) << c;
+        for (int c = 0; c < W; ++c) vs |= (uint32_t)(tmx[c] >= __builtin_fmaxf(0.0f, tmn[c])) << c;
         if (vs) {
-            // continue with the first hit slot, push the others in slot order (branch-free when the
-            // whole wave has LDS room for them)
+            if (__all(k.sp + W <= STK::kLds)) {
+                // the whole wave has LDS room: every hit slot written unconditionally, the first one
+                // on top, and the next node read back from the top
+#pragma unroll
+                for (int c = 0; c < W; ++c)
+                    stk.put_lds(((vs >> c) & 1u) ? k.sp + __builtin_popcount(vs >> (c + 1)) : STK::kLds,
+                                make_int2(wide_code(n, c), 0));
+                k.sp += __builtin_popcount(vs) - 1;
+                k.cur = stk.code_lds(k.sp);
+                return 0;
+            }
+            // continue with the first hit slot, push the others in slot order
             const uint32_t first = (uint32_t)__builtin_ctz(vs), pm = vs & (vs - 1u);
             int next = 0;
 #pragma unroll
             for (int c = 0; c < W; ++c) next = (uint32_t)c == first ? wide_code(n, c) : next;
-            if (__all(k.sp + W - 1 <= STK::kLds)) {
-#pragma unroll
-                for (int c = 0; c < W; ++c)
-                    stk.put_lds(((pm >> c) & 1u) ? k.sp + __builtin_popcount(pm & ((1u << c) - 1u)) : STK::kLds,
-                                make_int2(wide_code(n, c), 0));
-            } else {
+            {
 #pragma unroll
                 for (int c = 0; c < W; ++c)
                     if ((pm >> c) & 1u) stk.put(k.sp + __builtin_popcount(pm & ((1u << c) - 1u)), make_int2(wide_code(n, c), 0));

@@ -100,7 +100,8 @@ def main():
                 q = np.nonzero(okp)[0]
                 bs, be = rel(pb[okp, 0], t0), rel(pb[okp, 1], t0)
                 bd = be - bs
-                lv, stp = pb[okp, 2].astype(np.int64), pb[okp, 3].astype(np.int64)
+                lv, stp = (pb[okp, 2] & 255).astype(np.int64), pb[okp, 3].astype(np.int64)
+                wit = (pb[okp, 2] >> 8).astype(np.int64)      # the wave's walk iterations meanwhile
                 top = np.argsort(bd)[::-1][:8]
                 r["phase_b"] = {
                     "chains": int(okp.sum()),
@@ -108,9 +109,12 @@ def main():
                     "end_pct_us": {p: round(float(np.percentile(be, p)), 1) for p in (50, 90, 99, 99.9, 100)},
                     "dur_pct_us": {p: round(float(np.percentile(bd, p)), 1) for p in (50, 90, 99, 100)},
                     "steps_pct": {p: int(np.percentile(stp, p)) for p in (50, 90, 99, 100)},
+                    "wave_iters_pct": {p: int(np.percentile(wit, p)) for p in (50, 90, 99, 100)},
+                    "inflight_by_5pct": [int(((bs <= t) & (be > t)).sum()) for t in
+                                         np.linspace(bs.min(), be.max(), 21)[:-1]],
                     "last_level_hist": np.bincount(lv).tolist(),
                     "slowest": [{"q": int(q[j]), "start": round(float(bs[j]), 1), "dur": round(float(bd[j]), 1),
-                                 "level": int(lv[j]), "steps": int(stp[j]),
+                                 "level": int(lv[j]), "steps": int(stp[j]), "wave_iters": int(wit[j]),
                                  "us_per_step": round(float(bd[j]) / max(1, int(stp[j])), 2)} for j in top]}
             res.append(r)
         sc.close()
