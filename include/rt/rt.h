@@ -33,7 +33,7 @@
 extern "C" {
 #endif
 
-#define RT_ABI_VERSION 7
+#define RT_ABI_VERSION 8
 
 typedef enum rt_status {
     RT_OK = 0,
@@ -239,6 +239,11 @@ int rt_walk_timing(rt_scene* scene, const float* rays, int n, int lanes, int rep
  * (raytracer.cpp:414) -- on the current device (host arrays, synchronous;
  * ABI 5). */
 int rt_phong_pow(const float* base, const float* exponent, float* out, int n);
+/* Diagnostics: out[3i+j] = num[3i+j] / den[i] as the device's triangle test
+ * (raytracer.cpp:147, 154, 161) evaluates its three Cramer quotients: one
+ * shared reciprocal, the correctly rounded float quotients (host arrays,
+ * synchronous; ABI 8). */
+int rt_cramer_div(const float* den, const float* num, float* out, int n);
 /* HBM held by a scene on its (first) device (ABI 7): the uploaded scene (trees,
  * primitives, tables) and the render workspaces allocated so far (chain-path
  * arenas of every slot, output staging).  The workspaces grow on demand up to

@@ -164,6 +164,7 @@ _SIGS = [
                                                ctypes.c_int, ctypes.c_int, _P, _P, ctypes.c_int]),
     ("rt_walk_timing", ctypes.c_int, [_P, _P, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int, _P]),
     ("rt_phong_pow", ctypes.c_int, [_P, _P, _P, ctypes.c_int]),
+    ("rt_cramer_div", ctypes.c_int, [_P, _P, _P, ctypes.c_int]),
     ("rt_measure_peaks", ctypes.c_int, [ctypes.c_int, ctypes.c_uint64, _P]),
     ("rt_scene_memory", ctypes.c_int, [_P, ctypes.POINTER(ctypes.c_uint64), ctypes.POINTER(ctypes.c_uint64)]),
     ("rt_slab_rows", ctypes.c_int, [ctypes.c_int, ctypes.c_int, ctypes.c_int]),
@@ -225,6 +226,19 @@ def phong_pow(base, exponent) -> np.ndarray:
     out = np.empty_like(b)
     _check(lib().rt_phong_pow(b.ctypes.data_as(ctypes.c_void_p), e.ctypes.data_as(ctypes.c_void_p),
                               out.ctypes.data_as(ctypes.c_void_p), b.size))
+    return out
+
+
+def cramer_div(den, num) -> np.ndarray:
+    """Diagnostics (rt_cramer_div): num[i, j] / den[i] (j = 0..2) as the device's triangle test
+    computes its Cramer quotients (raytracer.cpp:147, 154, 161)."""
+    d = np.ascontiguousarray(den, dtype=np.float32).reshape(-1)
+    nm = np.ascontiguousarray(num, dtype=np.float32).reshape(-1, 3)
+    if nm.shape[0] != d.size:
+        raise ValueError("num must hold three numerators per denominator")
+    out = np.empty_like(nm)
+    _check(lib().rt_cramer_div(d.ctypes.data_as(ctypes.c_void_p), nm.ctypes.data_as(ctypes.c_void_p),
+                               out.ctypes.data_as(ctypes.c_void_p), d.size))
     return out
 
 

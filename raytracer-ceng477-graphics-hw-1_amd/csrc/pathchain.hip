@@ -1705,6 +1705,18 @@ hipError_t launch_phong_pow(const float* base, const float* expo, float* out, in
     return hipGetLastError();
 }
 
+// Diagnostics (rt_cramer_div): the triangle test's three quotients exactly as tri_hit evaluates
+// them (cramer_div3: one shared reciprocal, IEEE divisions for the lanes outside its range).
+__global__ __launch_bounds__(kBlock) void k_cramer_div(const float* den, const float* num, float* out, int n) {
+    const int i = (int)(blockIdx.x * kBlock + threadIdx.x);
+    if (i < n) rtd::cramer_div3(den[i], num[3 * i], num[3 * i + 1], num[3 * i + 2], out[3 * i], out[3 * i + 1], out[3 * i + 2]);
+}
+
+hipError_t launch_cramer_div(const float* den, const float* num, float* out, int n, hipStream_t st) {
+    hipLaunchKernelGGL(k_cramer_div, dim3((n + kBlock - 1) / kBlock), dim3(kBlock), 0, st, den, num, out, n);
+    return hipGetLastError();
+}
+
 // Diagnostics (RT_STEP_STATS builds): read (and optionally clear) g_step_stat.
 extern "C" int rt_debug_step_stats(unsigned long long* out, int reset) {
     if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_step_stat), sizeof(g_step_stat)) != hipSuccess) return -1;

@@ -1339,6 +1339,20 @@ int rt_phong_pow(const float* base, const float* exponent, float* out, int n) {
     return RT_OK;
 }
 
+int rt_cramer_div(const float* den, const float* num, float* out, int n) {
+    if (!den || !num || !out || n < 0) return fail(RT_ERR_ARG, "bad cramer_div arguments");
+    if (n == 0) return RT_OK;
+    float* d = nullptr;
+    HIP_TRY(hipMalloc(reinterpret_cast<void**>(&d), (size_t)n * 7 * sizeof(float)));
+    hipError_t e = hipMemcpy(d, den, (size_t)n * sizeof(float), hipMemcpyHostToDevice);
+    if (e == hipSuccess) e = hipMemcpy(d + n, num, (size_t)n * 3 * sizeof(float), hipMemcpyHostToDevice);
+    if (e == hipSuccess) e = rtc::launch_cramer_div(d, d + n, d + 4 * (size_t)n, n, nullptr);
+    if (e == hipSuccess) e = hipMemcpy(out, d + 4 * (size_t)n, (size_t)n * 3 * sizeof(float), hipMemcpyDeviceToHost);
+    (void)hipFree(d);
+    if (e != hipSuccess) return fail(RT_ERR_HIP, std::string("cramer_div: ") + hipGetErrorName(e));
+    return RT_OK;
+}
+
 int rt_unshuffle_stripes(const void* slabs, void* image, int width, int height, int stripe_rows, int nranks,
                          void* stream) {
     if (!slabs || !image || width < 1 || height < 1 || stripe_rows < 1 || nranks < 1)

@@ -104,15 +104,53 @@ __device__ __forceinline__ float det3(float m00, float m01, float m02, float m10
     return m00 * (m11 * m22 - m12 * m21) - m01 * (m10 * m22 - m12 * m20) + m02 * (m10 * m21 - m11 * m20);
 }
 
+// The three Cramer quotients n_i / den (raytracer.cpp:147, 154, 161), each the correctly rounded float
+// quotient, from ONE reciprocal instead of three IEEE division sequences:
+//   r = 1/den in double (the f32 reciprocal, ~2^-22, and two Newton steps: relative error
+//   < 2^-52.9), q_i = RN_53(n_i * r) (relative error < 2^-51.9), then RN_24(q_i).
+// Exact: for floats a, b (24-bit significands) the quotient a/b is never a rounding midpoint of
+// the float grid and lies at relative distance > 2^-49 from every one (a - m b is a non-zero
+// multiple of 2^min(e_a, e_m + e_b); |a/b| < 2^24 ulp), so a value within 2^-51.9 of a/b rounds to
+// RN_24(a/b).  That argument needs a normal-range result; zero is exact (sign included).  Lanes
+// with |den| outside [2^-100, 2^100] (or not finite) or any |q_i| < 2^-125 (zero included) take the IEEE
+// divisions (a wave-uniform branch, taken only when some lane needs it).  The float results are
+// checked: |RN_24(q)| >= 2^-125 implies q > 2^-126 (normal).
+__device__ __forceinline__ void cramer_div3(float den, float n0, float n1, float n2, float& q0, float& q1,
+                                            float& q2) {
+    const double D = (double)den;
+    double r = (double)__builtin_amdgcn_rcpf(den);
+    double e = __builtin_fma(-D, r, 1.0);
+    r = __builtin_fma(e, r, r);
+    e = __builtin_fma(-D, r, 1.0);
+    r = __builtin_fma(e, r, r);
+    const double d0 = (double)n0 * r, d1 = (double)n1 * r, d2 = (double)n2 * r;
+    q0 = (float)d0;
+    q1 = (float)d1;
+    q2 = (float)d2;
+    const float ad = __builtin_fabsf(den);
+    // (a zero quotient is exact too, but rare enough to send along: one min3 and one compare)
+    const bool tiny = !(__builtin_fminf(__builtin_fminf(__builtin_fabsf(q0), __builtin_fabsf(q1)), __builtin_fabsf(q2)) >=
+                        0x1p-125f);
+    const bool exact = !(ad >= 0x1p-100f && ad <= 0x1p100f) || tiny;
+    if (__builtin_expect(__any(exact), 0)) {
+        if (exact) {
+            q0 = n0 / den;
+            q1 = n1 / den;
+            q2 = n2 / den;
+        }
+    }
+}
+
 // Ray::intersects(Scene&, Triangle&) (raytracer.cpp:129-175), Cramer's rule.
 // e1 = a-b, e2 = a-c (precomputed bit-identically at build time).
 __device__ __forceinline__ bool tri_hit(const Ray& r, const float4 a, const float4 e1, const float4 e2, float* tout) {
     const V d = r.d;
     const float aox = a.x - r.o.x, aoy = a.y - r.o.y, aoz = a.z - r.o.z;
     const float detA = det3(e1.x, e2.x, d.x, e1.y, e2.y, d.y, e1.z, e2.z, d.z);
-    const float beta = det3(aox, e2.x, d.x, aoy, e2.y, d.y, aoz, e2.z, d.z) / detA;
-    const float gamma = det3(e1.x, aox, d.x, e1.y, aoy, d.y, e1.z, aoz, d.z) / detA;
-    const float t = det3(e1.x, e2.x, aox, e1.y, e2.y, aoy, e1.z, e2.z, aoz) / detA;
+    float beta, gamma, t;
+    cramer_div3(detA, det3(aox, e2.x, d.x, aoy, e2.y, d.y, aoz, e2.z, d.z),
+                det3(e1.x, aox, d.x, e1.y, aoy, d.y, e1.z, aoz, d.z),
+                det3(e1.x, e2.x, aox, e1.y, e2.y, aoy, e1.z, e2.z, aoz), beta, gamma, t);
     const float alpha = 1.0f - beta - gamma;
     *tout = t;
     return alpha >= 0 && beta >= 0 && gamma >= 0 && t >= 0.0f;

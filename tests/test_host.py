@@ -32,7 +32,7 @@ def test_library_exports_every_declared_symbol(pkg):
         assert hasattr(L, n), n
     bound = {s[0] for s in pkg._SIGS}
     assert set(names) == bound, "ctypes bindings out of sync with rt.h"
-    assert L.rt_abi_version() == 7
+    assert L.rt_abi_version() == 8
 
 
 def test_cli_binary_built(pkg):
@@ -264,3 +264,27 @@ def test_fused_slab_margin_is_conservative(tmp_path):
     checked, bad, left = out.stdout.split()[-3:]
     assert int(bad) == 0, out.stdout
     assert int(checked) > 15_000_000 and float(left) >= 0.5
+
+
+def test_cramer_shared_reciprocal_is_correctly_rounded(tmp_path):
+    """The triangle test's three quotients from one reciprocal (rt_device.hpp cramer_div3) equal
+    the reference's three IEEE float divisions (raytracer.cpp:147, 154, 161) wherever the fast path
+    is taken: 26 M quotients, random over the exponent range and built to lie within a few ulps of
+    the float grid's rounding midpoints, with the f32 reciprocal perturbed up to 2^-21.  Control:
+    one Newton step instead of two must fail on the near-midpoint cases."""
+    import shutil
+    import subprocess
+    from pathlib import Path
+    cxx = shutil.which("g++")
+    if cxx is None:
+        pytest.skip("g++ not available")
+    root = Path(__file__).resolve().parent.parent
+    exe = tmp_path / "cramer_div_check"
+    subprocess.run([cxx, "-O2", "-std=c++17", "-ffp-contract=off",
+                    str(root / "tests" / "native" / "cramer_div_check.cpp"), "-o", str(exe)], check=True)
+    out = subprocess.run([str(exe), "2000000"], capture_output=True, text=True, timeout=300)
+    checked, bad, frac = out.stdout.split()[-3:]
+    assert int(bad) == 0, out.stdout
+    assert int(checked) > 25_000_000 and float(frac) > 0.8
+    ctl = subprocess.run([str(exe), "200000", "1"], capture_output=True, text=True, timeout=300)
+    assert int(ctl.stdout.split()[-2]) > 0, "the check does not see a one-step reciprocal"

@@ -17,7 +17,7 @@ def main():
     src = sys.argv[1] if len(sys.argv) > 1 else "csrc/pathchain.hip"
     extra = sys.argv[2:]
     cmd = ["/opt/rocm/bin/hipcc", "-std=c++17", "-O3", "--offload-arch=gfx950", "-ffp-contract=off",
-           "-fno-fast-math", "-fPIC", f"-I{ROOT / 'include'}", "-Icsrc", "--cuda-device-only", "-c", src,
+           "-fno-fast-math", "-fno-slp-vectorize", "-fPIC", f"-I{ROOT / 'include'}", "-Icsrc", "--cuda-device-only", "-c", src,
            "-o", "/tmp/resource_usage.o", "-Rpass-analysis=kernel-resource-usage", *extra]
     out = subprocess.run(cmd, cwd=PKG, capture_output=True, text=True).stderr
     rows, cur = [], None
