@@ -48,7 +48,7 @@ constexpr int kBlock = 256;
 #define RT_FINISH_ANY_WAVES 1 // k_finish_any (large scenes): at 4 waves it spills a VGPR
 #endif
 #ifndef RT_OCC_WAVES_PER_EU
-#define RT_OCC_WAVES_PER_EU 5     // k_mix / k_occlude (the any-hit bulk); 5/5 measured best of 4..6
+#define RT_OCC_WAVES_PER_EU 6     // k_occlude (the any-hit bulk): 79 VGPRs, no spills (round 3; was 5)
 #endif
 
 enum LaneState : int { kIdle = 0, kTrav = 1, kDone = 2 };
