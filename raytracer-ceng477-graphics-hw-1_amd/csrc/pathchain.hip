@@ -908,6 +908,224 @@ __device__ void occlude_body(const rtk::DevScene& s, const PcParams& p, unsigned
     }
 }
 
+// ---------------------------------------------------------------------------
+// Any-hit walks with a wave leaf queue (A's shadow rays: k_occlude, and k_mix's shadow role).
+// Any hit is order-free (raytracer.cpp:227-280: the answer is whether SOME reachable leaf -- its
+// exact box hit -- holds a primitive with t < dist), so a lane that reaches a leaf record does not
+// test it: it appends (lane, record) to its wave's LDS queue and walks on.  Interior steps then run
+// with every walking lane (no lane waits at a leaf, no step issues both kinds), and once 64 records
+// are queued (or no lane walks) the whole wave tests 64 of them at once, each lane one record
+// against its owner lane's ray (fetched by lane shuffles).  A hit marks the owner occluded, which
+// ends its walk; a lane's ray is unoccluded when its walk is over and none of its queued records
+// hit.  A lane takes its next task only once its queued records are all tested.  The same leaves
+// are tested with the same arithmetic as wide_any_step, so the answer is the same; an occluded ray
+// may walk a few more nodes before its record is tested.
+// LDS: the walk-stack array g_lstk, re-cut as ints (this role has no closest-hit walks): per lane
+// kOStk stack entries + one sink entry, per wave a kLq-entry queue, per lane its queued count.
+// ---------------------------------------------------------------------------
+#ifndef RT_LEAF_QUEUE
+#define RT_LEAF_QUEUE 1
+#endif
+constexpr int kOStk = 22;                 // LDS stack entries per lane (deeper ones in scratch)
+constexpr int kLq = 128;                  // queued leaf records per wave (tested 64 at a time)
+constexpr int kLqSrcShift = 25;           // queue entry: leaf-record offset | owner lane << 25
+static_assert(2 * (kLdsStackEntries + 1) * kBlock >= (kOStk + 1) * kBlock + (kBlock / 64) * kLq + kBlock,
+              "the occlusion walker's stack, queues and counts must fit in g_lstk");
+__shared__ unsigned g_lqn[kBlock / 64];            // per wave: queued records
+__shared__ unsigned long long g_lhit[kBlock / 64]; // per wave: lanes whose ray a tested record occludes
+
+__device__ __forceinline__ int* oq_base() { return reinterpret_cast<int*>(g_lstk); }
+__device__ __forceinline__ void ostk_lds_put(int i, int v) { oq_base()[i * kBlock + threadIdx.x] = v; }
+__device__ __forceinline__ int ostk_lds_at(int i) { return oq_base()[i * kBlock + threadIdx.x]; }
+__device__ __forceinline__ unsigned* lq_base() {
+    return reinterpret_cast<unsigned*>(oq_base() + (kOStk + 1) * kBlock) + (threadIdx.x >> 6) * kLq;
+}
+__device__ __forceinline__ int* lpend_base() { return oq_base() + (kOStk + 1) * kBlock + (kBlock / 64) * kLq; }
+
+struct OStack {   // int entries: [0, kOStk) in LDS, deeper in scratch
+    int d[dl::kMaxStack > kOStk ? dl::kMaxStack - kOStk : 1];
+    __device__ __forceinline__ void put(int i, int v) {
+        if (i < kOStk) ostk_lds_put(i, v);
+        else d[i - kOStk] = v;
+    }
+    __device__ __forceinline__ int at(int i) { return i < kOStk ? ostk_lds_at(i) : d[i - kOStk]; }
+};
+
+// Test 64 queued records of this wave (lane j: entry j < n), mark the owners they occlude, retire
+// the entries and shift the rest down.
+__device__ __forceinline__ void lq_flush(const rtk::DevScene& s, const Ray& r, float tlim, unsigned nq) {
+    const int lane = lane_id(), wave = (int)(threadIdx.x >> 6);
+    unsigned* const q = lq_base();
+    const unsigned n = min(nq, 64u);
+    const bool valid = (unsigned)lane < n;
+    const unsigned e = valid ? q[lane] : 0u;
+    const int src = (int)(e >> kLqSrcShift);
+    // the owner lane's ray (every lane takes part in the shuffles)
+    Ray o;
+    o.o = V{__shfl(r.o.x, src, 64), __shfl(r.o.y, src, 64), __shfl(r.o.z, src, 64)};
+    o.d = V{__shfl(r.d.x, src, 64), __shfl(r.d.y, src, 64), __shfl(r.d.z, src, 64)};
+    o.inv = V{__shfl(r.inv.x, src, 64), __shfl(r.inv.y, src, 64), __shfl(r.inv.z, src, 64)};
+    const float olim = __shfl(tlim, src, 64);
+    // the rest of the queue moves down (all reads before any write: one wave, LDS in order)
+    const unsigned rest = nq - n;
+    const unsigned mv = (unsigned)lane < rest ? q[n + lane] : 0u;
+    if (valid) {
+        const float4* L = s.lrec + (e & ((1u << kLqSrcShift) - 1u));
+        const float4 h0 = L[0], h1 = L[1], c0 = L[2], c1 = L[3], c2 = L[4];
+        float bt;
+        bool hit = false;
+        if (box_hit_fast(o, h0, h1, &bt)) {          // the reference leaf's exact box (NaN-free ray)
+            const int cnt = __float_as_int(h0.w), slot0 = __float_as_int(h1.w);
+            hit = for_leaf_prims(L, slot0, cnt, c0, c1, c2, [&](int, const float4& p0, const float4& p1, const float4& p2) {
+                float t;
+                const bool h = __float_as_int(p0.w) >= 0 ? tri_hit(o, p0, p1, p2, &t) : sphere_hit(o, p0, p1, &t);
+                return h && t < olim;
+            });
+        }
+        if (hit) atomicOr(&g_lhit[wave], 1ull << src);
+        atomicSub(&lpend_base()[(wave << 6) + src], 1);
+    }
+    if ((unsigned)lane < rest) q[lane] = mv;
+    if (lane == 0) __atomic_store_n(&g_lqn[wave], rest, __ATOMIC_RELAXED);
+}
+
+// The shadow tasks tasks[j] of this workgroup (as occlude_body) with the leaf queue; production only.
+__device__ void occlude_queue_body(const rtk::DevScene& s, const PcParams& p, unsigned blk, unsigned G,
+                                   const unsigned* tasks, unsigned total) {
+    const int lane = lane_id(), wave = (int)(threadIdx.x >> 6);
+    const unsigned n = chunk_count(total, G, blk, (unsigned)p.ochunk);
+    // the queue count, the hit mask and the queued counts are written by other lanes of the wave:
+    // every read is an atomic load (no value kept in a register across the loop)
+    if (lane == 0) {
+        __atomic_store_n(&g_lqn[wave], 0u, __ATOMIC_RELAXED);
+        __atomic_store_n(&g_lhit[wave], 0ull, __ATOMIC_RELAXED);
+    }
+    int* const pend = lpend_base() + threadIdx.x;
+    __atomic_store_n(pend, 0, __ATOMIC_RELAXED);
+    OStack stk;
+    bool exhausted = n == 0;
+    bool have = false, trav = false, done = false;   // a task; walking it; its answer written
+    Ray r;
+    r.o = r.d = r.inv = V{0.0f, 0.0f, 0.0f};
+    float tlim = 0.0f;
+    unsigned owner = 0;
+    int cur = 0, sp = 0, steps = 0;
+    while (true) {
+        // (1) retire finished tasks: occluded (a record hit), or walked with every record tested
+        {
+            const unsigned long long hm = __atomic_load_n(&g_lhit[wave], __ATOMIC_RELAXED);
+            if (have && !done && ((hm >> lane) & 1ull)) {
+                p.occ[owner] = 1;
+                done = true;
+                trav = false;
+            }
+            if (have && !trav && __atomic_load_n(pend, __ATOMIC_RELAXED) == 0) {
+                if (!done) p.occ[owner] = 0;
+                have = false;
+            }
+            const unsigned long long freed = __ballot(!have) & hm;
+            if (freed && lane == 0) atomicAnd(&g_lhit[wave], ~freed);   // the next task starts unmarked
+        }
+        // (2) refill lanes without a task
+        if (!exhausted) {
+            const unsigned long long idle = __ballot(!have);
+            if (idle && __popcll(idle) >= 64 - p.orefill) {
+                const unsigned base = wave_grab_lds(&g_head, idle);
+                if (base + (unsigned)__popcll(idle) >= n) exhausted = true;
+                if (!have) {
+                    const unsigned idx = base + lane_rank(idle);
+                    if (idx < n) {
+                        owner = tasks[chunk_task(idx, G, blk, (unsigned)p.ochunk)];
+                        r = shadow_from_record(s, p, owner, &tlim);
+                        if (defer_any(s, r)) {
+                            fb_shadow(p, owner);
+                        } else if (s.nnodes <= 0) {   // nothing to hit (walk_begin)
+                            p.occ[owner] = 0;
+                        } else {
+                            have = true;
+                            trav = true;
+                            done = false;
+                            cur = s.swroot;
+                            sp = 0;
+                            steps = 0;
+                        }
+                    }
+                }
+            }
+        }
+        if (!__any(have)) {
+            if (exhausted) break;
+            continue;
+        }
+        // (3) walk: queue the leaf records reached, step the interior nodes, until 64 records wait
+        //     or no lane walks (or, with tasks left, too few lanes walk)
+        while (true) {
+            // drain leaf codes into the queue (each pass adds at most one record per lane)
+            while (true) {
+                const bool atleaf = trav && cur < 0;
+                const unsigned long long lm = __ballot(atleaf);
+                if (!lm) break;
+                const unsigned nq = __atomic_load_n(&g_lqn[wave], __ATOMIC_RELAXED);
+                if (nq + (unsigned)__popcll(lm) > (unsigned)kLq) break;
+                if (atleaf) {
+                    lq_base()[nq + lane_rank(lm)] = ((unsigned)cur & ~dl::kLeafBit) | ((unsigned)lane << kLqSrcShift);
+                    atomicAdd(pend, 1);
+                    if (sp > 0) cur = stk.at(--sp);
+                    else trav = false;
+                }
+                if (lane == 0) __atomic_store_n(&g_lqn[wave], nq + (unsigned)__popcll(lm), __ATOMIC_RELAXED);
+            }
+            const unsigned long long im = __ballot(trav && cur >= 0);
+            if (__atomic_load_n(&g_lqn[wave], __ATOMIC_RELAXED) >= 64u || !im) break;
+            if (__popcll(__ballot(have && !trav)) >= p.lq_wait) break;
+            if (!exhausted && __popcll(__ballot(have)) <= p.orefill) break;
+            if (trav && cur >= 0) {
+                constexpr int W = dl::kWideSlots;
+                WideNode nd;
+                wide_load(s.swnodes, cur, nd);
+                float tmn[W], tmx[W];
+                wide_slabs(nd, r, tmn, tmx);
+                uint32_t vs = 0;                  // empty slots: +inf / -inf planes, never hit
+#pragma unroll
+                for (int c = 0; c < W; ++c) vs |= (uint32_t)(tmx[c] >= __builtin_fmaxf(0.0f, tmn[c])) << c;
+                if (vs) {
+                    if (__all(!(trav && cur >= 0) || sp + W <= kOStk)) {
+                        // every hit slot written unconditionally (misses to the sink entry), the
+                        // first on top, which is the next node
+#pragma unroll
+                        for (int c = 0; c < W; ++c)
+                            ostk_lds_put(((vs >> c) & 1u) ? sp + __builtin_popcount(vs >> (c + 1)) : kOStk, wide_code(nd, c));
+                        sp += __builtin_popcount(vs) - 1;
+                        cur = ostk_lds_at(sp);
+                    } else {
+                        const uint32_t first = (uint32_t)__builtin_ctz(vs), pm = vs & (vs - 1u);
+                        int next = 0;
+#pragma unroll
+                        for (int c = 0; c < W; ++c) {
+                            next = (uint32_t)c == first ? wide_code(nd, c) : next;
+                            if ((pm >> c) & 1u) stk.put(sp + __builtin_popcount(pm & ((1u << c) - 1u)), wide_code(nd, c));
+                        }
+                        sp += __builtin_popcount(pm);
+                        cur = next;
+                    }
+                } else if (sp > 0) {
+                    cur = stk.at(--sp);
+                } else {
+                    trav = false;
+                }
+                if (trav && ++steps > s.walk_cap) {          // walk_runaway: ended as unoccluded
+                    __hip_atomic_fetch_or(s.err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    trav = false;
+                }
+            }
+        }
+        // (4) test queued records: 64 at a time, or what is left once no lane walks
+        const unsigned nq = __atomic_load_n(&g_lqn[wave], __ATOMIC_RELAXED);
+        if (nq >= 64u || (nq > 0u && (!__any(trav) || __popcll(__ballot(have && !trav)) >= p.lq_wait)))
+            lq_flush(s, r, tlim, nq);
+    }
+}
+
 __device__ __forceinline__ PhaseOut phase_a(const PcParams& p) {
     return PhaseOut{p.sqA, p.scapA, p.scntA, p.cq, p.ccapA, p.ccnt, p.kinline};
 }
@@ -986,15 +1204,25 @@ __global__ __launch_bounds__(kBlock, RT_MIX_WAVES) void k_mix(rtk::DevScene s, r
         if (p.bprio) __builtin_amdgcn_s_setprio(3);    // the deep chains are the frame's critical path
         chain_body<COUNT, true>(s, e, p, blockIdx.x, (unsigned)p.gb, phase_b(p));
     }
-    else if (!p.exp_skip_occ) occlude_body<COUNT>(s, p, blockIdx.x - p.gb, gridDim.x - p.gb, p.sflatA, p.totals[0], 0);
+    else if (!p.exp_skip_occ) {
+        if constexpr (!COUNT && RT_LEAF_QUEUE)
+            occlude_queue_body(s, p, blockIdx.x - p.gb, gridDim.x - p.gb, p.sflatA, p.totals[0]);
+        else
+            occlude_body<COUNT>(s, p, blockIdx.x - p.gb, gridDim.x - p.gb, p.sflatA, p.totals[0], 0);
+    }
 }
 
 // Phase B's shadow tasks (which = 1), or phase A's (which = 0: p.split_occ, frame batches).
 template <bool COUNT>
 __global__ __launch_bounds__(kBlock, RT_OCC_WAVES_PER_EU) void k_occlude(rtk::DevScene s, PcParams p, int which) {
     block_init(s);
-    if (which) occlude_body<COUNT>(s, p, blockIdx.x, gridDim.x, p.sflatB, p.totals[2], 1);
-    else occlude_body<COUNT>(s, p, blockIdx.x, gridDim.x, p.sflatA, p.totals[0], 0);
+    if constexpr (!COUNT && RT_LEAF_QUEUE) {
+        if (which) occlude_queue_body(s, p, blockIdx.x, gridDim.x, p.sflatB, p.totals[2]);
+        else occlude_queue_body(s, p, blockIdx.x, gridDim.x, p.sflatA, p.totals[0]);
+    } else {
+        if (which) occlude_body<COUNT>(s, p, blockIdx.x, gridDim.x, p.sflatB, p.totals[2], 1);
+        else occlude_body<COUNT>(s, p, blockIdx.x, gridDim.x, p.sflatA, p.totals[0], 0);
+    }
 }
 
 // ---------------------------------------------------------------------------

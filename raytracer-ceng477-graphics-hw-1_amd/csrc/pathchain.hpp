@@ -113,6 +113,7 @@ struct PcParams {
     int ochunk;       // ... and shadow tasks (k_mix occlusion role, k_occlude) in chunks of this many
     int packet;       // 1: eye rays of a wave walk as one packet when exact (packet_closest)
     int exp_skip_occ; // experiments only (RT_EXP_SKIP_OCC): k_mix's occlusion role does nothing (wrong images)
+    int lq_wait;      // leaf-queue walks: test the queued records once this many lanes wait on them (RT_LQ_WAIT)
     int grid;         // k_chain persistent grid (= number of shadow-queue regions)
     int ogrid;        // k_occlude persistent grid
     int split_occ;    // 1: A's shadow tasks in their own k_occlude launch (occ_grid workgroups), not in k_mix

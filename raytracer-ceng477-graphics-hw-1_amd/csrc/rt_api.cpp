@@ -788,6 +788,7 @@ int render_chain(rt_scene* s, const rtk::Eye& eye, const rtk::FrameParams& f, bo
     p.ochunk = s->tune_ochunk;
     p.packet = s->tune_packet && s->bvh.max_stack <= dl::kMaxStack;
     p.exp_skip_occ = std::getenv("RT_EXP_SKIP_OCC") ? 1 : 0;
+    p.lq_wait = std::getenv("RT_LQ_WAIT") ? std::max(1, std::min(64, std::atoi(std::getenv("RT_LQ_WAIT")))) : 32;
     p.spread = s->tune_spread;
     p.dyn_units = (int)P.dyn_units;
     p.ublk_h = s->tune_ublk_h;
