@@ -140,7 +140,7 @@ struct rt_scene {
                                 // default GPU_MAX_HW_QUEUES - 1)
     int tune_fgrid = 0;         // RT_FGRID: k_finish workgroups at most (0: 8 per CU; its waves are dispatch-bound
                                 // at a lane per pixel: 0.515 -> 0.49 ms per batched frame)
-    int tune_gb = 0;            // RT_GB: phase-B chain workgroups in k_mix (0: 1.5625 per CU for a lone frame, 0.5 for batches)
+    int tune_gb = 0;            // RT_GB: phase-B chain workgroups in k_mix (0: 1.875 per CU for a lone frame, 1 for batches)
     int tune_bq_cap = 1 << 30;  // RT_BQ_CAP: phase-B shadow queue slots (tests force the k_occlude spill path)
     int tune_bservice = 64;     // RT_BSERVICE: phase-B waves service finished walks once this many lanes are done
     int tune_btail = 64;        // RT_BTAIL: the same once the continuations are exhausted (1: 1.24, 4: 1.18, 16: 1.15, 64: 1.14 ms)
@@ -642,13 +642,15 @@ int render_chain(rt_scene* s, const rtk::Eye& eye, const rtk::FrameParams& f, bo
         // phase split: A walks levels [0, kinline], B the rest (k_mix chain role, gb workgroups)
         P.kinline = std::max(0, s->tune_kinline);
         P.phase_b = P.kinline < s->dev.max_depth;
-        // phase-B workgroups: a lone frame's deep chains are its critical path (1.5625 per CU best);
+        // phase-B workgroups: a lone frame's deep chains are its critical path (1.875 per CU best since
+        // round 3: C3 one frame, 61-frame medians, 1.5625 0.946-0.948, 1.72 0.940, 1.875 0.925-0.935,
+        // 2.03 0.956 ms);
         // in frame batches other frames hide them and the shadow role wants the CUs (C3: 0.5 per CU
         // 0.550 ms/frame, 0.75 0.552, 1 0.554, 1.25 0.557, 1.5625 0.568)
         // frame batches: A's shadow rays in their own 5-wave k_occlude launch (split_occ) and 1 phase-B
         // workgroup per CU (6 slots in flight: 0.504-0.512 -> 0.495 ms/frame; 0.5 per CU 0.500, 2 0.4995)
         P.split_occ = f.nframes > 1 && (!std::getenv("RT_SPLIT_OCC") || std::atoi(std::getenv("RT_SPLIT_OCC")));
-        const int gb_default = f.nframes > 1 ? (P.split_occ ? s->num_cus : s->num_cus / 2) : 25 * s->num_cus / 16;
+        const int gb_default = f.nframes > 1 ? (P.split_occ ? s->num_cus : s->num_cus / 2) : 30 * s->num_cus / 16;
         P.gb = P.phase_b ? std::max(1, std::min(s->mix_grid - 1, s->tune_gb > 0 ? s->tune_gb : gb_default)) : 0;
         P.levels_a = std::min(P.kinline, std::max(s->dev.max_depth, 0)) + 1;
         // dynamic phase-A units: a workgroup may take up to twice its static share (at most
