@@ -957,9 +957,11 @@ __device__ __forceinline__ void lq_flush(const rtk::DevScene& s, const Ray& r, f
     const int lane = lane_id(), wave = (int)(threadIdx.x >> 6);
     unsigned* const q = lq_base();
     const unsigned n = min(nq, 64u);
-    const bool valid = (unsigned)lane < n;
-    const unsigned e = valid ? q[lane] : 0u;
+    const unsigned e = (unsigned)lane < n ? q[lane] : 0u;
     const int src = (int)(e >> kLqSrcShift);
+    // a record of a ray already found occluded is retired untested
+    const bool valid = (unsigned)lane < n &&
+                       !((__atomic_load_n(&g_lhit[wave], __ATOMIC_RELAXED) >> src) & 1ull);
     // the owner lane's ray (every lane takes part in the shuffles)
     Ray o;
     o.o = V{__shfl(r.o.x, src, 64), __shfl(r.o.y, src, 64), __shfl(r.o.z, src, 64)};
@@ -983,8 +985,8 @@ __device__ __forceinline__ void lq_flush(const rtk::DevScene& s, const Ray& r, f
             });
         }
         if (hit) atomicOr(&g_lhit[wave], 1ull << src);
-        atomicSub(&lpend_base()[(wave << 6) + src], 1);
     }
+    if ((unsigned)lane < n) atomicSub(&lpend_base()[(wave << 6) + src], 1);
     if ((unsigned)lane < rest) q[lane] = mv;
     if (lane == 0) __atomic_store_n(&g_lqn[wave], rest, __ATOMIC_RELAXED);
 }
