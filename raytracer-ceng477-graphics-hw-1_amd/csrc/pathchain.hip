@@ -600,7 +600,7 @@ __device__ __forceinline__ unsigned unit_order(const PcParams& p, unsigned u, un
 
 // closest-hit chains of one phase (raytracer.cpp:385-439 minus the shading):
 // record each hit, queue its shadow tasks, follow (or hand on) mirrors.
-template <bool COUNT, bool CONT>
+template <bool COUNT, bool CONT, bool BQ = CONT>
 __device__ void chain_body(const rtk::DevScene& s, const rtk::Eye& e, const PcParams& p, unsigned blk, unsigned G,
                            const PhaseOut& o) {
     WalkStack stk;
@@ -645,7 +645,7 @@ __device__ void chain_body(const rtk::DevScene& s, const rtk::Eye& e, const PcPa
             // one shadow task per light (:399-404) whose ray can change the pixel (light_needed; the
             // counting passes trace every one, as the reference does); light-major within the wave
             const unsigned own0 = (unsigned)(lvp * nl);
-            if (CONT && kBq > 0 && __ballot(hit))
+            if (CONT && BQ && kBq > 0 && __ballot(hit))
                 __builtin_amdgcn_s_waitcnt(0);     // phase B: the record stores have completed before the
                                                    // owner ids are published to the workgroup (a workgroup
                                                    // fence alone does not wait for them on gfx950)
@@ -662,7 +662,7 @@ __device__ void chain_body(const rtk::DevScene& s, const rtk::Eye& e, const PcPa
                 if (!m) continue;
                 const unsigned cnt = (unsigned)__popcll(m), rank = lane_rank(m);
                 bool queued = false;
-                if (CONT && kBq > 0) {
+                if (CONT && BQ && kBq > 0) {
                     // phase B: into the workgroup queue (walked by its finished waves)
                     const int leader = __ffsll((unsigned long long)m) - 1;
                     unsigned base = 0;
@@ -814,7 +814,7 @@ __device__ void chain_body(const rtk::DevScene& s, const rtk::Eye& e, const PcPa
         wave_add_counter(&p.counters[CONT ? kCntBHits : kCntAHits], nhit);
         if (!CONT) wave_add_counter(&p.counters[kCntConts], ncont);
     }
-    if (CONT && kBq > 0) {
+    if (CONT && BQ && kBq > 0) {
         if (lane_id() == 0) atomicSub(&g_bq_prod, 1u);      // this wave produces no more shadow tasks
         Work wq;                                            // the queue's walks, counted apart (kCntBQ*)
         nshadow = bq_consume<COUNT>(s, p, stk, wq);
@@ -1193,18 +1193,25 @@ __global__ __launch_bounds__(kBlock) void k_pack_b(PcParams p) {
 }
 
 // Workgroups [0, gb): phase B chains (continuations); the rest: phase A's shadow tasks.
+// BQ: phase B's shadow tasks go to the workgroup LDS queue first (a lone frame: its waves whose
+// chains are done walk them during the deep-chain tail); without it (frame batches) they all go to
+// k_pack_b + k_occlude, and the kernel needs 26.7 instead of 32.8 KB of LDS and 96 VGPRs: 5 waves.
 #ifndef RT_MIX_WAVES
 #define RT_MIX_WAVES 4           // 4 waves/SIMD: no VGPR spills (5: 29 spilled); single frame 1.17-1.19 vs 1.22-1.24 ms
 #endif
-template <bool COUNT>
-__global__ __launch_bounds__(kBlock, RT_MIX_WAVES) void k_mix(rtk::DevScene s, rtk::Eye e, PcParams p) {
+#ifndef RT_MIX_NOBQ_WAVES
+#define RT_MIX_NOBQ_WAVES 5      // without the LDS queue: 96 VGPRs, no spills
+#endif
+template <bool COUNT, bool BQ>
+__global__ __launch_bounds__(kBlock, BQ || COUNT ? RT_MIX_WAVES : RT_MIX_NOBQ_WAVES) void k_mix(rtk::DevScene s,
+                                                                                                  rtk::Eye e, PcParams p) {
     const bool chain = blockIdx.x < (unsigned)p.gb;
     if (threadIdx.x == 0) g_ccnt = 0;
-    if (chain && kBq > 0) bq_init();
+    if (BQ && chain && kBq > 0) bq_init();
     block_init(s);
     if (chain) {
         if (p.bprio) __builtin_amdgcn_s_setprio(3);    // the deep chains are the frame's critical path
-        chain_body<COUNT, true>(s, e, p, blockIdx.x, (unsigned)p.gb, phase_b(p));
+        chain_body<COUNT, true, BQ>(s, e, p, blockIdx.x, (unsigned)p.gb, phase_b(p));
     }
     else if (!p.exp_skip_occ) {
         if constexpr (!COUNT && RT_LEAF_QUEUE)
@@ -1890,7 +1897,7 @@ void launch_finish(const rtk::DevScene& s, const PcParams& p, hipStream_t st) {
 
 hipError_t chain_occupancy(int* chain_blocks_per_cu, int* mix_blocks_per_cu, int* occlude_blocks_per_cu) {
     hipError_t e = hipOccupancyMaxActiveBlocksPerMultiprocessor(chain_blocks_per_cu, k_chain<false>, kBlock, 0);
-    if (e == hipSuccess) e = hipOccupancyMaxActiveBlocksPerMultiprocessor(mix_blocks_per_cu, k_mix<false>, kBlock, 0);
+    if (e == hipSuccess) e = hipOccupancyMaxActiveBlocksPerMultiprocessor(mix_blocks_per_cu, k_mix<false, true>, kBlock, 0);
     if (e == hipSuccess)
         e = hipOccupancyMaxActiveBlocksPerMultiprocessor(occlude_blocks_per_cu, k_occlude<false>, kBlock, 0);
     return e;
@@ -1987,8 +1994,14 @@ hipError_t launch_chain_chunk(const rtk::DevScene& s, const rtk::Eye& e, const P
     const bool split = p.split_occ && phase_b;
     const int mgrid = split ? q.gb : q.gb + p.ogrid;
     mark(kKMix);
-    if (count) hipLaunchKernelGGL(k_mix<true>, dim3(mgrid), blk, 0, st, s, e, q);
-    else hipLaunchKernelGGL(k_mix<false>, dim3(mgrid), blk, 0, st, s, e, q);
+    // frame batches (split): phase B's shadow tasks all through k_pack_b + k_occlude (no LDS queue)
+    if (count) {
+        if (split) hipLaunchKernelGGL((k_mix<true, false>), dim3(mgrid), blk, 0, st, s, e, q);
+        else hipLaunchKernelGGL((k_mix<true, true>), dim3(mgrid), blk, 0, st, s, e, q);
+    } else {
+        if (split) hipLaunchKernelGGL((k_mix<false, false>), dim3(mgrid), blk, 0, st, s, e, q);
+        else hipLaunchKernelGGL((k_mix<false, true>), dim3(mgrid), blk, 0, st, s, e, q);
+    }
     if (split) {
         mark(kKOccA);
         if (count) hipLaunchKernelGGL(k_occlude<true>, dim3(p.occ_grid), blk, 0, st, s, p, 0);
