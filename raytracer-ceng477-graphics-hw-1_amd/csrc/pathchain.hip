@@ -354,6 +354,37 @@ __device__ __forceinline__ unsigned chunk_task(unsigned v, unsigned G, unsigned 
     return (blk + (v / ch) * G) * ch + v % ch;
 }
 
+// Unsigned division by a wave-uniform divisor d > 0 with its reciprocal kept in a scalar register
+// (the compiler's own 32-bit expansion: an f32 reciprocal scaled to 2^32, one Newton step, the
+// quotient from a high multiply and two corrections -- exact for every 32-bit v).  The compiler
+// leaves that reciprocal in a VGPR, which the leaf-queue walker then spills.
+struct UDiv {
+    unsigned d, rcp;
+    __device__ __forceinline__ explicit UDiv(unsigned d_) : d(d_) {
+        unsigned r = (unsigned)(__builtin_amdgcn_rcpf((float)d_) * 4294966784.0f);   // 0x4f7ffffe
+        r += __umulhi(r, (0u - d_) * r);
+        rcp = __builtin_amdgcn_readfirstlane(r);
+    }
+    __device__ __forceinline__ unsigned div(unsigned v) const {
+        unsigned q = __umulhi(v, rcp), rem = v - q * d;
+        if (rem >= d) { ++q; rem -= d; }
+        if (rem >= d) ++q;
+        return q;
+    }
+};
+__device__ __forceinline__ unsigned chunk_task(unsigned v, unsigned G, unsigned blk, const UDiv& ch) {
+    const unsigned q = ch.div(v);
+    return (blk + q * G) * ch.d + (v - q * ch.d);
+}
+__device__ __forceinline__ Ray shadow_from_record(const rtk::DevScene& s, const PcParams& p, unsigned owner,
+                                                  float* tlim, const UDiv& nl) {
+    const unsigned lvp = nl.div(owner);
+    const int l = (int)(owner - lvp * nl.d);
+    const float4 a = p.rec[(size_t)lvp * kRecWords];
+    const V hitp{a.x, a.y, a.z};
+    return shadow_ray(s, hitp, surface_normal(s, hitp, __float_as_int(a.w)), l, tlim);
+}
+
 // ---------------------------------------------------------------------------
 // Packet closest-hit walk: the wave walks ONE shared DFS; every node and
 // leaf fetch is wave-uniform (scalar loads), each lane keeps its own tMax and
@@ -996,6 +1027,7 @@ __device__ void occlude_queue_body(const rtk::DevScene& s, const PcParams& p, un
                                    const unsigned* tasks, unsigned total) {
     const int lane = lane_id(), wave = (int)(threadIdx.x >> 6);
     const unsigned n = chunk_count(total, G, blk, (unsigned)p.ochunk);
+    const UDiv och((unsigned)p.ochunk), nld((unsigned)s.nlights);
     // the queue count, the hit mask and the queued counts are written by other lanes of the wave:
     // every read is an atomic load (no value kept in a register across the loop)
     if (lane == 0) {
@@ -1037,8 +1069,8 @@ __device__ void occlude_queue_body(const rtk::DevScene& s, const PcParams& p, un
                 if (!have) {
                     const unsigned idx = base + lane_rank(idle);
                     if (idx < n) {
-                        owner = tasks[chunk_task(idx, G, blk, (unsigned)p.ochunk)];
-                        r = shadow_from_record(s, p, owner, &tlim);
+                        owner = tasks[chunk_task(idx, G, blk, och)];
+                        r = shadow_from_record(s, p, owner, &tlim, nld);
                         if (defer_any(s, r)) {
                             fb_shadow(p, owner);
                         } else if (s.nnodes <= 0) {   // nothing to hit (walk_begin)

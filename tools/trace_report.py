@@ -85,15 +85,11 @@ def main():
             r = summarise(path + "/k_chain", smp[0::2], smp[1::2])
             ob = tr[2 * cap:2 * (cap + og)]
             okb = ob[1::2] != 0
-            if not okb.any():
-                res.append(r)
-                sc.close()
-                del os.environ["RT_TRACE"]
-                continue
             t0 = smp[0::2][smp[1::2] != 0].min()
-            os_, oe = rel(ob[0::2][okb], t0), rel(ob[1::2][okb], t0)
-            r["k_occlude_blocks"] = {"start_min": round(float(os_.min()), 1), "start_max": round(float(os_.max()), 1),
-                                     "end_pct_us": {p: round(float(np.percentile(oe, p)), 1) for p in (0, 50, 90, 99, 100)}}
+            if okb.any():      # k_occlude block spans (the leaf-queue walker does not record them)
+                os_, oe = rel(ob[0::2][okb], t0), rel(ob[1::2][okb], t0)
+                r["k_occlude_blocks"] = {"start_min": round(float(os_.min()), 1), "start_max": round(float(os_.max()), 1),
+                                         "end_pct_us": {p: round(float(np.percentile(oe, p)), 1) for p in (0, 50, 90, 99, 100)}}
             pb = tr[2 * (cap + og):2 * (cap + og) + 4 * cap].reshape(-1, 4)
             okp = pb[:, 1] != 0
             if okp.any():        # phase-B continuations (k_mix chain role): grab, end, last level, walk steps
@@ -103,6 +99,18 @@ def main():
                 lv, stp = (pb[okp, 2] & 255).astype(np.int64), pb[okp, 3].astype(np.int64)
                 wit = (pb[okp, 2] >> 8).astype(np.int64)      # the wave's walk iterations meanwhile
                 top = np.argsort(bd)[::-1][:8]
+                # each continuation's phase-A end (same path index): when a streaming A->B hand-off
+                # could have started it, and the frame end that would give at the same chain times
+                a_end = rel(smp[1::2][q], t0)
+                a_end = np.where(smp[1::2][q] != 0, a_end, 0.0)
+                last_b = np.argsort(be)[::-1][:8]
+                r["stream_whatif"] = {
+                    "end_if_started_at_a_end_us": round(float((a_end + bd).max()), 1),
+                    "end_pct_if_started_at_a_end_us": {p: round(float(np.percentile(a_end + bd, p)), 1)
+                                                       for p in (50, 99, 99.9, 100)},
+                    "last_to_finish": [{"q": int(q[j]), "a_end": round(float(a_end[j]), 1),
+                                        "b_start": round(float(bs[j]), 1), "b_dur": round(float(bd[j]), 1),
+                                        "level": int(lv[j])} for j in last_b]}
                 r["phase_b"] = {
                     "chains": int(okp.sum()),
                     "start_pct_us": {p: round(float(np.percentile(bs, p)), 1) for p in (0, 50, 100)},
