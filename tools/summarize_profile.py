@@ -30,7 +30,7 @@ prof.mkdir(exist_ok=True)
 
 def kname(s):
     """k_name, with '<true>' kept for counting-pass instantiations."""
-    m = re.search(r"(k_[a-z_0-9]+)(<(true|false)>)?", s)
+    m = re.search(r"(k_[a-z_0-9]+)(<(true|false)[,>])?", s)      # the first template argument: COUNT
     if not m:
         return s[:40]
     return m.group(1) + ("<true>" if m.group(3) == "true" else "")
