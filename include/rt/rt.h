@@ -33,7 +33,7 @@
 extern "C" {
 #endif
 
-#define RT_ABI_VERSION 8
+#define RT_ABI_VERSION 9
 
 typedef enum rt_status {
     RT_OK = 0,
@@ -244,6 +244,11 @@ int rt_phong_pow(const float* base, const float* exponent, float* out, int n);
  * shared reciprocal, the correctly rounded float quotients (host arrays,
  * synchronous; ABI 8). */
 int rt_cramer_div(const float* den, const float* num, float* out, int n);
+/* Diagnostics: q[j*nv + i] = v[i] / d[j] (unsigned 32-bit, d[j] > 0) as the
+ * shadow walkers' task dealing divides by a wave-uniform divisor (pathchain.hip
+ * UDiv: a scalar-register reciprocal, a high multiply and two corrections;
+ * host arrays, synchronous; ABI 9). */
+int rt_udiv(const uint32_t* v, int nv, const uint32_t* d, int nd, uint32_t* q);
 /* HBM held by a scene on its (first) device (ABI 7): the uploaded scene (trees,
  * primitives, tables) and the render workspaces allocated so far (chain-path
  * arenas of every slot, output staging).  The workspaces grow on demand up to

@@ -165,6 +165,7 @@ _SIGS = [
     ("rt_walk_timing", ctypes.c_int, [_P, _P, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int, _P]),
     ("rt_phong_pow", ctypes.c_int, [_P, _P, _P, ctypes.c_int]),
     ("rt_cramer_div", ctypes.c_int, [_P, _P, _P, ctypes.c_int]),
+    ("rt_udiv", ctypes.c_int, [_P, ctypes.c_int, _P, ctypes.c_int, _P]),
     ("rt_measure_peaks", ctypes.c_int, [ctypes.c_int, ctypes.c_uint64, _P]),
     ("rt_scene_memory", ctypes.c_int, [_P, ctypes.POINTER(ctypes.c_uint64), ctypes.POINTER(ctypes.c_uint64)]),
     ("rt_slab_rows", ctypes.c_int, [ctypes.c_int, ctypes.c_int, ctypes.c_int]),
@@ -240,6 +241,17 @@ def cramer_div(den, num) -> np.ndarray:
     _check(lib().rt_cramer_div(d.ctypes.data_as(ctypes.c_void_p), nm.ctypes.data_as(ctypes.c_void_p),
                                out.ctypes.data_as(ctypes.c_void_p), d.size))
     return out
+
+
+def udiv(v, d) -> np.ndarray:
+    """Diagnostics (rt_udiv): v[i] // d[j] as the shadow walkers divide by a wave-uniform divisor
+    (pathchain.hip UDiv); returns shape (len(d), len(v)), uint32."""
+    vv = np.ascontiguousarray(v, dtype=np.uint32).reshape(-1)
+    dd = np.ascontiguousarray(d, dtype=np.uint32).reshape(-1)
+    q = np.empty((dd.size, vv.size), dtype=np.uint32)
+    _check(lib().rt_udiv(vv.ctypes.data_as(ctypes.c_void_p), vv.size, dd.ctypes.data_as(ctypes.c_void_p), dd.size,
+                         q.ctypes.data_as(ctypes.c_void_p)))
+    return q
 
 
 class Peaks(ctypes.Structure):

@@ -1986,6 +1986,18 @@ hipError_t launch_cramer_div(const float* den, const float* num, float* out, int
     return hipGetLastError();
 }
 
+// Diagnostics (rt_udiv): the walkers' uniform-divisor division (UDiv), one divisor per workgroup
+// (it must be wave-uniform): q[j * nv + i] = v[i] / d[j].
+__global__ __launch_bounds__(kBlock) void k_udiv(const unsigned* v, int nv, const unsigned* d, unsigned* q) {
+    const UDiv u(d[blockIdx.x]);
+    for (int i = threadIdx.x; i < nv; i += kBlock) q[(size_t)blockIdx.x * nv + i] = u.div(v[i]);
+}
+
+hipError_t launch_udiv(const unsigned* v, int nv, const unsigned* d, int nd, unsigned* q, hipStream_t st) {
+    hipLaunchKernelGGL(k_udiv, dim3(nd), dim3(kBlock), 0, st, v, nv, d, q);
+    return hipGetLastError();
+}
+
 // Diagnostics (RT_STEP_STATS builds): read (and optionally clear) g_step_stat.
 extern "C" int rt_debug_step_stats(unsigned long long* out, int reset) {
     if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_step_stat), sizeof(g_step_stat)) != hipSuccess) return -1;

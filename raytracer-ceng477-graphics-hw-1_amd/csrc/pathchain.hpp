@@ -174,6 +174,8 @@ hipError_t launch_fused_chunk(const rtk::DevScene& s, const rtk::Eye& e, const P
 hipError_t launch_phong_pow(const float* base, const float* expo, float* out, int n, hipStream_t st);
 // Diagnostics: the triangle test's Cramer quotients on the device (rt_cramer_div).
 hipError_t launch_cramer_div(const float* den, const float* num, float* out, int n, hipStream_t st);
+// Diagnostics: the leaf-queue walker's uniform-divisor division on the device (rt_udiv).
+hipError_t launch_udiv(const unsigned* v, int nv, const unsigned* d, int nd, unsigned* q, hipStream_t st);
 // Diagnostics: dependent-step latency of single closest-hit walks (rt_walk_timing).
 hipError_t launch_walk_timing(const rtk::DevScene& s, const float* rays, int n, int lanes, int reps, int mode,
                               unsigned long long* out, hipStream_t st);

@@ -1356,6 +1356,23 @@ int rt_cramer_div(const float* den, const float* num, float* out, int n) {
     return RT_OK;
 }
 
+int rt_udiv(const uint32_t* v, int nv, const uint32_t* d, int nd, uint32_t* q) {
+    if (!v || !d || !q || nv < 0 || nd < 0) return fail(RT_ERR_ARG, "bad udiv arguments");
+    for (int j = 0; j < nd; ++j)
+        if (d[j] == 0) return fail(RT_ERR_ARG, "udiv: divisor 0");
+    if (nv == 0 || nd == 0) return RT_OK;
+    unsigned* b = nullptr;
+    const size_t nq = (size_t)nv * nd;
+    HIP_TRY(hipMalloc(reinterpret_cast<void**>(&b), ((size_t)nv + nd + nq) * sizeof(unsigned)));
+    hipError_t e = hipMemcpy(b, v, (size_t)nv * sizeof(unsigned), hipMemcpyHostToDevice);
+    if (e == hipSuccess) e = hipMemcpy(b + nv, d, (size_t)nd * sizeof(unsigned), hipMemcpyHostToDevice);
+    if (e == hipSuccess) e = rtc::launch_udiv(b, nv, b + nv, nd, b + nv + nd, nullptr);
+    if (e == hipSuccess) e = hipMemcpy(q, b + nv + nd, nq * sizeof(unsigned), hipMemcpyDeviceToHost);
+    (void)hipFree(b);
+    if (e != hipSuccess) return fail(RT_ERR_HIP, std::string("udiv: ") + hipGetErrorName(e));
+    return RT_OK;
+}
+
 int rt_unshuffle_stripes(const void* slabs, void* image, int width, int height, int stripe_rows, int nranks,
                          void* stream) {
     if (!slabs || !image || width < 1 || height < 1 || stripe_rows < 1 || nranks < 1)
