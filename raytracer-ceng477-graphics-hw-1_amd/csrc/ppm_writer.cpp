@@ -1,10 +1,15 @@
 // rt_write_ppm: byte-identical to the reference's write_ppm (ppm.cpp:4-39):
 //   "P3\n%d %d\n255\n", then per row the 3*W values as "%d" separated by one
 //   space, no space after the last value of a row, then "\n".
-// Instead of 3*W*H fprintf calls (0.33 s at 1080p in the reference) each row
-// is formatted into a buffer from a 256-entry digit table and written with
-// one fwrite per chunk.
+// Instead of 3*W*H fprintf calls (0.33 s at 1080p in the reference) every value
+// is one 4-byte copy from a 256-entry table (the digits, a space, padding) and a
+// length step, a row's last space becomes its "\n", and blocks of rows (~4 MB of
+// text) go out with one fwrite each.  Formatting runs at
+// ~5 GB/s of text on one core, faster than the page cache takes the file, so it
+// stays single-threaded (threads measured slower: 1080p 4 -> 10 ms, 8K 60 -> 68).
+#include <algorithm>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <string>
 #include <vector>
@@ -15,16 +20,41 @@
 namespace {
 
 struct DigitTable {
-    char text[256][4];
-    unsigned char len[256];
+    char text[256][4];      // the decimal digits of v, then ' ', zero padded to 4 bytes
+    unsigned char len[256]; // digits + 1
     DigitTable() {
-        for (int v = 0; v < 256; ++v) len[v] = (unsigned char)std::snprintf(text[v], sizeof text[v], "%d", v);
+        for (int v = 0; v < 256; ++v) {
+            char t[8];
+            const int n = std::snprintf(t, sizeof t, "%d", v);
+            std::memset(text[v], 0, 4);
+            std::memcpy(text[v], t, (size_t)n);
+            text[v][n] = ' ';
+            len[v] = (unsigned char)(n + 1);
+        }
     }
 };
 
 const DigitTable& digits() {
     static const DigitTable t;
     return t;
+}
+
+// Rows [y0, y1) of the image as text into out (resized to fit); returns the byte count.
+size_t format_rows(const uint8_t* rgb, size_t vals, int y0, int y1, std::vector<char>& out) {
+    const DigitTable& d = digits();
+    out.resize((size_t)(y1 - y0) * (vals * 4 + 1) + 4);
+    char* p = out.data();
+    for (int y = y0; y < y1; ++y) {
+        const uint8_t* row = rgb + (size_t)y * vals;
+        for (size_t i = 0; i < vals; ++i) {
+            const uint8_t v = row[i];
+            std::memcpy(p, d.text[v], 4);     // the buffer has 4 bytes of slack past every value
+            p += d.len[v];
+        }
+        if (vals > 0) p[-1] = '\n';          // the last value's space -> the row's newline
+        else *p++ = '\n';                    // an empty row (width 0): the reference's lone "\n"
+    }
+    return (size_t)(p - out.data());
 }
 
 }  // namespace
@@ -34,23 +64,18 @@ extern "C" int rt_write_ppm(const char* path, const uint8_t* rgb, int width, int
     FILE* f = std::fopen(path, "w");
     if (!f) return rt_internal_set_error(RT_ERR_IO, "Error: The ppm file cannot be opened for writing.");  // ppm.cpp:10
     std::fprintf(f, "P3\n%d %d\n255\n", width, height);
-    const DigitTable& d = digits();
-    std::vector<char> buf;
-    buf.reserve((size_t)width * 12 + 2);
     const size_t vals = (size_t)width * 3;
-    for (int y = 0; y < height; ++y) {
-        buf.clear();
-        const uint8_t* row = rgb + (size_t)y * vals;
-        for (size_t i = 0; i < vals; ++i) {
-            const uint8_t v = row[i];
-            buf.insert(buf.end(), d.text[v], d.text[v] + d.len[v]);
-            if (i + 1 < vals) buf.push_back(' ');
-        }
-        buf.push_back('\n');
-        if (std::fwrite(buf.data(), 1, buf.size(), f) != buf.size()) {
-            std::fclose(f);
-            return rt_internal_set_error(RT_ERR_IO, "short write");
-        }
+    const size_t row_max = vals * 4 + 1;
+    const int block = (int)std::max<size_t>(1, (4u << 20) / row_max);   // rows per ~4 MB of text
+    std::vector<char> buf;
+    bool ok = true;
+    for (int y = 0; y < height && ok; y += block) {
+        const size_t n = format_rows(rgb, vals, y, std::min(height, y + block), buf);
+        ok = std::fwrite(buf.data(), 1, n, f) == n;
+    }
+    if (!ok) {
+        std::fclose(f);
+        return rt_internal_set_error(RT_ERR_IO, "short write");
     }
     if (std::fclose(f) != 0) return rt_internal_set_error(RT_ERR_IO, "close failed");
     return RT_OK;

@@ -148,7 +148,7 @@ def test_write_ppm_byte_identical(name, pkg, oracle, goldens, tmp_path):
 
 def test_write_ppm_edge_shapes(pkg, oracle, tmp_path):
     rng = np.random.default_rng(0)
-    for h, w in [(1, 1), (3, 1), (1, 5), (7, 13)]:
+    for h, w in [(1, 1), (3, 1), (1, 5), (7, 13), (2, 0), (0, 3), (5, 700)]:
         img = rng.integers(0, 256, size=(h, w, 3), dtype=np.uint8)
         pkg.write_ppm(tmp_path / "a.ppm", img)
         oracle.write_ppm(tmp_path / "b.ppm", img)
