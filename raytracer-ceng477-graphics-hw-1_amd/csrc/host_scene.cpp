@@ -4,6 +4,7 @@
 #include <cfloat>
 #include <algorithm>
 #include <chrono>
+#include <new>
 #include <functional>
 #include <future>
 #include <thread>
@@ -928,8 +929,12 @@ void build_shadow_tree(FlatBVH& out, int threads) {
         for (int a = 0; a < 3; ++a) {
             const double ext = (double)cb.hi[a] - cb.lo[a];
             if (!(ext > 0)) continue;
-            Box bb[kMaxBins];
-            int cnt[kMaxBins] = {0};
+            // only the kBins bins in use are initialised (most nodes are small: 32 default-constructed
+            // boxes per axis were most of the build's time)
+            alignas(Box) unsigned char bb_raw[kMaxBins * sizeof(Box)];
+            Box* const bb = reinterpret_cast<Box*>(bb_raw);
+            int cnt[kMaxBins];
+            for (int k = 0; k < kBins; ++k) { new (&bb[k]) Box(); cnt[k] = 0; }
             for (int i = b; i < e; ++i) {
                 const Leaf& l = leaves[idx[i]];
                 int k = (int)((l.c[a] - cb.lo[a]) / ext * kBins);
