@@ -828,14 +828,25 @@ std::string build_bvh(const HostScene& s, FlatBVH& out, int threads) {
     out.root_info = info_of(0);
     out.root_lrec = lrec_of[0];
     if (!lrec_ok) out.lrec.clear();                  // no 4-wide trees: the binary trees only
+    // The occlusion tree (its own task when threads allow) and the reference-order wide tree are
+    // independent: both read the pairs and leaf records, each writes only its own fields.
+    const auto t1 = std::chrono::steady_clock::now();
+    double stree_ms = 0.0;
+    auto shadow = [&out, &stree_ms] {
+        const auto ts = std::chrono::steady_clock::now();
+        build_shadow_tree(out, out.threads);
+        stree_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - ts).count();
+    };
+    std::future<void> fs;
+    if (out.threads > 1 && out.pairs.size() >= 4096) fs = std::async(std::launch::async, shadow);   // large scenes
     if (!build_ref_wide(out) || out.lrec.empty()) out.wnodes.clear();
+    out.flat_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count() - out.ref_ms;
+    if (fs.valid()) fs.get(); else shadow();
+    out.stree_ms = stree_ms;
+    (void)t1;
     // Ordered DFS pushes two children per interior pop: stack <= depth + 2.
     out.max_stack = out.max_depth + 2;
     if (out.max_stack > dl::kMaxStack) return "Error: BVH deeper than the device stack";
-    const auto t1 = std::chrono::steady_clock::now();
-    out.flat_ms = std::chrono::duration<double, std::milli>(t1 - t0).count() - out.ref_ms;
-    build_shadow_tree(out, out.threads);
-    out.stree_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t1).count();
     if (out.smax_depth + 2 > dl::kMaxStack) return "Error: occlusion tree deeper than the device stack";
     out.build_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
     return "";
