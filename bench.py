@@ -35,6 +35,7 @@ from __future__ import annotations
 import argparse
 import json
 import os
+import re
 import subprocess
 import sys
 import tempfile
@@ -106,7 +107,12 @@ CONFIGS = {
     "C3": ("C3_hm_1080p_d6", "horse_and_mug.xml 1920x1080, MaxRecursionDepth 6, full BVH + mirror recursion"),
     "C2": ("C2_cornellbox_800_d0", "cornellbox.xml camera 2 800x800, primary+shadow only (depth 0)"),
     "C5": ("C5_hm_8k_d6", "horse_and_mug.xml 7680x4320, depth 6, 16x SSAA (factor 4)"),
+    # mirror-heavy reference scenes, verbatim (inputs/, 1024x1024, MaxRecursionDepth 6): deep mirror chains
+    # between spheres, where phase B's record space (cb) and k_fallback matter
+    "MS": ("mirror_spheres.xml", "mirror_spheres.xml verbatim 1024x1024, depth 6 (all-mirror spheres)"),
+    "MB": ("marbles.xml", "marbles.xml verbatim 1024x1024, depth 6 (mirror marbles, 2 lights)"),
 }
+HBM_GUIDE_GBPS = 6290.0    # MI355X_MICROARCH.md: measured float4 copy (79 % of spec), beside our own measurement
 
 
 def parse():
@@ -283,6 +289,7 @@ def main() -> int:
     pcnt = pscene.counters_read()
     roles = pscene.counters_raw()
     pscene.close()
+    scene.counters_reset(sp)      # from here on the slots count the timed kernels' fallback work (kCntFb*)
     if any(pcnt[k] != cnt[k] for k in ("primary_rays", "shadow_rays", "reflection_rays")):
         raise RuntimeError(f"production counting pass disagrees on ray counts: {pcnt} vs {cnt}")
     if traversal_bytes(roles) != pcnt["node_visits"]:
@@ -348,6 +355,14 @@ def main() -> int:
     elapsed = time.perf_counter() - t0
     note(f"timed {a.steps} steps")
     kern_ms = sum(e0.elapsed_time(e1) for e0, e1 in evs) / a.steps      # render time per frame (batch-amortised)
+    # what the timed kernels left to k_fallback, per frame (warmup + timed frames since the reset)
+    fbr = scene.counters_raw()
+    fb_frames = max(a.warmup, F) + a.steps
+    fallback = {k[3:]: round(fbr[k] / fb_frames, 2) for k in scene.FALLBACK_SLOTS if k != "fb_launches"}
+    fallback["launches_per_frame"] = round(fbr["fb_launches"] / fb_frames, 4)
+    fallback["note"] = ("per frame, timed kernels: continuations A->B, those beyond the phase-B record space "
+                        "(walked whole by k_fallback), deferred closest-hit / shadow rays (outside the wide "
+                        "trees' slab-test range), fallback shadow-queue overflows")
 
     # N>1: the assembled frames equal one GPU's whole-frame render (checked after timing, rank 0)
     frames_ok = None
@@ -421,13 +436,17 @@ def main() -> int:
             ktimes[mode]["launches_per_frame"] = round(launches / frames, 4)
         kscene.close()
 
+    # HBM bytes per frame from the committed rocprofv3 FETCH/WRITE passes of the SAME mode as the time they
+    # are priced against: frame batches (one workspace slot) for `value`, one frame alone for --inflight 1
     traffic, traffic_src = None, None
-    tfile = ROOT / "profiles" / "traffic.json"
-    if tfile.exists():       # HBM bytes per frame from the committed rocprofv3 FETCH/WRITE passes
+    mode = "batched" if F > 1 else "one_frame"
+    tfile = ROOT / "profiles" / f"traffic_{mode}.json"
+    if tfile.exists():
         t = json.loads(tfile.read_text())
         if t.get("config") == config and t.get("path") == a.path and t.get("hbm_bytes_per_frame"):
             traffic = int(t["hbm_bytes_per_frame"] / world)
-            traffic_src = f"profiles/{t.get('tag')}_traffic.json (rocprofv3 2*FETCH_SIZE+WRITE_SIZE, N=1 frame / N)"
+            traffic_src = (f"profiles/{t.get('tag')}_traffic.json ({mode}; rocprofv3 2*FETCH_SIZE+WRITE_SIZE, "
+                           f"N=1 frame / N)")
     if rank == 0:
         ms = elapsed / a.steps * 1e3
         value = ps_frame * a.steps / elapsed / 1e6
@@ -457,7 +476,7 @@ def main() -> int:
             "ms_per_step": round(ms, 4), "higher_is_better": True, "scaling": "strong",
             "vs_baseline": None, "dtype": "f32", "data": "synthetic (reference scene file, derived per SURVEY §8d)",
             "config": {"workload": config, "description": desc, "width": W, "height": H, "aa": aa,
-                       "max_recursion_depth": 6 if config != "C2_cornellbox_800_d0" else 0,
+                       "max_recursion_depth": int(re.search(r"<MaxRecursionDepth>\s*(-?\d+)", Path(xml).read_text()).group(1)),
                        "parallelism": f"stripes{S}x{world}" + ("+rccl_gather" if world > 1 else ""),
                        "frames_in_flight": F, "frame_latency_ms": round(lat_ms, 4) if lat else None,
                        "workspace_slots": int(os.environ.get("RT_SLOTS", max(1, min(6, int(os.environ["GPU_MAX_HW_QUEUES"]) - 1)))),
@@ -488,6 +507,7 @@ def main() -> int:
                               "definition": "one frame alone on the GPU (rt_render_device), device time"}
                              if lat else None),
             "hbm_footprint": footprint,
+            "fallback": fallback,
             "kernel_ms_one_slot": ktimes,
             "drop_in": ({"ms_per_frame": round(host_ms, 4), "mray_s": round(ps_frame / host_ms / 1e3, 3),
                          "definition": "SURVEY §8(d): rt_render wall time, camera upload to the uint8 frame in "
@@ -508,10 +528,13 @@ def main() -> int:
                          "alg_bytes_split": {"traversal": int(trav_bytes), "workspace": int(ws_bytes)},
                          "per_kernel": per_kernel,
                          "dominant": dominant,
+                         "alg_bytes_per_kernel": {k: int(v) for k, v in kbytes.items()},
                          "hbm": {"bytes_per_frame": traffic, "gbps": round(traffic_gbps, 2) if traffic else None,
-                                 "peak": round(peaks["hbm_copy_gbps"], 1), "spec": HBM_SPEC_GBPS,
+                                 "peak": round(peaks["hbm_copy_gbps"], 1), "peak_guide": HBM_GUIDE_GBPS,
+                                 "spec": HBM_SPEC_GBPS,
                                  "frac": round(traffic_gbps / peaks["hbm_copy_gbps"], 4) if traffic else None,
-                                 "source": traffic_src},
+                                 "frac_of_guide": round(traffic_gbps / HBM_GUIDE_GBPS, 4) if traffic else None,
+                                 "mode": mode, "source": traffic_src},
                          "reference_model": {"bytes_per_frame": int(ref_alg_bytes),
                                              "note": "SURVEY §8(d) per-operation model of the reference's own walk "
                                                      "(32 B/node visit, 36 B/triangle test, 16 B/sphere test, 3 B/px)",

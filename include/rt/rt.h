@@ -286,7 +286,10 @@ int rt_counters_read(rt_scene* scene, rt_stats* stats);   /* synchronises the de
  * CounterSlot): phase-A / phase-B closest-hit walk bytes (or node visits), walks
  * and hits, continuations, and the shadow rays of A, of B's workgroup queue and
  * of B's overflow -- bytes and rays each.  Bytes when the scene was created with
- * RT_COUNT_PROD=1 (the production walks' fetched bytes). */
+ * RT_COUNT_PROD=1 (the production walks' fetched bytes).  24..29 (every launch,
+ * timed or counting; round 4): chain launches, continuations, continuations
+ * beyond the phase-B record space (walked by k_fallback), deferred closest-hit
+ * rays, deferred shadow rays, launches whose fallback shadow queue overflowed. */
 int rt_counters_read_raw(rt_scene* scene, uint64_t* out, int n);
 /* Diagnostics (ABI 7): per-kernel device time of the chain path's launches
  * since the last reset, for a scene created with env RT_KTIME=1 (events between

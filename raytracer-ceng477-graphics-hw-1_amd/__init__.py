@@ -432,7 +432,13 @@ class Scene:
         n = lib().rt_counters_read_raw(self._h, out.ctypes.data_as(ctypes.c_void_p), 32)
         if n < 0:
             _check(n)
-        return {k: int(out[8 + i]) for i, k in enumerate(self.COUNTER_SLOTS)}
+        res = {k: int(out[8 + i]) for i, k in enumerate(self.COUNTER_SLOTS)}
+        res.update({k: int(out[24 + i]) for i, k in enumerate(self.FALLBACK_SLOTS)})
+        return res
+
+    # slots 24.. (pathchain.hpp kCntFb*): per chain launch, what the timed walks left to k_fallback
+    FALLBACK_SLOTS = ("fb_launches", "fb_continuations", "fb_continuations_beyond_cb", "fb_deferred_closest",
+                      "fb_deferred_shadow", "fb_shadow_queue_overflows")
 
     KERNEL_KINDS = ("k_chain", "k_pack_a", "k_mix", "k_occlude_a", "k_pack_b", "k_occlude_b", "k_finish", "k_fallback")
 

@@ -149,6 +149,26 @@ __device__ __forceinline__ void block_init(const rtk::DevScene& s) {
 
 __device__ __forceinline__ int lane_id() { return (int)(threadIdx.x & 63); }
 
+// Always-on bound on a loop that waits on other lanes or waves of the workgroup without progress of
+// its own (the phase-A unit hand-off, the phase-B LDS shadow queue, the wave leaf queue): after
+// s.spin_cap such iterations it gives up, sets bit 1 of the scene's device error word (rt_render* /
+// rt_scene_check return RT_ERR_LIMIT) and the caller leaves the loop, so a scheduling bug ends the
+// kernel with an error instead of hanging the GPU.  n counts the iterations of the current wait.
+__device__ __forceinline__ bool spin_over(const rtk::DevScene& s, unsigned& n) {
+    if (++n <= (unsigned)s.spin_cap) return false;
+    __hip_atomic_fetch_or(s.err, 2u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    return true;
+}
+
+// LDS words written by other waves of the workgroup: atomic loads and stores (a plain or volatile
+// load may be kept in a register across the wait loop).
+__device__ __forceinline__ unsigned lds_load(const unsigned* p) {
+    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+__device__ __forceinline__ void lds_store(unsigned* p, unsigned v) {
+    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+
 __device__ __forceinline__ unsigned lane_rank(unsigned long long mask) {
     const int lane = threadIdx.x & 63;
     return (unsigned)__popcll(mask & ((1ull << lane) - 1ull));
@@ -555,6 +575,7 @@ __device__ uint32_t bq_consume(const rtk::DevScene& s, const PcParams& p, WalkSt
     unsigned owner = 0;
     Walk wk;
     uint32_t n = 0;
+    unsigned spins = 0;      // consecutive iterations with no lane walking (spin_over)
     StepStat stat;
     while (true) {
         const unsigned long long want = __ballot(!active && !have && !out);
@@ -591,10 +612,11 @@ __device__ uint32_t bq_consume(const rtk::DevScene& s, const PcParams& p, WalkSt
             }
         }
         if (!__any(active)) {
-            if (__all(out)) break;
+            if (__all(out) || spin_over(s, spins)) break;
             if (__any(idle)) __builtin_amdgcn_s_sleep(2);
             continue;
         }
+        spins = 0;
         stat.step(active, wk.cur >= 0, RT_STEP_STATS && active && wk.tree == nullptr && leaf_postponed(s.leaf_wait_any, wk));
         if (active) {
             const int res = occl_step_timed<COUNT>(s, r, tlim, stk, wk, w);
@@ -763,14 +785,24 @@ __device__ void chain_body(const rtk::DevScene& s, const rtk::Eye& e, const PcPa
                     // beyond the counter's end means no later one either
                     const unsigned jf = (base + 255u) >> 8;
                     if (lane_id() == 0 && jf * 256u < base + (unsigned)__popcll(idle) && jf < (unsigned)p.dyn_units) {
+                        bool late = false;          // spin_over: the previous unit never came
+                        unsigned n = 0;
                         if (jf > 0)
-                            while (*(volatile unsigned*)&g_uid[jf - 1] == kUidUnset) __builtin_amdgcn_s_sleep(1);
-                        const unsigned u = atomicAdd(&p.totals[3], 1u);
-                        *(volatile unsigned*)&g_uid[jf] = u < units ? unit_order(p, u, units) : kUidNone;
+                            while (lds_load(&g_uid[jf - 1]) == kUidUnset) {
+                                if (spin_over(s, n)) { late = true; break; }
+                                __builtin_amdgcn_s_sleep(1);
+                            }
+                        const unsigned u = late ? units : atomicAdd(&p.totals[3], 1u);
+                        lds_store(&g_uid[jf], u < units ? unit_order(p, u, units) : kUidNone);
                     }
                     const unsigned v = base + lane_rank(idle);
-                    if (st == kIdle && v < nb)
-                        while ((uid = *(volatile unsigned*)&g_uid[v >> 8]) == kUidUnset) __builtin_amdgcn_s_sleep(1);
+                    if (st == kIdle && v < nb) {
+                        unsigned n = 0;
+                        while ((uid = lds_load(&g_uid[v >> 8])) == kUidUnset) {
+                            if (spin_over(s, n)) { uid = kUidNone; break; }
+                            __builtin_amdgcn_s_sleep(1);
+                        }
+                    }
                     if (__any(st == kIdle && v < nb && uid == kUidNone)) exhausted = true;
                 }
                 if (st == kIdle) {
@@ -1044,7 +1076,9 @@ __device__ void occlude_queue_body(const rtk::DevScene& s, const PcParams& p, un
     float tlim = 0.0f;
     unsigned owner = 0;
     int cur = 0, sp = 0, steps = 0;
+    unsigned spins = 0;      // consecutive iterations without a step, a test, a retired task or a grab (spin_over)
     while (true) {
+        bool prog = false;   // this iteration made progress (wave-uniform)
         // (1) retire finished tasks: occluded (a record hit), or walked with every record tested
         {
             const unsigned long long hm = __atomic_load_n(&g_lhit[wave], __ATOMIC_RELAXED);
@@ -1053,10 +1087,12 @@ __device__ void occlude_queue_body(const rtk::DevScene& s, const PcParams& p, un
                 done = true;
                 trav = false;
             }
-            if (have && !trav && __atomic_load_n(pend, __ATOMIC_RELAXED) == 0) {
+            const bool retire = have && !trav && __atomic_load_n(pend, __ATOMIC_RELAXED) == 0;
+            if (retire) {
                 if (!done) p.occ[owner] = 0;
                 have = false;
             }
+            prog = __any(retire);
             const unsigned long long freed = __ballot(!have) & hm;
             if (freed && lane == 0) atomicAnd(&g_lhit[wave], ~freed);   // the next task starts unmarked
         }
@@ -1064,6 +1100,7 @@ __device__ void occlude_queue_body(const rtk::DevScene& s, const PcParams& p, un
         if (!exhausted) {
             const unsigned long long idle = __ballot(!have);
             if (idle && __popcll(idle) >= 64 - p.orefill) {
+                prog = true;
                 const unsigned base = wave_grab_lds(&g_head, idle);
                 if (base + (unsigned)__popcll(idle) >= n) exhausted = true;
                 if (!have) {
@@ -1113,6 +1150,7 @@ __device__ void occlude_queue_body(const rtk::DevScene& s, const PcParams& p, un
             if (__atomic_load_n(&g_lqn[wave], __ATOMIC_RELAXED) >= 64u || !im) break;
             if (__popcll(__ballot(have && !trav)) >= p.lq_wait) break;
             if (!exhausted && __popcll(__ballot(have)) <= p.orefill) break;
+            prog = true;
             if (trav && cur >= 0) {
                 constexpr int W = dl::kWideSlots;
                 WideNode nd;
@@ -1155,8 +1193,12 @@ __device__ void occlude_queue_body(const rtk::DevScene& s, const PcParams& p, un
         }
         // (4) test queued records: 64 at a time, or what is left once no lane walks
         const unsigned nq = __atomic_load_n(&g_lqn[wave], __ATOMIC_RELAXED);
-        if (nq >= 64u || (nq > 0u && (!__any(trav) || __popcll(__ballot(have && !trav)) >= p.lq_wait)))
+        if (nq >= 64u || (nq > 0u && (!__any(trav) || __popcll(__ballot(have && !trav)) >= p.lq_wait))) {
             lq_flush(s, r, tlim, nq);
+            prog = true;
+        }
+        if (prog) spins = 0;
+        else if (spin_over(s, spins)) break;
     }
 }
 
@@ -1400,7 +1442,7 @@ __global__ __launch_bounds__(kBlock, RT_WAVES_PER_EU) void k_fused(rtk::DevScene
         bool active = false;
         float tlim = 0.0f;
         unsigned owner = 0;
-        int spin = 0;
+        unsigned spin = 0;   // consecutive waits with nothing taken (spin_over)
         while (true) {
             const unsigned long long idle = __ballot(!active);
             unsigned gq = 0, gt = 0, gn = 0;
@@ -1450,11 +1492,11 @@ __global__ __launch_bounds__(kBlock, RT_WAVES_PER_EU) void k_fused(rtk::DevScene
                     }
                 }
             }
+            if (gn > 0) spin = 0;
             if (!__any(active)) {
                 if (gn == 0) {
-                    if (!live) break;                 // producers done and every queue drained
+                    if (!live || spin_over(s, spin)) break;   // producers done and every queue drained
                     __builtin_amdgcn_s_sleep(2);
-                    ++spin;
                 }
                 continue;
             }
@@ -1470,7 +1512,6 @@ __global__ __launch_bounds__(kBlock, RT_WAVES_PER_EU) void k_fused(rtk::DevScene
                 }
             }
         }
-        (void)spin;
     }
     if (COUNT) {
         wave_add_counter(&p.counters[0], nprim);
@@ -1816,6 +1857,14 @@ __global__ __launch_bounds__(kBlock) void k_fallback(rtk::DevScene s, rtk::Eye e
     const unsigned gt = blockIdx.x * kBlock + threadIdx.x, gs = gridDim.x * kBlock;
     const unsigned nfc = min(p.totals[4], p.fbc_cap);
     const unsigned ncont = p.totals[1], novf = ncont > p.cb ? ncont - p.cb : 0u;
+    if (gt == 0 && p.counters) {                   // what this launch left to k_fallback (rt_counters_read_raw)
+        atomicAdd(&p.counters[kCntFbLaunches], 1ull);
+        atomicAdd(&p.counters[kCntFbConts], (unsigned long long)ncont);
+        atomicAdd(&p.counters[kCntFbContOvf], (unsigned long long)novf);
+        atomicAdd(&p.counters[kCntFbChains], (unsigned long long)p.totals[4]);
+        atomicAdd(&p.counters[kCntFbShadows], (unsigned long long)p.totals[5]);
+        if (p.totals[6]) atomicAdd(&p.counters[kCntFbOvfScans], 1ull);
+    }
     for (unsigned i = gt; i < nfc + novf; i += gs)
         fallback_chain(s, e, p, i < nfc ? p.fbc[i] : p.cflat[p.cb + (i - nfc)], stk, w);
     const unsigned nfs = min(p.totals[5], p.fbs_cap);

@@ -65,6 +65,13 @@ enum CounterSlot : int {
     kCntBQRays,
     kCntBOBytes,          // B's shadow rays that overflowed to k_occlude
     kCntBORays,
+    // every launch (timed or counting), added by k_fallback: what the timed walks left to it
+    kCntFbLaunches = 24,  // chain launches
+    kCntFbConts,          //   continuations handed from A to B (all of them)
+    kCntFbContOvf,        //   of those, beyond the phase-B record space (cb): walked whole by k_fallback
+    kCntFbChains,         //   closest-hit rays deferred (not in range of the wide trees' slab test)
+    kCntFbShadows,        //   shadow rays deferred
+    kCntFbOvfScans,       //   launches whose fallback shadow queue overflowed (occlusion bytes scanned)
 };
 
 struct PcParams {

@@ -27,19 +27,23 @@ namespace {
 
 constexpr int kBlk = 256;
 
-// four 16-B loads in flight per lane before their (nontemporal) stores (n: a multiple of 4 x the grid's
-// threads)
+// U 16-B loads in flight per lane before their stores (plain or nontemporal); n: a multiple of U x the
+// grid's threads.  rt_measure_peaks keeps the best variant and grid (MI355X_MICROARCH.md: ~6.3 TB/s).
 typedef float f4v __attribute__((ext_vector_type(4)));
+template <int U, bool NT>
 __global__ __launch_bounds__(kBlk) void k_copy(const float4* __restrict__ src_, float4* __restrict__ dst_, size_t n) {
     const f4v* src = reinterpret_cast<const f4v*>(src_);
     f4v* dst = reinterpret_cast<f4v*>(dst_);
     const size_t stride = (size_t)gridDim.x * kBlk;
-    for (size_t i = (size_t)blockIdx.x * kBlk + threadIdx.x; i + 3 * stride < n; i += 4 * stride) {
-        const f4v a = src[i], b = src[i + stride], c = src[i + 2 * stride], d = src[i + 3 * stride];
-        __builtin_nontemporal_store(a, dst + i);
-        __builtin_nontemporal_store(b, dst + i + stride);
-        __builtin_nontemporal_store(c, dst + i + 2 * stride);
-        __builtin_nontemporal_store(d, dst + i + 3 * stride);
+    for (size_t i = (size_t)blockIdx.x * kBlk + threadIdx.x; i + (U - 1) * stride < n; i += U * stride) {
+        f4v v[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) v[u] = src[i + u * stride];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            if (NT) __builtin_nontemporal_store(v[u], dst + i + u * stride);
+            else dst[i + u * stride] = v[u];
+        }
     }
 }
 
@@ -155,6 +159,8 @@ extern "C" int rt_measure_peaks(int device, uint64_t scene_table_bytes, rt_peaks
     const size_t scene_table = std::max<size_t>(128, std::min<size_t>(scene_table_bytes, size_t(64) << 20)) & ~size_t(127);
     const size_t tab_bytes = std::max(small_table, scene_table);
     int cus = 256;
+    int caller_dev = -1;                                           // restored on exit (the caller's current device)
+    (void)hipGetDevice(&caller_dev);
     {
         if (device >= 0) PK_TRY(hipSetDevice(device));
         hipDeviceProp_t prop;
@@ -187,17 +193,25 @@ extern "C" int rt_measure_peaks(int device, uint64_t scene_table_bytes, rt_peaks
         };
         const dim3 grid(cus * 8), blk(kBlk);
         float ms = 0;
-        for (int wpc : {8, 16, 32}) {              // best over the grid size (2 GiB divides every grid's 4 x threads)
-            const dim3 cg(cus * wpc / 4);
-            ms = best_ms([&] { hipLaunchKernelGGL(k_copy, cg, blk, 0, st, big, big2, nbig); }, 5);
-            if (ms <= 0) { err = "peaks: copy timing failed"; goto done; }
-            out->hbm_copy_gbps = std::max(out->hbm_copy_gbps, 2.0 * (double)big_bytes / (ms * 1e-3) / 1e9);
+        for (int wpc : {4, 8, 16, 32})             // best over the grid size and the copy variant (2 GiB divides
+            for (int var = 0; var < 4; ++var) {     // every grid's 8 x threads)
+                const dim3 cg(cus * wpc / 4);
+                ms = best_ms([&] {
+                    if (var == 0) hipLaunchKernelGGL((k_copy<4, true>), cg, blk, 0, st, big, big2, nbig);
+                    else if (var == 1) hipLaunchKernelGGL((k_copy<4, false>), cg, blk, 0, st, big, big2, nbig);
+                    else if (var == 2) hipLaunchKernelGGL((k_copy<8, true>), cg, blk, 0, st, big, big2, nbig);
+                    else hipLaunchKernelGGL((k_copy<8, false>), cg, blk, 0, st, big, big2, nbig);
+                }, 4);
+                if (ms <= 0) { err = "peaks: copy timing failed"; goto done; }
+                out->hbm_copy_gbps = std::max(out->hbm_copy_gbps, 2.0 * (double)big_bytes / (ms * 1e-3) / 1e9);
+            }
+        for (int wpc : {8, 16, 32}) {
+            const dim3 rg(cus * wpc / 4);
+            ms = best_ms([&] { hipLaunchKernelGGL(k_read, rg, blk, 0, st, big, nbig, sink); }, 4);
+            if (ms <= 0) { err = "peaks: read timing failed"; goto done; }
+            out->hbm_read_gbps = std::max(out->hbm_read_gbps, (double)big_bytes / (ms * 1e-3) / 1e9);
         }
-        ms = best_ms([&] { hipLaunchKernelGGL(k_read, grid, blk, 0, st, big, nbig, sink); }, 5);
-        if (ms <= 0) { err = "peaks: read timing failed"; goto done; }
-        out->hbm_read_gbps = (double)big_bytes / (ms * 1e-3) / 1e9;
         const int iters = 64;
-        const double gbytes = (double)grid.x * kBlk * iters * 128.0;
         PK_TRY(hipMemcpyAsync(tab, big, tab_bytes, hipMemcpyDeviceToDevice, st));   // varied words (the walk's hash)
         for (int which = 0; which < 4; ++which) {
             const size_t tb = (which & 1) == 0 ? small_table : scene_table;
@@ -212,9 +226,16 @@ extern "C" int rt_measure_peaks(int device, uint64_t scene_table_bytes, rt_peaks
                     gbps = std::max(gbps, (double)wg.x * kBlk * wsteps * 128.0 / (ms * 1e-3) / 1e9);
                 }
             } else {                   // full-line fetches: 8 lanes per line
-                ms = best_ms([&] { hipLaunchKernelGGL((k_gather<2, true>), grid, blk, 0, st, tab, nlines, iters, 17u + which, sink); }, 5);
-                if (ms <= 0) { err = "peaks: gather timing failed"; goto done; }
-                gbps = gbytes / (ms * 1e-3) / 1e9;
+                for (int var = 0; var < 4; ++var) {     // 2 or 4 lines in flight per lane; 16 or 32 waves per CU
+                    const dim3 gg(var & 2 ? cus * 4 : cus * 8);
+                    const double gb = (double)gg.x * kBlk * iters * 128.0;
+                    ms = best_ms([&] {
+                        if (var & 1) hipLaunchKernelGGL((k_gather<4, true>), gg, blk, 0, st, tab, nlines, iters, 17u + which, sink);
+                        else hipLaunchKernelGGL((k_gather<2, true>), gg, blk, 0, st, tab, nlines, iters, 17u + which, sink);
+                    }, 4);
+                    if (ms <= 0) { err = "peaks: gather timing failed"; goto done; }
+                    gbps = std::max(gbps, gb / (ms * 1e-3) / 1e9);
+                }
             }
             if (which == 0) { out->l2_gather_gbps = gbps; out->l2_table_bytes = (double)tb; }
             else if (which == 1) { out->scene_gather_gbps = gbps; out->scene_table_bytes = (double)tb; }
@@ -229,6 +250,7 @@ done:
     if (e0) (void)hipEventDestroy(e0);
     if (e1) (void)hipEventDestroy(e1);
     if (st) (void)hipStreamDestroy(st);
+    if (caller_dev >= 0) (void)hipSetDevice(caller_dev);
     if (!err.empty()) return rt_internal_set_error(RT_ERR_HIP, err.c_str());
     return RT_OK;
 }

@@ -47,8 +47,11 @@ struct DevScene {
     int wroot;
     int use_wide;         // NaN-free closest-hit rays walk wnodes (traverse2.hpp wide_closest_step)
     int leaf_wait_any;    // the same for any-hit walks (RT_LEAF_WAIT_ANY)
-    unsigned* err;        // device error word (bit 0: a walk exceeded walk_cap), read by the host after renders
+    unsigned* err;        // device error word (bit 0: a walk exceeded walk_cap; bit 1: a wait loop exceeded
+                          // spin_cap), read by the host after renders
     int walk_cap;         // always-on bound on one walk's step calls (traverse2.hpp walk_runaway)
+    int spin_cap;         // always-on bound on the iterations of a loop that waits on other lanes or waves
+                          // without progress (pathchain.hip spin_over; RT_SPIN_CAP overrides)
     int leaf_wait;        // 4-wide walks: a lane at a leaf record waits while fewer than leaf_wait/64 of the
                           // wave's walking lanes are at one (0: never waits; RT_LEAF_WAIT)
     int cull_shadows;     // chain path: shadow rays that cannot change the pixel are not traced

@@ -163,15 +163,7 @@ struct rt_scene {
     long long kt_launches = 0;
     rtc::KTimer kt;
     size_t slot_budget() const { return ws_budget / (size_t)std::max(1, std::min(tune_slots, kSlots)); }
-    // samples whose worst-case chain arena fits one slot's budget (pathchain.hip layout: records, path
-    // word, occlusion bytes, phase-A/B shadow queues and packed lists, continuation queues)
-    size_t slot_samples() const {
-        const size_t levels = (size_t)std::max(dev.max_depth, 0) + 1, nl = (size_t)std::max(dev.nlights, 1);
-        const size_t la = std::min((size_t)std::max(tune_kinline, 0), levels - 1) + 1;
-        const size_t per = la * (32 + nl) + 4 + 4 + 16 + 8 + la * nl * 12 + 12 +
-                           (levels - la) * (32 + nl + 8 * nl) / (size_t)std::max(1, tune_cont_den);
-        return std::max<size_t>(4096, slot_budget() / per / 32 * 31);
-    }
+    bool warned_budget = false;    // one row unit alone exceeds the slot budget (chain_launch_units): told once
     std::string trace_file;     // RT_TRACE: dump per-sample wall-clock timings after each render (diagnostics)
     unsigned* d_trace = nullptr;
     size_t trace_cap = 0;
@@ -433,6 +425,10 @@ int upload_scene(rt_scene* s, const rt_options* opts) {
         d.walk_cap = (int)std::min<long long>(INT32_MAX / 2, 64 * nodes);
         if (const char* e = std::getenv("RT_WALK_CAP")) d.walk_cap = std::max(1, std::atoi(e));
     }
+    // spin_over: 2^24 iterations of a wait that sees no progress (with s_sleep ~0.5 s, far beyond the
+    // longest legitimate wait: one walk of at most nodes + leaves steps); RT_SPIN_CAP overrides (tests)
+    d.spin_cap = 1 << 24;
+    if (const char* e = std::getenv("RT_SPIN_CAP")) d.spin_cap = std::max(0, std::atoi(e));   // 0: every wait gives up
     d.leaf_wait = 24;   // measured: 0 1.20, 8 1.19, 16-32 1.166, 48 1.22, 64 1.46 ms (C3)
     if (const char* e = std::getenv("RT_LEAF_WAIT")) d.leaf_wait = std::max(0, std::min(64, std::atoi(e)));
     d.leaf_wait_any = d.leaf_wait;
@@ -606,110 +602,144 @@ struct ChainPlan {
            o_fbc = 0, o_fbs = 0, bytes = 0;
 };
 
-int render_chain(rt_scene* s, const rtk::Eye& eye, const rtk::FrameParams& f, bool count, hipStream_t st,
-                 int slot = 0) {
-    rt_scene::Arena& arena = s->arenas[slot];
-    const int levels = std::max(s->dev.max_depth, 0) + 1;
-    const int nl = std::max(s->dev.nlights, 1);
-    const int wi = f.width * f.aa;
-    const int tiles_x = (wi + 7) / 8;
-    const int li = f.slab_rows * f.aa;
-    const int unit = 8 * f.aa;
-    const size_t unit_samples = (size_t)tiles_x * f.aa * 64;
-    const size_t units_total = (size_t)(li + unit - 1) / unit;
+// Geometry of one chain-path launch series (a frame, or a frame batch stacked as one slab).
+struct ChainGeom {
+    int levels, nl, wi, tiles_x, li, unit, nframes;
+    size_t unit_samples, units_total;
+};
+ChainGeom chain_geom(const rt_scene* s, const rtk::FrameParams& f) {
+    ChainGeom g;
+    g.levels = std::max(s->dev.max_depth, 0) + 1;
+    g.nl = std::max(s->dev.nlights, 1);
+    g.wi = f.width * f.aa;
+    g.tiles_x = (g.wi + 7) / 8;
+    g.li = f.slab_rows * f.aa;
+    g.unit = 8 * f.aa;
+    g.unit_samples = (size_t)g.tiles_x * f.aa * 64;
+    g.units_total = (size_t)(g.li + g.unit - 1) / g.unit;
+    g.nframes = std::max(1, f.nframes);
+    return g;
+}
+
+// The kernels' grids from their occupancy (once per scene).
+int ensure_chain_grids(rt_scene* s) {
+    if (s->chain_grid != 0) return RT_OK;
+    int cb = 0, mb = 0, ob = 0, fb = 0;
+    HIP_TRY(rtc::chain_occupancy(&cb, &mb, &ob));
+    HIP_TRY(rtc::fused_occupancy(&fb));
+    s->chain_grid = std::min(rtc::kMaxChainGrid, std::max(1, cb) * s->num_cus);
+    s->mix_grid = std::max(1, mb) * s->num_cus;
+    s->occl_grid = std::max(1, ob) * s->num_cus;
+    s->fused_grid = std::max(1, fb) * s->num_cus;
+    if (const char* e = std::getenv("RT_CGRID")) s->chain_grid = std::max(1, std::min(rtc::kMaxChainGrid, std::atoi(e)));
+    if (const char* e = std::getenv("RT_OGRID")) s->occl_grid = std::max(1, std::atoi(e));
+    if (const char* e = std::getenv("RT_MGRID")) s->mix_grid = std::max(2, std::atoi(e));
+    return RT_OK;
+}
+
+// Every size of a launch of `nunits` row units, and its arena layout: worst-case queue sizing (every
+// sample recording every level), so no queue can overflow.  (ensure_chain_grids first.)
+ChainPlan chain_plan(const rt_scene* s, const ChainGeom& g, size_t nunits, bool count) {
     const bool fused = s->path == rt_scene::kFused;
-    if (s->chain_grid == 0) {
-        int cb = 0, mb = 0, ob = 0, fb = 0;
-        HIP_TRY(rtc::chain_occupancy(&cb, &mb, &ob));
-        HIP_TRY(rtc::fused_occupancy(&fb));
-        s->chain_grid = std::min(rtc::kMaxChainGrid, std::max(1, cb) * s->num_cus);
-        s->mix_grid = std::max(1, mb) * s->num_cus;
-        s->occl_grid = std::max(1, ob) * s->num_cus;
-        s->fused_grid = std::max(1, fb) * s->num_cus;
-        if (const char* e = std::getenv("RT_CGRID")) s->chain_grid = std::max(1, std::min(rtc::kMaxChainGrid, std::atoi(e)));
-        if (const char* e = std::getenv("RT_OGRID")) s->occl_grid = std::max(1, std::atoi(e));
-        if (const char* e = std::getenv("RT_MGRID")) s->mix_grid = std::max(2, std::atoi(e));
-    }
+    const int levels = g.levels, nl = g.nl;
     const int max_grid = fused ? s->fused_grid : s->chain_grid;
-    auto grid_for = [&](int n0) { return std::max(1, std::min(max_grid, (n0 + 255) / 256)); };
-    // Every size of a launch of `units` row units, and its arena layout: worst-case queue sizing (every
-    // sample recording every level), so no queue can overflow.
-    auto plan = [&](size_t nunits) {
-        ChainPlan P;
-        P.cap = nunits * unit_samples;
-        const size_t cap = P.cap;
-        P.G = grid_for((int)std::min<size_t>(cap, INT32_MAX));
-        // phase split: A walks levels [0, kinline], B the rest (k_mix chain role, gb workgroups)
-        P.kinline = std::max(0, s->tune_kinline);
-        P.phase_b = P.kinline < s->dev.max_depth;
-        // phase-B workgroups: a lone frame's deep chains are its critical path (1.875 per CU best since
-        // round 3: C3 one frame, 61-frame medians, 1.5625 0.946-0.948, 1.72 0.940, 1.875 0.925-0.935,
-        // 2.03 0.956 ms);
-        // in frame batches other frames hide them and the shadow role wants the CUs (C3: 0.5 per CU
-        // 0.550 ms/frame, 0.75 0.552, 1 0.554, 1.25 0.557, 1.5625 0.568)
-        // frame batches: A's shadow rays in their own 5-wave k_occlude launch (split_occ) and 1 phase-B
-        // workgroup per CU (6 slots in flight: 0.504-0.512 -> 0.495 ms/frame; 0.5 per CU 0.500, 2 0.4995)
-        P.split_occ = f.nframes > 1 && (!std::getenv("RT_SPLIT_OCC") || std::atoi(std::getenv("RT_SPLIT_OCC")));
-        const int gb_default = f.nframes > 1 ? (P.split_occ ? s->num_cus : s->num_cus / 2) : 30 * s->num_cus / 16;
-        P.gb = P.phase_b ? std::max(1, std::min(s->mix_grid - 1, s->tune_gb > 0 ? s->tune_gb : gb_default)) : 0;
-        P.levels_a = std::min(P.kinline, std::max(s->dev.max_depth, 0)) + 1;
-        // dynamic phase-A units: a workgroup may take up to twice its static share (at most
-        // rtc::kDynUnits), and its queues are sized for that
-        const unsigned share = rtc::chain_block_units((int)std::min<size_t>(cap, INT32_MAX), P.G);
-        P.dyn_units = s->tune_dyn && share <= (unsigned)rtc::kDynUnits ? std::min(2u * share, (unsigned)rtc::kDynUnits) : 0u;
-        const unsigned units_a = P.dyn_units ? P.dyn_units : share;
-        P.scapA = units_a * 256u * (unsigned)(P.levels_a * nl);
-        P.ccapA = units_a * 256u;
-        // records: levels [0, la) for every sample; deeper ones (phase B) for the first cb continuations
-        // (the rest finish in k_fallback; counting passes keep every one: cb = cap)
-        P.la = fused || !P.phase_b ? levels : P.levels_a;
-        P.cb = P.la >= levels ? 0 : (count ? cap : std::min(cap, std::max(cap / (size_t)std::max(1, s->tune_cont_den),
-                                                                            std::min<size_t>(cap, 65536))));
-        if (s->tune_cont_cb > 0 && !count && P.la < levels) P.cb = std::min(cap, (size_t)s->tune_cont_cb);
-        P.tchunk = s->tune_tchunk > 0 ? s->tune_tchunk : (f.nframes > 1 ? 128 : 1);
-        {   // a phase-B workgroup's continuations: at most ceil(chunks / gb) chunks of tchunk (chunk_count)
-            const size_t ch = (size_t)P.tchunk, nch = (P.cb + ch - 1) / ch;
-            const size_t per_wg = P.gb > 0 ? (nch + P.gb - 1) / P.gb * ch : 0;
-            P.scapB = P.phase_b ? (unsigned)(per_wg * (size_t)(levels - P.la) * nl) : 0u;
-        }
-        P.wq_cap = fused ? rtc::fused_wave_qcap((int)std::min<size_t>(cap, INT32_MAX), P.G, levels, nl) : 0u;
-        const size_t nrec = cap * P.la + P.cb * (levels - P.la);
-        ArenaLayout L;
-        P.o_rec = L.take<float4>(2 * nrec);
-        P.o_pinfo = L.take<int>(cap);
-        P.o_occ = L.take<uint8_t>(nrec * nl + 8);   // + 8: k_finish reads aligned dwords
-        P.o_cid = L.take<unsigned>(cap);
-        P.o_tail = L.take<float4>(cap);
-        P.o_fbc = L.take<unsigned>(cap);
-        P.o_fbs = L.take<unsigned>(cap);
-        if (fused) {
-            P.o_wq = L.take<unsigned>((size_t)P.G * 4 * P.wq_cap);
-        } else {
-            P.o_sqA = L.take<unsigned>((size_t)P.G * P.scapA); P.o_scntA = L.take<unsigned>(P.G);
-            P.o_sflatA = L.take<unsigned>(cap * P.levels_a * nl);
-            P.o_cq = L.take<unsigned>((size_t)P.G * P.ccapA); P.o_ccnt = L.take<unsigned>(P.G);
-            P.o_cflat = L.take<unsigned>(cap);
-            P.o_sqB = L.take<unsigned>((size_t)P.gb * P.scapB); P.o_scntB = L.take<unsigned>(P.gb + 1);
-            P.o_sflatB = L.take<unsigned>(P.cb * (levels - P.la) * nl);
-        }
-        P.o_totals = L.take<unsigned>(8);
-        P.bytes = L.off;
-        return P;
-    };
-    // Launch size: as many row units as the chunk target (RT_CHUNK_SAMPLES), the u32 task ids and the
-    // slot's share of the workspace budget (RT_WS_BUDGET_MB over the slots) allow.
-    const size_t id_limit = (size_t)(INT32_MAX - 1) / ((size_t)levels * nl);   // u32 task owner ids (pathchain.hpp)
-    size_t units = std::min(units_total, std::max<size_t>(1, std::min(s->chunk_samples, id_limit) / unit_samples));
+    ChainPlan P;
+    P.cap = nunits * g.unit_samples;
+    const size_t cap = P.cap;
+    P.G = std::max(1, std::min(max_grid, (int)((std::min<size_t>(cap, INT32_MAX) + 255) / 256)));
+    // phase split: A walks levels [0, kinline], B the rest (k_mix chain role, gb workgroups)
+    P.kinline = std::max(0, s->tune_kinline);
+    P.phase_b = P.kinline < s->dev.max_depth;
+    // phase-B workgroups: a lone frame's deep chains are its critical path (1.875 per CU best since
+    // round 3: C3 one frame, 61-frame medians, 1.5625 0.946-0.948, 1.72 0.940, 1.875 0.925-0.935,
+    // 2.03 0.956 ms);
+    // in frame batches other frames hide them and the shadow role wants the CUs (C3: 0.5 per CU
+    // 0.550 ms/frame, 0.75 0.552, 1 0.554, 1.25 0.557, 1.5625 0.568)
+    // frame batches: A's shadow rays in their own 5-wave k_occlude launch (split_occ) and 1 phase-B
+    // workgroup per CU (6 slots in flight: 0.504-0.512 -> 0.495 ms/frame; 0.5 per CU 0.500, 2 0.4995)
+    P.split_occ = g.nframes > 1 && (!std::getenv("RT_SPLIT_OCC") || std::atoi(std::getenv("RT_SPLIT_OCC")));
+    const int gb_default = g.nframes > 1 ? (P.split_occ ? s->num_cus : s->num_cus / 2) : 30 * s->num_cus / 16;
+    P.gb = P.phase_b ? std::max(1, std::min(s->mix_grid - 1, s->tune_gb > 0 ? s->tune_gb : gb_default)) : 0;
+    P.levels_a = std::min(P.kinline, std::max(s->dev.max_depth, 0)) + 1;
+    // dynamic phase-A units: a workgroup may take up to twice its static share (at most
+    // rtc::kDynUnits), and its queues are sized for that
+    const unsigned share = rtc::chain_block_units((int)std::min<size_t>(cap, INT32_MAX), P.G);
+    P.dyn_units = s->tune_dyn && share <= (unsigned)rtc::kDynUnits ? std::min(2u * share, (unsigned)rtc::kDynUnits) : 0u;
+    const unsigned units_a = P.dyn_units ? P.dyn_units : share;
+    P.scapA = units_a * 256u * (unsigned)(P.levels_a * nl);
+    P.ccapA = units_a * 256u;
+    // records: levels [0, la) for every sample; deeper ones (phase B) for the first cb continuations
+    // (the rest finish in k_fallback; counting passes keep every one: cb = cap)
+    P.la = fused || !P.phase_b ? levels : P.levels_a;
+    P.cb = P.la >= levels ? 0 : (count ? cap : std::min(cap, std::max(cap / (size_t)std::max(1, s->tune_cont_den),
+                                                                        std::min<size_t>(cap, 65536))));
+    if (s->tune_cont_cb > 0 && !count && P.la < levels) P.cb = std::min(cap, (size_t)s->tune_cont_cb);
+    P.tchunk = s->tune_tchunk > 0 ? s->tune_tchunk : (g.nframes > 1 ? 128 : 1);
+    {   // a phase-B workgroup's continuations: at most ceil(chunks / gb) chunks of tchunk (chunk_count)
+        const size_t ch = (size_t)P.tchunk, nch = (P.cb + ch - 1) / ch;
+        const size_t per_wg = P.gb > 0 ? (nch + P.gb - 1) / P.gb * ch : 0;
+        P.scapB = P.phase_b ? (unsigned)(per_wg * (size_t)(levels - P.la) * nl) : 0u;
+    }
+    P.wq_cap = fused ? rtc::fused_wave_qcap((int)std::min<size_t>(cap, INT32_MAX), P.G, levels, nl) : 0u;
+    const size_t nrec = cap * P.la + P.cb * (levels - P.la);
+    ArenaLayout L;
+    P.o_rec = L.take<float4>(2 * nrec);
+    P.o_pinfo = L.take<int>(cap);
+    P.o_occ = L.take<uint8_t>(nrec * nl + 8);   // + 8: k_finish reads aligned dwords
+    P.o_cid = L.take<unsigned>(cap);
+    P.o_tail = L.take<float4>(cap);
+    P.o_fbc = L.take<unsigned>(cap);
+    P.o_fbs = L.take<unsigned>(cap);
+    if (fused) {
+        P.o_wq = L.take<unsigned>((size_t)P.G * 4 * P.wq_cap);
+    } else {
+        P.o_sqA = L.take<unsigned>((size_t)P.G * P.scapA); P.o_scntA = L.take<unsigned>(P.G);
+        P.o_sflatA = L.take<unsigned>(cap * P.levels_a * nl);
+        P.o_cq = L.take<unsigned>((size_t)P.G * P.ccapA); P.o_ccnt = L.take<unsigned>(P.G);
+        P.o_cflat = L.take<unsigned>(cap);
+        P.o_sqB = L.take<unsigned>((size_t)P.gb * P.scapB); P.o_scntB = L.take<unsigned>(P.gb + 1);
+        P.o_sflatB = L.take<unsigned>(P.cb * (levels - P.la) * nl);
+    }
+    P.o_totals = L.take<unsigned>(8);
+    P.bytes = L.off;
+    return P;
+}
+
+// Row units of one launch: as many as the chunk target (RT_CHUNK_SAMPLES), the u32 task ids and the
+// slot's share of the workspace budget (RT_WS_BUDGET_MB over the slots) allow -- the largest count
+// whose chain_plan arena fits the budget (at least one unit, whatever its size).
+size_t chain_launch_units(rt_scene* s, const ChainGeom& g, bool count) {
+    const size_t id_limit = (size_t)(INT32_MAX - 1) / ((size_t)g.levels * g.nl);   // u32 task owner ids (pathchain.hpp)
+    size_t units = std::min(g.units_total, std::max<size_t>(1, std::min(s->chunk_samples, id_limit) / g.unit_samples));
     const size_t budget = s->slot_budget();
-    if (plan(units).bytes > budget) {
+    if (chain_plan(s, g, units, count).bytes > budget) {
         size_t lo = 1, hi = units;                 // largest units in [1, units] whose arena fits the budget
         while (lo < hi) {
             const size_t mid = lo + (hi - lo + 1) / 2;
-            if (plan(mid).bytes <= budget) lo = mid; else hi = mid - 1;
+            if (chain_plan(s, g, mid, count).bytes <= budget) lo = mid; else hi = mid - 1;
         }
         units = lo;
+        if (units == 1 && chain_plan(s, g, 1, count).bytes > budget && !s->warned_budget) {
+            s->warned_budget = true;
+            std::fprintf(stderr, "librt_hip: one row unit (%zu samples) needs a %.1f MB workspace, over the slot's "
+                                 "%.1f MB share of RT_WS_BUDGET_MB; allocating it anyway\n",
+                         g.unit_samples, chain_plan(s, g, 1, count).bytes / 1e6, budget / 1e6);
+        }
     }
-    const ChainPlan P = plan(units);
+    return units;
+}
+
+int render_chain(rt_scene* s, const rtk::Eye& eye, const rtk::FrameParams& f, bool count, hipStream_t st,
+                 int slot = 0) {
+    rt_scene::Arena& arena = s->arenas[slot];
+    const ChainGeom g = chain_geom(s, f);
+    const int levels = g.levels, nl = g.nl, wi = g.wi, tiles_x = g.tiles_x, li = g.li, unit = g.unit;
+    const bool fused = s->path == rt_scene::kFused;
+    if (const int rc = ensure_chain_grids(s)) return rc;
+    const int max_grid = fused ? s->fused_grid : s->chain_grid;
+    auto grid_for = [&](int n0) { return std::max(1, std::min(max_grid, (n0 + 255) / 256)); };
+    const size_t units = chain_launch_units(s, g, count);
+    const ChainPlan P = chain_plan(s, g, units, count);
     const int chunk_rows = (int)units * unit;
     const size_t cap = P.cap;
     if (cap * levels * nl >= (size_t)INT32_MAX) return fail(RT_ERR_LIMIT, "frame chunk too large for the chain path");
@@ -768,7 +798,10 @@ int render_chain(rt_scene* s, const rtk::Eye& eye, const rtk::FrameParams& f, bo
     p.fbc_cap = (unsigned)cap;
     p.fbs = static_cast<unsigned*>(at(P.o_fbs));
     p.fbs_cap = s->tune_fbs_cap > 0 ? (unsigned)std::min<size_t>(cap, s->tune_fbs_cap) : (unsigned)cap;
-    p.fb_grid = s->num_cus;
+    // k_fallback: one workgroup per CU (it is empty or nearly so); a scene without the wide trees (their
+    // build or containment check failed, or RT_WIDE_WALK=0 / RT_STREE<2) defers every walk to it, so it
+    // then fills the GPU (those scenes would otherwise render in num_cus workgroups)
+    p.fb_grid = (s->dev.use_wide && s->dev.use_stree == 2 && !s->dev.force_fb) ? s->num_cus : 4 * s->num_cus;
     p.kinline = P.phase_b ? P.kinline : 1 << 30;
     p.gb = P.gb;
     p.ogrid = P.phase_b ? std::max(1, s->mix_grid - P.gb) : s->mix_grid;
@@ -845,12 +878,16 @@ int render_chain(rt_scene* s, const rtk::Eye& eye, const rtk::FrameParams& f, bo
 }
 
 // The device error word after the device is idle: RT_ERR_LIMIT (and the word
-// cleared) when a walk was cut off by walk_runaway since the last check.
+// cleared) when a walk was cut off by walk_runaway (bit 0) or a wait loop by
+// spin_over (bit 1) since the last check.
 int check_device_error(rt_scene* s) {
     unsigned e = 0;
     HIP_TRY(hipMemcpy(&e, s->d_err, sizeof(e), hipMemcpyDeviceToHost));
     if (e == 0) return RT_OK;
     HIP_TRY(hipMemset(s->d_err, 0, sizeof(unsigned)));
+    if (e & 2u)
+        return fail(RT_ERR_LIMIT, "a wait on other lanes or waves exceeded its bound (spin_cap) and was cut off; "
+                                  "the frame is invalid");
     return fail(RT_ERR_LIMIT, "a BVH walk exceeded its step bound (walk_cap) and was cut off; the frame is invalid");
 }
 
@@ -1146,14 +1183,23 @@ int render_cameras(rt_scene* s, const rt_camera* cams, int n, int aa, void* cons
         const int nslot = std::max(1, std::min(s->tune_slots, rt_scene::kSlots));
         const int bmax = std::min({s->tune_batch, rtc::kMaxFrames, (n + nslot - 1) / nslot});
         std::vector<int> starts;
+        HIP_TRY(hipSetDevice(s->device));
+        if (const int rc = ensure_chain_grids(s)) return rc;
         for (int i = 0; i < n;) {
             const auto& c = cams[i];
-            const long long per = (long long)rt_slab_rows(c.image_height, rows_of(i), nranks) * aa *
-                                  ((long long)c.image_width * aa);
+            // a batch of k frames: one launch (render_chain's own plan fits the slot's workspace share)
+            auto fits = [&](int k) {
+                rtk::FrameParams f;
+                f.width = c.image_width;
+                f.aa = aa;
+                f.slab_rows = rt_slab_rows(c.image_height, rows_of(i), nranks) * k;
+                f.nframes = k;
+                const ChainGeom g = chain_geom(s, f);
+                return chain_launch_units(s, g, (flags & RT_RENDER_COUNT) != 0) >= g.units_total;
+            };
             int j = i + 1;
             while (j < n && j - i < bmax &&
-                   cams[j].image_width == c.image_width && cams[j].image_height == c.image_height &&
-                   (long long)(j - i + 1) * per <= (long long)std::min(s->chunk_samples, s->slot_samples()))
+                   cams[j].image_width == c.image_width && cams[j].image_height == c.image_height && fits(j - i + 1))
                 ++j;
             starts.push_back(i);
             i = j;

@@ -240,3 +240,25 @@ def test_walk_step_bound_reports_limit(pkg, scene_dir, torch_cuda, monkeypatch):
     with pkg.Scene.from_xml(xml, device=0) as s:
         s.render(s.camera(0), aa=1)
         s.check()
+
+
+def test_wait_bound_reports_limit(pkg, scene_dir, goldens, torch_cuda, monkeypatch):
+    """The always-on bound on the loops that wait on other lanes or waves (pathchain.hip spin_over: the
+    phase-A unit hand-off, the phase-B LDS shadow queue, the wave leaf queue), forced to 0: every wait
+    gives up at once, so a lone C3 frame (whose phase-B waves wait on the workgroup's shadow queue) ends
+    with RT_ERR_LIMIT instead of hanging; with the default bound the same scene renders the golden."""
+    from conftest import config_path, golden_by_name, load_golden_image
+    g = golden_by_name(goldens, "C3_hm_1080p_d6_aa1")
+    xml = config_path(scene_dir, g["config"])
+    monkeypatch.setenv("RT_SPIN_CAP", "0")
+    with pkg.Scene.from_xml(xml, device=0) as s:
+        with pytest.raises(pkg.RtError) as ei:
+            s.render(s.camera(0), aa=1)
+        assert ei.value.code == -6
+        assert "spin_cap" in str(ei.value)
+        s.check()                                  # the error word was cleared by the failing call
+    monkeypatch.delenv("RT_SPIN_CAP")
+    with pkg.Scene.from_xml(xml, device=0) as s:
+        img = s.render(s.camera(0), aa=1)
+        s.check()
+    assert np.array_equal(img, load_golden_image(g["cameras"][0]))

@@ -7,7 +7,8 @@
                          WRITE_SIZE (MI355X_MICROARCH.md §HBM: FETCH_SIZE tallies 128-B requests at
                          64 B on gfx950) summed the same way
   TAG_bench.jsonl        the bench JSON lines of the same build (--trace line, then the full line)
-Also writes profiles/traffic.json (the file bench.py reads for `roofline.hbm`).
+Also writes profiles/traffic_{batched,one_frame}.json (the files bench.py reads for `roofline.hbm`, by the
+line's mode).
 Counting-pass kernels (k_*<true>) are excluded; the untemplated kernels they share (k_pack_*, k_finish)
 are charged their counting-pass calls at the average duration.
 
@@ -78,16 +79,35 @@ for k in frame_kernels:
         per_kernel_bytes[k] = b / frames
         hbm += b
 hbm /= frames
-res = {"tag": tag, "config": trace.get("config", {}).get("workload"), "path": trace.get("roofline", {}).get("path"),
+# each kernel's ALGORITHMIC bytes per frame (the line's counting pass, bench.py kernel_bytes) beside its
+# rocprof time and HBM bytes, so every per-kernel fraction can be recomputed from this file
+rl = trace.get("roofline", {})
+kb = dict(rl.get("alg_bytes_per_kernel") or {})
+if kb:
+    kb["k_occlude"] = kb.pop("k_occlude_a", 0) + kb.pop("k_occlude_b", 0)
+peak = (rl.get("peak_measured") or {}).get("l2_line_gbps")
+per_kernel_roofline = {}
+for k, b in kb.items():
+    t = per_kernel_ms.get(k)
+    gbps = b / (t / 1e3) / 1e9 if t else None
+    per_kernel_roofline[k] = {"alg_bytes_per_frame": b, "ms_per_frame_rocprof": t,
+                              "achieved_gbps": round(gbps, 1) if gbps else None,
+                              "frac_of_l2_line_peak": round(gbps / peak, 4) if gbps and peak else None,
+                              "hbm_bytes_per_frame": per_kernel_bytes.get(k)}
+mode = "batched" if (trace.get("config", {}).get("frames_in_flight") or 1) > 1 else "one_frame"
+res = {"tag": tag, "mode": mode, "config": trace.get("config", {}).get("workload"), "path": trace.get("roofline", {}).get("path"),
        "frames": frames, "workspace_slots": trace.get("config", {}).get("workspace_slots"),
        "frames_in_flight": trace.get("config", {}).get("frames_in_flight"),
        "kernel_ms_per_frame_rocprof": kernel_ms_sum, "per_kernel_ms_per_frame": per_kernel_ms,
        "kernel_ms_bench_trace": trace.get("roofline", {}).get("kernel_ms"),
        "hbm_bytes_per_frame": hbm, "per_kernel_hbm_bytes_per_frame": per_kernel_bytes,
+       "alg_bytes_per_frame": sum(kb.values()) if kb else None,
+       "l2_line_peak_gbps": peak, "per_kernel_roofline": per_kernel_roofline,
        "note": "timed (non-counting) kernels only; per frame = run totals / (warmup + timed frames); "
-               "HBM bytes = 2*FETCH_SIZE + WRITE_SIZE"}
+               "HBM bytes = 2*FETCH_SIZE + WRITE_SIZE; alg bytes = the traced line's roofline.alg_bytes_per_kernel "
+               "(k_occlude = A's + B's shadow walks); achieved = alg bytes / rocprof ms"}
 (prof / f"{tag}_traffic.json").write_text(json.dumps(res, indent=1))
-(prof / "traffic.json").write_text(json.dumps(res, indent=1))
+(prof / f"traffic_{mode}.json").write_text(json.dumps(res, indent=1))
 with open(prof / f"{tag}_bench.jsonl", "w") as f:
     for l in (trace, full):
         if l:
