@@ -902,15 +902,16 @@ void build_shadow_tree(FlatBVH& out, int threads) {
             return dx * dy + dy * dz + dz * dx;
         }
     };
-    // binned SAH over leaf centroids; each tree leaf is one reference leaf
+    // binned SAH over leaf centroids; each tree leaf is one reference leaf.  The leaves themselves are
+    // partitioned in place (std::partition's swaps depend only on the predicate, so the order -- and
+    // with it the count split of equal centroids -- is what partitioning an index array gave, and the
+    // tree is bit-identical to it), so every pass reads them sequentially; a node's box and centroid
+    // box are one pass, the three axes' bins another.
     struct TNode { Box box; int left = -1, right = -1, axis = 0; int32_t info = 0, rec = -1; };
-    std::vector<int> idx(leaves.size());
-    for (size_t i = 0; i < idx.size(); ++i) idx[i] = (int)i;
-    // Subtrees are independent (disjoint ranges of idx): the top levels are
+    // Subtrees are independent (disjoint ranges of the leaf array): the top levels are
     // built as concurrent tasks into their own node pools, spliced afterwards.
     struct Sah {
-        const std::vector<Leaf>& leaves;
-        std::vector<int>& idx;
+        std::vector<Leaf>& lv;
         int fork;
         std::vector<TNode> tn;
         int smax_depth = 0;
@@ -918,56 +919,65 @@ void build_shadow_tree(FlatBVH& out, int threads) {
         int build(int b, int e, int depth) { return fn(*this, b, e, depth); }
     };
     auto sah_build = [](Sah& me_, int b, int e, int depth) -> int {
-        const std::vector<Leaf>& leaves = me_.leaves;
-        std::vector<int>& idx = me_.idx;
+        std::vector<Leaf>& lv = me_.lv;
         std::vector<TNode>& tn = me_.tn;
         TNode node;
-        for (int i = b; i < e; ++i) node.box.grow(leaves[idx[i]].lo, leaves[idx[i]].hi);
+        Box cb;
+        for (int i = b; i < e; ++i) {
+            node.box.grow(lv[i].lo, lv[i].hi);
+            cb.grow(lv[i].c, lv[i].c);
+        }
         me_.smax_depth = std::max(me_.smax_depth, depth);
         const int me = (int)tn.size();
         tn.push_back(node);
         if (e - b == 1) {
-            tn[me].info = leaves[idx[b]].info;
-            tn[me].rec = leaves[idx[b]].rec;
+            tn[me].info = lv[b].info;
+            tn[me].rec = lv[b].rec;
             return me;
         }
-        Box cb;
-        for (int i = b; i < e; ++i) cb.grow(leaves[idx[i]].c, leaves[idx[i]].c);
         constexpr int kMaxBins = 32;
         const int kBins = std::min(kMaxBins, e - b);   // O(n) per node: small nodes use fewer bins
         double best = 1e300;
         int best_axis = -1, best_split = 0;
+        // only the kBins bins in use are initialised (most nodes are small)
+        alignas(Box) unsigned char bb_raw[3 * kMaxBins * sizeof(Box)];
+        Box* const bb = reinterpret_cast<Box*>(bb_raw);
+        int cnt[3][kMaxBins];
+        double ext[3];
+        bool live[3];
         for (int a = 0; a < 3; ++a) {
-            const double ext = (double)cb.hi[a] - cb.lo[a];
-            if (!(ext > 0)) continue;
-            // only the kBins bins in use are initialised (most nodes are small: 32 default-constructed
-            // boxes per axis were most of the build's time)
-            alignas(Box) unsigned char bb_raw[kMaxBins * sizeof(Box)];
-            Box* const bb = reinterpret_cast<Box*>(bb_raw);
-            int cnt[kMaxBins];
-            for (int k = 0; k < kBins; ++k) { new (&bb[k]) Box(); cnt[k] = 0; }
-            for (int i = b; i < e; ++i) {
-                const Leaf& l = leaves[idx[i]];
-                int k = (int)((l.c[a] - cb.lo[a]) / ext * kBins);
+            ext[a] = (double)cb.hi[a] - cb.lo[a];
+            live[a] = ext[a] > 0;
+            for (int k = 0; k < kBins; ++k) { new (&bb[a * kMaxBins + k]) Box(); cnt[a][k] = 0; }
+        }
+        for (int i = b; i < e; ++i) {
+            const Leaf& l = lv[i];
+            for (int a = 0; a < 3; ++a) {
+                if (!live[a]) continue;
+                int k = (int)((l.c[a] - cb.lo[a]) / ext[a] * kBins);
                 k = std::min(kBins - 1, std::max(0, k));
-                bb[k].grow(l.lo, l.hi);
-                cnt[k]++;
+                bb[a * kMaxBins + k].grow(l.lo, l.hi);
+                cnt[a][k]++;
             }
+        }
+        for (int a = 0; a < 3; ++a) {
+            if (!live[a]) continue;
+            const Box* const ba = bb + a * kMaxBins;
             double right_area[kMaxBins];
             int right_cnt[kMaxBins];
             Box acc;
             int n = 0;
             for (int k = kBins - 1; k > 0; --k) {
-                if (cnt[k]) acc.grow(bb[k].lo, bb[k].hi);
-                n += cnt[k];
+                if (cnt[a][k]) acc.grow(ba[k].lo, ba[k].hi);
+                n += cnt[a][k];
                 right_area[k] = acc.area();
                 right_cnt[k] = n;
             }
             Box lacc;
             int ln = 0;
             for (int k = 1; k < kBins; ++k) {
-                if (cnt[k - 1]) lacc.grow(bb[k - 1].lo, bb[k - 1].hi);
-                ln += cnt[k - 1];
+                if (cnt[a][k - 1]) lacc.grow(ba[k - 1].lo, ba[k - 1].hi);
+                ln += cnt[a][k - 1];
                 if (ln == 0 || right_cnt[k] == 0) continue;
                 const double cost = lacc.area() * ln + right_area[k] * right_cnt[k];
                 if (cost < best) { best = cost; best_axis = a; best_split = k; }
@@ -979,18 +989,19 @@ void build_shadow_tree(FlatBVH& out, int threads) {
             axis = 0;
             mid = (b + e) / 2;
         } else {
-            const double ext = (double)cb.hi[axis] - cb.lo[axis];
-            auto it = std::partition(idx.begin() + b, idx.begin() + e, [&](int i) {
-                int k = (int)((leaves[i].c[axis] - cb.lo[axis]) / ext * kBins);
+            const double ex = ext[axis];
+            const float lo_a = cb.lo[axis];
+            auto it = std::partition(lv.begin() + b, lv.begin() + e, [&](const Leaf& l) {
+                int k = (int)((l.c[axis] - lo_a) / ex * kBins);
                 k = std::min(kBins - 1, std::max(0, k));
                 return k < best_split;
             });
-            mid = (int)(it - idx.begin());
+            mid = (int)(it - lv.begin());
             if (mid == b || mid == e) mid = (b + e) / 2;
         }
         int l, r;
-        if (depth < me_.fork) {
-            Sah lb{leaves, idx, me_.fork, {}, 0, me_.fn}, rb{leaves, idx, me_.fork, {}, 0, me_.fn};
+        if (depth < me_.fork && std::min(mid - b, e - mid) >= 512) {
+            Sah lb{lv, me_.fork, {}, 0, me_.fn}, rb{lv, me_.fork, {}, 0, me_.fn};
             lb.tn.reserve(2 * (size_t)(mid - b));       // one allocation per pool (page faults are costly)
             rb.tn.reserve(2 * (size_t)(e - mid));
             auto fr = std::async(std::launch::async, [&, mid, e, depth] { return rb.build(mid, e, depth + 1); });
@@ -1008,7 +1019,7 @@ void build_shadow_tree(FlatBVH& out, int threads) {
         tn[me].axis = axis;
         return me;
     };
-    Sah top{leaves, idx, fork_depth(threads), {}, 0, +sah_build};
+    Sah top{leaves, fork_depth(threads), {}, 0, +sah_build};
     top.tn.reserve(2 * leaves.size());
     const int root = top.build(0, (int)leaves.size(), 0);
     std::vector<TNode> tn = std::move(top.tn);
