@@ -33,7 +33,7 @@
 extern "C" {
 #endif
 
-#define RT_ABI_VERSION 9
+#define RT_ABI_VERSION 10
 
 typedef enum rt_status {
     RT_OK = 0,
@@ -129,6 +129,11 @@ typedef struct rt_bvh_info {
     uint64_t occ_wide_bytes;     /* occlusion wide tree (any hit)                      */
     uint64_t leaf_record_bytes;  /* leaf records: exact leaf box + primitive copies    */
     uint64_t tri_shade_bytes;    /* per-triangle normal + material (hit epilogues)     */
+    /* scene creation phases, host wall ms (ABI 10): XML read + parse (0 for
+     * rt_scene_create), triangle normals/centres, flatten (device layout, leaf
+     * records, child pairs), reference-order wide tree, occlusion tree (built
+     * concurrently with the wide tree when threads allow), device upload */
+    double xml_ms, prep_ms, flat_ms, refwide_ms, stree_ms, upload_ms;
 } rt_bvh_info;
 
 /* ---- errors / devices ---- */

@@ -73,7 +73,9 @@ class BvhInfo(ctypes.Structure):
                 ("ref_ms", ctypes.c_double), ("wide_ms", ctypes.c_double), ("build_threads", ctypes.c_int),
                 ("wide_nodes", ctypes.c_int), ("wide_hash", ctypes.c_uint64),
                 ("ref_wide_bytes", ctypes.c_uint64), ("occ_wide_bytes", ctypes.c_uint64),
-                ("leaf_record_bytes", ctypes.c_uint64), ("tri_shade_bytes", ctypes.c_uint64)]
+                ("leaf_record_bytes", ctypes.c_uint64), ("tri_shade_bytes", ctypes.c_uint64),
+                ("xml_ms", ctypes.c_double), ("prep_ms", ctypes.c_double), ("flat_ms", ctypes.c_double),
+                ("refwide_ms", ctypes.c_double), ("stree_ms", ctypes.c_double), ("upload_ms", ctypes.c_double)]
 
     def as_dict(self) -> dict:
         return {k: getattr(self, k) for k, _ in self._fields_}

@@ -560,27 +560,26 @@ inline float ibits(int32_t i) { float f; std::memcpy(&f, &i, 4); return f; }
 // fp16 value <= / >= x (x >= 0, finite, < 65504 for up), normal or zero
 // (offsets below the smallest normal go to 0 / 2^-14, so no decode depends on
 // the device's fp16 denormal mode).  Values are returned as floats (exact).
+// (Bit arithmetic; the same values as the ldexp / frexp / floor / ceil definitions: for a normal double
+// x in [2^E, 2^(E+1)) the fp16 mantissa of floor(x) on the 2^(E-10) grid is its top 10 mantissa bits.)
 float h16_value(uint16_t b) {
-    const int ex = (b >> 10) & 31, man = b & 1023;
-    return ex == 0 ? std::ldexp((float)man, -24) : std::ldexp((float)(1024 + man), ex - 25);
+    const uint32_t ex = (b >> 10) & 31u, man = b & 1023u;
+    return ex == 0 ? (float)man * 0x1p-24f : ibits((int32_t)(((ex - 15u + 127u) << 23) | (man << 13)));
 }
+inline uint64_t dbits(double x) { uint64_t u; std::memcpy(&u, &x, 8); return u; }
 uint16_t h16_down(double x) {
     if (!(x >= 0x1p-14)) return 0;
     if (x >= 65504.0) return 0x7bff;
-    int e;
-    std::frexp(x, &e);                                   // x in [2^(e-1), 2^e)
-    const double step = std::ldexp(1.0, e - 11);
-    const int m = (int)std::floor(x / step);             // [1024, 2047]
-    return (uint16_t)(((e - 1 + 15) << 10) | (m - 1024));
+    const uint64_t u = dbits(x);
+    const int E = (int)((u >> 52) & 0x7ff) - 1023;        // x in [2^E, 2^(E+1)), E in [-14, 15]
+    return (uint16_t)(((E + 15) << 10) | (int)((u >> 42) & 1023u));
 }
 uint16_t h16_up(double x) {
     if (!(x > 0.0)) return 0;
     if (x <= 0x1p-14) return (uint16_t)(1 << 10);       // smallest normal
-    int e;
-    std::frexp(x, &e);
-    const double step = std::ldexp(1.0, e - 11);
-    int m = (int)std::ceil(x / step);                    // [1024, 2048]
-    int ex = e - 1 + 15;
+    const uint64_t u = dbits(x);
+    int ex = (int)((u >> 52) & 0x7ff) - 1023 + 15;
+    int m = 1024 + (int)((u >> 42) & 1023u) + ((u & ((uint64_t(1) << 42) - 1)) != 0 ? 1 : 0);   // [1024, 2048]
     if (m == 2048) { m = 1024; ++ex; }
     if (ex >= 31) return 0x7bff;                         // caller keeps offsets far below 65504
     return (uint16_t)((ex << 10) | (m - 1024));
@@ -832,6 +831,7 @@ std::string build_bvh(const HostScene& s, FlatBVH& out, int threads) {
     // independent: both read the pairs and leaf records, each writes only its own fields.
     const auto t1 = std::chrono::steady_clock::now();
     double stree_ms = 0.0;
+    out.flat_ms = std::chrono::duration<double, std::milli>(t1 - t0).count() - out.ref_ms;
     auto shadow = [&out, &stree_ms] {
         const auto ts = std::chrono::steady_clock::now();
         build_shadow_tree(out, out.threads);
@@ -840,10 +840,9 @@ std::string build_bvh(const HostScene& s, FlatBVH& out, int threads) {
     std::future<void> fs;
     if (out.threads > 1 && out.pairs.size() >= 4096) fs = std::async(std::launch::async, shadow);   // large scenes
     if (!build_ref_wide(out) || out.lrec.empty()) out.wnodes.clear();
-    out.flat_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count() - out.ref_ms;
+    out.refwide_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t1).count();
     if (fs.valid()) fs.get(); else shadow();
     out.stree_ms = stree_ms;
-    (void)t1;
     // Ordered DFS pushes two children per interior pop: stack <= depth + 2.
     out.max_stack = out.max_depth + 2;
     if (out.max_stack > dl::kMaxStack) return "Error: BVH deeper than the device stack";

@@ -77,7 +77,9 @@ struct FlatBVH {
     int wmax_stack = 0;              // worst-case stack entries of a walk over them
     int leaves = 0, max_leaf = 0, max_depth = 0, max_stack = 0;
     double build_ms = 0;
-    double ref_ms = 0, flat_ms = 0, stree_ms = 0;
+    double ref_ms = 0, flat_ms = 0, stree_ms = 0, refwide_ms = 0;   // phases: reference tree, flatten (layout,
+                                                                    // leaf records, pairs), occlusion tree,
+                                                                    // reference-order wide tree
     int threads = 1;                 // host threads the build used   // phases of build_ms: reference tree, flatten, wide trees
 };
 

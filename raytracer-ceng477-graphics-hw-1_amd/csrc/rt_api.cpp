@@ -163,6 +163,7 @@ struct rt_scene {
     long long kt_launches = 0;
     rtc::KTimer kt;
     size_t slot_budget() const { return ws_budget / (size_t)std::max(1, std::min(tune_slots, kSlots)); }
+    double xml_ms = 0, prep_ms = 0, upload_ms = 0;   // scene creation phases (rt_scene_bvh_info)
     bool warned_budget = false;    // one row unit alone exceeds the slot budget (chain_launch_units): told once
     std::string trace_file;     // RT_TRACE: dump per-sample wall-clock timings after each render (diagnostics)
     unsigned* d_trace = nullptr;
@@ -242,22 +243,33 @@ int select_device(const rt_options* opts, int* dev) {
 
 int upload_scene(rt_scene* s, const rt_options* opts);
 
+double ms_since(std::chrono::steady_clock::time_point t) {
+    return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t).count();
+}
+
 int finish_scene(rt_scene* s, const rt_options* opts) {
+    auto t = std::chrono::steady_clock::now();
     rtx::prepare_triangles(s->host);
+    s->prep_ms = ms_since(t);
     std::string err = rtx::build_bvh(s->host, s->bvh, opts ? opts->build_threads : 0);
     if (!err.empty()) return fail(RT_ERR_LIMIT, err);
     s->host_only = opts && (opts->flags & RT_OPT_HOST_ONLY);
     s->opt_flags = opts ? opts->flags : 0;
     if (s->host_only) return RT_OK;
     const int ndev = g_devices.load();
+    t = std::chrono::steady_clock::now();
     if (ndev >= 1) {                      // device group: the primary on device 0, replicas on 1..n-1
         rt_options o = opts ? *opts : rt_options{0, 0, 0};
         o.device = 0;
         int rc = upload_scene(s, &o);
         if (rc) return rc;
-        return rt_internal_group_create(s, ndev, &s->group);
+        rc = rt_internal_group_create(s, ndev, &s->group);
+        s->upload_ms = ms_since(t);
+        return rc;
     }
-    return upload_scene(s, opts);
+    const int rc = upload_scene(s, opts);
+    s->upload_ms = ms_since(t);
+    return rc;
 }
 
 // Device copies of a built scene (s->host, s->bvh) on opts->device, plus the
@@ -954,7 +966,9 @@ int rt_scene_load_xml(const char* path, const rt_options* opts, rt_scene** out) 
     *out = nullptr;
     rt_scene* s = new (std::nothrow) rt_scene();
     if (!s) return fail(RT_ERR_ARG, "out of host memory");
+    const auto t = std::chrono::steady_clock::now();
     std::string err = rtx::load_xml(path, s->host, opts ? opts->build_threads : 0);
+    s->xml_ms = ms_since(t);
     if (!err.empty()) {
         delete s;
         return fail(err.find("cannot be loaded") != std::string::npos ? RT_ERR_IO : RT_ERR_PARSE, err);
@@ -1000,6 +1014,12 @@ int rt_scene_bvh_info(const rt_scene* s, rt_bvh_info* info) {
     info->build_ms = s->bvh.build_ms;
     info->ref_ms = s->bvh.ref_ms;
     info->wide_ms = s->bvh.stree_ms;
+    info->xml_ms = s->xml_ms;
+    info->prep_ms = s->prep_ms;
+    info->flat_ms = s->bvh.flat_ms;
+    info->refwide_ms = s->bvh.refwide_ms;
+    info->stree_ms = s->bvh.stree_ms;
+    info->upload_ms = s->upload_ms;
     info->build_threads = s->bvh.threads;
     info->wide_nodes = (int)(s->bvh.swnodes.size() + s->bvh.wnodes.size());
     uint64_t h = 1469598103934665603ull;           // FNV-1a over the 4-wide tree's bytes
