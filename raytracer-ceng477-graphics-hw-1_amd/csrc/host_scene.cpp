@@ -390,6 +390,25 @@ int fork_depth(int threads) {
     return threads <= 1 ? 0 : d + 1;
 }
 
+// fn(i) for i in [0, n) on `threads` threads (contiguous chunks; fn must only write item i's outputs).
+template <class F>
+void parallel_for(int n, int threads, F&& fn) {
+    const int t = std::max(1, std::min(threads, n / 64));
+    if (t <= 1) {
+        for (int i = 0; i < n; ++i) fn(i);
+        return;
+    }
+    std::vector<std::thread> pool;
+    pool.reserve(t - 1);
+    auto run = [&](int k) {
+        const int b = (int)((long long)n * k / t), e = (int)((long long)n * (k + 1) / t);
+        for (int i = b; i < e; ++i) fn(i);
+    };
+    for (int k = 1; k < t; ++k) pool.emplace_back(run, k);
+    run(0);
+    for (auto& th : pool) th.join();
+}
+
 template <class N>
 int splice_pool(std::vector<N>& dst, std::vector<N>&& src, int root) {
     if (root < 0) return -1;
@@ -1056,48 +1075,69 @@ void build_shadow_tree(FlatBVH& out, int threads) {
     // child's box, all the any-hit argument needs): a node's slots are a
     // frontier below an SAH node, grown by replacing the interior slot of
     // largest box area by its two children.  Leaves are the shared leaf records.
+    // The shape (slots, child codes, pre-order node numbers) is one cheap serial
+    // recursion; the quantization of every node runs in parallel.
     out.swnodes.clear();
     out.swmax_stack = 0;
     bool contain_ok = !out.lrec.empty();
+    struct Shape { int n = 0; int ch[dl::kWideSlots]; int32_t code[dl::kWideSlots]; };
+    std::vector<Shape> shapes;
+    shapes.reserve(leaves.size());
     // returns the node code; *stack = worst-case stack entries of a walk from here down
-    std::function<int32_t(int, int*)> emit = [&](int n, int* stack) -> int32_t {
+    std::function<int32_t(int, int*)> shape = [&](int n, int* stack) -> int32_t {
         const TNode& t = tn[n];
         *stack = 0;
         if (t.left < 0) {
             if (t.rec < 0) contain_ok = false;
             return dl::kLeafBit | t.rec;
         }
-        std::vector<int> ch{t.left, t.right};
-        while ((int)ch.size() < dl::kWideSlots) {
+        int ch[dl::kWideSlots] = {t.left, t.right};
+        int nch = 2;
+        while (nch < dl::kWideSlots) {
             int best = -1;
             double ba = -1.0;
-            for (size_t i = 0; i < ch.size(); ++i)
-                if (tn[ch[i]].left >= 0 && tn[ch[i]].box.area() > ba) { ba = tn[ch[i]].box.area(); best = (int)i; }
+            for (int i = 0; i < nch; ++i)
+                if (tn[ch[i]].left >= 0 && tn[ch[i]].box.area() > ba) { ba = tn[ch[i]].box.area(); best = i; }
             if (best < 0) break;
             const int c = ch[best];
+            for (int i = nch; i > best + 1; --i) ch[i] = ch[i - 1];
             ch[best] = tn[c].left;
-            ch.insert(ch.begin() + best + 1, tn[c].right);
+            ch[best + 1] = tn[c].right;
+            ++nch;
         }
-        const int me = (int)out.swnodes.size();
-        out.swnodes.emplace_back();
-        dl::Wide w{};
-        float lo[dl::kWideSlots][3] = {}, hi[dl::kWideSlots][3] = {};
+        const int me = (int)shapes.size();
+        shapes.emplace_back();
         int deepest = 0;
-        for (int i = 0; i < dl::kWideSlots; ++i) w.child[i] = INT32_MAX;
-        for (size_t i = 0; i < ch.size(); ++i) {
+        Shape sh;
+        sh.n = nch;
+        for (int i = 0; i < nch; ++i) {
             int st = 0;
-            w.child[i] = emit(ch[i], &st);
+            sh.ch[i] = ch[i];
+            sh.code[i] = shape(ch[i], &st);
             deepest = std::max(deepest, st);
-            for (int a = 0; a < 3; ++a) { lo[i][a] = tn[ch[i]].box.lo[a]; hi[i][a] = tn[ch[i]].box.hi[a]; }
         }
-        *stack = (int)ch.size() - 1 + deepest;        // a step pushes at most n - 1, then goes below one
-        if (!quantize_wide(lo, hi, (int)ch.size(), (1u << ch.size()) - 1u, w)) contain_ok = false;
-        out.swnodes[me] = w;
+        shapes[me] = sh;
+        *stack = nch - 1 + deepest;        // a step pushes at most n - 1, then goes below one
         return me;
     };
     int stack = 0;
-    out.swroot = emit(root, &stack);
+    out.swroot = shape(root, &stack);
     out.swmax_stack = stack + 1;
+    out.swnodes.resize(shapes.size());
+    std::vector<char> qok(shapes.size(), 1);
+    parallel_for((int)shapes.size(), threads, [&](int i) {
+        const Shape& sh = shapes[i];
+        dl::Wide w{};
+        float lo[dl::kWideSlots][3] = {}, hi[dl::kWideSlots][3] = {};
+        for (int j = 0; j < dl::kWideSlots; ++j) w.child[j] = INT32_MAX;
+        for (int j = 0; j < sh.n; ++j) {
+            w.child[j] = sh.code[j];
+            for (int a = 0; a < 3; ++a) { lo[j][a] = tn[sh.ch[j]].box.lo[a]; hi[j][a] = tn[sh.ch[j]].box.hi[a]; }
+        }
+        if (!quantize_wide(lo, hi, sh.n, (1u << sh.n) - 1u, w)) qok[i] = 0;
+        out.swnodes[i] = w;
+    });
+    for (char q : qok) contain_ok = contain_ok && q;
     if (!contain_ok || out.swmax_stack > dl::kMaxStack) out.swnodes.clear();   // binary occlusion tree only
 }
 
@@ -1135,47 +1175,88 @@ bool build_ref_wide(FlatBVH& out) {
         const double dx = (double)c.hi[0] - c.lo[0], dy = (double)c.hi[1] - c.lo[1], dz = (double)c.hi[2] - c.lo[2];
         return dx * dy + dy * dz + dz * dx;
     };
+    // expansion tree over slot ranges: split (axis, lo, mid, hi) cuts [lo, hi) at mid
+    struct Split { int axis, lo, mid, hi; };
+    // A node's shape: its slots, the splits that produced them and the child codes.  The shapes come
+    // from one serial recursion (pre-order node numbers); the rank words and quantization of every
+    // node run in parallel.
+    struct Shape { int n = 0; Slot fr[W]; Split sp[W]; int nsp = 0; int32_t code[W]; };
+    std::vector<Shape> shapes;
+    shapes.reserve(out.pairs.size() / 2 + 1);
     // returns the node index; *stack = worst-case stack entries of a walk from this node down
-    std::function<int32_t(int32_t, int*)> emit = [&](int32_t pi, int* stack) -> int32_t {
-        // expansion tree over slot ranges: split (axis, lo, mid, hi) cuts [lo, hi) at mid
-        struct Split { int axis, lo, mid, hi; };
-        std::vector<Slot> fr(2);
-        std::vector<Split> sp{{kids(pi, &fr[0], &fr[1]), 0, 1, 2}};
-        while ((int)fr.size() < W) {
+    std::function<int32_t(int32_t, int*)> shape = [&](int32_t pi, int* stack) -> int32_t {
+        Shape sh;
+        sh.n = 2;
+        sh.sp[0] = {kids(pi, &sh.fr[0], &sh.fr[1]), 0, 1, 2};
+        sh.nsp = 1;
+        while (sh.n < W) {
             int best = -1;
             double ba = -1.0;
-            for (size_t i = 0; i < fr.size(); ++i)
-                if (fr[i].info >= 0 && area(fr[i]) > ba) { ba = area(fr[i]); best = (int)i; }
+            for (int i = 0; i < sh.n; ++i)
+                if (sh.fr[i].info >= 0 && area(sh.fr[i]) > ba) { ba = area(sh.fr[i]); best = i; }
             if (best < 0) break;
             Slot a, b;
-            const int ax = kids(fr[best].info, &a, &b);
-            fr[best] = a;
-            fr.insert(fr.begin() + best + 1, b);
-            for (Split& e : sp) {
+            const int ax = kids(sh.fr[best].info, &a, &b);
+            for (int i = sh.n; i > best + 1; --i) sh.fr[i] = sh.fr[i - 1];
+            sh.fr[best] = a;
+            sh.fr[best + 1] = b;
+            ++sh.n;
+            for (int k = 0; k < sh.nsp; ++k) {
+                Split& e = sh.sp[k];
                 if (e.lo > best) e.lo++;
                 if (e.mid > best) e.mid++;
                 if (e.hi > best) e.hi++;
             }
-            sp.push_back({ax, best, best + 1, best + 2});
+            sh.sp[sh.nsp++] = {ax, best, best + 1, best + 2};
         }
-        const int n = (int)fr.size();
+        const int me = (int)shapes.size();
+        shapes.emplace_back();
+        int deepest = 0;
+        for (int i = 0; i < sh.n; ++i) {
+            if (sh.fr[i].info < 0) {
+                if (sh.fr[i].rec < 0) ok = false;
+                sh.code[i] = dl::kLeafBit | sh.fr[i].rec;
+            } else {
+                int st = 0;
+                sh.code[i] = shape(sh.fr[i].info, &st);
+                deepest = std::max(deepest, st);
+            }
+        }
+        shapes[me] = sh;
+        // a step pushes at most n - 1 entries, then continues below one of them
+        *stack = sh.n - 1 + deepest;
+        return me;
+    };
+    int stack = 0;
+    out.wroot = shape(out.root_info, &stack);
+    out.wmax_stack = stack + 1;
+    out.wnodes.resize(shapes.size());
+    std::vector<char> nok(shapes.size(), 1);
+    parallel_for((int)shapes.size(), out.threads, [&](int idx) {
+        const Shape& sh = shapes[idx];
+        const int n = sh.n;
+        bool good = true;
         dl::Wide w{};
         // ranks for the octants o = 0..3 (d[2] <= 0); an octant o >= 4 visits in the reverse order of o ^ 7
         for (int oct = 0; oct < 8; ++oct) {
             int order[dl::kWideSlots], no = 0;
-            std::function<void(int, int)> visit = [&](int lo, int hi) {
-                if (hi - lo == 1) { if (no < dl::kWideSlots) order[no++] = lo; return; }
-                for (const Split& e : sp)
-                    if (e.lo == lo && e.hi == hi) {
-                        const bool left_first = (oct >> e.axis) & 1;
-                        if (left_first) { visit(e.lo, e.mid); visit(e.mid, e.hi); }
-                        else { visit(e.mid, e.hi); visit(e.lo, e.mid); }
-                        return;
-                    }
-                ok = false;
-            };
-            visit(0, n);
-            if (no != n) ok = false;
+            // the DFS over the splits (left first iff d[axis] > 0), iteratively: a stack of slot ranges
+            int rs[2 * W][2], nr = 0;
+            rs[nr][0] = 0; rs[nr][1] = n; ++nr;
+            while (nr > 0) {
+                --nr;
+                const int lo = rs[nr][0], hi = rs[nr][1];
+                if (hi - lo == 1) { if (no < dl::kWideSlots) order[no++] = lo; continue; }
+                int k = 0;
+                while (k < sh.nsp && !(sh.sp[k].lo == lo && sh.sp[k].hi == hi)) ++k;
+                if (k == sh.nsp || nr + 2 > 2 * W) { good = false; break; }
+                const Split& e = sh.sp[k];
+                const bool left_first = (oct >> e.axis) & 1;
+                // pushed in reverse: the first visited range on top
+                if (left_first) { rs[nr][0] = e.mid; rs[nr][1] = e.hi; ++nr; rs[nr][0] = e.lo; rs[nr][1] = e.mid; ++nr; }
+                else { rs[nr][0] = e.lo; rs[nr][1] = e.mid; ++nr; rs[nr][0] = e.mid; rs[nr][1] = e.hi; ++nr; }
+            }
+            if (no != n) good = false;
             uint32_t rw = 0;
             for (int r = 0; r < no; ++r) rw |= (uint32_t)r << (3 * order[r]);
             for (int j = n; j < dl::kWideSlots; ++j) rw |= (uint32_t)(n - 1) << (3 * j);   // empty: never valid
@@ -1184,35 +1265,21 @@ bool build_ref_wide(FlatBVH& out) {
             } else {                        // check the reversal the device relies on (real slots)
                 const uint32_t all = 01111111u & ((1u << (3 * dl::kWideSlots)) - 1u);   // one per 3-bit field
                 const uint32_t real = (1u << (3 * n)) - 1u;
-                if ((rw & real) != (((uint32_t)(n - 1) * all - w.rank[oct ^ 7]) & real)) ok = false;
+                if ((rw & real) != (((uint32_t)(n - 1) * all - w.rank[oct ^ 7]) & real)) good = false;
             }
         }
-        const int me = (int)out.wnodes.size();
-        out.wnodes.emplace_back();
         float lo[dl::kWideSlots][3] = {}, hi[dl::kWideSlots][3] = {};
-        int deepest = 0;
         for (int i = 0; i < dl::kWideSlots; ++i) w.child[i] = INT32_MAX;
         for (int i = 0; i < n; ++i) {
-            std::memcpy(lo[i], fr[i].lo, sizeof(lo[i]));
-            std::memcpy(hi[i], fr[i].hi, sizeof(hi[i]));
-            if (fr[i].info < 0) {
-                if (fr[i].rec < 0) ok = false;
-                w.child[i] = dl::kLeafBit | fr[i].rec;
-            } else {
-                int st = 0;
-                w.child[i] = emit(fr[i].info, &st);
-                deepest = std::max(deepest, st);
-            }
+            std::memcpy(lo[i], sh.fr[i].lo, sizeof(lo[i]));
+            std::memcpy(hi[i], sh.fr[i].hi, sizeof(hi[i]));
+            w.child[i] = sh.code[i];
         }
-        // a step pushes at most n - 1 entries, then continues below one of them
-        *stack = n - 1 + deepest;
-        if (!quantize_wide(lo, hi, n, (1u << n) - 1u, w)) ok = false;
-        out.wnodes[me] = w;
-        return me;
-    };
-    int stack = 0;
-    out.wroot = emit(out.root_info, &stack);
-    out.wmax_stack = stack + 1;
+        if (!quantize_wide(lo, hi, n, (1u << n) - 1u, w)) good = false;
+        out.wnodes[idx] = w;
+        nok[idx] = good ? 1 : 0;
+    });
+    for (char g : nok) ok = ok && g;
     return ok && out.wmax_stack <= dl::kMaxStack;
 }
 

@@ -13,3 +13,4 @@ run() { local name=$1; shift; timeout -k 10 300 python3 bench.py "$@" > $OUT/$na
 run c3 --no-cpu-baseline && run c3_f1 --inflight 1 --steps 32 --warmup 3 --no-cpu-baseline \
   && run ms --config MS --steps 96 --no-cpu-baseline && run ms_f1 --config MS --inflight 1 --steps 32 --warmup 3 --no-cpu-baseline \
   && run mb --config MB --steps 96 --no-cpu-baseline && run mb_f1 --config MB --inflight 1 --steps 32 --warmup 3 --no-cpu-baseline
+timeout -k 10 200 python3 tools/exp_scene_load.py C3_hm_1080p_d6 16,8,4,1 > $OUT/scene_load.json 2> $OUT/scene_load.err; echo "scene_load rc=$?"
