@@ -634,6 +634,207 @@ __device__ uint32_t bq_consume(const rtk::DevScene& s, const PcParams& p, WalkSt
     return n;
 }
 
+// ---------------------------------------------------------------------------
+// Cooperative tail walks (lone-frame phase B, p.coop).  Once a phase-B wave has no continuation left
+// to take and at most p.coop_live of its chains still walk, each walk runs on a GROUP of 8 lanes
+// (lanes 8g..8g+7): lane q tests slot q of the wide node (one slot's six planes instead of all 36),
+// a leaf record's primitives are tested one per lane, and the group's lanes agree through ballots.
+// The dependent-instruction chain of a wide step -- what sets the deep mirror chains' time when the
+// GPU is otherwise idle -- shrinks from ~250 to ~100 instructions.  The walk is the
+// same: the same slot order (each slot's rank in the reference's visiting order), the same pushes at
+// the same stack positions, the same pops, and the leaf's primitives folded in stored order with the
+// reference's update rule (raytracer.cpp:210-222), so the result is bit-identical.
+// The group keeps the walk's stack in its OWNER lane's LDS column, exactly where the owner's own
+// walk keeps it, so a walk moves between the owner (per-lane steps) and a group at any step with
+// only its registers: a group takes a walk whose stack is all in LDS (sp <= kLds) and hands it back
+// unchanged (before the step) when a step would push past the LDS entries (the deeper ones live in
+// the owner's private scratch).
+// ---------------------------------------------------------------------------
+struct CoopW {              // a group's walk (the same in its 8 lanes); its ray is in g_cray
+    int cur, sp, steps;
+    int owner;              // lane whose walk this is, or -1 (group free)
+    float tmax;
+    HitRec best;
+};
+__shared__ float g_cray[kBlock / 8][9];    // per group (wave * 8 + group): ray o, d, inv
+
+__device__ __forceinline__ Ray coop_ray() {
+    const float* a = g_cray[threadIdx.x >> 3];
+    Ray r;
+    r.o = V{a[0], a[1], a[2]};
+    r.d = V{a[3], a[4], a[5]};
+    r.inv = V{a[6], a[7], a[8]};
+    return r;
+}
+
+// One step of group walk c (every lane of the group calls it with the same c): 0 = continues,
+// 1 = finished (result in c.best), 2 = not taken: the step would push past the owner's LDS
+// entries, c unchanged (the owner walks on with its own stack).
+__device__ __forceinline__ int coop_step(const rtk::DevScene& s, CoopW& c) {
+    constexpr int W = dl::kWideSlots;
+    const int lane = lane_id(), q = lane & 7, gbase = lane & 56;
+    const int col = (int)(threadIdx.x & ~63u) + c.owner;       // the owner's LDS stack column
+    if (c.steps >= s.walk_cap) {                                // walk_runaway
+        __hip_atomic_fetch_or(s.err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        return 1;
+    }
+    if (c.cur >= 0) {
+        // lane q reads only what slot q needs from the node's line: the header, its six plane words,
+        // its child code and the rank word (one line per group per load instruction)
+        const uint32_t* N = reinterpret_cast<const uint32_t*>(&s.wnodes[c.cur]);
+        const Ray cr = coop_ray();
+        const int sgn = (cr.d.x > 0.0f ? 1 : 0) | (cr.d.y > 0.0f ? 2 : 0) | (cr.d.z > 0.0f ? 4 : 0);   // walk_begin's
+        const int ridx = (sgn & 4) ? (sgn ^ 7) : sgn;
+        const int qs = q < W ? q : W - 1, pr = qs >> 1;
+        const float4 hd = *reinterpret_cast<const float4*>(N);
+        uint32_t pl[6];
+#pragma unroll
+        for (int a = 0; a < 3; ++a) {
+            pl[a] = N[4 + a * 3 + pr];
+            pl[3 + a] = N[13 + a * 3 + pr];
+        }
+        const int code_q = (int)N[22 + qs];
+        uint32_t rw = N[28 + ridx];
+        const uint32_t ex = __float_as_uint(hd.w);
+        if (sgn & 4) rw = (uint32_t)(__builtin_popcount(ex >> 24) - 1) * 0111111u - rw;
+        // slot q's box (wide_slabs for one slot: the same operations on the same words)
+        const float org[3] = {hd.x, hd.y, hd.z};
+        const float ro[3] = {cr.o.x, cr.o.y, cr.o.z}, ri[3] = {cr.inv.x, cr.inv.y, cr.inv.z};
+        const uint32_t hs = (uint32_t)(q & 1) << 4;
+        float tmn = 0.0f, tmx = 0.0f;
+#pragma unroll
+        for (int a = 0; a < 3; ++a) {
+            const float sc = __uint_as_float(((ex >> (8 * a)) & 255u) << 23);
+            const bool neg = __float_as_int(ri[a]) < 0;
+            const float si = sc * ri[a];
+            const float z = org[a] - ro[a];
+            const float oi = z * ri[a];
+            const float cc = __builtin_fmaf(sc, 0x1p-5f, __builtin_fabsf(org[a]) * 0x1p-23f);
+            const float m = __builtin_fmaf(__builtin_fabsf(z), 6.0f * 0x1p-23f, cc);
+            const float M = __builtin_fmaf(m, __builtin_fabsf(ri[a]), 0x1p-126f);
+            const uint32_t lw = pl[a] >> hs, hw = pl[3 + a] >> hs;
+            const uint32_t nw = neg ? hw : lw, fw = neg ? lw : hw;
+            const float tn = fma_mix_h<0>(nw, si, oi - M), tf = fma_mix_h<0>(fw, si, oi + M);
+            tmn = a == 0 ? tn : __builtin_fmaxf(tmn, tn);
+            tmx = a == 0 ? tf : __builtin_fminf(tmx, tf);
+        }
+        const bool valid = q < W && tmx >= __builtin_fmaxf(0.0f, tmn) && tmn <= c.tmax;
+        const uint32_t m6 = (uint32_t)(__ballot(valid) >> gbase) & 63u;
+        uint32_t vm = 0;                                          // valid slots in rank order
+#pragma unroll
+        for (int j = 0; j < W; ++j) vm |= ((m6 >> j) & 1u) << ((rw >> (3 * j)) & 7u);
+        if (vm) {
+            const int np = __builtin_popcount(vm) - 1;
+            if (c.sp + np > StackLds::kLds) return 2;             // deeper entries: the owner's scratch
+            const uint32_t first = (uint32_t)__builtin_ctz(vm);
+            const uint32_t rq = (rw >> (3 * q)) & 7u;
+            const bool isfirst = valid && rq == first;
+            const int cf = __builtin_ctz((uint32_t)(__ballot(isfirst) >> gbase) & 63u);
+            if (valid && !isfirst)                                // the same entry at the same position
+                g_lstk[(c.sp + __builtin_popcount(vm >> (rq + 1u))) * kBlock + col] =
+                    make_int2(code_q, __float_as_int(tmn));
+            c.sp += np;
+            c.cur = __shfl(code_q, gbase + cf, 64);
+            ++c.steps;
+            return 0;
+        }
+    } else {
+        const float4* L = s.lrec + (c.cur & ~dl::kLeafBit);
+        const float4 h0 = L[0], h1 = L[1];
+        const Ray r = coop_ray();
+        float lt;
+        if (box_hit_fast(r, h0, h1, &lt) && lt <= c.tmax) {      // the reference leaf's exact box (:184)
+            const int cnt = __float_as_int(h0.w), slot0 = __float_as_int(h1.w);
+            for (int b0 = 0; b0 < cnt; b0 += 8) {
+                const int j = b0 + q;
+                bool h = false;
+                float t = 0.0f;
+                if (j < cnt) {
+                    const float4 p0 = L[2 + 3 * j], p1 = L[3 + 3 * j], p2 = L[4 + 3 * j];
+                    h = __float_as_int(p0.w) >= 0 ? tri_hit(r, p0, p1, p2, &t) : sphere_hit(r, p0, p1, &t);
+                }
+                // the hits in stored order, with the reference's update rule (:213-221)
+                uint32_t hm = (uint32_t)(__ballot(h) >> gbase) & 255u;
+                while (hm) {
+                    const int jj = __builtin_ctz(hm);
+                    hm &= hm - 1u;
+                    const float tj = __shfl(t, gbase + jj, 64);
+                    if (tj < c.best.t || c.best.t == -1.0f) {
+                        c.best.t = tj;
+                        c.best.prim = slot0 + b0 + jj;
+                        c.tmax = tj;
+                    }
+                }
+            }
+        }
+    }
+    ++c.steps;
+    while (c.sp > 0) {
+        --c.sp;
+        const int2 e = g_lstk[c.sp * kBlock + col];
+        if (__int_as_float(e.y) <= c.tmax) {
+            c.cur = e.x;
+            return 0;
+        }
+    }
+    return 1;
+}
+
+// A wave in coop mode: free groups take the walks of candidate lanes (their stacks all in LDS),
+// every group steps its walk, and finished or handed-back walks return to their owners.
+// st: the owner's lane state (kCoop while a group has its walk); cg: the leader lane of that group.
+constexpr int kCoop = 3;
+__device__ __forceinline__ void coop_round(const rtk::DevScene& s, CoopW& c, int& st, int& cg, bool& coop_ok,
+                                           const Ray& r, Walk& wk) {
+    const int lane = lane_id();
+    // (1) assign: the i-th candidate walk to the i-th free group
+    unsigned long long cand = __ballot(st == kTrav && coop_ok && wk.sp <= StackLds::kLds);
+    unsigned long long freeg = __ballot(c.owner < 0 && (lane & 7) == 0);
+    unsigned long long fresh = 0;     // leader lanes of groups that took a walk now
+    while (cand && freeg) {
+        const int o = __builtin_ctzll(cand), gl = __builtin_ctzll(freeg);
+        cand &= cand - 1ull;
+        freeg &= freeg - 1ull;
+        fresh |= 1ull << gl;
+        if ((lane & 56) == gl) c.owner = o;
+        if (lane == o) { st = kCoop; cg = gl; }
+    }
+    if (fresh) {
+        if (st == kCoop && ((fresh >> cg) & 1ull)) {     // the owner puts its ray where its group reads it
+            float* a = g_cray[((threadIdx.x & ~63u) + (unsigned)cg) >> 3];
+            a[0] = r.o.x; a[1] = r.o.y; a[2] = r.o.z;
+            a[3] = r.d.x; a[4] = r.d.y; a[5] = r.d.z;
+            a[6] = r.inv.x; a[7] = r.inv.y; a[8] = r.inv.z;
+        }
+        const int src = c.owner >= 0 ? c.owner : lane;
+        const bool f = (fresh >> (lane & 56)) & 1ull;
+        auto take = [&](auto& dst, auto v) { const auto x = __shfl(v, src, 64); if (f) dst = x; };
+        take(c.cur, wk.cur); take(c.sp, wk.sp); take(c.steps, wk.steps);
+        take(c.tmax, wk.tmax); take(c.best.t, wk.best.t); take(c.best.prim, wk.best.prim);
+    }
+    // (2) step every group's walk (a walk not taken, 2, stays as it was: the owner redoes the step)
+    const int res = c.owner >= 0 ? coop_step(s, c) : 0;
+    // (3) finished (1) or handed back (2): the walk's registers return to its owner lane
+    const unsigned long long ended = __ballot(res != 0 && (lane & 7) == 0);
+    if (ended) {
+        const int src = st == kCoop ? cg : lane;
+        const bool mine = st == kCoop && ((ended >> cg) & 1ull);
+        auto give = [&](auto& dst, auto v) { const auto x = __shfl(v, src, 64); if (mine) dst = x; };
+        const int rs = __shfl(res, src, 64);
+        give(wk.cur, c.cur); give(wk.sp, c.sp); give(wk.steps, c.steps);
+        give(wk.tmax, c.tmax); give(wk.best.t, c.best.t); give(wk.best.prim, c.best.prim);
+        if (mine) {
+            if (rs == 1) {
+                st = kDone;
+            } else {
+                st = kTrav;           // per-lane from here (this walk's stack grows into scratch)
+                coop_ok = false;
+            }
+        }
+        if ((ended >> (lane & 56)) & 1ull) c.owner = -1;
+    }
+}
+
 // The u-th unit taken -> the unit id.  The slab's rows of units (tiles_x / 4 units each) are cut
 // into super-rows of ublk_h tile rows (< 0: one frame of the batch), each walked in column blocks
 // ublk_w units wide, so the units in flight (a launch-wide counter: the whole GPU on them at once)
@@ -681,6 +882,13 @@ __device__ void chain_body(const rtk::DevScene& s, const rtk::Eye& e, const PcPa
     unsigned t_grab = 0, tsteps = 0, twit = 0, wit = 0;   // trace: grab time, own steps, wave steps
     bool fresh = false;      // lane just took an eye ray (packet walk pending)
     StepStat stat;
+    // cooperative tail walks (lone-frame phase B: coop_round): the group walk this lane works on, the
+    // leader lane of the group walking this lane's own walk, and whether that walk may go to a group
+    constexpr bool COOPK = CONT && BQ && !COUNT;
+    CoopW cw;
+    cw.owner = -1;
+    int cg = 0;
+    bool coop_ok = true;
     while (true) {
         // (1) epilogue of finished walks: record, queue shadow tasks, reflect or hand on
         if (st == kDone) {
@@ -768,6 +976,7 @@ __device__ void chain_body(const rtk::DevScene& s, const rtk::Eye& e, const PcPa
                     st = kIdle;
                 } else {
                     st = walk_begin<COUNT>(s, r, wk, w) ? kTrav : kDone;
+                    coop_ok = true;
                 }
             }
         }
@@ -819,6 +1028,7 @@ __device__ void chain_body(const rtk::DevScene& s, const rtk::Eye& e, const PcPa
                             nrefl++;
                             if (!COUNT && defer_closest(s, r)) fb_chain(p, lvp);
                             else st = walk_begin<COUNT>(s, r, wk, w) ? kTrav : kDone;
+                            coop_ok = true;
                         } else {
                             const unsigned idx = (dyn ? uid : blk + (v >> 8) * G) * 256u + (v & 255u);
                             if (slab_sample_ray(e, p, idx, &r)) {
@@ -857,10 +1067,20 @@ __device__ void chain_body(const rtk::DevScene& s, const rtk::Eye& e, const PcPa
         // (3) walk until enough lanes need service
         const int thresh = exhausted ? 0 : (CONT ? p.brefill : p.refill);
         while (true) {
-            const int nt = __popcll(__ballot(st == kTrav));
+            const int nt = __popcll(__ballot(st == kTrav || (COOPK && st == kCoop)));
+            const bool tail = COOPK && p.coop && exhausted && nt <= p.coop_live;
             if (nt <= thresh ||
-                __popcll(__ballot(st == kDone)) >= (CONT ? (exhausted ? p.btail : p.bservice) : p.service))
+                __popcll(__ballot(st == kDone)) >= (tail ? p.coop_tail : CONT ? (exhausted ? p.btail : p.bservice) : p.service))
                 break;
+            if constexpr (COOPK) {
+                if (tail) {          // the wave's last chains: each walk on a group of 8 lanes
+                    coop_round(s, cw, st, cg, coop_ok, r, wk);
+                    if (__any(st == kTrav))      // walks whose stacks reach into scratch: per lane
+                        if (st == kTrav && (closest_step_timed<COUNT, CONT>(s, r, stk, wk, w) || walk_runaway(s, wk)))
+                            st = kDone;
+                    continue;
+                }
+            }
             stat.step(st == kTrav, wk.cur >= 0, RT_STEP_STATS && st == kTrav && wk.tree == nullptr && leaf_postponed(s.leaf_wait, wk));
             if (CONT && p.trace) ++wit;
             if (st == kTrav) {

@@ -135,6 +135,9 @@ struct PcParams {
     int bservice;     // the same for phase-B chains
     int btail;        // phase-B chains once no continuation is left to take: service at this many done lanes
     int bq_cap;       // phase-B workgroup shadow queue slots in use (<= kBq; 0: every task to k_occlude)
+    int coop;         // lone-frame phase B: once a wave has no continuation left and <= coop_live chains walk,
+    int coop_live;    // each walk runs on a group of 8 lanes (one wide-node slot per lane; coop_step);
+    int coop_tail;    // ... and a wave services its finished walks once this many are done (0: coop off)
     int spread;       // tiles interleaved per wave within a 256-sample unit (1, 2 or 4)
     int dyn_units;    // > 0: phase-A waves take 256-sample units from a launch-wide counter (totals[3]),
                       // at most this many per workgroup; 0: static per-workgroup interleave

@@ -143,6 +143,9 @@ struct rt_scene {
     int tune_gb = 0;            // RT_GB: phase-B chain workgroups in k_mix (0: 1.875 per CU for a lone frame, 1 for batches)
     int tune_bq_cap = 1 << 30;  // RT_BQ_CAP: phase-B shadow queue slots (tests force the k_occlude spill path)
     int tune_bservice = 64;     // RT_BSERVICE: phase-B waves service finished walks once this many lanes are done
+    int tune_coop = 1;          // RT_COOP: lone-frame phase B walks its tail chains on 8-lane groups (pathchain.hip coop_step)
+    int tune_coop_live = 8;     // RT_COOP_LIVE: ... once at most this many chains of the wave walk (<= 8)
+    int tune_coop_tail = 1;     // RT_COOP_TAIL: ... servicing finished walks once this many are done
     int tune_btail = 64;        // RT_BTAIL: the same once the continuations are exhausted (1: 1.24, 4: 1.18, 16: 1.15, 64: 1.14 ms)
     int tune_dyn = 1;           // RT_DYN_UNITS: phase-A waves take sample units from a launch-wide counter
     int tune_ublk_h = -1, tune_ublk_w = 8;  // RT_UBLK_H / RT_UBLK_W: phase-A unit column blocks (unit_order;
@@ -367,6 +370,9 @@ int upload_scene(rt_scene* s, const rt_options* opts) {
     if (const char* e = std::getenv("RT_BQ_CAP")) s->tune_bq_cap = std::max(0, std::atoi(e));
     if (const char* e = std::getenv("RT_BSERVICE")) s->tune_bservice = std::max(1, std::min(64, std::atoi(e)));
     if (const char* e = std::getenv("RT_BTAIL")) s->tune_btail = std::max(1, std::min(64, std::atoi(e)));
+    if (const char* e = std::getenv("RT_COOP")) s->tune_coop = std::atoi(e) != 0;
+    if (const char* e = std::getenv("RT_COOP_LIVE")) s->tune_coop_live = std::max(1, std::min(8, std::atoi(e)));
+    if (const char* e = std::getenv("RT_COOP_TAIL")) s->tune_coop_tail = std::max(1, std::min(64, std::atoi(e)));
     if (const char* e = std::getenv("RT_SPLIT")) s->tune_split = std::max(1, std::atoi(e));
     if (const char* e = std::getenv("RT_DYN_UNITS")) s->tune_dyn = std::atoi(e) != 0;
     if (const char* e = std::getenv("RT_UBLK_H")) s->tune_ublk_h = std::max(-1, std::atoi(e));
@@ -825,6 +831,9 @@ int render_chain(rt_scene* s, const rtk::Eye& eye, const rtk::FrameParams& f, bo
     p.bservice = s->tune_bservice;
     p.btail = s->tune_btail;
     p.bq_cap = std::min(s->tune_bq_cap, rtc::kMaxBq);
+    p.coop = s->tune_coop;
+    p.coop_live = s->tune_coop_live;
+    p.coop_tail = s->tune_coop_tail;
     p.producers = s->tune_producers;
     p.orefill = s->tune_orefill;
     p.brefill = s->tune_brefill;
