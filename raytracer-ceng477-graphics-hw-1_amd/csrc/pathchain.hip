@@ -650,6 +650,9 @@ __device__ uint32_t bq_consume(const rtk::DevScene& s, const PcParams& p, WalkSt
 // unchanged (before the step) when a step would push past the LDS entries (the deeper ones live in
 // the owner's private scratch).
 // ---------------------------------------------------------------------------
+#ifndef RT_COOP_BUILD
+#define RT_COOP_BUILD 1      // 0: k_mix without the cooperative tail walks (A/B builds)
+#endif
 struct CoopW {              // a group's walk (the same in its 8 lanes); its ray is in g_cray
     int cur, sp, steps;
     int owner;              // lane whose walk this is, or -1 (group free)
@@ -884,7 +887,7 @@ __device__ void chain_body(const rtk::DevScene& s, const rtk::Eye& e, const PcPa
     StepStat stat;
     // cooperative tail walks (lone-frame phase B: coop_round): the group walk this lane works on, the
     // leader lane of the group walking this lane's own walk, and whether that walk may go to a group
-    constexpr bool COOPK = CONT && BQ && !COUNT;
+    constexpr bool COOPK = RT_COOP_BUILD && CONT && BQ && !COUNT;
     CoopW cw;
     cw.owner = -1;
     int cg = 0;
@@ -1074,6 +1077,7 @@ __device__ void chain_body(const rtk::DevScene& s, const rtk::Eye& e, const PcPa
                 break;
             if constexpr (COOPK) {
                 if (tail) {          // the wave's last chains: each walk on a group of 8 lanes
+                    if (p.trace) { ++wit; tsteps |= 1u << 31; }      // trace: coop rounds count as wave iterations
                     coop_round(s, cw, st, cg, coop_ok, r, wk);
                     if (__any(st == kTrav))      // walks whose stacks reach into scratch: per lane
                         if (st == kTrav && (closest_step_timed<COUNT, CONT>(s, r, stk, wk, w) || walk_runaway(s, wk)))

@@ -901,15 +901,19 @@ int render_chain(rt_scene* s, const rtk::Eye& eye, const rtk::FrameParams& f, bo
 // The device error word after the device is idle: RT_ERR_LIMIT (and the word
 // cleared) when a walk was cut off by walk_runaway (bit 0) or a wait loop by
 // spin_over (bit 1) since the last check.
+int device_error(unsigned e) {
+    if (e & 2u)
+        return fail(RT_ERR_LIMIT, "a wait on other lanes or waves exceeded its bound (spin_cap) and was cut off; "
+                                  "the frame is invalid");
+    return fail(RT_ERR_LIMIT, "a BVH walk exceeded its step bound (walk_cap) and was cut off; the frame is invalid");
+}
+
 int check_device_error(rt_scene* s) {
     unsigned e = 0;
     HIP_TRY(hipMemcpy(&e, s->d_err, sizeof(e), hipMemcpyDeviceToHost));
     if (e == 0) return RT_OK;
     HIP_TRY(hipMemset(s->d_err, 0, sizeof(unsigned)));
-    if (e & 2u)
-        return fail(RT_ERR_LIMIT, "a wait on other lanes or waves exceeded its bound (spin_cap) and was cut off; "
-                                  "the frame is invalid");
-    return fail(RT_ERR_LIMIT, "a BVH walk exceeded its step bound (walk_cap) and was cut off; the frame is invalid");
+    return device_error(e);
 }
 
 }  // namespace
@@ -1552,10 +1556,10 @@ int rt_render(rt_scene* s, const rt_camera* cam, int aa, uint8_t* out_rgb, rt_st
     HIP_TRY(hipMemcpyAsync(s->h_err, s->d_err, sizeof(unsigned), hipMemcpyDeviceToHost, nullptr));
     HIP_TRY(hipMemcpy(out_rgb, s->d_out, bytes, hipMemcpyDeviceToHost));
     HIP_TRY(hipEventSynchronize(s->ev1));
-    if (*s->h_err) {
+    if (const unsigned e = *s->h_err) {
         *s->h_err = 0;
         HIP_TRY(hipMemset(s->d_err, 0, sizeof(unsigned)));
-        return fail(RT_ERR_LIMIT, "a BVH walk exceeded its step bound (walk_cap) and was cut off; the frame is invalid");
+        return device_error(e);
     }
     if (stats) {
         rc = rt_counters_read(s, stats);

@@ -96,7 +96,8 @@ def main():
                 q = np.nonzero(okp)[0]
                 bs, be = rel(pb[okp, 0], t0), rel(pb[okp, 1], t0)
                 bd = be - bs
-                lv, stp = (pb[okp, 2] & 255).astype(np.int64), pb[okp, 3].astype(np.int64)
+                lv, stp = (pb[okp, 2] & 255).astype(np.int64), (pb[okp, 3] & 0x7fffffff).astype(np.int64)
+                coop = (pb[okp, 3] >> 31).astype(np.int64)      # the chain walked in coop rounds (pathchain.hip)
                 wit = (pb[okp, 2] >> 8).astype(np.int64)      # the wave's walk iterations meanwhile
                 top = np.argsort(bd)[::-1][:8]
                 # each continuation's phase-A end (same path index): when a streaming A->B hand-off
@@ -121,8 +122,11 @@ def main():
                     "inflight_by_5pct": [int(((bs <= t) & (be > t)).sum()) for t in
                                          np.linspace(bs.min(), be.max(), 21)[:-1]],
                     "last_level_hist": np.bincount(lv).tolist(),
+                    "coop_chains": int(coop.sum()),
+                    "coop_by_level": np.bincount(lv[coop == 1], minlength=lv.max() + 1).tolist(),
                     "slowest": [{"q": int(q[j]), "start": round(float(bs[j]), 1), "dur": round(float(bd[j]), 1),
                                  "level": int(lv[j]), "steps": int(stp[j]), "wave_iters": int(wit[j]),
+                                 "coop": int(coop[j]),
                                  "us_per_step": round(float(bd[j]) / max(1, int(stp[j])), 2)} for j in top]}
             res.append(r)
         sc.close()
