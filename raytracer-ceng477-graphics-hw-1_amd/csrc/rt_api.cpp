@@ -7,6 +7,8 @@
 #include <algorithm>
 #include <atomic>
 #include <chrono>
+#include <future>
+#include <mutex>
 #include <cstdlib>
 #include <cmath>
 #include <cstdio>
@@ -246,6 +248,36 @@ int select_device(const rt_options* opts, int* dev) {
 
 int upload_scene(rt_scene* s, const rt_options* opts);
 
+// The process's first scene: HIP's runtime and device initialisation (~0.25 s on the GPU box: runtime,
+// device context, the kernels' code objects) runs on a helper thread while this thread reads the XML
+// and builds the trees on the host, and is joined before the upload (a drop-in caller's first frame no
+// longer pays both in sequence).  RT_NO_WARMUP=1 disables it (A/B).
+std::mutex g_warm_mu;
+std::future<void> g_warm;
+bool g_warm_started = false;
+
+void start_device_warmup(const rt_options* opts) {
+    if ((opts && (opts->flags & RT_OPT_HOST_ONLY)) || std::getenv("RT_NO_WARMUP")) return;
+    std::lock_guard<std::mutex> lk(g_warm_mu);
+    if (g_warm_started) return;
+    g_warm_started = true;
+    const int want = opts ? opts->device : -1;
+    g_warm = std::async(std::launch::async, [want] {
+        int n = 0;
+        if (hipGetDeviceCount(&n) != hipSuccess || n == 0) return;
+        (void)hipSetDevice(want >= 0 && want < n ? want : 0);
+        (void)hipFree(nullptr);
+        int a = 0, b = 0, c = 0;
+        (void)rtc::chain_occupancy(&a, &b, &c);     // loads the kernels' code objects
+        (void)rtc::fused_occupancy(&a);
+    });
+}
+
+void join_device_warmup() {
+    std::lock_guard<std::mutex> lk(g_warm_mu);
+    if (g_warm.valid()) g_warm.get();
+}
+
 double ms_since(std::chrono::steady_clock::time_point t) {
     return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t).count();
 }
@@ -259,6 +291,7 @@ int finish_scene(rt_scene* s, const rt_options* opts) {
     s->host_only = opts && (opts->flags & RT_OPT_HOST_ONLY);
     s->opt_flags = opts ? opts->flags : 0;
     if (s->host_only) return RT_OK;
+    join_device_warmup();
     const int ndev = g_devices.load();
     t = std::chrono::steady_clock::now();
     if (ndev >= 1) {                      // device group: the primary on device 0, replicas on 1..n-1
@@ -936,6 +969,7 @@ int rt_scene_create(const rt_scene_desc* desc, const rt_options* opts, rt_scene*
     *out = nullptr;
     rt_scene* s = new (std::nothrow) rt_scene();
     if (!s) return fail(RT_ERR_ARG, "out of host memory");
+    start_device_warmup(opts);
     rtx::HostScene& h = s->host;
     for (int i = 0; i < 3; ++i) h.bg[i] = desc->background_color[i];
     h.eps = desc->shadow_ray_epsilon;
@@ -979,6 +1013,7 @@ int rt_scene_load_xml(const char* path, const rt_options* opts, rt_scene** out) 
     *out = nullptr;
     rt_scene* s = new (std::nothrow) rt_scene();
     if (!s) return fail(RT_ERR_ARG, "out of host memory");
+    start_device_warmup(opts);
     const auto t = std::chrono::steady_clock::now();
     std::string err = rtx::load_xml(path, s->host, opts ? opts->build_threads : 0);
     s->xml_ms = ms_since(t);
