@@ -651,7 +651,7 @@ __device__ uint32_t bq_consume(const rtk::DevScene& s, const PcParams& p, WalkSt
 // the owner's private scratch).
 // ---------------------------------------------------------------------------
 #ifndef RT_COOP_BUILD
-#define RT_COOP_BUILD 1      // 0: k_mix without the cooperative tail walks (A/B builds)
+#define RT_COOP_BUILD 0      // 1: k_mix with the cooperative tail walks (measured slower; off)
 #endif
 struct CoopW {              // a group's walk (the same in its 8 lanes); its ray is in g_cray
     int cur, sp, steps;
@@ -2163,6 +2163,24 @@ __global__ __launch_bounds__(kBlock) void k_walk_timing(rtk::DevScene s, const f
                     }
                     h = HitRec{0.0f, cur};
                 }
+            } else if (mode == 5) {              // the cooperative walk (coop_step): lanes 0-7, one group
+                if (threadIdx.x < 8) {
+                    if (threadIdx.x == 0) {
+                        float* a = g_cray[0];
+                        a[0] = r.o.x; a[1] = r.o.y; a[2] = r.o.z; a[3] = r.d.x; a[4] = r.d.y; a[5] = r.d.z;
+                        a[6] = r.inv.x; a[7] = r.inv.y; a[8] = r.inv.z;
+                    }
+                    CoopW c;
+                    c.owner = 0; c.cur = s.wroot; c.sp = 0; c.steps = 0; c.tmax = FLT_MAX; c.best = HitRec{-1.0f, -1};
+#pragma unroll 1
+                    while (true) {
+                        ++steps;
+                        const int res = coop_step(s, c);
+                        if (res == 1) break;
+                        if (res == 2) { c.best.prim = -2; break; }   // would need the scratch stack
+                    }
+                    h = c.best;
+                }
             } else if ((int)threadIdx.x < lanes) {
                 Walk wk;
                 bool go = mode == 0 ? walk_begin<false>(s, r, wk, w) : walk_begin<true>(s, r, wk, w);
@@ -2231,6 +2249,7 @@ hipError_t launch_walk_timing(const rtk::DevScene& s, const float* rays, int n, 
     if (mode == 0) hipLaunchKernelGGL(k_walk_timing<0>, dim3(1), dim3(kBlock), 0, st, s, rays, n, lanes, reps, out);
     else if (mode == 1) hipLaunchKernelGGL(k_walk_timing<1>, dim3(1), dim3(kBlock), 0, st, s, rays, n, lanes, reps, out);
     else if (mode == 3) hipLaunchKernelGGL(k_walk_timing<3>, dim3(1), dim3(kBlock), 0, st, s, rays, n, lanes, reps, out);
+    else if (mode == 5) hipLaunchKernelGGL(k_walk_timing<5>, dim3(1), dim3(kBlock), 0, st, s, rays, n, lanes, reps, out);
     else hipLaunchKernelGGL(k_walk_timing<4>, dim3(1), dim3(kBlock), 0, st, s, rays, n, lanes, reps, out);
     return hipGetLastError();
 }

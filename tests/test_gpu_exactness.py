@@ -259,6 +259,6 @@ def test_wait_bound_reports_limit(pkg, scene_dir, goldens, torch_cuda, monkeypat
         s.check()                                  # the error word was cleared by the failing call
     monkeypatch.delenv("RT_SPIN_CAP")
     with pkg.Scene.from_xml(xml, device=0) as s:
-        img = s.render(s.camera(0), aa=1)
+        img, _ = s.render(s.camera(0), aa=1)
         s.check()
     assert np.array_equal(img, load_golden_image(g["cameras"][0]))

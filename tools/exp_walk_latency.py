@@ -5,7 +5,8 @@ The rays (tools/heavy_rays_c3.txt, hex floats: o.xyz dir.xyz) are the mirror
 chain of the C3 frame's heaviest pixel (row 495, col 1227) followed by an
 ordinary eye ray, dumped by tools/exp_sah_closest.cpp --dump.  One wave walks
 each ray alone (1 lane) or with 64 lanes on the same ray, on the 4-wide tree
-(mode 0), on the reference tree (mode 1) and with a 4-lane group (mode 2); cycles are s_memtime ticks.
+(mode 0), on the reference tree (mode 1), memory-only chases (modes 3, 4) and as a cooperative walk
+(mode 5: coop_step, 8 lanes, one wide-node slot per lane); cycles are s_memtime ticks.
 """
 import json
 import sys
@@ -23,8 +24,8 @@ rays = np.array([[float.fromhex(x) for x in l.split()] for l in
 xml = pkg.scenes.write_config("C3_hm_1080p_d6", tempfile.mkdtemp())
 s = pkg.Scene.from_xml(xml, device=0)
 res = {}
-for mode in (0, 1, 2, 3, 4):
-    for lanes in ((1, 64) if mode < 2 else (4,)):
+for mode in (0, 1, 3, 4, 5):
+    for lanes in ((1, 8, 64) if mode < 2 else (8,)):
         o = s.walk_timing(rays, lanes=lanes, reps=4, mode=mode)
         res[f"mode{mode}_lanes{lanes}"] = [{"cycles": int(a), "steps": int(b), "prim": int(np.int64(c)), "cold": int(d),
                                             "cyc_per_step": round(int(a) / max(1, int(b)), 1)} for a, b, c, d in o]
