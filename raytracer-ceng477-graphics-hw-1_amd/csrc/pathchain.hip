@@ -809,6 +809,7 @@ __device__ __forceinline__ void coop_round(const rtk::DevScene& s, CoopW& c, int
             a[3] = r.d.x; a[4] = r.d.y; a[5] = r.d.z;
             a[6] = r.inv.x; a[7] = r.inv.y; a[8] = r.inv.z;
         }
+        __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");   // the owners' LDS words, seen by their groups
         const int src = c.owner >= 0 ? c.owner : lane;
         const bool f = (fresh >> (lane & 56)) & 1ull;
         auto take = [&](auto& dst, auto v) { const auto x = __shfl(v, src, 64); if (f) dst = x; };
@@ -817,6 +818,7 @@ __device__ __forceinline__ void coop_round(const rtk::DevScene& s, CoopW& c, int
     }
     // (2) step every group's walk (a walk not taken, 2, stays as it was: the owner redoes the step)
     const int res = c.owner >= 0 ? coop_step(s, c) : 0;
+    __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");   // the groups' stack writes, seen by their owners
     // (3) finished (1) or handed back (2): the walk's registers return to its owner lane
     const unsigned long long ended = __ballot(res != 0 && (lane & 7) == 0);
     if (ended) {
@@ -2170,6 +2172,7 @@ __global__ __launch_bounds__(kBlock) void k_walk_timing(rtk::DevScene s, const f
                         a[0] = r.o.x; a[1] = r.o.y; a[2] = r.o.z; a[3] = r.d.x; a[4] = r.d.y; a[5] = r.d.z;
                         a[6] = r.inv.x; a[7] = r.inv.y; a[8] = r.inv.z;
                     }
+                    __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");   // lane 0's LDS words, seen by lanes 1-7
                     CoopW c;
                     c.owner = 0; c.cur = s.wroot; c.sp = 0; c.steps = 0; c.tmax = FLT_MAX; c.best = HitRec{-1.0f, -1};
 #pragma unroll 1
