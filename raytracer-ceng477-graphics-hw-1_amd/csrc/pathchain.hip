@@ -787,7 +787,7 @@ __device__ __forceinline__ int coop_step(const rtk::DevScene& s, CoopW& c) {
 // every group steps its walk, and finished or handed-back walks return to their owners.
 // st: the owner's lane state (kCoop while a group has its walk); cg: the leader lane of that group.
 constexpr int kCoop = 3;
-__device__ __forceinline__ void coop_round(const rtk::DevScene& s, CoopW& c, int& st, int& cg, bool& coop_ok,
+[[maybe_unused]] __device__ __forceinline__ void coop_round(const rtk::DevScene& s, CoopW& c, int& st, int& cg, bool& coop_ok,
                                            const Ray& r, Walk& wk) {
     const int lane = lane_id();
     // (1) assign: the i-th candidate walk to the i-th free group

@@ -690,7 +690,7 @@ int ensure_chain_grids(rt_scene* s) {
 
 // Every size of a launch of `nunits` row units, and its arena layout: worst-case queue sizing (every
 // sample recording every level), so no queue can overflow.  (ensure_chain_grids first.)
-ChainPlan chain_plan(const rt_scene* s, const ChainGeom& g, size_t nunits, bool count) {
+ChainPlan chain_plan(const rt_scene* s, const ChainGeom& g, size_t nunits, bool count, size_t cb_want = 0) {
     const bool fused = s->path == rt_scene::kFused;
     const int levels = g.levels, nl = g.nl;
     const int max_grid = fused ? s->fused_grid : s->chain_grid;
@@ -724,6 +724,7 @@ ChainPlan chain_plan(const rt_scene* s, const ChainGeom& g, size_t nunits, bool 
     P.la = fused || !P.phase_b ? levels : P.levels_a;
     P.cb = P.la >= levels ? 0 : (count ? cap : std::min(cap, std::max(cap / (size_t)std::max(1, s->tune_cont_den),
                                                                         std::min<size_t>(cap, 65536))));
+    if (cb_want > 0 && !count && P.la < levels) P.cb = std::min(cap, std::max(P.cb, cb_want));
     if (s->tune_cont_cb > 0 && !count && P.la < levels) P.cb = std::min(cap, (size_t)s->tune_cont_cb);
     P.tchunk = s->tune_tchunk > 0 ? s->tune_tchunk : (g.nframes > 1 ? 128 : 1);
     {   // a phase-B workgroup's continuations: at most ceil(chunks / gb) chunks of tchunk (chunk_count)
@@ -759,7 +760,7 @@ ChainPlan chain_plan(const rt_scene* s, const ChainGeom& g, size_t nunits, bool 
 // Row units of one launch: as many as the chunk target (RT_CHUNK_SAMPLES), the u32 task ids and the
 // slot's share of the workspace budget (RT_WS_BUDGET_MB over the slots) allow -- the largest count
 // whose chain_plan arena fits the budget (at least one unit, whatever its size).
-size_t chain_launch_units(rt_scene* s, const ChainGeom& g, bool count) {
+size_t chain_launch_units(rt_scene* s, const ChainGeom& g, bool count, size_t* cb_out = nullptr) {
     const size_t id_limit = (size_t)(INT32_MAX - 1) / ((size_t)g.levels * g.nl);   // u32 task owner ids (pathchain.hpp)
     size_t units = std::min(g.units_total, std::max<size_t>(1, std::min(s->chunk_samples, id_limit) / g.unit_samples));
     const size_t budget = s->slot_budget();
@@ -777,6 +778,26 @@ size_t chain_launch_units(rt_scene* s, const ChainGeom& g, bool count) {
                          g.unit_samples, chain_plan(s, g, 1, count).bytes / 1e6, budget / 1e6);
         }
     }
+    if (cb_out) {
+        // phase-B record space: cap/6 continuations by default (C3 continues ~9 % of its samples); the
+        // rest of the slot's budget then raises it, up to every sample, so a mirror-heavy frame
+        // (marbles: 60 % continue) keeps its deep chains in phase B instead of k_fallback's serial
+        // whole-path walks.  Bytes grow linearly with cb.
+        const ChainPlan P = chain_plan(s, g, units, count);
+        *cb_out = P.cb;
+        if (!count && P.la < g.levels && P.cb < P.cap && P.bytes < budget) {
+            const ChainPlan F = chain_plan(s, g, units, count, P.cap);
+            if (F.bytes <= budget) {
+                *cb_out = P.cap;
+            } else {
+                const double per = (double)(F.bytes - P.bytes) / (double)(F.cb - P.cb);
+                const size_t extra = (size_t)((double)(budget - P.bytes) / per * 0.98);
+                *cb_out = std::min(P.cap, P.cb + extra);
+                while (*cb_out > P.cb && chain_plan(s, g, units, count, *cb_out).bytes > budget)
+                    *cb_out = P.cb + (*cb_out - P.cb) / 2;
+            }
+        }
+    }
     return units;
 }
 
@@ -789,8 +810,9 @@ int render_chain(rt_scene* s, const rtk::Eye& eye, const rtk::FrameParams& f, bo
     if (const int rc = ensure_chain_grids(s)) return rc;
     const int max_grid = fused ? s->fused_grid : s->chain_grid;
     auto grid_for = [&](int n0) { return std::max(1, std::min(max_grid, (n0 + 255) / 256)); };
-    const size_t units = chain_launch_units(s, g, count);
-    const ChainPlan P = chain_plan(s, g, units, count);
+    size_t cb = 0;
+    const size_t units = chain_launch_units(s, g, count, &cb);
+    const ChainPlan P = chain_plan(s, g, units, count, cb);
     const int chunk_rows = (int)units * unit;
     const size_t cap = P.cap;
     if (cap * levels * nl >= (size_t)INT32_MAX) return fail(RT_ERR_LIMIT, "frame chunk too large for the chain path");
