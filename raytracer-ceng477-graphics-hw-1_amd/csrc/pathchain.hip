@@ -885,6 +885,7 @@ __device__ void chain_body(const rtk::DevScene& s, const rtk::Eye& e, const PcPa
     Ray r;
     Walk wk;
     unsigned t_grab = 0, tsteps = 0, twit = 0, wit = 0;   // trace: grab time, own steps, wave steps
+    unsigned apoll = 0;      // phase A: iterations since the last look at the finished-wave count (p.abandon)
     bool fresh = false;      // lane just took an eye ray (packet walk pending)
     StepStat stat;
     // cooperative tail walks (lone-frame phase B: coop_round): the group walk this lane works on, the
@@ -1025,13 +1026,19 @@ __device__ void chain_body(const rtk::DevScene& s, const rtk::Eye& e, const PcPa
                         if (CONT) {
                             const unsigned j = chunk_task(v, G, blk, (unsigned)p.tchunk);
                             const unsigned lvp = p.cflat[j];
-                            path = lvp % (unsigned)p.cap;
-                            k = (int)(lvp / (unsigned)p.cap) + 1;
                             cix = j;
                             if (p.trace) { t_grab = (unsigned)wall_clock64(); tsteps = 0; twit = wit; }
-                            r = reflect_from_record(s, p, lvp);
-                            nrefl++;
-                            if (!COUNT && defer_closest(s, r)) fb_chain(p, lvp);
+                            // a walk phase A gave up on (p.abandon: lone frames only, so only the BQ kernel has them)
+                            const bool eye = BQ && (lvp & kFbEye) != 0;
+                            path = eye ? lvp & ~kFbEye : lvp % (unsigned)p.cap;
+                            k = eye ? 0 : (int)(lvp / (unsigned)p.cap) + 1;
+                            if (eye) {
+                                slab_sample_ray(e, p, path, &r);
+                            } else {
+                                r = reflect_from_record(s, p, lvp);
+                                nrefl++;
+                            }
+                            if (!COUNT && defer_closest(s, r)) fb_chain(p, lvp);   // (an eye entry keeps its kFbEye bit)
                             else st = walk_begin<COUNT>(s, r, wk, w) ? kTrav : kDone;
                             coop_ok = true;
                         } else {
@@ -1071,7 +1078,17 @@ __device__ void chain_body(const rtk::DevScene& s, const rtk::Eye& e, const PcPa
         }
         // (3) walk until enough lanes need service
         const int thresh = exhausted ? 0 : (CONT ? p.brefill : p.refill);
+        bool abandon = false;
         while (true) {
+            if constexpr (!CONT && !COUNT) {
+                // phase A's stragglers: once nearly every k_chain wave has finished, a wave with no unit left
+                // hands its unfinished walks to phase B (wave-uniform test, every 32 iterations)
+                if (exhausted && p.abandon && (++apoll & 31u) == 0u) {
+                    unsigned done = 0;
+                    if (lane_id() == 0) done = __hip_atomic_load(&p.totals[7], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    if (__shfl(done, 0, 64) >= p.abandon) { abandon = true; break; }
+                }
+            }
             const int nt = __popcll(__ballot(st == kTrav || (COOPK && st == kCoop)));
             const bool tail = COOPK && p.coop && exhausted && nt <= p.coop_live;
             if (nt <= thresh ||
@@ -1094,8 +1111,23 @@ __device__ void chain_body(const rtk::DevScene& s, const rtk::Eye& e, const PcPa
                 if (closest_step_timed<COUNT, CONT>(s, r, stk, wk, w) || walk_runaway(s, wk)) st = kDone;
             }
         }
+        if constexpr (!CONT && !COUNT) {
+            if (abandon) {   // every unfinished walk restarts in phase B: the eye ray, or the reflection of its last record
+                const bool h = st == kTrav;
+                const unsigned long long cm = __ballot(h);
+                const unsigned base = cm ? wave_grab_lds(&g_ccnt, cm) : 0u;
+                if (h) {
+                    const unsigned entry = k == 0 ? (kFbEye | path) : (unsigned)((size_t)(k - 1) * p.cap + path);
+                    o.cq[(size_t)blk * o.ccap + base + lane_rank(cm)] = entry;
+                    p.pinfo[path] = kPathCont;
+                    st = kIdle;
+                }
+                // walks already done are serviced as usual (the loop's next pass); then the wave has nothing left
+            }
+        }
     }
     stat.flush(CONT ? 1 : 0);
+    if (!CONT && !COUNT && p.abandon && lane_id() == 0) atomicAdd(&p.totals[7], 1u);   // this wave is done
     uint32_t nshadow = 0;
     if (COUNT) {
         wave_add_counter(&p.counters[CONT ? kCntBWalkBytes : kCntAWalkBytes], w.nodes);
@@ -1470,14 +1502,14 @@ __device__ void pack_region(const unsigned* q, unsigned cap, const unsigned* cnt
         const unsigned v0 = src[k], v1 = src[k + kBlock], v2 = src[k + 2 * kBlock], v3 = src[k + 3 * kBlock];
         flat[off + k] = v0; flat[off + k + kBlock] = v1; flat[off + k + 2 * kBlock] = v2; flat[off + k + 3 * kBlock] = v3;
         if (cid) {
-            cid[v0 % ncap] = off + k; cid[v1 % ncap] = off + k + kBlock;
-            cid[v2 % ncap] = off + k + 2 * kBlock; cid[v3 % ncap] = off + k + 3 * kBlock;
+            cid[(v0 & ~kFbEye) % ncap] = off + k; cid[(v1 & ~kFbEye) % ncap] = off + k + kBlock;
+            cid[(v2 & ~kFbEye) % ncap] = off + k + 2 * kBlock; cid[(v3 & ~kFbEye) % ncap] = off + k + 3 * kBlock;
         }
     }
     for (; k < n; k += kBlock) {
         const unsigned v = src[k];
         flat[off + k] = v;
-        if (cid) cid[v % ncap] = off + k;
+        if (cid) cid[(v & ~kFbEye) % ncap] = off + k;
     }
     if (b == 0 && threadIdx.x == 0) *total = s_all;
     __syncthreads();
@@ -1936,7 +1968,7 @@ __device__ __forceinline__ void finish_pixels(const rtk::DevScene& s, const PcPa
     if (p.fin_cont) {
         const unsigned n = p.totals[1];
         for (unsigned j = gtid; j < n; j += gstride) {
-            const unsigned path = p.cflat[j] % (unsigned)p.cap;
+            const unsigned path = (p.cflat[j] & ~kFbEye) % (unsigned)p.cap;
             const unsigned tile = path >> 6, lane = path & 63u;
             const int ix = (int)(tile % (unsigned)p.tiles_x) * 8 + (int)(lane & 7u);
             const int iyc = (int)(tile / (unsigned)p.tiles_x) * 8 + (int)(lane >> 3);
@@ -2009,7 +2041,7 @@ __device__ __forceinline__ bool fallback_any(const rtk::DevScene& s, const Ray& 
 }
 
 __device__ void fallback_chain(const rtk::DevScene& s, const rtk::Eye& e, const PcParams& p, unsigned entry,
-                               WalkStack& stk, Work& w) {
+                               WalkStack& stk, Work& w, bool cont = false) {   // cont: a continuation (cflat)
     const unsigned cap = (unsigned)p.cap;
     unsigned path;
     int k;
@@ -2027,7 +2059,7 @@ __device__ void fallback_chain(const rtk::DevScene& s, const rtk::Eye& e, const 
         } else {
             const size_t q = entry - aspace;
             kprev = p.la + (int)(q / p.cb);
-            path = p.cflat[q % p.cb] % cap;
+            path = (p.cflat[q % p.cb] & ~kFbEye) % cap;
         }
         k = kprev + 1;
         r = reflect_from_record(s, p, entry);
@@ -2073,7 +2105,7 @@ __device__ void fallback_chain(const rtk::DevScene& s, const rtk::Eye& e, const 
     }
     for (int i = n - 1; i >= 0; --i) c = vclamp(add(Ls[i], had(c, Km[i])), 0.0f, FLT_MAX);   // :436-451
     p.tail[path] = make_float4(c.x, c.y, c.z, 0.0f);
-    p.pinfo[path] = k0 | (kEndTail << 8) | (k0 >= p.la ? kPathCont : 0);
+    p.pinfo[path] = k0 | (kEndTail << 8) | (k0 >= p.la || cont ? kPathCont : 0);
 }
 
 __global__ __launch_bounds__(kBlock) void k_fallback(rtk::DevScene s, rtk::Eye e, PcParams p) {
@@ -2092,7 +2124,7 @@ __global__ __launch_bounds__(kBlock) void k_fallback(rtk::DevScene s, rtk::Eye e
         if (p.totals[6]) atomicAdd(&p.counters[kCntFbOvfScans], 1ull);
     }
     for (unsigned i = gt; i < nfc + novf; i += gs)
-        fallback_chain(s, e, p, i < nfc ? p.fbc[i] : p.cflat[p.cb + (i - nfc)], stk, w);
+        fallback_chain(s, e, p, i < nfc ? p.fbc[i] : p.cflat[p.cb + (i - nfc)], stk, w, i >= nfc);
     const unsigned nfs = min(p.totals[5], p.fbs_cap);
     for (unsigned i = gt; i < nfs; i += gs) {
         const unsigned owner = p.fbs[i];
@@ -2318,7 +2350,7 @@ hipError_t launch_chain_chunk(const rtk::DevScene& s, const rtk::Eye& e, const P
     auto mark = [&](int k) { if (kt) kt->mark(k, st); };
     const bool phase_b = p.kinline < s.max_depth;     // any continuation possible
     {   // the dynamic unit counter and k_fallback's counts
-        const hipError_t me = hipMemsetAsync(p.totals + 3, 0, 4 * sizeof(unsigned), st);
+        const hipError_t me = hipMemsetAsync(p.totals + 3, 0, 5 * sizeof(unsigned), st);
         if (me != hipSuccess) return me;
     }
     mark(kKChain);

@@ -113,7 +113,8 @@ struct PcParams {
     unsigned scapB;
     unsigned* scntB;  // [gb]
     unsigned* sflatB; // B's shadow tasks packed (k_pack_b), totals[2] of them
-    unsigned* totals; // [8]: packed task counts (3), phase-A unit counter, k_fallback chains / shadows / overflow
+    unsigned* totals; // [8]: packed task counts (3), phase-A unit counter, k_fallback chains / shadows / overflow,
+                      // finished k_chain waves
     int kinline;      // deepest level phase A walks (>= max_depth: no phase B)
     int gb;           // k_mix workgroups in the chain role (the other p.ogrid ones occlude A's tasks)
     int tchunk;       // continuation tasks (phase B) are dealt to workgroups in chunks of this many
@@ -135,6 +136,8 @@ struct PcParams {
     int bservice;     // the same for phase-B chains
     int btail;        // phase-B chains once no continuation is left to take: service at this many done lanes
     int bq_cap;       // phase-B workgroup shadow queue slots in use (<= kBq; 0: every task to k_occlude)
+    unsigned abandon; // phase A: once this many k_chain waves have finished (totals[7]), a wave with no unit
+                      // left hands its unfinished walks to phase B as continuations (0: never)
     int coop;         // lone-frame phase B: once a wave has no continuation left and <= coop_live chains walk,
     int coop_live;    // each walk runs on a group of 8 lanes (one wide-node slot per lane; coop_step);
     int coop_tail;    // ... and a wave services its finished walks once this many are done (0: coop off)

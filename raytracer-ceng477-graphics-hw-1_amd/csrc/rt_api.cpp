@@ -145,6 +145,7 @@ struct rt_scene {
     int tune_gb = 0;            // RT_GB: phase-B chain workgroups in k_mix (0: 1.875 per CU for a lone frame, 1 for batches)
     int tune_bq_cap = 1 << 30;  // RT_BQ_CAP: phase-B shadow queue slots (tests force the k_occlude spill path)
     int tune_bservice = 64;     // RT_BSERVICE: phase-B waves service finished walks once this many lanes are done
+    int tune_abandon = 970;     // RT_ABANDON: per mille of k_chain's waves done before the stragglers hand off (0: off)
     int tune_coop = 1;          // RT_COOP (builds with RT_COOP_BUILD=1): lone-frame phase B walks its tail chains on 8-lane groups (pathchain.hip coop_step)
     int tune_coop_live = 8;     // RT_COOP_LIVE: ... once at most this many chains of the wave walk (<= 8)
     int tune_coop_tail = 1;     // RT_COOP_TAIL: ... servicing finished walks once this many are done
@@ -404,6 +405,7 @@ int upload_scene(rt_scene* s, const rt_options* opts) {
     if (const char* e = std::getenv("RT_BSERVICE")) s->tune_bservice = std::max(1, std::min(64, std::atoi(e)));
     if (const char* e = std::getenv("RT_BTAIL")) s->tune_btail = std::max(1, std::min(64, std::atoi(e)));
     if (const char* e = std::getenv("RT_COOP")) s->tune_coop = std::atoi(e) != 0;
+    if (const char* e = std::getenv("RT_ABANDON")) s->tune_abandon = std::max(0, std::min(1000, std::atoi(e)));
     if (const char* e = std::getenv("RT_COOP_LIVE")) s->tune_coop_live = std::max(1, std::min(8, std::atoi(e)));
     if (const char* e = std::getenv("RT_COOP_TAIL")) s->tune_coop_tail = std::max(1, std::min(64, std::atoi(e)));
     if (const char* e = std::getenv("RT_SPLIT")) s->tune_split = std::max(1, std::atoi(e));
@@ -926,6 +928,10 @@ int render_chain(rt_scene* s, const rtk::Eye& eye, const rtk::FrameParams& f, bo
         p.chunk_rows = std::min(chunk_rows, li - r0);
         p.n0 = tiles_x * ((p.chunk_rows + 7) / 8) * 64;
         p.grid = grid_for(p.n0);
+        // phase A's stragglers hand their walks to phase B once this share of k_chain's waves is done
+        p.abandon = s->tune_abandon > 0 && !count && P.phase_b && !P.split_occ   // lone frames (k_mix with the BQ)
+                        ? (unsigned)std::max<long long>(1, (long long)p.grid * 4 * s->tune_abandon / 1000)   // 4 waves per 256-thread workgroup
+                        : 0u;
         if (p.grid > P.G) return fail(RT_ERR_LIMIT, "internal: chain grid exceeds the workspace");
         if (fused) {
             HIP_TRY(rtc::launch_fused_chunk(s->dev, eye, p, count, st));

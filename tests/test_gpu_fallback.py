@@ -11,7 +11,10 @@ branch of it and compare with the reference goldens (raytracer.cpp:385-452):
   * =3: both;
   * RT_CONT_CB=1000: continuations beyond 1,000 finish in k_fallback;
   * RT_FBS_CAP=64 with =2: the shadow queue overflows (marked occlusion bytes
-    scanned by k_fallback).
+    scanned by k_fallback);
+  * RT_ABANDON=1: phase A's unfinished walks restart in phase B (eye rays as
+    kFbEye continuations, level-1 walks as reflections of their level-0 record),
+    alone and with RT_CONT_CB=1000 (the restarts beyond it in k_fallback).
 """
 from __future__ import annotations
 
@@ -33,6 +36,11 @@ def torch_cuda():
 
 
 ENVS = [
+    # phase A's stragglers handed to phase B (pathchain.hip p.abandon) after 1 of 1000 k_chain waves has
+    # finished: nearly every walk restarts in phase B (eye rays and level-1 reflections as continuations)
+    {"RT_ABANDON": "1"},
+    # the same with a phase-B record space of 1,000: the restarted walks beyond it finish in k_fallback
+    {"RT_ABANDON": "1", "RT_CONT_CB": "1000"},
     {"RT_FORCE_FALLBACK": "1"},
     {"RT_FORCE_FALLBACK": "2"},
     {"RT_FORCE_FALLBACK": "3"},
