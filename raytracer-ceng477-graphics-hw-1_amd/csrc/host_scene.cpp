@@ -926,17 +926,19 @@ void build_shadow_tree(FlatBVH& out, int threads) {
     // tree is bit-identical to it), so every pass reads them sequentially; a node's box and centroid
     // box are one pass, the three axes' bins another.
     struct TNode { Box box; int left = -1, right = -1, axis = 0; int32_t info = 0, rec = -1; };
-    // Subtrees are independent (disjoint ranges of the leaf array): the top levels are
-    // built as concurrent tasks into their own node pools, spliced afterwards.
+    // Subtrees are independent (disjoint ranges of the leaf array), and a subtree over leaves [b, e) has
+    // exactly 2(e - b) - 1 nodes: rooted at node slot `at`, it takes slots [at, at + 2(e - b) - 1) of
+    // one array (the left subtree from at + 1, the right one from at + 2(mid - b)), so the top levels run
+    // as concurrent tasks that write disjoint slots, with no per-task pools to splice.
     struct Sah {
         std::vector<Leaf>& lv;
         int fork;
-        std::vector<TNode> tn;
+        std::vector<TNode>& tn;
         int smax_depth = 0;
-        int (*fn)(Sah&, int, int, int);
-        int build(int b, int e, int depth) { return fn(*this, b, e, depth); }
+        int (*fn)(Sah&, int, int, int, int);
+        int build(int b, int e, int depth, int at) { return fn(*this, b, e, depth, at); }
     };
-    auto sah_build = [](Sah& me_, int b, int e, int depth) -> int {
+    auto sah_build = [](Sah& me_, int b, int e, int depth, int at) -> int {
         std::vector<Leaf>& lv = me_.lv;
         std::vector<TNode>& tn = me_.tn;
         TNode node;
@@ -946,8 +948,8 @@ void build_shadow_tree(FlatBVH& out, int threads) {
             cb.grow(lv[i].c, lv[i].c);
         }
         me_.smax_depth = std::max(me_.smax_depth, depth);
-        const int me = (int)tn.size();
-        tn.push_back(node);
+        const int me = at;
+        tn[me] = node;
         if (e - b == 1) {
             tn[me].info = lv[b].info;
             tn[me].rec = lv[b].rec;
@@ -1019,28 +1021,24 @@ void build_shadow_tree(FlatBVH& out, int threads) {
         }
         int l, r;
         if (depth < me_.fork && std::min(mid - b, e - mid) >= 512) {
-            Sah lb{lv, me_.fork, {}, 0, me_.fn}, rb{lv, me_.fork, {}, 0, me_.fn};
-            lb.tn.reserve(2 * (size_t)(mid - b));       // one allocation per pool (page faults are costly)
-            rb.tn.reserve(2 * (size_t)(e - mid));
-            auto fr = std::async(std::launch::async, [&, mid, e, depth] { return rb.build(mid, e, depth + 1); });
-            const int lr = lb.build(b, mid, depth + 1);
-            const int rr = fr.get();
-            l = splice_pool(tn, std::move(lb.tn), lr);
-            r = splice_pool(tn, std::move(rb.tn), rr);
-            me_.smax_depth = std::max({me_.smax_depth, lb.smax_depth, rb.smax_depth});
+            Sah rb{lv, me_.fork, tn, 0, me_.fn};
+            const int rat = at + 2 * (mid - b);
+            auto fr = std::async(std::launch::async, [&rb, mid, e, depth, rat] { return rb.build(mid, e, depth + 1, rat); });
+            l = me_.build(b, mid, depth + 1, at + 1);
+            r = fr.get();
+            me_.smax_depth = std::max(me_.smax_depth, rb.smax_depth);
         } else {
-            l = me_.build(b, mid, depth + 1);
-            r = me_.build(mid, e, depth + 1);
+            l = me_.build(b, mid, depth + 1, at + 1);
+            r = me_.build(mid, e, depth + 1, at + 2 * (mid - b));
         }
         tn[me].left = l;
         tn[me].right = r;
         tn[me].axis = axis;
         return me;
     };
-    Sah top{leaves, fork_depth(threads), {}, 0, +sah_build};
-    top.tn.reserve(2 * leaves.size());
-    const int root = top.build(0, (int)leaves.size(), 0);
-    std::vector<TNode> tn = std::move(top.tn);
+    std::vector<TNode> tn(2 * leaves.size());
+    Sah top{leaves, fork_depth(threads), tn, 0, +sah_build};
+    const int root = top.build(0, (int)leaves.size(), 0, 0);
     out.smax_depth = top.smax_depth;
     // pairs in pre-order of interior nodes
     std::vector<int32_t> pair_of(tn.size(), -1);

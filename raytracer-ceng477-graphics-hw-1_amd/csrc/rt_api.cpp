@@ -145,7 +145,9 @@ struct rt_scene {
     int tune_gb = 0;            // RT_GB: phase-B chain workgroups in k_mix (0: 1.875 per CU for a lone frame, 1 for batches)
     int tune_bq_cap = 1 << 30;  // RT_BQ_CAP: phase-B shadow queue slots (tests force the k_occlude spill path)
     int tune_bservice = 64;     // RT_BSERVICE: phase-B waves service finished walks once this many lanes are done
-    int tune_abandon = 970;     // RT_ABANDON: per mille of k_chain's waves done before the stragglers hand off (0: off)
+    int tune_abandon = 0;       // RT_ABANDON: per mille of k_chain's waves done before the stragglers hand off (0: off;
+                                // 900-990 measured 2-4 % slower for C3 one frame: the restarted walks are the
+                                // heaviest, deepest chains, which then start phase B from scratch)
     int tune_coop = 1;          // RT_COOP (builds with RT_COOP_BUILD=1): lone-frame phase B walks its tail chains on 8-lane groups (pathchain.hip coop_step)
     int tune_coop_live = 8;     // RT_COOP_LIVE: ... once at most this many chains of the wave walk (<= 8)
     int tune_coop_tail = 1;     // RT_COOP_TAIL: ... servicing finished walks once this many are done
