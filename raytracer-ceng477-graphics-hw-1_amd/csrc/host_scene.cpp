@@ -385,9 +385,12 @@ struct BNode {
 // concurrent tasks (each into its own node pool, spliced afterwards).  The
 // tree depends only on the split rule, never on thread timing.
 int fork_depth(int threads) {
+    // 2^d concurrent tasks for `threads` threads, no more: every task is a thread, and a process held to
+    // a CPU quota (a cgroup share of a larger host, as on the GPU boxes) is throttled once it runs more
+    // threads than its share
     int d = 0;
-    while ((1 << d) < threads && d < 6) ++d;
-    return threads <= 1 ? 0 : d + 1;
+    while ((2 << d) <= threads && d < 6) ++d;
+    return threads <= 1 ? 0 : d;
 }
 
 // fn(i) for i in [0, n) on `threads` threads (contiguous chunks; fn must only write item i's outputs).
@@ -409,17 +412,6 @@ void parallel_for(int n, int threads, F&& fn) {
     for (auto& th : pool) th.join();
 }
 
-template <class N>
-int splice_pool(std::vector<N>& dst, std::vector<N>&& src, int root) {
-    if (root < 0) return -1;
-    const int off = (int)dst.size();
-    for (N& n : src) {
-        if (n.left >= 0) n.left += off;
-        if (n.right >= 0) n.right += off;
-        dst.push_back(std::move(n));
-    }
-    return root + off;
-}
 
 // Per-triangle box (the three vertices folded with the reference's `<` / `>`
 // updates, parser.h:272-317) and split key, computed once: a node's box is the
@@ -437,14 +429,18 @@ constexpr int kForkMin = 2048;   // a split forks only when both sides have this
 
 class Builder {
   public:
-    Builder(const HostScene& s, const std::vector<TriBox>& tb, std::vector<int>& pt, std::vector<int>& ps, int fork)
-        : s_(s), tb_(tb), pt_(pt), ps_(ps), fork_(fork) {}
-    std::vector<BNode> nodes;
+    // nodes: the shared node array, 2 (triangles + spheres) - 1 slots: a subtree over n primitives
+    // (n >= 1) has at most 2n - 1 nodes, so rooted at slot `at` it owns [at, at + 2n - 1) -- the left
+    // subtree from at + 1, the right one from at + 2 nl -- and concurrent subtrees write disjoint slots
+    // (unused slots stay default nodes, never reached from the root)
+    Builder(const HostScene& s, const std::vector<TriBox>& tb, std::vector<int>& pt, std::vector<int>& ps, int fork,
+            std::vector<BNode>& nodes)
+        : nodes(nodes), s_(s), tb_(tb), pt_(pt), ps_(ps), fork_(fork) {}
+    std::vector<BNode>& nodes;
 
-    int build(int t0, int t1, int s0, int s1, int depth) {
+    int build(int t0, int t1, int s0, int s1, int depth, int at) {
         if (t0 == t1 && s0 == s1) return -1;
-        const int id = (int)nodes.size();
-        nodes.emplace_back();
+        const int id = at;
         BNode nd;
         nd.depth = depth;
         bounds(t0, t1, s0, s1, nd.lo, nd.hi);
@@ -462,18 +458,15 @@ class Builder {
         nodes[id] = nd;
         int r, l;
         const int nl = (tm - t0) + (sm - s0), nr = (t1 - tm) + (s1 - sm);
+        const int lat = at + 1, rat = at + 2 * nl;
         if (depth < fork_ && std::min(nl, nr) >= kForkMin) {
-            Builder rb(s_, tb_, pt_, ps_, fork_), lb(s_, tb_, pt_, ps_, fork_);
-            rb.nodes.reserve(2 * (size_t)nr + 1);     // one allocation per pool (page faults are costly)
-            lb.nodes.reserve(2 * (size_t)nl + 1);
-            auto fr = std::async(std::launch::async, [&] { return rb.build(tm, t1, sm, s1, depth + 1); });
-            const int lr = lb.build(t0, tm, s0, sm, depth + 1);
-            const int rr = fr.get();
-            r = splice_pool(nodes, std::move(rb.nodes), rr);
-            l = splice_pool(nodes, std::move(lb.nodes), lr);
+            Builder rb(s_, tb_, pt_, ps_, fork_, nodes);
+            auto fr = std::async(std::launch::async, [&] { return rb.build(tm, t1, sm, s1, depth + 1, rat); });
+            l = build(t0, tm, s0, sm, depth + 1, lat);
+            r = fr.get();
         } else {
-            r = build(tm, t1, sm, s1, depth + 1);     // right first (bvh.h:69-70)
-            l = build(t0, tm, s0, sm, depth + 1);
+            r = build(tm, t1, sm, s1, depth + 1, rat);     // right first (bvh.h:69-70)
+            l = build(t0, tm, s0, sm, depth + 1, lat);
         }
         nodes[id].right = r;
         nodes[id].left = l;
@@ -699,9 +692,9 @@ std::string build_bvh(const HostScene& s, FlatBVH& out, int threads) {
     std::vector<int> pt(s.tris.size()), ps(s.spheres.size());
     for (size_t i = 0; i < pt.size(); ++i) pt[i] = (int)i;
     for (size_t i = 0; i < ps.size(); ++i) ps[i] = (int)i;
-    Builder b(s, tb, pt, ps, fork_depth(out.threads));
-    b.nodes.reserve(2 * (pt.size() + ps.size()) + 1);
-    const int root = b.build(0, (int)pt.size(), 0, (int)ps.size(), 0);
+    std::vector<BNode> bnodes(std::max<size_t>(1, 2 * (pt.size() + ps.size())));
+    Builder b(s, tb, pt, ps, fork_depth(out.threads), bnodes);
+    const int root = b.build(0, (int)pt.size(), 0, (int)ps.size(), 0, 0);
     out.ref_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
 
     out.tri_shade.resize(s.tris.size());
@@ -712,7 +705,6 @@ std::string build_bvh(const HostScene& s, FlatBVH& out, int threads) {
     if (root < 0) return "";
 
     // Pre-order flatten (bvh.h:81-105): node, left subtree, right subtree.
-    out.nodes.resize(b.nodes.size());
     std::vector<int> flat_of(b.nodes.size(), -1);
     std::vector<int> order;
     order.reserve(b.nodes.size());
@@ -726,6 +718,17 @@ std::string build_bvh(const HostScene& s, FlatBVH& out, int threads) {
             if (b.nodes[n].right >= 0) st.push_back(b.nodes[n].right);
             if (b.nodes[n].left >= 0) st.push_back(b.nodes[n].left);
         }
+    }
+    out.nodes.resize(order.size());
+    {   // every primitive once, every leaf record its head + prims (one allocation each)
+        size_t np = 0, nleaf = 0;
+        for (int n : order)
+            if (b.nodes[n].left < 0 && b.nodes[n].right < 0) {
+                np += (size_t)(b.nodes[n].t1 - b.nodes[n].t0) + (size_t)(b.nodes[n].s1 - b.nodes[n].s0);
+                ++nleaf;
+            }
+        out.prims.reserve(np);
+        out.lrec.reserve(2 * nleaf + 3 * np + 3);
     }
     for (size_t f = 0; f < order.size(); ++f) {
         const BNode& n = b.nodes[order[f]];
@@ -809,9 +812,18 @@ std::string build_bvh(const HostScene& s, FlatBVH& out, int threads) {
         int top_levels = 0, top_count = 0;
         while (top_levels < 63 && top_count + per_level[top_levels] <= dl::kTopPairs && per_level[top_levels] > 0)
             top_count += per_level[top_levels++];
-        for (int lvl = 0; lvl < top_levels; ++lvl)
-            for (size_t f = 0; f < out.nodes.size(); ++f)
-                if (out.nodes[f].b >= 0 && depth[f] == lvl) pair_of[f] = npairs++;
+        // level by level, each level left to right (= pre-order within a level): breadth-first
+        std::vector<int> cur, nxt;
+        if (!out.nodes.empty() && out.nodes[0].b >= 0) cur.push_back(0);
+        for (int lvl = 0; lvl < top_levels && !cur.empty(); ++lvl) {
+            nxt.clear();
+            for (int f : cur) {
+                pair_of[f] = npairs++;
+                if (out.nodes[f + 1].b >= 0) nxt.push_back(f + 1);
+                if (out.nodes[out.nodes[f].a].b >= 0) nxt.push_back(out.nodes[f].a);
+            }
+            cur.swap(nxt);
+        }
         out.top_pairs = npairs;
         for (size_t f = 0; f < out.nodes.size(); ++f)
             if (out.nodes[f].b >= 0 && pair_of[f] < 0) pair_of[f] = npairs++;
@@ -853,7 +865,7 @@ std::string build_bvh(const HostScene& s, FlatBVH& out, int threads) {
     out.flat_ms = std::chrono::duration<double, std::milli>(t1 - t0).count() - out.ref_ms;
     auto shadow = [&out, &stree_ms] {
         const auto ts = std::chrono::steady_clock::now();
-        build_shadow_tree(out, out.threads);
+        build_shadow_tree(out, std::max(1, out.threads - out.threads / 4));   // the wide tree's quantization takes the rest
         stree_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - ts).count();
     };
     std::future<void> fs;
@@ -882,6 +894,11 @@ std::string build_bvh(const HostScene& s, FlatBVH& out, int threads) {
 // boxes above them, so shadow rays visit far fewer nodes with the same
 // answers.  Kernels use it only for NaN-free rays outside counting passes.
 void build_shadow_tree(FlatBVH& out, int threads) {
+    const auto T0 = std::chrono::steady_clock::now();
+    auto since = [](std::chrono::steady_clock::time_point t) {
+        return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t).count();
+    };
+    double t_sah = 0, t_shape = 0;
     struct Leaf { float lo[3], hi[3], c[3]; int32_t info, rec; };
     std::vector<Leaf> leaves;
     auto add_leaf = [&](const float* lo, const float* hi, int32_t info, int32_t rec) {
@@ -959,27 +976,39 @@ void build_shadow_tree(FlatBVH& out, int threads) {
         const int kBins = std::min(kMaxBins, e - b);   // O(n) per node: small nodes use fewer bins
         double best = 1e300;
         int best_axis = -1, best_split = 0;
-        // only the kBins bins in use are initialised (most nodes are small)
-        alignas(Box) unsigned char bb_raw[3 * kMaxBins * sizeof(Box)];
+        // only the kBins bins in use are initialised (most nodes are small).  Large nodes bin into two
+        // interleaved copies (even / odd items) merged afterwards: neighbouring leaves fall in the same bin,
+        // and one copy makes every grow wait on the previous one's stores.  (min / max of the same values in
+        // any order: the same box.)
+        const int ncopy = e - b >= 256 ? 2 : 1;
+        alignas(Box) unsigned char bb_raw[2 * 3 * kMaxBins * sizeof(Box)];
         Box* const bb = reinterpret_cast<Box*>(bb_raw);
-        int cnt[3][kMaxBins];
+        int cnt[2][3][kMaxBins];
         double ext[3];
         bool live[3];
         for (int a = 0; a < 3; ++a) {
             ext[a] = (double)cb.hi[a] - cb.lo[a];
             live[a] = ext[a] > 0;
-            for (int k = 0; k < kBins; ++k) { new (&bb[a * kMaxBins + k]) Box(); cnt[a][k] = 0; }
+            for (int cp = 0; cp < ncopy; ++cp)
+                for (int k = 0; k < kBins; ++k) { new (&bb[(cp * 3 + a) * kMaxBins + k]) Box(); cnt[cp][a][k] = 0; }
         }
         for (int i = b; i < e; ++i) {
             const Leaf& l = lv[i];
+            const int cp = ncopy > 1 ? (i & 1) : 0;
             for (int a = 0; a < 3; ++a) {
                 if (!live[a]) continue;
                 int k = (int)((l.c[a] - cb.lo[a]) / ext[a] * kBins);
                 k = std::min(kBins - 1, std::max(0, k));
-                bb[a * kMaxBins + k].grow(l.lo, l.hi);
-                cnt[a][k]++;
+                bb[(cp * 3 + a) * kMaxBins + k].grow(l.lo, l.hi);
+                cnt[cp][a][k]++;
             }
         }
+        if (ncopy > 1)
+            for (int a = 0; a < 3; ++a)
+                for (int k = 0; k < kBins; ++k) {
+                    bb[a * kMaxBins + k].grow(bb[(3 + a) * kMaxBins + k].lo, bb[(3 + a) * kMaxBins + k].hi);
+                    cnt[0][a][k] += cnt[1][a][k];
+                }
         for (int a = 0; a < 3; ++a) {
             if (!live[a]) continue;
             const Box* const ba = bb + a * kMaxBins;
@@ -988,16 +1017,16 @@ void build_shadow_tree(FlatBVH& out, int threads) {
             Box acc;
             int n = 0;
             for (int k = kBins - 1; k > 0; --k) {
-                if (cnt[a][k]) acc.grow(ba[k].lo, ba[k].hi);
-                n += cnt[a][k];
+                if (cnt[0][a][k]) acc.grow(ba[k].lo, ba[k].hi);
+                n += cnt[0][a][k];
                 right_area[k] = acc.area();
                 right_cnt[k] = n;
             }
             Box lacc;
             int ln = 0;
             for (int k = 1; k < kBins; ++k) {
-                if (cnt[a][k - 1]) lacc.grow(ba[k - 1].lo, ba[k - 1].hi);
-                ln += cnt[a][k - 1];
+                if (cnt[0][a][k - 1]) lacc.grow(ba[k - 1].lo, ba[k - 1].hi);
+                ln += cnt[0][a][k - 1];
                 if (ln == 0 || right_cnt[k] == 0) continue;
                 const double cost = lacc.area() * ln + right_area[k] * right_cnt[k];
                 if (cost < best) { best = cost; best_axis = a; best_split = k; }
@@ -1036,10 +1065,12 @@ void build_shadow_tree(FlatBVH& out, int threads) {
         tn[me].axis = axis;
         return me;
     };
+    const double t_leaves = since(T0);
     std::vector<TNode> tn(2 * leaves.size());
     Sah top{leaves, fork_depth(threads), tn, 0, +sah_build};
     const int root = top.build(0, (int)leaves.size(), 0, 0);
     out.smax_depth = top.smax_depth;
+    t_sah = since(T0);
     // pairs in pre-order of interior nodes
     std::vector<int32_t> pair_of(tn.size(), -1);
     int32_t np = 0;
@@ -1118,9 +1149,11 @@ void build_shadow_tree(FlatBVH& out, int threads) {
         *stack = nch - 1 + deepest;        // a step pushes at most n - 1, then goes below one
         return me;
     };
+    const double t_pairs = since(T0);
     int stack = 0;
     out.swroot = shape(root, &stack);
     out.swmax_stack = stack + 1;
+    t_shape = since(T0);
     out.swnodes.resize(shapes.size());
     std::vector<char> qok(shapes.size(), 1);
     parallel_for((int)shapes.size(), threads, [&](int i) {
@@ -1136,6 +1169,9 @@ void build_shadow_tree(FlatBVH& out, int threads) {
         out.swnodes[i] = w;
     });
     for (char q : qok) contain_ok = contain_ok && q;
+    if (std::getenv("RT_BUILD_TRACE"))          // diagnostics: the occlusion tree's phases, ms from its start
+        std::fprintf(stderr, "stree: leaves %.2f sah %.2f pairs %.2f shape %.2f quantize %.2f (%zu leaves, %zu nodes)\n",
+                     t_leaves, t_sah, t_pairs, t_shape, since(T0), leaves.size(), shapes.size());
     if (!contain_ok || out.swmax_stack > dl::kMaxStack) out.swnodes.clear();   // binary occlusion tree only
 }
 
@@ -1230,7 +1266,7 @@ bool build_ref_wide(FlatBVH& out) {
     out.wmax_stack = stack + 1;
     out.wnodes.resize(shapes.size());
     std::vector<char> nok(shapes.size(), 1);
-    parallel_for((int)shapes.size(), out.threads, [&](int idx) {
+    parallel_for((int)shapes.size(), std::max(1, out.threads / 4), [&](int idx) {   // beside the occlusion tree's build
         const Shape& sh = shapes[idx];
         const int n = sh.n;
         bool good = true;
