@@ -1,6 +1,7 @@
 // XML scene loader, triangle preparation and bit-exact BVH builder (host).
 #include "host_scene.hpp"
 
+#include <atomic>
 #include <cfloat>
 #include <algorithm>
 #include <chrono>
@@ -381,16 +382,15 @@ struct BNode {
     int t0 = 0, t1 = 0, s0 = 0, s1 = 0;   // leaf: its triangles pt[t0, t1), spheres ps[s0, s1)
 };
 
-// Fork-join depth for `threads` workers: subtrees above it are built as
-// concurrent tasks (each into its own node pool, spliced afterwards).  The
-// tree depends only on the split rule, never on thread timing.
-int fork_depth(int threads) {
-    // 2^d concurrent tasks for `threads` threads, no more: every task is a thread, and a process held to
-    // a CPU quota (a cgroup share of a larger host, as on the GPU boxes) is throttled once it runs more
-    // threads than its share
-    int d = 0;
-    while ((2 << d) <= threads && d < 6) ++d;
-    return threads <= 1 ? 0 : d;
+
+// Dynamic fork-join: a split starts its right half on a new thread while `spare` (the threads the build
+// may still start) allows, so the biggest subtrees get the threads whatever the split balance; the task
+// gives its thread back when done.  The trees do not depend on it (every subtree owns fixed node slots).
+constexpr int kForkMinSah = 1024;
+inline bool take_thread(std::atomic<int>* spare) {
+    if (spare->fetch_sub(1) > 0) return true;
+    spare->fetch_add(1);
+    return false;
 }
 
 // fn(i) for i in [0, n) on `threads` threads (contiguous chunks; fn must only write item i's outputs).
@@ -425,7 +425,7 @@ struct TriBox { float lo[3], hi[3], c[3]; };
 // two vectors), so a leaf's range lists its primitives in the reference's
 // order.  Subtrees below a split touch disjoint ranges, so the top levels run
 // as concurrent tasks, each into its own node pool (spliced afterwards).
-constexpr int kForkMin = 2048;   // a split forks only when both sides have this many primitives
+constexpr int kForkMin = 1024;   // a split forks only when both sides have this many primitives
 
 class Builder {
   public:
@@ -433,9 +433,9 @@ class Builder {
     // (n >= 1) has at most 2n - 1 nodes, so rooted at slot `at` it owns [at, at + 2n - 1) -- the left
     // subtree from at + 1, the right one from at + 2 nl -- and concurrent subtrees write disjoint slots
     // (unused slots stay default nodes, never reached from the root)
-    Builder(const HostScene& s, const std::vector<TriBox>& tb, std::vector<int>& pt, std::vector<int>& ps, int fork,
-            std::vector<BNode>& nodes)
-        : nodes(nodes), s_(s), tb_(tb), pt_(pt), ps_(ps), fork_(fork) {}
+    Builder(const HostScene& s, const std::vector<TriBox>& tb, std::vector<int>& pt, std::vector<int>& ps,
+            std::atomic<int>* spare, std::vector<BNode>& nodes)
+        : nodes(nodes), s_(s), tb_(tb), pt_(pt), ps_(ps), spare_(spare) {}
     std::vector<BNode>& nodes;
 
     int build(int t0, int t1, int s0, int s1, int depth, int at) {
@@ -459,9 +459,13 @@ class Builder {
         int r, l;
         const int nl = (tm - t0) + (sm - s0), nr = (t1 - tm) + (s1 - sm);
         const int lat = at + 1, rat = at + 2 * nl;
-        if (depth < fork_ && std::min(nl, nr) >= kForkMin) {
-            Builder rb(s_, tb_, pt_, ps_, fork_, nodes);
-            auto fr = std::async(std::launch::async, [&] { return rb.build(tm, t1, sm, s1, depth + 1, rat); });
+        if (std::min(nl, nr) >= kForkMin && take_thread(spare_)) {
+            Builder rb(s_, tb_, pt_, ps_, spare_, nodes);
+            auto fr = std::async(std::launch::async, [&] {
+                const int v = rb.build(tm, t1, sm, s1, depth + 1, rat);
+                spare_->fetch_add(1);
+                return v;
+            });
             l = build(t0, tm, s0, sm, depth + 1, lat);
             r = fr.get();
         } else {
@@ -478,7 +482,7 @@ class Builder {
     const std::vector<TriBox>& tb_;
     std::vector<int>& pt_;
     std::vector<int>& ps_;
-    int fork_;
+    std::atomic<int>* spare_;
     std::vector<int> scratch_;
 
     // Scene::getBoundingBox + extendBoundingBox (parser.h:272-317)
@@ -693,7 +697,8 @@ std::string build_bvh(const HostScene& s, FlatBVH& out, int threads) {
     for (size_t i = 0; i < pt.size(); ++i) pt[i] = (int)i;
     for (size_t i = 0; i < ps.size(); ++i) ps[i] = (int)i;
     std::vector<BNode> bnodes(std::max<size_t>(1, 2 * (pt.size() + ps.size())));
-    Builder b(s, tb, pt, ps, fork_depth(out.threads), bnodes);
+    std::atomic<int> spare(std::max(0, out.threads - 1));
+    Builder b(s, tb, pt, ps, &spare, bnodes);
     const int root = b.build(0, (int)pt.size(), 0, (int)ps.size(), 0, 0);
     out.ref_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
 
@@ -949,7 +954,7 @@ void build_shadow_tree(FlatBVH& out, int threads) {
     // as concurrent tasks that write disjoint slots, with no per-task pools to splice.
     struct Sah {
         std::vector<Leaf>& lv;
-        int fork;
+        std::atomic<int>* spare;   // threads that may still be started (a task returns its own when done)
         std::vector<TNode>& tn;
         int smax_depth = 0;
         int (*fn)(Sah&, int, int, int, int);
@@ -1012,23 +1017,27 @@ void build_shadow_tree(FlatBVH& out, int threads) {
         for (int a = 0; a < 3; ++a) {
             if (!live[a]) continue;
             const Box* const ba = bb + a * kMaxBins;
+            // (an area is recomputed only where its box grew: an empty bin leaves it, and the empty box's
+            // area is 0)
             double right_area[kMaxBins];
             int right_cnt[kMaxBins];
             Box acc;
+            double ra = 0.0;
             int n = 0;
             for (int k = kBins - 1; k > 0; --k) {
-                if (cnt[0][a][k]) acc.grow(ba[k].lo, ba[k].hi);
+                if (cnt[0][a][k]) { acc.grow(ba[k].lo, ba[k].hi); ra = acc.area(); }
                 n += cnt[0][a][k];
-                right_area[k] = acc.area();
+                right_area[k] = ra;
                 right_cnt[k] = n;
             }
             Box lacc;
+            double la = 0.0;
             int ln = 0;
             for (int k = 1; k < kBins; ++k) {
-                if (cnt[0][a][k - 1]) lacc.grow(ba[k - 1].lo, ba[k - 1].hi);
+                if (cnt[0][a][k - 1]) { lacc.grow(ba[k - 1].lo, ba[k - 1].hi); la = lacc.area(); }
                 ln += cnt[0][a][k - 1];
                 if (ln == 0 || right_cnt[k] == 0) continue;
-                const double cost = lacc.area() * ln + right_area[k] * right_cnt[k];
+                const double cost = la * ln + right_area[k] * right_cnt[k];
                 if (cost < best) { best = cost; best_axis = a; best_split = k; }
             }
         }
@@ -1049,10 +1058,14 @@ void build_shadow_tree(FlatBVH& out, int threads) {
             if (mid == b || mid == e) mid = (b + e) / 2;
         }
         int l, r;
-        if (depth < me_.fork && std::min(mid - b, e - mid) >= 512) {
-            Sah rb{lv, me_.fork, tn, 0, me_.fn};
+        if (std::min(mid - b, e - mid) >= kForkMinSah && take_thread(me_.spare)) {
+            Sah rb{lv, me_.spare, tn, 0, me_.fn};
             const int rat = at + 2 * (mid - b);
-            auto fr = std::async(std::launch::async, [&rb, mid, e, depth, rat] { return rb.build(mid, e, depth + 1, rat); });
+            auto fr = std::async(std::launch::async, [&rb, mid, e, depth, rat] {
+                const int v = rb.build(mid, e, depth + 1, rat);
+                rb.spare->fetch_add(1);
+                return v;
+            });
             l = me_.build(b, mid, depth + 1, at + 1);
             r = fr.get();
             me_.smax_depth = std::max(me_.smax_depth, rb.smax_depth);
@@ -1067,7 +1080,8 @@ void build_shadow_tree(FlatBVH& out, int threads) {
     };
     const double t_leaves = since(T0);
     std::vector<TNode> tn(2 * leaves.size());
-    Sah top{leaves, fork_depth(threads), tn, 0, +sah_build};
+    std::atomic<int> spare(std::max(0, threads - 1));
+    Sah top{leaves, &spare, tn, 0, +sah_build};
     const int root = top.build(0, (int)leaves.size(), 0, 0);
     out.smax_depth = top.smax_depth;
     t_sah = since(T0);
