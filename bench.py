@@ -60,7 +60,7 @@ HBM_SPEC_GBPS = 8000.0     # MI355X spec (MI355X_MICROARCH.md §HBM); the line p
 B_NODE, B_TRI, B_SPH, B_PIX = 32, 36, 16, 3
 
 
-def kernel_bytes(r: dict, c: dict, out_pixels: int, batched: bool) -> dict:
+def kernel_bytes(r: dict, c: dict, out_pixels: int, batched: bool, nlights: int) -> dict:
     """Algorithmic bytes of one frame per kernel of the chain path (pathchain.hip), from a
     production-fetch counting pass: `r` = its per-role counter slots (Scene.counters_raw: the bytes
     each role's walks fetch -- wide-node lines, leaf records, primitives -- and its ray / hit counts),
@@ -69,7 +69,8 @@ def kernel_bytes(r: dict, c: dict, out_pixels: int, batched: bool) -> dict:
     the record's first 16 B and the normal, and its 1-B result written; a skipped one (light_needed)
     writes its 1-B result; a continuation id is written in phase A and read in phase B with its
     record and normal; packing reads and writes each task id; k_finish reads every sample's path
-    word (4 B) and every hit's record, normal and occlusion dwords (8 B), and writes 3 B per pixel.
+    word (4 B) and every hit's record, normal and occlusion dword(s) (4 B when the record's bytes sit in one
+    dword: 1, 2 or 4 lights; else 8), and writes 3 B per pixel.
     One frame alone, A's shadow rays run in k_mix's shadow role; in frame batches in k_occlude."""
     REC, NRM, TASK, OCC = 32, 16, 4, 1
     samples, skipped = c["primary_rays"], c["shadow_rays_skipped"]
@@ -84,7 +85,8 @@ def kernel_bytes(r: dict, c: dict, out_pixels: int, batched: bool) -> dict:
         "k_occlude_a": r["a_shadow_bytes"] + a_sh * shadow_ws,
         "k_pack_b": bo * 2 * TASK,
         "k_occlude_b": r["bo_shadow_bytes"] + bo * shadow_ws,
-        "k_finish": samples * 4 + (r["a_hits"] + r["b_hits"]) * (REC + NRM + 8) + out_pixels * 3,
+        "k_finish": samples * 4 + (r["a_hits"] + r["b_hits"]) * (REC + NRM + (4 if nlights in (1, 2, 4) else 8))
+                    + out_pixels * 3,
     }
     if not batched:                       # one frame: A's shadow rays are k_mix's shadow role
         k["k_mix"] += k.pop("k_occlude_a")
@@ -294,7 +296,8 @@ def main() -> int:
         raise RuntimeError(f"production counting pass disagrees on ray counts: {pcnt} vs {cnt}")
     if traversal_bytes(roles) != pcnt["node_visits"]:
         raise RuntimeError(f"per-role fetch bytes do not add up: {roles} vs {pcnt['node_visits']}")
-    kbytes = kernel_bytes(roles, cnt, rows * W, batched=F > 1)
+    nlights = len(re.findall(r"<PointLight\b", Path(xml).read_text()))
+    kbytes = kernel_bytes(roles, cnt, rows * W, batched=F > 1, nlights=nlights)
     alg_bytes = sum(kbytes.values())
     trav_bytes = traversal_bytes(roles)
     ws_bytes = alg_bytes - trav_bytes

@@ -1873,7 +1873,8 @@ __device__ __forceinline__ OccRaw occ_load(const PcParams& p, unsigned rid, int 
     if (SMALL) {
         const uint32_t* wd = reinterpret_cast<const uint32_t*>(p.occ) + (o.off >> 2);
         o.w0 = wd[0];
-        o.w1 = wd[1];
+        // the second dword only when the record's bytes cross into it (never for 1, 2 or 4 lights)
+        o.w1 = (o.off & 3u) + (unsigned)nl > 4u ? wd[1] : 0u;
     } else {
         o.w0 = o.w1 = 0;
     }
