@@ -663,7 +663,17 @@ bool quantize_wide(const float (*lo)[3], const float (*hi)[3], int n, unsigned m
 
 }  // namespace
 
-void build_shadow_tree(FlatBVH& out, int threads);
+// One reference leaf under the occlusion tree: its exact box, the box centre, and the leaf's flat
+// (pre-order) node index, resolved to its info word and leaf record once the flatten is done.
+struct ShadowLeaf { float lo[3], hi[3], c[3]; int32_t f; };
+// The flatten's per-node results the occlusion tree's finish reads, valid once ready() returns true
+// (false: the flatten failed and there is nothing to finish).
+struct FlatHandoff {
+    std::function<bool()> ready;
+    const std::vector<int32_t>* leaf_info;
+    const std::vector<int32_t>* lrec_of;
+};
+void build_shadow_tree(FlatBVH& out, int threads, std::vector<ShadowLeaf>& leaves, const FlatHandoff& flat);
 bool build_ref_wide(FlatBVH& out);
 
 int build_threads(int requested) {
@@ -724,7 +734,93 @@ std::string build_bvh(const HostScene& s, FlatBVH& out, int threads) {
             if (b.nodes[n].left >= 0) st.push_back(b.nodes[n].left);
         }
     }
-    out.nodes.resize(order.size());
+    // Child-pair layout: one pair per interior node.  The top levels (every
+    // walk passes through them) are numbered first, breadth-first, so a
+    // kernel can cache pairs [0, top_pairs) in LDS; the rest follow in
+    // pre-order, which keeps a node's left-child pair next to its own.  The
+    // numbering needs only the tree's shape (interior f: left child f + 1,
+    // right child rchild[f]; a leaf: -1), so it comes before the flatten, and
+    // so can the occlusion tree's SAH, which reads the leaves in pair order.
+    const size_t nn = order.size();
+    std::vector<int32_t> rchild(nn, -1);
+    for (size_t f = 0; f < nn; ++f) {
+        const BNode& n = b.nodes[order[f]];
+        if (!(n.left < 0 && n.right < 0)) rchild[f] = flat_of[n.right];   // bvh.h:107-109
+    }
+    std::vector<int32_t> pair_of(nn, -1), pair_node;
+    int32_t npairs = 0;
+    {
+        std::vector<int> depth(nn, 0);
+        std::vector<int> per_level(64, 0);
+        for (size_t f = 0; f < nn; ++f) {
+            if (rchild[f] < 0) continue;
+            per_level[std::min(depth[f], 63)]++;
+            depth[f + 1] = depth[f] + 1;
+            depth[rchild[f]] = depth[f] + 1;
+        }
+        int top_levels = 0, top_count = 0;
+        while (top_levels < 63 && top_count + per_level[top_levels] <= dl::kTopPairs && per_level[top_levels] > 0)
+            top_count += per_level[top_levels++];
+        // level by level, each level left to right (= pre-order within a level): breadth-first
+        std::vector<int> cur, nxt;
+        if (rchild[0] >= 0) cur.push_back(0);
+        for (int lvl = 0; lvl < top_levels && !cur.empty(); ++lvl) {
+            nxt.clear();
+            for (int f : cur) {
+                pair_of[f] = npairs++;
+                if (rchild[f + 1] >= 0) nxt.push_back(f + 1);
+                if (rchild[rchild[f]] >= 0) nxt.push_back(rchild[f]);
+            }
+            cur.swap(nxt);
+        }
+        out.top_pairs = npairs;
+        for (size_t f = 0; f < nn; ++f)
+            if (rchild[f] >= 0 && pair_of[f] < 0) pair_of[f] = npairs++;
+        pair_node.resize(npairs);
+        for (size_t f = 0; f < nn; ++f)
+            if (pair_of[f] >= 0) pair_node[pair_of[f]] = (int32_t)f;
+    }
+    // The occlusion tree's leaves: every leaf child of a pair, in pair order (left, then right).
+    std::vector<ShadowLeaf> sleaves;
+    sleaves.reserve((size_t)npairs + 1);
+    auto add_leaf = [&](int32_t f) {
+        const BNode& n = b.nodes[order[f]];
+        const float lo[3] = {(float)n.lo.x, (float)n.lo.y, (float)n.lo.z};
+        const float hi[3] = {(float)n.hi.x, (float)n.hi.y, (float)n.hi.z};
+        ShadowLeaf l;
+        for (int a = 0; a < 3; ++a) { l.lo[a] = lo[a]; l.hi[a] = hi[a]; l.c[a] = 0.5f * (lo[a] + hi[a]); }
+        l.f = f;
+        sleaves.push_back(l);
+    };
+    for (int32_t i = 0; i < npairs; ++i) {
+        const int32_t f = pair_node[i];
+        if (rchild[f + 1] < 0) add_leaf(f + 1);
+        if (rchild[rchild[f]] < 0) add_leaf(rchild[f]);
+    }
+    // Large scenes build the occlusion tree's SAH in its own task while this thread flattens; the task
+    // then waits for the flatten's leaf info words and records (flat_done; false when the flatten fails,
+    // set on every return by `release`) to finish its pairs and wide nodes.
+    std::vector<int32_t> leaf_info(nn, 0), lrec_of(nn, -1);
+    std::promise<bool> flat_done;
+    std::shared_future<bool> flat_ready = flat_done.get_future().share();
+    const FlatHandoff hand{[flat_ready] { return flat_ready.get(); }, &leaf_info, &lrec_of};
+    double stree_ms = 0.0;
+    const int sthreads = std::max(1, out.threads - out.threads / 4);   // the wide tree's quantization takes the rest
+    auto shadow = [&out, &stree_ms, &sleaves, &hand, sthreads] {
+        const auto ts = std::chrono::steady_clock::now();
+        build_shadow_tree(out, sthreads, sleaves, hand);
+        stree_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - ts).count();
+    };
+    std::future<void> fs;
+    struct Release {
+        std::promise<bool>& p;
+        bool done = false;
+        void operator()(bool ok) { if (!done) { done = true; p.set_value(ok); } }
+        ~Release() { (*this)(false); }   // before fs joins the task (declared after it)
+    } release{flat_done};
+    if (out.threads > 1 && npairs >= 4096) fs = std::async(std::launch::async, shadow);   // large scenes
+
+    out.nodes.resize(nn);
     {   // every primitive once, every leaf record its head + prims (one allocation each)
         size_t np = 0, nleaf = 0;
         for (int n : order)
@@ -780,7 +876,6 @@ std::string build_bvh(const HostScene& s, FlatBVH& out, int threads) {
     // Leaf records (dl::LeafHead + copies of the leaf's prims), one per
     // reference leaf in pre-order (the closest-hit walk's visit order), shared
     // by both 4-wide trees.
-    std::vector<int32_t> lrec_of(out.nodes.size(), -1);
     bool lrec_ok = true;
     for (size_t f = 0; f < out.nodes.size(); ++f) {
         const dl::Node& n = out.nodes[f];
@@ -798,41 +893,6 @@ std::string build_bvh(const HostScene& s, FlatBVH& out, int threads) {
     }
     out.lrec.resize(out.lrec.size() + 3);    // a leaf's first-prim loads may run past a 0-prim last leaf
 
-    // Child-pair layout: one pair per interior node.  The top levels (every
-    // walk passes through them) are numbered first, breadth-first, so a
-    // kernel can cache pairs [0, top_pairs) in LDS; the rest follow in
-    // pre-order, which keeps a node's left-child pair next to its own.
-    std::vector<int32_t> pair_of(out.nodes.size(), -1);
-    int32_t npairs = 0;
-    {
-        std::vector<int> depth(out.nodes.size(), 0);
-        std::vector<int> per_level(64, 0);
-        for (size_t f = 0; f < out.nodes.size(); ++f) {
-            const dl::Node& n = out.nodes[f];
-            if (n.b < 0) continue;
-            per_level[std::min(depth[f], 63)]++;
-            depth[f + 1] = depth[f] + 1;
-            depth[n.a] = depth[f] + 1;
-        }
-        int top_levels = 0, top_count = 0;
-        while (top_levels < 63 && top_count + per_level[top_levels] <= dl::kTopPairs && per_level[top_levels] > 0)
-            top_count += per_level[top_levels++];
-        // level by level, each level left to right (= pre-order within a level): breadth-first
-        std::vector<int> cur, nxt;
-        if (!out.nodes.empty() && out.nodes[0].b >= 0) cur.push_back(0);
-        for (int lvl = 0; lvl < top_levels && !cur.empty(); ++lvl) {
-            nxt.clear();
-            for (int f : cur) {
-                pair_of[f] = npairs++;
-                if (out.nodes[f + 1].b >= 0) nxt.push_back(f + 1);
-                if (out.nodes[out.nodes[f].a].b >= 0) nxt.push_back(out.nodes[f].a);
-            }
-            cur.swap(nxt);
-        }
-        out.top_pairs = npairs;
-        for (size_t f = 0; f < out.nodes.size(); ++f)
-            if (out.nodes[f].b >= 0 && pair_of[f] < 0) pair_of[f] = npairs++;
-    }
     auto info_of = [&](size_t f) -> int32_t {
         const dl::Node& n = out.nodes[f];
         if (n.b >= 0) return pair_of[f];
@@ -856,6 +916,8 @@ std::string build_bvh(const HostScene& s, FlatBVH& out, int threads) {
         p.r_maxx = R.maxx; p.r_maxy = R.maxy; p.r_maxz = R.maxz; p.pad = 0;
         out.pair_lrec[2 * pair_of[f]] = lrec_of[f + 1];
         out.pair_lrec[2 * pair_of[f] + 1] = lrec_of[n.a];
+        if (L.b < 0) leaf_info[f + 1] = p.l_info;
+        if (R.b < 0) leaf_info[n.a] = p.r_info;
     }
     if ((int)out.leaf_big.size() > dl::kLeafStartMask) return "Error: too many large BVH leaves";
     out.root_lo[0] = out.nodes[0].minx; out.root_lo[1] = out.nodes[0].miny; out.root_lo[2] = out.nodes[0].minz;
@@ -863,18 +925,11 @@ std::string build_bvh(const HostScene& s, FlatBVH& out, int threads) {
     out.root_info = info_of(0);
     out.root_lrec = lrec_of[0];
     if (!lrec_ok) out.lrec.clear();                  // no 4-wide trees: the binary trees only
+    release(true);
     // The occlusion tree (its own task when threads allow) and the reference-order wide tree are
     // independent: both read the pairs and leaf records, each writes only its own fields.
     const auto t1 = std::chrono::steady_clock::now();
-    double stree_ms = 0.0;
     out.flat_ms = std::chrono::duration<double, std::milli>(t1 - t0).count() - out.ref_ms;
-    auto shadow = [&out, &stree_ms] {
-        const auto ts = std::chrono::steady_clock::now();
-        build_shadow_tree(out, std::max(1, out.threads - out.threads / 4));   // the wide tree's quantization takes the rest
-        stree_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - ts).count();
-    };
-    std::future<void> fs;
-    if (out.threads > 1 && out.pairs.size() >= 4096) fs = std::async(std::launch::async, shadow);   // large scenes
     if (!build_ref_wide(out) || out.lrec.empty()) out.wnodes.clear();
     out.refwide_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t1).count();
     if (fs.valid()) fs.get(); else shadow();
@@ -898,36 +953,18 @@ std::string build_bvh(const HostScene& s, FlatBVH& out, int threads) {
 // exact leaf boxes, tested exactly) and puts a binned-SAH hierarchy of union
 // boxes above them, so shadow rays visit far fewer nodes with the same
 // answers.  Kernels use it only for NaN-free rays outside counting passes.
-void build_shadow_tree(FlatBVH& out, int threads) {
+void build_shadow_tree(FlatBVH& out, int threads, std::vector<ShadowLeaf>& leaves, const FlatHandoff& flat) {
     const auto T0 = std::chrono::steady_clock::now();
     auto since = [](std::chrono::steady_clock::time_point t) {
         return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t).count();
     };
-    double t_sah = 0, t_shape = 0;
-    struct Leaf { float lo[3], hi[3], c[3]; int32_t info, rec; };
-    std::vector<Leaf> leaves;
-    auto add_leaf = [&](const float* lo, const float* hi, int32_t info, int32_t rec) {
-        Leaf l;
-        for (int a = 0; a < 3; ++a) { l.lo[a] = lo[a]; l.hi[a] = hi[a]; l.c[a] = 0.5f * (lo[a] + hi[a]); }
-        l.info = info;
-        l.rec = rec;
-        leaves.push_back(l);
-    };
-    for (size_t i = 0; i < out.pairs.size(); ++i) {
-        const dl::Pair& p = out.pairs[i];
-        if (p.l_info < 0) {
-            const float lo[3] = {p.l_minx, p.l_miny, p.l_minz}, hi[3] = {p.l_maxx, p.l_maxy, p.l_maxz};
-            add_leaf(lo, hi, p.l_info, out.pair_lrec[2 * i]);
-        }
-        if (p.r_info < 0) {
-            const float lo[3] = {p.r_minx, p.r_miny, p.r_minz}, hi[3] = {p.r_maxx, p.r_maxy, p.r_maxz};
-            add_leaf(lo, hi, p.r_info, out.pair_lrec[2 * i + 1]);
-        }
-    }
-    for (int a = 0; a < 3; ++a) { out.sroot_lo[a] = out.root_lo[a]; out.sroot_hi[a] = out.root_hi[a]; }
+    double t_sah = 0, t_wait = 0, t_shape = 0;
+    using Leaf = ShadowLeaf;
     out.spairs.clear();
     out.smax_depth = 0;
     if (leaves.size() < 2) {           // empty tree or a single root leaf: same as the reference
+        if (!flat.ready()) return;
+        for (int a = 0; a < 3; ++a) { out.sroot_lo[a] = out.root_lo[a]; out.sroot_hi[a] = out.root_hi[a]; }
         out.sroot_info = out.root_info;
         return;
     }
@@ -973,8 +1010,7 @@ void build_shadow_tree(FlatBVH& out, int threads) {
         const int me = at;
         tn[me] = node;
         if (e - b == 1) {
-            tn[me].info = lv[b].info;
-            tn[me].rec = lv[b].rec;
+            tn[me].rec = lv[b].f;          // the flat index until the flatten's words resolve it
             return me;
         }
         constexpr int kMaxBins = 32;
@@ -1078,13 +1114,20 @@ void build_shadow_tree(FlatBVH& out, int threads) {
         tn[me].axis = axis;
         return me;
     };
-    const double t_leaves = since(T0);
     std::vector<TNode> tn(2 * leaves.size());
     std::atomic<int> spare(std::max(0, threads - 1));
     Sah top{leaves, &spare, tn, 0, +sah_build};
     const int root = top.build(0, (int)leaves.size(), 0, 0);
     out.smax_depth = top.smax_depth;
     t_sah = since(T0);
+    if (!flat.ready()) return;
+    t_wait = since(T0);
+    for (size_t n = 0; n + 1 < tn.size(); ++n)     // the 2L - 1 nodes: leaf info words and records
+        if (tn[n].left < 0) {
+            const int32_t f = tn[n].rec;
+            tn[n].info = (*flat.leaf_info)[f];
+            tn[n].rec = (*flat.lrec_of)[f];
+        }
     // pairs in pre-order of interior nodes
     std::vector<int32_t> pair_of(tn.size(), -1);
     int32_t np = 0;
@@ -1184,8 +1227,8 @@ void build_shadow_tree(FlatBVH& out, int threads) {
     });
     for (char q : qok) contain_ok = contain_ok && q;
     if (std::getenv("RT_BUILD_TRACE"))          // diagnostics: the occlusion tree's phases, ms from its start
-        std::fprintf(stderr, "stree: leaves %.2f sah %.2f pairs %.2f shape %.2f quantize %.2f (%zu leaves, %zu nodes)\n",
-                     t_leaves, t_sah, t_pairs, t_shape, since(T0), leaves.size(), shapes.size());
+        std::fprintf(stderr, "stree: sah %.2f flatten-wait %.2f pairs %.2f shape %.2f quantize %.2f (%zu leaves, %zu nodes)\n",
+                     t_sah, t_wait, t_pairs, t_shape, since(T0), leaves.size(), shapes.size());
     if (!contain_ok || out.swmax_stack > dl::kMaxStack) out.swnodes.clear();   // binary occlusion tree only
 }
 
