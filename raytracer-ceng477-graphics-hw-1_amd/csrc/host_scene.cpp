@@ -820,36 +820,50 @@ std::string build_bvh(const HostScene& s, FlatBVH& out, int threads) {
     } release{flat_done};
     if (out.threads > 1 && npairs >= 4096) fs = std::async(std::launch::async, shadow);   // large scenes
 
+    // Flatten.  A serial pass in pre-order gives every leaf its first prim slot and its leaf-record
+    // offset (the order a serial fill pushes them in) and checks the encodings; the nodes, prims, leaf
+    // records and pairs are then filled in parallel (beside the occlusion tree's SAH when it runs).
     out.nodes.resize(nn);
-    {   // every primitive once, every leaf record its head + prims (one allocation each)
-        size_t np = 0, nleaf = 0;
-        for (int n : order)
-            if (b.nodes[n].left < 0 && b.nodes[n].right < 0) {
-                np += (size_t)(b.nodes[n].t1 - b.nodes[n].t0) + (size_t)(b.nodes[n].s1 - b.nodes[n].s0);
-                ++nleaf;
-            }
-        out.prims.reserve(np);
-        out.lrec.reserve(2 * nleaf + 3 * np + 3);
+    bool lrec_ok = true;
+    {
+        size_t np = 0, nrec = 0;
+        for (size_t f = 0; f < nn; ++f) {
+            const BNode& n = b.nodes[order[f]];
+            out.max_depth = std::max(out.max_depth, n.depth);
+            if (rchild[f] >= 0) continue;
+            const int ntri = n.t1 - n.t0, nsph = n.s1 - n.s0;
+            if (ntri > dl::kNtriMask || nsph > dl::kMaxLeafSpheres)
+                return "Error: BVH leaf exceeds the device encoding limits";
+            out.leaves++;
+            out.max_leaf = std::max(out.max_leaf, ntri + nsph);
+            dl::Node& o = out.nodes[f];
+            o.a = (int32_t)np;
+            o.b = dl::kLeafBit | ((int32_t)nsph << dl::kNtriBits) | (int32_t)ntri;
+            const size_t count = (size_t)(ntri + nsph);
+            // Leaf records (dl::LeafHead + copies of the leaf's prims), one per reference leaf in
+            // pre-order (the closest-hit walk's visit order), shared by both 4-wide trees
+            if (nrec > (size_t)INT32_MAX - 1 - (2 + 3 * count)) lrec_ok = false;
+            lrec_of[f] = (int32_t)nrec;
+            np += count;
+            nrec += 2 + 3 * count;
+        }
+        out.prims.resize(np);
+        // (+ 3: a leaf's first-prim loads may run past a 0-prim last leaf)
+        out.lrec.resize(lrec_ok ? nrec + 3 : 0);
     }
-    for (size_t f = 0; f < order.size(); ++f) {
+    (void)ibits; (void)fbits;
+    const int fth = fs.valid() ? std::max(1, out.threads / 4) : out.threads;   // the SAH task has the rest
+    parallel_for((int)nn, fth, [&](int f) {
         const BNode& n = b.nodes[order[f]];
         dl::Node& o = out.nodes[f];
         o.minx = n.lo.x; o.miny = n.lo.y; o.minz = n.lo.z;
         o.maxx = n.hi.x; o.maxy = n.hi.y; o.maxz = n.hi.z;
-        out.max_depth = std::max(out.max_depth, n.depth);
-        const bool leaf = n.left < 0 && n.right < 0;                 // bvh.h:107-109
-        if (!leaf) {
-            o.a = flat_of[n.right];
+        if (rchild[f] >= 0) {                                        // bvh.h:107-109
+            o.a = rchild[f];
             o.b = n.axis;
-            continue;
+            return;
         }
-        const int ntri = n.t1 - n.t0, nsph = n.s1 - n.s0;
-        if (ntri > dl::kNtriMask || nsph > dl::kMaxLeafSpheres)
-            return "Error: BVH leaf exceeds the device encoding limits";
-        out.leaves++;
-        out.max_leaf = std::max(out.max_leaf, ntri + nsph);
-        o.a = (int32_t)out.prims.size();
-        o.b = dl::kLeafBit | ((int32_t)nsph << dl::kNtriBits) | (int32_t)ntri;
+        dl::Prim* pp = out.prims.data() + o.a;
         for (int j = n.t0; j < n.t1; ++j) {
             const int t = pt[j];
             const TriRec& tr = s.tris[t];
@@ -858,7 +872,7 @@ std::string build_bvh(const HostScene& s, FlatBVH& out, int threads) {
             p.p0x = a.x; p.p0y = a.y; p.p0z = a.z; p.id = t;
             p.p1x = a.x - bb.x; p.p1y = a.y - bb.y; p.p1z = a.z - bb.z; p.p1w = 0;
             p.p2x = a.x - c.x; p.p2y = a.y - c.y; p.p2z = a.z - c.z; p.p2w = 0;
-            out.prims.push_back(p);
+            *pp++ = p;
         }
         for (int j = n.s0; j < n.s1; ++j) {
             const int k = ps[j];
@@ -868,45 +882,39 @@ std::string build_bvh(const HostScene& s, FlatBVH& out, int threads) {
             p.p0x = c.x; p.p0y = c.y; p.p0z = c.z; p.id = ~k;   // negative id marks a sphere
             p.p1x = sp.radius; p.p1y = sp.radius * sp.radius; p.p1z = 0; p.p1w = 0;
             p.p2x = 0; p.p2y = 0; p.p2z = 0; p.p2w = sp.material_id;
-            out.prims.push_back(p);
+            *pp++ = p;
         }
-    }
-    (void)ibits; (void)fbits;
-
-    // Leaf records (dl::LeafHead + copies of the leaf's prims), one per
-    // reference leaf in pre-order (the closest-hit walk's visit order), shared
-    // by both 4-wide trees.
-    bool lrec_ok = true;
-    for (size_t f = 0; f < out.nodes.size(); ++f) {
-        const dl::Node& n = out.nodes[f];
-        if (n.b >= 0) continue;
-        const int32_t count = (n.b & dl::kNtriMask) + ((n.b >> dl::kNtriBits) & dl::kMaxLeafSpheres);
-        const size_t off = out.lrec.size();
-        if (off > (size_t)INT32_MAX - 1 - (2 + 3 * (size_t)count)) lrec_ok = false;
+        if (!lrec_ok) return;
+        const int32_t count = (o.b & dl::kNtriMask) + ((o.b >> dl::kNtriBits) & dl::kMaxLeafSpheres);
         dl::LeafHead h{};
-        h.minx = n.minx; h.miny = n.miny; h.minz = n.minz; h.count = count;
-        h.maxx = n.maxx; h.maxy = n.maxy; h.maxz = n.maxz; h.slot0 = n.a;
-        out.lrec.resize(off + 2 + 3 * (size_t)count);
+        h.minx = o.minx; h.miny = o.miny; h.minz = o.minz; h.count = count;
+        h.maxx = o.maxx; h.maxy = o.maxy; h.maxz = o.maxz; h.slot0 = o.a;
+        const size_t off = (size_t)lrec_of[f];
         std::memcpy(&out.lrec[off], &h, sizeof(h));
-        if (count > 0) std::memcpy(&out.lrec[off + 2], &out.prims[n.a], sizeof(dl::Prim) * (size_t)count);
-        lrec_of[f] = (int32_t)off;
-    }
-    out.lrec.resize(out.lrec.size() + 3);    // a leaf's first-prim loads may run past a 0-prim last leaf
+        if (count > 0) std::memcpy(&out.lrec[off + 2], &out.prims[o.a], sizeof(dl::Prim) * (size_t)count);
+    });
 
-    auto info_of = [&](size_t f) -> int32_t {
+    // a leaf's info word: inline (count and first prim slot) or an index into leaf_big, assigned in the
+    // order a serial pairs fill meets the leaves (each leaf is one pair's child; the root last)
+    auto leaf_word = [&](size_t f) -> int32_t {
         const dl::Node& n = out.nodes[f];
-        if (n.b >= 0) return pair_of[f];
         const int32_t count = (n.b & dl::kNtriMask) + ((n.b >> dl::kNtriBits) & dl::kMaxLeafSpheres);
         if (count >= 1 && count <= dl::kLeafMaxCount && n.a <= dl::kLeafStartMask)
             return dl::kLeafBit | (count << dl::kLeafCountShift) | n.a;
         out.leaf_big.push_back(dl::LeafBig{n.a, count});
         return dl::kLeafBit | (int32_t)(out.leaf_big.size() - 1);
     };
+    for (size_t f = 0; f < nn; ++f) {
+        if (rchild[f] < 0) continue;
+        if (rchild[f + 1] < 0) leaf_info[f + 1] = leaf_word(f + 1);
+        if (rchild[rchild[f]] < 0) leaf_info[rchild[f]] = leaf_word(rchild[f]);
+    }
+    auto info_of = [&](size_t f) -> int32_t { return rchild[f] >= 0 ? pair_of[f] : leaf_info[f]; };
     out.pairs.resize(npairs);
     out.pair_lrec.assign(2 * (size_t)npairs, -1);
-    for (size_t f = 0; f < out.nodes.size(); ++f) {
+    parallel_for((int)nn, fth, [&](int f) {
         const dl::Node& n = out.nodes[f];
-        if (n.b < 0) continue;
+        if (n.b < 0) return;
         const dl::Node& L = out.nodes[f + 1];
         const dl::Node& R = out.nodes[n.a];
         dl::Pair& p = out.pairs[pair_of[f]];
@@ -916,13 +924,11 @@ std::string build_bvh(const HostScene& s, FlatBVH& out, int threads) {
         p.r_maxx = R.maxx; p.r_maxy = R.maxy; p.r_maxz = R.maxz; p.pad = 0;
         out.pair_lrec[2 * pair_of[f]] = lrec_of[f + 1];
         out.pair_lrec[2 * pair_of[f] + 1] = lrec_of[n.a];
-        if (L.b < 0) leaf_info[f + 1] = p.l_info;
-        if (R.b < 0) leaf_info[n.a] = p.r_info;
-    }
+    });
     if ((int)out.leaf_big.size() > dl::kLeafStartMask) return "Error: too many large BVH leaves";
     out.root_lo[0] = out.nodes[0].minx; out.root_lo[1] = out.nodes[0].miny; out.root_lo[2] = out.nodes[0].minz;
     out.root_hi[0] = out.nodes[0].maxx; out.root_hi[1] = out.nodes[0].maxy; out.root_hi[2] = out.nodes[0].maxz;
-    out.root_info = info_of(0);
+    out.root_info = rchild[0] >= 0 ? pair_of[0] : (leaf_info[0] = leaf_word(0));
     out.root_lrec = lrec_of[0];
     if (!lrec_ok) out.lrec.clear();                  // no 4-wide trees: the binary trees only
     release(true);
@@ -1011,6 +1017,30 @@ void build_shadow_tree(FlatBVH& out, int threads, std::vector<ShadowLeaf>& leave
         tn[me] = node;
         if (e - b == 1) {
             tn[me].rec = lv[b].f;          // the flat index until the flatten's words resolve it
+            return me;
+        }
+        if (e - b == 2) {
+            // two leaves: what the binned code below gives, without its bins.  Each live axis puts the
+            // leaves in bins 0 and 1 at the same cost (the two leaf areas), so the first live axis wins
+            // the strict comparison; the leaf of bin 0 goes left; no finite cost (or no live axis): a
+            // count split on axis 0 with the leaves as they are.
+            int axis = -1;
+            for (int a = 0; a < 3 && axis < 0; ++a)
+                if ((double)cb.hi[a] - cb.lo[a] > 0) axis = a;
+            Box A, B;
+            A.grow(lv[b].lo, lv[b].hi);
+            B.grow(lv[b + 1].lo, lv[b + 1].hi);
+            if (axis >= 0 && A.area() * 1 + B.area() * 1 < 1e300) {
+                const double ex = (double)cb.hi[axis] - cb.lo[axis];
+                int k = (int)((lv[b].c[axis] - cb.lo[axis]) / ex * 2);
+                k = std::min(1, std::max(0, k));
+                if (k != 0) std::swap(lv[b], lv[b + 1]);
+            } else {
+                axis = 0;
+            }
+            tn[me].left = me_.build(b, b + 1, depth + 1, at + 1);
+            tn[me].right = me_.build(b + 1, e, depth + 1, at + 2);
+            tn[me].axis = axis;
             return me;
         }
         constexpr int kMaxBins = 32;
