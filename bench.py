@@ -64,29 +64,37 @@ def kernel_bytes(r: dict, c: dict, out_pixels: int, batched: bool, nlights: int)
     """Algorithmic bytes of one frame per kernel of the chain path (pathchain.hip), from a
     production-fetch counting pass: `r` = its per-role counter slots (Scene.counters_raw: the bytes
     each role's walks fetch -- wide-node lines, leaf records, primitives -- and its ray / hit counts),
-    `c` = the reference's counters.  Workspace traffic per item: a hit writes its 32-B record and reads
-    its 16-B face normal (TriShade); a traced shadow task id is written (4 B), read by its walker with
-    the record's first 16 B and the normal, and its 1-B result written; a skipped one (light_needed)
-    writes its 1-B result; a continuation id is written in phase A and read in phase B with its
-    record and normal; packing reads and writes each task id; k_finish reads every sample's path
-    word (4 B) and every hit's record, normal and occlusion dword(s) (4 B when the record's bytes sit in one
-    dword: 1, 2 or 4 lights; else 8), and writes 3 B per pixel.
+    `c` = the reference's counters.  Workspace traffic per item: a hit writes its record -- 16 B in
+    phase A (compact records, pathchain.hpp dbase: hit point and surface code), 32 B in phase B (with
+    the direction and material) -- and reads its 16-B face normal (TriShade); a traced shadow task id
+    is written (4 B), read by its walker with the record's first 16 B and the normal, and its 1-B
+    result written; a skipped one (light_needed) writes its 1-B result; a continuation id and its
+    direction word (16 B, tail) are written in phase A and read in phase B with its record and normal;
+    packing reads and writes each task id (in frame batches only the continuations'); k_finish reads every sample's path word (4 B) and every
+    hit's record, normal and occlusion dword(s) (4 B when the record's bytes sit in one dword: 1, 2 or
+    4 lights; else 8), and writes 3 B per pixel.
     One frame alone, A's shadow rays run in k_mix's shadow role; in frame batches in k_occlude."""
-    REC, NRM, TASK, OCC = 32, 16, 4, 1
+    NRM, TASK, OCC = 16, 4, 1
+    REC_B = 32
+    REC_A = 32 if os.environ.get("RT_COMPACT", "1") == "0" else 16
+    DIRW = 16 if REC_A == 16 else 0
+    inplace = batched and os.environ.get("RT_OCC_INPLACE", "1") != "0"
     samples, skipped = c["primary_rays"], c["shadow_rays_skipped"]
     a_sh, bq, bo, conts = r["a_shadow_rays"], r["bq_shadow_rays"], r["bo_shadow_rays"], r["continuations"]
     shadow_ws = TASK + 16 + NRM + OCC
     k = {
-        "k_chain": r["a_walk_bytes"] + samples * 4 + r["a_hits"] * (REC + NRM) + a_sh * TASK + skipped * OCC
-                   + conts * TASK,
-        "k_pack_a": (a_sh + conts) * 2 * TASK,
-        "k_mix": r["b_walk_bytes"] + r["bq_shadow_bytes"] + conts * (TASK + REC + NRM) + r["b_hits"] * (REC + NRM)
-                 + bq * (16 + NRM + OCC) + bo * TASK,
+        "k_chain": r["a_walk_bytes"] + samples * 4 + r["a_hits"] * (REC_A + NRM) + a_sh * TASK + skipped * OCC
+                   + conts * (TASK + DIRW),
+        # frame batches walk A's shadow tasks in their phase-A regions (PcParams::occ_inplace): only the
+        # continuations are packed
+        "k_pack_a": ((0 if inplace else a_sh) + conts) * 2 * TASK,
+        "k_mix": r["b_walk_bytes"] + r["bq_shadow_bytes"] + conts * (TASK + 16 + DIRW + (REC_A - 16) + NRM)
+                 + r["b_hits"] * (REC_B + NRM) + bq * (16 + NRM + OCC) + bo * TASK,
         "k_occlude_a": r["a_shadow_bytes"] + a_sh * shadow_ws,
         "k_pack_b": bo * 2 * TASK,
         "k_occlude_b": r["bo_shadow_bytes"] + bo * shadow_ws,
-        "k_finish": samples * 4 + (r["a_hits"] + r["b_hits"]) * (REC + NRM + (4 if nlights in (1, 2, 4) else 8))
-                    + out_pixels * 3,
+        "k_finish": samples * 4 + r["a_hits"] * (REC_A + NRM) + r["b_hits"] * (REC_B + NRM)
+                    + (r["a_hits"] + r["b_hits"]) * (4 if nlights in (1, 2, 4) else 8) + out_pixels * 3,
     }
     if not batched:                       # one frame: A's shadow rays are k_mix's shadow role
         k["k_mix"] += k.pop("k_occlude_a")

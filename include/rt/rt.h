@@ -156,7 +156,9 @@ int rt_device_count(int* count);
  * RT_GROUP_VIRTUAL=1 rehearsal -- n ranks on device 0, device copies in place
  * of RCCL -- are tested bit-exact).  rt_render_cameras on a group renders each
  * run of consecutive same-size cameras as one frame batch on every device
- * (frames in flight together) with one grouped gather.  The asynchronous
+ * (frames in flight together) with one grouped gather (env RT_GROUP_BATCH:
+ * at most that many frames per gather; 1 = one ncclGather per call, the
+ * escape hatch while the grouped call is unrun at n > 1).  The asynchronous
  * device-buffer entry points (rt_render_device, rt_render_frames_device,
  * rt_render_cameras_device) keep using device 0 only: a one-process-per-GPU
  * caller shards with their stripe/rank arguments instead.  n = 1 runs the

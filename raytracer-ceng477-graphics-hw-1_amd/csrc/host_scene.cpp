@@ -380,6 +380,7 @@ struct BNode {
     int axis = 0, depth = 0;
     int left = -1, right = -1;
     int t0 = 0, t1 = 0, s0 = 0, s1 = 0;   // leaf: its triangles pt[t0, t1), spheres ps[s0, s1)
+    int used = 0;                         // 1: a node of the tree (unused slots stay default)
 };
 
 
@@ -443,6 +444,7 @@ class Builder {
         const int id = at;
         BNode nd;
         nd.depth = depth;
+        nd.used = 1;
         bounds(t0, t1, s0, s1, nd.lo, nd.hi);
         int tm = 0, sm = 0;
         bool leaf = (t1 - t0) + (s1 - s0) <= 1 || depth >= kMaxDepth;
@@ -718,22 +720,20 @@ std::string build_bvh(const HostScene& s, FlatBVH& out, int threads) {
         out.tri_shade[i] = dl::TriShade{t.normal.x, t.normal.y, t.normal.z, t.material_id};
     }
     if (root < 0) return "";
+    auto tms = [t0] { return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count(); };
+    double tr_num = 0, tr_sah = 0, tr_off = 0, tr_fill = 0;   // RT_BUILD_TRACE: the flatten's steps, ms from t0
 
-    // Pre-order flatten (bvh.h:81-105): node, left subtree, right subtree.
+    // Pre-order flatten (bvh.h:81-105): node, left subtree, right subtree.  That is the order of the
+    // node slots (Builder: a subtree rooted at slot `at` has its left subtree from at + 1 and its right
+    // one after the left's whole slot range), so a node's flat index is the count of used slots before it.
     std::vector<int> flat_of(b.nodes.size(), -1);
     std::vector<int> order;
     order.reserve(b.nodes.size());
-    {
-        std::vector<int> st{root};
-        while (!st.empty()) {
-            int n = st.back();
-            st.pop_back();
-            flat_of[n] = (int)order.size();
-            order.push_back(n);
-            if (b.nodes[n].right >= 0) st.push_back(b.nodes[n].right);
-            if (b.nodes[n].left >= 0) st.push_back(b.nodes[n].left);
+    for (size_t i = 0; i < b.nodes.size(); ++i)
+        if (b.nodes[i].used) {
+            flat_of[i] = (int)order.size();
+            order.push_back((int)i);
         }
-    }
     // Child-pair layout: one pair per interior node.  The top levels (every
     // walk passes through them) are numbered first, breadth-first, so a
     // kernel can cache pairs [0, top_pairs) in LDS; the rest follow in
@@ -750,14 +750,9 @@ std::string build_bvh(const HostScene& s, FlatBVH& out, int threads) {
     std::vector<int32_t> pair_of(nn, -1), pair_node;
     int32_t npairs = 0;
     {
-        std::vector<int> depth(nn, 0);
         std::vector<int> per_level(64, 0);
-        for (size_t f = 0; f < nn; ++f) {
-            if (rchild[f] < 0) continue;
-            per_level[std::min(depth[f], 63)]++;
-            depth[f + 1] = depth[f] + 1;
-            depth[rchild[f]] = depth[f] + 1;
-        }
+        for (size_t f = 0; f < nn; ++f)
+            if (rchild[f] >= 0) per_level[std::min(b.nodes[order[f]].depth, 63)]++;
         int top_levels = 0, top_count = 0;
         while (top_levels < 63 && top_count + per_level[top_levels] <= dl::kTopPairs && per_level[top_levels] > 0)
             top_count += per_level[top_levels++];
@@ -780,6 +775,7 @@ std::string build_bvh(const HostScene& s, FlatBVH& out, int threads) {
         for (size_t f = 0; f < nn; ++f)
             if (pair_of[f] >= 0) pair_node[pair_of[f]] = (int32_t)f;
     }
+    tr_num = tms();
     // The occlusion tree's leaves: every leaf child of a pair, in pair order (left, then right).
     std::vector<ShadowLeaf> sleaves;
     sleaves.reserve((size_t)npairs + 1);
@@ -819,6 +815,7 @@ std::string build_bvh(const HostScene& s, FlatBVH& out, int threads) {
         ~Release() { (*this)(false); }   // before fs joins the task (declared after it)
     } release{flat_done};
     if (out.threads > 1 && npairs >= 4096) fs = std::async(std::launch::async, shadow);   // large scenes
+    tr_sah = tms();
 
     // Flatten.  A serial pass in pre-order gives every leaf its first prim slot and its leaf-record
     // offset (the order a serial fill pushes them in) and checks the encodings; the nodes, prims, leaf
@@ -848,11 +845,15 @@ std::string build_bvh(const HostScene& s, FlatBVH& out, int threads) {
             nrec += 2 + 3 * count;
         }
         out.prims.resize(np);
-        // (+ 3: a leaf's first-prim loads may run past a 0-prim last leaf)
+        // (+ 3: a leaf's first-prim loads may run past a 0-prim last leaf; zeros)
         out.lrec.resize(lrec_ok ? nrec + 3 : 0);
+        if (lrec_ok) std::memset(out.lrec.data() + nrec, 0, 3 * sizeof(dl::Vec4));
     }
     (void)ibits; (void)fbits;
-    const int fth = fs.valid() ? std::max(1, out.threads / 4) : out.threads;   // the SAH task has the rest
+    tr_off = tms();
+    // beside the occlusion tree's SAH task (its threads take the cores) the fill runs on this thread alone:
+    // more threads only contend with it (C3 on the box: 3.1 ms with 4 threads beside it, 1.9 ms serial)
+    const int fth = fs.valid() ? 1 : out.threads;
     parallel_for((int)nn, fth, [&](int f) {
         const BNode& n = b.nodes[order[f]];
         dl::Node& o = out.nodes[f];
@@ -894,6 +895,7 @@ std::string build_bvh(const HostScene& s, FlatBVH& out, int threads) {
         if (count > 0) std::memcpy(&out.lrec[off + 2], &out.prims[o.a], sizeof(dl::Prim) * (size_t)count);
     });
 
+    tr_fill = tms();
     // a leaf's info word: inline (count and first prim slot) or an index into leaf_big, assigned in the
     // order a serial pairs fill meets the leaves (each leaf is one pair's child; the root last)
     auto leaf_word = [&](size_t f) -> int32_t {
@@ -938,8 +940,13 @@ std::string build_bvh(const HostScene& s, FlatBVH& out, int threads) {
     out.flat_ms = std::chrono::duration<double, std::milli>(t1 - t0).count() - out.ref_ms;
     if (!build_ref_wide(out) || out.lrec.empty()) out.wnodes.clear();
     out.refwide_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t1).count();
+    const double tr_wide = tms();
     if (fs.valid()) fs.get(); else shadow();
     out.stree_ms = stree_ms;
+    if (std::getenv("RT_BUILD_TRACE"))
+        std::fprintf(stderr, "build: ref %.2f numbering %.2f leaves+sah start %.2f offsets %.2f fill %.2f pairs %.2f "
+                             "refwide %.2f stree joined %.2f (ms from start)\n",
+                     out.ref_ms, tr_num, tr_sah, tr_off, tr_fill, out.ref_ms + out.flat_ms, tr_wide, tms());
     // Ordered DFS pushes two children per interior pop: stack <= depth + 2.
     out.max_stack = out.max_depth + 2;
     if (out.max_stack > dl::kMaxStack) return "Error: BVH deeper than the device stack";

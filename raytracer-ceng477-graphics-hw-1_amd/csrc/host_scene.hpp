@@ -8,7 +8,10 @@
 #pragma once
 
 #include <cstdint>
+#include <memory>
 #include <string>
+#include <type_traits>
+#include <utility>
 #include <vector>
 
 #include "device_layout.hpp"
@@ -45,34 +48,51 @@ struct HostScene {
     std::vector<SphereRec> spheres;
 };
 
+// A vector whose resize(n) leaves new elements of a trivial type uninitialized: the build writes every
+// byte of the device arrays itself (in parallel), so the serial zero-fill and its first-touch page
+// faults are not paid twice.
+template <class T>
+struct NoInitAlloc : std::allocator<T> {
+    template <class U> struct rebind { using other = NoInitAlloc<U>; };
+    NoInitAlloc() = default;
+    template <class U> NoInitAlloc(const NoInitAlloc<U>&) noexcept {}
+    template <class U> void construct(U* p) noexcept(std::is_nothrow_default_constructible<U>::value) {
+        ::new (static_cast<void*>(p)) U;
+    }
+    template <class U, class... A> void construct(U* p, A&&... a) {
+        ::new (static_cast<void*>(p)) U(std::forward<A>(a)...);
+    }
+};
+template <class T> using DevVec = std::vector<T, NoInitAlloc<T>>;
+
 // Flattened BVH in device layout.
 struct FlatBVH {
-    std::vector<dl::Node> nodes;        // pre-order, left child = i + 1
-    std::vector<dl::Prim> prims;        // leaf primitive copies, leaf-contiguous
-    std::vector<dl::TriShade> tri_shade;  // per triangle id: normal + material
+    DevVec<dl::Node> nodes;             // pre-order, left child = i + 1
+    DevVec<dl::Prim> prims;             // leaf primitive copies, leaf-contiguous
+    DevVec<dl::TriShade> tri_shade;     // per triangle id: normal + material
     // child-pair layout of the same tree (device_layout.hpp dl::Pair)
-    std::vector<dl::Pair> pairs;
+    DevVec<dl::Pair> pairs;
     std::vector<dl::LeafBig> leaf_big;
     float root_lo[3] = {0, 0, 0}, root_hi[3] = {0, 0, 0};
     int32_t root_info = 0;
     int top_pairs = 0;               // pairs [0, top_pairs) = the top levels, breadth-first
     // Occlusion tree: an SAH hierarchy over the SAME leaves (same prim ranges,
     // same exact leaf boxes) with union boxes above them (build_shadow_tree).
-    std::vector<dl::Pair> spairs;
+    DevVec<dl::Pair> spairs;
     float sroot_lo[3] = {0, 0, 0}, sroot_hi[3] = {0, 0, 0};
     int32_t sroot_info = 0;
     int smax_depth = 0;
     // leaf records (LeafHead + prims), 16-B units, one per reference leaf in
     // pre-order, + 3 units of tail pad; shared by both wide trees
-    std::vector<dl::Vec4> lrec;
+    DevVec<dl::Vec4> lrec;
     std::vector<int32_t> pair_lrec;  // [2 * pair + side]: leaf record offset of a leaf child, else -1
     int32_t root_lrec = -1;          // the root's record when the root is a leaf
     // the occlusion tree collapsed to wide nodes (any-hit walks)
-    std::vector<dl::Wide> swnodes;
+    DevVec<dl::Wide> swnodes;
     int32_t swroot = 0;              // >= 0 node index, < 0 kLeafBit | leaf-record offset
     int swmax_stack = 0;             // worst-case stack entries of a walk over them
     // the reference tree collapsed to wide nodes (closest-hit walks, reference order)
-    std::vector<dl::Wide> wnodes;
+    DevVec<dl::Wide> wnodes;
     int32_t wroot = 0;
     int wmax_stack = 0;              // worst-case stack entries of a walk over them
     int leaves = 0, max_leaf = 0, max_depth = 0, max_stack = 0;

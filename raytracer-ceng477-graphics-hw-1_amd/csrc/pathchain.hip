@@ -232,14 +232,23 @@ struct PhaseOut {              // where a chain phase writes its tasks
     int kinline;               // deepest level walked here
 };
 
-// Hit records (one per recorded level lvp = k*cap + sample), 32 bytes:
-//   rec[2*lvp]     = {hit point xyz, surface code (hit_surface: triangle index or ~sphere slot)}
-//   rec[2*lvp + 1] = {ray direction xyz, material id}
+// Hit records (one per recorded level, by record id lvp):
+//   rec[lvp]           = {hit point xyz, surface code (hit_surface: triangle index or ~sphere slot)}
+//   recd[lvp - dbase]  = {ray direction xyz, material id}, for lvp >= p.dbase only
 // The normal is not stored: surface_normal rebuilds it bit-identically from
 // the hit point and the code (a 16-byte face-normal read from the L2-resident
 // scene instead of 16 more bytes per record through HBM, written once and read
-// by every shadow task, the mirror bounce and the shading of the record).
-constexpr int kRecWords = 2;
+// by every shadow task, the mirror bounce and the shading of the record).  Nor,
+// below dbase (phase A's levels 0 and 1 of every sample, most of a frame's
+// records), are the direction and material: the direction of level 0 is the
+// sample's eye ray's and that of level 1 the reflection of level 0's (k_finish
+// path_shade_fold: the chain's arithmetic on the same values, so bit-identical),
+// the material is the surface's (surface_mat); where a phase-A record's
+// reflection is read back later (a continuation, a deferred reflected ray) the
+// chain leaves the direction in tail[sample] (reflect_from_record).  16 bytes
+// per phase-A record through HBM instead of 32, written by k_chain, read by
+// k_finish and by the shadow walks.
+
 // Record id of level k of sample `path` (continuation index c when k >= p.la): levels below la at
 // k * cap + path, deeper ones (phase B) only for the first cb continuations, after them.
 // (Record ids, and owner ids rid * nl + l, stay below 2^31: rt_api.cpp checks cap * levels * nl.)
@@ -249,9 +258,15 @@ __device__ __forceinline__ unsigned rec_id(const PcParams& p, int k, unsigned pa
 }
 __device__ __forceinline__ void rec_write(const PcParams& p, size_t lvp, const V& hitp, int code, const V& d,
                                           int mat) {
-    float4* rc = p.rec + lvp * kRecWords;
-    rc[0] = make_float4(hitp.x, hitp.y, hitp.z, __int_as_float(code));
-    rc[1] = make_float4(d.x, d.y, d.z, __int_as_float(mat));
+    p.rec[lvp] = make_float4(hitp.x, hitp.y, hitp.z, __int_as_float(code));
+    if (lvp >= p.dbase) p.recd[lvp - p.dbase] = make_float4(d.x, d.y, d.z, __int_as_float(mat));
+}
+
+// The surface's material id (hit_surface's *mat): the triangle's shading word, or the sphere
+// primitive's material word.
+__device__ __forceinline__ int surface_mat(const rtk::DevScene& s, int code) {
+    if (code >= 0) return __float_as_int(ld4(&s.tri_shade[code]).w);
+    return __float_as_int(reinterpret_cast<const float4*>(&s.prims[~code])[2].w);
 }
 
 // Can light l's shadow ray from this hit change the pixel?  The shading
@@ -281,11 +296,14 @@ __device__ __forceinline__ Ray reflect_ray(const rtk::DevScene& s, const V& hitp
     return make_ray(pnt, add(d2, mul(mul(n2, 2.0f), rcos)));
 }
 
-// Reflected ray of recorded level lvp.
-__device__ __forceinline__ Ray reflect_from_record(const rtk::DevScene& s, const PcParams& p, size_t lvp) {
-    const float4* rc = p.rec + lvp * kRecWords;
-    const float4 a = rc[0], c = rc[1];
+// Reflected ray of recorded level lvp of sample `path`.  A phase-A record below dbase has no direction;
+// the chain left it in tail[path] where a reflection is read back (a continuation handed to phase B or
+// k_fallback, or a deferred reflected ray), tail's colour use coming later (k_fallback's kEndTail).
+__device__ __forceinline__ Ray reflect_from_record(const rtk::DevScene& s, const PcParams& p, size_t lvp,
+                                                   unsigned path) {
+    const float4 a = p.rec[lvp];
     const V hitp{a.x, a.y, a.z};
+    const float4 c = lvp >= p.dbase ? p.recd[lvp - p.dbase] : p.tail[path];
     return reflect_ray(s, hitp, surface_normal(s, hitp, __float_as_int(a.w)), V{c.x, c.y, c.z});
 }
 
@@ -304,7 +322,7 @@ __device__ __forceinline__ Ray shadow_from_record(const rtk::DevScene& s, const 
                                                   float* tlim) {
     const unsigned lvp = owner / (unsigned)s.nlights;
     const int l = (int)(owner - lvp * (unsigned)s.nlights);
-    const float4 a = p.rec[(size_t)lvp * kRecWords];
+    const float4 a = p.rec[lvp];
     const V hitp{a.x, a.y, a.z};
     return shadow_ray(s, hitp, surface_normal(s, hitp, __float_as_int(a.w)), l, tlim);
 }
@@ -344,7 +362,7 @@ __device__ __forceinline__ Ray shadow_from_record_l2(const rtk::DevScene& s, con
                                                      float* tlim) {
     const unsigned lvp = owner / (unsigned)s.nlights;
     const int l = (int)(owner - lvp * (unsigned)s.nlights);
-    const float4 a = ld4_l2(p.rec + (size_t)lvp * kRecWords);
+    const float4 a = ld4_l2(p.rec + lvp);
     const V hitp{a.x, a.y, a.z};
     return shadow_ray(s, hitp, surface_normal(s, hitp, __float_as_int(a.w)), l, tlim);
 }
@@ -400,7 +418,7 @@ __device__ __forceinline__ Ray shadow_from_record(const rtk::DevScene& s, const 
                                                   float* tlim, const UDiv& nl) {
     const unsigned lvp = nl.div(owner);
     const int l = (int)(owner - lvp * nl.d);
-    const float4 a = p.rec[(size_t)lvp * kRecWords];
+    const float4 a = p.rec[lvp];
     const V hitp{a.x, a.y, a.z};
     return shadow_ray(s, hitp, surface_normal(s, hitp, __float_as_int(a.w)), l, tlim);
 }
@@ -845,7 +863,7 @@ constexpr int kCoop = 3;
 // ublk_w units wide, so the units in flight (a launch-wide counter: the whole GPU on them at once)
 // cover a column of the image instead of a full-width band (C3, 256-px columns a frame high: ~1 %
 // per batched frame, ~2 % one frame).  Identity when ublk_h == 0 or the units do not tile the rows.
-__device__ __forceinline__ unsigned unit_order(const PcParams& p, unsigned u, unsigned units) {
+__device__ __forceinline__ unsigned unit_col_order(const PcParams& p, unsigned u, unsigned units) {
     const unsigned upr = (unsigned)p.tiles_x / 4u;
     if (p.ublk_h == 0 || (p.tiles_x & 3) || units % upr) return u;
     const unsigned rows = units / upr, bw = (unsigned)p.ublk_w;
@@ -855,6 +873,19 @@ __device__ __forceinline__ unsigned unit_order(const PcParams& p, unsigned u, un
     const unsigned c0 = i / (h * bw) * bw, w = min(bw, upr - c0);
     const unsigned l = i - c0 * h;
     return (r0 + l / w) * upr + c0 + l % w;
+}
+// The unit of deal number u (a launch-wide counter), kUidNone once there is none: with uorder_on the
+// previous frame's hot units first, then the column order without them (a skipped unit costs one more
+// deal); else the column order.
+__device__ __forceinline__ unsigned unit_deal(const PcParams& p, unsigned units) {
+    const unsigned H = p.uorder_on ? min(units, __hip_atomic_load(p.uhcount_r, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) : 0u;
+    while (true) {
+        const unsigned u = atomicAdd(&p.totals[3], 1u);
+        if (u < H) return p.uhot_r[u];
+        if (u >= units + H) return kUidNone;
+        const unsigned c = unit_col_order(p, u - H, units);
+        if (H == 0u || p.umark_r[c] != p.ugen - 1u) return c;
+    }
 }
 
 // closest-hit chains of one phase (raytracer.cpp:385-439 minus the shading):
@@ -886,6 +917,7 @@ __device__ void chain_body(const rtk::DevScene& s, const rtk::Eye& e, const PcPa
     Walk wk;
     unsigned t_grab = 0, tsteps = 0, twit = 0, wit = 0;   // trace: grab time, own steps, wave steps
     unsigned apoll = 0;      // phase A: iterations since the last look at the finished-wave count (p.abandon)
+    unsigned ssteps = 0;     // phase A (p.urank): walk steps of the lane's current sample
     bool fresh = false;      // lane just took an eye ray (packet walk pending)
     StepStat stat;
     // cooperative tail walks (lone-frame phase B: coop_round): the group walk this lane works on, the
@@ -965,19 +997,29 @@ __device__ void chain_body(const rtk::DevScene& s, const rtk::Eye& e, const PcPa
                 const unsigned base = wave_grab_lds(&g_ccnt, cm);
                 o.cq[(size_t)blk * o.ccap + base + lane_rank(cm)] = (unsigned)((size_t)k * p.cap + path);
                 p.pinfo[path] = kPathCont;        // continued in phase B (finish_pixels' order)
+                if (lvp < p.dbase) p.tail[path] = make_float4(r.d.x, r.d.y, r.d.z, 0.0f);   // reflect_from_record
             }
             if (ends || handoff) {
                 st = kIdle;
+                if (!CONT && !COUNT && p.urank && ssteps >= kHotSteps) {   // the unit is hot: listed once
+                    const unsigned u = path >> 8;
+                    if (atomicMax(&p.umark_w[u], p.ugen) != p.ugen) {
+                        const unsigned i = atomicAdd(p.uhcount_w, 1u);
+                        if (i < ((unsigned)p.n0 + 255u) / 256u) p.uhot_w[i] = u;   // (at most once per unit)
+                    }
+                }
                 if (p.trace && !CONT) { p.trace[2 * path] = t_grab; p.trace[2 * path + 1] = (unsigned)wall_clock64(); }
                 if (p.trace && CONT) {       // phase B: {grab, end, last level, walk steps} after A's entries
                     unsigned* tb = p.trace + 2 * ((size_t)p.cap + p.trace_blocks) + 4 * (size_t)path;
                     tb[0] = t_grab; tb[1] = (unsigned)wall_clock64(); tb[2] = (unsigned)k | ((wit - twit) << 8); tb[3] = tsteps;
                 }
             } else {
+                const V dk = r.d;
                 r = reflect_ray(s, hitp, nn, r.d);
                 ++k;
                 nrefl++;
                 if (!COUNT && defer_closest(s, r)) {     // the rest of this path: k_fallback
+                    if (lvp < p.dbase) p.tail[path] = make_float4(dk.x, dk.y, dk.z, 0.0f);   // reflect_from_record
                     fb_chain(p, (unsigned)lvp);
                     st = kIdle;
                 } else {
@@ -1007,8 +1049,7 @@ __device__ void chain_body(const rtk::DevScene& s, const rtk::Eye& e, const PcPa
                                 if (spin_over(s, n)) { late = true; break; }
                                 __builtin_amdgcn_s_sleep(1);
                             }
-                        const unsigned u = late ? units : atomicAdd(&p.totals[3], 1u);
-                        lds_store(&g_uid[jf], u < units ? unit_order(p, u, units) : kUidNone);
+                        lds_store(&g_uid[jf], late ? kUidNone : unit_deal(p, units));
                     }
                     const unsigned v = base + lane_rank(idle);
                     if (st == kIdle && v < nb) {
@@ -1033,9 +1074,9 @@ __device__ void chain_body(const rtk::DevScene& s, const rtk::Eye& e, const PcPa
                             path = eye ? lvp & ~kFbEye : lvp % (unsigned)p.cap;
                             k = eye ? 0 : (int)(lvp / (unsigned)p.cap) + 1;
                             if (eye) {
-                                slab_sample_ray(e, p, path, &r);
+                                slab_sample_ray(p, path, &r);
                             } else {
-                                r = reflect_from_record(s, p, lvp);
+                                r = reflect_from_record(s, p, lvp, path);
                                 nrefl++;
                             }
                             if (!COUNT && defer_closest(s, r)) fb_chain(p, lvp);   // (an eye entry keeps its kFbEye bit)
@@ -1043,9 +1084,10 @@ __device__ void chain_body(const rtk::DevScene& s, const rtk::Eye& e, const PcPa
                             coop_ok = true;
                         } else {
                             const unsigned idx = (dyn ? uid : blk + (v >> 8) * G) * 256u + (v & 255u);
-                            if (slab_sample_ray(e, p, idx, &r)) {
+                            if (slab_sample_ray(p, idx, &r)) {
                                 path = idx;
                                 k = 0;
+                                ssteps = 0;
                                 if (p.trace) t_grab = (unsigned)wall_clock64();
                                 nprim++;
                                 if (s.max_depth < 0) p.pinfo[path] = 0 | (kEndZero << 8);   // depth 0 > max: black
@@ -1108,6 +1150,7 @@ __device__ void chain_body(const rtk::DevScene& s, const rtk::Eye& e, const PcPa
             if (CONT && p.trace) ++wit;
             if (st == kTrav) {
                 if (CONT && p.trace) ++tsteps;
+                if (!CONT) ++ssteps;
                 if (closest_step_timed<COUNT, CONT>(s, r, stk, wk, w) || walk_runaway(s, wk)) st = kDone;
             }
         }
@@ -1517,8 +1560,9 @@ __device__ void pack_region(const unsigned* q, unsigned cap, const unsigned* cnt
 
 // After phase A: pack its shadow tasks and continuations (one workgroup per region).
 __global__ __launch_bounds__(kBlock) void k_pack_a(PcParams p) {
-    pack_region(p.sqA, p.scapA, p.scntA, p.grid, p.sflatA, &p.totals[0], blockIdx.x);
+    if (!p.occ_inplace) pack_region(p.sqA, p.scapA, p.scntA, p.grid, p.sflatA, &p.totals[0], blockIdx.x);
     pack_region(p.cq, p.ccapA, p.ccnt, p.grid, p.cflat, &p.totals[1], blockIdx.x, p.cid, (unsigned)p.cap);
+    if (p.urank && blockIdx.x == 0 && threadIdx.x == 0) *p.uhcount_r = 0;   // k_chain is done with it: the next frame's count
 }
 __global__ __launch_bounds__(kBlock) void k_pack_b(PcParams p) {
     pack_region(p.sqB, p.scapB, p.scntB, p.gb, p.sflatB, &p.totals[2], blockIdx.x);
@@ -1558,8 +1602,22 @@ template <bool COUNT>
 __global__ __launch_bounds__(kBlock, RT_OCC_WAVES_PER_EU) void k_occlude(rtk::DevScene s, PcParams p, int which) {
     block_init(s);
     if constexpr (!COUNT && RT_LEAF_QUEUE) {
-        if (which) occlude_queue_body(s, p, blockIdx.x, gridDim.x, p.sflatB, p.totals[2]);
-        else occlude_queue_body(s, p, blockIdx.x, gridDim.x, p.sflatA, p.totals[0]);
+        if (which) {
+            occlude_queue_body(s, p, blockIdx.x, gridDim.x, p.sflatB, p.totals[2]);
+        } else if (p.occ_inplace) {
+            // A's tasks where k_chain left them: phase-A region r (k_chain workgroup r's queue) to
+            // workgroup r mod G, one region at a time (no packed copy of 4 B in and out per task)
+            for (unsigned r = blockIdx.x; r < (unsigned)p.grid; r += gridDim.x) {
+                if (r != blockIdx.x) {
+                    __syncthreads();            // every wave is done with the previous region
+                    if (threadIdx.x == 0) g_head = 0;
+                    __syncthreads();
+                }
+                occlude_queue_body(s, p, 0, 1, p.sqA + (size_t)r * p.scapA, p.scntA[r]);
+            }
+        } else {
+            occlude_queue_body(s, p, blockIdx.x, gridDim.x, p.sflatA, p.totals[0]);
+        }
     } else {
         if (which) occlude_body<COUNT>(s, p, blockIdx.x, gridDim.x, p.sflatB, p.totals[2], 1);
         else occlude_body<COUNT>(s, p, blockIdx.x, gridDim.x, p.sflatA, p.totals[0], 0);
@@ -1672,7 +1730,7 @@ __global__ __launch_bounds__(kBlock, RT_WAVES_PER_EU) void k_fused(rtk::DevScene
                         const unsigned v = gb + lane_rank(idle);
                         if (v < nb) {
                             const unsigned idx = block_sample(v, G, (unsigned)p.n0, (unsigned)p.spread);
-                            if (slab_sample_ray(e, p, idx, &r)) {
+                            if (slab_sample_ray(p, idx, &r)) {
                                 path = idx;
                                 k = 0;
                                 nprim++;
@@ -1737,7 +1795,7 @@ __global__ __launch_bounds__(kBlock, RT_WAVES_PER_EU) void k_fused(rtk::DevScene
                         owner = qbase[(size_t)gq * p.wq_cap + gt + rank];
                         const unsigned lvp = owner / (unsigned)nl;
                         const int l = (int)(owner - lvp * (unsigned)nl);
-                        const float4 a = p.rec[(size_t)lvp * kRecWords];
+                        const float4 a = p.rec[lvp];
                         const V hitp{a.x, a.y, a.z};
                         const V pnt = add(hitp, mul(surface_normal(s, hitp, __float_as_int(a.w)), s.eps));   // :397
                         const float4 lp = ld4(&s.lights[l].px);
@@ -1846,13 +1904,13 @@ __device__ __forceinline__ V shade_core(const rtk::DevScene& s, const V hitp, co
     return L;
 }
 
-// The same for record rid from its already-loaded words: occ bit l set = light l occluded (lights >= 32
-// read their byte directly).
+// The same for record rid from its already-loaded words (hit point a.xyz, ray direction dir): occ bit
+// l set = light l occluded (lights >= 32 read their byte directly).
 template <bool LDS>
 __device__ __forceinline__ V shade_words(const rtk::DevScene& s, const PcParams& p, unsigned rid, const float4 a,
-                                         const V n_, const float4 c, const float4 mA, const float4 mD,
+                                         const V n_, const V dir, const float4 mA, const float4 mD,
                                          const float4 mS, uint32_t occ32) {
-    return shade_core<LDS>(s, V{a.x, a.y, a.z}, V{c.x, c.y, c.z}, n_, mA, mD, mS, [&](int l) {
+    return shade_core<LDS>(s, V{a.x, a.y, a.z}, dir, n_, mA, mD, mS, [&](int l) {
         return (LDS || l < 32) ? ((occ32 >> l) & 1u) != 0 : p.occ[(size_t)rid * s.nlights + l] != 0;
     });
 }
@@ -1897,8 +1955,13 @@ __device__ __forceinline__ uint32_t occ_bits(const PcParams& p, const OccRaw& o,
 // Shade and fold one sample's recorded levels deepest-first, the next
 // (shallower) level's record and occlusion bytes in flight while the current
 // one is shaded: c_k = clamp(L_k + c_{k+1} (x) km_k) (raytracer.cpp:436-451).
-template <bool LDS>
-__device__ __forceinline__ V path_shade_fold(const rtk::DevScene& s, const PcParams& p, unsigned path) {
+// Compact phase-A levels (k < ca <= kCompactLevels, PcParams::dbase) get their
+// direction words when they come up: level 0's direction is the sample's eye
+// ray's, level 1's its reflection at level 0 (the chain's own arithmetic
+// on the same values), their materials the surfaces' (surface_mat).
+template <bool LDS, bool CMP>
+__device__ __forceinline__ V path_shade_fold(const rtk::DevScene& s, const rtk::Eye& e, const PcParams& p,
+                                             unsigned path) {
     const int info = p.pinfo[path];
     const int nlev = info & 0xff, kind = (info >> 8) & 0xff;
     V c = kind == kEndBg ? V{s.bgx, s.bgy, s.bgz} : V{0.0f, 0.0f, 0.0f};
@@ -1908,28 +1971,46 @@ __device__ __forceinline__ V path_shade_fold(const rtk::DevScene& s, const PcPar
     }
     if (nlev == 0) return c;
     const int nl = s.nlights;
+    const int ca = CMP ? min(nlev, p.clevels) : 0;   // (k_finish<.., false>: launches without compact records)
+    auto compact_d = [&](int k, const float4 ak) {   // {direction, material} of compact level k (record ak)
+        Ray r0;
+        slab_sample_ray(p, path, &r0);      // the sample's eye ray, from the slot (nothing held for it)
+        V dk = r0.d;
+        if (kCompactLevels > 1 && k == 1) {
+            const float4 a0 = p.rec[path];
+            const V h0{a0.x, a0.y, a0.z};
+            dk = reflect_ray(s, h0, surface_normal(s, h0, __float_as_int(a0.w)), dk).d;
+        }
+        return make_float4(dk.x, dk.y, dk.z, __int_as_float(surface_mat(s, __float_as_int(ak.w))));
+    };
     const unsigned cx = nlev > p.la ? p.cid[path] : 0u;   // continued paths: their phase-B records
     unsigned rid = rec_id(p, nlev - 1, path, cx);
-    float4 a = p.rec[(size_t)rid * kRecWords], d = p.rec[(size_t)rid * kRecWords + 1];
+    float4 a = p.rec[rid], ds = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+    if (nlev - 1 >= ca) ds = p.recd[rid - p.dbase];
     OccRaw oc = occ_load<LDS>(p, rid, nl);
     for (int k = nlev - 1; k >= 0; --k) {
+        const float4 d = k < ca ? compact_d(k, a) : ds;
         const dl::Material& M = fin_mat<LDS>(s, __float_as_int(d.w) - 1);   // before the prefetch (vmcnt order)
         const float4 mA = ld4(&M.kax), mD = ld4(&M.kdx), mS = ld4(&M.ksx), km = ld4(&M.kmx);
         const V n_ = surface_normal(s, V{a.x, a.y, a.z}, __float_as_int(a.w));
         // the next (shallower) record: phase-B ids step down by cb, phase-A ids are (k-1) * cap + path
         const unsigned rn = k - 1 >= p.la ? rid - p.cb : (unsigned)max(k - 1, 0) * (unsigned)p.cap + path;
+        const bool stored = !CMP || k - 1 >= ca;   // the next level's record has its direction word
 #if RT_FINISH_PREFETCH
-        const float4 na = p.rec[(size_t)rn * kRecWords], nd = p.rec[(size_t)rn * kRecWords + 1];
+        const float4 na = p.rec[rn];
+        float4 nd = ds;
+        if (stored) nd = p.recd[rn - p.dbase];
         const OccRaw noc = occ_load<LDS>(p, rn, nl);
 #endif
-        const V L = shade_words<LDS>(s, p, rid, a, n_, d, mA, mD, mS, occ_bits<LDS>(p, oc, nl));
+        const V L = shade_words<LDS>(s, p, rid, a, n_, V{d.x, d.y, d.z}, mA, mD, mS, occ_bits<LDS>(p, oc, nl));
         if (kind == kEndLast && k == nlev - 1) c = vclamp(L, 0.0f, FLT_MAX);
         else c = vclamp(add(L, had(c, V{km.x, km.y, km.z})), 0.0f, FLT_MAX);
 #if RT_FINISH_PREFETCH
-        rid = rn; a = na; d = nd; oc = noc;
+        rid = rn; a = na; ds = nd; oc = noc;
 #else
         if (k > 0) {
-            rid = rn; a = p.rec[(size_t)rn * kRecWords]; d = p.rec[(size_t)rn * kRecWords + 1];
+            rid = rn; a = p.rec[rn];
+            if (stored) ds = p.recd[rn - p.dbase];
             oc = occ_load<LDS>(p, rn, nl);
         }
 #endif
@@ -1938,8 +2019,9 @@ __device__ __forceinline__ V path_shade_fold(const rtk::DevScene& s, const PcPar
 }
 
 // One output pixel (rr, ocol) of the chunk: its F x F samples shaded, folded, quantised and averaged.
-template <bool LDS>
-__device__ __forceinline__ void finish_pixel(const rtk::DevScene& s, const PcParams& p, int rr, int ocol) {
+template <bool LDS, bool CMP>
+__device__ __forceinline__ void finish_pixel(const rtk::DevScene& s, const rtk::Eye& e, const PcParams& p, int rr,
+                                             int ocol) {
     const int F = p.aa;
     const int lr = p.chunk_row0 / p.aa + rr;
     if (lr >= p.slab_rows) return;
@@ -1951,7 +2033,7 @@ __device__ __forceinline__ void finish_pixel(const rtk::DevScene& s, const PcPar
     uint32_t sr = 0, sg = 0, sb = 0;
     for (int k = 0; k < F; ++k)
         for (int l = 0; l < F; ++l) {
-            const V c = path_shade_fold<LDS>(s, p, slab_slot(p.tiles_x, ocol * F + l, rr * F + k));
+            const V c = path_shade_fold<LDS, CMP>(s, e, p, slab_slot(p.tiles_x, ocol * F + l, rr * F + k));
             sr += quantise(c.x); sg += quantise(c.y); sb += quantise(c.z);
         }
     const uint32_t ff = (uint32_t)(F * F);
@@ -1962,8 +2044,8 @@ __device__ __forceinline__ void finish_pixel(const rtk::DevScene& s, const PcPar
 // p.fin_cont (chain path): the pixels of the paths continued in phase B first (cflat, totals[1] of
 // them; each pixel once, by the lane holding its first continued sample), so their long folds
 // overlap the rest; then every pixel without a continued sample (pinfo's kPathCont bit)
-template <bool LDS>
-__device__ __forceinline__ void finish_pixels(const rtk::DevScene& s, const PcParams& p) {
+template <bool LDS, bool CMP>
+__device__ __forceinline__ void finish_pixels(const rtk::DevScene& s, const rtk::Eye& e, const PcParams& p) {
     const int F = p.aa;
     const unsigned gtid = blockIdx.x * kBlock + threadIdx.x, gstride = gridDim.x * kBlock;
     if (p.fin_cont) {
@@ -1980,7 +2062,7 @@ __device__ __forceinline__ void finish_pixels(const rtk::DevScene& s, const PcPa
                     const unsigned sl = slab_slot(p.tiles_x, ocol * F + l, rr * F + k);
                     if (p.pinfo[sl] & kPathCont) first = sl;
                 }
-            if (first == path) finish_pixel<LDS>(s, p, rr, ocol);
+            if (first == path) finish_pixel<LDS, CMP>(s, e, p, rr, ocol);
         }
     }
     const int npix = (p.chunk_rows / p.aa) * p.width;
@@ -1993,14 +2075,15 @@ __device__ __forceinline__ void finish_pixels(const rtk::DevScene& s, const PcPa
                     cont |= (p.pinfo[slab_slot(p.tiles_x, ocol * F + l, rr * F + k)] & kPathCont) != 0;
             if (cont) continue;
         }
-        finish_pixel<LDS>(s, p, rr, ocol);
+        finish_pixel<LDS, CMP>(s, e, p, rr, ocol);
     }
 }
 
 // k_finish: k_shade + k_compose in one pass, one lane per output pixel, with
 // the scene's materials and lights in LDS (host checks they fit);
 // k_finish_any: the same for larger scenes, tables read from global memory.
-__global__ __launch_bounds__(kBlock, RT_FINISH_WAVES) void k_finish(rtk::DevScene s, PcParams p) {
+template <bool CMP>
+__global__ __launch_bounds__(kBlock, RT_FINISH_WAVES) void k_finish(rtk::DevScene s, rtk::Eye e, PcParams p) {
     float4* dm = reinterpret_cast<float4*>(g_fmats);
     const float4* sm = reinterpret_cast<const float4*>(s.mats);
     for (int i = threadIdx.x; i < s.nmats * 4; i += kBlock) dm[i] = sm[i];
@@ -2008,10 +2091,11 @@ __global__ __launch_bounds__(kBlock, RT_FINISH_WAVES) void k_finish(rtk::DevScen
     const float4* sl = reinterpret_cast<const float4*>(s.lights);
     for (int i = threadIdx.x; i < s.nlights * 2; i += kBlock) dl_[i] = sl[i];
     __syncthreads();
-    finish_pixels<true>(s, p);
+    finish_pixels<true, CMP>(s, e, p);
 }
-__global__ __launch_bounds__(kBlock, RT_FINISH_ANY_WAVES) void k_finish_any(rtk::DevScene s, PcParams p) {
-    finish_pixels<false>(s, p);
+template <bool CMP>
+__global__ __launch_bounds__(kBlock, RT_FINISH_ANY_WAVES) void k_finish_any(rtk::DevScene s, rtk::Eye e, PcParams p) {
+    finish_pixels<false, CMP>(s, e, p);
 }
 
 // ---------------------------------------------------------------------------
@@ -2050,7 +2134,7 @@ __device__ void fallback_chain(const rtk::DevScene& s, const rtk::Eye& e, const 
     if (entry & kFbEye) {                          // a deferred eye ray
         path = entry & ~kFbEye;
         k = 0;
-        if (!slab_sample_ray(e, p, path, &r)) return;
+        if (!slab_sample_ray(p, path, &r)) return;
     } else {                                       // the reflection of record `entry`
         const size_t aspace = (size_t)p.la * cap;
         int kprev;
@@ -2063,7 +2147,7 @@ __device__ void fallback_chain(const rtk::DevScene& s, const rtk::Eye& e, const 
             path = (p.cflat[q % p.cb] & ~kFbEye) % cap;
         }
         k = kprev + 1;
-        r = reflect_from_record(s, p, entry);
+        r = reflect_from_record(s, p, entry, path);
     }
     const int k0 = k;
     V Ls[kFbMaxLevels], Km[kFbMaxLevels];          // the mirror levels' shading and km, k0 onward
@@ -2245,13 +2329,17 @@ __global__ __launch_bounds__(kBlock) void k_walk_timing(rtk::DevScene s, const f
 
 // Shading + fold + SSAA: k_finish (a lane per pixel; materials and lights in LDS), or k_finish_any for
 // larger scenes.
-void launch_finish(const rtk::DevScene& s, const PcParams& p, hipStream_t st) {
+void launch_finish(const rtk::DevScene& s, const rtk::Eye& e, const PcParams& p, hipStream_t st) {
     const int npix = (p.chunk_rows / p.aa) * p.width;
     const dim3 pgrid(std::max(1, std::min((npix + kBlock - 1) / kBlock, p.fin_grid > 0 ? p.fin_grid : INT32_MAX)));
     if (s.nmats <= kFinishMats && s.nlights <= kFinishLights)
-        hipLaunchKernelGGL(k_finish, pgrid, dim3(kBlock), 0, st, s, p);
-    else
-        hipLaunchKernelGGL(k_finish_any, pgrid, dim3(kBlock), 0, st, s, p);
+    {
+        if (p.clevels) hipLaunchKernelGGL(k_finish<true>, pgrid, dim3(kBlock), 0, st, s, e, p);
+        else hipLaunchKernelGGL(k_finish<false>, pgrid, dim3(kBlock), 0, st, s, e, p);
+    } else {
+        if (p.clevels) hipLaunchKernelGGL(k_finish_any<true>, pgrid, dim3(kBlock), 0, st, s, e, p);
+        else hipLaunchKernelGGL(k_finish_any<false>, pgrid, dim3(kBlock), 0, st, s, e, p);
+    }
 }
 
 hipError_t chain_occupancy(int* chain_blocks_per_cu, int* mix_blocks_per_cu, int* occlude_blocks_per_cu) {
@@ -2276,7 +2364,7 @@ hipError_t launch_fused_chunk(const rtk::DevScene& s, const rtk::Eye& e, const P
         hipLaunchKernelGGL(k_fused<true>, dim3(p.grid), dim3(kBlock), 0, st, s, e, p);
     else
         hipLaunchKernelGGL(k_fused<false>, dim3(p.grid), dim3(kBlock), 0, st, s, e, p);
-    launch_finish(s, p, st);
+    launch_finish(s, e, p, st);
     return hipGetLastError();
 }
 
@@ -2394,7 +2482,7 @@ hipError_t launch_chain_chunk(const rtk::DevScene& s, const rtk::Eye& e, const P
     PcParams f = p;
     f.fin_cont = phase_b && p.aa == 1;
     mark(kKFinish);
-    launch_finish(s, f, st);
+    launch_finish(s, e, f, st);
     mark(kKEnd);
     return hipGetLastError();
 }

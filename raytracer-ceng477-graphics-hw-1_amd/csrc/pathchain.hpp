@@ -74,16 +74,33 @@ enum CounterSlot : int {
     kCntFbOvfScans,       //   launches whose fallback shadow queue overflowed (occlusion bytes scanned)
 };
 
+// Phase-A levels whose records may leave out the direction (PcParams::dbase): k_finish rebuilds them
+// forward from the eye ray, one reflection per level.
+#ifndef RT_COMPACT_LEVELS
+#define RT_COMPACT_LEVELS 2
+#endif
+constexpr int kCompactLevels = RT_COMPACT_LEVELS;
+// Samples whose phase-A walks take at least this many steps mark their unit hot (PcParams::umark_w): the
+// heaviest units only (the list is dealt in the order the units were marked, so it must be short enough
+// to start at once; a 32-step threshold listed too many, measured no gain).
+constexpr unsigned kHotSteps = 96;
+
 struct PcParams {
     int width, height, aa, stripe_rows, rank, nranks, slab_rows;
     int wi, tiles_x, chunk_row0, chunk_rows, n0;
     int cap;          // path slots per chunk (>= n0)
     int levels;       // max_depth + 1 (>= 1)
     int nlights;
-    // Hit records, 32 B (pathchain.hip rec_write), by record id (rec_id): levels [0, la) of every sample
+    // Hit records (pathchain.hip rec_write), by record id (rec_id): levels [0, la) of every sample
     // at k * cap + sample (phase A), deeper levels only for the first cb continuations, at
     // la * cap + (k - la) * cb + c for continuation c (phase B); occlusion bytes by record id * nl.
+    // rec[id] = {hit point, surface code} for every record; recd[id - dbase] = {ray direction,
+    // material} only for ids >= dbase (the chain path: dbase = la * cap, phase A's records rebuild
+    // their directions from the eye ray; the fused path: dbase = 0).
     float4* rec;
+    float4* recd;
+    unsigned dbase;   // clevels * cap: records below it have no direction word
+    int clevels;      // min(la, kCompactLevels) levels of every sample without direction words (0: none)
     int* pinfo;       // [cap]: nlev | kind << 8 | kPathCont
     uint8_t* occ;
     int la;           // levels stored for every sample (phase A's; all levels on the fused path)
@@ -126,6 +143,20 @@ struct PcParams {
     int ogrid;        // k_occlude persistent grid
     int split_occ;    // 1: A's shadow tasks in their own k_occlude launch (occ_grid workgroups), not in k_mix
     int occ_grid;     // resident k_occlude workgroups
+    // Lone frames' phase-A units, the previous frame's heaviest first (rt_api.cpp render_chain, hot_units).
+    // Frame g (ugen) marks a unit hot when a sample of it walked at least kHotSteps steps: umark_w[u] = g
+    // (atomicMax: the first mark appends u to uhot_w, *uhcount_w of them); with uorder_on it deals the
+    // previous frame's list (uhot_r, *uhcount_r) before the column order, whose units marked in that
+    // frame (umark_r[u] == g - 1) it then skips.  The read and write arrays alternate by frame (no
+    // clearing but the list count, which k_pack_a zeroes once k_chain is done with it).  Where the work
+    // goes, never what it computes.
+    unsigned *umark_w, *uhot_w, *uhcount_w;
+    const unsigned *umark_r, *uhot_r;
+    unsigned* uhcount_r;
+    unsigned ugen;
+    int urank, uorder_on;
+    int occ_inplace;  // 1 (split_occ production launches): k_occlude walks A's shadow tasks in their phase-A
+                      // regions (workgroup w: regions w, w + G, ...); k_pack_a packs only the continuations
     int fin_grid;     // k_finish workgroups at most (0: a lane per output pixel), a grid-stride loop beyond
     int fin_cont;     // k_finish: the continued paths' pixels first (chain path: cflat, totals[1], kPathCont)
     int refill;       // a wave refills once <= refill of its lanes are still walking

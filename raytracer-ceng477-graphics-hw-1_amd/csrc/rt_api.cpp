@@ -73,15 +73,6 @@ float cos_threshold() {
     return from_ordered(hi);
 }
 
-template <typename T>
-int upload(T** dst, const std::vector<T>& src) {
-    *dst = nullptr;
-    const size_t bytes = std::max<size_t>(sizeof(T), src.size() * sizeof(T));
-    HIP_TRY(hipMalloc(reinterpret_cast<void**>(dst), bytes));
-    if (!src.empty()) HIP_TRY(hipMemcpy(*dst, src.data(), src.size() * sizeof(T), hipMemcpyHostToDevice));
-    return RT_OK;
-}
-
 }  // namespace
 
 int rt_internal_set_error(int code, const char* msg) { return fail(code, msg); }
@@ -99,6 +90,7 @@ struct rt_scene {
     dl::TriShade* d_tri = nullptr;
     dl::Material* d_mats = nullptr;
     dl::Light* d_lights = nullptr;
+    char* d_block = nullptr;                   // one allocation holding every d_ array above and the two below
     unsigned long long* d_counters = nullptr;
     unsigned* d_err = nullptr;                 // device error word (DevScene.err)
     unsigned* h_err = nullptr;                 // pinned host copy of it (rt_render reads it with the frame)
@@ -148,6 +140,10 @@ struct rt_scene {
     int tune_abandon = 0;       // RT_ABANDON: per mille of k_chain's waves done before the stragglers hand off (0: off;
                                 // 900-990 measured 2-4 % slower for C3 one frame: the restarted walks are the
                                 // heaviest, deepest chains, which then start phase B from scratch)
+    int tune_hot_units = 1;     // RT_HOT_UNITS: lone frames deal phase-A units heaviest-first by the previous frame's steps
+    int tune_occ_inplace = 1;   // RT_OCC_INPLACE: frame batches' k_occlude reads A's shadow tasks in their regions (0: packed)
+    int tune_compact = 1;       // RT_COMPACT: phase-A records without directions (16 B instead of 32): 1 frame batches,
+                                // 2 every launch, 0 none
     int tune_coop = 1;          // RT_COOP (builds with RT_COOP_BUILD=1): lone-frame phase B walks its tail chains on 8-lane groups (pathchain.hip coop_step)
     int tune_coop_live = 8;     // RT_COOP_LIVE: ... once at most this many chains of the wave walk (<= 8)
     int tune_coop_tail = 1;     // RT_COOP_TAIL: ... servicing finished walks once this many are done
@@ -187,6 +183,12 @@ struct rt_scene {
         size_t bytes = 0;
         hipEvent_t last = nullptr;
         hipStream_t last_stream = nullptr;
+        // lone frames' hot phase-A units (PcParams::umark_* / uhot_* / uhcount_*): mark[2][n], hot[2][n],
+        // count[2] for hist_units = n units, alternating by frame generation hist_gen
+        unsigned* hist = nullptr;
+        unsigned hist_units = 0;
+        unsigned hist_gen = 1;
+        uint64_t hist_key = 0;               // the launch geometry of the last frame that marked units
     } arenas[kSlots];
     hipStream_t slot_stream[kSlots] = {};
     hipEvent_t slot_done[kSlots] = {};
@@ -226,10 +228,10 @@ struct rt_scene {
         if (fork_ev) (void)hipEventDestroy(fork_ev);
         for (auto& e : kt.ev)
             if (e) (void)hipEventDestroy(e);
+        for (auto& a : arenas) (void)hipFree(a.hist);
         (void)hipFree(batch_out);
-        (void)hipFree(d_pairs); (void)hipFree(d_leafbig); (void)hipFree(d_spairs); (void)hipFree(d_swnodes); (void)hipFree(d_wnodes); (void)hipFree(d_lrec);
-        (void)hipFree(d_nodes); (void)hipFree(d_prims); (void)hipFree(d_tri); (void)hipFree(d_mats); (void)hipFree(d_lights);
-        (void)hipFree(d_counters); (void)hipFree(d_err); (void)hipFree(d_out); (void)hipFree(d_trace);
+        (void)hipFree(d_block);           // the scene arrays, counters and error word (upload_scene)
+        (void)hipFree(d_out); (void)hipFree(d_trace);
         if (h_err) (void)hipHostFree(h_err);
         if (ev0) (void)hipEventDestroy(ev0);
         if (ev1) (void)hipEventDestroy(ev1);
@@ -334,35 +336,44 @@ int upload_scene(rt_scene* s, const rt_options* opts) {
         lights[i] = dl::Light{l.position.x, l.position.y, l.position.z, 0, l.intensity.x, l.intensity.y,
                               l.intensity.z, 0};
     }
-    if ((rc = upload(&s->d_nodes, s->bvh.nodes))) return rc;
-    if ((rc = upload(&s->d_prims, s->bvh.prims))) return rc;
-    if ((rc = upload(&s->d_tri, s->bvh.tri_shade))) return rc;
-    if ((rc = upload(&s->d_mats, mats))) return rc;
-    if ((rc = upload(&s->d_lights, lights))) return rc;
-    if ((rc = upload(&s->d_pairs, s->bvh.pairs))) return rc;
-    if ((rc = upload(&s->d_leafbig, s->bvh.leaf_big))) return rc;
-    if ((rc = upload(&s->d_spairs, s->bvh.spairs))) return rc;
-    if ((rc = upload(&s->d_swnodes, s->bvh.swnodes))) return rc;
-    if ((rc = upload(&s->d_wnodes, s->bvh.wnodes))) return rc;
-    if ((rc = upload(&s->d_lrec, s->bvh.lrec))) return rc;
-    {
-        auto vb = [](const auto& v) { return v.size() * sizeof(v[0]); };
-        s->scene_bytes = vb(s->bvh.nodes) + vb(s->bvh.prims) + vb(s->bvh.tri_shade) + vb(mats) + vb(lights) +
-                         vb(s->bvh.pairs) + vb(s->bvh.leaf_big) + vb(s->bvh.spairs) + vb(s->bvh.swnodes) +
-                         vb(s->bvh.wnodes) + vb(s->bvh.lrec);
+    {   // one device allocation for every scene array, the counters and the error word (256-B aligned
+        // parts, each at least one element), the arrays copied in, counters and error word zeroed at once
+        struct Part { void** dst; const void* src; size_t bytes, min; };
+        auto part = [](auto** dst, const auto& v) {
+            return Part{reinterpret_cast<void**>(dst), v.data(), v.size() * sizeof(v[0]), sizeof(v[0])};
+        };
+        const Part parts[] = {part(&s->d_nodes, s->bvh.nodes), part(&s->d_prims, s->bvh.prims),
+                              part(&s->d_tri, s->bvh.tri_shade), part(&s->d_mats, mats), part(&s->d_lights, lights),
+                              part(&s->d_pairs, s->bvh.pairs), part(&s->d_leafbig, s->bvh.leaf_big),
+                              part(&s->d_spairs, s->bvh.spairs), part(&s->d_swnodes, s->bvh.swnodes),
+                              part(&s->d_wnodes, s->bvh.wnodes), part(&s->d_lrec, s->bvh.lrec)};
+        auto up = [](size_t b) { return (b + 255) & ~size_t(255); };
+        size_t off = 0;
+        s->scene_bytes = 0;
+        for (const Part& q : parts) {
+            off += up(std::max(q.bytes, q.min));
+            s->scene_bytes += q.bytes;
+        }
+        const size_t zero_off = off, zero_bytes = up(rtc::kCounters * sizeof(unsigned long long)) + up(sizeof(unsigned));
+        HIP_TRY(hipMalloc(reinterpret_cast<void**>(&s->d_block), zero_off + zero_bytes));
+        off = 0;
+        for (const Part& q : parts) {
+            *q.dst = s->d_block + off;
+            if (q.bytes) HIP_TRY(hipMemcpy(*q.dst, q.src, q.bytes, hipMemcpyHostToDevice));
+            off += up(std::max(q.bytes, q.min));
+        }
+        s->d_counters = reinterpret_cast<unsigned long long*>(s->d_block + zero_off);
+        s->d_err = reinterpret_cast<unsigned*>(s->d_block + zero_off + up(rtc::kCounters * sizeof(unsigned long long)));
+        HIP_TRY(hipMemset(s->d_block + zero_off, 0, zero_bytes));
     }
-    HIP_TRY(hipMalloc(reinterpret_cast<void**>(&s->d_counters), rtc::kCounters * sizeof(unsigned long long)));
-    HIP_TRY(hipMemset(s->d_counters, 0, rtc::kCounters * sizeof(unsigned long long)));
-    HIP_TRY(hipMalloc(reinterpret_cast<void**>(&s->d_err), sizeof(unsigned)));
-    HIP_TRY(hipMemset(s->d_err, 0, sizeof(unsigned)));
     HIP_TRY(hipEventCreate(&s->ev0));
     HIP_TRY(hipEventCreate(&s->ev1));
 
     {
-        hipDeviceProp_t prop;
-        HIP_TRY(hipGetDeviceProperties(&prop, s->device));
-        s->grid_blocks = std::max(1, prop.multiProcessorCount) * 8;
-        s->num_cus = std::max(1, prop.multiProcessorCount);
+        int cus = 0;
+        HIP_TRY(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, s->device));
+        s->grid_blocks = std::max(1, cus) * 8;
+        s->num_cus = std::max(1, cus);
     }
     s->path = rt_scene::kChain;
     if (opts && (opts->flags & RT_OPT_WAVEFRONT)) s->path = rt_scene::kWavefront;
@@ -407,6 +418,9 @@ int upload_scene(rt_scene* s, const rt_options* opts) {
     if (const char* e = std::getenv("RT_BSERVICE")) s->tune_bservice = std::max(1, std::min(64, std::atoi(e)));
     if (const char* e = std::getenv("RT_BTAIL")) s->tune_btail = std::max(1, std::min(64, std::atoi(e)));
     if (const char* e = std::getenv("RT_COOP")) s->tune_coop = std::atoi(e) != 0;
+    if (const char* e = std::getenv("RT_COMPACT")) s->tune_compact = std::max(0, std::min(2, std::atoi(e)));
+    if (const char* e = std::getenv("RT_OCC_INPLACE")) s->tune_occ_inplace = std::atoi(e) != 0;
+    if (const char* e = std::getenv("RT_HOT_UNITS")) s->tune_hot_units = std::atoi(e) != 0;
     if (const char* e = std::getenv("RT_ABANDON")) s->tune_abandon = std::max(0, std::min(1000, std::atoi(e)));
     if (const char* e = std::getenv("RT_COOP_LIVE")) s->tune_coop_live = std::max(1, std::min(8, std::atoi(e)));
     if (const char* e = std::getenv("RT_COOP_TAIL")) s->tune_coop_tail = std::max(1, std::min(64, std::atoi(e)));
@@ -652,7 +666,9 @@ struct ChainPlan {
     int la = 1, tchunk = 1;         // levels stored per sample; phase-B continuation chunk
     size_t cb = 0;                  // continuations with phase-B records
     // arena offsets
-    size_t o_rec = 0, o_pinfo = 0, o_occ = 0, o_sqA = 0, o_scntA = 0, o_sflatA = 0, o_cq = 0, o_ccnt = 0,
+    size_t dbase = 0;               // records below it without directions (pathchain.hpp)
+    int clevels = 0;
+    size_t o_rec = 0, o_recd = 0, o_pinfo = 0, o_occ = 0, o_sqA = 0, o_scntA = 0, o_sflatA = 0, o_cq = 0, o_ccnt = 0,
            o_cflat = 0, o_sqB = 0, o_scntB = 0, o_sflatB = 0, o_totals = 0, o_wq = 0, o_cid = 0, o_tail = 0,
            o_fbc = 0, o_fbs = 0, bytes = 0;
 };
@@ -739,7 +755,15 @@ ChainPlan chain_plan(const rt_scene* s, const ChainGeom& g, size_t nunits, bool 
     P.wq_cap = fused ? rtc::fused_wave_qcap((int)std::min<size_t>(cap, INT32_MAX), P.G, levels, nl) : 0u;
     const size_t nrec = cap * P.la + P.cb * (levels - P.la);
     ArenaLayout L;
-    P.o_rec = L.take<float4>(2 * nrec);
+    // phase A's records without their directions where k_finish can rebuild them (pathchain.hpp dbase)
+    // (not with RT_ABANDON: its restarts reflect phase-A records no direction was kept for)
+    // (frame batches by default: a lone frame's k_finish is on its critical path and the rebuilt
+    // directions cost it more than the saved bytes; RT_COMPACT=2 everywhere, 0 nowhere)
+    const bool cmp = s->tune_compact == 2 || (s->tune_compact == 1 && g.nframes > 1);
+    P.clevels = !fused && cmp && s->tune_abandon == 0 ? std::min(P.la, rtc::kCompactLevels) : 0;
+    P.dbase = cap * (size_t)P.clevels;
+    P.o_rec = L.take<float4>(nrec);
+    P.o_recd = L.take<float4>(nrec - P.dbase);
     P.o_pinfo = L.take<int>(cap);
     P.o_occ = L.take<uint8_t>(nrec * nl + 8);   // + 8: k_finish reads aligned dwords
     P.o_cid = L.take<unsigned>(cap);
@@ -858,6 +882,9 @@ int render_chain(rt_scene* s, const rtk::Eye& eye, const rtk::FrameParams& f, bo
     p.rank = f.rank; p.nranks = f.nranks; p.slab_rows = f.slab_rows;
     p.wi = wi; p.tiles_x = tiles_x; p.cap = (int)cap; p.levels = levels; p.nlights = s->dev.nlights;
     p.rec = static_cast<float4*>(at(P.o_rec));
+    p.recd = static_cast<float4*>(at(P.o_recd));
+    p.dbase = (unsigned)P.dbase;
+    p.clevels = P.clevels;
     p.pinfo = static_cast<int*>(at(P.o_pinfo));
     p.occ = static_cast<uint8_t*>(at(P.o_occ));
     p.sqA = static_cast<unsigned*>(at(P.o_sqA)); p.scapA = P.scapA;
@@ -885,6 +912,7 @@ int render_chain(rt_scene* s, const rtk::Eye& eye, const rtk::FrameParams& f, bo
     p.occ_grid = s->occl_grid;
     p.fin_grid = s->tune_fgrid > 0 ? s->tune_fgrid : 8 * s->num_cus;
     p.split_occ = P.split_occ ? 1 : 0;
+    p.occ_inplace = P.split_occ && !count && s->tune_occ_inplace ? 1 : 0;
     p.refill = s->tune_refill >= 0 ? s->tune_refill : 0;
     p.service = s->tune_service >= 0 ? s->tune_service : 64;
     p.bservice = s->tune_bservice;
@@ -925,11 +953,47 @@ int render_chain(rt_scene* s, const rtk::Eye& eye, const rtk::FrameParams& f, bo
     p.trace_blocks = std::max(s->mix_grid, s->occl_grid);
     const size_t trace_n = 2 * (cap + (size_t)p.trace_blocks) + 4 * cap;
     p.trace = trace_buffer(s, trace_n);
+    // lone frames in one launch (a drop-in caller's repeated frames): phase-A units heaviest-first by the
+    // previous frame of the same geometry (PcParams::uorder), and this frame's costs ranked for the next
+    const bool hot = s->tune_hot_units && !count && !fused && p.nframes == 1 && P.dyn_units > 0 &&
+                     units == g.units_total && !p.trace;
+    p.urank = p.uorder_on = 0;
     for (int r0 = f.chunk_j * chunk_rows; r0 < li; r0 += f.chunk_k * chunk_rows) {
         p.chunk_row0 = r0;
         p.chunk_rows = std::min(chunk_rows, li - r0);
         p.n0 = tiles_x * ((p.chunk_rows + 7) / 8) * 64;
         p.grid = grid_for(p.n0);
+        if (hot) {
+            const unsigned nu = (unsigned)((p.n0 + 255) / 256);
+            if (arena.hist_units != nu) {
+                if (arena.hist) HIP_TRY(hipStreamSynchronize(st));   // earlier frames may still use it
+                (void)hipFree(arena.hist);
+                arena.hist = nullptr;
+                arena.hist_units = 0;
+                arena.hist_key = 0;
+                const size_t words = 4 * (size_t)nu + 2;
+                HIP_TRY(hipMalloc(reinterpret_cast<void**>(&arena.hist), words * sizeof(unsigned)));
+                HIP_TRY(hipMemsetAsync(arena.hist, 0, words * sizeof(unsigned), st));
+                arena.hist_units = nu;
+                arena.hist_gen = 1;            // marks start at 0: generations from 2 on never match them
+            }
+            uint64_t key = 1469598103934665603ull;   // the geometry the order is valid for
+            for (long long v : {(long long)p.width, (long long)p.height, (long long)p.aa, (long long)p.stripe_rows,
+                                (long long)p.rank, (long long)p.nranks, (long long)p.slab_rows, (long long)p.n0,
+                                (long long)p.tiles_x, (long long)p.ublk_h, (long long)p.ublk_w})
+                key = (key ^ (uint64_t)v) * 1099511628211ull;
+            const unsigned g_ = ++arena.hist_gen, w = g_ & 1u, r = w ^ 1u;
+            unsigned* const mark = arena.hist;
+            unsigned* const list = arena.hist + 2 * (size_t)nu;
+            unsigned* const cnt = arena.hist + 4 * (size_t)nu;
+            p.umark_w = mark + w * (size_t)nu; p.umark_r = mark + r * (size_t)nu;
+            p.uhot_w = list + w * (size_t)nu; p.uhot_r = list + r * (size_t)nu;
+            p.uhcount_w = cnt + w; p.uhcount_r = cnt + r;
+            p.ugen = g_;
+            p.urank = 1;
+            p.uorder_on = arena.hist_key == key ? 1 : 0;   // the previous frame marked this geometry
+            arena.hist_key = key;
+        }
         // phase A's stragglers hand their walks to phase B once this share of k_chain's waves is done
         p.abandon = s->tune_abandon > 0 && !count && P.phase_b && !P.split_occ   // lone frames (k_mix with the BQ)
                         ? (unsigned)std::max<long long>(1, (long long)p.grid * 4 * s->tune_abandon / 1000)   // 4 waves per 256-thread workgroup
@@ -1395,10 +1459,14 @@ int rt_render_cameras(rt_scene* s, const rt_camera* cams, int n, int aa, uint8_t
     if (s->group) {
         // device group: runs of consecutive same-size cameras as frame batches (every device renders its
         // stripes of all of them in flight together, one grouped gather per run)
+        // (RT_GROUP_BATCH: at most this many frames per grouped gather; 1 = one gather per frame, the
+        // path without several gathers per communicator in one RCCL group)
+        int batch = rtc::kMaxFrames;
+        if (const char* e = std::getenv("RT_GROUP_BATCH")) batch = std::max(1, std::min(rtc::kMaxFrames, std::atoi(e)));
         rt_stats sum{}, one{};
         for (int i = 0; i < n;) {
             int j = i + 1;
-            while (j < n && j - i < rtc::kMaxFrames && cams[j].image_width == cams[i].image_width &&
+            while (j < n && j - i < batch && cams[j].image_width == cams[i].image_width &&
                    cams[j].image_height == cams[i].image_height)
                 ++j;
             const int rc = rt_internal_group_render_frames(s->group, cams + i, j - i, aa, outs + i,

@@ -47,9 +47,12 @@ __device__ __forceinline__ int batch_frame(const P& p, int* lr) {
 // Slab-local sample slot -> eye ray.  Slots are ordered by 8x8 internal-pixel
 // tiles (one tile per wave) for ray coherence; slab rows map to global rows
 // through the stripe round-robin.  P needs: wi tiles_x chunk_row0 chunk_rows
-// aa slab_rows stripe_rows nranks rank height nframes frame_rows eyes.
+// aa slab_rows stripe_rows nranks rank height nframes frame_rows eyes, with
+// eyes[0] the camera of a lone frame too (read per lane from the kernel
+// arguments: a kernel that also kept a separate Eye argument live held its
+// 13 words in scalar registers, which the walk loops then spilled).
 template <class P>
-__device__ __forceinline__ bool slab_sample_ray(const rtk::Eye& e, const P& p, unsigned s, Ray* r) {
+__device__ __forceinline__ bool slab_sample_ray(const P& p, unsigned s, Ray* r) {
     const unsigned tile = s >> 6, lane = s & 63;
     const int tx = (int)(tile % (unsigned)p.tiles_x), ty = (int)(tile / (unsigned)p.tiles_x);
     const int ix = tx * 8 + (int)(lane & 7);
@@ -63,7 +66,7 @@ __device__ __forceinline__ bool slab_sample_ray(const rtk::Eye& e, const P& p, u
     const int stripe = lr / p.stripe_rows;
     const int g = (stripe * p.nranks + p.rank) * p.stripe_rows + (lr - stripe * p.stripe_rows);
     if (g >= p.height) return false;
-    *r = eye_ray(p.nframes > 1 ? p.eyes[f] : e, g * p.aa + sub, ix);
+    *r = eye_ray(p.eyes[f], g * p.aa + sub, ix);
     return true;
 }
 

@@ -69,6 +69,10 @@ CONFIGS: dict[str, tuple[str, dict]] = {
     "C5_hm_8k_d6": ("horse_and_mug.xml", dict(depth=6, res=(7680, 4320),
                                               near=(-1, 1, -0.5625, 0.5625),
                                               image_name="horse_and_mug_8k_d6.ppm")),
+    # timing probe for k_fallback (not a §8d config): an axis-aligned camera at an odd resolution, whose
+    # centre column and row have eye-ray direction components of exactly 0 (deferred by the timed walks)
+    "X_cornell_801_axis": ("cornellbox.xml", dict(keep_camera="1", res=(801, 801),
+                                                   image_name="cornellbox_801_axis.ppm")),
 }
 
 

@@ -262,3 +262,22 @@ def test_wait_bound_reports_limit(pkg, scene_dir, goldens, torch_cuda, monkeypat
         img, _ = s.render(s.camera(0), aa=1)
         s.check()
     assert np.array_equal(img, load_golden_image(g["cameras"][0]))
+
+
+@pytest.mark.parametrize("hot", ["1", "0"])
+def test_repeated_lone_frames_equal_golden(pkg, scene_dir, goldens, torch_cuda, monkeypatch, hot):
+    """Lone frames deal their phase-A units by the previous frame's hot units (rt_api.cpp hot_units,
+    pathchain.hip unit_deal: the listed units first, then the column order without them; the mark and
+    list arrays alternate by frame).  Frames of one geometry in a row, another geometry between them
+    (the lists' key changes) and back: every frame is the golden."""
+    from conftest import config_path, golden_by_name, load_golden_image
+    monkeypatch.setenv("RT_HOT_UNITS", hot)
+    g1 = golden_by_name(goldens, "C3_hm_1080p_d6_aa1")
+    g2 = golden_by_name(goldens, "C3_hm_1080p_d6_aa2")
+    ref1, ref2 = load_golden_image(g1["cameras"][0]), load_golden_image(g2["cameras"][0])
+    with pkg.Scene.from_xml(config_path(scene_dir, g1["config"]), device=0) as s:
+        cam = s.camera(0)
+        for aa, ref in ((1, ref1), (1, ref1), (1, ref1), (2, ref2), (1, ref1), (1, ref1)):
+            img, _ = s.render(cam, aa=aa)
+            assert np.array_equal(img, ref)
+        s.check()

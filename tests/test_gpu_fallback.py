@@ -12,6 +12,8 @@ branch of it and compare with the reference goldens (raytracer.cpp:385-452):
   * RT_CONT_CB=1000: continuations beyond 1,000 finish in k_fallback;
   * RT_FBS_CAP=64 with =2: the shadow queue overflows (marked occlusion bytes
     scanned by k_fallback);
+  * RT_COMPACT=0 with RT_CONT_CB=1000: full 32-B phase-A records (the compact
+    16-B records leave the directions of continued paths in tail[]);
   * RT_ABANDON=1: phase A's unfinished walks restart in phase B (eye rays as
     kFbEye continuations, level-1 walks as reflections of their level-0 record),
     alone and with RT_CONT_CB=1000 (the restarts beyond it in k_fallback).
@@ -45,6 +47,9 @@ ENVS = [
     {"RT_FORCE_FALLBACK": "2"},
     {"RT_FORCE_FALLBACK": "3"},
     {"RT_CONT_CB": "1000"},
+    # phase-A records with their directions (RT_COMPACT=0, pathchain.hpp dbase = 0): the continuations
+    # and k_fallback read the stored direction words instead of the chain's tail copies
+    {"RT_COMPACT": "0", "RT_CONT_CB": "1000"},
     {"RT_FORCE_FALLBACK": "2", "RT_FBS_CAP": "64"},
 ]
 

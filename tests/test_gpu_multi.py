@@ -98,12 +98,15 @@ def virtual_group(request, pkg, torch_cuda, monkeypatch):
     pkg.set_devices(0)
 
 
-@pytest.mark.parametrize("stripe", ["8", "5"])
-def test_virtual_group_frames_equal_golden(virtual_group, stripe, goldens, pkg, scene_dir, monkeypatch):
+@pytest.mark.parametrize("stripe,batch", [("8", None), ("5", None), ("8", "1")])
+def test_virtual_group_frames_equal_golden(virtual_group, stripe, batch, goldens, pkg, scene_dir, monkeypatch):
     """N > 1 group path on one GPU: single frames (rt_render) and frame batches (rt_render_cameras:
     every rank renders its stripes of a run of same-size cameras in flight together, one grouped
-    gather, per-frame unshuffle) equal the goldens; counters are summed over the ranks."""
+    gather, per-frame unshuffle) equal the goldens; counters are summed over the ranks.
+    RT_GROUP_BATCH=1: the escape hatch, one frame (one gather) per call."""
     monkeypatch.setenv("RT_GROUP_STRIPE", stripe)
+    if batch:
+        monkeypatch.setenv("RT_GROUP_BATCH", batch)
     g = golden_by_name(goldens, "C3_hm_1080p_d6_aa1")
     cam_g = g["cameras"][0]
     ref = load_golden_image(cam_g)

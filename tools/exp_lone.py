@@ -28,6 +28,7 @@ def child():
         for _ in range(3):
             s.render_device(cam, 1, out.data_ptr(), st.cuda_stream)
         torch.cuda.synchronize()
+        s.counters_reset(st.cuda_stream)
         ts = []
         for _ in range(reps):
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -41,7 +42,9 @@ def child():
         if os.environ.get("RT_KTIME"):
             ms, n = s.kernel_times(reset=True)
             kt = {k: round(v / (reps + 3), 4) for k, v in ms.items()}
-        print(json.dumps({"median_ms": round(ts[len(ts) // 2], 4), "min_ms": round(ts[0], 4),
+        fbr = s.counters_raw()           # what the timed kernels left to k_fallback, per frame
+        fb = {k[3:]: round(fbr[k] / reps, 1) for k in s.FALLBACK_SLOTS if k != "fb_launches" and fbr[k]}
+        print(json.dumps({"median_ms": round(ts[len(ts) // 2], 4), "min_ms": round(ts[0], 4), "fallback": fb,
                           "sha_prefix": __import__("hashlib").sha256(out.cpu().numpy().tobytes()).hexdigest()[:12],
                           "kernel_times": kt}))
 

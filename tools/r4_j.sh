@@ -1,0 +1,17 @@
+#!/bin/bash
+# Round-4 build: parity; lone-frame / batched A/B (hot units, compact records, in-place shadow tasks vs the
+# early-round build); scene creation phases; k_fallback timing probes; lone-frame stripe shards
+cd "$GRAFT_REPO_ROOT" || exit 1
+export TMPDIR=/tmp
+OUT=gpurun_out/j_${1:-a}
+mkdir -p $OUT
+P=$GRAFT_REPO_ROOT/raytracer-ceng477-graphics-hw-1_amd
+timeout -k 10 400 python -u -m pytest -x -q --timeout 200 --timeout-method thread tests -m gpu > $OUT/tests.log 2>&1
+rc=$?; echo "tests rc=$rc"; tail -2 $OUT/tests.log; [ $rc -ne 0 ] && exit $rc
+RT_KTIME=1 EXP_REPS=61 timeout -k 10 500 python3 tools/exp_lone.py - RT_HOT_UNITS=0 RT_LIB=$P/librt_base.so RT_COMPACT=0 - RT_HOT_UNITS=0 RT_LIB=$P/librt_base.so > $OUT/lone.jsonl 2> $OUT/lone.err; echo "lone rc=$?"; cat $OUT/lone.jsonl
+printf -- "- \nRT_LIB=$P/librt_base.so \nRT_OCC_INPLACE=0 \nRT_COMPACT=0 \n- \nRT_LIB=$P/librt_base.so \n" | bash tools/ab2.sh > $OUT/batched.txt 2>&1; echo "batched rc=$?"; cat $OUT/batched.txt
+timeout -k 10 200 python3 tools/exp_scene_load.py C3_hm_1080p_d6 16,8,1 > $OUT/scene_load.json 2> $OUT/scene_load.err; echo "scene_load rc=$?"
+RT_BUILD_TRACE=1 timeout -k 10 100 python3 tools/exp_scene_load.py C3_hm_1080p_d6 16 > /dev/null 2> $OUT/build_trace.err; echo "build trace rc=$?"; grep -m3 "build:" $OUT/build_trace.err
+bash tools/r4_h.sh j > $OUT/h.txt 2>&1; echo "fallback probes rc=$?"; cat $OUT/h.txt
+EXP_F=1 EXP_S="1 8" timeout -k 10 300 python3 tools/exp_shard.py 1 2 4 8 > $OUT/shard_f1.jsonl 2> $OUT/shard_f1.err; echo "shard rc=$?"; cat $OUT/shard_f1.jsonl
+echo done
