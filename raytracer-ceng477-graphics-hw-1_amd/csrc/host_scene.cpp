@@ -688,7 +688,7 @@ int build_threads(int requested) {
     return (int)std::max(1u, std::min(hc, 16u));
 }
 
-std::string build_bvh(const HostScene& s, FlatBVH& out, int threads) {
+std::string build_bvh(const HostScene& s, FlatBVH& out, int threads, const std::function<void()>* on_flat) {
     auto t0 = std::chrono::steady_clock::now();
     out = FlatBVH();
     out.threads = build_threads(threads);
@@ -934,6 +934,7 @@ std::string build_bvh(const HostScene& s, FlatBVH& out, int threads) {
     out.root_lrec = lrec_of[0];
     if (!lrec_ok) out.lrec.clear();                  // no 4-wide trees: the binary trees only
     release(true);
+    if (on_flat) (*on_flat)();
     // The occlusion tree (its own task when threads allow) and the reference-order wide tree are
     // independent: both read the pairs and leaf records, each writes only its own fields.
     const auto t1 = std::chrono::steady_clock::now();
@@ -1165,24 +1166,16 @@ void build_shadow_tree(FlatBVH& out, int threads, std::vector<ShadowLeaf>& leave
             tn[n].info = (*flat.leaf_info)[f];
             tn[n].rec = (*flat.lrec_of)[f];
         }
-    // pairs in pre-order of interior nodes
+    // pairs in pre-order of interior nodes: the order of their slots (a subtree at slot `at` has its
+    // left subtree from at + 1 and its right one after the left's whole range), so a count, no walk
     std::vector<int32_t> pair_of(tn.size(), -1);
     int32_t np = 0;
-    {
-        std::vector<int> st{root};
-        while (!st.empty()) {
-            const int n = st.back();
-            st.pop_back();
-            if (tn[n].left < 0) continue;
-            pair_of[n] = np++;
-            st.push_back(tn[n].right);
-            st.push_back(tn[n].left);
-        }
-    }
+    for (size_t n = 0; n + 1 < tn.size(); ++n)
+        if (tn[n].left >= 0) pair_of[n] = np++;
     auto info = [&](int n) { return tn[n].left < 0 ? tn[n].info : pair_of[n]; };
     out.spairs.resize(np);
-    for (size_t n = 0; n < tn.size(); ++n) {
-        if (tn[n].left < 0) continue;
+    parallel_for((int)tn.size(), threads, [&](int n) {
+        if (tn[n].left < 0) return;
         const TNode& L = tn[tn[n].left];
         const TNode& R = tn[tn[n].right];
         dl::Pair& p = out.spairs[pair_of[n]];
@@ -1190,7 +1183,7 @@ void build_shadow_tree(FlatBVH& out, int threads, std::vector<ShadowLeaf>& leave
         p.l_maxx = L.box.hi[0]; p.l_maxy = L.box.hi[1]; p.l_maxz = L.box.hi[2]; p.axis = tn[n].axis;
         p.r_minx = R.box.lo[0]; p.r_miny = R.box.lo[1]; p.r_minz = R.box.lo[2]; p.r_info = info(tn[n].right);
         p.r_maxx = R.box.hi[0]; p.r_maxy = R.box.hi[1]; p.r_maxz = R.box.hi[2]; p.pad = 0;
-    }
+    });
     for (int a = 0; a < 3; ++a) { out.sroot_lo[a] = tn[root].box.lo[a]; out.sroot_hi[a] = tn[root].box.hi[a]; }
     out.sroot_info = info(root);
 

@@ -8,6 +8,7 @@
 #pragma once
 
 #include <cstdint>
+#include <functional>
 #include <memory>
 #include <string>
 #include <type_traits>
@@ -114,7 +115,10 @@ void prepare_triangles(HostScene& s);
 // error message.  threads: host build threads (0: RT_BUILD_THREADS, else the
 // hardware concurrency capped at 16; 1: serial).  The output does not depend
 // on the thread count.
-std::string build_bvh(const HostScene& s, FlatBVH& out, int threads = 0);
+// on_flat (optional) is called once the flatten's arrays (nodes, prims, tri_shade, pairs, leaf_big,
+// lrec) are final, while the wide trees are still being built (they only read those arrays).
+std::string build_bvh(const HostScene& s, FlatBVH& out, int threads = 0,
+                      const std::function<void()>* on_flat = nullptr);
 int build_threads(int requested);
 
 }  // namespace rtx

@@ -864,28 +864,11 @@ constexpr int kCoop = 3;
 // cover a column of the image instead of a full-width band (C3, 256-px columns a frame high: ~1 %
 // per batched frame, ~2 % one frame).  Identity when ublk_h == 0 or the units do not tile the rows.
 __device__ __forceinline__ unsigned unit_col_order(const PcParams& p, unsigned u, unsigned units) {
-    const unsigned upr = (unsigned)p.tiles_x / 4u;
-    if (p.ublk_h == 0 || (p.tiles_x & 3) || units % upr) return u;
-    const unsigned rows = units / upr, bw = (unsigned)p.ublk_w;
-    const unsigned bh = p.ublk_h > 0 ? (unsigned)p.ublk_h : (rows % (unsigned)p.nframes ? rows : rows / (unsigned)p.nframes);
-    const unsigned r0 = u / (bh * upr) * bh, h = min(bh, rows - r0);
-    const unsigned i = u - r0 * upr;            // index within the super-row (h rows x upr units)
-    const unsigned c0 = i / (h * bw) * bw, w = min(bw, upr - c0);
-    const unsigned l = i - c0 * h;
-    return (r0 + l / w) * upr + c0 + l % w;
+    return unit_col(p.tiles_x, p.ublk_h, p.ublk_w, p.nframes, u, units);
 }
-// The unit of deal number u (a launch-wide counter), kUidNone once there is none: with uorder_on the
-// previous frame's hot units first, then the column order without them (a skipped unit costs one more
-// deal); else the column order.
-__device__ __forceinline__ unsigned unit_deal(const PcParams& p, unsigned units) {
-    const unsigned H = p.uorder_on ? min(units, __hip_atomic_load(p.uhcount_r, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) : 0u;
-    while (true) {
-        const unsigned u = atomicAdd(&p.totals[3], 1u);
-        if (u < H) return p.uhot_r[u];
-        if (u >= units + H) return kUidNone;
-        const unsigned c = unit_col_order(p, u - H, units);
-        if (H == 0u || p.umark_r[c] != p.ugen - 1u) return c;
-    }
+// The unit dealt u-th: the previous frame's heaviest units first (PcParams::uorder_on), else the column order.
+__device__ __forceinline__ unsigned unit_order(const PcParams& p, unsigned u, unsigned units) {
+    return p.uorder_on ? p.uorder[u] : unit_col_order(p, u, units);
 }
 
 // closest-hit chains of one phase (raytracer.cpp:385-439 minus the shading):
@@ -1001,13 +984,7 @@ __device__ void chain_body(const rtk::DevScene& s, const rtk::Eye& e, const PcPa
             }
             if (ends || handoff) {
                 st = kIdle;
-                if (!CONT && !COUNT && p.urank && ssteps >= kHotSteps) {   // the unit is hot: listed once
-                    const unsigned u = path >> 8;
-                    if (atomicMax(&p.umark_w[u], p.ugen) != p.ugen) {
-                        const unsigned i = atomicAdd(p.uhcount_w, 1u);
-                        if (i < ((unsigned)p.n0 + 255u) / 256u) p.uhot_w[i] = u;   // (at most once per unit)
-                    }
-                }
+                if (!CONT && !COUNT && p.urank && ssteps >= kHotSteps[1]) atomicMax(&p.ucost[path >> 8], ssteps);
                 if (p.trace && !CONT) { p.trace[2 * path] = t_grab; p.trace[2 * path + 1] = (unsigned)wall_clock64(); }
                 if (p.trace && CONT) {       // phase B: {grab, end, last level, walk steps} after A's entries
                     unsigned* tb = p.trace + 2 * ((size_t)p.cap + p.trace_blocks) + 4 * (size_t)path;
@@ -1049,7 +1026,8 @@ __device__ void chain_body(const rtk::DevScene& s, const rtk::Eye& e, const PcPa
                                 if (spin_over(s, n)) { late = true; break; }
                                 __builtin_amdgcn_s_sleep(1);
                             }
-                        lds_store(&g_uid[jf], late ? kUidNone : unit_deal(p, units));
+                        const unsigned u = late ? units : atomicAdd(&p.totals[3], 1u);
+                        lds_store(&g_uid[jf], u < units ? unit_order(p, u, units) : kUidNone);
                     }
                     const unsigned v = base + lane_rank(idle);
                     if (st == kIdle && v < nb) {
@@ -1559,10 +1537,45 @@ __device__ void pack_region(const unsigned* q, unsigned cap, const unsigned* cnt
 }
 
 // After phase A: pack its shadow tasks and continuations (one workgroup per region).
+// The next frame's phase-A unit order (PcParams::uorder, k_mix's last shadow-role workgroup in lone frames):
+// the units by cost class (kHotSteps), each class in
+// the column order (the table ucol, made on the host); ucost cleared for the next frame's marks.  One
+// workgroup: thread t takes a contiguous run of the column order; the per-class offsets come from one block-wide exclusive scan of the three
+// counts packed into a 64-bit word (21 bits each: at most 2^21 units).
+__device__ __forceinline__ int unit_class(unsigned c) { return c >= kHotSteps[0] ? 0 : c >= kHotSteps[1] ? 1 : 2; }
+__device__ void rank_units(const PcParams& p) {
+    __shared__ unsigned long long s_wave[kBlock / 64];
+    const unsigned units = ((unsigned)p.n0 + 255u) / 256u;
+    const unsigned per = (units + kBlock - 1) / kBlock, j0 = min(units, threadIdx.x * per), j1 = min(units, j0 + per);
+    unsigned long long mine = 0;               // class counts of this thread's run, 21 bits each
+    for (unsigned j = j0; j < j1; ++j) mine += 1ull << (21 * unit_class(p.ucost[p.ucol[j]]));
+    unsigned long long inc = mine;             // inclusive scan in the wave, then over the waves
+    const int lane = lane_id(), wave = (int)(threadIdx.x >> 6);
+    for (int off = 1; off < 64; off <<= 1) {
+        const unsigned long long v = __shfl_up(inc, off, 64);
+        if (lane >= off) inc += v;
+    }
+    if (lane == 63) s_wave[wave] = inc;
+    __syncthreads();
+    unsigned long long before = 0, total = 0;
+    for (int w = 0; w < kBlock / 64; ++w) {
+        if (w < wave) before += s_wave[w];
+        total += s_wave[w];
+    }
+    const unsigned long long ex = before + inc - mine;
+    const unsigned m = (1u << 21) - 1u;
+    const unsigned t0 = (unsigned)total & m, t1 = (unsigned)(total >> 21) & m;
+    unsigned at[3] = {(unsigned)ex & m, t0 + ((unsigned)(ex >> 21) & m), t0 + t1 + ((unsigned)(ex >> 42) & m)};
+    for (unsigned j = j0; j < j1; ++j) {
+        const unsigned u = p.ucol[j];
+        p.uorder[at[unit_class(p.ucost[u])]++] = u;
+        p.ucost[u] = 0;
+    }
+}
+
 __global__ __launch_bounds__(kBlock) void k_pack_a(PcParams p) {
     if (!p.occ_inplace) pack_region(p.sqA, p.scapA, p.scntA, p.grid, p.sflatA, &p.totals[0], blockIdx.x);
     pack_region(p.cq, p.ccapA, p.ccnt, p.grid, p.cflat, &p.totals[1], blockIdx.x, p.cid, (unsigned)p.cap);
-    if (p.urank && blockIdx.x == 0 && threadIdx.x == 0) *p.uhcount_r = 0;   // k_chain is done with it: the next frame's count
 }
 __global__ __launch_bounds__(kBlock) void k_pack_b(PcParams p) {
     pack_region(p.sqB, p.scapB, p.scntB, p.gb, p.sflatB, &p.totals[2], blockIdx.x);
@@ -1595,6 +1608,9 @@ __global__ __launch_bounds__(kBlock, BQ || COUNT ? RT_MIX_WAVES : RT_MIX_NOBQ_WA
         else
             occlude_body<COUNT>(s, p, blockIdx.x - p.gb, gridDim.x - p.gb, p.sflatA, p.totals[0], 0);
     }
+    // a lone frame's next unit order, by the last shadow-role workgroup once its shadow rays are done:
+    // beside phase B's deep chains, off the frame's critical path (in k_pack_a it cost 30 us there)
+    if (!COUNT && !chain && p.urank && blockIdx.x == gridDim.x - 1) rank_units(p);
 }
 
 // Phase B's shadow tasks (which = 1), or phase A's (which = 0: p.split_occ, frame batches).

@@ -80,10 +80,25 @@ enum CounterSlot : int {
 #define RT_COMPACT_LEVELS 2
 #endif
 constexpr int kCompactLevels = RT_COMPACT_LEVELS;
-// Samples whose phase-A walks take at least this many steps mark their unit hot (PcParams::umark_w): the
-// heaviest units only (the list is dealt in the order the units were marked, so it must be short enough
-// to start at once; a 32-step threshold listed too many, measured no gain).
-constexpr unsigned kHotSteps = 96;
+// Phase-A unit u's column-order unit (pathchain.hip unit_order): the 256-sample units of a launch dealt
+// in blocks ublk_w units wide and ublk_h rows high (-1: a frame high), so the units in flight cover a
+// column of the image; identity when ublk_h == 0 or the units do not tile the rows.  Host and device
+// (the host makes lone frames' column-order table, PcParams::ucol).
+__host__ __device__ inline unsigned unit_col(int tiles_x, int ublk_h, int ublk_w, int nframes, unsigned u,
+                                             unsigned units) {
+    const unsigned upr = (unsigned)tiles_x / 4u;
+    if (ublk_h == 0 || (tiles_x & 3) || units % upr) return u;
+    const unsigned rows = units / upr, bw = (unsigned)ublk_w;
+    const unsigned bh = ublk_h > 0 ? (unsigned)ublk_h : (rows % (unsigned)nframes ? rows : rows / (unsigned)nframes);
+    const unsigned r0 = u / (bh * upr) * bh, h = bh < rows - r0 ? bh : rows - r0;
+    const unsigned i = u - r0 * upr;            // index within the super-row (h rows x upr units)
+    const unsigned c0 = i / (h * bw) * bw, w = bw < upr - c0 ? bw : upr - c0;
+    const unsigned l = i - c0 * h;
+    return (r0 + l / w) * upr + c0 + l % w;
+}
+
+// Unit cost classes (PcParams::ucost): the most phase-A walk steps a sample of the unit took.
+constexpr unsigned kHotSteps[2] = {96, 32};
 
 struct PcParams {
     int width, height, aa, stripe_rows, rank, nranks, slab_rows;
@@ -143,17 +158,15 @@ struct PcParams {
     int ogrid;        // k_occlude persistent grid
     int split_occ;    // 1: A's shadow tasks in their own k_occlude launch (occ_grid workgroups), not in k_mix
     int occ_grid;     // resident k_occlude workgroups
-    // Lone frames' phase-A units, the previous frame's heaviest first (rt_api.cpp render_chain, hot_units).
-    // Frame g (ugen) marks a unit hot when a sample of it walked at least kHotSteps steps: umark_w[u] = g
-    // (atomicMax: the first mark appends u to uhot_w, *uhcount_w of them); with uorder_on it deals the
-    // previous frame's list (uhot_r, *uhcount_r) before the column order, whose units marked in that
-    // frame (umark_r[u] == g - 1) it then skips.  The read and write arrays alternate by frame (no
-    // clearing but the list count, which k_pack_a zeroes once k_chain is done with it).  Where the work
-    // goes, never what it computes.
-    unsigned *umark_w, *uhot_w, *uhcount_w;
-    const unsigned *umark_r, *uhot_r;
-    unsigned* uhcount_r;
-    unsigned ugen;
+    // Lone frames' phase-A units, the previous frame's heaviest first (rt_api.cpp render_chain,
+    // hot_units): k_chain records per unit the most walk steps a sample of it took (ucost: samples of at
+    // least kHotSteps[1] only, atomicMax), k_pack_a ranks the units into uorder by that cost's class
+    // (>= kHotSteps[0], >= kHotSteps[1], the rest; each class in the column order) and clears ucost; the
+    // next frame of the same geometry deals its units in that order (uorder_on).  Where the work goes,
+    // never what it computes.
+    unsigned* ucost;
+    unsigned* uorder;
+    const unsigned* ucol;   // [units]: unit_col of 0, 1, ... (rank_units reads it instead of dividing)
     int urank, uorder_on;
     int occ_inplace;  // 1 (split_occ production launches): k_occlude walks A's shadow tasks in their phase-A
                       // regions (workgroup w: regions w, w + G, ...); k_pack_a packs only the continuations

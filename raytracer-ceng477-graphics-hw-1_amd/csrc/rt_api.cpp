@@ -90,7 +90,8 @@ struct rt_scene {
     dl::TriShade* d_tri = nullptr;
     dl::Material* d_mats = nullptr;
     dl::Light* d_lights = nullptr;
-    char* d_block = nullptr;                   // one allocation holding every d_ array above and the two below
+    char* d_block = nullptr;                   // the flat arrays above and the two below (upload_flat)
+    char* d_block2 = nullptr;                  // the wide trees and the occlusion pairs (upload_rest)
     unsigned long long* d_counters = nullptr;
     unsigned* d_err = nullptr;                 // device error word (DevScene.err)
     unsigned* h_err = nullptr;                 // pinned host copy of it (rt_render reads it with the frame)
@@ -183,13 +184,19 @@ struct rt_scene {
         size_t bytes = 0;
         hipEvent_t last = nullptr;
         hipStream_t last_stream = nullptr;
-        // lone frames' hot phase-A units (PcParams::umark_* / uhot_* / uhcount_*): mark[2][n], hot[2][n],
-        // count[2] for hist_units = n units, alternating by frame generation hist_gen
+        // lone frames' phase-A unit order (PcParams::ucost / uorder): ucost then uorder, hist_units each
         unsigned* hist = nullptr;
         unsigned hist_units = 0;
-        unsigned hist_gen = 1;
-        uint64_t hist_key = 0;               // the launch geometry of the last frame that marked units
+        uint64_t hist_key = 0;               // the launch geometry uorder was ranked for (0: none yet)
     } arenas[kSlots];
+    // continuation share of frame batches (phase B's record space, cb): each batched launch copies its
+    // continuation count (k_pack_a's total) to pinned memory behind it; once that copy is done the share
+    // is folded into cont_frac, which sizes the next launches' cb (and so their frames per launch)
+    double cont_frac = 0;                      // 0: none seen yet (cap / tune_cont_den)
+    unsigned* h_cont = nullptr;                // pinned, per slot
+    hipEvent_t cont_ev[kSlots] = {};
+    size_t cont_cap[kSlots] = {};
+    bool cont_pending[kSlots] = {};
     hipStream_t slot_stream[kSlots] = {};
     hipEvent_t slot_done[kSlots] = {};
     hipEvent_t fork_ev = nullptr;
@@ -229,8 +236,12 @@ struct rt_scene {
         for (auto& e : kt.ev)
             if (e) (void)hipEventDestroy(e);
         for (auto& a : arenas) (void)hipFree(a.hist);
+        for (auto& e : cont_ev)
+            if (e) (void)hipEventDestroy(e);
+        if (h_cont) (void)hipHostFree(h_cont);
         (void)hipFree(batch_out);
-        (void)hipFree(d_block);           // the scene arrays, counters and error word (upload_scene)
+        (void)hipFree(d_block);           // the scene arrays, counters and error word (upload_flat / _rest)
+        (void)hipFree(d_block2);
         (void)hipFree(d_out); (void)hipFree(d_trace);
         if (h_err) (void)hipHostFree(h_err);
         if (ev0) (void)hipEventDestroy(ev0);
@@ -287,38 +298,87 @@ double ms_since(std::chrono::steady_clock::time_point t) {
     return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t).count();
 }
 
+int upload_flat(rt_scene* s);
+int upload_rest(rt_scene* s, const rt_options* opts);
+
 int finish_scene(rt_scene* s, const rt_options* opts) {
     auto t = std::chrono::steady_clock::now();
     rtx::prepare_triangles(s->host);
     s->prep_ms = ms_since(t);
-    std::string err = rtx::build_bvh(s->host, s->bvh, opts ? opts->build_threads : 0);
-    if (!err.empty()) return fail(RT_ERR_LIMIT, err);
     s->host_only = opts && (opts->flags & RT_OPT_HOST_ONLY);
     s->opt_flags = opts ? opts->flags : 0;
-    if (s->host_only) return RT_OK;
-    join_device_warmup();
     const int ndev = g_devices.load();
+    rt_options o = opts ? *opts : rt_options{0, 0, 0};
+    if (ndev >= 1) o.device = 0;          // device group: the primary on device 0, replicas on 1..n-1
+    // the arrays final after the flatten go to the device while the wide trees are still being built
+    // (their own thread, which also joins the HIP warm-up): an explicit device only, since -1 means the
+    // calling thread's current device
+    std::future<int> early;
+    bool started = false;
+    std::function<void()> on_flat = [&] {
+        started = true;
+        early = std::async(std::launch::async, [s, o]() -> int {
+            join_device_warmup();
+            const int rc = select_device(&o, &s->device);
+            return rc ? rc : upload_flat(s);
+        });
+    };
+    std::string err = rtx::build_bvh(s->host, s->bvh, opts ? opts->build_threads : 0,
+                                     !s->host_only && o.device >= 0 ? &on_flat : nullptr);
     t = std::chrono::steady_clock::now();
-    if (ndev >= 1) {                      // device group: the primary on device 0, replicas on 1..n-1
-        rt_options o = opts ? *opts : rt_options{0, 0, 0};
-        o.device = 0;
-        int rc = upload_scene(s, &o);
-        if (rc) return rc;
-        rc = rt_internal_group_create(s, ndev, &s->group);
-        s->upload_ms = ms_since(t);
-        return rc;
+    int rc = early.valid() ? early.get() : RT_OK;
+    if (!err.empty()) return fail(RT_ERR_LIMIT, err);
+    if (s->host_only || rc) return rc;
+    if (!started) {
+        join_device_warmup();
+        if ((rc = select_device(&o, &s->device)) || (rc = upload_flat(s))) return rc;
+    } else {
+        HIP_TRY(hipSetDevice(s->device));    // (the early upload set it on its own thread)
     }
-    const int rc = upload_scene(s, opts);
-    s->upload_ms = ms_since(t);
+    rc = upload_rest(s, &o);
+    if (!rc && ndev >= 1) rc = rt_internal_group_create(s, ndev, &s->group);
+    s->upload_ms = ms_since(t);              // (the part after the build: the early upload overlaps it)
     return rc;
+}
+
+// Device copies of scene arrays in one fresh allocation: 256-B aligned parts, each at least one element,
+// then `zero` bytes zeroed; returns the zeroed region's offset in *zero_at.
+struct UpPart { void** dst; const void* src; size_t bytes, min; };
+template <class T, class V>
+UpPart up_part(T** dst, const V& v) {
+    return UpPart{reinterpret_cast<void**>(dst), v.data(), v.size() * sizeof(v[0]), sizeof(v[0])};
+}
+int upload_parts(char** block, const UpPart* parts, int n, size_t zero, size_t* zero_at, size_t* bytes) {
+    auto up = [](size_t b) { return (b + 255) & ~size_t(255); };
+    size_t off = 0;
+    *bytes = 0;
+    for (int i = 0; i < n; ++i) {
+        off += up(std::max(parts[i].bytes, parts[i].min));
+        *bytes += parts[i].bytes;
+    }
+    if (zero_at) *zero_at = off;
+    HIP_TRY(hipMalloc(reinterpret_cast<void**>(block), std::max<size_t>(off + zero, 1)));
+    off = 0;
+    for (int i = 0; i < n; ++i) {
+        *parts[i].dst = *block + off;
+        if (parts[i].bytes) HIP_TRY(hipMemcpy(*parts[i].dst, parts[i].src, parts[i].bytes, hipMemcpyHostToDevice));
+        off += up(std::max(parts[i].bytes, parts[i].min));
+    }
+    if (zero) HIP_TRY(hipMemset(*block + off, 0, zero));
+    return RT_OK;
 }
 
 // Device copies of a built scene (s->host, s->bvh) on opts->device, plus the
 // per-scene tuning knobs.
 int upload_scene(rt_scene* s, const rt_options* opts) {
     int rc = select_device(opts, &s->device);
-    if (rc) return rc;
+    if (!rc) rc = upload_flat(s);
+    return rc ? rc : upload_rest(s, opts);
+}
 
+// The arrays final once the flatten is done (the reference tree, its prims, pairs and leaf records, the
+// shading tables), the counters and the error word; on the current device.
+int upload_flat(rt_scene* s) {
     std::vector<dl::Material> mats(s->host.materials.size());
     for (size_t i = 0; i < mats.size(); ++i) {
         const rtx::MaterialRec& m = s->host.materials[i];
@@ -336,35 +396,27 @@ int upload_scene(rt_scene* s, const rt_options* opts) {
         lights[i] = dl::Light{l.position.x, l.position.y, l.position.z, 0, l.intensity.x, l.intensity.y,
                               l.intensity.z, 0};
     }
-    {   // one device allocation for every scene array, the counters and the error word (256-B aligned
-        // parts, each at least one element), the arrays copied in, counters and error word zeroed at once
-        struct Part { void** dst; const void* src; size_t bytes, min; };
-        auto part = [](auto** dst, const auto& v) {
-            return Part{reinterpret_cast<void**>(dst), v.data(), v.size() * sizeof(v[0]), sizeof(v[0])};
-        };
-        const Part parts[] = {part(&s->d_nodes, s->bvh.nodes), part(&s->d_prims, s->bvh.prims),
-                              part(&s->d_tri, s->bvh.tri_shade), part(&s->d_mats, mats), part(&s->d_lights, lights),
-                              part(&s->d_pairs, s->bvh.pairs), part(&s->d_leafbig, s->bvh.leaf_big),
-                              part(&s->d_spairs, s->bvh.spairs), part(&s->d_swnodes, s->bvh.swnodes),
-                              part(&s->d_wnodes, s->bvh.wnodes), part(&s->d_lrec, s->bvh.lrec)};
-        auto up = [](size_t b) { return (b + 255) & ~size_t(255); };
-        size_t off = 0;
-        s->scene_bytes = 0;
-        for (const Part& q : parts) {
-            off += up(std::max(q.bytes, q.min));
-            s->scene_bytes += q.bytes;
-        }
-        const size_t zero_off = off, zero_bytes = up(rtc::kCounters * sizeof(unsigned long long)) + up(sizeof(unsigned));
-        HIP_TRY(hipMalloc(reinterpret_cast<void**>(&s->d_block), zero_off + zero_bytes));
-        off = 0;
-        for (const Part& q : parts) {
-            *q.dst = s->d_block + off;
-            if (q.bytes) HIP_TRY(hipMemcpy(*q.dst, q.src, q.bytes, hipMemcpyHostToDevice));
-            off += up(std::max(q.bytes, q.min));
-        }
-        s->d_counters = reinterpret_cast<unsigned long long*>(s->d_block + zero_off);
-        s->d_err = reinterpret_cast<unsigned*>(s->d_block + zero_off + up(rtc::kCounters * sizeof(unsigned long long)));
-        HIP_TRY(hipMemset(s->d_block + zero_off, 0, zero_bytes));
+    const UpPart parts[] = {up_part(&s->d_nodes, s->bvh.nodes), up_part(&s->d_prims, s->bvh.prims),
+                            up_part(&s->d_tri, s->bvh.tri_shade), up_part(&s->d_mats, mats),
+                            up_part(&s->d_lights, lights), up_part(&s->d_pairs, s->bvh.pairs),
+                            up_part(&s->d_leafbig, s->bvh.leaf_big), up_part(&s->d_lrec, s->bvh.lrec)};
+    const size_t cbytes = (rtc::kCounters * sizeof(unsigned long long) + 255) & ~size_t(255);
+    size_t zat = 0, bytes = 0;
+    if (const int rc = upload_parts(&s->d_block, parts, 8, cbytes + 256, &zat, &bytes)) return rc;
+    s->d_counters = reinterpret_cast<unsigned long long*>(s->d_block + zat);
+    s->d_err = reinterpret_cast<unsigned*>(s->d_block + zat + cbytes);
+    s->scene_bytes = bytes;
+    return RT_OK;
+}
+
+// The wide trees and the occlusion tree's pairs (the build's last results), events, grids and knobs.
+int upload_rest(rt_scene* s, const rt_options* opts) {
+    {
+        const UpPart parts[] = {up_part(&s->d_spairs, s->bvh.spairs), up_part(&s->d_swnodes, s->bvh.swnodes),
+                                up_part(&s->d_wnodes, s->bvh.wnodes)};
+        size_t bytes = 0;
+        if (const int rc = upload_parts(&s->d_block2, parts, 3, 0, nullptr, &bytes)) return rc;
+        s->scene_bytes += bytes;
     }
     HIP_TRY(hipEventCreate(&s->ev0));
     HIP_TRY(hipEventCreate(&s->ev1));
@@ -441,8 +493,8 @@ int upload_scene(rt_scene* s, const rt_options* opts) {
     rtk::DevScene& d = s->dev;
     d.nodes = s->d_nodes; d.prims = s->d_prims; d.tri_shade = s->d_tri; d.mats = s->d_mats; d.lights = s->d_lights;
     d.nnodes = (int)s->bvh.nodes.size();
-    d.nlights = (int)lights.size();
-    d.nmats = (int)mats.size();
+    d.nlights = (int)s->host.lights.size();
+    d.nmats = (int)s->host.materials.size();
     d.max_depth = s->host.max_depth;
     d.stack_entries = std::max(2, s->bvh.max_stack);
     d.eps = s->host.eps;
@@ -504,8 +556,8 @@ int upload_scene(rt_scene* s, const rt_options* opts) {
     if (const char* e = std::getenv("RT_LEAF_WAIT_ANY")) d.leaf_wait_any = std::max(0, std::min(64, std::atoi(e)));
     // shadow rays of lights behind the surface add +-0 when kd is finite (pathchain.hip light_needed)
     d.cull_shadows = 1;
-    for (const auto& m : mats)
-        if (!std::isfinite(m.kdx) || !std::isfinite(m.kdy) || !std::isfinite(m.kdz)) d.cull_shadows = 0;
+    for (const auto& m : s->host.materials)
+        if (!std::isfinite(m.diffuse.x) || !std::isfinite(m.diffuse.y) || !std::isfinite(m.diffuse.z)) d.cull_shadows = 0;
     if (const char* e = std::getenv("RT_CULL")) d.cull_shadows = d.cull_shadows && std::atoi(e) != 0;
     d.force_fb = std::getenv("RT_FORCE_FALLBACK") ? std::atoi(std::getenv("RT_FORCE_FALLBACK")) : 0;
     // measurement: counting passes walk the production trees and count fetched bytes (bench.py)
@@ -742,8 +794,11 @@ ChainPlan chain_plan(const rt_scene* s, const ChainGeom& g, size_t nunits, bool 
     // records: levels [0, la) for every sample; deeper ones (phase B) for the first cb continuations
     // (the rest finish in k_fallback; counting passes keep every one: cb = cap)
     P.la = fused || !P.phase_b ? levels : P.levels_a;
-    P.cb = P.la >= levels ? 0 : (count ? cap : std::min(cap, std::max(cap / (size_t)std::max(1, s->tune_cont_den),
-                                                                        std::min<size_t>(cap, 65536))));
+    // (at least cap / RT_CONT_DEN, more once frame batches report a larger continuation share: that share
+    // + 10 %)
+    const size_t cb_guess = std::max(cap / (size_t)std::max(1, s->tune_cont_den),
+                                     (size_t)((double)cap * std::min(1.0, s->cont_frac * 1.1 + 0.005)));
+    P.cb = P.la >= levels ? 0 : (count ? cap : std::min(cap, std::max(cb_guess, std::min<size_t>(cap, 65536))));
     if (cb_want > 0 && !count && P.la < levels) P.cb = std::min(cap, std::max(P.cb, cb_want));
     if (s->tune_cont_cb > 0 && !count && P.la < levels) P.cb = std::min(cap, (size_t)s->tune_cont_cb);
     P.tchunk = s->tune_tchunk > 0 ? s->tune_tchunk : (g.nframes > 1 ? 128 : 1);
@@ -971,28 +1026,28 @@ int render_chain(rt_scene* s, const rtk::Eye& eye, const rtk::FrameParams& f, bo
                 arena.hist = nullptr;
                 arena.hist_units = 0;
                 arena.hist_key = 0;
-                const size_t words = 4 * (size_t)nu + 2;
-                HIP_TRY(hipMalloc(reinterpret_cast<void**>(&arena.hist), words * sizeof(unsigned)));
-                HIP_TRY(hipMemsetAsync(arena.hist, 0, words * sizeof(unsigned), st));
+                HIP_TRY(hipMalloc(reinterpret_cast<void**>(&arena.hist), 3 * (size_t)nu * sizeof(unsigned)));
+                HIP_TRY(hipMemsetAsync(arena.hist, 0, 2 * (size_t)nu * sizeof(unsigned), st));
                 arena.hist_units = nu;
-                arena.hist_gen = 1;            // marks start at 0: generations from 2 on never match them
             }
             uint64_t key = 1469598103934665603ull;   // the geometry the order is valid for
             for (long long v : {(long long)p.width, (long long)p.height, (long long)p.aa, (long long)p.stripe_rows,
                                 (long long)p.rank, (long long)p.nranks, (long long)p.slab_rows, (long long)p.n0,
                                 (long long)p.tiles_x, (long long)p.ublk_h, (long long)p.ublk_w})
                 key = (key ^ (uint64_t)v) * 1099511628211ull;
-            const unsigned g_ = ++arena.hist_gen, w = g_ & 1u, r = w ^ 1u;
-            unsigned* const mark = arena.hist;
-            unsigned* const list = arena.hist + 2 * (size_t)nu;
-            unsigned* const cnt = arena.hist + 4 * (size_t)nu;
-            p.umark_w = mark + w * (size_t)nu; p.umark_r = mark + r * (size_t)nu;
-            p.uhot_w = list + w * (size_t)nu; p.uhot_r = list + r * (size_t)nu;
-            p.uhcount_w = cnt + w; p.uhcount_r = cnt + r;
-            p.ugen = g_;
+            p.ucost = arena.hist;
+            p.uorder = arena.hist + nu;
+            p.ucol = arena.hist + 2 * (size_t)nu;
+            if (arena.hist_key != key) {           // this geometry's column order (unit_col), once
+                std::vector<unsigned> col(nu);
+                for (unsigned u = 0; u < nu; ++u) col[u] = rtc::unit_col(p.tiles_x, p.ublk_h, p.ublk_w, p.nframes, u, nu);
+                HIP_TRY(hipMemcpyAsync(arena.hist + 2 * (size_t)nu, col.data(), nu * sizeof(unsigned),
+                                       hipMemcpyHostToDevice, st));
+                HIP_TRY(hipStreamSynchronize(st));   // (the pageable source goes out of scope)
+            }
             p.urank = 1;
-            p.uorder_on = arena.hist_key == key ? 1 : 0;   // the previous frame marked this geometry
-            arena.hist_key = key;
+            p.uorder_on = arena.hist_key == key ? 1 : 0;   // ranked by the previous frame of this geometry
+            arena.hist_key = key;                          // (its k_pack_a ran before this k_chain: stream order)
         }
         // phase A's stragglers hand their walks to phase B once this share of k_chain's waves is done
         p.abandon = s->tune_abandon > 0 && !count && P.phase_b && !P.split_occ   // lone frames (k_mix with the BQ)
@@ -1017,6 +1072,14 @@ int render_chain(rt_scene* s, const rtk::Eye& eye, const rtk::FrameParams& f, bo
         } else {
             HIP_TRY(rtc::launch_chain_chunk(s->dev, eye, p, count, st));
         }
+    }
+    if (!count && !fused && P.phase_b && p.nframes > 1 && s->tune_cont_cb == 0) {   // the share, read back later
+        if (!s->h_cont) HIP_TRY(hipHostMalloc(reinterpret_cast<void**>(&s->h_cont), rt_scene::kSlots * sizeof(unsigned)));
+        if (!s->cont_ev[slot]) HIP_TRY(hipEventCreateWithFlags(&s->cont_ev[slot], hipEventDisableTiming));
+        HIP_TRY(hipMemcpyAsync(&s->h_cont[slot], p.totals + 1, sizeof(unsigned), hipMemcpyDeviceToHost, st));
+        HIP_TRY(hipEventRecord(s->cont_ev[slot], st));
+        s->cont_cap[slot] = cap;
+        s->cont_pending[slot] = true;
     }
     if (p.trace) trace_dump(s, st, 0, (unsigned)cap, (unsigned)p.trace_blocks, trace_n);   // last chunk only
     if (!arena.last) HIP_TRY(hipEventCreateWithFlags(&arena.last, hipEventDisableTiming));
@@ -1347,6 +1410,13 @@ int render_cameras(rt_scene* s, const rt_camera* cams, int n, int aa, void* cons
         std::vector<int> starts;
         HIP_TRY(hipSetDevice(s->device));
         if (const int rc = ensure_chain_grids(s)) return rc;
+        // completed continuation-share read-backs (never waited for): the largest recent share, decaying
+        for (int k = 0; k < rt_scene::kSlots; ++k)
+            if (s->cont_pending[k] && hipEventQuery(s->cont_ev[k]) == hipSuccess) {
+                s->cont_pending[k] = false;
+                const double f = s->cont_cap[k] ? (double)s->h_cont[k] / (double)s->cont_cap[k] : 0.0;
+                s->cont_frac = std::max(f, s->cont_frac * 0.75);
+            }
         for (int i = 0; i < n;) {
             const auto& c = cams[i];
             // a batch of k frames: one launch (render_chain's own plan fits the slot's workspace share)

@@ -266,10 +266,10 @@ def test_wait_bound_reports_limit(pkg, scene_dir, goldens, torch_cuda, monkeypat
 
 @pytest.mark.parametrize("hot", ["1", "0"])
 def test_repeated_lone_frames_equal_golden(pkg, scene_dir, goldens, torch_cuda, monkeypatch, hot):
-    """Lone frames deal their phase-A units by the previous frame's hot units (rt_api.cpp hot_units,
-    pathchain.hip unit_deal: the listed units first, then the column order without them; the mark and
-    list arrays alternate by frame).  Frames of one geometry in a row, another geometry between them
-    (the lists' key changes) and back: every frame is the golden."""
+    """Lone frames deal their phase-A units in the order the previous frame ranked them (rt_api.cpp
+    hot_units, pathchain.hip rank_units: the units whose samples walked the most steps first).  Frames of
+    one geometry in a row, another geometry between them (the ranking's key changes) and back: every
+    frame is the golden."""
     from conftest import config_path, golden_by_name, load_golden_image
     monkeypatch.setenv("RT_HOT_UNITS", hot)
     g1 = golden_by_name(goldens, "C3_hm_1080p_d6_aa1")
