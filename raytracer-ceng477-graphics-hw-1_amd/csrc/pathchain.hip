@@ -40,6 +40,11 @@ constexpr int kBlock = 256;
 #ifndef RT_FINISH_PREFETCH
 #define RT_FINISH_PREFETCH 1   // k_finish: next level's record in flight while shading
 #endif
+#ifndef RT_FINISH_CMP_WAVES
+#define RT_FINISH_CMP_WAVES 3 // k_finish<true> (compact records: the rebuilt directions): 4 waves spilled 28 VGPRs,
+                              // whose scratch traffic reached HBM (k_finish 150 MB per batched frame, 77 MB of
+                              // algorithmic bytes); 3 waves: no spills
+#endif
 #ifndef RT_FINISH_WAVES
 #define RT_FINISH_WAVES 4     // k_finish: 128 VGPRs, 4 waves/SIMD, no spills (unbounded: 129, 3 waves): C3 batches
                               // 0.507-0.508 -> 0.502-0.504 ms/frame; 5 (spills) 0.532, 6 0.559
@@ -2099,7 +2104,8 @@ __device__ __forceinline__ void finish_pixels(const rtk::DevScene& s, const rtk:
 // the scene's materials and lights in LDS (host checks they fit);
 // k_finish_any: the same for larger scenes, tables read from global memory.
 template <bool CMP>
-__global__ __launch_bounds__(kBlock, RT_FINISH_WAVES) void k_finish(rtk::DevScene s, rtk::Eye e, PcParams p) {
+__global__ __launch_bounds__(kBlock, CMP ? RT_FINISH_CMP_WAVES : RT_FINISH_WAVES) void k_finish(rtk::DevScene s,
+                                                                                                 rtk::Eye e, PcParams p) {
     float4* dm = reinterpret_cast<float4*>(g_fmats);
     const float4* sm = reinterpret_cast<const float4*>(s.mats);
     for (int i = threadIdx.x; i < s.nmats * 4; i += kBlock) dm[i] = sm[i];

@@ -884,6 +884,19 @@ size_t chain_launch_units(rt_scene* s, const ChainGeom& g, bool count, size_t* c
     return units;
 }
 
+// Fold the continuation-share read-backs that are done (wait: wait for them) into s->cont_frac: the
+// largest recent share, decaying.
+void poll_cont(rt_scene* s, bool wait) {
+    for (int k = 0; k < rt_scene::kSlots; ++k) {
+        if (!s->cont_pending[k]) continue;
+        if (wait) (void)hipEventSynchronize(s->cont_ev[k]);
+        if (hipEventQuery(s->cont_ev[k]) != hipSuccess) continue;
+        s->cont_pending[k] = false;
+        const double f = s->cont_cap[k] ? (double)s->h_cont[k] / (double)s->cont_cap[k] : 0.0;
+        s->cont_frac = std::max(f, s->cont_frac * 0.75);
+    }
+}
+
 int render_chain(rt_scene* s, const rtk::Eye& eye, const rtk::FrameParams& f, bool count, hipStream_t st,
                  int slot = 0) {
     rt_scene::Arena& arena = s->arenas[slot];
@@ -894,6 +907,7 @@ int render_chain(rt_scene* s, const rtk::Eye& eye, const rtk::FrameParams& f, bo
     const int max_grid = fused ? s->fused_grid : s->chain_grid;
     auto grid_for = [&](int n0) { return std::max(1, std::min(max_grid, (n0 + 255) / 256)); };
     size_t cb = 0;
+    if (f.chunk_k == 1) poll_cont(s, false);   // (read-backs of earlier frames' chunks, C5-sized frames)
     const size_t units = chain_launch_units(s, g, count, &cb);
     const ChainPlan P = chain_plan(s, g, units, count, cb);
     const int chunk_rows = (int)units * unit;
@@ -1073,7 +1087,7 @@ int render_chain(rt_scene* s, const rtk::Eye& eye, const rtk::FrameParams& f, bo
             HIP_TRY(rtc::launch_chain_chunk(s->dev, eye, p, count, st));
         }
     }
-    if (!count && !fused && P.phase_b && p.nframes > 1 && s->tune_cont_cb == 0) {   // the share, read back later
+    if (!count && !fused && P.phase_b && (p.nframes > 1 || chunk_rows < li) && s->tune_cont_cb == 0) {   // the share, read back later
         if (!s->h_cont) HIP_TRY(hipHostMalloc(reinterpret_cast<void**>(&s->h_cont), rt_scene::kSlots * sizeof(unsigned)));
         if (!s->cont_ev[slot]) HIP_TRY(hipEventCreateWithFlags(&s->cont_ev[slot], hipEventDisableTiming));
         HIP_TRY(hipMemcpyAsync(&s->h_cont[slot], p.totals + 1, sizeof(unsigned), hipMemcpyDeviceToHost, st));
@@ -1410,13 +1424,7 @@ int render_cameras(rt_scene* s, const rt_camera* cams, int n, int aa, void* cons
         std::vector<int> starts;
         HIP_TRY(hipSetDevice(s->device));
         if (const int rc = ensure_chain_grids(s)) return rc;
-        // completed continuation-share read-backs (never waited for): the largest recent share, decaying
-        for (int k = 0; k < rt_scene::kSlots; ++k)
-            if (s->cont_pending[k] && hipEventQuery(s->cont_ev[k]) == hipSuccess) {
-                s->cont_pending[k] = false;
-                const double f = s->cont_cap[k] ? (double)s->h_cont[k] / (double)s->cont_cap[k] : 0.0;
-                s->cont_frac = std::max(f, s->cont_frac * 0.75);
-            }
+        poll_cont(s, false);
         for (int i = 0; i < n;) {
             const auto& c = cams[i];
             // a batch of k frames: one launch (render_chain's own plan fits the slot's workspace share)
@@ -1439,6 +1447,18 @@ int render_cameras(rt_scene* s, const rt_camera* cams, int n, int aa, void* cons
         starts.push_back(n);
         const int nb = (int)starts.size() - 1;
         if (nb == 1) return render_batch(s, cams, n, aa, rows_of(0), rank, nranks, outs_dev, stream, flags, 0);
+        if (s->cont_frac == 0 && !(flags & RT_RENDER_COUNT) && s->tune_cont_cb == 0 &&
+            s->dev.max_depth > s->tune_kinline) {
+            // the scene's continuation share is not known yet: one batch first, waited for, so the rest
+            // are sized by it (once per scene; a mirror-heavy scene otherwise sends most of its deep
+            // chains to k_fallback until the first read-backs arrive)
+            const int rc = render_batch(s, cams, starts[1], aa, rows_of(0), rank, nranks, outs_dev, stream, flags, 0);
+            if (rc) return rc;
+            poll_cont(s, true);
+            s->cont_frac = std::max(s->cont_frac, 1e-9);
+            return render_cameras(s, cams + starts[1], n - starts[1], aa, outs_dev + starts[1], stream, flags,
+                                  stripe_rows, rank, nranks);
+        }
         if (!s->fork_ev) HIP_TRY(hipEventCreateWithFlags(&s->fork_ev, hipEventDisableTiming));
         HIP_TRY(hipEventRecord(s->fork_ev, stream));
         const int used = std::min(nb, nslot);

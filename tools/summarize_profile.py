@@ -30,10 +30,13 @@ prof.mkdir(exist_ok=True)
 
 
 def kname(s):
-    """k_name, with '<true>' kept for counting-pass instantiations."""
+    """k_name, with '<true>' kept for counting-pass instantiations (k_finish's template argument is not
+    COUNT but whether the launch's records are compact: both are the production kernel)."""
     m = re.search(r"(k_[a-z_0-9]+)(<(true|false)[,>])?", s)      # the first template argument: COUNT
     if not m:
         return s[:40]
+    if m.group(1) in ("k_finish", "k_finish_any"):
+        return m.group(1)
     return m.group(1) + ("<true>" if m.group(3) == "true" else "")
 
 
@@ -55,13 +58,15 @@ if stats:
     shutil.copy(stats[0], prof / f"{tag}_kernel_stats.csv")
     rows = list(csv.DictReader(open(stats[0])))
     counting_calls = sum(int(r["Calls"]) for r in rows if kname(r["Name"]) == "k_chain<true>")
+    agg = collections.defaultdict(lambda: [0, 0.0])              # calls, total ns (instantiations merged)
     for r in rows:
         k = kname(r["Name"])
-        if k not in frame_kernels:
-            continue
-        calls, tot = int(r["Calls"]), float(r["TotalDurationNs"])
-        if k in ("k_pack_a", "k_pack_b", "k_finish", "k_finish_any", "k_occlude", "k_fallback"):
-            tot -= min(calls, counting_calls) * float(r["AverageNs"])     # the counting passes' launches
+        if k in frame_kernels:
+            agg[k][0] += int(r["Calls"])
+            agg[k][1] += float(r["TotalDurationNs"])
+    for k, (calls, tot) in agg.items():
+        if k in ("k_pack_a", "k_pack_b", "k_finish", "k_finish_any", "k_occlude", "k_fallback") and calls:
+            tot -= min(calls, counting_calls) * tot / calls              # the counting passes' launches
         per_kernel_ms[k] = tot / frames / 1e6
 kernel_ms_sum = sum(per_kernel_ms.values())
 
