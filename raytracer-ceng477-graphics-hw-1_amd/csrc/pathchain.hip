@@ -1623,19 +1623,25 @@ template <bool COUNT>
 __global__ __launch_bounds__(kBlock, RT_OCC_WAVES_PER_EU) void k_occlude(rtk::DevScene s, PcParams p, int which) {
     block_init(s);
     if constexpr (!COUNT && RT_LEAF_QUEUE) {
-        if (which) {
-            occlude_queue_body(s, p, blockIdx.x, gridDim.x, p.sflatB, p.totals[2]);
-        } else if (p.occ_inplace) {
-            // A's tasks where k_chain left them: phase-A region r (k_chain workgroup r's queue) to
-            // workgroup r mod G, one region at a time (no packed copy of 4 B in and out per task)
-            for (unsigned r = blockIdx.x; r < (unsigned)p.grid; r += gridDim.x) {
+        // tasks where their phase left them: region r (phase workgroup r's queue) to workgroup r mod G,
+        // one region at a time (no packed copy of 4 B in and out per task): A's in frame batches, B's
+        // LDS-queue overflow in lone frames (few tasks; no k_pack_b launch on the frame's critical path)
+        const bool inplace = which ? p.occ_inplace_b != 0 : p.occ_inplace != 0;
+        if (inplace) {
+            const unsigned nreg = which ? (unsigned)p.gb : (unsigned)p.grid;
+            const unsigned* const q = which ? p.sqB : p.sqA;
+            const unsigned* const cnt = which ? p.scntB : p.scntA;
+            const size_t qcap = which ? p.scapB : p.scapA;
+            for (unsigned r = blockIdx.x; r < nreg; r += gridDim.x) {
                 if (r != blockIdx.x) {
                     __syncthreads();            // every wave is done with the previous region
                     if (threadIdx.x == 0) g_head = 0;
                     __syncthreads();
                 }
-                occlude_queue_body(s, p, 0, 1, p.sqA + (size_t)r * p.scapA, p.scntA[r]);
+                occlude_queue_body(s, p, 0, 1, q + (size_t)r * qcap, cnt[r]);
             }
+        } else if (which) {
+            occlude_queue_body(s, p, blockIdx.x, gridDim.x, p.sflatB, p.totals[2]);
         } else {
             occlude_queue_body(s, p, blockIdx.x, gridDim.x, p.sflatA, p.totals[0]);
         }
@@ -2491,7 +2497,7 @@ hipError_t launch_chain_chunk(const rtk::DevScene& s, const rtk::Eye& e, const P
     }
     if (phase_b) {
         mark(kKPackB);
-        hipLaunchKernelGGL(k_pack_b, dim3(p.gb), blk, 0, st, p);
+        if (count || !p.occ_inplace_b) hipLaunchKernelGGL(k_pack_b, dim3(p.gb), blk, 0, st, p);
         const int og = split ? p.occ_grid : p.ogrid;
         mark(kKOccB);
         if (count) hipLaunchKernelGGL(k_occlude<true>, dim3(og), blk, 0, st, s, p, 1);

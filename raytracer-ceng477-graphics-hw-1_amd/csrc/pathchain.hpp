@@ -168,6 +168,8 @@ struct PcParams {
     unsigned* uorder;
     const unsigned* ucol;   // [units]: unit_col of 0, 1, ... (rank_units reads it instead of dividing)
     int urank, uorder_on;
+    int occ_inplace_b;  // 1 (lone-frame production launches): k_occlude walks B's LDS-queue overflow in its
+                        // phase-B regions (no k_pack_b)
     int occ_inplace;  // 1 (split_occ production launches): k_occlude walks A's shadow tasks in their phase-A
                       // regions (workgroup w: regions w, w + G, ...); k_pack_a packs only the continuations
     int fin_grid;     // k_finish workgroups at most (0: a lane per output pixel), a grid-stride loop beyond

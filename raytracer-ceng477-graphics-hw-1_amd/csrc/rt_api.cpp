@@ -982,6 +982,7 @@ int render_chain(rt_scene* s, const rtk::Eye& eye, const rtk::FrameParams& f, bo
     p.fin_grid = s->tune_fgrid > 0 ? s->tune_fgrid : 8 * s->num_cus;
     p.split_occ = P.split_occ ? 1 : 0;
     p.occ_inplace = P.split_occ && !count && s->tune_occ_inplace ? 1 : 0;
+    p.occ_inplace_b = !P.split_occ && !count && !fused && s->tune_occ_inplace ? 1 : 0;
     p.refill = s->tune_refill >= 0 ? s->tune_refill : 0;
     p.service = s->tune_service >= 0 ? s->tune_service : 64;
     p.bservice = s->tune_bservice;
