@@ -226,6 +226,8 @@ __device__ __forceinline__ unsigned block_sample(unsigned v, unsigned G, unsigne
 __shared__ unsigned g_ccnt;    // block-local continuation count
 __shared__ unsigned g_uid[kDynUnits];   // dynamic phase-A units: the workgroup's k-th unit (kUidUnset: not yet taken)
 constexpr unsigned kUidUnset = ~0u, kUidNone = ~0u - 1u;
+// k_mix's early finish: how long a shadow-role workgroup waits for the others (wall_clock64 ticks, 100 MHz)
+constexpr unsigned long long kEarlyFinWait = 20000;
 
 struct PhaseOut {              // where a chain phase writes its tasks
     unsigned* sq;              // shadow tasks, region blk at sq + blk * scap
@@ -1002,6 +1004,7 @@ __device__ void chain_body(const rtk::DevScene& s, const rtk::Eye& e, const PcPa
                 nrefl++;
                 if (!COUNT && defer_closest(s, r)) {     // the rest of this path: k_fallback
                     if (lvp < p.dbase) p.tail[path] = make_float4(dk.x, dk.y, dk.z, 0.0f);   // reflect_from_record
+                    if (!CONT) p.pinfo[path] = kPathCont;   // not finished before k_fallback (early_finish)
                     fb_chain(p, (unsigned)lvp);
                     st = kIdle;
                 } else {
@@ -1074,7 +1077,10 @@ __device__ void chain_body(const rtk::DevScene& s, const rtk::Eye& e, const PcPa
                                 if (p.trace) t_grab = (unsigned)wall_clock64();
                                 nprim++;
                                 if (s.max_depth < 0) p.pinfo[path] = 0 | (kEndZero << 8);   // depth 0 > max: black
-                                else if (!COUNT && defer_closest(s, r)) fb_chain(p, kFbEye | path);
+                                else if (!COUNT && defer_closest(s, r)) {
+                                    p.pinfo[path] = kPathCont;   // (early_finish: k_fallback's)
+                                    fb_chain(p, kFbEye | path);
+                                }
                                 else if (RT_PACKET_WALK && p.packet) fresh = true;
                                 else st = walk_begin<COUNT>(s, r, wk, w) ? kTrav : kDone;
                             }
@@ -1596,6 +1602,13 @@ __global__ __launch_bounds__(kBlock) void k_pack_b(PcParams p) {
 #ifndef RT_MIX_NOBQ_WAVES
 #define RT_MIX_NOBQ_WAVES 5      // without the LDS queue: 96 VGPRs, no spills
 #endif
+// Early finish (PcParams::early_fin, lone frames): pixels without a continued sample, taken 64 at a time
+// from totals[9] (defined with k_finish; k_finish takes what is left)
+__shared__ unsigned g_efin;
+template <bool LDS, bool CMP>
+__device__ void finish_taken(const rtk::DevScene& s, const rtk::Eye& e, const PcParams& p, unsigned* ctr,
+                             unsigned stop_at);
+
 template <bool COUNT, bool BQ>
 __global__ __launch_bounds__(kBlock, BQ || COUNT ? RT_MIX_WAVES : RT_MIX_NOBQ_WAVES) void k_mix(rtk::DevScene s,
                                                                                                   rtk::Eye e, PcParams p) {
@@ -1606,16 +1619,55 @@ __global__ __launch_bounds__(kBlock, BQ || COUNT ? RT_MIX_WAVES : RT_MIX_NOBQ_WA
     if (chain) {
         if (p.bprio) __builtin_amdgcn_s_setprio(3);    // the deep chains are the frame's critical path
         chain_body<COUNT, true, BQ>(s, e, p, blockIdx.x, (unsigned)p.gb, phase_b(p));
+        if (!COUNT && BQ && p.early_fin && lane_id() == 0) atomicAdd(&p.totals[10], 1u);   // this chain wave is done
+        return;
     }
-    else if (!p.exp_skip_occ) {
+    if (!p.exp_skip_occ) {
         if constexpr (!COUNT && RT_LEAF_QUEUE)
             occlude_queue_body(s, p, blockIdx.x - p.gb, gridDim.x - p.gb, p.sflatA, p.totals[0]);
         else
             occlude_body<COUNT>(s, p, blockIdx.x - p.gb, gridDim.x - p.gb, p.sflatA, p.totals[0], 0);
     }
+    const bool ranker = !COUNT && p.urank && blockIdx.x == gridDim.x - 1;
+    if constexpr (!COUNT && BQ) {
+        if (p.early_fin) {
+            // A lone frame's pixels without a continued sample: their records and A's occlusion bytes are
+            // final once every shadow-role workgroup has walked its tasks, so these workgroups shade and
+            // fold them beside phase B's deep chains instead of k_finish after them.  The wait for the
+            // other workgroups is bounded (kEarlyFinWait, no error: k_finish then takes their share), and
+            // pixels are taken only while phase B still runs (totals[10]), so the launch is no longer.
+            const unsigned nshadow = gridDim.x - (unsigned)p.gb, nchain = (unsigned)p.gb * (kBlock / 64);
+            __syncthreads();                        // every wave of this workgroup is done with its tasks
+            if (threadIdx.x == 0) {
+                __threadfence();                    // (release) this workgroup's occlusion bytes
+                atomicAdd(&p.totals[8], 1u);
+            }
+            if (ranker) rank_units(p);              // (after the arrival: no other workgroup waits for it)
+            if (threadIdx.x == 0) {
+                const unsigned long long t0 = wall_clock64();
+                unsigned ok = 0;
+                while (true) {
+                    if (__hip_atomic_load(&p.totals[8], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= nshadow) {
+                        ok = 1;
+                        break;
+                    }
+                    if (__hip_atomic_load(&p.totals[10], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= nchain ||
+                        wall_clock64() - t0 > (p.early_fin > 1 ? 0ull : kEarlyFinWait))
+                        break;
+                    __builtin_amdgcn_s_sleep(8);
+                }
+                g_efin = ok;
+            }
+            __syncthreads();
+            if (!g_efin) return;
+            __threadfence();                        // (acquire) the other workgroups' occlusion bytes
+            finish_taken<false, false>(s, e, p, &p.totals[9], nchain);
+            return;
+        }
+    }
     // a lone frame's next unit order, by the last shadow-role workgroup once its shadow rays are done:
     // beside phase B's deep chains, off the frame's critical path (in k_pack_a it cost 30 us there)
-    if (!COUNT && !chain && p.urank && blockIdx.x == gridDim.x - 1) rank_units(p);
+    if (ranker) rank_units(p);
 }
 
 // Phase B's shadow tasks (which = 1), or phase A's (which = 0: p.split_occ, frame batches).
@@ -2068,40 +2120,93 @@ __device__ __forceinline__ void finish_pixel(const rtk::DevScene& s, const rtk::
     o[0] = (uint8_t)(sr / ff); o[1] = (uint8_t)(sg / ff); o[2] = (uint8_t)(sb / ff);
 }
 
+// Output pixel (rr, ocol) of the chunk: does any of its samples continue in phase B (pinfo's kPathCont)?
+__device__ __forceinline__ bool pixel_cont(const PcParams& p, int rr, int ocol) {
+    bool cont = false;
+    for (int k = 0; k < p.aa; ++k)
+        for (int l = 0; l < p.aa; ++l)
+            cont |= (p.pinfo[slab_slot(p.tiles_x, ocol * p.aa + l, rr * p.aa + k)] & kPathCont) != 0;
+    return cont;
+}
+
+// Pixels without a continued sample, taken by whole waves 64 at a time from counter *ctr (totals[9]: k_mix's
+// early finish, then k_finish the rest), while fewer than stop_at waves have counted themselves done in
+// totals[10] (k_mix: its phase-B waves; k_finish: ~0u, to the end)
+template <bool LDS, bool CMP>
+__device__ void finish_taken(const rtk::DevScene& s, const rtk::Eye& e, const PcParams& p, unsigned* ctr,
+                             unsigned stop_at) {
+    const unsigned npix = (unsigned)((p.chunk_rows / p.aa) * p.width);
+    while (true) {
+        unsigned q0 = 0;
+        if (lane_id() == 0) q0 = atomicAdd(ctr, 64u);
+        q0 = (unsigned)uni((int)__shfl((int)q0, 0));
+        if (q0 >= npix) break;
+        const unsigned q = q0 + (unsigned)lane_id();
+        if (q < npix) {
+            const int rr = (int)(q / (unsigned)p.width), ocol = (int)(q - (unsigned)rr * (unsigned)p.width);
+            if (!pixel_cont(p, rr, ocol)) finish_pixel<LDS, CMP>(s, e, p, rr, ocol);
+        }
+        if (stop_at != ~0u && __hip_atomic_load(&p.totals[10], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= stop_at)
+            break;
+    }
+}
+
 // p.fin_cont (chain path): the pixels of the paths continued in phase B first (cflat, totals[1] of
 // them; each pixel once, by the lane holding its first continued sample), so their long folds
-// overlap the rest; then every pixel without a continued sample (pinfo's kPathCont bit)
-template <bool LDS, bool CMP>
+// overlap the rest; then every pixel without a continued sample (pinfo's kPathCont bit).
+// EF (p.early_fin): k_mix took most of the latter already (finish_taken), so k_finish takes the rest
+// from the same counter, and every pixel k_fallback changed again (the phase-A entries of fbc and fbs:
+// k_mix may have finished them before), beside the continued ones; after a fallback shadow-queue overflow
+// (occlusion bytes left kOccDeferred, totals[6]) every pixel again, from a fresh counter (totals[11]).
+template <bool LDS, bool CMP, bool EF>
 __device__ __forceinline__ void finish_pixels(const rtk::DevScene& s, const rtk::Eye& e, const PcParams& p) {
+    static_assert(!(EF && CMP), "early finish: no compact records");
     const int F = p.aa;
     const unsigned gtid = blockIdx.x * kBlock + threadIdx.x, gstride = gridDim.x * kBlock;
     if (p.fin_cont) {
         const unsigned n = p.totals[1];
-        for (unsigned j = gtid; j < n; j += gstride) {
-            const unsigned path = (p.cflat[j] & ~kFbEye) % (unsigned)p.cap;
+        const unsigned aspace = (unsigned)p.la * (unsigned)p.cap, nl = (unsigned)s.nlights;
+        const unsigned nfc = EF ? min(p.totals[4], p.fbc_cap) : 0u, nfs = EF ? min(p.totals[5], p.fbs_cap) : 0u;
+        for (unsigned j = gtid; j < n + nfc + nfs; j += gstride) {
+            unsigned path;
+            if (!EF || j < n) {
+                path = (p.cflat[j] & ~kFbEye) % (unsigned)p.cap;
+            } else if (j < n + nfc) {
+                const unsigned en = p.fbc[j - n];
+                if (!(en & kFbEye) && en >= aspace) continue;        // a phase-B level: a continued path
+                path = (en & kFbEye) ? en & ~kFbEye : en % (unsigned)p.cap;
+            } else {
+                const unsigned lvp = p.fbs[j - n - nfc] / nl;
+                if (lvp >= aspace) continue;
+                path = lvp % (unsigned)p.cap;
+            }
             const unsigned tile = path >> 6, lane = path & 63u;
             const int ix = (int)(tile % (unsigned)p.tiles_x) * 8 + (int)(lane & 7u);
             const int iyc = (int)(tile / (unsigned)p.tiles_x) * 8 + (int)(lane >> 3);
             const int ocol = ix / F, rr = iyc / F;
-            unsigned first = path;
-            for (int k = F - 1; k >= 0; --k)
-                for (int l = F - 1; l >= 0; --l) {
-                    const unsigned sl = slab_slot(p.tiles_x, ocol * F + l, rr * F + k);
-                    if (p.pinfo[sl] & kPathCont) first = sl;
-                }
-            if (first == path) finish_pixel<LDS, CMP>(s, e, p, rr, ocol);
+            bool go;
+            if (!EF || j < n) {
+                unsigned first = path;
+                for (int k = F - 1; k >= 0; --k)
+                    for (int l = F - 1; l >= 0; --l) {
+                        const unsigned sl = slab_slot(p.tiles_x, ocol * F + l, rr * F + k);
+                        if (p.pinfo[sl] & kPathCont) first = sl;
+                    }
+                go = first == path;
+            } else {
+                go = !pixel_cont(p, rr, ocol);   // (repeated entries write the same bytes)
+            }
+            if (go) finish_pixel<LDS, CMP>(s, e, p, rr, ocol);
         }
+    }
+    if constexpr (EF) {
+        finish_taken<LDS, CMP>(s, e, p, p.totals[6] ? &p.totals[11] : &p.totals[9], ~0u);
+        return;
     }
     const int npix = (p.chunk_rows / p.aa) * p.width;
     for (int q = (int)gtid; q < npix; q += (int)gstride) {
         const int rr = q / p.width, ocol = q - rr * p.width;
-        if (p.fin_cont) {
-            bool cont = false;
-            for (int k = 0; k < F; ++k)
-                for (int l = 0; l < F; ++l)
-                    cont |= (p.pinfo[slab_slot(p.tiles_x, ocol * F + l, rr * F + k)] & kPathCont) != 0;
-            if (cont) continue;
-        }
+        if (p.fin_cont && pixel_cont(p, rr, ocol)) continue;
         finish_pixel<LDS, CMP>(s, e, p, rr, ocol);
     }
 }
@@ -2109,7 +2214,7 @@ __device__ __forceinline__ void finish_pixels(const rtk::DevScene& s, const rtk:
 // k_finish: k_shade + k_compose in one pass, one lane per output pixel, with
 // the scene's materials and lights in LDS (host checks they fit);
 // k_finish_any: the same for larger scenes, tables read from global memory.
-template <bool CMP>
+template <bool CMP, bool EF = false>
 __global__ __launch_bounds__(kBlock, CMP ? RT_FINISH_CMP_WAVES : RT_FINISH_WAVES) void k_finish(rtk::DevScene s,
                                                                                                  rtk::Eye e, PcParams p) {
     float4* dm = reinterpret_cast<float4*>(g_fmats);
@@ -2119,11 +2224,11 @@ __global__ __launch_bounds__(kBlock, CMP ? RT_FINISH_CMP_WAVES : RT_FINISH_WAVES
     const float4* sl = reinterpret_cast<const float4*>(s.lights);
     for (int i = threadIdx.x; i < s.nlights * 2; i += kBlock) dl_[i] = sl[i];
     __syncthreads();
-    finish_pixels<true, CMP>(s, e, p);
+    finish_pixels<true, CMP, EF>(s, e, p);
 }
-template <bool CMP>
+template <bool CMP, bool EF = false>
 __global__ __launch_bounds__(kBlock, RT_FINISH_ANY_WAVES) void k_finish_any(rtk::DevScene s, rtk::Eye e, PcParams p) {
-    finish_pixels<false, CMP>(s, e, p);
+    finish_pixels<false, CMP, EF>(s, e, p);
 }
 
 // ---------------------------------------------------------------------------
@@ -2360,13 +2465,17 @@ __global__ __launch_bounds__(kBlock) void k_walk_timing(rtk::DevScene s, const f
 void launch_finish(const rtk::DevScene& s, const rtk::Eye& e, const PcParams& p, hipStream_t st) {
     const int npix = (p.chunk_rows / p.aa) * p.width;
     const dim3 pgrid(std::max(1, std::min((npix + kBlock - 1) / kBlock, p.fin_grid > 0 ? p.fin_grid : INT32_MAX)));
+    // (p.early_fin: the rest of k_mix's early finish; lone frames, never with compact records; tables from
+    // global memory: with them in LDS this variant spills 3 VGPRs)
     if (s.nmats <= kFinishMats && s.nlights <= kFinishLights)
     {
-        if (p.clevels) hipLaunchKernelGGL(k_finish<true>, pgrid, dim3(kBlock), 0, st, s, e, p);
-        else hipLaunchKernelGGL(k_finish<false>, pgrid, dim3(kBlock), 0, st, s, e, p);
+        if (p.clevels) hipLaunchKernelGGL((k_finish<true>), pgrid, dim3(kBlock), 0, st, s, e, p);
+        else if (p.early_fin) hipLaunchKernelGGL((k_finish_any<false, true>), pgrid, dim3(kBlock), 0, st, s, e, p);
+        else hipLaunchKernelGGL((k_finish<false>), pgrid, dim3(kBlock), 0, st, s, e, p);
     } else {
-        if (p.clevels) hipLaunchKernelGGL(k_finish_any<true>, pgrid, dim3(kBlock), 0, st, s, e, p);
-        else hipLaunchKernelGGL(k_finish_any<false>, pgrid, dim3(kBlock), 0, st, s, e, p);
+        if (p.clevels) hipLaunchKernelGGL((k_finish_any<true>), pgrid, dim3(kBlock), 0, st, s, e, p);
+        else if (p.early_fin) hipLaunchKernelGGL((k_finish_any<false, true>), pgrid, dim3(kBlock), 0, st, s, e, p);
+        else hipLaunchKernelGGL((k_finish_any<false>), pgrid, dim3(kBlock), 0, st, s, e, p);
     }
 }
 
@@ -2467,7 +2576,7 @@ hipError_t launch_chain_chunk(const rtk::DevScene& s, const rtk::Eye& e, const P
     auto mark = [&](int k) { if (kt) kt->mark(k, st); };
     const bool phase_b = p.kinline < s.max_depth;     // any continuation possible
     {   // the dynamic unit counter and k_fallback's counts
-        const hipError_t me = hipMemsetAsync(p.totals + 3, 0, 5 * sizeof(unsigned), st);
+        const hipError_t me = hipMemsetAsync(p.totals + 3, 0, 9 * sizeof(unsigned), st);
         if (me != hipSuccess) return me;
     }
     mark(kKChain);
@@ -2508,7 +2617,8 @@ hipError_t launch_chain_chunk(const rtk::DevScene& s, const rtk::Eye& e, const P
     mark(kKFallback);
     hipLaunchKernelGGL(k_fallback, dim3(p.fb_grid), blk, 0, st, s, e, p);
     PcParams f = p;
-    f.fin_cont = phase_b && p.aa == 1;
+    f.fin_cont = phase_b && (p.aa == 1 || p.early_fin);
+    f.early_fin = phase_b && !split && !count ? p.early_fin : 0;
     mark(kKFinish);
     launch_finish(s, e, f, st);
     mark(kKEnd);

@@ -145,8 +145,9 @@ struct PcParams {
     unsigned scapB;
     unsigned* scntB;  // [gb]
     unsigned* sflatB; // B's shadow tasks packed (k_pack_b), totals[2] of them
-    unsigned* totals; // [8]: packed task counts (3), phase-A unit counter, k_fallback chains / shadows / overflow,
-                      // finished k_chain waves
+    unsigned* totals; // [12]: packed task counts (3), phase-A unit counter, k_fallback chains / shadows / overflow,
+                      // finished k_chain waves; early finish (early_fin): k_mix shadow-role workgroups done,
+                      // next pixel, finished phase-B waves
     int kinline;      // deepest level phase A walks (>= max_depth: no phase B)
     int gb;           // k_mix workgroups in the chain role (the other p.ogrid ones occlude A's tasks)
     int tchunk;       // continuation tasks (phase B) are dealt to workgroups in chunks of this many
@@ -174,6 +175,10 @@ struct PcParams {
                       // regions (workgroup w: regions w, w + G, ...); k_pack_a packs only the continuations
     int fin_grid;     // k_finish workgroups at most (0: a lane per output pixel), a grid-stride loop beyond
     int fin_cont;     // k_finish: the continued paths' pixels first (chain path: cflat, totals[1], kPathCont)
+    int early_fin;    // 1 (lone frames, k_mix with the LDS queue, no compact records): k_mix's shadow-role
+                      // workgroups finish the pixels without a continued sample once A's occlusion is done
+                      // (pathchain.hip early finish); k_finish the rest and what k_fallback changed
+                      // (2: tests, no wait for the other workgroups)
     int refill;       // a wave refills once <= refill of its lanes are still walking
     int orefill;      // the same for the shadow (any-hit) walks
     int brefill;      // the same for phase-B chains

@@ -142,6 +142,8 @@ struct rt_scene {
                                 // 900-990 measured 2-4 % slower for C3 one frame: the restarted walks are the
                                 // heaviest, deepest chains, which then start phase B from scratch)
     int tune_hot_units = 1;     // RT_HOT_UNITS: lone frames deal phase-A units heaviest-first by the previous frame's steps
+    int tune_early_fin = 1;     // RT_EARLY_FIN: lone frames' k_mix finishes the pixels without a continued sample
+                                // (2: tests, its workgroups do not wait for each other: k_finish takes the rest)
     int tune_occ_inplace = 1;   // RT_OCC_INPLACE: frame batches' k_occlude reads A's shadow tasks in their regions (0: packed)
     int tune_compact = 1;       // RT_COMPACT: phase-A records without directions (16 B instead of 32): 1 frame batches,
                                 // 2 every launch, 0 none
@@ -472,6 +474,7 @@ int upload_rest(rt_scene* s, const rt_options* opts) {
     if (const char* e = std::getenv("RT_COOP")) s->tune_coop = std::atoi(e) != 0;
     if (const char* e = std::getenv("RT_COMPACT")) s->tune_compact = std::max(0, std::min(2, std::atoi(e)));
     if (const char* e = std::getenv("RT_OCC_INPLACE")) s->tune_occ_inplace = std::atoi(e) != 0;
+    if (const char* e = std::getenv("RT_EARLY_FIN")) s->tune_early_fin = std::max(0, std::min(2, std::atoi(e)));
     if (const char* e = std::getenv("RT_HOT_UNITS")) s->tune_hot_units = std::atoi(e) != 0;
     if (const char* e = std::getenv("RT_ABANDON")) s->tune_abandon = std::max(0, std::min(1000, std::atoi(e)));
     if (const char* e = std::getenv("RT_COOP_LIVE")) s->tune_coop_live = std::max(1, std::min(8, std::atoi(e)));
@@ -835,7 +838,7 @@ ChainPlan chain_plan(const rt_scene* s, const ChainGeom& g, size_t nunits, bool 
         P.o_sqB = L.take<unsigned>((size_t)P.gb * P.scapB); P.o_scntB = L.take<unsigned>(P.gb + 1);
         P.o_sflatB = L.take<unsigned>(P.cb * (levels - P.la) * nl);
     }
-    P.o_totals = L.take<unsigned>(8);
+    P.o_totals = L.take<unsigned>(12);
     P.bytes = L.off;
     return P;
 }
@@ -983,6 +986,11 @@ int render_chain(rt_scene* s, const rtk::Eye& eye, const rtk::FrameParams& f, bo
     p.split_occ = P.split_occ ? 1 : 0;
     p.occ_inplace = P.split_occ && !count && s->tune_occ_inplace ? 1 : 0;
     p.occ_inplace_b = !P.split_occ && !count && !fused && s->tune_occ_inplace ? 1 : 0;
+    // lone frames in one launch: k_mix's shadow-role workgroups finish the pixels without a continued
+    // sample beside phase B (pathchain.hip k_mix); not with compact records (the rebuilt directions are
+    // k_finish<true>'s) nor beside other chunks' kernels (its workgroups wait for each other, bounded)
+    p.early_fin = !P.split_occ && !count && !fused && P.phase_b && P.clevels == 0 && units == g.units_total &&
+                  s->tune_early_fin ? s->tune_early_fin : 0;
     p.refill = s->tune_refill >= 0 ? s->tune_refill : 0;
     p.service = s->tune_service >= 0 ? s->tune_service : 64;
     p.bservice = s->tune_bservice;
