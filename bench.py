@@ -73,10 +73,15 @@ def kernel_bytes(r: dict, c: dict, out_pixels: int, batched: bool, nlights: int)
     packing reads and writes each task id (in frame batches only the continuations'); k_finish reads every sample's path word (4 B) and every
     hit's record, normal and occlusion dword(s) (4 B when the record's bytes sit in one dword: 1, 2 or
     4 lights; else 8), and writes 3 B per pixel.
-    One frame alone, A's shadow rays run in k_mix's shadow role; in frame batches in k_occlude."""
+    One frame alone, A's shadow rays run in k_mix's shadow role; in frame batches in k_occlude.  One
+    frame alone keeps 32-B phase-A records (rt_api.cpp chain_plan: compact records in frame batches
+    only, RT_COMPACT=2 everywhere), and k_mix's shadow-role workgroups finish the pixels without a
+    continued sample (PcParams::early_fin, RT_EARLY_FIN): their share of k_finish's bytes is charged to
+    k_mix (the share of samples not continued; k_finish keeps the continued pixels')."""
     NRM, TASK, OCC = 16, 4, 1
     REC_B = 32
-    REC_A = 32 if os.environ.get("RT_COMPACT", "1") == "0" else 16
+    compact = os.environ.get("RT_COMPACT", "1")
+    REC_A = 16 if compact == "2" or (compact == "1" and batched) else 32
     DIRW = 16 if REC_A == 16 else 0
     inplace = batched and os.environ.get("RT_OCC_INPLACE", "1") != "0"
     samples, skipped = c["primary_rays"], c["shadow_rays_skipped"]
@@ -98,6 +103,10 @@ def kernel_bytes(r: dict, c: dict, out_pixels: int, batched: bool, nlights: int)
     }
     if not batched:                       # one frame: A's shadow rays are k_mix's shadow role
         k["k_mix"] += k.pop("k_occlude_a")
+        if os.environ.get("RT_EARLY_FIN", "1") != "0" and REC_A == 32 and samples:
+            moved = int(k["k_finish"] * max(0.0, 1.0 - conts / samples))
+            k["k_mix"] += moved
+            k["k_finish"] -= moved
     return k
 
 
