@@ -1603,11 +1603,10 @@ __global__ __launch_bounds__(kBlock) void k_pack_b(PcParams p) {
 #define RT_MIX_NOBQ_WAVES 5      // without the LDS queue: 96 VGPRs, no spills
 #endif
 // Early finish (PcParams::early_fin, lone frames): pixels without a continued sample, taken 64 at a time
-// from totals[9] (defined with k_finish; k_finish takes what is left)
+// from the stripes' counters (defined with k_finish; k_finish takes what is left)
 __shared__ unsigned g_efin;
 template <bool LDS, bool CMP>
-__device__ void finish_taken(const rtk::DevScene& s, const rtk::Eye& e, const PcParams& p, unsigned* ctr,
-                             unsigned stop_at);
+__device__ void finish_taken(const rtk::DevScene& s, const rtk::Eye& e, const PcParams& p, unsigned stop_at);
 
 template <bool COUNT, bool BQ>
 __global__ __launch_bounds__(kBlock, BQ || COUNT ? RT_MIX_WAVES : RT_MIX_NOBQ_WAVES) void k_mix(rtk::DevScene s,
@@ -1654,14 +1653,14 @@ __global__ __launch_bounds__(kBlock, BQ || COUNT ? RT_MIX_WAVES : RT_MIX_NOBQ_WA
                     if (__hip_atomic_load(&p.totals[10], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= nchain ||
                         wall_clock64() - t0 > (p.early_fin > 1 ? 0ull : kEarlyFinWait))
                         break;
-                    __builtin_amdgcn_s_sleep(8);
+                    __builtin_amdgcn_s_sleep(127);   // (~3 us: few polls of the two words)
                 }
                 g_efin = ok;
             }
             __syncthreads();
             if (!g_efin) return;
             __threadfence();                        // (acquire) the other workgroups' occlusion bytes
-            finish_taken<false, false>(s, e, p, &p.totals[9], nchain);
+            finish_taken<false, false>(s, e, p, nchain);
             return;
         }
     }
@@ -2129,24 +2128,28 @@ __device__ __forceinline__ bool pixel_cont(const PcParams& p, int rr, int ocol) 
     return cont;
 }
 
-// Pixels without a continued sample, taken by whole waves 64 at a time from counter *ctr (totals[9]: k_mix's
-// early finish, then k_finish the rest), while fewer than stop_at waves have counted themselves done in
-// totals[10] (k_mix: its phase-B waves; k_finish: ~0u, to the end)
+// k_mix's early finish: pixels without a continued sample, taken by whole waves 64 at a time from the
+// counter of stripe wave-id mod kFinStripes (~136 waves per stripe in a C3 frame) while fewer than
+// stop_at phase-B waves have counted themselves done (totals[10], read every 4th grab).  A grab below
+// the stripe's end is always finished, so the stripe's pixels [0, min(counter, length)) are done and
+// k_finish takes the rest (finish_pixels).
 template <bool LDS, bool CMP>
-__device__ void finish_taken(const rtk::DevScene& s, const rtk::Eye& e, const PcParams& p, unsigned* ctr,
-                             unsigned stop_at) {
-    const unsigned npix = (unsigned)((p.chunk_rows / p.aa) * p.width);
-    while (true) {
+__device__ void finish_taken(const rtk::DevScene& s, const rtk::Eye& e, const PcParams& p, unsigned stop_at) {
+    const unsigned npix = (unsigned)((p.chunk_rows / p.aa) * p.width), len = fin_stripe_len(npix);
+    const unsigned j = (unsigned)uni((int)(((blockIdx.x * kBlock + threadIdx.x) >> 6) % (unsigned)kFinStripes));
+    const unsigned lo = j * len, hi = min(npix, lo + len);
+    unsigned* const ctr = &p.totals[kFinCtr0 + j * kFinCtrStride];
+    for (unsigned it = 1; lo < hi; ++it) {
         unsigned q0 = 0;
         if (lane_id() == 0) q0 = atomicAdd(ctr, 64u);
-        q0 = (unsigned)uni((int)__shfl((int)q0, 0));
-        if (q0 >= npix) break;
+        q0 = lo + (unsigned)uni((int)__shfl((int)q0, 0));
+        if (q0 >= hi) break;
         const unsigned q = q0 + (unsigned)lane_id();
-        if (q < npix) {
+        if (q < hi) {
             const int rr = (int)(q / (unsigned)p.width), ocol = (int)(q - (unsigned)rr * (unsigned)p.width);
             if (!pixel_cont(p, rr, ocol)) finish_pixel<LDS, CMP>(s, e, p, rr, ocol);
         }
-        if (stop_at != ~0u && __hip_atomic_load(&p.totals[10], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= stop_at)
+        if ((it & 3u) == 0 && __hip_atomic_load(&p.totals[10], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= stop_at)
             break;
     }
 }
@@ -2154,10 +2157,10 @@ __device__ void finish_taken(const rtk::DevScene& s, const rtk::Eye& e, const Pc
 // p.fin_cont (chain path): the pixels of the paths continued in phase B first (cflat, totals[1] of
 // them; each pixel once, by the lane holding its first continued sample), so their long folds
 // overlap the rest; then every pixel without a continued sample (pinfo's kPathCont bit).
-// EF (p.early_fin): k_mix took most of the latter already (finish_taken), so k_finish takes the rest
-// from the same counter, and every pixel k_fallback changed again (the phase-A entries of fbc and fbs:
-// k_mix may have finished them before), beside the continued ones; after a fallback shadow-queue overflow
-// (occlusion bytes left kOccDeferred, totals[6]) every pixel again, from a fresh counter (totals[11]).
+// EF (p.early_fin): k_mix took most of the latter already (finish_taken), so k_finish takes the rest of
+// each stripe, and every pixel k_fallback changed again (the phase-A entries of fbc and fbs: k_mix may
+// have finished them before), beside the continued ones; after a fallback shadow-queue overflow
+// (occlusion bytes left kOccDeferred, totals[6]) every pixel again.
 template <bool LDS, bool CMP, bool EF>
 __device__ __forceinline__ void finish_pixels(const rtk::DevScene& s, const rtk::Eye& e, const PcParams& p) {
     static_assert(!(EF && CMP), "early finish: no compact records");
@@ -2200,7 +2203,16 @@ __device__ __forceinline__ void finish_pixels(const rtk::DevScene& s, const rtk:
         }
     }
     if constexpr (EF) {
-        finish_taken<LDS, CMP>(s, e, p, p.totals[6] ? &p.totals[11] : &p.totals[9], ~0u);
+        const unsigned npix = (unsigned)((p.chunk_rows / p.aa) * p.width), len = fin_stripe_len(npix);
+        const bool all = p.totals[6] != 0;
+        for (unsigned j = 0; j < (unsigned)kFinStripes; ++j) {
+            const unsigned hi = min(npix, (j + 1) * len);
+            const unsigned lo = all ? j * len : min(hi, j * len + p.totals[kFinCtr0 + j * kFinCtrStride]);
+            for (unsigned q = lo + gtid; q < hi; q += gstride) {
+                const int rr = (int)(q / (unsigned)p.width), ocol = (int)(q - (unsigned)rr * (unsigned)p.width);
+                if (!pixel_cont(p, rr, ocol)) finish_pixel<LDS, CMP>(s, e, p, rr, ocol);
+            }
+        }
         return;
     }
     const int npix = (p.chunk_rows / p.aa) * p.width;
@@ -2576,7 +2588,7 @@ hipError_t launch_chain_chunk(const rtk::DevScene& s, const rtk::Eye& e, const P
     auto mark = [&](int k) { if (kt) kt->mark(k, st); };
     const bool phase_b = p.kinline < s.max_depth;     // any continuation possible
     {   // the dynamic unit counter and k_fallback's counts
-        const hipError_t me = hipMemsetAsync(p.totals + 3, 0, 9 * sizeof(unsigned), st);
+        const hipError_t me = hipMemsetAsync(p.totals + 3, 0, (kTotalsWords - 3) * sizeof(unsigned), st);
         if (me != hipSuccess) return me;
     }
     mark(kKChain);

@@ -97,6 +97,15 @@ __host__ __device__ inline unsigned unit_col(int tiles_x, int ublk_h, int ublk_w
     return (r0 + l / w) * upr + c0 + l % w;
 }
 
+// Early finish (PcParams::early_fin): the pixels in kFinStripes equal stripes, each with a launch-wide
+// counter of pixels taken, 256 B apart (atomics on one word serialise: 64-pixel grabs on a single
+// counter cost a lone frame 0.4 ms), from totals word kFinCtr0 on.
+constexpr int kFinStripes = 16, kFinCtrStride = 64, kFinCtr0 = 64;
+constexpr int kTotalsWords = kFinCtr0 + kFinStripes * kFinCtrStride;
+__host__ __device__ inline unsigned fin_stripe_len(unsigned npix) {
+    return ((npix + kFinStripes - 1) / kFinStripes + 63u) & ~63u;
+}
+
 // Unit cost classes (PcParams::ucost): the most phase-A walk steps a sample of the unit took.
 constexpr unsigned kHotSteps[2] = {96, 32};
 
@@ -145,9 +154,9 @@ struct PcParams {
     unsigned scapB;
     unsigned* scntB;  // [gb]
     unsigned* sflatB; // B's shadow tasks packed (k_pack_b), totals[2] of them
-    unsigned* totals; // [12]: packed task counts (3), phase-A unit counter, k_fallback chains / shadows / overflow,
-                      // finished k_chain waves; early finish (early_fin): k_mix shadow-role workgroups done,
-                      // next pixel, finished phase-B waves
+    unsigned* totals; // [kTotalsWords]: packed task counts (3), phase-A unit counter, k_fallback chains / shadows /
+                      // overflow, finished k_chain waves; early finish (early_fin): k_mix shadow-role workgroups
+                      // done (8), finished phase-B waves (10), the stripes' pixel counters (kFinCtr0 on)
     int kinline;      // deepest level phase A walks (>= max_depth: no phase B)
     int gb;           // k_mix workgroups in the chain role (the other p.ogrid ones occlude A's tasks)
     int tchunk;       // continuation tasks (phase B) are dealt to workgroups in chunks of this many

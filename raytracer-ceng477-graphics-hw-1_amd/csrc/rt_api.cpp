@@ -838,7 +838,7 @@ ChainPlan chain_plan(const rt_scene* s, const ChainGeom& g, size_t nunits, bool 
         P.o_sqB = L.take<unsigned>((size_t)P.gb * P.scapB); P.o_scntB = L.take<unsigned>(P.gb + 1);
         P.o_sflatB = L.take<unsigned>(P.cb * (levels - P.la) * nl);
     }
-    P.o_totals = L.take<unsigned>(12);
+    P.o_totals = L.take<unsigned>(rtc::kTotalsWords);
     P.bytes = L.off;
     return P;
 }
