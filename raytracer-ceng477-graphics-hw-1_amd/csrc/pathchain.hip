@@ -1587,6 +1587,7 @@ __device__ void rank_units(const PcParams& p) {
 __global__ __launch_bounds__(kBlock) void k_pack_a(PcParams p) {
     if (!p.occ_inplace) pack_region(p.sqA, p.scapA, p.scntA, p.grid, p.sflatA, &p.totals[0], blockIdx.x);
     pack_region(p.cq, p.ccapA, p.ccnt, p.grid, p.cflat, &p.totals[1], blockIdx.x, p.cid, (unsigned)p.cap);
+    if (p.cont_peak && blockIdx.x == 0 && threadIdx.x == 0) atomicMax(p.cont_peak, p.totals[1]);   // (its own write)
 }
 __global__ __launch_bounds__(kBlock) void k_pack_b(PcParams p) {
     pack_region(p.sqB, p.scapB, p.scntB, p.gb, p.sflatB, &p.totals[2], blockIdx.x);

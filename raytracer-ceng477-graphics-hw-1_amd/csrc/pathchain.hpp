@@ -183,6 +183,7 @@ struct PcParams {
     int occ_inplace;  // 1 (split_occ production launches): k_occlude walks A's shadow tasks in their phase-A
                       // regions (workgroup w: regions w, w + G, ...); k_pack_a packs only the continuations
     int fin_grid;     // k_finish workgroups at most (0: a lane per output pixel), a grid-stride loop beyond
+    unsigned* cont_peak;  // frames of several chunks: the most continuations of one chunk (k_pack_a, atomicMax)
     int fin_cont;     // k_finish: the continued paths' pixels first (chain path: cflat, totals[1], kPathCont)
     int early_fin;    // 1 (lone frames, k_mix with the LDS queue, no compact records): k_mix's shadow-role
                       // workgroups finish the pixels without a continued sample once A's occlusion is done

@@ -196,6 +196,7 @@ struct rt_scene {
     // is folded into cont_frac, which sizes the next launches' cb (and so their frames per launch)
     double cont_frac = 0;                      // 0: none seen yet (cap / tune_cont_den)
     unsigned* h_cont = nullptr;                // pinned, per slot
+    unsigned* d_cont_peak = nullptr;           // a frame of several chunks: its chunks' most continuations
     hipEvent_t cont_ev[kSlots] = {};
     size_t cont_cap[kSlots] = {};
     bool cont_pending[kSlots] = {};
@@ -241,6 +242,7 @@ struct rt_scene {
         for (auto& e : cont_ev)
             if (e) (void)hipEventDestroy(e);
         if (h_cont) (void)hipHostFree(h_cont);
+        (void)hipFree(d_cont_peak);
         (void)hipFree(batch_out);
         (void)hipFree(d_block);           // the scene arrays, counters and error word (upload_flat / _rest)
         (void)hipFree(d_block2);
@@ -921,6 +923,14 @@ int render_chain(rt_scene* s, const rtk::Eye& eye, const rtk::FrameParams& f, bo
     // disjoint output rows.
     const int nchunks = (li + chunk_rows - 1) / chunk_rows;
     const int K = std::min({nchunks, s->tune_slots, rt_scene::kSlots});
+    // a frame of several chunks reports its chunks' largest continuation share (the record space must
+    // hold the mirror-heavy chunks', not the last chunk's): k_pack_a's atomicMax into one word, cleared
+    // here, on the caller's stream before the chunks fork
+    const bool peak = nchunks > 1 && !count && !fused && P.phase_b && s->tune_cont_cb == 0;
+    if (peak && f.chunk_k == 1) {
+        if (!s->d_cont_peak) HIP_TRY(hipMalloc(reinterpret_cast<void**>(&s->d_cont_peak), sizeof(unsigned)));
+        HIP_TRY(hipMemsetAsync(s->d_cont_peak, 0, sizeof(unsigned), st));
+    }
     if (f.chunk_k == 1 && K > 1 && !s->trace_file.size()) {
         if (!s->fork_ev) HIP_TRY(hipEventCreateWithFlags(&s->fork_ev, hipEventDisableTiming));
         HIP_TRY(hipEventRecord(s->fork_ev, st));
@@ -986,6 +996,7 @@ int render_chain(rt_scene* s, const rtk::Eye& eye, const rtk::FrameParams& f, bo
     p.split_occ = P.split_occ ? 1 : 0;
     p.occ_inplace = P.split_occ && !count && s->tune_occ_inplace ? 1 : 0;
     p.occ_inplace_b = !P.split_occ && !count && !fused && s->tune_occ_inplace ? 1 : 0;
+    p.cont_peak = peak ? s->d_cont_peak : nullptr;
     // lone frames in one launch: k_mix's shadow-role workgroups finish the pixels without a continued
     // sample beside phase B (pathchain.hip k_mix); not with compact records (the rebuilt directions are
     // k_finish<true>'s) nor beside other chunks' kernels (its workgroups wait for each other, bounded)
@@ -1099,7 +1110,8 @@ int render_chain(rt_scene* s, const rtk::Eye& eye, const rtk::FrameParams& f, bo
     if (!count && !fused && P.phase_b && (p.nframes > 1 || chunk_rows < li) && s->tune_cont_cb == 0) {   // the share, read back later
         if (!s->h_cont) HIP_TRY(hipHostMalloc(reinterpret_cast<void**>(&s->h_cont), rt_scene::kSlots * sizeof(unsigned)));
         if (!s->cont_ev[slot]) HIP_TRY(hipEventCreateWithFlags(&s->cont_ev[slot], hipEventDisableTiming));
-        HIP_TRY(hipMemcpyAsync(&s->h_cont[slot], p.totals + 1, sizeof(unsigned), hipMemcpyDeviceToHost, st));
+        HIP_TRY(hipMemcpyAsync(&s->h_cont[slot], p.cont_peak ? p.cont_peak : p.totals + 1, sizeof(unsigned),
+                               hipMemcpyDeviceToHost, st));
         HIP_TRY(hipEventRecord(s->cont_ev[slot], st));
         s->cont_cap[slot] = cap;
         s->cont_pending[slot] = true;
