@@ -75,9 +75,9 @@ def kernel_bytes(r: dict, c: dict, out_pixels: int, batched: bool, nlights: int)
     4 lights; else 8), and writes 3 B per pixel.
     One frame alone, A's shadow rays run in k_mix's shadow role; in frame batches in k_occlude.  One
     frame alone keeps 32-B phase-A records (rt_api.cpp chain_plan: compact records in frame batches
-    only, RT_COMPACT=2 everywhere), and k_mix's shadow-role workgroups finish the pixels without a
-    continued sample (PcParams::early_fin, RT_EARLY_FIN): their share of k_finish's bytes is charged to
-    k_mix (the share of samples not continued; k_finish keeps the continued pixels')."""
+    only, RT_COMPACT=2 everywhere); with RT_EARLY_FIN=1 (off by default) k_mix's shadow-role workgroups
+    finish the pixels without a continued sample, and their share of k_finish's bytes is charged to k_mix
+    (the share of samples not continued; k_finish keeps the continued pixels')."""
     NRM, TASK, OCC = 16, 4, 1
     REC_B = 32
     compact = os.environ.get("RT_COMPACT", "1")
@@ -103,7 +103,7 @@ def kernel_bytes(r: dict, c: dict, out_pixels: int, batched: bool, nlights: int)
     }
     if not batched:                       # one frame: A's shadow rays are k_mix's shadow role
         k["k_mix"] += k.pop("k_occlude_a")
-        if os.environ.get("RT_EARLY_FIN", "1") != "0" and REC_A == 32 and samples:
+        if os.environ.get("RT_EARLY_FIN", "0") in ("1", "2") and REC_A == 32 and samples:
             moved = int(k["k_finish"] * max(0.0, 1.0 - conts / samples))
             k["k_mix"] += moved
             k["k_finish"] -= moved

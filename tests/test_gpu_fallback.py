@@ -17,8 +17,8 @@ branch of it and compare with the reference goldens (raytracer.cpp:385-452):
   * RT_ABANDON=1: phase A's unfinished walks restart in phase B (eye rays as
     kFbEye continuations, level-1 walks as reflections of their level-0 record),
     alone and with RT_CONT_CB=1000 (the restarts beyond it in k_fallback);
-  * RT_EARLY_FIN=0 / 2: a lone frame's pixels all in k_finish / k_mix's early
-    finish without its wait (every fallback mode above runs with the early finish on).
+  * RT_EARLY_FIN=1 / 2: a lone frame's early finish in k_mix, with its wait /
+    without it.
 """
 from __future__ import annotations
 
@@ -53,11 +53,13 @@ ENVS = [
     # and k_fallback read the stored direction words instead of the chain's tail copies
     {"RT_COMPACT": "0", "RT_CONT_CB": "1000"},
     {"RT_FORCE_FALLBACK": "2", "RT_FBS_CAP": "64"},
-    # a lone frame's early finish (k_mix's shadow-role workgroups finish the pixels without a continued
-    # sample, k_finish the rest and what k_fallback changed): off; and without the wait for the other
-    # workgroups (k_finish takes most pixels from the shared counter), alone and with every shadow ray
-    # deferred and the fallback shadow queue overflowing (every pixel finished again)
-    {"RT_EARLY_FIN": "0", "RT_CONT_CB": "1000"},
+    # a lone frame's early finish (RT_EARLY_FIN, off by default: k_mix's shadow-role workgroups finish the
+    # pixels without a continued sample, k_finish the rest and what k_fallback changed): with deferred
+    # paths and shadow rays, with continuations beyond the record space, and without the wait for the
+    # other workgroups (k_finish takes most pixels), alone and with the fallback shadow queue overflowing
+    # (every pixel finished again)
+    {"RT_EARLY_FIN": "1", "RT_FORCE_FALLBACK": "3"},
+    {"RT_EARLY_FIN": "1", "RT_CONT_CB": "1000"},
     {"RT_EARLY_FIN": "2"},
     {"RT_EARLY_FIN": "2", "RT_FORCE_FALLBACK": "2", "RT_FBS_CAP": "64"},
 ]
