@@ -1619,18 +1619,18 @@ __global__ __launch_bounds__(kBlock, BQ || COUNT ? RT_MIX_WAVES : RT_MIX_NOBQ_WA
     if (chain) {
         if (p.bprio) __builtin_amdgcn_s_setprio(3);    // the deep chains are the frame's critical path
         chain_body<COUNT, true, BQ>(s, e, p, blockIdx.x, (unsigned)p.gb, phase_b(p));
-        if (!COUNT && BQ && p.early_fin && lane_id() == 0) atomicAdd(&p.totals[10], 1u);   // this chain wave is done
-        return;
+        if (!COUNT && BQ && RT_EARLY_FIN_BUILD && p.early_fin && lane_id() == 0)
+            atomicAdd(&p.totals[10], 1u);          // this chain wave is done (early finish)
     }
-    if (!p.exp_skip_occ) {
+    else if (!p.exp_skip_occ) {
         if constexpr (!COUNT && RT_LEAF_QUEUE)
             occlude_queue_body(s, p, blockIdx.x - p.gb, gridDim.x - p.gb, p.sflatA, p.totals[0]);
         else
             occlude_body<COUNT>(s, p, blockIdx.x - p.gb, gridDim.x - p.gb, p.sflatA, p.totals[0], 0);
     }
-    const bool ranker = !COUNT && p.urank && blockIdx.x == gridDim.x - 1;
-    if constexpr (!COUNT && BQ) {
-        if (p.early_fin) {
+    const bool ranker = !COUNT && !chain && p.urank && blockIdx.x == gridDim.x - 1;
+    if constexpr (!COUNT && BQ && RT_EARLY_FIN_BUILD) {
+        if (!chain && p.early_fin) {
             // A lone frame's pixels without a continued sample: their records and A's occlusion bytes are
             // final once every shadow-role workgroup has walked its tasks, so these workgroups shade and
             // fold them beside phase B's deep chains instead of k_finish after them.  The wait for the

@@ -97,6 +97,9 @@ __host__ __device__ inline unsigned unit_col(int tiles_x, int ublk_h, int ublk_w
     return (r0 + l / w) * upr + c0 + l % w;
 }
 
+#ifndef RT_EARLY_FIN_BUILD
+#define RT_EARLY_FIN_BUILD 0   // 1: k_mix with the early finish (RT_EARLY_FIN; measured slower; off)
+#endif
 // Early finish (PcParams::early_fin): the pixels in kFinStripes equal stripes, each with a launch-wide
 // counter of pixels taken, 256 B apart (atomics on one word serialise: 64-pixel grabs on a single
 // counter cost a lone frame 0.4 ms), from totals word kFinCtr0 on.
@@ -183,12 +186,7 @@ struct PcParams {
     int occ_inplace;  // 1 (split_occ production launches): k_occlude walks A's shadow tasks in their phase-A
                       // regions (workgroup w: regions w, w + G, ...); k_pack_a packs only the continuations
     int fin_grid;     // k_finish workgroups at most (0: a lane per output pixel), a grid-stride loop beyond
-    unsigned* cont_peak;  // frames of several chunks: the most continuations of one chunk (k_pack_a, atomicMax)
     int fin_cont;     // k_finish: the continued paths' pixels first (chain path: cflat, totals[1], kPathCont)
-    int early_fin;    // 1 (lone frames, k_mix with the LDS queue, no compact records): k_mix's shadow-role
-                      // workgroups finish the pixels without a continued sample once A's occlusion is done
-                      // (pathchain.hip early finish); k_finish the rest and what k_fallback changed
-                      // (2: tests, no wait for the other workgroups)
     int refill;       // a wave refills once <= refill of its lanes are still walking
     int orefill;      // the same for the shadow (any-hit) walks
     int brefill;      // the same for phase-B chains
@@ -223,6 +221,13 @@ struct PcParams {
                       // k_occlude workgroup {start, end}, then [cap][4] phase-B continuation {grab, end,
                       // last level, walk steps}; wall clock; or null
     int trace_blocks;
+    // (new fields at the end: kernel arguments are loaded in runs of neighbours, so a field inserted
+    // among the walk kernels' ones changed their SGPR spills 28 -> 67)
+    unsigned* cont_peak;  // frames of several chunks: the most continuations of one chunk (k_pack_a, atomicMax)
+    int early_fin;    // 1 (lone frames, k_mix with the LDS queue, no compact records): k_mix's shadow-role
+                      // workgroups finish the pixels without a continued sample once A's occlusion is done
+                      // (pathchain.hip early finish); k_finish the rest and what k_fallback changed
+                      // (2: tests, no wait for the other workgroups)
 };
 
 // Worst-case task-queue slots per workgroup: every sample of the workgroup

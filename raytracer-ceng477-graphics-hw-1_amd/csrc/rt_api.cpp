@@ -142,9 +142,9 @@ struct rt_scene {
                                 // 900-990 measured 2-4 % slower for C3 one frame: the restarted walks are the
                                 // heaviest, deepest chains, which then start phase B from scratch)
     int tune_hot_units = 1;     // RT_HOT_UNITS: lone frames deal phase-A units heaviest-first by the previous frame's steps
-    int tune_early_fin = 0;     // RT_EARLY_FIN=1: lone frames' k_mix finishes the pixels without a continued sample
-                                // (2: tests, its workgroups do not wait for each other: k_finish takes the rest);
-                                // off by default: measured slower
+    int tune_early_fin = 0;     // RT_EARLY_FIN=1 (builds with RT_EARLY_FIN_BUILD=1): lone frames' k_mix finishes
+                                // the pixels without a continued sample (2: tests, its workgroups do not wait for
+                                // each other: k_finish takes the rest); measured slower
     int tune_occ_inplace = 1;   // RT_OCC_INPLACE: frame batches' k_occlude reads A's shadow tasks in their regions (0: packed)
     int tune_compact = 1;       // RT_COMPACT: phase-A records without directions (16 B instead of 32): 1 frame batches,
                                 // 2 every launch, 0 none
@@ -1002,7 +1002,7 @@ int render_chain(rt_scene* s, const rtk::Eye& eye, const rtk::FrameParams& f, bo
     // sample beside phase B (pathchain.hip k_mix); not with compact records (the rebuilt directions are
     // k_finish<true>'s) nor beside other chunks' kernels (its workgroups wait for each other, bounded)
     p.early_fin = !P.split_occ && !count && !fused && P.phase_b && P.clevels == 0 && units == g.units_total &&
-                  s->tune_early_fin ? s->tune_early_fin : 0;
+                  RT_EARLY_FIN_BUILD && s->tune_early_fin ? s->tune_early_fin : 0;
     p.refill = s->tune_refill >= 0 ? s->tune_refill : 0;
     p.service = s->tune_service >= 0 ? s->tune_service : 64;
     p.bservice = s->tune_bservice;
