@@ -18,7 +18,7 @@ branch of it and compare with the reference goldens (raytracer.cpp:385-452):
     kFbEye continuations, level-1 walks as reflections of their level-0 record),
     alone and with RT_CONT_CB=1000 (the restarts beyond it in k_fallback);
   * RT_EARLY_FIN=1 / 2: a lone frame's early finish in k_mix, with its wait /
-    without it.
+    without it (builds with RT_EARLY_FIN_BUILD=1).
 """
 from __future__ import annotations
 
@@ -53,7 +53,8 @@ ENVS = [
     # and k_fallback read the stored direction words instead of the chain's tail copies
     {"RT_COMPACT": "0", "RT_CONT_CB": "1000"},
     {"RT_FORCE_FALLBACK": "2", "RT_FBS_CAP": "64"},
-    # a lone frame's early finish (RT_EARLY_FIN, off by default: k_mix's shadow-role workgroups finish the
+    # a lone frame's early finish (RT_EARLY_FIN in builds with RT_EARLY_FIN_BUILD=1, off by default and
+    # not built by default: these then run the default path; k_mix's shadow-role workgroups finish the
     # pixels without a continued sample, k_finish the rest and what k_fallback changed): with deferred
     # paths and shadow rays, with continuations beyond the record space, and without the wait for the
     # other workgroups (k_finish takes most pixels), alone and with the fallback shadow queue overflowing
