@@ -952,6 +952,9 @@ int render_chain(rt_scene* s, const rtk::Eye& eye, const rtk::FrameParams& f, bo
     // order this use after the arena's previous one (possibly on another stream)
     if (arena.last && arena.last_stream != st) HIP_TRY(hipStreamWaitEvent(st, arena.last, 0));
     if (arena.bytes < P.bytes) {
+        if (std::getenv("RT_LOG_ALLOC"))            // diagnostics: a growth inside a timed region serialises it
+            std::fprintf(stderr, "librt_hip: slot %d workspace %.1f -> %.1f MB (frames %d, cb %zu of %zu)\n", slot,
+                         arena.bytes / 1e6, P.bytes / 1e6, g.nframes, P.cb, P.cap);
         if (arena.p) HIP_TRY(hipStreamSynchronize(st));   // the previous frames on it may still use it
         (void)hipFree(arena.p);
         arena.p = nullptr;
