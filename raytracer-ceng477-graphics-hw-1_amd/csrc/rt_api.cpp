@@ -959,8 +959,11 @@ int render_chain(rt_scene* s, const rtk::Eye& eye, const rtk::FrameParams& f, bo
         (void)hipFree(arena.p);
         arena.p = nullptr;
         arena.bytes = 0;
-        HIP_TRY(hipMalloc(reinterpret_cast<void**>(&arena.p), P.bytes));
-        arena.bytes = P.bytes;
+        // (+1/16: a slightly larger plan later -- the measured record space moving -- fits without another
+        // synchronising reallocation)
+        const size_t want = P.bytes + P.bytes / 16;
+        HIP_TRY(hipMalloc(reinterpret_cast<void**>(&arena.p), want));
+        arena.bytes = want;
     }
     auto at = [&](size_t o) { return static_cast<void*>(arena.p + o); };
     rtc::PcParams p{};
@@ -1437,7 +1440,8 @@ int render_batch(rt_scene* s, const rt_camera* cams, int n, int aa, int stripe_r
 // stripe_rows <= 0: whole frames (each camera's own height); otherwise every
 // frame is this rank's row stripes (rt_render_frames_device).
 int render_cameras(rt_scene* s, const rt_camera* cams, int n, int aa, void* const* outs_dev, hipStream_t stream,
-                   int flags, int stripe_rows = 0, int rank = 0, int nranks = 1) {
+                   int flags, int stripe_rows = 0, int rank = 0, int nranks = 1, int batch_max = 0,
+                   int slot0 = 0) {
     auto rows_of = [&](int i) { return stripe_rows > 0 ? stripe_rows : cams[i].image_height; };
     const bool batching = (s->path == rt_scene::kChain || s->path == rt_scene::kFused) && n > 1 &&
                           s->tune_batch > 1;
@@ -1445,7 +1449,9 @@ int render_cameras(rt_scene* s, const rt_camera* cams, int n, int aa, void* cons
         // consecutive same-size frames, up to kMaxFrames and one chain chunk of samples per batch
         // at least nslot batches when the frames allow (concurrent batches overlap each other's tails)
         const int nslot = std::max(1, std::min(s->tune_slots, rt_scene::kSlots));
-        const int bmax = std::min({s->tune_batch, rtc::kMaxFrames, (n + nslot - 1) / nslot});
+        // (batch_max, slot0: the rest of a call after its first batch, on the next slots -- batches of the
+        // same size as the calls that follow, on every slot, so no workspace grows inside those)
+        const int bmax = std::min({s->tune_batch, rtc::kMaxFrames, batch_max > 0 ? batch_max : (n + nslot - 1) / nslot});
         std::vector<int> starts;
         HIP_TRY(hipSetDevice(s->device));
         if (const int rc = ensure_chain_grids(s)) return rc;
@@ -1482,23 +1488,25 @@ int render_cameras(rt_scene* s, const rt_camera* cams, int n, int aa, void* cons
             poll_cont(s, true);
             s->cont_frac = std::max(s->cont_frac, 1e-9);
             return render_cameras(s, cams + starts[1], n - starts[1], aa, outs_dev + starts[1], stream, flags,
-                                  stripe_rows, rank, nranks);
+                                  stripe_rows, rank, nranks, bmax, 1);
         }
         if (!s->fork_ev) HIP_TRY(hipEventCreateWithFlags(&s->fork_ev, hipEventDisableTiming));
         HIP_TRY(hipEventRecord(s->fork_ev, stream));
         const int used = std::min(nb, nslot);
-        for (int k = 0; k < used; ++k) {
+        for (int j = 0; j < used; ++j) {
+            const int k = (j + slot0) % nslot;
             if (!s->slot_stream[k]) HIP_TRY(hipStreamCreateWithFlags(&s->slot_stream[k], hipStreamNonBlocking));
             if (!s->slot_done[k]) HIP_TRY(hipEventCreateWithFlags(&s->slot_done[k], hipEventDisableTiming));
             HIP_TRY(hipStreamWaitEvent(s->slot_stream[k], s->fork_ev, 0));
         }
         for (int b = 0; b < nb; ++b) {
-            const int k = b % nslot, i = starts[b];
+            const int k = (b + slot0) % nslot, i = starts[b];
             const int rc = render_batch(s, cams + i, starts[b + 1] - i, aa, rows_of(i), rank, nranks, outs_dev + i,
                                         s->slot_stream[k], flags, k);
             if (rc) return rc;
         }
-        for (int k = 0; k < used; ++k) {
+        for (int j = 0; j < used; ++j) {
+            const int k = (j + slot0) % nslot;
             HIP_TRY(hipEventRecord(s->slot_done[k], s->slot_stream[k]));
             HIP_TRY(hipStreamWaitEvent(stream, s->slot_done[k], 0));
         }
