@@ -104,7 +104,7 @@ __host__ __device__ inline unsigned unit_col(int tiles_x, int ublk_h, int ublk_w
 // counter of pixels taken, 256 B apart (atomics on one word serialise: 64-pixel grabs on a single
 // counter cost a lone frame 0.4 ms), from totals word kFinCtr0 on.
 constexpr int kFinStripes = 16, kFinCtrStride = 64, kFinCtr0 = 64;
-constexpr int kTotalsWords = kFinCtr0 + kFinStripes * kFinCtrStride;
+constexpr int kTotalsWords = RT_EARLY_FIN_BUILD ? kFinCtr0 + kFinStripes * kFinCtrStride : 12;
 __host__ __device__ inline unsigned fin_stripe_len(unsigned npix) {
     return ((npix + kFinStripes - 1) / kFinStripes + 63u) & ~63u;
 }
