@@ -913,7 +913,10 @@ int render_chain(rt_scene* s, const rtk::Eye& eye, const rtk::FrameParams& f, bo
     const int max_grid = fused ? s->fused_grid : s->chain_grid;
     auto grid_for = [&](int n0) { return std::max(1, std::min(max_grid, (n0 + 255) / 256)); };
     size_t cb = 0;
-    if (f.chunk_k == 1) poll_cont(s, false);   // (read-backs of earlier frames' chunks, C5-sized frames)
+    // read-backs of earlier frames' chunks (C5-sized lone frames); never for a frame batch: its frame count
+    // was fitted to one launch with the share its caller (render_cameras) polled, and a larger share
+    // here would split the batch into chunks forked over every slot, from inside one slot's stream
+    if (f.chunk_k == 1 && f.nframes <= 1) poll_cont(s, false);
     const size_t units = chain_launch_units(s, g, count, &cb);
     const ChainPlan P = chain_plan(s, g, units, count, cb);
     const int chunk_rows = (int)units * unit;
