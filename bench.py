@@ -83,15 +83,16 @@ def kernel_bytes(r: dict, c: dict, out_pixels: int, batched: bool, nlights: int)
     compact = os.environ.get("RT_COMPACT", "1")
     REC_A = 16 if compact == "2" or (compact == "1" and batched) else 32
     DIRW = 16 if REC_A == 16 else 0
-    inplace = batched and os.environ.get("RT_OCC_INPLACE", "1") != "0"
+    occ_env = os.environ.get("RT_OCC_INPLACE", "1")
+    inplace = occ_env == "1" or (batched and occ_env == "2")   # A's tasks walked where k_chain left them
     samples, skipped = c["primary_rays"], c["shadow_rays_skipped"]
     a_sh, bq, bo, conts = r["a_shadow_rays"], r["bq_shadow_rays"], r["bo_shadow_rays"], r["continuations"]
     shadow_ws = TASK + 16 + NRM + OCC
     k = {
         "k_chain": r["a_walk_bytes"] + samples * 4 + r["a_hits"] * (REC_A + NRM) + a_sh * TASK + skipped * OCC
                    + conts * (TASK + DIRW),
-        # frame batches walk A's shadow tasks in their phase-A regions (PcParams::occ_inplace): only the
-        # continuations are packed
+        # A's shadow tasks walked in their phase-A regions (PcParams::occ_inplace: k_occlude in frame
+        # batches, k_mix's shadow role in a lone frame): only the continuations are packed
         "k_pack_a": ((0 if inplace else a_sh) + conts) * 2 * TASK,
         "k_mix": r["b_walk_bytes"] + r["bq_shadow_bytes"] + conts * (TASK + 16 + DIRW + (REC_A - 16) + NRM)
                  + r["b_hits"] * (REC_B + NRM) + bq * (16 + NRM + OCC) + bo * TASK,

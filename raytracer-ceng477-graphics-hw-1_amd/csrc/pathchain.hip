@@ -1603,6 +1603,25 @@ __global__ __launch_bounds__(kBlock) void k_pack_b(PcParams p) {
 #ifndef RT_MIX_NOBQ_WAVES
 #define RT_MIX_NOBQ_WAVES 5      // without the LDS queue: 96 VGPRs, no spills
 #endif
+// Shadow tasks where their phase left them (p.occ_inplace / occ_inplace_b): region r (phase workgroup
+// r's queue) to workgroup w + k W, one region at a time -- no packed copy of 4 B in and out per task.
+// which = 0: A's (k_occlude in frame batches, k_mix's shadow role in a lone frame), 1: B's overflow.
+__device__ __forceinline__ void occlude_regions(const rtk::DevScene& s, const PcParams& p, int which, unsigned w,
+                                                unsigned W) {
+    const unsigned nreg = which ? (unsigned)p.gb : (unsigned)p.grid;
+    const unsigned* const q = which ? p.sqB : p.sqA;
+    const unsigned* const cnt = which ? p.scntB : p.scntA;
+    const size_t qcap = which ? p.scapB : p.scapA;
+    for (unsigned r = w; r < nreg; r += W) {
+        if (r != w) {
+            __syncthreads();                    // every wave is done with the previous region
+            if (threadIdx.x == 0) g_head = 0;
+            __syncthreads();
+        }
+        occlude_queue_body(s, p, 0, 1, q + (size_t)r * qcap, cnt[r]);
+    }
+}
+
 // Early finish (PcParams::early_fin, lone frames): pixels without a continued sample, taken 64 at a time
 // from the stripes' counters (defined with k_finish; k_finish takes what is left)
 __shared__ unsigned g_efin;
@@ -1623,9 +1642,12 @@ __global__ __launch_bounds__(kBlock, BQ || COUNT ? RT_MIX_WAVES : RT_MIX_NOBQ_WA
             atomicAdd(&p.totals[10], 1u);          // this chain wave is done (early finish)
     }
     else if (!p.exp_skip_occ) {
-        if constexpr (!COUNT && RT_LEAF_QUEUE)
-            occlude_queue_body(s, p, blockIdx.x - p.gb, gridDim.x - p.gb, p.sflatA, p.totals[0]);
-        else
+        // (a lone frame with p.occ_inplace: A's tasks where k_chain left them, region by region: the
+        // shadow role ends unevenly, but beside phase B's deep chains, and k_pack_a copies no task)
+        if constexpr (!COUNT && RT_LEAF_QUEUE) {
+            if (p.occ_inplace) occlude_regions(s, p, 0, blockIdx.x - p.gb, gridDim.x - p.gb);
+            else occlude_queue_body(s, p, blockIdx.x - p.gb, gridDim.x - p.gb, p.sflatA, p.totals[0]);
+        } else
             occlude_body<COUNT>(s, p, blockIdx.x - p.gb, gridDim.x - p.gb, p.sflatA, p.totals[0], 0);
     }
     const bool ranker = !COUNT && !chain && p.urank && blockIdx.x == gridDim.x - 1;
@@ -1680,18 +1702,7 @@ __global__ __launch_bounds__(kBlock, RT_OCC_WAVES_PER_EU) void k_occlude(rtk::De
         // LDS-queue overflow in lone frames (few tasks; no k_pack_b launch on the frame's critical path)
         const bool inplace = which ? p.occ_inplace_b != 0 : p.occ_inplace != 0;
         if (inplace) {
-            const unsigned nreg = which ? (unsigned)p.gb : (unsigned)p.grid;
-            const unsigned* const q = which ? p.sqB : p.sqA;
-            const unsigned* const cnt = which ? p.scntB : p.scntA;
-            const size_t qcap = which ? p.scapB : p.scapA;
-            for (unsigned r = blockIdx.x; r < nreg; r += gridDim.x) {
-                if (r != blockIdx.x) {
-                    __syncthreads();            // every wave is done with the previous region
-                    if (threadIdx.x == 0) g_head = 0;
-                    __syncthreads();
-                }
-                occlude_queue_body(s, p, 0, 1, q + (size_t)r * qcap, cnt[r]);
-            }
+            occlude_regions(s, p, which, blockIdx.x, gridDim.x);
         } else if (which) {
             occlude_queue_body(s, p, blockIdx.x, gridDim.x, p.sflatB, p.totals[2]);
         } else {
