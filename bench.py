@@ -84,7 +84,7 @@ def kernel_bytes(r: dict, c: dict, out_pixels: int, batched: bool, nlights: int)
     REC_A = 16 if compact == "2" or (compact == "1" and batched) else 32
     DIRW = 16 if REC_A == 16 else 0
     occ_env = os.environ.get("RT_OCC_INPLACE", "1")
-    inplace = occ_env == "1" or (batched and occ_env == "2")   # A's tasks walked where k_chain left them
+    inplace = occ_env == "2" or (batched and occ_env == "1")   # A's tasks walked where k_chain left them
     samples, skipped = c["primary_rays"], c["shadow_rays_skipped"]
     a_sh, bq, bo, conts = r["a_shadow_rays"], r["bq_shadow_rays"], r["bo_shadow_rays"], r["continuations"]
     shadow_ws = TASK + 16 + NRM + OCC
@@ -92,7 +92,7 @@ def kernel_bytes(r: dict, c: dict, out_pixels: int, batched: bool, nlights: int)
         "k_chain": r["a_walk_bytes"] + samples * 4 + r["a_hits"] * (REC_A + NRM) + a_sh * TASK + skipped * OCC
                    + conts * (TASK + DIRW),
         # A's shadow tasks walked in their phase-A regions (PcParams::occ_inplace: k_occlude in frame
-        # batches, k_mix's shadow role in a lone frame): only the continuations are packed
+        # batches; k_mix's shadow role in a lone frame with RT_OCC_INPLACE=2): only the continuations packed
         "k_pack_a": ((0 if inplace else a_sh) + conts) * 2 * TASK,
         "k_mix": r["b_walk_bytes"] + r["bq_shadow_bytes"] + conts * (TASK + 16 + DIRW + (REC_A - 16) + NRM)
                  + r["b_hits"] * (REC_B + NRM) + bq * (16 + NRM + OCC) + bo * TASK,

@@ -1642,8 +1642,8 @@ __global__ __launch_bounds__(kBlock, BQ || COUNT ? RT_MIX_WAVES : RT_MIX_NOBQ_WA
             atomicAdd(&p.totals[10], 1u);          // this chain wave is done (early finish)
     }
     else if (!p.exp_skip_occ) {
-        // (a lone frame with p.occ_inplace: A's tasks where k_chain left them, region by region: the
-        // shadow role ends unevenly, but beside phase B's deep chains, and k_pack_a copies no task)
+        // (a lone frame with p.occ_inplace, RT_OCC_INPLACE=2: A's tasks where k_chain left them, region
+        // by region, k_pack_a copying none -- measured slower: the uneven regions cost k_mix 60 us)
         if constexpr (!COUNT && RT_LEAF_QUEUE) {
             if (p.occ_inplace) occlude_regions(s, p, 0, blockIdx.x - p.gb, gridDim.x - p.gb);
             else occlude_queue_body(s, p, blockIdx.x - p.gb, gridDim.x - p.gb, p.sflatA, p.totals[0]);

@@ -145,8 +145,8 @@ struct rt_scene {
     int tune_early_fin = 0;     // RT_EARLY_FIN=1 (builds with RT_EARLY_FIN_BUILD=1): lone frames' k_mix finishes
                                 // the pixels without a continued sample (2: tests, its workgroups do not wait for
                                 // each other: k_finish takes the rest); measured slower
-    int tune_occ_inplace = 1;   // RT_OCC_INPLACE: A's shadow tasks read in their regions (k_occlude in frame batches,
-                                // k_mix's shadow role in lone frames; 2: batches only; 0: packed)
+    int tune_occ_inplace = 1;   // RT_OCC_INPLACE: A's shadow tasks read in their regions by k_occlude in frame
+                                // batches (2: also by k_mix's shadow role in lone frames, slower; 0: packed)
     int tune_compact = 1;       // RT_COMPACT: phase-A records without directions (16 B instead of 32): 1 frame batches,
                                 // 2 every launch, 0 none
     int tune_coop = 1;          // RT_COOP (builds with RT_COOP_BUILD=1): lone-frame phase B walks its tail chains on 8-lane groups (pathchain.hip coop_step)
@@ -1005,9 +1005,9 @@ int render_chain(rt_scene* s, const rtk::Eye& eye, const rtk::FrameParams& f, bo
     p.occ_grid = s->occl_grid;
     p.fin_grid = s->tune_fgrid > 0 ? s->tune_fgrid : 8 * s->num_cus;
     p.split_occ = P.split_occ ? 1 : 0;
-    // A's shadow tasks walked where k_chain left them: by k_occlude in frame batches, by k_mix's shadow
-    // role in a lone frame (RT_OCC_INPLACE=2: batches only)
-    p.occ_inplace = !count && !fused && (P.split_occ ? s->tune_occ_inplace != 0 : s->tune_occ_inplace == 1) ? 1 : 0;
+    // A's shadow tasks walked where k_chain left them: by k_occlude in frame batches; by k_mix's shadow
+    // role in a lone frame only with RT_OCC_INPLACE=2 (its uneven regions cost k_mix +60 us, k_pack_a -10)
+    p.occ_inplace = !count && !fused && (P.split_occ ? s->tune_occ_inplace != 0 : s->tune_occ_inplace == 2) ? 1 : 0;
     p.occ_inplace_b = !P.split_occ && !count && !fused && s->tune_occ_inplace ? 1 : 0;
     p.cont_peak = peak ? s->d_cont_peak : nullptr;
     // lone frames in one launch: k_mix's shadow-role workgroups finish the pixels without a continued
