@@ -75,16 +75,13 @@ def kernel_bytes(r: dict, c: dict, out_pixels: int, batched: bool, nlights: int)
     4 lights; else 8), and writes 3 B per pixel.
     One frame alone, A's shadow rays run in k_mix's shadow role; in frame batches in k_occlude.  One
     frame alone keeps 32-B phase-A records (rt_api.cpp chain_plan: compact records in frame batches
-    only, RT_COMPACT=2 everywhere); with RT_EARLY_FIN=1 (off by default) k_mix's shadow-role workgroups
-    finish the pixels without a continued sample, and their share of k_finish's bytes is charged to k_mix
-    (the share of samples not continued; k_finish keeps the continued pixels')."""
+    only, RT_COMPACT=2 everywhere)."""
     NRM, TASK, OCC = 16, 4, 1
     REC_B = 32
     compact = os.environ.get("RT_COMPACT", "1")
     REC_A = 16 if compact == "2" or (compact == "1" and batched) else 32
     DIRW = 16 if REC_A == 16 else 0
-    occ_env = os.environ.get("RT_OCC_INPLACE", "1")
-    inplace = occ_env == "2" or (batched and occ_env == "1")   # A's tasks walked where k_chain left them
+    inplace = batched and os.environ.get("RT_OCC_INPLACE", "1") != "0"   # A's tasks walked where k_chain left them
     samples, skipped = c["primary_rays"], c["shadow_rays_skipped"]
     a_sh, bq, bo, conts = r["a_shadow_rays"], r["bq_shadow_rays"], r["bo_shadow_rays"], r["continuations"]
     shadow_ws = TASK + 16 + NRM + OCC
@@ -92,7 +89,7 @@ def kernel_bytes(r: dict, c: dict, out_pixels: int, batched: bool, nlights: int)
         "k_chain": r["a_walk_bytes"] + samples * 4 + r["a_hits"] * (REC_A + NRM) + a_sh * TASK + skipped * OCC
                    + conts * (TASK + DIRW),
         # A's shadow tasks walked in their phase-A regions (PcParams::occ_inplace: k_occlude in frame
-        # batches; k_mix's shadow role in a lone frame with RT_OCC_INPLACE=2): only the continuations packed
+        # batches): only the continuations packed
         "k_pack_a": ((0 if inplace else a_sh) + conts) * 2 * TASK,
         "k_mix": r["b_walk_bytes"] + r["bq_shadow_bytes"] + conts * (TASK + 16 + DIRW + (REC_A - 16) + NRM)
                  + r["b_hits"] * (REC_B + NRM) + bq * (16 + NRM + OCC) + bo * TASK,
@@ -104,10 +101,6 @@ def kernel_bytes(r: dict, c: dict, out_pixels: int, batched: bool, nlights: int)
     }
     if not batched:                       # one frame: A's shadow rays are k_mix's shadow role
         k["k_mix"] += k.pop("k_occlude_a")
-        if os.environ.get("RT_EARLY_FIN", "0") in ("1", "2") and REC_A == 32 and samples:
-            moved = int(k["k_finish"] * max(0.0, 1.0 - conts / samples))
-            k["k_mix"] += moved
-            k["k_finish"] -= moved
     return k
 
 
@@ -118,9 +111,6 @@ def traversal_bytes(r: dict) -> int:
 # kernels one frame launches, per render path (the roofline covers all of them)
 PATH_KERNELS = {
     "chain": ["k_chain", "k_pack_a", "k_mix", "k_pack_b", "k_occlude", "k_fallback", "k_finish", "k_finish_any"],
-    "fused": ["k_fused", "k_finish", "k_finish_any"],
-    "megakernel": ["k_render"],
-    "wavefront": ["k_trace", "k_shadow", "k_shade", "k_fold", "k_resolve"],
 }
 
 CONFIGS = {
@@ -133,6 +123,19 @@ CONFIGS = {
     "MB": ("marbles.xml", "marbles.xml verbatim 1024x1024, depth 6 (mirror marbles, 2 lights)"),
 }
 HBM_GUIDE_GBPS = 6290.0    # MI355X_MICROARCH.md: measured float4 copy (79 % of spec), beside our own measurement
+L2_GUIDE_GBPS = 34500.0    # MI355X_MICROARCH.md:316: aggregate L2 streaming bandwidth, beside the measured line gather
+
+
+def golden_sha(config: str, aa: int) -> str | None:
+    """sha256 of the reference's RGB for this workload (tests/golden/goldens.json, made by running the
+    compiled reference: tests/golden/make_goldens.py), or None when no golden covers it."""
+    gfile = ROOT / "tests" / "golden" / "goldens.json"
+    if not gfile.exists():
+        return None
+    for g in json.loads(gfile.read_text())["goldens"]:
+        if g["name"] == f"{config}_aa{aa}" and len(g["cameras"]) >= 1:
+            return g["cameras"][0].get("sha256_rgb")
+    return None
 
 
 def parse():
@@ -144,7 +147,7 @@ def parse():
     ap.add_argument("--aa", type=int, default=None, help="SSAA factor (default 1; C5: 4)")
     ap.add_argument("--stripe-rows", type=int, default=4,
                     help="output rows per round-robin stripe (4: best rank balance at N=8, tools/exp_shard.py)")
-    ap.add_argument("--path", default="chain", choices=sorted(PATH_KERNELS), help="render path (all bit-identical)")
+    ap.add_argument("--path", default="chain", choices=sorted(PATH_KERNELS), help="render path (the chain path)")
     ap.add_argument("--cpu-seconds", type=float, default=15.0, help="CPU baseline budget (rank 0, N=1)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--trace", action="store_true",
@@ -316,6 +319,7 @@ def main() -> int:
         raise RuntimeError(f"per-role fetch bytes do not add up: {roles} vs {pcnt['node_visits']}")
     nlights = len(re.findall(r"<PointLight\b", Path(xml).read_text()))
     kbytes = kernel_bytes(roles, cnt, rows * W, batched=F > 1, nlights=nlights)
+    kbytes_one = kernel_bytes(roles, cnt, rows * W, batched=False, nlights=nlights)
     alg_bytes = sum(kbytes.values())
     trav_bytes = traversal_bytes(roles)
     ws_bytes = alg_bytes - trav_bytes
@@ -358,7 +362,9 @@ def main() -> int:
     def groups(k):
         return [min(F, k - i) for i in range(0, k, F)]
 
-    for n in groups(max(a.warmup, F)):       # at least one full group: every workspace is allocated
+    # at least one full group, twice: every workspace is allocated, and sized by the continuation share
+    # the first group's read-backs measured (rt_render_frames_device never waits for them on the host)
+    for n in groups(max(a.warmup, F)) + ([F] if F > 1 else []):
         step(n)
     torch.cuda.synchronize(dev)
     note("warmup done")
@@ -385,6 +391,18 @@ def main() -> int:
                         "(walked whole by k_fallback), deferred closest-hit / shadow rays (outside the wide "
                         "trees' slab-test range), fallback shadow-queue overflows")
 
+    # N=1: the last timed batch's frames, as the timed kernels left them, against the reference's golden
+    # RGB (every frame bit-equal to the first, whose sha256 is the golden's)
+    golden_ok = None
+    if world == 1:
+        import hashlib
+        want = golden_sha(config, aa)
+        n_last = gs[-1]
+        frames = slab_bufs[(nxt[0] - 1) % NB][:n_last]
+        sha0 = hashlib.sha256(frames[0].cpu().numpy().tobytes()).hexdigest()
+        golden_ok = {"frames_checked": n_last, "equal_to_first": all(torch.equal(frames[i], frames[0]) for i in range(n_last)),
+                     "sha256_first": sha0, "golden_sha256": want,
+                     "equal": (want is not None and sha0 == want)}
     # N>1: the assembled frames equal one GPU's whole-frame render (checked after timing, rank 0)
     frames_ok = None
     if world > 1 and rank == 0:
@@ -403,6 +421,63 @@ def main() -> int:
         torch.cuda.synchronize(dev)
         lat.append(e0.elapsed_time(e1))
     lat_ms = sorted(lat)[len(lat) // 2] if lat else float("nan")
+
+    def dev_ms(fn, reps=5):
+        out = []
+        for i in range(reps):
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record(stream)
+            fn(i)
+            e1.record(stream)
+            torch.cuda.synchronize(dev)
+            out.append(e0.elapsed_time(e1))
+        return out
+
+    # the drop-in caller's other lone frames (reported, not `value`): a moving camera (a different eye every
+    # frame: the phase-A unit order comes from the previous, different frame), and cold frames -- a scene
+    # whose frames never use a previous frame's unit costs (RT_HOT_UNITS=0: every frame dealt as a first
+    # one is), its first call's wall time (workspace allocation included) beside the device time of the rest
+    lone_extra = None
+    if not a.trace and world == 1:
+        import ctypes as _ct
+
+        def moved(i):
+            c = pkg.Camera()
+            _ct.memmove(_ct.addressof(c), _ct.addressof(cam), _ct.sizeof(c))
+            c.position.x = cam.position.x + 0.002 * (i + 1)
+            c.position.y = cam.position.y + 0.001 * (i + 1)
+            return c
+
+        mv = dev_ms(lambda i: scene.render_device(moved(i), aa, slab.data_ptr(), sp, S, rank, world), reps=7)
+        saved = os.environ.get("RT_HOT_UNITS")
+        os.environ["RT_HOT_UNITS"] = "0"
+        try:
+            cscene = pkg.Scene.from_xml(xml, device=local, render_path=a.path)
+        finally:
+            if saved is None:
+                os.environ.pop("RT_HOT_UNITS", None)
+            else:
+                os.environ["RT_HOT_UNITS"] = saved
+        torch.cuda.synchronize(dev)
+        t1 = time.perf_counter()
+        cscene.render_device(cam, aa, slab.data_ptr(), sp, S, rank, world)
+        torch.cuda.synchronize(dev)
+        first_wall = (time.perf_counter() - t1) * 1e3
+        cold = dev_ms(lambda i: cscene.render_device(cam, aa, slab.data_ptr(), sp, S, rank, world), reps=7)
+        cold_ws = cscene.memory()["workspace_bytes"]
+        cscene.close()
+        lone_extra = {
+            "single_frame_cold": {"ms": round(sorted(cold)[len(cold) // 2], 4),
+                                  "first_call_wall_ms": round(first_wall, 3),
+                                  "workspace_bytes": cold_ws,
+                                  "definition": "one frame alone, device time, phase-A units dealt without any "
+                                                "previous frame's costs (RT_HOT_UNITS=0: what a first render of a "
+                                                "camera does), median of 7; first_call_wall_ms: the scene's first "
+                                                "call incl. workspace allocation, host wall"},
+            "single_frame_moving": {"ms": round(sorted(mv)[len(mv) // 2], 4),
+                                    "definition": "one frame alone, device time, camera moved every frame (the unit "
+                                                  "order comes from the previous, different view), median of 7"},
+        }
     tmax = torch.tensor([elapsed, kern_ms, lat_ms], dtype=torch.float64, device=dev)
     tmax = all_reduce(tmax, dist.ReduceOp.MAX)
     elapsed, kern_ms_max, lat_ms = tmax.tolist()
@@ -471,23 +546,29 @@ def main() -> int:
     if rank == 0:
         ms = elapsed / a.steps * 1e3
         value = ps_frame * a.steps / elapsed / 1e6
-        achieved = alg_bytes / (kern_ms / 1e3) / 1e9
+        # priced against the driver-timed wall time per frame (ms_per_step), as the headline is
+        achieved = alg_bytes / (ms / 1e3) / 1e9
         # each kernel's own fraction: its alg bytes per frame / its one-slot time per frame (RT_KTIME),
         # against the measured L2 full-line peak (and the divergent-gather ceiling of its fetch shape)
-        per_kernel, dominant = None, None
-        if ktimes:
-            kt = ktimes["batched" if F > 1 else "one_frame"]
-            per_kernel = {}
-            for k, b in kbytes.items():
+        per_kernel, per_kernel_one, dominant = None, None, None
+
+        def kernel_fracs(kb, kt):
+            out = {}
+            for k, b in kb.items():
                 t = kt.get(k)
                 gbps = b / (t / 1e3) / 1e9 if t else None
-                per_kernel[k] = {"alg_bytes": int(b), "ms_one_slot": t,
-                                 "achieved": round(gbps, 1) if gbps else None,
-                                 "frac": round(gbps / peaks["l2_line_gbps"], 4) if gbps else None,
-                                 "frac_of_divergent_gather": round(gbps / peaks["l2_gather_gbps"], 4) if gbps else None}
+                out[k] = {"alg_bytes": int(b), "ms_one_slot": t,
+                          "achieved": round(gbps, 1) if gbps else None,
+                          "frac": round(gbps / peaks["l2_line_gbps"], 4) if gbps else None,
+                          "frac_of_guide_l2": round(gbps / L2_GUIDE_GBPS, 4) if gbps else None,
+                          "frac_of_divergent_gather": round(gbps / peaks["l2_gather_gbps"], 4) if gbps else None}
+            return out
+        if ktimes:
+            per_kernel = kernel_fracs(kbytes, ktimes["batched" if F > 1 else "one_frame"])
+            per_kernel_one = kernel_fracs(kbytes_one, ktimes["one_frame"])
             dk = max((k for k in per_kernel if per_kernel[k]["ms_one_slot"]), key=lambda k: per_kernel[k]["ms_one_slot"])
             dominant = {"kernel": dk, **per_kernel[dk]}
-        traffic_gbps = traffic / (kern_ms / 1e3) / 1e9 if traffic else None
+        traffic_gbps = traffic / (ms / 1e3) / 1e9 if traffic else None
         if backend != "nccl":
             desc += f" [REHEARSAL: {backend} host-staged gather, all ranks on one GPU; not a measurement]"
         line = {
@@ -504,11 +585,12 @@ def main() -> int:
                        "hw_queues": int(os.environ["GPU_MAX_HW_QUEUES"]),
                        # every frame this process rendered on the GPU (counting pass, warmup, timed, latency,
                        # host-buffer runs): the divisor for whole-run PMC totals (tools/summarize_profile.py)
-                       "frames_rendered_total": 2 + max(a.warmup, F) + a.steps
-                                                + (0 if a.trace else 5 + (8 if world == 1 else 0)),
+                       "frames_rendered_total": 2 + max(a.warmup, F) + (F if F > 1 else 0) + a.steps
+                                                + (0 if a.trace else 5 + (8 + 15 if world == 1 else 0)),
                        # frames the non-counting kernels rendered in a --trace run (warmup + timed)
-                       "trace_frames": max(a.warmup, F) + a.steps if a.trace else None,
+                       "trace_frames": max(a.warmup, F) + (F if F > 1 else 0) + a.steps if a.trace else None,
                        "assembled_frames_equal_single_gpu": frames_ok,
+                       "timed_frames_equal_golden": golden_ok,
                        "primary_rays": prim_frame, "shadow_rays": shadow_frame, "reflection_rays": refl_frame,
                        # of shadow_rays: rays the timed kernels do not trace because their result cannot
                        # change the pixel (light behind the surface, pathchain.hip light_needed); the
@@ -527,6 +609,7 @@ def main() -> int:
             "single_frame": ({"ms": round(lat_ms, 4), "mray_s": round(ps_frame / lat_ms / 1e3, 3),
                               "definition": "one frame alone on the GPU (rt_render_device), device time"}
                              if lat else None),
+            **(lone_extra or {}),
             "hbm_footprint": footprint,
             "fallback": fallback,
             "kernel_ms_one_slot": ktimes,
@@ -535,6 +618,8 @@ def main() -> int:
                                        "host memory (PCIe included), one frame at a time"} if host_ms else None),
             "roofline": {"bound": "l2", "achieved": round(achieved, 2), "peak": round(peaks["l2_line_gbps"], 1),
                          "unit": "GB/s", "frac": round(achieved / peaks["l2_line_gbps"], 4), "traffic": traffic,
+                         "frac_of_guide_l2": round(achieved / L2_GUIDE_GBPS, 4), "peak_guide_l2": L2_GUIDE_GBPS,
+                         "time_basis": "ms_per_step (the driver-timed wall time per frame); kernel_ms beside it",
                          "bound_note": "the walks gather 128-B lines of a ~5 MB cache-resident scene; the bytes the "
                                        "timed kernels fetch and move are priced against the MEASURED L2 bandwidth for "
                                        "full-line fetches (rt_measure_peaks l2_line_gbps: random lines of a table inside "
@@ -548,6 +633,7 @@ def main() -> int:
                          "alg_bytes_per_launch": int(alg_bytes), "launch_unit": "one frame (this rank's stripes)",
                          "alg_bytes_split": {"traversal": int(trav_bytes), "workspace": int(ws_bytes)},
                          "per_kernel": per_kernel,
+                         "per_kernel_one_frame": per_kernel_one,
                          "dominant": dominant,
                          "alg_bytes_per_kernel": {k: int(v) for k, v in kbytes.items()},
                          "hbm": {"bytes_per_frame": traffic, "gbps": round(traffic_gbps, 2) if traffic else None,

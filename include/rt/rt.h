@@ -33,7 +33,7 @@
 extern "C" {
 #endif
 
-#define RT_ABI_VERSION 10
+#define RT_ABI_VERSION 11
 
 typedef enum rt_status {
     RT_OK = 0,
@@ -84,14 +84,11 @@ typedef struct rt_scene_desc {
 } rt_scene_desc;
 
 #define RT_OPT_HOST_ONLY 1   /* load + BVH build only, no device upload (no GPU needed) */
-/* Render paths (all bit-identical; default = chain: closest-hit chains in one
- * kernel, shadow rays and shading deferred).  Env RT_PATH=chain|wave|mega
- * overrides at scene creation (also =fused). */
-#define RT_OPT_MEGAKERNEL 2  /* one kernel per frame, whole recursion per lane   */
-#define RT_OPT_WAVEFRONT 4   /* per-bounce queues, 3 kernels per recursion level */
-#define RT_OPT_CHAIN 8       /* chain kernel + deferred any-hit kernel + compose    */
-#define RT_OPT_FUSED 16      /* chains and shadow rays in one persistent kernel
-                                (per-wave task queues) + compose                  */
+/* The render path is the chain renderer (closest-hit chains, deferred any-hit
+ * shadow walks, shading + fold + SSAA in one pass).  Bits 2, 4 and 16 named the
+ * megakernel, wavefront and fused comparison paths up to ABI 10; they were
+ * bit-identical and slower, and are accepted and ignored since ABI 11. */
+#define RT_OPT_CHAIN 8       /* the chain path (the default; accepted for ABI <= 10 callers) */
 
 typedef struct rt_options {
     int device;       /* HIP device ordinal; -1 = current device            */

@@ -26,11 +26,8 @@ LIB_PATH = Path(os.environ["RT_LIB"]) if os.environ.get("RT_LIB") else PKG_DIR /
 CLI_PATH = PKG_DIR / "raytracer"
 
 RT_OPT_HOST_ONLY = 1
-RT_OPT_MEGAKERNEL = 2
-RT_OPT_WAVEFRONT = 4
 RT_OPT_CHAIN = 8
-RT_OPT_FUSED = 16
-PATHS = ("chain", "wavefront", "megakernel", "fused")
+PATHS = ("chain",)        # the one render path (rt.h: the comparison paths were removed in ABI 11)
 RT_RENDER_COUNT = 1
 
 
@@ -283,13 +280,11 @@ class Scene:
     @classmethod
     def from_xml(cls, path: str | os.PathLike, device: int = -1, host_only: bool = False,
                  render_path: str = "chain", build_threads: int = 0) -> "Scene":
-        """render_path: "chain", "fused", "wavefront", "megakernel" or "default" (the library's
-        default path); all are bit-identical.  build_threads: host BVH build threads (0: default,
-        1: serial); the tree does not depend on it."""
+        """render_path: "chain" or "default" (the same: the library has one render path).
+        build_threads: host BVH build threads (0: default, 1: serial); the tree does not depend on it."""
         h = ctypes.c_void_p()
         flags = RT_OPT_HOST_ONLY if host_only else 0
-        flags |= {"chain": RT_OPT_CHAIN, "wavefront": RT_OPT_WAVEFRONT, "megakernel": RT_OPT_MEGAKERNEL,
-                  "fused": RT_OPT_FUSED, "default": 0}[render_path]
+        flags |= {"chain": RT_OPT_CHAIN, "default": 0}[render_path]
         opts = Options(device, flags, build_threads)
         _check(lib().rt_scene_load_xml(str(path).encode(), ctypes.byref(opts), ctypes.byref(h)))
         return cls(h.value)
@@ -302,8 +297,7 @@ class Scene:
         desc, keep = make_desc(arrays)
         h = ctypes.c_void_p()
         flags = RT_OPT_HOST_ONLY if host_only else 0
-        flags |= {"chain": RT_OPT_CHAIN, "wavefront": RT_OPT_WAVEFRONT, "megakernel": RT_OPT_MEGAKERNEL,
-                  "fused": RT_OPT_FUSED, "default": 0}[render_path]
+        flags |= {"chain": RT_OPT_CHAIN, "default": 0}[render_path]
         opts = Options(device, flags, 0)
         _check(lib().rt_scene_create(ctypes.byref(desc), ctypes.byref(opts), ctypes.byref(h)))
         del keep

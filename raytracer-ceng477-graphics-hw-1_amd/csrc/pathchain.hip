@@ -188,27 +188,6 @@ __device__ __forceinline__ unsigned wave_grab_lds(unsigned* ctr, unsigned long l
     return __shfl(base, leader, 64);
 }
 
-// Block b's samples: units b, b+G, b+2G, ... of 256 consecutive slots.
-__device__ __forceinline__ unsigned block_samples(unsigned n0, unsigned G) {
-    const unsigned units = (n0 + 255u) / 256u;
-    if (blockIdx.x >= units) return 0;
-    const unsigned mine = (units - 1u - blockIdx.x) / G + 1u;
-    const unsigned last_unit = blockIdx.x + (mine - 1u) * G;
-    return (mine - 1u) * 256u + min(256u, n0 - last_unit * 256u);
-}
-// Within a full unit, `spread` > 1 interleaves its 4 tiles over consecutive
-// v (a wave takes 64/spread-sample strips of `spread` tiles), so one heavy
-// 8x8 tile is shared by several waves instead of serialising one.
-__device__ __forceinline__ unsigned block_sample(unsigned v, unsigned G, unsigned n0, unsigned spread) {
-    const unsigned unit = blockIdx.x + (v >> 8) * G;
-    unsigned u = v & 255u;
-    if (spread > 1u && (unit + 1u) * 256u <= n0) {
-        const unsigned grp = u / (64u * spread), j = u % (64u * spread);
-        u = (grp * spread + j % spread) * 64u + j / spread;
-    }
-    return unit * 256u + u;
-}
-
 // ---------------------------------------------------------------------------
 // Chain phases.  Phase A (k_chain) walks every sample's closest-hit chain up
 // to level `kinline`; a mirror bounce below it is handed on as a
@@ -226,8 +205,6 @@ __device__ __forceinline__ unsigned block_sample(unsigned v, unsigned G, unsigne
 __shared__ unsigned g_ccnt;    // block-local continuation count
 __shared__ unsigned g_uid[kDynUnits];   // dynamic phase-A units: the workgroup's k-th unit (kUidUnset: not yet taken)
 constexpr unsigned kUidUnset = ~0u, kUidNone = ~0u - 1u;
-// k_mix's early finish: how long a shadow-role workgroup waits for the others (wall_clock64 ticks, 100 MHz)
-constexpr unsigned long long kEarlyFinWait = 20000;
 
 struct PhaseOut {              // where a chain phase writes its tasks
     unsigned* sq;              // shadow tasks, region blk at sq + blk * scap
@@ -430,140 +407,6 @@ __device__ __forceinline__ Ray shadow_from_record(const rtk::DevScene& s, const 
     return shadow_ray(s, hitp, surface_normal(s, hitp, __float_as_int(a.w)), l, tlim);
 }
 
-// ---------------------------------------------------------------------------
-// Packet closest-hit walk: the wave walks ONE shared DFS; every node and
-// leaf fetch is wave-uniform (scalar loads), each lane keeps its own tMax and
-// best hit.  Exact when every active lane agrees on the near/far predicate
-// d[axis] > 0 for all three axes (caller checks): then the shared order IS
-// each lane's own order (raytracer.cpp:200-206), a lane is active exactly on
-// the nodes its own walk pops with a passing test (box hit at the parent,
-// bt <= its tMax at the pop, :184), in the same sequence, so its leaf tests
-// and updates (:210-222) happen in the same order.  Stack entries: node and
-// lane mask wave-uniform (LDS, per wave), each lane's deferred bt in its own
-// WalkStack slot.  8x8 tiles of eye rays agree almost everywhere and visit
-// ~1.2x the nodes of their average ray, so one uniform walk replaces 64
-// divergent ones.
-// ---------------------------------------------------------------------------
-#ifndef RT_PACKET_WALK
-#define RT_PACKET_WALK 0     // measured slower than per-lane walks on C3 (latency-bound); kept, exact
-#endif
-constexpr int kPktDepth = dl::kMaxStack;
-__shared__ int g_pnode[(kBlock / 64) * kPktDepth];
-__shared__ unsigned long long g_pmask[(kBlock / 64) * kPktDepth];
-
-__device__ __forceinline__ int uni(int v) { return __builtin_amdgcn_readfirstlane(v); }
-
-template <bool COUNT>
-__device__ HitRec packet_closest(const rtk::DevScene& s, const Ray& r, bool act, WalkStack& stk, Work& w) {
-    const int lane = lane_id();
-    const int base = uni((int)(threadIdx.x >> 6) * kPktDepth);
-    HitRec best{-1.0f, -1};
-    float tmax = FLT_MAX;
-    if (s.nnodes <= 0) return best;
-    const bool fast = __all(!act || ray_nan_free(r));
-    unsigned long long A;
-    {
-        float bt;
-        const float4 lo = make_float4(s.root_lo[0], s.root_lo[1], s.root_lo[2], 0.0f);
-        const float4 hi = make_float4(s.root_hi[0], s.root_hi[1], s.root_hi[2], 0.0f);
-        if (COUNT && act) w.nodes++;
-        A = __ballot(act && box_hit(r, lo, hi, &bt) && bt <= tmax);
-    }
-    int cur = s.root_info;
-    int sp = 0;
-    // near/far predicate of the (agreeing) active lanes, per axis
-    const int lead = __ffsll((unsigned long long)__ballot(act)) - 1;
-    const int sx = __shfl((int)(r.d.x > 0.0f), lead, 64), sy = __shfl((int)(r.d.y > 0.0f), lead, 64),
-              sz = __shfl((int)(r.d.z > 0.0f), lead, 64);
-    while (true) {
-        if (A) {
-            const bool in = (A >> lane) & 1ull;
-            if (cur >= 0) {
-                const float4* q = reinterpret_cast<const float4*>(&s.pairs[uni(cur)]);
-                const float4 l0 = q[0], l1 = q[1], r0 = q[2], r1 = q[3];
-                float tl, tr;
-                bool hl, hr;
-                if (fast) {
-                    hl = box_hit_fast(r, l0, l1, &tl);
-                    hr = box_hit_fast(r, r0, r1, &tr);
-                } else {
-                    hl = box_hit(r, l0, l1, &tl);
-                    hr = box_hit(r, r0, r1, &tr);
-                }
-                const int axis = __float_as_int(l1.w);
-                const bool left_first = (axis == 0 ? sx : (axis == 1 ? sy : sz)) != 0;
-                const bool hn = left_first ? hl : hr, hf = left_first ? hr : hl;
-                const float tn = left_first ? tl : tr, tf = left_first ? tr : tl;
-                const int in_ = left_first ? __float_as_int(l0.w) : __float_as_int(r0.w);
-                const int if_ = left_first ? __float_as_int(r0.w) : __float_as_int(l0.w);
-                if (COUNT && in) w.nodes += 2;
-                const unsigned long long mf = __ballot(in && hf);
-                if (mf) {
-                    stk.put(sp, make_int2(0, __float_as_int(tf)));
-                    if (lane == 0) {
-                        g_pnode[base + sp] = if_;
-                        g_pmask[base + sp] = mf;
-                    }
-                    ++sp;
-                }
-                A = __ballot(in && hn && tn <= tmax);
-                if (A) {
-                    cur = in_;
-                    continue;
-                }
-            } else {
-                int a, cnt;
-                leaf_range(s, cur, &a, &cnt);
-                a = uni(a);
-                cnt = uni(cnt);
-                for (int i = a; i < a + cnt; ++i) {
-                    const float4* pr = reinterpret_cast<const float4*>(&s.prims[i]);
-                    const float4 p0 = pr[0], p1 = pr[1];
-                    float t;
-                    bool h;
-                    if (__float_as_int(p0.w) >= 0) {
-                        if (COUNT && in) w.tris++;
-                        h = tri_hit(r, p0, p1, pr[2], &t);
-                    } else {
-                        if (COUNT && in) w.spheres++;
-                        h = sphere_hit(r, p0, p1, &t);
-                    }
-                    if (in && h && (t < best.t || best.t == -1.0f)) {
-                        best.t = t;
-                        best.prim = i;
-                        tmax = t;
-                    }
-                }
-                A = 0;
-            }
-        }
-        // pop until some lane's deferred test passes
-        if (sp == 0) break;
-        while (sp > 0) {
-            --sp;
-            const int2 e = stk.at(sp);
-            const int node = uni(g_pnode[base + sp]);
-            const unsigned long long m = g_pmask[base + sp];
-            A = __ballot(((m >> lane) & 1ull) && __int_as_float(e.y) <= tmax);
-            if (A) {
-                cur = node;
-                break;
-            }
-        }
-        if (!A) break;
-    }
-    return best;
-}
-
-// Do the active lanes agree on d[axis] > 0 for every axis (packet walk exact)?
-__device__ __forceinline__ bool packet_ok(const Ray& r, bool act) {
-    const unsigned long long m = __ballot(act);
-    if (!m) return false;
-    const unsigned long long bx = __ballot(act && r.d.x > 0.0f), by = __ballot(act && r.d.y > 0.0f),
-                             bz = __ballot(act && r.d.z > 0.0f);
-    return (bx == 0 || bx == m) && (by == 0 || by == m) && (bz == 0 || bz == m);
-}
-
 // Phase-B shadow tasks go to a workgroup queue in LDS (owner ids) while it has
 // room; the workgroup's waves whose chains are done walk them while the other
 // waves' long mirror chains still run, so those shadow rays no longer wait for
@@ -659,212 +502,6 @@ __device__ uint32_t bq_consume(const rtk::DevScene& s, const PcParams& p, WalkSt
     return n;
 }
 
-// ---------------------------------------------------------------------------
-// Cooperative tail walks (lone-frame phase B, p.coop).  Once a phase-B wave has no continuation left
-// to take and at most p.coop_live of its chains still walk, each walk runs on a GROUP of 8 lanes
-// (lanes 8g..8g+7): lane q tests slot q of the wide node (one slot's six planes instead of all 36),
-// a leaf record's primitives are tested one per lane, and the group's lanes agree through ballots.
-// The dependent-instruction chain of a wide step -- what sets the deep mirror chains' time when the
-// GPU is otherwise idle -- shrinks from ~250 to ~100 instructions.  The walk is the
-// same: the same slot order (each slot's rank in the reference's visiting order), the same pushes at
-// the same stack positions, the same pops, and the leaf's primitives folded in stored order with the
-// reference's update rule (raytracer.cpp:210-222), so the result is bit-identical.
-// The group keeps the walk's stack in its OWNER lane's LDS column, exactly where the owner's own
-// walk keeps it, so a walk moves between the owner (per-lane steps) and a group at any step with
-// only its registers: a group takes a walk whose stack is all in LDS (sp <= kLds) and hands it back
-// unchanged (before the step) when a step would push past the LDS entries (the deeper ones live in
-// the owner's private scratch).
-// ---------------------------------------------------------------------------
-#ifndef RT_COOP_BUILD
-#define RT_COOP_BUILD 0      // 1: k_mix with the cooperative tail walks (measured slower; off)
-#endif
-struct CoopW {              // a group's walk (the same in its 8 lanes); its ray is in g_cray
-    int cur, sp, steps;
-    int owner;              // lane whose walk this is, or -1 (group free)
-    float tmax;
-    HitRec best;
-};
-__shared__ float g_cray[kBlock / 8][9];    // per group (wave * 8 + group): ray o, d, inv
-
-__device__ __forceinline__ Ray coop_ray() {
-    const float* a = g_cray[threadIdx.x >> 3];
-    Ray r;
-    r.o = V{a[0], a[1], a[2]};
-    r.d = V{a[3], a[4], a[5]};
-    r.inv = V{a[6], a[7], a[8]};
-    return r;
-}
-
-// One step of group walk c (every lane of the group calls it with the same c): 0 = continues,
-// 1 = finished (result in c.best), 2 = not taken: the step would push past the owner's LDS
-// entries, c unchanged (the owner walks on with its own stack).
-__device__ __forceinline__ int coop_step(const rtk::DevScene& s, CoopW& c) {
-    constexpr int W = dl::kWideSlots;
-    const int lane = lane_id(), q = lane & 7, gbase = lane & 56;
-    const int col = (int)(threadIdx.x & ~63u) + c.owner;       // the owner's LDS stack column
-    if (c.steps >= s.walk_cap) {                                // walk_runaway
-        __hip_atomic_fetch_or(s.err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        return 1;
-    }
-    if (c.cur >= 0) {
-        // lane q reads only what slot q needs from the node's line: the header, its six plane words,
-        // its child code and the rank word (one line per group per load instruction)
-        const uint32_t* N = reinterpret_cast<const uint32_t*>(&s.wnodes[c.cur]);
-        const Ray cr = coop_ray();
-        const int sgn = (cr.d.x > 0.0f ? 1 : 0) | (cr.d.y > 0.0f ? 2 : 0) | (cr.d.z > 0.0f ? 4 : 0);   // walk_begin's
-        const int ridx = (sgn & 4) ? (sgn ^ 7) : sgn;
-        const int qs = q < W ? q : W - 1, pr = qs >> 1;
-        const float4 hd = *reinterpret_cast<const float4*>(N);
-        uint32_t pl[6];
-#pragma unroll
-        for (int a = 0; a < 3; ++a) {
-            pl[a] = N[4 + a * 3 + pr];
-            pl[3 + a] = N[13 + a * 3 + pr];
-        }
-        const int code_q = (int)N[22 + qs];
-        uint32_t rw = N[28 + ridx];
-        const uint32_t ex = __float_as_uint(hd.w);
-        if (sgn & 4) rw = (uint32_t)(__builtin_popcount(ex >> 24) - 1) * 0111111u - rw;
-        // slot q's box (wide_slabs for one slot: the same operations on the same words)
-        const float org[3] = {hd.x, hd.y, hd.z};
-        const float ro[3] = {cr.o.x, cr.o.y, cr.o.z}, ri[3] = {cr.inv.x, cr.inv.y, cr.inv.z};
-        const uint32_t hs = (uint32_t)(q & 1) << 4;
-        float tmn = 0.0f, tmx = 0.0f;
-#pragma unroll
-        for (int a = 0; a < 3; ++a) {
-            const float sc = __uint_as_float(((ex >> (8 * a)) & 255u) << 23);
-            const bool neg = __float_as_int(ri[a]) < 0;
-            const float si = sc * ri[a];
-            const float z = org[a] - ro[a];
-            const float oi = z * ri[a];
-            const float cc = __builtin_fmaf(sc, 0x1p-5f, __builtin_fabsf(org[a]) * 0x1p-23f);
-            const float m = __builtin_fmaf(__builtin_fabsf(z), 6.0f * 0x1p-23f, cc);
-            const float M = __builtin_fmaf(m, __builtin_fabsf(ri[a]), 0x1p-126f);
-            const uint32_t lw = pl[a] >> hs, hw = pl[3 + a] >> hs;
-            const uint32_t nw = neg ? hw : lw, fw = neg ? lw : hw;
-            const float tn = fma_mix_h<0>(nw, si, oi - M), tf = fma_mix_h<0>(fw, si, oi + M);
-            tmn = a == 0 ? tn : __builtin_fmaxf(tmn, tn);
-            tmx = a == 0 ? tf : __builtin_fminf(tmx, tf);
-        }
-        const bool valid = q < W && tmx >= __builtin_fmaxf(0.0f, tmn) && tmn <= c.tmax;
-        const uint32_t m6 = (uint32_t)(__ballot(valid) >> gbase) & 63u;
-        uint32_t vm = 0;                                          // valid slots in rank order
-#pragma unroll
-        for (int j = 0; j < W; ++j) vm |= ((m6 >> j) & 1u) << ((rw >> (3 * j)) & 7u);
-        if (vm) {
-            const int np = __builtin_popcount(vm) - 1;
-            if (c.sp + np > StackLds::kLds) return 2;             // deeper entries: the owner's scratch
-            const uint32_t first = (uint32_t)__builtin_ctz(vm);
-            const uint32_t rq = (rw >> (3 * q)) & 7u;
-            const bool isfirst = valid && rq == first;
-            const int cf = __builtin_ctz((uint32_t)(__ballot(isfirst) >> gbase) & 63u);
-            if (valid && !isfirst)                                // the same entry at the same position
-                g_lstk[(c.sp + __builtin_popcount(vm >> (rq + 1u))) * kBlock + col] =
-                    make_int2(code_q, __float_as_int(tmn));
-            c.sp += np;
-            c.cur = __shfl(code_q, gbase + cf, 64);
-            ++c.steps;
-            return 0;
-        }
-    } else {
-        const float4* L = s.lrec + (c.cur & ~dl::kLeafBit);
-        const float4 h0 = L[0], h1 = L[1];
-        const Ray r = coop_ray();
-        float lt;
-        if (box_hit_fast(r, h0, h1, &lt) && lt <= c.tmax) {      // the reference leaf's exact box (:184)
-            const int cnt = __float_as_int(h0.w), slot0 = __float_as_int(h1.w);
-            for (int b0 = 0; b0 < cnt; b0 += 8) {
-                const int j = b0 + q;
-                bool h = false;
-                float t = 0.0f;
-                if (j < cnt) {
-                    const float4 p0 = L[2 + 3 * j], p1 = L[3 + 3 * j], p2 = L[4 + 3 * j];
-                    h = __float_as_int(p0.w) >= 0 ? tri_hit(r, p0, p1, p2, &t) : sphere_hit(r, p0, p1, &t);
-                }
-                // the hits in stored order, with the reference's update rule (:213-221)
-                uint32_t hm = (uint32_t)(__ballot(h) >> gbase) & 255u;
-                while (hm) {
-                    const int jj = __builtin_ctz(hm);
-                    hm &= hm - 1u;
-                    const float tj = __shfl(t, gbase + jj, 64);
-                    if (tj < c.best.t || c.best.t == -1.0f) {
-                        c.best.t = tj;
-                        c.best.prim = slot0 + b0 + jj;
-                        c.tmax = tj;
-                    }
-                }
-            }
-        }
-    }
-    ++c.steps;
-    while (c.sp > 0) {
-        --c.sp;
-        const int2 e = g_lstk[c.sp * kBlock + col];
-        if (__int_as_float(e.y) <= c.tmax) {
-            c.cur = e.x;
-            return 0;
-        }
-    }
-    return 1;
-}
-
-// A wave in coop mode: free groups take the walks of candidate lanes (their stacks all in LDS),
-// every group steps its walk, and finished or handed-back walks return to their owners.
-// st: the owner's lane state (kCoop while a group has its walk); cg: the leader lane of that group.
-constexpr int kCoop = 3;
-[[maybe_unused]] __device__ __forceinline__ void coop_round(const rtk::DevScene& s, CoopW& c, int& st, int& cg, bool& coop_ok,
-                                           const Ray& r, Walk& wk) {
-    const int lane = lane_id();
-    // (1) assign: the i-th candidate walk to the i-th free group
-    unsigned long long cand = __ballot(st == kTrav && coop_ok && wk.sp <= StackLds::kLds);
-    unsigned long long freeg = __ballot(c.owner < 0 && (lane & 7) == 0);
-    unsigned long long fresh = 0;     // leader lanes of groups that took a walk now
-    while (cand && freeg) {
-        const int o = __builtin_ctzll(cand), gl = __builtin_ctzll(freeg);
-        cand &= cand - 1ull;
-        freeg &= freeg - 1ull;
-        fresh |= 1ull << gl;
-        if ((lane & 56) == gl) c.owner = o;
-        if (lane == o) { st = kCoop; cg = gl; }
-    }
-    if (fresh) {
-        if (st == kCoop && ((fresh >> cg) & 1ull)) {     // the owner puts its ray where its group reads it
-            float* a = g_cray[((threadIdx.x & ~63u) + (unsigned)cg) >> 3];
-            a[0] = r.o.x; a[1] = r.o.y; a[2] = r.o.z;
-            a[3] = r.d.x; a[4] = r.d.y; a[5] = r.d.z;
-            a[6] = r.inv.x; a[7] = r.inv.y; a[8] = r.inv.z;
-        }
-        __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");   // the owners' LDS words, seen by their groups
-        const int src = c.owner >= 0 ? c.owner : lane;
-        const bool f = (fresh >> (lane & 56)) & 1ull;
-        auto take = [&](auto& dst, auto v) { const auto x = __shfl(v, src, 64); if (f) dst = x; };
-        take(c.cur, wk.cur); take(c.sp, wk.sp); take(c.steps, wk.steps);
-        take(c.tmax, wk.tmax); take(c.best.t, wk.best.t); take(c.best.prim, wk.best.prim);
-    }
-    // (2) step every group's walk (a walk not taken, 2, stays as it was: the owner redoes the step)
-    const int res = c.owner >= 0 ? coop_step(s, c) : 0;
-    __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");   // the groups' stack writes, seen by their owners
-    // (3) finished (1) or handed back (2): the walk's registers return to its owner lane
-    const unsigned long long ended = __ballot(res != 0 && (lane & 7) == 0);
-    if (ended) {
-        const int src = st == kCoop ? cg : lane;
-        const bool mine = st == kCoop && ((ended >> cg) & 1ull);
-        auto give = [&](auto& dst, auto v) { const auto x = __shfl(v, src, 64); if (mine) dst = x; };
-        const int rs = __shfl(res, src, 64);
-        give(wk.cur, c.cur); give(wk.sp, c.sp); give(wk.steps, c.steps);
-        give(wk.tmax, c.tmax); give(wk.best.t, c.best.t); give(wk.best.prim, c.best.prim);
-        if (mine) {
-            if (rs == 1) {
-                st = kDone;
-            } else {
-                st = kTrav;           // per-lane from here (this walk's stack grows into scratch)
-                coop_ok = false;
-            }
-        }
-        if ((ended >> (lane & 56)) & 1ull) c.owner = -1;
-    }
-}
-
 // The u-th unit taken -> the unit id.  The slab's rows of units (tiles_x / 4 units each) are cut
 // into super-rows of ublk_h tile rows (< 0: one frame of the batch), each walked in column blocks
 // ublk_w units wide, so the units in flight (a launch-wide counter: the whole GPU on them at once)
@@ -906,17 +543,8 @@ __device__ void chain_body(const rtk::DevScene& s, const rtk::Eye& e, const PcPa
     Ray r;
     Walk wk;
     unsigned t_grab = 0, tsteps = 0, twit = 0, wit = 0;   // trace: grab time, own steps, wave steps
-    unsigned apoll = 0;      // phase A: iterations since the last look at the finished-wave count (p.abandon)
     unsigned ssteps = 0;     // phase A (p.urank): walk steps of the lane's current sample
-    bool fresh = false;      // lane just took an eye ray (packet walk pending)
     StepStat stat;
-    // cooperative tail walks (lone-frame phase B: coop_round): the group walk this lane works on, the
-    // leader lane of the group walking this lane's own walk, and whether that walk may go to a group
-    constexpr bool COOPK = RT_COOP_BUILD && CONT && BQ && !COUNT;
-    CoopW cw;
-    cw.owner = -1;
-    int cg = 0;
-    bool coop_ok = true;
     while (true) {
         // (1) epilogue of finished walks: record, queue shadow tasks, reflect or hand on
         if (st == kDone) {
@@ -992,8 +620,8 @@ __device__ void chain_body(const rtk::DevScene& s, const rtk::Eye& e, const PcPa
             if (ends || handoff) {
                 st = kIdle;
                 if (!CONT && !COUNT && p.urank && ssteps >= kHotSteps[1]) atomicMax(&p.ucost[path >> 8], ssteps);
-                if (p.trace && !CONT) { p.trace[2 * path] = t_grab; p.trace[2 * path + 1] = (unsigned)wall_clock64(); }
-                if (p.trace && CONT) {       // phase B: {grab, end, last level, walk steps} after A's entries
+                if (kTraceBuild && p.trace && !CONT) { p.trace[2 * path] = t_grab; p.trace[2 * path + 1] = (unsigned)wall_clock64(); }
+                if (kTraceBuild && p.trace && CONT) {       // phase B: {grab, end, last level, walk steps} after A's entries
                     unsigned* tb = p.trace + 2 * ((size_t)p.cap + p.trace_blocks) + 4 * (size_t)path;
                     tb[0] = t_grab; tb[1] = (unsigned)wall_clock64(); tb[2] = (unsigned)k | ((wit - twit) << 8); tb[3] = tsteps;
                 }
@@ -1004,12 +632,11 @@ __device__ void chain_body(const rtk::DevScene& s, const rtk::Eye& e, const PcPa
                 nrefl++;
                 if (!COUNT && defer_closest(s, r)) {     // the rest of this path: k_fallback
                     if (lvp < p.dbase) p.tail[path] = make_float4(dk.x, dk.y, dk.z, 0.0f);   // reflect_from_record
-                    if (!CONT) p.pinfo[path] = kPathCont;   // not finished before k_fallback (early_finish)
+                    if (!CONT) p.pinfo[path] = kPathCont;   // (k_fallback's path)
                     fb_chain(p, (unsigned)lvp);
                     st = kIdle;
                 } else {
                     st = walk_begin<COUNT>(s, r, wk, w) ? kTrav : kDone;
-                    coop_ok = true;
                 }
             }
         }
@@ -1054,34 +681,26 @@ __device__ void chain_body(const rtk::DevScene& s, const rtk::Eye& e, const PcPa
                             const unsigned j = chunk_task(v, G, blk, (unsigned)p.tchunk);
                             const unsigned lvp = p.cflat[j];
                             cix = j;
-                            if (p.trace) { t_grab = (unsigned)wall_clock64(); tsteps = 0; twit = wit; }
-                            // a walk phase A gave up on (p.abandon: lone frames only, so only the BQ kernel has them)
-                            const bool eye = BQ && (lvp & kFbEye) != 0;
-                            path = eye ? lvp & ~kFbEye : lvp % (unsigned)p.cap;
-                            k = eye ? 0 : (int)(lvp / (unsigned)p.cap) + 1;
-                            if (eye) {
-                                slab_sample_ray(p, path, &r);
-                            } else {
-                                r = reflect_from_record(s, p, lvp, path);
-                                nrefl++;
-                            }
-                            if (!COUNT && defer_closest(s, r)) fb_chain(p, lvp);   // (an eye entry keeps its kFbEye bit)
+                            if (kTraceBuild && p.trace) { t_grab = (unsigned)wall_clock64(); tsteps = 0; twit = wit; }
+                            path = lvp % (unsigned)p.cap;
+                            k = (int)(lvp / (unsigned)p.cap) + 1;
+                            r = reflect_from_record(s, p, lvp, path);
+                            nrefl++;
+                            if (!COUNT && defer_closest(s, r)) fb_chain(p, lvp);
                             else st = walk_begin<COUNT>(s, r, wk, w) ? kTrav : kDone;
-                            coop_ok = true;
                         } else {
                             const unsigned idx = (dyn ? uid : blk + (v >> 8) * G) * 256u + (v & 255u);
                             if (slab_sample_ray(p, idx, &r)) {
                                 path = idx;
                                 k = 0;
                                 ssteps = 0;
-                                if (p.trace) t_grab = (unsigned)wall_clock64();
+                                if (kTraceBuild && p.trace) t_grab = (unsigned)wall_clock64();
                                 nprim++;
                                 if (s.max_depth < 0) p.pinfo[path] = 0 | (kEndZero << 8);   // depth 0 > max: black
                                 else if (!COUNT && defer_closest(s, r)) {
-                                    p.pinfo[path] = kPathCont;   // (early_finish: k_fallback's)
+                                    p.pinfo[path] = kPathCont;   // (k_fallback's path)
                                     fb_chain(p, kFbEye | path);
                                 }
-                                else if (RT_PACKET_WALK && p.packet) fresh = true;
                                 else st = walk_begin<COUNT>(s, r, wk, w) ? kTrav : kDone;
                             }
                         }
@@ -1089,77 +708,26 @@ __device__ void chain_body(const rtk::DevScene& s, const rtk::Eye& e, const PcPa
                 }
             }
         }
-        if (RT_PACKET_WALK && !CONT && p.packet && __any(fresh)) {
-            // fresh eye rays of this wave (a tile): one packet walk when they agree on the
-            // near/far predicates and no other lane of the wave has entries on its stack
-            if (packet_ok(r, fresh) && __all(st != kTrav || wk.sp == 0)) {
-                const HitRec h = packet_closest<COUNT>(s, r, fresh, stk, w);
-                if (fresh) {
-                    wk.best = h;
-                    st = kDone;
-                }
-            } else if (fresh) {
-                st = walk_begin<COUNT>(s, r, wk, w) ? kTrav : kDone;
-            }
-            fresh = false;
-        }
         if (!__any(st != kIdle)) {
             if (exhausted) break;
             continue;
         }
         // (3) walk until enough lanes need service
         const int thresh = exhausted ? 0 : (CONT ? p.brefill : p.refill);
-        bool abandon = false;
         while (true) {
-            if constexpr (!CONT && !COUNT) {
-                // phase A's stragglers: once nearly every k_chain wave has finished, a wave with no unit left
-                // hands its unfinished walks to phase B (wave-uniform test, every 32 iterations)
-                if (exhausted && p.abandon && (++apoll & 31u) == 0u) {
-                    unsigned done = 0;
-                    if (lane_id() == 0) done = __hip_atomic_load(&p.totals[7], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                    if (__shfl(done, 0, 64) >= p.abandon) { abandon = true; break; }
-                }
-            }
-            const int nt = __popcll(__ballot(st == kTrav || (COOPK && st == kCoop)));
-            const bool tail = COOPK && p.coop && exhausted && nt <= p.coop_live;
-            if (nt <= thresh ||
-                __popcll(__ballot(st == kDone)) >= (tail ? p.coop_tail : CONT ? (exhausted ? p.btail : p.bservice) : p.service))
+            if (__popcll(__ballot(st == kTrav)) <= thresh ||
+                __popcll(__ballot(st == kDone)) >= (CONT ? (exhausted ? p.btail : p.bservice) : p.service))
                 break;
-            if constexpr (COOPK) {
-                if (tail) {          // the wave's last chains: each walk on a group of 8 lanes
-                    if (p.trace) { ++wit; tsteps |= 1u << 31; }      // trace: coop rounds count as wave iterations
-                    coop_round(s, cw, st, cg, coop_ok, r, wk);
-                    if (__any(st == kTrav))      // walks whose stacks reach into scratch: per lane
-                        if (st == kTrav && (closest_step_timed<COUNT, CONT>(s, r, stk, wk, w) || walk_runaway(s, wk)))
-                            st = kDone;
-                    continue;
-                }
-            }
             stat.step(st == kTrav, wk.cur >= 0, RT_STEP_STATS && st == kTrav && wk.tree == nullptr && leaf_postponed(s.leaf_wait, wk));
-            if (CONT && p.trace) ++wit;
+            if (kTraceBuild && CONT && p.trace) ++wit;
             if (st == kTrav) {
-                if (CONT && p.trace) ++tsteps;
+                if (kTraceBuild && CONT && p.trace) ++tsteps;
                 if (!CONT) ++ssteps;
                 if (closest_step_timed<COUNT, CONT>(s, r, stk, wk, w) || walk_runaway(s, wk)) st = kDone;
             }
         }
-        if constexpr (!CONT && !COUNT) {
-            if (abandon) {   // every unfinished walk restarts in phase B: the eye ray, or the reflection of its last record
-                const bool h = st == kTrav;
-                const unsigned long long cm = __ballot(h);
-                const unsigned base = cm ? wave_grab_lds(&g_ccnt, cm) : 0u;
-                if (h) {
-                    const unsigned entry = k == 0 ? (kFbEye | path) : (unsigned)((size_t)(k - 1) * p.cap + path);
-                    o.cq[(size_t)blk * o.ccap + base + lane_rank(cm)] = entry;
-                    p.pinfo[path] = kPathCont;
-                    st = kIdle;
-                }
-                // walks already done are serviced as usual (the loop's next pass); then the wave has nothing left
-            }
-        }
     }
     stat.flush(CONT ? 1 : 0);
-    if (!CONT && !COUNT && p.abandon && lane_id() == 0) atomicAdd(&p.totals[7], 1u);   // this wave is done
     uint32_t nshadow = 0;
     if (COUNT) {
         wave_add_counter(&p.counters[CONT ? kCntBWalkBytes : kCntAWalkBytes], w.nodes);
@@ -1201,7 +769,7 @@ __device__ void occlude_body(const rtk::DevScene& s, const PcParams& p, unsigned
     WalkStack stk;
     Work w;
     uint32_t nrays = 0;
-    const unsigned t_start = p.trace ? (unsigned)wall_clock64() : 0u;
+    const unsigned t_start = kTraceBuild && p.trace ? (unsigned)wall_clock64() : 0u;
     const unsigned n = chunk_count(total, G, blk, (unsigned)p.ochunk);
     bool active = false, exhausted = n == 0;
     Ray r;
@@ -1247,7 +815,7 @@ __device__ void occlude_body(const rtk::DevScene& s, const PcParams& p, unsigned
         }
     }
     stat.flush(2);
-    if (p.trace && threadIdx.x == 0 && blk < (unsigned)p.ogrid) {
+    if (kTraceBuild && p.trace && threadIdx.x == 0 && blk < (unsigned)p.ogrid) {
         p.trace[2 * ((size_t)p.cap + blk)] = t_start;
         p.trace[2 * ((size_t)p.cap + blk) + 1] = (unsigned)wall_clock64();
     }
@@ -1276,9 +844,6 @@ __device__ void occlude_body(const rtk::DevScene& s, const PcParams& p, unsigned
 // LDS: the walk-stack array g_lstk, re-cut as ints (this role has no closest-hit walks): per lane
 // kOStk stack entries + one sink entry, per wave a kLq-entry queue, per lane its queued count.
 // ---------------------------------------------------------------------------
-#ifndef RT_LEAF_QUEUE
-#define RT_LEAF_QUEUE 1
-#endif
 constexpr int kOStk = 22;                 // LDS stack entries per lane (deeper ones in scratch)
 constexpr int kLq = 128;                  // queued leaf records per wave (tested 64 at a time)
 constexpr int kLqSrcShift = 25;           // queue entry: leaf-record offset | owner lane << 25
@@ -1622,12 +1187,6 @@ __device__ __forceinline__ void occlude_regions(const rtk::DevScene& s, const Pc
     }
 }
 
-// Early finish (PcParams::early_fin, lone frames): pixels without a continued sample, taken 64 at a time
-// from the stripes' counters (defined with k_finish; k_finish takes what is left)
-__shared__ unsigned g_efin;
-template <bool LDS, bool CMP>
-__device__ void finish_taken(const rtk::DevScene& s, const rtk::Eye& e, const PcParams& p, unsigned stop_at);
-
 template <bool COUNT, bool BQ>
 __global__ __launch_bounds__(kBlock, BQ || COUNT ? RT_MIX_WAVES : RT_MIX_NOBQ_WAVES) void k_mix(rtk::DevScene s,
                                                                                                   rtk::Eye e, PcParams p) {
@@ -1638,58 +1197,15 @@ __global__ __launch_bounds__(kBlock, BQ || COUNT ? RT_MIX_WAVES : RT_MIX_NOBQ_WA
     if (chain) {
         if (p.bprio) __builtin_amdgcn_s_setprio(3);    // the deep chains are the frame's critical path
         chain_body<COUNT, true, BQ>(s, e, p, blockIdx.x, (unsigned)p.gb, phase_b(p));
-        if (!COUNT && BQ && RT_EARLY_FIN_BUILD && p.early_fin && lane_id() == 0)
-            atomicAdd(&p.totals[10], 1u);          // this chain wave is done (early finish)
-    }
-    else if (!p.exp_skip_occ) {
-        // (a lone frame with p.occ_inplace, RT_OCC_INPLACE=2: A's tasks where k_chain left them, region
-        // by region, k_pack_a copying none -- measured slower: the uneven regions cost k_mix 60 us)
-        if constexpr (!COUNT && RT_LEAF_QUEUE) {
-            if (p.occ_inplace) occlude_regions(s, p, 0, blockIdx.x - p.gb, gridDim.x - p.gb);
-            else occlude_queue_body(s, p, blockIdx.x - p.gb, gridDim.x - p.gb, p.sflatA, p.totals[0]);
-        } else
+    } else {
+        if constexpr (!COUNT && RT_LEAF_QUEUE)
+            occlude_queue_body(s, p, blockIdx.x - p.gb, gridDim.x - p.gb, p.sflatA, p.totals[0]);
+        else
             occlude_body<COUNT>(s, p, blockIdx.x - p.gb, gridDim.x - p.gb, p.sflatA, p.totals[0], 0);
-    }
-    const bool ranker = !COUNT && !chain && p.urank && blockIdx.x == gridDim.x - 1;
-    if constexpr (!COUNT && BQ && RT_EARLY_FIN_BUILD) {
-        if (!chain && p.early_fin) {
-            // A lone frame's pixels without a continued sample: their records and A's occlusion bytes are
-            // final once every shadow-role workgroup has walked its tasks, so these workgroups shade and
-            // fold them beside phase B's deep chains instead of k_finish after them.  The wait for the
-            // other workgroups is bounded (kEarlyFinWait, no error: k_finish then takes their share), and
-            // pixels are taken only while phase B still runs (totals[10]), so the launch is no longer.
-            const unsigned nshadow = gridDim.x - (unsigned)p.gb, nchain = (unsigned)p.gb * (kBlock / 64);
-            __syncthreads();                        // every wave of this workgroup is done with its tasks
-            if (threadIdx.x == 0) {
-                __threadfence();                    // (release) this workgroup's occlusion bytes
-                atomicAdd(&p.totals[8], 1u);
-            }
-            if (ranker) rank_units(p);              // (after the arrival: no other workgroup waits for it)
-            if (threadIdx.x == 0) {
-                const unsigned long long t0 = wall_clock64();
-                unsigned ok = 0;
-                while (true) {
-                    if (__hip_atomic_load(&p.totals[8], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= nshadow) {
-                        ok = 1;
-                        break;
-                    }
-                    if (__hip_atomic_load(&p.totals[10], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= nchain ||
-                        wall_clock64() - t0 > (p.early_fin > 1 ? 0ull : kEarlyFinWait))
-                        break;
-                    __builtin_amdgcn_s_sleep(127);   // (~3 us: few polls of the two words)
-                }
-                g_efin = ok;
-            }
-            __syncthreads();
-            if (!g_efin) return;
-            __threadfence();                        // (acquire) the other workgroups' occlusion bytes
-            finish_taken<false, false>(s, e, p, nchain);
-            return;
-        }
     }
     // a lone frame's next unit order, by the last shadow-role workgroup once its shadow rays are done:
     // beside phase B's deep chains, off the frame's critical path (in k_pack_a it cost 30 us there)
-    if (ranker) rank_units(p);
+    if (!COUNT && !chain && p.urank && blockIdx.x == gridDim.x - 1) rank_units(p);
 }
 
 // Phase B's shadow tasks (which = 1), or phase A's (which = 0: p.split_occ, frame batches).
@@ -1711,221 +1227,6 @@ __global__ __launch_bounds__(kBlock, RT_OCC_WAVES_PER_EU) void k_occlude(rtk::De
     } else {
         if (which) occlude_body<COUNT>(s, p, blockIdx.x, gridDim.x, p.sflatB, p.totals[2], 1);
         else occlude_body<COUNT>(s, p, blockIdx.x, gridDim.x, p.sflatA, p.totals[0], 0);
-    }
-}
-
-// ---------------------------------------------------------------------------
-// k_fused: chains and shadow rays in ONE persistent kernel, by wave role.
-// Waves [0, P) of a workgroup are producers: exactly k_chain's loop (closest-
-// hit chains, uninterrupted by shadow work), except that each finished hit
-// appends one u32 task per light (owner id) to the wave's own queue and
-// publishes the new tail with a workgroup-scope release.  The other waves are
-// consumers from the start, and producers turn into consumers once the
-// workgroup's samples are gone: they take published tasks from any producer
-// queue (LDS CAS on the taken count), re-derive the shadow ray from the hit
-// record and walk it (any-hit).  Shadow work thus overlaps the chains instead
-// of waiting for the slowest chain of the frame (k_chain -> k_occlude).
-// Queue capacity is the worst case (every sample of the workgroup recording
-// every level), so no queue can overflow.
-// ---------------------------------------------------------------------------
-__shared__ unsigned g_pub[kBlock / 64];    // per producer wave: tasks published
-__shared__ unsigned g_take[kBlock / 64];   // per producer wave: tasks taken
-__shared__ unsigned g_live;                // producer waves still producing
-
-__device__ __forceinline__ unsigned lds_acquire(unsigned* p) {
-    return __hip_atomic_load(p, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP);
-}
-__device__ __forceinline__ void lds_release(unsigned* p, unsigned v) {
-    __hip_atomic_store(p, v, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
-}
-
-template <bool COUNT>
-__global__ __launch_bounds__(kBlock, RT_WAVES_PER_EU) void k_fused(rtk::DevScene s, rtk::Eye e, PcParams p) {
-    const int wave = (int)(threadIdx.x >> 6), lane = (int)(threadIdx.x & 63);
-    const int P = p.producers;
-    if (threadIdx.x < kBlock / 64) {
-        g_pub[threadIdx.x] = 0;
-        g_take[threadIdx.x] = 0;
-    }
-    if (threadIdx.x == 0) g_live = (unsigned)P;
-    block_init(s);
-    WalkStack stk;
-    Work w;
-    uint32_t nprim = 0, nrefl = 0, nshadow = 0;
-    const int nl = s.nlights;
-    unsigned* const qbase = p.wq + (size_t)blockIdx.x * (kBlock / 64) * p.wq_cap;
-    Ray r;
-    Walk wk;
-    if (wave < P) {
-        // ---- producer: k_chain's loop ----
-        const unsigned G = gridDim.x;
-        const unsigned nb = block_samples((unsigned)p.n0, G);
-        unsigned* q = qbase + (size_t)wave * p.wq_cap;
-        unsigned pub = 0;                                   // wave-uniform
-        int st = kIdle;
-        bool exhausted = nb == 0;
-        unsigned path = 0;
-        int k = 0;
-        unsigned t_grab = 0;
-        while (true) {
-            const bool done = st == kDone;
-            const bool hit = done && wk.best.prim >= 0;
-            const unsigned long long hm = __ballot(hit);
-            const unsigned hcnt = (unsigned)__popcll(hm);
-            const unsigned base = pub;
-            pub += hcnt * (unsigned)nl;
-            if (done) {
-                const HitRec h = wk.best;
-                V nn{0.0f, 0.0f, 0.0f}, pnt{0.0f, 0.0f, 0.0f};
-                int mat = 0, code = 0;
-                if (hit) {
-                    hit_surface(s, r, h, &nn, &mat, &code);
-                    const V hitp = add(r.o, mul(r.d, h.t));
-                    rec_write(p, (size_t)k * p.cap + path, hitp, code, r.d, mat);
-                    pnt = add(hitp, mul(nn, s.eps));                              // :397
-                    const unsigned rank = lane_rank(hm);
-                    const unsigned own0 = (unsigned)(((size_t)k * p.cap + path) * nl);
-                    for (int l = 0; l < nl; ++l) q[base + (unsigned)l * hcnt + rank] = own0 + (unsigned)l;
-                }
-                if (!hit) {                                                       // :442-449
-                    p.pinfo[path] = k | ((k == 0 ? kEndBg : kEndZero) << 8);
-                    st = kIdle;
-                } else if (!s.mats[mat - 1].is_mirror) {
-                    p.pinfo[path] = (k + 1) | (kEndLast << 8);
-                    st = kIdle;
-                } else if (k >= s.max_depth) {      // child beyond MaxRecursionDepth: 0 (:387-389)
-                    p.pinfo[path] = (k + 1) | (kEndZero << 8);
-                    st = kIdle;
-                } else {
-                    const V d2 = nrm(r.d);                                       // :431-435
-                    const V n2 = nrm(nn);
-                    const float rcos = dot(neg(d2), n2);
-                    r = make_ray(pnt, add(d2, mul(mul(n2, 2.0f), rcos)));
-                    ++k;
-                    nrefl++;
-                    st = walk_begin<COUNT>(s, r, wk, w) ? kTrav : kDone;
-                }
-                if (p.trace && st == kIdle) {
-                    p.trace[2 * path] = t_grab;
-                    p.trace[2 * path + 1] = (unsigned)wall_clock64();
-                }
-            }
-            if (hcnt && lane == 0) lds_release(&g_pub[wave], pub);   // records + tasks before the tail
-            if (!exhausted) {
-                const unsigned long long idle = __ballot(st == kIdle);
-                if (idle) {
-                    const unsigned gb = wave_grab_lds(&g_head, idle);
-                    if (gb + (unsigned)__popcll(idle) >= nb) exhausted = true;
-                    if (st == kIdle) {
-                        const unsigned v = gb + lane_rank(idle);
-                        if (v < nb) {
-                            const unsigned idx = block_sample(v, G, (unsigned)p.n0, (unsigned)p.spread);
-                            if (slab_sample_ray(p, idx, &r)) {
-                                path = idx;
-                                k = 0;
-                                nprim++;
-                                if (p.trace) t_grab = (unsigned)wall_clock64();
-                                if (s.max_depth < 0) p.pinfo[path] = 0 | (kEndZero << 8);   // depth 0 > max: black
-                                else st = walk_begin<COUNT>(s, r, wk, w) ? kTrav : kDone;
-                            }
-                        }
-                    }
-                }
-            }
-            if (!__any(st != kIdle)) {
-                if (exhausted) break;
-                continue;
-            }
-            const int thresh = exhausted ? 0 : p.refill;
-            while (__popcll(__ballot(st == kTrav)) > thresh && __popcll(__ballot(st == kDone)) < p.service) {
-                if (st == kTrav && (closest_step<COUNT, FetchTop>(s, r, stk, wk, w) || walk_runaway(s, wk))) st = kDone;
-            }
-        }
-        if (lane == 0) __hip_atomic_fetch_add(&g_live, -1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
-    }
-    // ---- consumer: shadow tasks from every producer queue ----
-    {
-        bool active = false;
-        float tlim = 0.0f;
-        unsigned owner = 0;
-        unsigned spin = 0;   // consecutive waits with nothing taken (spin_over)
-        while (true) {
-            const unsigned long long idle = __ballot(!active);
-            unsigned gq = 0, gt = 0, gn = 0;
-            bool live = true;
-            if (idle) {
-                const unsigned ni = (unsigned)__popcll(idle);
-                if (lane == __ffsll((unsigned long long)idle) - 1) {
-                    live = lds_acquire(&g_live) != 0;    // read before the queues: a 0 here means every tail is final
-                    for (int i = 0; i < P && gn == 0; ++i) {
-                        const int qq = (wave + i) % P;
-                        while (true) {
-                            const unsigned t = __hip_atomic_load(&g_take[qq], __ATOMIC_RELAXED,
-                                                                 __HIP_MEMORY_SCOPE_WORKGROUP);
-                            const unsigned pb = lds_acquire(&g_pub[qq]);
-                            if (pb <= t) break;
-                            const unsigned n = min(ni, pb - t);
-                            unsigned expect = t;
-                            if (__hip_atomic_compare_exchange_strong(&g_take[qq], &expect, t + n, __ATOMIC_RELAXED,
-                                                                     __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)) {
-                                gq = (unsigned)qq; gt = t; gn = n;
-                                break;
-                            }
-                        }
-                    }
-                }
-                const int leader = __ffsll((unsigned long long)idle) - 1;
-                gq = __shfl(gq, leader, 64);
-                gt = __shfl(gt, leader, 64);
-                gn = __shfl(gn, leader, 64);
-                live = __shfl((int)live, leader, 64) != 0;
-                if (!active) {
-                    const unsigned rank = lane_rank(idle);
-                    if (rank < gn) {
-                        owner = qbase[(size_t)gq * p.wq_cap + gt + rank];
-                        const unsigned lvp = owner / (unsigned)nl;
-                        const int l = (int)(owner - lvp * (unsigned)nl);
-                        const float4 a = p.rec[lvp];
-                        const V hitp{a.x, a.y, a.z};
-                        const V pnt = add(hitp, mul(surface_normal(s, hitp, __float_as_int(a.w)), s.eps));   // :397
-                        const float4 lp = ld4(&s.lights[l].px);
-                        const V lpos{lp.x, lp.y, lp.z};
-                        tlim = len(sub(lpos, pnt));                                          // :400-404
-                        r = make_ray(pnt, nrm(sub(lpos, pnt)));
-                        nshadow++;
-                        if (walk_begin<COUNT>(s, r, wk, w, true)) active = true;
-                        else p.occ[owner] = 0;
-                    }
-                }
-            }
-            if (gn > 0) spin = 0;
-            if (!__any(active)) {
-                if (gn == 0) {
-                    if (!live || spin_over(s, spin)) break;   // producers done and every queue drained
-                    __builtin_amdgcn_s_sleep(2);
-                }
-                continue;
-            }
-            // walk until enough lanes are free (all of them once nothing is queued)
-            const int thresh = (gn > 0 || live) ? p.crefill : 0;
-            while (__popcll(__ballot(active)) > thresh) {
-                if (active) {
-                    const int res = occl_step<COUNT, FetchTop>(s, r, tlim, stk, wk, w);
-                    if (res || walk_runaway(s, wk)) {
-                        p.occ[owner] = res == 2 ? 1 : 0;
-                        active = false;
-                    }
-                }
-            }
-        }
-    }
-    if (COUNT) {
-        wave_add_counter(&p.counters[0], nprim);
-        wave_add_counter(&p.counters[1], nshadow);
-        wave_add_counter(&p.counters[2], nrefl);
-        wave_add_counter(&p.counters[3], w.nodes);
-        wave_add_counter(&p.counters[4], w.tris);
-        wave_add_counter(&p.counters[5], w.spheres);
     }
 }
 
@@ -1981,11 +1282,7 @@ __device__ __forceinline__ V shade_core(const rtk::DevScene& s, const V hitp, co
         if (cos_t >= s.cos_thr && cos_t <= 1.0f) {
             const V hh = nrm(add(ldir, neg(nrm(d))));
             const float base = smax(0.0f, dot(nrm(n_), hh));
-#ifdef RT_EXP_FASTPOW
-            const float ca = __powf(base, mA.w);      // experiment only: NOT the reference's rounding
-#else
             const float ca = phong_pow(base, mA.w);
-#endif
             L = add(L, had(mul(V{mS.x, mS.y, mS.z}, ca), E));
         }
         const float cl = smax(0.0f, smin(1.0f, cos_t));
@@ -2140,92 +1437,29 @@ __device__ __forceinline__ bool pixel_cont(const PcParams& p, int rr, int ocol) 
     return cont;
 }
 
-// k_mix's early finish: pixels without a continued sample, taken by whole waves 64 at a time from the
-// counter of stripe wave-id mod kFinStripes (~136 waves per stripe in a C3 frame) while fewer than
-// stop_at phase-B waves have counted themselves done (totals[10], read every 4th grab).  A grab below
-// the stripe's end is always finished, so the stripe's pixels [0, min(counter, length)) are done and
-// k_finish takes the rest (finish_pixels).
-template <bool LDS, bool CMP>
-__device__ void finish_taken(const rtk::DevScene& s, const rtk::Eye& e, const PcParams& p, unsigned stop_at) {
-    const unsigned npix = (unsigned)((p.chunk_rows / p.aa) * p.width), len = fin_stripe_len(npix);
-    const unsigned j = (unsigned)uni((int)(((blockIdx.x * kBlock + threadIdx.x) >> 6) % (unsigned)kFinStripes));
-    const unsigned lo = j * len, hi = min(npix, lo + len);
-    unsigned* const ctr = &p.totals[kFinCtr0 + j * kFinCtrStride];
-    for (unsigned it = 1; lo < hi; ++it) {
-        unsigned q0 = 0;
-        if (lane_id() == 0) q0 = atomicAdd(ctr, 64u);
-        q0 = lo + (unsigned)uni((int)__shfl((int)q0, 0));
-        if (q0 >= hi) break;
-        const unsigned q = q0 + (unsigned)lane_id();
-        if (q < hi) {
-            const int rr = (int)(q / (unsigned)p.width), ocol = (int)(q - (unsigned)rr * (unsigned)p.width);
-            if (!pixel_cont(p, rr, ocol)) finish_pixel<LDS, CMP>(s, e, p, rr, ocol);
-        }
-        if ((it & 3u) == 0 && __hip_atomic_load(&p.totals[10], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= stop_at)
-            break;
-    }
-}
-
 // p.fin_cont (chain path): the pixels of the paths continued in phase B first (cflat, totals[1] of
 // them; each pixel once, by the lane holding its first continued sample), so their long folds
 // overlap the rest; then every pixel without a continued sample (pinfo's kPathCont bit).
-// EF (p.early_fin): k_mix took most of the latter already (finish_taken), so k_finish takes the rest of
-// each stripe, and every pixel k_fallback changed again (the phase-A entries of fbc and fbs: k_mix may
-// have finished them before), beside the continued ones; after a fallback shadow-queue overflow
-// (occlusion bytes left kOccDeferred, totals[6]) every pixel again.
-template <bool LDS, bool CMP, bool EF>
+template <bool LDS, bool CMP>
 __device__ __forceinline__ void finish_pixels(const rtk::DevScene& s, const rtk::Eye& e, const PcParams& p) {
-    static_assert(!(EF && CMP), "early finish: no compact records");
     const int F = p.aa;
     const unsigned gtid = blockIdx.x * kBlock + threadIdx.x, gstride = gridDim.x * kBlock;
     if (p.fin_cont) {
         const unsigned n = p.totals[1];
-        const unsigned aspace = (unsigned)p.la * (unsigned)p.cap, nl = (unsigned)s.nlights;
-        const unsigned nfc = EF ? min(p.totals[4], p.fbc_cap) : 0u, nfs = EF ? min(p.totals[5], p.fbs_cap) : 0u;
-        for (unsigned j = gtid; j < n + nfc + nfs; j += gstride) {
-            unsigned path;
-            if (!EF || j < n) {
-                path = (p.cflat[j] & ~kFbEye) % (unsigned)p.cap;
-            } else if (j < n + nfc) {
-                const unsigned en = p.fbc[j - n];
-                if (!(en & kFbEye) && en >= aspace) continue;        // a phase-B level: a continued path
-                path = (en & kFbEye) ? en & ~kFbEye : en % (unsigned)p.cap;
-            } else {
-                const unsigned lvp = p.fbs[j - n - nfc] / nl;
-                if (lvp >= aspace) continue;
-                path = lvp % (unsigned)p.cap;
-            }
+        for (unsigned j = gtid; j < n; j += gstride) {
+            const unsigned path = (p.cflat[j] & ~kFbEye) % (unsigned)p.cap;
             const unsigned tile = path >> 6, lane = path & 63u;
             const int ix = (int)(tile % (unsigned)p.tiles_x) * 8 + (int)(lane & 7u);
             const int iyc = (int)(tile / (unsigned)p.tiles_x) * 8 + (int)(lane >> 3);
             const int ocol = ix / F, rr = iyc / F;
-            bool go;
-            if (!EF || j < n) {
-                unsigned first = path;
-                for (int k = F - 1; k >= 0; --k)
-                    for (int l = F - 1; l >= 0; --l) {
-                        const unsigned sl = slab_slot(p.tiles_x, ocol * F + l, rr * F + k);
-                        if (p.pinfo[sl] & kPathCont) first = sl;
-                    }
-                go = first == path;
-            } else {
-                go = !pixel_cont(p, rr, ocol);   // (repeated entries write the same bytes)
-            }
-            if (go) finish_pixel<LDS, CMP>(s, e, p, rr, ocol);
+            unsigned first = path;
+            for (int k = F - 1; k >= 0; --k)
+                for (int l = F - 1; l >= 0; --l) {
+                    const unsigned sl = slab_slot(p.tiles_x, ocol * F + l, rr * F + k);
+                    if (p.pinfo[sl] & kPathCont) first = sl;
+                }
+            if (first == path) finish_pixel<LDS, CMP>(s, e, p, rr, ocol);
         }
-    }
-    if constexpr (EF) {
-        const unsigned npix = (unsigned)((p.chunk_rows / p.aa) * p.width), len = fin_stripe_len(npix);
-        const bool all = p.totals[6] != 0;
-        for (unsigned j = 0; j < (unsigned)kFinStripes; ++j) {
-            const unsigned hi = min(npix, (j + 1) * len);
-            const unsigned lo = all ? j * len : min(hi, j * len + p.totals[kFinCtr0 + j * kFinCtrStride]);
-            for (unsigned q = lo + gtid; q < hi; q += gstride) {
-                const int rr = (int)(q / (unsigned)p.width), ocol = (int)(q - (unsigned)rr * (unsigned)p.width);
-                if (!pixel_cont(p, rr, ocol)) finish_pixel<LDS, CMP>(s, e, p, rr, ocol);
-            }
-        }
-        return;
     }
     const int npix = (p.chunk_rows / p.aa) * p.width;
     for (int q = (int)gtid; q < npix; q += (int)gstride) {
@@ -2238,7 +1472,7 @@ __device__ __forceinline__ void finish_pixels(const rtk::DevScene& s, const rtk:
 // k_finish: k_shade + k_compose in one pass, one lane per output pixel, with
 // the scene's materials and lights in LDS (host checks they fit);
 // k_finish_any: the same for larger scenes, tables read from global memory.
-template <bool CMP, bool EF = false>
+template <bool CMP>
 __global__ __launch_bounds__(kBlock, CMP ? RT_FINISH_CMP_WAVES : RT_FINISH_WAVES) void k_finish(rtk::DevScene s,
                                                                                                  rtk::Eye e, PcParams p) {
     float4* dm = reinterpret_cast<float4*>(g_fmats);
@@ -2248,11 +1482,11 @@ __global__ __launch_bounds__(kBlock, CMP ? RT_FINISH_CMP_WAVES : RT_FINISH_WAVES
     const float4* sl = reinterpret_cast<const float4*>(s.lights);
     for (int i = threadIdx.x; i < s.nlights * 2; i += kBlock) dl_[i] = sl[i];
     __syncthreads();
-    finish_pixels<true, CMP, EF>(s, e, p);
+    finish_pixels<true, CMP>(s, e, p);
 }
-template <bool CMP, bool EF = false>
+template <bool CMP>
 __global__ __launch_bounds__(kBlock, RT_FINISH_ANY_WAVES) void k_finish_any(rtk::DevScene s, rtk::Eye e, PcParams p) {
-    finish_pixels<false, CMP, EF>(s, e, p);
+    finish_pixels<false, CMP>(s, e, p);
 }
 
 // ---------------------------------------------------------------------------
@@ -2439,25 +1673,6 @@ __global__ __launch_bounds__(kBlock) void k_walk_timing(rtk::DevScene s, const f
                     }
                     h = HitRec{0.0f, cur};
                 }
-            } else if (mode == 5) {              // the cooperative walk (coop_step): lanes 0-7, one group
-                if (threadIdx.x < 8) {
-                    if (threadIdx.x == 0) {
-                        float* a = g_cray[0];
-                        a[0] = r.o.x; a[1] = r.o.y; a[2] = r.o.z; a[3] = r.d.x; a[4] = r.d.y; a[5] = r.d.z;
-                        a[6] = r.inv.x; a[7] = r.inv.y; a[8] = r.inv.z;
-                    }
-                    __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");   // lane 0's LDS words, seen by lanes 1-7
-                    CoopW c;
-                    c.owner = 0; c.cur = s.wroot; c.sp = 0; c.steps = 0; c.tmax = FLT_MAX; c.best = HitRec{-1.0f, -1};
-#pragma unroll 1
-                    while (true) {
-                        ++steps;
-                        const int res = coop_step(s, c);
-                        if (res == 1) break;
-                        if (res == 2) { c.best.prim = -2; break; }   // would need the scratch stack
-                    }
-                    h = c.best;
-                }
             } else if ((int)threadIdx.x < lanes) {
                 Walk wk;
                 bool go = mode == 0 ? walk_begin<false>(s, r, wk, w) : walk_begin<true>(s, r, wk, w);
@@ -2489,16 +1704,11 @@ __global__ __launch_bounds__(kBlock) void k_walk_timing(rtk::DevScene s, const f
 void launch_finish(const rtk::DevScene& s, const rtk::Eye& e, const PcParams& p, hipStream_t st) {
     const int npix = (p.chunk_rows / p.aa) * p.width;
     const dim3 pgrid(std::max(1, std::min((npix + kBlock - 1) / kBlock, p.fin_grid > 0 ? p.fin_grid : INT32_MAX)));
-    // (p.early_fin: the rest of k_mix's early finish; lone frames, never with compact records; tables from
-    // global memory: with them in LDS this variant spills 3 VGPRs)
-    if (s.nmats <= kFinishMats && s.nlights <= kFinishLights)
-    {
+    if (s.nmats <= kFinishMats && s.nlights <= kFinishLights) {
         if (p.clevels) hipLaunchKernelGGL((k_finish<true>), pgrid, dim3(kBlock), 0, st, s, e, p);
-        else if (p.early_fin) hipLaunchKernelGGL((k_finish_any<false, true>), pgrid, dim3(kBlock), 0, st, s, e, p);
         else hipLaunchKernelGGL((k_finish<false>), pgrid, dim3(kBlock), 0, st, s, e, p);
     } else {
         if (p.clevels) hipLaunchKernelGGL((k_finish_any<true>), pgrid, dim3(kBlock), 0, st, s, e, p);
-        else if (p.early_fin) hipLaunchKernelGGL((k_finish_any<false, true>), pgrid, dim3(kBlock), 0, st, s, e, p);
         else hipLaunchKernelGGL((k_finish_any<false>), pgrid, dim3(kBlock), 0, st, s, e, p);
     }
 }
@@ -2511,30 +1721,11 @@ hipError_t chain_occupancy(int* chain_blocks_per_cu, int* mix_blocks_per_cu, int
     return e;
 }
 
-hipError_t fused_occupancy(int* blocks_per_cu) {
-    return hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks_per_cu, k_fused<false>, kBlock, 0);
-}
-
-unsigned fused_wave_qcap(int n0, int grid, int levels, int nlights) {
-    return chain_block_scap(n0, grid, levels, nlights);   // a producer wave may take all of its block's samples
-}
-
-hipError_t launch_fused_chunk(const rtk::DevScene& s, const rtk::Eye& e, const PcParams& p, bool count,
-                              hipStream_t st) {
-    if (count)
-        hipLaunchKernelGGL(k_fused<true>, dim3(p.grid), dim3(kBlock), 0, st, s, e, p);
-    else
-        hipLaunchKernelGGL(k_fused<false>, dim3(p.grid), dim3(kBlock), 0, st, s, e, p);
-    launch_finish(s, e, p, st);
-    return hipGetLastError();
-}
-
 hipError_t launch_walk_timing(const rtk::DevScene& s, const float* rays, int n, int lanes, int reps, int mode,
                               unsigned long long* out, hipStream_t st) {
     if (mode == 0) hipLaunchKernelGGL(k_walk_timing<0>, dim3(1), dim3(kBlock), 0, st, s, rays, n, lanes, reps, out);
     else if (mode == 1) hipLaunchKernelGGL(k_walk_timing<1>, dim3(1), dim3(kBlock), 0, st, s, rays, n, lanes, reps, out);
     else if (mode == 3) hipLaunchKernelGGL(k_walk_timing<3>, dim3(1), dim3(kBlock), 0, st, s, rays, n, lanes, reps, out);
-    else if (mode == 5) hipLaunchKernelGGL(k_walk_timing<5>, dim3(1), dim3(kBlock), 0, st, s, rays, n, lanes, reps, out);
     else hipLaunchKernelGGL(k_walk_timing<4>, dim3(1), dim3(kBlock), 0, st, s, rays, n, lanes, reps, out);
     return hipGetLastError();
 }
@@ -2641,8 +1832,7 @@ hipError_t launch_chain_chunk(const rtk::DevScene& s, const rtk::Eye& e, const P
     mark(kKFallback);
     hipLaunchKernelGGL(k_fallback, dim3(p.fb_grid), blk, 0, st, s, e, p);
     PcParams f = p;
-    f.fin_cont = phase_b && (p.aa == 1 || p.early_fin);
-    f.early_fin = phase_b && !split && !count ? p.early_fin : 0;
+    f.fin_cont = phase_b && p.aa == 1;
     mark(kKFinish);
     launch_finish(s, e, f, st);
     mark(kKEnd);

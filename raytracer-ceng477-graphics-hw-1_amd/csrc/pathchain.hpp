@@ -30,7 +30,20 @@ constexpr int kMaxFrames = 32;        // frames of one batched launch (PcParams 
 #ifndef RT_BQ
 #define RT_BQ 1536
 #endif
-constexpr int kMaxBq = RT_BQ;          // phase-B workgroup shadow queue (LDS slots, pathchain.hip)
+constexpr int kMaxBq = RT_BQ;
+// Diagnostics build (RT_TRACE_BUILD=1, tools/trace_report.py): the chain kernels record wall-clock
+// timings per sample, continuation and shadow workgroup into PcParams::trace (env RT_TRACE names the
+// dump).  Off in the product build: its counters cost the walk kernels registers.
+#ifndef RT_TRACE_BUILD
+#define RT_TRACE_BUILD 0
+#endif
+constexpr bool kTraceBuild = RT_TRACE_BUILD != 0;
+// Shadow walks with the wave leaf queue (pathchain.hip occlude_queue_body), the only walker that reads
+// task regions in place (PcParams::occ_inplace / occ_inplace_b): the host enables those only when it is
+// built.
+#ifndef RT_LEAF_QUEUE
+#define RT_LEAF_QUEUE 1
+#endif          // phase-B workgroup shadow queue (LDS slots, pathchain.hip)
 
 enum PathKind : int {
     kEndBg = 0,     // deepest ray missed at depth 0: background
@@ -97,17 +110,9 @@ __host__ __device__ inline unsigned unit_col(int tiles_x, int ublk_h, int ublk_w
     return (r0 + l / w) * upr + c0 + l % w;
 }
 
-#ifndef RT_EARLY_FIN_BUILD
-#define RT_EARLY_FIN_BUILD 0   // 1: k_mix with the early finish (RT_EARLY_FIN; measured slower; off)
-#endif
-// Early finish (PcParams::early_fin): the pixels in kFinStripes equal stripes, each with a launch-wide
-// counter of pixels taken, 256 B apart (atomics on one word serialise: 64-pixel grabs on a single
-// counter cost a lone frame 0.4 ms), from totals word kFinCtr0 on.
-constexpr int kFinStripes = 16, kFinCtrStride = 64, kFinCtr0 = 64;
-constexpr int kTotalsWords = RT_EARLY_FIN_BUILD ? kFinCtr0 + kFinStripes * kFinCtrStride : 12;
-__host__ __device__ inline unsigned fin_stripe_len(unsigned npix) {
-    return ((npix + kFinStripes - 1) / kFinStripes + 63u) & ~63u;
-}
+// PcParams::totals words: packed task counts (0-2), the phase-A unit counter (3), k_fallback's chain /
+// shadow counts and shadow-queue overflow (4-6), the rest spare.
+constexpr int kTotalsWords = 12;
 
 // Unit cost classes (PcParams::ucost): the most phase-A walk steps a sample of the unit took.
 constexpr unsigned kHotSteps[2] = {96, 32};
@@ -158,14 +163,11 @@ struct PcParams {
     unsigned* scntB;  // [gb]
     unsigned* sflatB; // B's shadow tasks packed (k_pack_b), totals[2] of them
     unsigned* totals; // [kTotalsWords]: packed task counts (3), phase-A unit counter, k_fallback chains / shadows /
-                      // overflow, finished k_chain waves; early finish (early_fin): k_mix shadow-role workgroups
-                      // done (8), finished phase-B waves (10), the stripes' pixel counters (kFinCtr0 on)
+                      // overflow
     int kinline;      // deepest level phase A walks (>= max_depth: no phase B)
     int gb;           // k_mix workgroups in the chain role (the other p.ogrid ones occlude A's tasks)
     int tchunk;       // continuation tasks (phase B) are dealt to workgroups in chunks of this many
     int ochunk;       // ... and shadow tasks (k_mix occlusion role, k_occlude) in chunks of this many
-    int packet;       // 1: eye rays of a wave walk as one packet when exact (packet_closest)
-    int exp_skip_occ; // experiments only (RT_EXP_SKIP_OCC): k_mix's occlusion role does nothing (wrong images)
     int lq_wait;      // leaf-queue walks: test the queued records once this many lanes wait on them (RT_LQ_WAIT)
     int grid;         // k_chain persistent grid (= number of shadow-queue regions)
     int ogrid;        // k_occlude persistent grid
@@ -195,12 +197,6 @@ struct PcParams {
     int bservice;     // the same for phase-B chains
     int btail;        // phase-B chains once no continuation is left to take: service at this many done lanes
     int bq_cap;       // phase-B workgroup shadow queue slots in use (<= kBq; 0: every task to k_occlude)
-    unsigned abandon; // phase A: once this many k_chain waves have finished (totals[7]), a wave with no unit
-                      // left hands its unfinished walks to phase B as continuations (0: never)
-    int coop;         // lone-frame phase B: once a wave has no continuation left and <= coop_live chains walk,
-    int coop_live;    // each walk runs on a group of 8 lanes (one wide-node slot per lane; coop_step);
-    int coop_tail;    // ... and a wave services its finished walks once this many are done (0: coop off)
-    int spread;       // tiles interleaved per wave within a 256-sample unit (1, 2 or 4)
     int dyn_units;    // > 0: phase-A waves take 256-sample units from a launch-wide counter (totals[3]),
                       // at most this many per workgroup; 0: static per-workgroup interleave
     int ublk_h, ublk_w; // dynamic units taken in column blocks of ublk_h tile rows (< 0: a frame; 0: off)
@@ -213,10 +209,6 @@ struct PcParams {
     uint8_t* fouts[kMaxFrames];
     int out_k, out_j;   // sub-frame j of k interleaved sub-frames (out_row); 1, 0 for a whole frame
     unsigned long long* counters;
-    unsigned* wq;     // k_fused: per-wave task queues, [grid*4][wq_cap] u32 shadow-task owner ids
-    unsigned wq_cap;
-    int producers;    // k_fused: chain-producing waves per workgroup (1..4), the rest consume
-    int crefill;      // k_fused consumers refill once <= crefill lanes are still walking
     unsigned* trace;  // diagnostics (RT_TRACE): [cap][2] sample {grab, chain end}, then [trace_blocks][2]
                       // k_occlude workgroup {start, end}, then [cap][4] phase-B continuation {grab, end,
                       // last level, walk steps}; wall clock; or null
@@ -224,10 +216,6 @@ struct PcParams {
     // (new fields at the end: kernel arguments are loaded in runs of neighbours, so a field inserted
     // among the walk kernels' ones changed their SGPR spills 28 -> 67)
     unsigned* cont_peak;  // frames of several chunks: the most continuations of one chunk (k_pack_a, atomicMax)
-    int early_fin;    // 1 (lone frames, k_mix with the LDS queue, no compact records): k_mix's shadow-role
-                      // workgroups finish the pixels without a continued sample once A's occlusion is done
-                      // (pathchain.hip early finish); k_finish the rest and what k_fallback changed
-                      // (2: tests, no wait for the other workgroups)
 };
 
 // Worst-case task-queue slots per workgroup: every sample of the workgroup
@@ -242,12 +230,6 @@ constexpr int kDynUnits = 128;
 // the persistent grids are sized so every workgroup starts at t = 0 (a late-
 // starting workgroup that owns slow pixels would stretch the frame).
 hipError_t chain_occupancy(int* chain_blocks_per_cu, int* mix_blocks_per_cu, int* occlude_blocks_per_cu);
-
-// Fused path: k_fused (chains + shadow rays, per-wave task queues) + k_finish.
-hipError_t fused_occupancy(int* blocks_per_cu);
-unsigned fused_wave_qcap(int n0, int grid, int levels, int nlights);
-hipError_t launch_fused_chunk(const rtk::DevScene& s, const rtk::Eye& e, const PcParams& p, bool count,
-                              hipStream_t stream);
 
 // Diagnostics: phong_pow on the device (rt_phong_pow).
 hipError_t launch_phong_pow(const float* base, const float* expo, float* out, int n, hipStream_t st);

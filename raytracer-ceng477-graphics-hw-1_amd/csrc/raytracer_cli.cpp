@@ -39,7 +39,8 @@ int main(int argc, char** argv) {
     if (const char* q = std::getenv("RT_HW_QUEUES")) setenv("GPU_MAX_HW_QUEUES", q, 1);
     else setenv("GPU_MAX_HW_QUEUES", "8", 0);
     const char* scene_path = nullptr;
-    int aa = 2, max_depth = -1000, device = -1, gpus = 0;
+    int aa = 2, max_depth = -1000, device = 0, gpus = 0;   // device 0 unless --device: an explicit device lets
+                                                          // the library start HIP while the XML is read
     bool write = true;
     for (int i = 1; i < argc; ++i) {
         if (!std::strcmp(argv[i], "--aa") && i + 1 < argc) aa = std::atoi(argv[++i]);

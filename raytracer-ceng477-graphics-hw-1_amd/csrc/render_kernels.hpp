@@ -1,5 +1,5 @@
 // Kernel-launch interface between the C-ABI layer (rt_api.cpp) and the HIP
-// kernels (render_kernels.hip).  Plain structs passed by value as kernel args.
+// kernels (pathchain.hip, render_kernels.hip).  Plain structs passed by value as kernel args.
 #pragma once
 
 #include <hip/hip_runtime.h>
@@ -30,9 +30,6 @@ struct DevScene {
     const dl::LeafBig* leaf_big;
     float root_lo[3], root_hi[3];
     int root_info;
-    int pair_stack;       // LDS stack entries (8 B each) for the pair traversal
-    int top_pairs;        // pairs [0, top_pairs) are the top BVH levels (cached in LDS)
-    int prio;             // 1: raise wave priority with recursion depth (RT_PRIO=0 disables)
     // occlusion tree (host_scene.cpp build_shadow_tree): same leaves, SAH hierarchy above them
     const dl::Pair* spairs;
     float sroot_lo[3], sroot_hi[3];
@@ -81,7 +78,6 @@ struct FrameParams {
     int out_k = 1, out_j = 0;   // chain path: sub-frame j of out_k interleaved sub-frames (pathchain.hip out_row)
     int chunk_k = 1, chunk_j = 0;   // chain path: this call renders sample chunks j, j+k, ... of the frame
     unsigned long long* counters;  // 6 x u64 (RT_RENDER_COUNT)
-    unsigned* trace;      // diagnostics (RT_TRACE): per output pixel {wave start, pixel end} wall clock, or null
     // chain path, frame batches (rt_render_frames_device): slab_rows = nframes * frame_rows virtual
     // rows, frame f's rows rendered with eyes[f] into outs[f] (host arrays of nframes entries)
     int nframes = 1, frame_rows = 0;
@@ -89,8 +85,6 @@ struct FrameParams {
     uint8_t* const* outs = nullptr;
 };
 
-size_t render_lds_bytes(const DevScene& s);
-hipError_t launch_render(const DevScene& s, const Eye& e, const FrameParams& p, bool count, hipStream_t stream);
 hipError_t launch_primary_hits(const DevScene& s, const Eye& e, int W, int H, float* t, int* m, hipStream_t stream);
 hipError_t launch_unshuffle(const uint8_t* slabs, uint8_t* img, int width, int height, int stripe_rows, int nranks,
                             int slab_rows, hipStream_t stream);

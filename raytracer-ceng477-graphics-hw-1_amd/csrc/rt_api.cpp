@@ -20,7 +20,6 @@
 #include "host_scene.hpp"
 #include "render_kernels.hpp"
 #include "pathchain.hpp"
-#include "wavefront.hpp"
 #include "rt_internal.hpp"
 
 namespace {
@@ -104,16 +103,10 @@ struct rt_scene {
     dl::Wide* d_wnodes = nullptr;
     dl::Vec4* d_lrec = nullptr;
     dl::LeafBig* d_leafbig = nullptr;
-    enum Path { kChain, kWavefront, kMegakernel, kFused } path = kChain;
-    int grid_blocks = 2048;
     int num_cus = 256;
     int chain_grid = 0, occl_grid = 0, mix_grid = 0;   // resident-sized persistent grids (lazily queried)
     int tune_refill = -1;       // RT_REFILL (-1: path default)
     int tune_service = -1;      // RT_SERVICE (-1: path default)
-    int fused_grid = 0;
-    int tune_producers = 3;     // RT_PROD
-    int tune_crefill = 16;      // RT_CREFILL
-    int tune_spread = 1;        // RT_SPREAD
     int tune_orefill = 32;      // RT_OREFILL
     int tune_brefill = 32;      // RT_BREFILL
     int tune_bprio = 1;         // RT_BPRIO
@@ -124,13 +117,13 @@ struct rt_scene {
     // but a lone frame 1.15 -> 1.36 ms, so a lone frame keeps fine interleaving.
     int tune_tchunk = 0;        // RT_TCHUNK (0: 128 for frame batches, 1 for one frame)
     int tune_ochunk = 256;      // RT_OCHUNK
-    int tune_packet = 1;        // RT_PACKET
     int tune_kinline = 1;       // RT_KINLINE: deepest level of phase A
     // RT_CHUNK_SAMPLES: samples per chain-path launch (chunk / frame batch).  Bigger launches leave
     // fewer tails per sample: C3 batches 4 M 0.72, 8 M 0.66, 16 M 0.63, 32 M 0.59 ms/frame; C5 8 M
     // 159.6, 16 M 147.4, 32 M 140.6 ms/frame.  32 M samples = 15 GB of workspace per slot (C3).
     size_t chunk_samples = size_t(32) << 20;
     int tune_batch = 32;        // RT_BATCH: frames per batched launch (rt_render_frames/cameras; 1 = off)
+    bool tune_balance = true;   // RT_BALANCE: a call's frames dealt evenly over every slot (render_cameras)
     int tune_slots = 3;         // RT_SLOTS: frame batches in flight together (workspace slots, <= kSlots;
                                 // default GPU_MAX_HW_QUEUES - 1)
     int tune_fgrid = 0;         // RT_FGRID: k_finish workgroups at most (0: 8 per CU; its waves are dispatch-bound
@@ -138,28 +131,21 @@ struct rt_scene {
     int tune_gb = 0;            // RT_GB: phase-B chain workgroups in k_mix (0: 1.875 per CU for a lone frame, 1 for batches)
     int tune_bq_cap = 1 << 30;  // RT_BQ_CAP: phase-B shadow queue slots (tests force the k_occlude spill path)
     int tune_bservice = 64;     // RT_BSERVICE: phase-B waves service finished walks once this many lanes are done
-    int tune_abandon = 0;       // RT_ABANDON: per mille of k_chain's waves done before the stragglers hand off (0: off;
-                                // 900-990 measured 2-4 % slower for C3 one frame: the restarted walks are the
-                                // heaviest, deepest chains, which then start phase B from scratch)
     int tune_hot_units = 1;     // RT_HOT_UNITS: lone frames deal phase-A units heaviest-first by the previous frame's steps
-    int tune_early_fin = 0;     // RT_EARLY_FIN=1 (builds with RT_EARLY_FIN_BUILD=1): lone frames' k_mix finishes
-                                // the pixels without a continued sample (2: tests, its workgroups do not wait for
-                                // each other: k_finish takes the rest); measured slower
     int tune_occ_inplace = 1;   // RT_OCC_INPLACE: A's shadow tasks read in their regions by k_occlude in frame
-                                // batches (2: also by k_mix's shadow role in lone frames, slower; 0: packed)
+                                // batches, and B's LDS-queue overflow in lone frames (0: packed)
     int tune_compact = 1;       // RT_COMPACT: phase-A records without directions (16 B instead of 32): 1 frame batches,
                                 // 2 every launch, 0 none
-    int tune_coop = 1;          // RT_COOP (builds with RT_COOP_BUILD=1): lone-frame phase B walks its tail chains on 8-lane groups (pathchain.hip coop_step)
-    int tune_coop_live = 8;     // RT_COOP_LIVE: ... once at most this many chains of the wave walk (<= 8)
-    int tune_coop_tail = 1;     // RT_COOP_TAIL: ... servicing finished walks once this many are done
     int tune_btail = 64;        // RT_BTAIL: the same once the continuations are exhausted (1: 1.24, 4: 1.18, 16: 1.15, 64: 1.14 ms)
     int tune_dyn = 1;           // RT_DYN_UNITS: phase-A waves take sample units from a launch-wide counter
     int tune_ublk_h = -1, tune_ublk_w = 8;  // RT_UBLK_H / RT_UBLK_W: phase-A unit column blocks (unit_order;
                                             // H -1: a frame high, 0: row-major units)
     int tune_split = 1;         // RT_SPLIT: a frame runs as this many concurrent interleaved sub-frames (2: +8%, 3: +18% on C3)
-    // RT_WS_BUDGET_MB: HBM for the chain-path workspace arenas of all slots together.  A launch's arena
-    // is sized for the worst case (every sample recording every level), so the budget bounds the
-    // samples per launch (and the frames per frame batch); it is split evenly over the slots.
+    // RT_WS_BUDGET_MB: HBM for the scene on its device -- the uploaded scene, a 64 MB reserve for output
+    // staging, and the chain-path workspace arenas of all slots together, each slot's arena (headroom
+    // included) within an even share of the rest.  A launch's arena is sized for the worst case (every
+    // sample recording every level), so the budget bounds the samples per launch (and the frames per frame
+    // batch).  A lone frame's arena follows the frame (chain_launch_units), not the share.
     size_t ws_budget = size_t(16) << 30;
     // RT_CONT_DEN: phase-B records for cap / den continuations per launch (C3: ~9 % of the samples
     // continue; the rest, if any, finish in k_fallback); 1 = every sample
@@ -171,7 +157,12 @@ struct rt_scene {
     double kt_ms[rtc::kKKinds] = {};
     long long kt_launches = 0;
     rtc::KTimer kt;
-    size_t slot_budget() const { return ws_budget / (size_t)std::max(1, std::min(tune_slots, kSlots)); }
+    static constexpr size_t kStagingReserve = size_t(64) << 20;
+    size_t slot_budget() const {
+        const size_t fixed = scene_bytes + kStagingReserve;
+        const size_t arenas = ws_budget > 2 * fixed ? ws_budget - fixed : ws_budget / 2;
+        return arenas / (size_t)std::max(1, std::min(tune_slots, kSlots));
+    }
     double xml_ms = 0, prep_ms = 0, upload_ms = 0;   // scene creation phases (rt_scene_bvh_info)
     bool warned_budget = false;    // one row unit alone exceeds the slot budget (chain_launch_units): told once
     std::string trace_file;     // RT_TRACE: dump per-sample wall-clock timings after each render (diagnostics)
@@ -208,29 +199,8 @@ struct rt_scene {
     uint8_t* batch_out = nullptr;              // device frames of rt_render_cameras (host outputs)
     size_t batch_out_cap = 0;
 
-    // wavefront workspace (grown on demand)
-    struct {
-        int cap = 0, levels = 0, nlights = 0;
-        float4* q[2] = {nullptr, nullptr};
-        float4* hit = nullptr;
-        float4* sray = nullptr;
-        uint8_t* occ = nullptr;
-        float4* R = nullptr;
-        int* child = nullptr;
-        unsigned* counts = nullptr;
-        size_t bytes = 0;
-    } ws;
-
-    void free_ws() {
-        (void)hipFree(ws.q[0]); (void)hipFree(ws.q[1]); (void)hipFree(ws.hit); (void)hipFree(ws.sray);
-        (void)hipFree(ws.occ); (void)hipFree(ws.R); (void)hipFree(ws.child); (void)hipFree(ws.counts);
-        ws.q[0] = ws.q[1] = nullptr; ws.hit = ws.sray = ws.R = nullptr; ws.occ = nullptr; ws.child = nullptr;
-        ws.counts = nullptr; ws.cap = ws.levels = ws.nlights = 0; ws.bytes = 0;
-    }
-
     ~rt_scene() {
         if (group) rt_internal_group_destroy(group);
-        free_ws();
         for (int i = 0; i < kSlots; ++i) {
             (void)hipFree(arenas[i].p);
             if (arenas[i].last) (void)hipEventDestroy(arenas[i].last);
@@ -278,20 +248,24 @@ std::mutex g_warm_mu;
 std::future<void> g_warm;
 bool g_warm_started = false;
 
+// Only for an explicit device (opts->device >= 0) or a device group (whose primary is device 0): -1
+// means the calling thread's current device, which a helper thread cannot know without initialising HIP
+// on the caller's thread first (a one-process-per-GPU caller passing -1 got an extra context
+// and code-object load on GPU 0 in every rank).
 void start_device_warmup(const rt_options* opts) {
     if ((opts && (opts->flags & RT_OPT_HOST_ONLY)) || std::getenv("RT_NO_WARMUP")) return;
+    const int want = g_devices.load() >= 1 ? 0 : (opts ? opts->device : -1);
+    if (want < 0) return;
     std::lock_guard<std::mutex> lk(g_warm_mu);
     if (g_warm_started) return;
     g_warm_started = true;
-    const int want = opts ? opts->device : -1;
     g_warm = std::async(std::launch::async, [want] {
         int n = 0;
-        if (hipGetDeviceCount(&n) != hipSuccess || n == 0) return;
-        (void)hipSetDevice(want >= 0 && want < n ? want : 0);
+        if (hipGetDeviceCount(&n) != hipSuccess || n == 0 || want >= n) return;
+        (void)hipSetDevice(want);
         (void)hipFree(nullptr);
         int a = 0, b = 0, c = 0;
         (void)rtc::chain_occupancy(&a, &b, &c);     // loads the kernels' code objects
-        (void)rtc::fused_occupancy(&a);
     });
 }
 
@@ -430,34 +404,17 @@ int upload_rest(rt_scene* s, const rt_options* opts) {
     {
         int cus = 0;
         HIP_TRY(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, s->device));
-        s->grid_blocks = std::max(1, cus) * 8;
         s->num_cus = std::max(1, cus);
-    }
-    s->path = rt_scene::kChain;
-    if (opts && (opts->flags & RT_OPT_WAVEFRONT)) s->path = rt_scene::kWavefront;
-    if (opts && (opts->flags & RT_OPT_MEGAKERNEL)) s->path = rt_scene::kMegakernel;
-    if (opts && (opts->flags & RT_OPT_CHAIN)) s->path = rt_scene::kChain;
-    if (opts && (opts->flags & RT_OPT_FUSED)) s->path = rt_scene::kFused;
-    if (const char* e = std::getenv("RT_PATH")) {
-        const std::string v(e);
-        if (v == "mega") s->path = rt_scene::kMegakernel;
-        else if (v == "wave") s->path = rt_scene::kWavefront;
-        else if (v == "chain") s->path = rt_scene::kChain;
-        else if (v == "fused") s->path = rt_scene::kFused;
     }
     if (const char* e = std::getenv("RT_REFILL")) s->tune_refill = std::max(0, std::min(63, std::atoi(e)));
     if (const char* e = std::getenv("RT_SERVICE")) s->tune_service = std::max(1, std::min(64, std::atoi(e)));
-    if (const char* e = std::getenv("RT_SPREAD")) {
-        const int v = std::atoi(e);
-        s->tune_spread = v >= 4 ? 4 : v >= 2 ? 2 : 1;
-    }
-    if (const char* e = std::getenv("RT_PACKET")) s->tune_packet = std::atoi(e) != 0;
     if (const char* e = std::getenv("RT_TCHUNK")) s->tune_tchunk = std::max(1, std::min(4096, std::atoi(e)));
     if (const char* e = std::getenv("RT_OCHUNK")) s->tune_ochunk = std::max(1, std::min(4096, std::atoi(e)));
     if (const char* e = std::getenv("RT_BPRIO")) s->tune_bprio = std::atoi(e) != 0;
     if (const char* e = std::getenv("RT_BREFILL")) s->tune_brefill = std::max(0, std::min(63, std::atoi(e)));
     if (const char* e = std::getenv("RT_OREFILL")) s->tune_orefill = std::max(0, std::min(63, std::atoi(e)));
     if (const char* e = std::getenv("RT_BATCH")) s->tune_batch = std::max(1, std::atoi(e));
+    if (const char* e = std::getenv("RT_BALANCE")) s->tune_balance = std::atoi(e) != 0;
     // frame batches in flight: one HIP stream each beside the caller's; HIP multiplexes streams beyond
     // GPU_MAX_HW_QUEUES hardware queues (4 by default) onto the same queues, which serialises them
     // (C3: 4 slots on 4 queues 0.60 ms/frame, on 8 queues 0.51)
@@ -475,20 +432,13 @@ int upload_rest(rt_scene* s, const rt_options* opts) {
     if (const char* e = std::getenv("RT_BQ_CAP")) s->tune_bq_cap = std::max(0, std::atoi(e));
     if (const char* e = std::getenv("RT_BSERVICE")) s->tune_bservice = std::max(1, std::min(64, std::atoi(e)));
     if (const char* e = std::getenv("RT_BTAIL")) s->tune_btail = std::max(1, std::min(64, std::atoi(e)));
-    if (const char* e = std::getenv("RT_COOP")) s->tune_coop = std::atoi(e) != 0;
     if (const char* e = std::getenv("RT_COMPACT")) s->tune_compact = std::max(0, std::min(2, std::atoi(e)));
-    if (const char* e = std::getenv("RT_OCC_INPLACE")) s->tune_occ_inplace = std::max(0, std::min(2, std::atoi(e)));
-    if (const char* e = std::getenv("RT_EARLY_FIN")) s->tune_early_fin = std::max(0, std::min(2, std::atoi(e)));
+    if (const char* e = std::getenv("RT_OCC_INPLACE")) s->tune_occ_inplace = std::atoi(e) != 0;
     if (const char* e = std::getenv("RT_HOT_UNITS")) s->tune_hot_units = std::atoi(e) != 0;
-    if (const char* e = std::getenv("RT_ABANDON")) s->tune_abandon = std::max(0, std::min(1000, std::atoi(e)));
-    if (const char* e = std::getenv("RT_COOP_LIVE")) s->tune_coop_live = std::max(1, std::min(8, std::atoi(e)));
-    if (const char* e = std::getenv("RT_COOP_TAIL")) s->tune_coop_tail = std::max(1, std::min(64, std::atoi(e)));
     if (const char* e = std::getenv("RT_SPLIT")) s->tune_split = std::max(1, std::atoi(e));
     if (const char* e = std::getenv("RT_DYN_UNITS")) s->tune_dyn = std::atoi(e) != 0;
     if (const char* e = std::getenv("RT_UBLK_H")) s->tune_ublk_h = std::max(-1, std::atoi(e));
     if (const char* e = std::getenv("RT_UBLK_W")) s->tune_ublk_w = std::max(1, std::atoi(e));
-    if (const char* e = std::getenv("RT_PROD")) s->tune_producers = std::max(1, std::min(4, std::atoi(e)));
-    if (const char* e = std::getenv("RT_CREFILL")) s->tune_crefill = std::max(0, std::min(63, std::atoi(e)));
     if (const char* e = std::getenv("RT_TRACE")) s->trace_file = e;
     s->ktime = std::getenv("RT_KTIME") && std::atoi(std::getenv("RT_KTIME")) != 0;
     if (const char* e = std::getenv("RT_CONT_DEN")) s->tune_cont_den = std::max(1, std::atoi(e));
@@ -514,9 +464,6 @@ int upload_rest(rt_scene* s, const rt_options* opts) {
         d.root_hi[i] = s->bvh.root_hi[i];
     }
     d.root_info = s->bvh.root_info;
-    d.pair_stack = std::max(2, s->bvh.max_stack);
-    d.top_pairs = s->bvh.top_pairs;
-    d.prio = 0;
     d.spairs = s->d_spairs;
     for (int i = 0; i < 3; ++i) {
         d.sroot_lo[i] = s->bvh.sroot_lo[i];
@@ -539,14 +486,6 @@ int upload_rest(rt_scene* s, const rt_options* opts) {
     d.use_wide = !s->bvh.nodes.empty() && !s->bvh.lrec.empty() &&
                  (!s->bvh.wnodes.empty() || (s->bvh.root_info < 0 && s->bvh.root_lrec >= 0));
     if (const char* e = std::getenv("RT_WIDE_WALK")) d.use_wide = d.use_wide && std::atoi(e) != 0;
-    // experiment (RT_SHADOW_ON_REF=1): any-hit walks on the reference-order wide tree instead of the SAH
-    // occlusion tree (exact either way: any hit is order-free and both trees hold the same leaf records);
-    // one tree means a smaller walk hot set
-    if (std::getenv("RT_SHADOW_ON_REF") && std::atoi(std::getenv("RT_SHADOW_ON_REF")) && !s->bvh.wnodes.empty() &&
-        d.use_stree == 2) {
-        d.swnodes = s->d_wnodes;
-        d.swroot = s->bvh.wroot;
-    }
     d.err = s->d_err;
     {   // walk_runaway: 64 x (every node of the largest tree + leaves); RT_WALK_CAP overrides (tests)
         const long long nodes = (long long)s->bvh.pairs.size() + s->bvh.leaves + 64;   // the largest tree
@@ -569,8 +508,6 @@ int upload_rest(rt_scene* s, const rt_options* opts) {
     d.force_fb = std::getenv("RT_FORCE_FALLBACK") ? std::atoi(std::getenv("RT_FORCE_FALLBACK")) : 0;
     // measurement: counting passes walk the production trees and count fetched bytes (bench.py)
     d.count_prod = std::getenv("RT_COUNT_PROD") ? 1 : 0;
-    if (const char* e = std::getenv("RT_PRIO")) d.prio = std::atoi(e) != 0;
-    if (const char* e = std::getenv("RT_TOP")) d.top_pairs = std::min(d.top_pairs, std::max(0, std::atoi(e)));
     return RT_OK;
 }
 
@@ -606,40 +543,17 @@ int check_camera(const rt_camera* cam, int aa) {
     return RT_OK;
 }
 
-constexpr size_t kTargetSamples = size_t(8) << 20;   // level-0 samples per chunk
 constexpr long long kSplitMinSamples = 1 << 19;      // smaller frames are not split into sub-frames
-
-template <typename T>
-int alloc_dev(T** p, size_t n) {
-    HIP_TRY(hipMalloc(reinterpret_cast<void**>(p), std::max<size_t>(n, 1) * sizeof(T)));
-    return RT_OK;
-}
-
-int ensure_workspace(rt_scene* s, int cap, int levels, int nlights) {
-    auto& w = s->ws;
-    if (w.cap >= cap && w.levels >= levels && w.nlights >= nlights) return RT_OK;
-    cap = std::max(cap, w.cap);
-    levels = std::max(levels, w.levels);
-    nlights = std::max(nlights, std::max(1, w.nlights));
-    s->free_ws();
-    const size_t c = (size_t)cap;
-    int rc;
-    if ((rc = alloc_dev(&w.q[0], 2 * c)) || (rc = alloc_dev(&w.q[1], 2 * c)) || (rc = alloc_dev(&w.hit, 2 * c)) ||
-        (rc = alloc_dev(&w.sray, 2 * c * nlights)) || (rc = alloc_dev(&w.occ, c * nlights)) ||
-        (rc = alloc_dev(&w.R, c * levels)) || (rc = alloc_dev(&w.child, c * levels)) ||
-        (rc = alloc_dev(&w.counts, 2 * (size_t)levels + 2))) {
-        s->free_ws();
-        return rc;
-    }
-    w.cap = cap; w.levels = levels; w.nlights = nlights;
-    w.bytes = c * (32 * 3 + 32 * nlights + nlights + 20 * levels);
-    return RT_OK;
-}
 
 // RT_TRACE diagnostics: a device buffer of n u32 and, after the frame, a raw
 // dump {magic, path, a, b, n, payload...} (see tools/trace_report.py).
 unsigned* trace_buffer(rt_scene* s, size_t n) {
     if (s->trace_file.empty()) return nullptr;
+    if (!rtc::kTraceBuild) {
+        std::fprintf(stderr, "librt_hip: RT_TRACE needs a build with RT_TRACE_BUILD=1 (make EXTRA=-DRT_TRACE_BUILD=1)\n");
+        s->trace_file.clear();
+        return nullptr;
+    }
     if (s->trace_cap < n) {
         (void)hipFree(s->d_trace);
         s->d_trace = nullptr;
@@ -665,41 +579,6 @@ void trace_dump(rt_scene* s, hipStream_t st, unsigned path, unsigned a, unsigned
     }
 }
 
-// Chunked wavefront frame: chunks are whole groups of 8*aa slab-local
-// internal rows (whole output rows, whole 8x8 tiles).
-int render_wavefront(rt_scene* s, const rtk::Eye& eye, const rtk::FrameParams& f, bool count, hipStream_t st) {
-    const int levels = std::max(s->dev.max_depth, 0) + 1;
-    const int nl = std::max(s->dev.nlights, 1);
-    const int wi = f.width * f.aa;
-    const int tiles_x = (wi + 7) / 8;
-    const int li = f.slab_rows * f.aa;                           // slab-local internal rows
-    const int unit = 8 * f.aa;                                   // rows per chunk unit
-    const size_t unit_samples = (size_t)tiles_x * f.aa * 64;
-    const size_t units_total = (size_t)(li + unit - 1) / unit;
-    size_t units = std::max<size_t>(1, kTargetSamples / unit_samples);
-    units = std::min(units, units_total);
-    const int chunk_rows = (int)units * unit;
-    const size_t cap = units * unit_samples;
-    if (cap * nl >= (size_t)INT32_MAX) return fail(RT_ERR_LIMIT, "frame chunk too large for the wavefront path");
-    int rc = ensure_workspace(s, (int)cap, levels, nl);
-    if (rc) return rc;
-    rtw::WfParams p;
-    p.width = f.width; p.height = f.height; p.aa = f.aa; p.stripe_rows = f.stripe_rows;
-    p.rank = f.rank; p.nranks = f.nranks; p.slab_rows = f.slab_rows;
-    p.wi = wi; p.tiles_x = tiles_x; p.cap = s->ws.cap; p.nlights = s->dev.nlights;
-    p.q[0] = s->ws.q[0]; p.q[1] = s->ws.q[1]; p.hit = s->ws.hit; p.sray = s->ws.sray; p.occ = s->ws.occ;
-    p.R = s->ws.R; p.child = s->ws.child;
-    p.qcount = s->ws.counts; p.scount = s->ws.counts + levels + 1;
-    p.out = f.out; p.counters = f.counters;
-    for (int r0 = f.chunk_j * chunk_rows; r0 < li; r0 += f.chunk_k * chunk_rows) {
-        p.chunk_row0 = r0;
-        p.chunk_rows = std::min(chunk_rows, li - r0);
-        p.n0 = tiles_x * ((p.chunk_rows + 7) / 8) * 64;
-        HIP_TRY(rtw::launch_frame_chunk(s->dev, eye, p, s->grid_blocks, count, st));
-    }
-    return RT_OK;
-}
-
 // Chain path: chunks of whole 8*aa-row groups, workspace sized for the worst
 // case (every sample recording every level) so no queue can overflow; the
 // arenas of all slots together stay within the scene's workspace budget
@@ -721,14 +600,14 @@ struct ChainPlan {
     size_t cap = 0;                 // samples of the launch
     int G = 1, gb = 0, levels_a = 1, kinline = 0;
     bool phase_b = false, split_occ = false;
-    unsigned dyn_units = 0, scapA = 0, ccapA = 0, scapB = 0, wq_cap = 0;
+    unsigned dyn_units = 0, scapA = 0, ccapA = 0, scapB = 0;
     int la = 1, tchunk = 1;         // levels stored per sample; phase-B continuation chunk
     size_t cb = 0;                  // continuations with phase-B records
     // arena offsets
     size_t dbase = 0;               // records below it without directions (pathchain.hpp)
     int clevels = 0;
     size_t o_rec = 0, o_recd = 0, o_pinfo = 0, o_occ = 0, o_sqA = 0, o_scntA = 0, o_sflatA = 0, o_cq = 0, o_ccnt = 0,
-           o_cflat = 0, o_sqB = 0, o_scntB = 0, o_sflatB = 0, o_totals = 0, o_wq = 0, o_cid = 0, o_tail = 0,
+           o_cflat = 0, o_sqB = 0, o_scntB = 0, o_sflatB = 0, o_totals = 0, o_cid = 0, o_tail = 0,
            o_fbc = 0, o_fbs = 0, bytes = 0;
 };
 
@@ -754,13 +633,11 @@ ChainGeom chain_geom(const rt_scene* s, const rtk::FrameParams& f) {
 // The kernels' grids from their occupancy (once per scene).
 int ensure_chain_grids(rt_scene* s) {
     if (s->chain_grid != 0) return RT_OK;
-    int cb = 0, mb = 0, ob = 0, fb = 0;
+    int cb = 0, mb = 0, ob = 0;
     HIP_TRY(rtc::chain_occupancy(&cb, &mb, &ob));
-    HIP_TRY(rtc::fused_occupancy(&fb));
     s->chain_grid = std::min(rtc::kMaxChainGrid, std::max(1, cb) * s->num_cus);
     s->mix_grid = std::max(1, mb) * s->num_cus;
     s->occl_grid = std::max(1, ob) * s->num_cus;
-    s->fused_grid = std::max(1, fb) * s->num_cus;
     if (const char* e = std::getenv("RT_CGRID")) s->chain_grid = std::max(1, std::min(rtc::kMaxChainGrid, std::atoi(e)));
     if (const char* e = std::getenv("RT_OGRID")) s->occl_grid = std::max(1, std::atoi(e));
     if (const char* e = std::getenv("RT_MGRID")) s->mix_grid = std::max(2, std::atoi(e));
@@ -770,9 +647,8 @@ int ensure_chain_grids(rt_scene* s) {
 // Every size of a launch of `nunits` row units, and its arena layout: worst-case queue sizing (every
 // sample recording every level), so no queue can overflow.  (ensure_chain_grids first.)
 ChainPlan chain_plan(const rt_scene* s, const ChainGeom& g, size_t nunits, bool count, size_t cb_want = 0) {
-    const bool fused = s->path == rt_scene::kFused;
     const int levels = g.levels, nl = g.nl;
-    const int max_grid = fused ? s->fused_grid : s->chain_grid;
+    const int max_grid = s->chain_grid;
     ChainPlan P;
     P.cap = nunits * g.unit_samples;
     const size_t cap = P.cap;
@@ -800,7 +676,7 @@ ChainPlan chain_plan(const rt_scene* s, const ChainGeom& g, size_t nunits, bool 
     P.ccapA = units_a * 256u;
     // records: levels [0, la) for every sample; deeper ones (phase B) for the first cb continuations
     // (the rest finish in k_fallback; counting passes keep every one: cb = cap)
-    P.la = fused || !P.phase_b ? levels : P.levels_a;
+    P.la = !P.phase_b ? levels : P.levels_a;
     // (at least cap / RT_CONT_DEN, more once frame batches report a larger continuation share: that share
     // + 10 %)
     const size_t cb_guess = std::max(cap / (size_t)std::max(1, s->tune_cont_den),
@@ -814,15 +690,13 @@ ChainPlan chain_plan(const rt_scene* s, const ChainGeom& g, size_t nunits, bool 
         const size_t per_wg = P.gb > 0 ? (nch + P.gb - 1) / P.gb * ch : 0;
         P.scapB = P.phase_b ? (unsigned)(per_wg * (size_t)(levels - P.la) * nl) : 0u;
     }
-    P.wq_cap = fused ? rtc::fused_wave_qcap((int)std::min<size_t>(cap, INT32_MAX), P.G, levels, nl) : 0u;
     const size_t nrec = cap * P.la + P.cb * (levels - P.la);
     ArenaLayout L;
     // phase A's records without their directions where k_finish can rebuild them (pathchain.hpp dbase)
-    // (not with RT_ABANDON: its restarts reflect phase-A records no direction was kept for)
     // (frame batches by default: a lone frame's k_finish is on its critical path and the rebuilt
     // directions cost it more than the saved bytes; RT_COMPACT=2 everywhere, 0 nowhere)
     const bool cmp = s->tune_compact == 2 || (s->tune_compact == 1 && g.nframes > 1);
-    P.clevels = !fused && cmp && s->tune_abandon == 0 ? std::min(P.la, rtc::kCompactLevels) : 0;
+    P.clevels = cmp ? std::min(P.la, rtc::kCompactLevels) : 0;
     P.dbase = cap * (size_t)P.clevels;
     P.o_rec = L.take<float4>(nrec);
     P.o_recd = L.take<float4>(nrec - P.dbase);
@@ -832,9 +706,7 @@ ChainPlan chain_plan(const rt_scene* s, const ChainGeom& g, size_t nunits, bool 
     P.o_tail = L.take<float4>(cap);
     P.o_fbc = L.take<unsigned>(cap);
     P.o_fbs = L.take<unsigned>(cap);
-    if (fused) {
-        P.o_wq = L.take<unsigned>((size_t)P.G * 4 * P.wq_cap);
-    } else {
+    {
         P.o_sqA = L.take<unsigned>((size_t)P.G * P.scapA); P.o_scntA = L.take<unsigned>(P.G);
         P.o_sflatA = L.take<unsigned>(cap * P.levels_a * nl);
         P.o_cq = L.take<unsigned>((size_t)P.G * P.ccapA); P.o_ccnt = L.take<unsigned>(P.G);
@@ -904,14 +776,25 @@ void poll_cont(rt_scene* s, bool wait) {
     }
 }
 
+// A launch's continuation count (k_pack_a's total, or a frame's chunk peak) copied to pinned memory behind
+// it on `st`; poll_cont folds it into the scene's continuation share once the copy is done.
+int read_back_cont(rt_scene* s, hipStream_t st, int slot, const unsigned* src, size_t cap) {
+    if (!s->h_cont) HIP_TRY(hipHostMalloc(reinterpret_cast<void**>(&s->h_cont), rt_scene::kSlots * sizeof(unsigned)));
+    if (!s->cont_ev[slot]) HIP_TRY(hipEventCreateWithFlags(&s->cont_ev[slot], hipEventDisableTiming));
+    HIP_TRY(hipMemcpyAsync(&s->h_cont[slot], src, sizeof(unsigned), hipMemcpyDeviceToHost, st));
+    HIP_TRY(hipEventRecord(s->cont_ev[slot], st));
+    s->cont_cap[slot] = cap;
+    s->cont_pending[slot] = true;
+    return RT_OK;
+}
+
 int render_chain(rt_scene* s, const rtk::Eye& eye, const rtk::FrameParams& f, bool count, hipStream_t st,
                  int slot = 0) {
     rt_scene::Arena& arena = s->arenas[slot];
     const ChainGeom g = chain_geom(s, f);
     const int levels = g.levels, nl = g.nl, wi = g.wi, tiles_x = g.tiles_x, li = g.li, unit = g.unit;
-    const bool fused = s->path == rt_scene::kFused;
     if (const int rc = ensure_chain_grids(s)) return rc;
-    const int max_grid = fused ? s->fused_grid : s->chain_grid;
+    const int max_grid = s->chain_grid;
     auto grid_for = [&](int n0) { return std::max(1, std::min(max_grid, (n0 + 255) / 256)); };
     size_t cb = 0;
     // read-backs of earlier frames' chunks (C5-sized lone frames); never for a frame batch: its frame count
@@ -931,7 +814,7 @@ int render_chain(rt_scene* s, const rtk::Eye& eye, const rtk::FrameParams& f, bo
     // a frame of several chunks reports its chunks' largest continuation share (the record space must
     // hold the mirror-heavy chunks', not the last chunk's): k_pack_a's atomicMax into one word, cleared
     // here, on the caller's stream before the chunks fork
-    const bool peak = nchunks > 1 && !count && !fused && P.phase_b && s->tune_cont_cb == 0;
+    const bool peak = nchunks > 1 && !count && P.phase_b && s->tune_cont_cb == 0;
     if (peak && f.chunk_k == 1) {
         if (!s->d_cont_peak) HIP_TRY(hipMalloc(reinterpret_cast<void**>(&s->d_cont_peak), sizeof(unsigned)));
         HIP_TRY(hipMemsetAsync(s->d_cont_peak, 0, sizeof(unsigned), st));
@@ -951,6 +834,9 @@ int render_chain(rt_scene* s, const rtk::Eye& eye, const rtk::FrameParams& f, bo
             HIP_TRY(hipEventRecord(s->slot_done[j], s->slot_stream[j]));
             HIP_TRY(hipStreamWaitEvent(st, s->slot_done[j], 0));
         }
+        // the frame's chunk peak, once every slot's chunks have folded theirs in (a read-back per
+        // sub-call could miss other slots' pending atomicMax)
+        if (peak) return read_back_cont(s, st, slot, s->d_cont_peak, cap);
         return RT_OK;
     }
     // order this use after the arena's previous one (possibly on another stream)
@@ -963,9 +849,10 @@ int render_chain(rt_scene* s, const rtk::Eye& eye, const rtk::FrameParams& f, bo
         (void)hipFree(arena.p);
         arena.p = nullptr;
         arena.bytes = 0;
-        // (+1/16: a slightly larger plan later -- the measured record space moving -- fits without another
-        // synchronising reallocation)
-        const size_t want = P.bytes + P.bytes / 16;
+        // (+1/16, within the slot's share of the budget: a slightly larger plan later -- the measured record
+        // space moving -- fits without another synchronising reallocation; ADVICE r4: the headroom is part
+        // of the budget, not on top of it)
+        const size_t want = std::min(P.bytes + P.bytes / 16, std::max(P.bytes, s->slot_budget()));
         HIP_TRY(hipMalloc(reinterpret_cast<void**>(&arena.p), want));
         arena.bytes = want;
     }
@@ -1005,25 +892,18 @@ int render_chain(rt_scene* s, const rtk::Eye& eye, const rtk::FrameParams& f, bo
     p.occ_grid = s->occl_grid;
     p.fin_grid = s->tune_fgrid > 0 ? s->tune_fgrid : 8 * s->num_cus;
     p.split_occ = P.split_occ ? 1 : 0;
-    // A's shadow tasks walked where k_chain left them: by k_occlude in frame batches; by k_mix's shadow
-    // role in a lone frame only with RT_OCC_INPLACE=2 (its uneven regions cost k_mix +60 us, k_pack_a -10)
-    p.occ_inplace = !count && !fused && (P.split_occ ? s->tune_occ_inplace != 0 : s->tune_occ_inplace == 2) ? 1 : 0;
-    p.occ_inplace_b = !P.split_occ && !count && !fused && s->tune_occ_inplace ? 1 : 0;
+    // A's shadow tasks walked where k_chain left them by k_occlude in frame batches (a lone frame's k_mix
+    // shadow role deals them packed: in place, its uneven regions cost k_mix +60 us, k_pack_a -10); B's
+    // LDS-queue overflow likewise in a lone frame.  The in-place walks are the leaf-queue walker's
+    // (RT_LEAF_QUEUE builds), the only device code that reads task regions unpacked.
+    p.occ_inplace = RT_LEAF_QUEUE && !count && P.split_occ && s->tune_occ_inplace ? 1 : 0;
+    p.occ_inplace_b = RT_LEAF_QUEUE && !P.split_occ && !count && s->tune_occ_inplace ? 1 : 0;
     p.cont_peak = peak ? s->d_cont_peak : nullptr;
-    // lone frames in one launch: k_mix's shadow-role workgroups finish the pixels without a continued
-    // sample beside phase B (pathchain.hip k_mix); not with compact records (the rebuilt directions are
-    // k_finish<true>'s) nor beside other chunks' kernels (its workgroups wait for each other, bounded)
-    p.early_fin = !P.split_occ && !count && !fused && P.phase_b && P.clevels == 0 && units == g.units_total &&
-                  RT_EARLY_FIN_BUILD && s->tune_early_fin ? s->tune_early_fin : 0;
     p.refill = s->tune_refill >= 0 ? s->tune_refill : 0;
     p.service = s->tune_service >= 0 ? s->tune_service : 64;
     p.bservice = s->tune_bservice;
     p.btail = s->tune_btail;
     p.bq_cap = std::min(s->tune_bq_cap, rtc::kMaxBq);
-    p.coop = s->tune_coop;
-    p.coop_live = s->tune_coop_live;
-    p.coop_tail = s->tune_coop_tail;
-    p.producers = s->tune_producers;
     p.orefill = s->tune_orefill;
     p.brefill = s->tune_brefill;
     p.bprio = s->tune_bprio;
@@ -1031,16 +911,10 @@ int render_chain(rt_scene* s, const rtk::Eye& eye, const rtk::FrameParams& f, bo
     // the phase-B workgroups: 1.12 -> 1.10 ms; 2: 1.11-1.14, 4: 1.12-1.13), in chunks of 128 in batches
     p.tchunk = P.tchunk;
     p.ochunk = s->tune_ochunk;
-    p.packet = s->tune_packet && s->bvh.max_stack <= dl::kMaxStack;
-    p.exp_skip_occ = std::getenv("RT_EXP_SKIP_OCC") ? 1 : 0;
     p.lq_wait = std::getenv("RT_LQ_WAIT") ? std::max(1, std::min(64, std::atoi(std::getenv("RT_LQ_WAIT")))) : 32;
-    p.spread = s->tune_spread;
     p.dyn_units = (int)P.dyn_units;
     p.ublk_h = s->tune_ublk_h;
     p.ublk_w = std::max(1, s->tune_ublk_w);
-    p.crefill = s->tune_crefill;
-    p.wq = static_cast<unsigned*>(at(P.o_wq));
-    p.wq_cap = P.wq_cap;
     p.out = f.out; p.counters = f.counters;
     p.out_k = f.out_k; p.out_j = f.out_j;
     p.nframes = std::max(1, f.nframes);
@@ -1057,7 +931,7 @@ int render_chain(rt_scene* s, const rtk::Eye& eye, const rtk::FrameParams& f, bo
     p.trace = trace_buffer(s, trace_n);
     // lone frames in one launch (a drop-in caller's repeated frames): phase-A units heaviest-first by the
     // previous frame of the same geometry (PcParams::uorder), and this frame's costs ranked for the next
-    const bool hot = s->tune_hot_units && !count && !fused && p.nframes == 1 && P.dyn_units > 0 &&
+    const bool hot = s->tune_hot_units && !count && p.nframes == 1 && P.dyn_units > 0 &&
                      units == g.units_total && !p.trace;
     p.urank = p.uorder_on = 0;
     for (int r0 = f.chunk_j * chunk_rows; r0 < li; r0 += f.chunk_k * chunk_rows) {
@@ -1096,14 +970,8 @@ int render_chain(rt_scene* s, const rtk::Eye& eye, const rtk::FrameParams& f, bo
             p.uorder_on = arena.hist_key == key ? 1 : 0;   // ranked by the previous frame of this geometry
             arena.hist_key = key;                          // (its k_pack_a ran before this k_chain: stream order)
         }
-        // phase A's stragglers hand their walks to phase B once this share of k_chain's waves is done
-        p.abandon = s->tune_abandon > 0 && !count && P.phase_b && !P.split_occ   // lone frames (k_mix with the BQ)
-                        ? (unsigned)std::max<long long>(1, (long long)p.grid * 4 * s->tune_abandon / 1000)   // 4 waves per 256-thread workgroup
-                        : 0u;
         if (p.grid > P.G) return fail(RT_ERR_LIMIT, "internal: chain grid exceeds the workspace");
-        if (fused) {
-            HIP_TRY(rtc::launch_fused_chunk(s->dev, eye, p, count, st));
-        } else if (s->ktime) {
+        if (s->ktime) {
             // diagnostics: events between the kernels, then the launch's per-kernel split (synchronous)
             for (int i = 0; i < rtc::KTimer::kMax; ++i)
                 if (!s->kt.ev[i]) HIP_TRY(hipEventCreate(&s->kt.ev[i]));
@@ -1120,14 +988,10 @@ int render_chain(rt_scene* s, const rtk::Eye& eye, const rtk::FrameParams& f, bo
             HIP_TRY(rtc::launch_chain_chunk(s->dev, eye, p, count, st));
         }
     }
-    if (!count && !fused && P.phase_b && (p.nframes > 1 || chunk_rows < li) && s->tune_cont_cb == 0) {   // the share, read back later
-        if (!s->h_cont) HIP_TRY(hipHostMalloc(reinterpret_cast<void**>(&s->h_cont), rt_scene::kSlots * sizeof(unsigned)));
-        if (!s->cont_ev[slot]) HIP_TRY(hipEventCreateWithFlags(&s->cont_ev[slot], hipEventDisableTiming));
-        HIP_TRY(hipMemcpyAsync(&s->h_cont[slot], p.cont_peak ? p.cont_peak : p.totals + 1, sizeof(unsigned),
-                               hipMemcpyDeviceToHost, st));
-        HIP_TRY(hipEventRecord(s->cont_ev[slot], st));
-        s->cont_cap[slot] = cap;
-        s->cont_pending[slot] = true;
+    // the share, read back later (a chunk of a forked frame: the parent call reads the frame's peak)
+    if (!count && P.phase_b && (p.nframes > 1 || chunk_rows < li) && s->tune_cont_cb == 0 && f.chunk_k == 1) {
+        const int rc = read_back_cont(s, st, slot, p.cont_peak ? p.cont_peak : p.totals + 1, cap);
+        if (rc) return rc;
     }
     if (p.trace) trace_dump(s, st, 0, (unsigned)cap, (unsigned)p.trace_blocks, trace_n);   // last chunk only
     if (!arena.last) HIP_TRY(hipEventCreateWithFlags(&arena.last, hipEventDisableTiming));
@@ -1311,7 +1175,7 @@ int rt_scene_export_nodes(const rt_scene* s, void* out, int capacity) {
 
 int rt_scene_memory(const rt_scene* s, uint64_t* scene_bytes, uint64_t* workspace_bytes) {
     if (!s) return fail(RT_ERR_ARG, "scene is NULL");
-    size_t ws = s->ws.bytes + s->out_cap + s->batch_out_cap + s->trace_cap * sizeof(unsigned);
+    size_t ws = s->out_cap + s->batch_out_cap + s->trace_cap * sizeof(unsigned);
     for (const auto& a : s->arenas) ws += a.bytes;
     if (scene_bytes) *scene_bytes = s->host_only ? 0 : s->scene_bytes;
     if (workspace_bytes) *workspace_bytes = ws;
@@ -1379,19 +1243,10 @@ int render_frame(rt_scene* s, const rt_camera* cam, int aa, int stripe_rows, int
     p.slab_rows = rt_slab_rows(cam->image_height, stripe_rows, nranks);
     p.out = static_cast<uint8_t*>(out_dev);
     p.counters = s->d_counters;
-    p.trace = nullptr;
     const bool count = (flags & RT_RENDER_COUNT) != 0;
-    if (s->path == rt_scene::kMegakernel) {
-        const size_t trace_n = 2 * (size_t)p.slab_rows * p.width;
-        p.trace = trace_buffer(s, trace_n);
-        HIP_TRY(rtk::launch_render(s->dev, eye, p, count, stream));
-        if (p.trace) trace_dump(s, stream, 2, (unsigned)p.width, (unsigned)p.slab_rows, trace_n);
-        return RT_OK;
-    }
-    if (s->path == rt_scene::kWavefront) return render_wavefront(s, eye, p, count, stream);
     const int K = std::min(rt_scene::kSlots, std::max(1, s->tune_split));
     const long long samples = (long long)p.slab_rows * p.width * aa * aa;
-    if (split_ok && s->path == rt_scene::kChain && K > 1 && samples >= kSplitMinSamples)
+    if (split_ok && K > 1 && samples >= kSplitMinSamples)
         return render_split(s, eye, p, count, stream, K);
     return render_chain(s, eye, p, count, stream, slot);
 }
@@ -1439,25 +1294,23 @@ int render_batch(rt_scene* s, const rt_camera* cams, int n, int aa, int stripe_r
     p.outs = reinterpret_cast<uint8_t* const*>(outs_dev);
     p.out = static_cast<uint8_t*>(outs_dev[0]);
     p.counters = s->d_counters;
-    p.trace = nullptr;
     return render_chain(s, eyes[0], p, (flags & RT_RENDER_COUNT) != 0, stream, slot);
 }
 
 // stripe_rows <= 0: whole frames (each camera's own height); otherwise every
-// frame is this rank's row stripes (rt_render_frames_device).
+// frame is this rank's row stripes (rt_render_frames_device).  may_wait: a synchronous entry point
+// (rt_render_cameras), which may wait on the host for a scene's first batch (below).
 int render_cameras(rt_scene* s, const rt_camera* cams, int n, int aa, void* const* outs_dev, hipStream_t stream,
-                   int flags, int stripe_rows = 0, int rank = 0, int nranks = 1, int batch_max = 0,
-                   int slot0 = 0) {
+                   int flags, int stripe_rows = 0, int rank = 0, int nranks = 1, bool may_wait = false,
+                   int batch_max = 0, int slot0 = 0) {
     auto rows_of = [&](int i) { return stripe_rows > 0 ? stripe_rows : cams[i].image_height; };
-    const bool batching = (s->path == rt_scene::kChain || s->path == rt_scene::kFused) && n > 1 &&
-                          s->tune_batch > 1;
+    const bool batching = n > 1 && s->tune_batch > 1;
     if (batching) {
         // consecutive same-size frames, up to kMaxFrames and one chain chunk of samples per batch
-        // at least nslot batches when the frames allow (concurrent batches overlap each other's tails)
         const int nslot = std::max(1, std::min(s->tune_slots, rt_scene::kSlots));
         // (batch_max, slot0: the rest of a call after its first batch, on the next slots -- batches of the
         // same size as the calls that follow, on every slot, so no workspace grows inside those)
-        const int bmax = std::min({s->tune_batch, rtc::kMaxFrames, batch_max > 0 ? batch_max : (n + nslot - 1) / nslot});
+        const int bmax = std::min({s->tune_batch, rtc::kMaxFrames, batch_max > 0 ? batch_max : rtc::kMaxFrames});
         std::vector<int> starts;
         HIP_TRY(hipSetDevice(s->device));
         if (const int rc = ensure_chain_grids(s)) return rc;
@@ -1469,6 +1322,12 @@ int render_cameras(rt_scene* s, const rt_camera* cams, int n, int aa, void* cons
             if (!s->slot_done[k]) HIP_TRY(hipEventCreateWithFlags(&s->slot_done[k], hipEventDisableTiming));
         }
         poll_cont(s, false);
+        // runs of consecutive same-size frames; a run of L frames goes out as nb batches of (nearly) equal
+        // size, nb = max(min(nslot, L), ceil(L / m)) where m is the most frames one launch's plan fits in the
+        // slot's workspace share (at most bmax): every slot busy when the run allows (concurrent batches
+        // overlap each other's tails), and no slot with more frames than another (a 20-frame call on 6
+        // slots: 4,4,3,3,3,3 rather than 4,4,4,4,4 on 5; RT_BALANCE=0: the greedy m-frame batches)
+        const bool balance = s->tune_balance;
         for (int i = 0; i < n;) {
             const auto& c = cams[i];
             // a batch of k frames: one launch (render_chain's own plan fits the slot's workspace share)
@@ -1481,27 +1340,36 @@ int render_cameras(rt_scene* s, const rt_camera* cams, int n, int aa, void* cons
                 const ChainGeom g = chain_geom(s, f);
                 return chain_launch_units(s, g, (flags & RT_RENDER_COUNT) != 0) >= g.units_total;
             };
-            int j = i + 1;
-            while (j < n && j - i < bmax &&
-                   cams[j].image_width == c.image_width && cams[j].image_height == c.image_height && fits(j - i + 1))
-                ++j;
-            starts.push_back(i);
-            i = j;
+            int L = 1;
+            while (i + L < n && cams[i + L].image_width == c.image_width && cams[i + L].image_height == c.image_height)
+                ++L;
+            int m = 1;
+            while (m < std::min(bmax, L) && fits(m + 1)) ++m;
+            if (balance) {
+                const int nbr = std::max(std::min(nslot, L), (L + m - 1) / m);
+                for (int b = 0; b < nbr; ++b) starts.push_back(i + (int)((long long)L * b / nbr));
+            } else {                               // round 4: batches of min(m, ceil(L / nslot)) frames
+                const int ch = std::min(m, (L + nslot - 1) / nslot);
+                for (int b = 0; b < L; b += ch) starts.push_back(i + b);
+            }
+            i += L;
         }
         starts.push_back(n);
         const int nb = (int)starts.size() - 1;
         if (nb == 1) return render_batch(s, cams, n, aa, rows_of(0), rank, nranks, outs_dev, stream, flags, 0);
-        if (s->cont_frac == 0 && !(flags & RT_RENDER_COUNT) && s->tune_cont_cb == 0 &&
+        if (may_wait && s->cont_frac == 0 && !(flags & RT_RENDER_COUNT) && s->tune_cont_cb == 0 &&
             s->dev.max_depth > s->tune_kinline) {
             // the scene's continuation share is not known yet: one batch first, waited for, so the rest
             // are sized by it (once per scene; a mirror-heavy scene otherwise sends most of its deep
-            // chains to k_fallback until the first read-backs arrive)
+            // chains to k_fallback until the first read-backs arrive).  Synchronous callers only (ADVICE
+            // r4): the asynchronous entries never block the caller's stream; their first call runs with
+            // the default record space and the later calls are sized by the read-backs that are done.
             const int rc = render_batch(s, cams, starts[1], aa, rows_of(0), rank, nranks, outs_dev, stream, flags, 0);
             if (rc) return rc;
             poll_cont(s, true);
             s->cont_frac = std::max(s->cont_frac, 1e-9);
             return render_cameras(s, cams + starts[1], n - starts[1], aa, outs_dev + starts[1], stream, flags,
-                                  stripe_rows, rank, nranks, bmax, 1);
+                                  stripe_rows, rank, nranks, may_wait, starts[2] - starts[1], 1);
         }
         if (!s->fork_ev) HIP_TRY(hipEventCreateWithFlags(&s->fork_ev, hipEventDisableTiming));
         HIP_TRY(hipEventRecord(s->fork_ev, stream));
@@ -1525,8 +1393,7 @@ int render_cameras(rt_scene* s, const rt_camera* cams, int n, int aa, void* cons
         }
         return RT_OK;
     }
-    const bool conc = s->path == rt_scene::kChain && n > 1;
-    if (!conc) {
+    if (n == 1) {
         for (int i = 0; i < n; ++i) {
             const int rc = render_frame(s, &cams[i], aa, rows_of(i), rank, nranks, outs_dev[i], stream, flags, 0);
             if (rc) return rc;
@@ -1637,7 +1504,7 @@ int rt_render_cameras(rt_scene* s, const rt_camera* cams, int n, int aa, uint8_t
     for (int i = 0; i < n; ++i) dev[i] = s->batch_out + off[i];
     const bool count = stats != nullptr;
     if (count) HIP_TRY(hipMemset(s->d_counters, 0, rtc::kCounters * sizeof(unsigned long long)));
-    int rc = render_cameras(s, cams, n, aa, dev.data(), nullptr, count ? RT_RENDER_COUNT : 0);
+    int rc = render_cameras(s, cams, n, aa, dev.data(), nullptr, count ? RT_RENDER_COUNT : 0, 0, 0, 1, true);
     if (rc == RT_OK) {
         HIP_TRY(hipDeviceSynchronize());
         for (int i = 0; i < n; ++i)

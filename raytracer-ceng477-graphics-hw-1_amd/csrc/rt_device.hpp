@@ -182,14 +182,4 @@ __device__ __forceinline__ V sphere_normal(const Ray& r, const float4 c, float r
     return nrm(divs(sub(p, V{c.x, c.y, c.z}), radius));     // :91
 }
 
-// Wave issue priority from the deepest recursion level among the active
-// lanes: deep mirror chains are the frame's critical path, so their waves win
-// VALU/memory issue arbitration over waves still on shallow work.
-__device__ __forceinline__ void wave_priority(int level) {
-    if (__any(level >= 3)) __builtin_amdgcn_s_setprio(3);
-    else if (__any(level >= 2)) __builtin_amdgcn_s_setprio(2);
-    else if (__any(level >= 1)) __builtin_amdgcn_s_setprio(1);
-    else __builtin_amdgcn_s_setprio(0);
-}
-
 }  // namespace rtd

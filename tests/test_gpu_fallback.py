@@ -14,11 +14,6 @@ branch of it and compare with the reference goldens (raytracer.cpp:385-452):
     scanned by k_fallback);
   * RT_COMPACT=0 with RT_CONT_CB=1000: full 32-B phase-A records (the compact
     16-B records leave the directions of continued paths in tail[]);
-  * RT_ABANDON=1: phase A's unfinished walks restart in phase B (eye rays as
-    kFbEye continuations, level-1 walks as reflections of their level-0 record),
-    alone and with RT_CONT_CB=1000 (the restarts beyond it in k_fallback);
-  * RT_EARLY_FIN=1 / 2: a lone frame's early finish in k_mix, with its wait /
-    without it (builds with RT_EARLY_FIN_BUILD=1).
 """
 from __future__ import annotations
 
@@ -40,11 +35,6 @@ def torch_cuda():
 
 
 ENVS = [
-    # phase A's stragglers handed to phase B (pathchain.hip p.abandon) after 1 of 1000 k_chain waves has
-    # finished: nearly every walk restarts in phase B (eye rays and level-1 reflections as continuations)
-    {"RT_ABANDON": "1"},
-    # the same with a phase-B record space of 1,000: the restarted walks beyond it finish in k_fallback
-    {"RT_ABANDON": "1", "RT_CONT_CB": "1000"},
     {"RT_FORCE_FALLBACK": "1"},
     {"RT_FORCE_FALLBACK": "2"},
     {"RT_FORCE_FALLBACK": "3"},
@@ -53,16 +43,6 @@ ENVS = [
     # and k_fallback read the stored direction words instead of the chain's tail copies
     {"RT_COMPACT": "0", "RT_CONT_CB": "1000"},
     {"RT_FORCE_FALLBACK": "2", "RT_FBS_CAP": "64"},
-    # a lone frame's early finish (RT_EARLY_FIN in builds with RT_EARLY_FIN_BUILD=1, off by default and
-    # not built by default: these then run the default path; k_mix's shadow-role workgroups finish the
-    # pixels without a continued sample, k_finish the rest and what k_fallback changed): with deferred
-    # paths and shadow rays, with continuations beyond the record space, and without the wait for the
-    # other workgroups (k_finish takes most pixels), alone and with the fallback shadow queue overflowing
-    # (every pixel finished again)
-    {"RT_EARLY_FIN": "1", "RT_FORCE_FALLBACK": "3"},
-    {"RT_EARLY_FIN": "1", "RT_CONT_CB": "1000"},
-    {"RT_EARLY_FIN": "2"},
-    {"RT_EARLY_FIN": "2", "RT_FORCE_FALLBACK": "2", "RT_FBS_CAP": "64"},
 ]
 
 

@@ -13,7 +13,7 @@ import pytest
 
 from conftest import GOLDEN_DIR, config_path, golden_by_name, load_golden_image
 
-PATHS = ["fused", "chain", "wavefront", "megakernel"]
+PATHS = ["chain"]
 from test_oracle import CPU_GOLDENS
 
 pytestmark = pytest.mark.gpu
@@ -246,7 +246,7 @@ def test_full_size_c5_sha(name, path, goldens, pkg, scene_dir, torch_cuda):
     assert _stats(st) == _counters(cam_g["counters"])
 
 
-@pytest.mark.parametrize("path", ["chain", "fused", "megakernel"])
+@pytest.mark.parametrize("path", PATHS)
 @pytest.mark.parametrize("name", ["cornellbox_aa1", "car_aa1", "hm_verbatim_aa2"])
 def test_render_cameras_batched(name, path, goldens, pkg, scene_dir, torch_cuda):
     # (f4) multi-camera batching (raytracer.cpp:505-519): every camera of the scene in one call,
@@ -269,7 +269,7 @@ def test_render_cameras_batched(name, path, goldens, pkg, scene_dir, torch_cuda)
 
 
 @pytest.mark.parametrize("batch", ["16", "1"])
-@pytest.mark.parametrize("path", ["chain", "fused"])
+@pytest.mark.parametrize("path", PATHS)
 @pytest.mark.parametrize("nranks,nframes,gname", [(1, 2, "C3_hm_1080p_d6_aa1"), (8, 8, "C3_hm_1080p_d6_aa1"),
                                                   (3, 5, "C3_hm_1080p_d6_aa1"), (8, 3, "C3_hm_1080p_d6_aa2"),
                                                   (2, 17, "C3_hm_1080p_d6_aa1")])
@@ -355,7 +355,7 @@ def test_render_frames_device_many_cameras(goldens, pkg, scene_dir, torch_cuda):
         assert not torch.equal(outs[0], outs[1])
 
 
-@pytest.mark.parametrize("path", ["chain", "fused"])
+@pytest.mark.parametrize("path", PATHS)
 def test_render_frames_device_mixed_cameras(path, goldens, pkg, scene_dir, torch_cuda):
     """One batch holding different cameras of one size (cornellbox's two 800x800 cameras),
     split over 2 ranks: each frame uses its own eye."""
