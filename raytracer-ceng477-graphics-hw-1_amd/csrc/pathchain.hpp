@@ -85,6 +85,7 @@ enum CounterSlot : int {
     kCntFbChains,         //   closest-hit rays deferred (not in range of the wide trees' slab test)
     kCntFbShadows,        //   shadow rays deferred
     kCntFbOvfScans,       //   launches whose fallback shadow queue overflowed (occlusion bytes scanned)
+    kCntFbTail,           //   phase-B chains handed to k_tail
 };
 
 // Phase-A levels whose records may leave out the direction (PcParams::dbase): k_finish rebuilds them
@@ -111,8 +112,11 @@ __host__ __device__ inline unsigned unit_col(int tiles_x, int ublk_h, int ublk_w
 }
 
 // PcParams::totals words: packed task counts (0-2), the phase-A unit counter (3), k_fallback's chain /
-// shadow counts and shadow-queue overflow (4-6), the rest spare.
-constexpr int kTotalsWords = 12;
+// shadow counts and shadow-queue overflow (4-6), phase B's tail entries (7), k_tail's entry counter (8),
+// k_mix's dynamic shadow-chunk counter (10); phase B's ended chains in 8 shards, one 128-B line each
+// (kLiveShard0 + kLiveStride * i: a wave adds to shard blk % 8).
+constexpr int kLiveShard0 = 32, kLiveStride = 32;
+constexpr int kTotalsWords = kLiveShard0 + 8 * kLiveStride;
 
 // Unit cost classes (PcParams::ucost): the most phase-A walk steps a sample of the unit took.
 constexpr unsigned kHotSteps[2] = {96, 32};
@@ -216,6 +220,16 @@ struct PcParams {
     // (new fields at the end: kernel arguments are loaded in runs of neighbours, so a field inserted
     // among the walk kernels' ones changed their SGPR spills 28 -> 67)
     unsigned* cont_peak;  // frames of several chunks: the most continuations of one chunk (k_pack_a, atomicMax)
+    // Phase B's tail (pathchain.hip k_tail): once at most tail_live of the launch's phase-B chains are left (0:
+    // never), a k_mix chain wave with no continuation left to take hands its chains on, each as the record id
+    // whose reflection is its next ray, into tailq (totals[7] entries, at most cb); k_tail walks each on a
+    // whole wave, tail_grid one-wave workgroups
+    unsigned* tailq;
+    int tail_live;
+    int tail_grid;
+    int tail_all;     // tests: every chain handed on at its first phase-B walk, exhausted or not
+    int dchunk;       // k_mix (lone frames): A's shadow tasks dealt dynamically in chunks of this many (totals[10]),
+                      // the chain workgroups joining once their chains are done; 0: static dealing
 };
 
 // Worst-case task-queue slots per workgroup: every sample of the workgroup
@@ -244,7 +258,7 @@ hipError_t launch_walk_timing(const rtk::DevScene& s, const float* rays, int n, 
 // Diagnostics (RT_KTIME=1 scenes, rt_kernel_times): HIP events recorded between the kernels of a
 // chain launch on its stream, so the host can split the launch's time per kernel (one slot: the
 // kernels run back to back).
-enum KernelKind : int { kKChain = 0, kKPackA, kKMix, kKOccA, kKPackB, kKOccB, kKFinish, kKFallback, kKEnd, kKKinds };
+enum KernelKind : int { kKChain = 0, kKPackA, kKMix, kKOccA, kKPackB, kKOccB, kKFinish, kKFallback, kKTail, kKEnd, kKKinds };
 struct KTimer {
     static constexpr int kMax = 16;
     hipEvent_t ev[kMax] = {};

@@ -136,6 +136,11 @@ struct rt_scene {
                                 // batches, and B's LDS-queue overflow in lone frames (0: packed)
     int tune_compact = 1;       // RT_COMPACT: phase-A records without directions (16 B instead of 32): 1 frame batches,
                                 // 2 every launch, 0 none
+    int tune_tail = 0;          // RT_TAIL: a lone frame's phase-B chains go to k_tail once at most this many are left (0: off)
+    int tune_tail_b = 0;        // RT_TAIL_B: the same in frame batches
+    int tune_tail_all = 0;      // RT_TAIL_ALL=1 (tests): every phase-B chain to k_tail at its first walk (where a tail is on)
+    int tune_dchunk = 0;        // RT_DCHUNK: a lone frame's A shadow tasks dealt dynamically in chunks of this many (0: static)
+    int tune_tail_grid = 0;     // RT_TAIL_GRID: k_tail's one-wave workgroups (0: 16 per CU)
     int tune_btail = 64;        // RT_BTAIL: the same once the continuations are exhausted (1: 1.24, 4: 1.18, 16: 1.15, 64: 1.14 ms)
     int tune_dyn = 1;           // RT_DYN_UNITS: phase-A waves take sample units from a launch-wide counter
     int tune_ublk_h = -1, tune_ublk_w = 8;  // RT_UBLK_H / RT_UBLK_W: phase-A unit column blocks (unit_order;
@@ -431,6 +436,11 @@ int upload_rest(rt_scene* s, const rt_options* opts) {
     if (const char* e = std::getenv("RT_FGRID")) s->tune_fgrid = std::max(0, std::atoi(e));
     if (const char* e = std::getenv("RT_BQ_CAP")) s->tune_bq_cap = std::max(0, std::atoi(e));
     if (const char* e = std::getenv("RT_BSERVICE")) s->tune_bservice = std::max(1, std::min(64, std::atoi(e)));
+    if (const char* e = std::getenv("RT_TAIL")) s->tune_tail = std::max(0, std::atoi(e));
+    if (const char* e = std::getenv("RT_TAIL_B")) s->tune_tail_b = std::max(0, std::atoi(e));
+    if (const char* e = std::getenv("RT_TAIL_ALL")) s->tune_tail_all = std::atoi(e) != 0;
+    if (const char* e = std::getenv("RT_TAIL_GRID")) s->tune_tail_grid = std::max(1, std::atoi(e));
+    if (const char* e = std::getenv("RT_DCHUNK")) s->tune_dchunk = std::max(0, std::atoi(e));
     if (const char* e = std::getenv("RT_BTAIL")) s->tune_btail = std::max(1, std::min(64, std::atoi(e)));
     if (const char* e = std::getenv("RT_COMPACT")) s->tune_compact = std::max(0, std::min(2, std::atoi(e)));
     if (const char* e = std::getenv("RT_OCC_INPLACE")) s->tune_occ_inplace = std::atoi(e) != 0;
@@ -607,7 +617,7 @@ struct ChainPlan {
     size_t dbase = 0;               // records below it without directions (pathchain.hpp)
     int clevels = 0;
     size_t o_rec = 0, o_recd = 0, o_pinfo = 0, o_occ = 0, o_sqA = 0, o_scntA = 0, o_sflatA = 0, o_cq = 0, o_ccnt = 0,
-           o_cflat = 0, o_sqB = 0, o_scntB = 0, o_sflatB = 0, o_totals = 0, o_cid = 0, o_tail = 0,
+           o_cflat = 0, o_sqB = 0, o_scntB = 0, o_sflatB = 0, o_totals = 0, o_cid = 0, o_tailq = 0, o_tail = 0,
            o_fbc = 0, o_fbs = 0, bytes = 0;
 };
 
@@ -713,6 +723,7 @@ ChainPlan chain_plan(const rt_scene* s, const ChainGeom& g, size_t nunits, bool 
         P.o_cflat = L.take<unsigned>(cap);
         P.o_sqB = L.take<unsigned>((size_t)P.gb * P.scapB); P.o_scntB = L.take<unsigned>(P.gb + 1);
         P.o_sflatB = L.take<unsigned>(P.cb * (levels - P.la) * nl);
+        P.o_tailq = L.take<unsigned>(P.phase_b ? P.cb : 0);
     }
     P.o_totals = L.take<unsigned>(rtc::kTotalsWords);
     P.bytes = L.off;
@@ -899,6 +910,19 @@ int render_chain(rt_scene* s, const rtk::Eye& eye, const rtk::FrameParams& f, bo
     p.occ_inplace = RT_LEAF_QUEUE && !count && P.split_occ && s->tune_occ_inplace ? 1 : 0;
     p.occ_inplace_b = RT_LEAF_QUEUE && !P.split_occ && !count && s->tune_occ_inplace ? 1 : 0;
     p.cont_peak = peak ? s->d_cont_peak : nullptr;
+    // phase B's last chains on one wave each (k_tail): production launches only (the counting passes walk
+    // the reference tree with the reference's counters)
+    p.tailq = static_cast<unsigned*>(at(P.o_tailq));
+    p.tail_live = !count && P.phase_b ? (P.split_occ ? s->tune_tail_b : s->tune_tail) : 0;
+    p.tail_grid = s->tune_tail_grid > 0 ? s->tune_tail_grid : 16 * s->num_cus;
+    p.tail_all = s->tune_tail_all;
+    p.dchunk = !count && !P.split_occ && RT_LEAF_QUEUE ? s->tune_dchunk : 0;
+    if (p.dchunk > 0) {   // every task reachable: k_mix's workgroups take at most kDynUnits chunks each; and at
+                          // least a wave's grab (64), which then holds at most one chunk's first task
+        const size_t worst = cap * (size_t)P.levels_a * nl, wgs = (size_t)std::max(1, s->mix_grid);
+        p.dchunk = (int)std::max<size_t>({(size_t)p.dchunk, 64,
+                                          (worst + wgs * rtc::kDynUnits - 1) / (wgs * rtc::kDynUnits)});
+    }
     p.refill = s->tune_refill >= 0 ? s->tune_refill : 0;
     p.service = s->tune_service >= 0 ? s->tune_service : 64;
     p.bservice = s->tune_bservice;
@@ -927,7 +951,7 @@ int render_chain(rt_scene* s, const rtk::Eye& eye, const rtk::FrameParams& f, bo
         p.fouts[i] = i < p.nframes && p.nframes > 1 ? f.outs[i] : f.out;
     }
     p.trace_blocks = std::max(s->mix_grid, s->occl_grid);
-    const size_t trace_n = 2 * (cap + (size_t)p.trace_blocks) + 4 * cap;
+    const size_t trace_n = 2 * (cap + (size_t)p.trace_blocks) + 4 * cap + 4 * (size_t)p.trace_blocks;
     p.trace = trace_buffer(s, trace_n);
     // lone frames in one launch (a drop-in caller's repeated frames): phase-A units heaviest-first by the
     // previous frame of the same geometry (PcParams::uorder), and this frame's costs ranked for the next
