@@ -522,6 +522,15 @@ __device__ __forceinline__ void tail_push(const PcParams& p, unsigned entry) {
     if (i < p.cb) p.tailq[i] = entry;
 }
 
+// A phase-A sample handed to k_tail_a: {sample | level << 31, the k_chain workgroup whose queue regions take
+// its tasks} (PcParams::tailqA, totals[11] entries, at most one per sample).  Its unit is marked heavy for the
+// next frame's dealing (the hand-off cut its step count short).
+__device__ __forceinline__ void tail_push_a(const PcParams& p, unsigned path, int level, unsigned blk, unsigned steps) {
+    const unsigned i = atomicAdd(&p.totals[11], 1u);
+    if (i < (unsigned)p.cap) p.tailqA[i] = make_uint2(path | ((unsigned)level << 31), blk);
+    if (p.urank) atomicMax(&p.ucost[path >> 8], max(steps, kHotSteps[0]));
+}
+
 // closest-hit chains of one phase (raytracer.cpp:385-439 minus the shading):
 // record each hit, queue its shadow tasks, follow (or hand on) mirrors.
 template <bool COUNT, bool CONT, bool BQ = CONT>
@@ -554,9 +563,13 @@ __device__ void chain_body(const rtk::DevScene& s, const rtk::Eye& e, const PcPa
     // phase B's tail (PcParams::tail_live): this wave hands its chains to k_tail (wave-uniform), once the launch's
     // live chains -- its continuations with records less those ended or handed on, counted in 8 sharded words
     // (kLiveShard0) -- are at most tail_live
+    // phase A likewise (PcParams::tail_a): once every unit is taken and at most tail_a started samples are
+    // still in phase A (word 2 of a shard counts the samples started, word 1 those ended), a wave hands its
+    // samples to k_tail_a
     bool to_tail = false, tail_go = false;
-    const unsigned nconts = CONT && !COUNT && p.tail_live > 0 ? min(p.totals[1], p.cb) : 0u;
-    unsigned* const live_shard = &p.totals[kLiveShard0 + kLiveStride * (blk & 7u)];
+    const bool tail_on = !COUNT && (CONT ? p.tail_live > 0 : p.tail_a > 0);
+    const unsigned nconts = CONT && tail_on ? min(p.totals[1], p.cb) : 0u;
+    unsigned* const live_shard = &p.totals[kLiveShard0 + kLiveStride * (blk & 7u) + (CONT ? 0 : 1)];
     (void)to_tail;
     (void)tail_go;
     (void)nconts;
@@ -564,7 +577,8 @@ __device__ void chain_body(const rtk::DevScene& s, const rtk::Eye& e, const PcPa
     StepStat stat;
     while (true) {
         // (1) epilogue of finished walks: record, queue shadow tasks, reflect or hand on
-        bool fin = false;        // phase B: this lane's chain ended or left for k_tail / k_fallback here
+        bool fin = false;        // this lane's chain ended here or left for k_tail(_a) / k_fallback / phase B
+        bool started = false;    // phase A: this lane took a sample here
         if (st == kDone) {
             const HitRec h = wk.best;
             const bool hit = h.prim >= 0;
@@ -644,8 +658,9 @@ __device__ void chain_body(const rtk::DevScene& s, const rtk::Eye& e, const PcPa
                     unsigned* tb = p.trace + 2 * ((size_t)p.cap + p.trace_blocks) + 4 * (size_t)path;
                     tb[0] = t_grab; tb[1] = (unsigned)wall_clock64(); tb[2] = (unsigned)k | ((wit - twit) << 8); tb[3] = tsteps;
                 }
-            } else if (CONT && !COUNT && to_tail) {   // the next level in k_tail: its ray is this record's reflection
-                tail_push(p, (unsigned)lvp);
+            } else if (!COUNT && to_tail) {   // the next level in k_tail(_a): its ray is this record's reflection
+                if (CONT) tail_push(p, (unsigned)lvp);
+                else tail_push_a(p, path, k + 1, blk, ssteps);
                 st = kIdle;
                 fin = true;
             } else {
@@ -662,12 +677,6 @@ __device__ void chain_body(const rtk::DevScene& s, const rtk::Eye& e, const PcPa
                 } else {
                     st = walk_begin<COUNT>(s, r, wk, w) ? kTrav : kDone;
                 }
-            }
-        }
-        if constexpr (CONT && !COUNT) {
-            if (p.tail_live > 0) {
-                const unsigned nf = (unsigned)__popcll(__ballot(fin));
-                if (nf && lane_id() == 0) atomicAdd(live_shard, nf);
             }
         }
         // (2) refill idle lanes with this workgroup's next samples / continuations
@@ -716,8 +725,12 @@ __device__ void chain_body(const rtk::DevScene& s, const rtk::Eye& e, const PcPa
                             k = (int)(lvp / (unsigned)p.cap) + 1;
                             r = reflect_from_record(s, p, lvp, path);
                             nrefl++;
-                            if (!COUNT && defer_closest(s, r)) fb_chain(p, lvp);
-                            else st = walk_begin<COUNT>(s, r, wk, w) ? kTrav : kDone;
+                            if (!COUNT && defer_closest(s, r)) {
+                                fb_chain(p, lvp);
+                                fin = true;
+                            } else {
+                                st = walk_begin<COUNT>(s, r, wk, w) ? kTrav : kDone;
+                            }
                         } else {
                             const unsigned idx = (dyn ? uid : blk + (v >> 8) * G) * 256u + (v & 255u);
                             if (slab_sample_ray(p, idx, &r)) {
@@ -726,10 +739,14 @@ __device__ void chain_body(const rtk::DevScene& s, const rtk::Eye& e, const PcPa
                                 ssteps = 0;
                                 if (kTraceBuild && p.trace) t_grab = (unsigned)wall_clock64();
                                 nprim++;
-                                if (s.max_depth < 0) p.pinfo[path] = 0 | (kEndZero << 8);   // depth 0 > max: black
-                                else if (!COUNT && defer_closest(s, r)) {
+                                started = true;
+                                if (s.max_depth < 0) {
+                                    p.pinfo[path] = 0 | (kEndZero << 8);   // depth 0 > max: black
+                                    fin = true;
+                                } else if (!COUNT && defer_closest(s, r)) {
                                     p.pinfo[path] = kPathCont;   // (k_fallback's path)
                                     fb_chain(p, kFbEye | path);
+                                    fin = true;
                                 }
                                 else st = walk_begin<COUNT>(s, r, wk, w) ? kTrav : kDone;
                             }
@@ -737,6 +754,11 @@ __device__ void chain_body(const rtk::DevScene& s, const rtk::Eye& e, const PcPa
                     }
                 }
             }
+        }
+        if (tail_on) {               // the live-chain counts (ended, and phase A's started)
+            const unsigned nf = (unsigned)__popcll(__ballot(fin)), ns = (unsigned)__popcll(__ballot(started));
+            if (nf && lane_id() == 0) atomicAdd(live_shard, nf);
+            if (!CONT && ns && lane_id() == 0) atomicAdd(live_shard + 1, ns);
         }
         if (!__any(st != kIdle)) {
             if (exhausted) break;
@@ -750,24 +772,32 @@ __device__ void chain_body(const rtk::DevScene& s, const rtk::Eye& e, const PcPa
             // phase B's tail starts once at most tail_live of the launch's chains are left (polled every 32
             // iterations by an exhausted wave): then most of the GPU is idle, and the chains left walk on whole
             // waves in k_tail instead of beside each other here
-            if (CONT && !COUNT && exhausted && p.tail_live > 0 && !tail_go && (poll++ & 31u) == 0u) {
+            if (tail_on && exhausted && !tail_go && (poll++ & 31u) == 0u) {
                 const int ln = lane_id();
-                unsigned v = ln < 8 ? __hip_atomic_load(&p.totals[kLiveShard0 + kLiveStride * ln], __ATOMIC_RELAXED,
+                const int wd = CONT ? 0 : 1;
+                unsigned v = ln < 8 ? __hip_atomic_load(&p.totals[kLiveShard0 + kLiveStride * ln + wd], __ATOMIC_RELAXED,
                                                         __HIP_MEMORY_SCOPE_AGENT)
                                     : 0u;
-                v += __shfl_xor(v, 1, 64);
-                v += __shfl_xor(v, 2, 64);
-                v += __shfl_xor(v, 4, 64);
-                tail_go = __shfl(v, 0, 64) + (unsigned)p.tail_live >= nconts;
+                unsigned u = !CONT && ln < 8 ? __hip_atomic_load(&p.totals[kLiveShard0 + kLiveStride * ln + 2],
+                                                                 __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
+                                             : 0u;
+#pragma unroll
+                for (int o = 1; o < 8; o <<= 1) {
+                    v += __shfl_xor(v, o, 64);
+                    u += __shfl_xor(u, o, 64);
+                }
+                const unsigned ended = __shfl(v, 0, 64), begun = CONT ? nconts : __shfl(u, 0, 64);
+                tail_go = ended + (unsigned)(CONT ? p.tail_live : p.tail_a) >= begun;
             }
             // phase B's tail: each chain hands on the walk it is on (k_tail restarts it from its ray, the reflection
             // of the previous level's record), and the lanes whose walk just finished record it and hand on the next
             // level (the epilogue above); (tail_all, tests: every chain's first phase-B walk, exhausted or not)
-            if (CONT && !COUNT && p.tail_live > 0 && ((exhausted && tail_go) || p.tail_all)) {
+            if (tail_on && ((exhausted && tail_go) || p.tail_all)) {
                 to_tail = true;
                 const bool tr = st == kTrav;
                 if (tr) {
-                    tail_push(p, (unsigned)rec_id(p, k - 1, path, cix));
+                    if (CONT) tail_push(p, (unsigned)rec_id(p, k - 1, path, cix));
+                    else tail_push_a(p, path, k, blk, ssteps);
                     st = kIdle;
                 }
                 const unsigned nf = (unsigned)__popcll(__ballot(tr));
@@ -973,12 +1003,15 @@ __device__ __forceinline__ void lq_flush(const rtk::DevScene& s, const Ray& r, f
 // p.dchunk consecutive tasks, the workgroup's k-th chunk taken from the counter by the wave whose grab first
 // reaches it (in order, as chain_body's dynamic units; g_uid, reset by the caller), so workgroups that start
 // late or finish early balance the work; at most kDynUnits chunks per workgroup.
+// ochunk: static chunk size (0: p.ochunk).
 __device__ void occlude_queue_body(const rtk::DevScene& s, const PcParams& p, unsigned blk, unsigned G,
-                                   const unsigned* tasks, unsigned total, unsigned* dctr = nullptr) {
+                                   const unsigned* tasks, unsigned total, unsigned* dctr = nullptr,
+                                   unsigned ochunk = 0) {
     const int lane = lane_id(), wave = (int)(threadIdx.x >> 6);
+    const unsigned sC = ochunk ? ochunk : (unsigned)p.ochunk;
     const unsigned dC = (unsigned)p.dchunk, nchunks = dctr ? (total + dC - 1) / dC : 0u;
-    const unsigned n = dctr ? (unsigned)kDynUnits * dC : chunk_count(total, G, blk, (unsigned)p.ochunk);
-    const UDiv och((unsigned)p.ochunk), nld((unsigned)s.nlights);
+    const unsigned n = dctr ? (unsigned)kDynUnits * dC : chunk_count(total, G, blk, sC);
+    const UDiv och(sC), nld((unsigned)s.nlights);
     // the queue count, the hit mask and the queued counts are written by other lanes of the wave:
     // every read is an atomic load (no value kept in a register across the loop)
     if (lane == 0) {
@@ -1550,6 +1583,95 @@ __device__ void tail_chain(const rtk::DevScene& s, const PcParams& p, unsigned e
     }
 }
 
+// Phase A's stragglers (PcParams::tailqA), one wave each: sample `path` from level `level` to the end of phase
+// A -- chain_body's phase-A epilogue per level (record, shadow tasks into the owning k_chain workgroup's region,
+// path end, or the continuation handed to phase B in that workgroup's continuation region), so k_pack_a and
+// phase B see exactly what k_chain would have left.
+__device__ void tail_chain_a(const rtk::DevScene& s, const PcParams& p, uint2 e) {
+    const unsigned path = e.x & 0x7fffffffu, blk = e.y;
+    int k = (int)(e.x >> 31);
+    const int nl = s.nlights;
+    const bool lead = lane_id() == 0;
+    Ray r;
+    slab_sample_ray(p, path, &r);                  // the eye ray (level 0)
+    if (k == 1) {                                  // level 1: the reflection of record 0 (reflect_from_record's values)
+        const float4 a = p.rec[path];
+        const V h0{a.x, a.y, a.z};
+        r = reflect_ray(s, h0, surface_normal(s, h0, __float_as_int(a.w)), r.d);
+    }
+    while (true) {
+        if (defer_closest(s, r)) {                 // the rest of this path: k_fallback
+            if (lead) {
+                p.pinfo[path] = kPathCont;         // (k_fallback's path)
+                if (k == 0) {
+                    fb_chain(p, kFbEye | path);
+                } else {
+                    const unsigned prev = (unsigned)rec_id(p, k - 1, path, 0);
+                    if (prev < p.dbase) {          // reflect_from_record: the direction of level k - 1
+                        Ray r0;
+                        slab_sample_ray(p, path, &r0);
+                        p.tail[path] = make_float4(r0.d.x, r0.d.y, r0.d.z, 0.0f);
+                    }
+                    fb_chain(p, prev);
+                }
+            }
+            return;
+        }
+        const HitRec h = tail_closest(s, r);
+        const bool hit = h.prim >= 0;
+        V nn{0.0f, 0.0f, 0.0f}, hitp{0.0f, 0.0f, 0.0f};
+        int mat = 0, code = 0;
+        const size_t lvp = rec_id(p, k, path, 0);
+        if (hit) {
+            hit_surface(s, r, h, &nn, &mat, &code);
+            hitp = add(r.o, mul(r.d, h.t));
+            if (lead) rec_write(p, lvp, hitp, code, r.d, mat);
+            const unsigned own0 = (unsigned)(lvp * nl);
+            unsigned* const sq = p.sqA + (size_t)blk * p.scapA;
+            for (int l = 0; l < nl; ++l) {
+                if (s.cull_shadows && !light_needed(s, hitp, nn, l)) {
+                    if (lead) p.occ[lvp * nl + l] = 1;     // shaded as occluded: the same sum (light_needed)
+                } else if (lead) {
+                    sq[atomicAdd(&p.scntA[blk], 1u)] = own0 + (unsigned)l;
+                }
+            }
+        }
+        if (!hit) {                                                          // :442-449
+            if (lead) p.pinfo[path] = k | ((k == 0 ? kEndBg : kEndZero) << 8);
+            return;
+        }
+        if (!s.mats[mat - 1].is_mirror) {
+            if (lead) p.pinfo[path] = (k + 1) | (kEndLast << 8);
+            return;
+        }
+        if (k >= s.max_depth) {                    // child beyond MaxRecursionDepth: 0 (:387-389)
+            if (lead) p.pinfo[path] = (k + 1) | (kEndZero << 8);
+            return;
+        }
+        if (k >= p.kinline) {                      // deeper levels: phase B, a continuation of this workgroup
+            if (lead) {
+                p.cq[(size_t)blk * p.ccapA + atomicAdd(&p.ccnt[blk], 1u)] = (unsigned)((size_t)k * p.cap + path);
+                p.pinfo[path] = kPathCont;
+                if (lvp < p.dbase) p.tail[path] = make_float4(r.d.x, r.d.y, r.d.z, 0.0f);   // reflect_from_record
+            }
+            return;
+        }
+        r = reflect_ray(s, hitp, nn, r.d);
+        ++k;
+    }
+}
+
+__global__ __launch_bounds__(64) void k_tail_a(rtk::DevScene s, PcParams p) {
+    const unsigned n = min(p.totals[11], (unsigned)p.cap);
+    unsigned i = blockIdx.x;
+    while (i < n) {
+        tail_chain_a(s, p, p.tailqA[i]);
+        unsigned next = 0;
+        if (lane_id() == 0) next = gridDim.x + atomicAdd(&p.totals[12], 1u);
+        i = (unsigned)__builtin_amdgcn_readfirstlane((int)next);
+    }
+}
+
 // One wave per workgroup; wave w first takes entry w, then the next entries from a launch-wide counter
 // (totals[8]), so a long chain does not hold up others behind it and the first round has no contention.
 __global__ __launch_bounds__(64) void k_tail(rtk::DevScene s, PcParams p) {
@@ -1578,7 +1700,8 @@ __global__ __launch_bounds__(kBlock, RT_OCC_WAVES_PER_EU) void k_occlude(rtk::De
                 __syncthreads();
                 if (threadIdx.x == 0) g_head = 0;
                 __syncthreads();
-                occlude_queue_body(s, p, blockIdx.x, gridDim.x, p.sflatB, p.totals[2]);
+                // (one task per workgroup at a time: few rays, from the deepest chains, spread over the GPU)
+                occlude_queue_body(s, p, blockIdx.x, gridDim.x, p.sflatB, p.totals[2], nullptr, 1u);
             }
         } else if (which) {
             occlude_queue_body(s, p, blockIdx.x, gridDim.x, p.sflatB, p.totals[2]);
@@ -1960,6 +2083,7 @@ __global__ __launch_bounds__(kBlock) void k_fallback(rtk::DevScene s, rtk::Eye e
         atomicAdd(&p.counters[kCntFbShadows], (unsigned long long)p.totals[5]);
         if (p.totals[6]) atomicAdd(&p.counters[kCntFbOvfScans], 1ull);
         atomicAdd(&p.counters[kCntFbTail], (unsigned long long)min(p.totals[7], p.cb));
+        atomicAdd(&p.counters[kCntFbTailA], (unsigned long long)min(p.totals[11], (unsigned)p.cap));
     }
     for (unsigned i = gt; i < nfc + novf; i += gs)
         fallback_chain(s, e, p, i < nfc ? p.fbc[i] : p.cflat[p.cb + (i - nfc)], stk, w, i >= nfc);
@@ -2163,6 +2287,10 @@ hipError_t launch_chain_chunk(const rtk::DevScene& s, const rtk::Eye& e, const P
     mark(kKChain);
     if (count) hipLaunchKernelGGL(k_chain<true>, dim3(p.grid), blk, 0, st, s, e, p);
     else hipLaunchKernelGGL(k_chain<false>, dim3(p.grid), blk, 0, st, s, e, p);
+    if (p.tail_a > 0 && !count) {                   // phase A's stragglers, one wave each
+        mark(kKTail);
+        hipLaunchKernelGGL(k_tail_a, dim3(p.tail_grid), dim3(64), 0, st, s, p);
+    }
     mark(kKPackA);
     hipLaunchKernelGGL(k_pack_a, dim3(p.grid), blk, 0, st, p);
     PcParams q = p;

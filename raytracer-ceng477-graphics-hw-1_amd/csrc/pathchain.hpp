@@ -86,6 +86,7 @@ enum CounterSlot : int {
     kCntFbShadows,        //   shadow rays deferred
     kCntFbOvfScans,       //   launches whose fallback shadow queue overflowed (occlusion bytes scanned)
     kCntFbTail,           //   phase-B chains handed to k_tail
+    kCntFbTailA,          //   phase-A samples handed to k_tail_a
 };
 
 // Phase-A levels whose records may leave out the direction (PcParams::dbase): k_finish rebuilds them
@@ -113,8 +114,9 @@ __host__ __device__ inline unsigned unit_col(int tiles_x, int ublk_h, int ublk_w
 
 // PcParams::totals words: packed task counts (0-2), the phase-A unit counter (3), k_fallback's chain /
 // shadow counts and shadow-queue overflow (4-6), phase B's tail entries (7), k_tail's entry counter (8),
-// k_mix's dynamic shadow-chunk counter (10); phase B's ended chains in 8 shards, one 128-B line each
-// (kLiveShard0 + kLiveStride * i: a wave adds to shard blk % 8).
+// k_mix's dynamic shadow-chunk counter (10), phase A's tail entries (11) and k_tail_a's entry counter (12);
+// the live-chain counts in 8 shards, one 128-B line each (kLiveShard0 + kLiveStride * i: a wave adds to shard
+// blk % 8): word 0 phase B's chains ended, 1 phase A's samples ended, 2 phase A's samples started.
 constexpr int kLiveShard0 = 32, kLiveStride = 32;
 constexpr int kTotalsWords = kLiveShard0 + 8 * kLiveStride;
 
@@ -228,6 +230,11 @@ struct PcParams {
     int tail_live;
     int tail_grid;
     int tail_all;     // tests: every chain handed on at its first phase-B walk, exhausted or not
+    // phase A's stragglers (pathchain.hip k_tail_a, between k_chain and k_pack_a): once every unit is taken and at
+    // most tail_a started samples are still in phase A (0: never), a k_chain wave hands its samples on as
+    // {sample | level << 31, workgroup} (totals[11] of them, at most cap)
+    uint2* tailqA;
+    int tail_a;
     int dchunk;       // k_mix (lone frames): A's shadow tasks dealt dynamically in chunks of this many (totals[10]),
                       // the chain workgroups joining once their chains are done; 0: static dealing
 };

@@ -10,6 +10,9 @@
 //   --device N       HIP device ordinal
 //   --gpus N         render every frame on GPUs 0..N-1 (row stripes + one RCCL gather, rt_set_devices)
 //   --no-write       skip write_ppm (timing)
+//   --timing         a JSON line on stderr: steady-clock stamps (ms) of main's phases and the scene-build split
+// The process ends with _exit once every image is written and stdout flushed: the HIP runtime's teardown at a
+// normal exit costs tens of ms and frees nothing the OS does not (RT_CLI_EXIT=normal: a normal exit).
 #include <chrono>
 #include <cstdio>
 #include <cstdlib>
@@ -32,7 +35,12 @@ int die(const char* what) {
 
 }  // namespace
 
+double stamp() {
+    return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now().time_since_epoch()).count();
+}
+
 int main(int argc, char** argv) {
+    const double t_main = stamp();
     // several cameras render as concurrent frame batches, one stream each: give HIP enough hardware
     // queues that they do not share (read at the runtime's first use).  RT_HW_QUEUES overrides; a
     // GPU_MAX_HW_QUEUES the user already set is kept; otherwise 8.
@@ -41,16 +49,17 @@ int main(int argc, char** argv) {
     const char* scene_path = nullptr;
     int aa = 2, max_depth = -1000, device = 0, gpus = 0;   // device 0 unless --device: an explicit device lets
                                                           // the library start HIP while the XML is read
-    bool write = true;
+    bool write = true, timing = false;
     for (int i = 1; i < argc; ++i) {
         if (!std::strcmp(argv[i], "--aa") && i + 1 < argc) aa = std::atoi(argv[++i]);
         else if (!std::strcmp(argv[i], "--max-depth") && i + 1 < argc) max_depth = std::atoi(argv[++i]);
         else if (!std::strcmp(argv[i], "--device") && i + 1 < argc) device = std::atoi(argv[++i]);
         else if (!std::strcmp(argv[i], "--gpus") && i + 1 < argc) gpus = std::atoi(argv[++i]);
         else if (!std::strcmp(argv[i], "--no-write")) write = false;
+        else if (!std::strcmp(argv[i], "--timing")) timing = true;
         else if (argv[i][0] != '-' && !scene_path) scene_path = argv[i];
         else {
-            std::fprintf(stderr, "usage: %s scene.xml [--aa F] [--max-depth D] [--device N] [--gpus N] [--no-write]\n", argv[0]);
+            std::fprintf(stderr, "usage: %s scene.xml [--aa F] [--max-depth D] [--device N] [--gpus N] [--no-write] [--timing]\n", argv[0]);
             return 2;
         }
     }
@@ -66,6 +75,7 @@ int main(int argc, char** argv) {
     if (rt_scene_load_xml(scene_path, &opts, &scene) != RT_OK) return die("load");
     if (max_depth != -1000 && rt_scene_set_max_depth(scene, max_depth) != RT_OK) return die("max-depth");
     const double planted = seconds_since(begin1);
+    const double t_load = stamp();
     std::printf("Planted trees in %.3f seconds.\n", planted);
     if (aa > 1) std::printf("Super Sampling Anti aliasing is enabled. (%d*%dx)\n", aa, aa);
 
@@ -86,12 +96,28 @@ int main(int argc, char** argv) {
     }
     std::fflush(stdout);
     if (ncam > 0 && rt_render_cameras(scene, cams.data(), ncam, aa, outs.data(), nullptr) != RT_OK) return die("render");
+    const double t_render = stamp();
     for (int c = 0; c < ncam && write; ++c)
         if (rt_write_ppm(names[c].c_str(), imgs[c].data(), cams[c].image_width, cams[c].image_height) != RT_OK)
             return die("write_ppm");
+    const double t_write = stamp();
     const double rendered = seconds_since(begin2);
     std::printf("Rendered in %.3f seconds.\n", rendered);
     std::printf("Total: %.3f seconds.\n", rendered + planted);
+    std::fflush(stdout);
+    if (timing) {
+        rt_bvh_info bi{};
+        rt_scene_bvh_info(scene, &bi);
+        std::fprintf(stderr,
+                     "{\"cli\": {\"main\": %.3f, \"loaded\": %.3f, \"rendered\": %.3f, \"written\": %.3f, "
+                     "\"xml_ms\": %.3f, \"prep_ms\": %.3f, \"ref_tree_ms\": %.3f, \"flat_ms\": %.3f, \"refwide_ms\": %.3f, "
+                     "\"stree_ms\": %.3f, \"upload_ms\": %.3f}}\n",
+                     t_main, t_load, t_render, t_write, bi.xml_ms, bi.prep_ms, bi.ref_ms, bi.flat_ms, bi.refwide_ms,
+                     bi.stree_ms, bi.upload_ms);
+        std::fflush(stderr);
+    }
+    const char* ex = std::getenv("RT_CLI_EXIT");
+    if (!ex || std::strcmp(ex, "normal")) std::_Exit(0);   // (every file is closed by rt_write_ppm)
     rt_scene_destroy(scene);
     return 0;
 }

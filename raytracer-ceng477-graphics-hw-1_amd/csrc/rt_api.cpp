@@ -138,6 +138,8 @@ struct rt_scene {
                                 // 2 every launch, 0 none
     int tune_tail = 0;          // RT_TAIL: a lone frame's phase-B chains go to k_tail once at most this many are left (0: off)
     int tune_tail_b = 0;        // RT_TAIL_B: the same in frame batches
+    int tune_tail_a = 0;        // RT_TAIL_A: a lone frame's phase-A samples go to k_tail_a once at most this many are left
+    int tune_tail_a_b = 0;      // RT_TAIL_A_B: the same in frame batches
     int tune_tail_all = 0;      // RT_TAIL_ALL=1 (tests): every phase-B chain to k_tail at its first walk (where a tail is on)
     int tune_dchunk = 0;        // RT_DCHUNK: a lone frame's A shadow tasks dealt dynamically in chunks of this many (0: static)
     int tune_tail_grid = 0;     // RT_TAIL_GRID: k_tail's one-wave workgroups (0: 16 per CU)
@@ -265,12 +267,21 @@ void start_device_warmup(const rt_options* opts) {
     if (g_warm_started) return;
     g_warm_started = true;
     g_warm = std::async(std::launch::async, [want] {
+        // RT_LOG_INIT=1 (diagnostics, tools/exp_cli.py --phases): the warm-up's steps on the steady clock, ms
+        const bool log = std::getenv("RT_LOG_INIT") != nullptr;
+        auto now = [] { return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now().time_since_epoch()).count(); };
+        const double t0 = log ? now() : 0.0;
         int n = 0;
         if (hipGetDeviceCount(&n) != hipSuccess || n == 0 || want >= n) return;
+        const double t1 = log ? now() : 0.0;
         (void)hipSetDevice(want);
         (void)hipFree(nullptr);
+        const double t2 = log ? now() : 0.0;
         int a = 0, b = 0, c = 0;
         (void)rtc::chain_occupancy(&a, &b, &c);     // loads the kernels' code objects
+        if (log)
+            std::fprintf(stderr, "{\"rt_init\": {\"start\": %.3f, \"device_count\": %.3f, \"context\": %.3f, \"code_objects\": %.3f}}\n",
+                         t0, t1, t2, now());
     });
 }
 
@@ -439,6 +450,8 @@ int upload_rest(rt_scene* s, const rt_options* opts) {
     if (const char* e = std::getenv("RT_TAIL")) s->tune_tail = std::max(0, std::atoi(e));
     if (const char* e = std::getenv("RT_TAIL_B")) s->tune_tail_b = std::max(0, std::atoi(e));
     if (const char* e = std::getenv("RT_TAIL_ALL")) s->tune_tail_all = std::atoi(e) != 0;
+    if (const char* e = std::getenv("RT_TAIL_A")) s->tune_tail_a = std::max(0, std::atoi(e));
+    if (const char* e = std::getenv("RT_TAIL_A_B")) s->tune_tail_a_b = std::max(0, std::atoi(e));
     if (const char* e = std::getenv("RT_TAIL_GRID")) s->tune_tail_grid = std::max(1, std::atoi(e));
     if (const char* e = std::getenv("RT_DCHUNK")) s->tune_dchunk = std::max(0, std::atoi(e));
     if (const char* e = std::getenv("RT_BTAIL")) s->tune_btail = std::max(1, std::min(64, std::atoi(e)));
@@ -617,7 +630,7 @@ struct ChainPlan {
     size_t dbase = 0;               // records below it without directions (pathchain.hpp)
     int clevels = 0;
     size_t o_rec = 0, o_recd = 0, o_pinfo = 0, o_occ = 0, o_sqA = 0, o_scntA = 0, o_sflatA = 0, o_cq = 0, o_ccnt = 0,
-           o_cflat = 0, o_sqB = 0, o_scntB = 0, o_sflatB = 0, o_totals = 0, o_cid = 0, o_tailq = 0, o_tail = 0,
+           o_cflat = 0, o_sqB = 0, o_scntB = 0, o_sflatB = 0, o_totals = 0, o_cid = 0, o_tailq = 0, o_tailqA = 0, o_tail = 0,
            o_fbc = 0, o_fbs = 0, bytes = 0;
 };
 
@@ -724,6 +737,7 @@ ChainPlan chain_plan(const rt_scene* s, const ChainGeom& g, size_t nunits, bool 
         P.o_sqB = L.take<unsigned>((size_t)P.gb * P.scapB); P.o_scntB = L.take<unsigned>(P.gb + 1);
         P.o_sflatB = L.take<unsigned>(P.cb * (levels - P.la) * nl);
         P.o_tailq = L.take<unsigned>(P.phase_b ? P.cb : 0);
+        P.o_tailqA = L.take<uint2>(cap);
     }
     P.o_totals = L.take<unsigned>(rtc::kTotalsWords);
     P.bytes = L.off;
@@ -916,6 +930,8 @@ int render_chain(rt_scene* s, const rtk::Eye& eye, const rtk::FrameParams& f, bo
     p.tail_live = !count && P.phase_b ? (P.split_occ ? s->tune_tail_b : s->tune_tail) : 0;
     p.tail_grid = s->tune_tail_grid > 0 ? s->tune_tail_grid : 16 * s->num_cus;
     p.tail_all = s->tune_tail_all;
+    p.tailqA = static_cast<uint2*>(at(P.o_tailqA));
+    p.tail_a = !count ? (P.split_occ ? s->tune_tail_a_b : s->tune_tail_a) : 0;
     p.dchunk = !count && !P.split_occ && RT_LEAF_QUEUE ? s->tune_dchunk : 0;
     if (p.dchunk > 0) {   // every task reachable: k_mix's workgroups take at most kDynUnits chunks each; and at
                           // least a wave's grab (64), which then holds at most one chunk's first task

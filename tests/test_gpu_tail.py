@@ -10,7 +10,8 @@ entry) and runs chain_body's epilogue (raytracer.cpp:385-452): the images must b
 the reference's whatever the threshold (the live chains left when the hand-off
 starts) -- 0 (off), 1, 500, 2000, every chain once the continuations run out, and
 RT_TAIL_ALL (every continuation handed on at its first phase-B walk: all of phase
-B in k_tail) --
+B in k_tail), and phase A's stragglers likewise to k_tail_a (RT_TAIL_A /
+RT_TAIL_A_B, the samples left once every unit is taken) --
 with the phase-B record space cut (RT_CONT_CB: the rest in k_fallback), with
 every shadow task of phase B through k_occlude (RT_BQ_CAP=0), and with k_mix's
 A shadow tasks dealt statically or dynamically in chunks (RT_DCHUNK).
@@ -45,6 +46,12 @@ ENVS = [
     {"RT_TAIL": "500", "RT_BQ_CAP": "0", "RT_TAIL_GRID": "7"},
     {"RT_TAIL": "1", "RT_TAIL_ALL": "1", "RT_COMPACT": "2", "RT_TAIL_B": "1"},
     {"RT_TAIL": "1000000", "RT_OCC_INPLACE": "0"},
+    # phase A's stragglers to k_tail_a (levels 0..1, then phase B as usual)
+    {"RT_TAIL_A": "1", "RT_TAIL_A_B": "1"},
+    {"RT_TAIL_A": "5000", "RT_TAIL_A_B": "5000", "RT_TAIL": "2000", "RT_TAIL_B": "2000"},
+    {"RT_TAIL_A": "100000000", "RT_TAIL_A_B": "100000000"},   # every sample left once the units run out
+    {"RT_TAIL_A": "1", "RT_TAIL_ALL": "1", "RT_TAIL": "1"},    # every sample from its first walk, A and B
+    {"RT_TAIL_A_B": "1", "RT_TAIL_ALL": "1", "RT_COMPACT": "2", "RT_CONT_CB": "1000"},
 ]
 
 

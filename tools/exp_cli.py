@@ -7,6 +7,7 @@ includes HIP initialisation); the PPM bytes of both are compared.  The README's 
 (reference README.md: horse_and_mug 0.452 s; 256x AA 40 s; low poly 4x AA 1 s; 8K 4x AA 44.7 s) sit beside them.
 
   python tools/exp_cli.py [--reps N] [--quick]
+  python tools/exp_cli.py --phases [--reps N]     (the CLI's wall time split by phase, horse_and_mug AA1/AA2)
 """
 import argparse
 import hashlib
@@ -46,13 +47,54 @@ def shas(d):
     return {p.name: hashlib.sha256(p.read_bytes()).hexdigest()[:16] for p in sorted(Path(d).glob("*.ppm"))}
 
 
+def phases(hm, reps, extra_env=None, aa=1):
+    """One CLI process per rep with --timing and RT_LOG_INIT=1: the steady-clock (CLOCK_MONOTONIC) stamps the
+    CLI and the library's warm-up thread print, against the parent's own stamps around the process."""
+    rows = []
+    for _ in range(reps):
+        wd = tempfile.mkdtemp()
+        env = dict(os.environ, RT_LOG_INIT="1", **(extra_env or {}))
+        t_spawn = time.monotonic() * 1e3
+        r = subprocess.run([str(CLI), hm, "--aa", str(aa), "--timing"], cwd=wd, capture_output=True, text=True,
+                           timeout=120, env=env)
+        t_end = time.monotonic() * 1e3
+        if r.returncode != 0:
+            raise RuntimeError(r.stderr[-400:])
+        ev = {}
+        for l in r.stderr.splitlines():
+            if l.startswith("{"):
+                ev.update(json.loads(l))
+        c, i = ev["cli"], ev.get("rt_init", {})
+        row = {"wall": t_end - t_spawn, "spawn_to_main": c["main"] - t_spawn,
+               "load": c["loaded"] - c["main"], "render_d2h": c["rendered"] - c["loaded"],
+               "write_ppm": c["written"] - c["rendered"], "after_write_to_exit": t_end - c["written"],
+               "xml": c["xml_ms"], "tree_build": c["prep_ms"] + c["ref_tree_ms"] + c["flat_ms"] + c["refwide_ms"],
+               "stree": c["stree_ms"], "upload_after_build": c["upload_ms"]}
+        if i:
+            row.update({"init_start_after_main": i["start"] - c["main"], "hip_device_count": i["device_count"] - i["start"],
+                        "hip_context": i["context"] - i["device_count"], "code_objects": i["code_objects"] - i["context"],
+                        "init_end_after_main": i["code_objects"] - c["main"]})
+        rows.append(row)
+    keys = rows[0].keys()
+    return {k: round(sorted(r[k] for r in rows)[len(rows) // 2], 2) for k in keys}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--reps", type=int, default=3)
     ap.add_argument("--quick", action="store_true", help="skip the 8K and 256x cases")
+    ap.add_argument("--phases", action="store_true", help="only the CLI's per-phase split (ms, medians)")
     a = ap.parse_args()
     pkg = graft.import_pkg()
     d = tempfile.mkdtemp()
+    if a.phases:
+        hm = pkg.scenes.write_config("hm_verbatim", d)
+        for aa in (1, 2):
+            for name, env in (("default", None), ("normal_exit", {"RT_CLI_EXIT": "normal"}),
+                              ("no_warmup", {"RT_NO_WARMUP": "1"})):
+                print(json.dumps({"scene": "horse_and_mug.xml", "aa": aa, "variant": name,
+                                  "median_ms": phases(hm, a.reps, env, aa)}), flush=True)
+        return
     hm = pkg.scenes.write_config("hm_verbatim", d)
     lp = pkg.scenes.write_config("low_poly.xml", d)
     text = Path(hm).read_text()

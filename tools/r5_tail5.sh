@@ -7,3 +7,8 @@ rc=$?; echo "tests rc=$rc"; tail -3 gpurun_out/r5t5/tests.log; [ $rc -ne 0 ] && 
 export EXP_REPS=21 RT_KTIME=1
 timeout -k 10 900 python3 tools/exp_lone.py RT_TAIL=0 RT_TAIL=500 RT_TAIL=1000 RT_TAIL=2000 RT_TAIL=4000 RT_TAIL=8000 \
   RT_TAIL=2000,RT_TAIL_GRID=2048 RT_TAIL=0 2>&1 | tee gpurun_out/r5t5/lone.txt
+timeout -k 10 300 python3 tools/exp_cli.py --phases --reps 7 2>&1 | tee gpurun_out/r5t5/cli_phases.jsonl
+timeout -k 10 300 python3 tools/exp_cli.py --quick --reps 5 > gpurun_out/r5t5/cli.jsonl 2> gpurun_out/r5t5/cli.err; tail -3 gpurun_out/r5t5/cli.jsonl
+for F in 6 32 96; do for S in 4 8; do
+  EXP_F=$F EXP_S=$S EXP_REPS=5 timeout -k 10 300 python3 tools/exp_shard.py 1 8 2>/dev/null | tail -2 | sed "s/^/F=$F S=$S /"
+done; done | tee gpurun_out/r5t5/shard.txt
