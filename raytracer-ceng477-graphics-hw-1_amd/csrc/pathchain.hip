@@ -325,6 +325,10 @@ __device__ __forceinline__ void fb_chain(const PcParams& p, unsigned entry) {
     if (i < p.fbc_cap) p.fbc[i] = entry;       // fbc_cap = cap: a sample defers at most one ray per launch
 }
 __device__ __forceinline__ void fb_shadow(const PcParams& p, unsigned owner) {
+    if (p.fin_mode) {                          // a phase-A record's shadow ray: its pixel waits for k_fallback
+        const unsigned lvp = owner / (unsigned)p.nlights;
+        if (lvp < (unsigned)p.la * (unsigned)p.cap) atomicOr(&p.pinfo[lvp % (unsigned)p.cap], kPathFb);
+    }
     const unsigned i = atomicAdd(&p.totals[5], 1u);
     if (i < p.fbs_cap) {
         p.fbs[i] = owner;
@@ -1928,7 +1932,7 @@ template <bool LDS, bool CMP>
 __device__ __forceinline__ void finish_pixels(const rtk::DevScene& s, const rtk::Eye& e, const PcParams& p) {
     const int F = p.aa;
     const unsigned gtid = blockIdx.x * kBlock + threadIdx.x, gstride = gridDim.x * kBlock;
-    if (p.fin_cont) {
+    if (p.fin_cont && p.fin_mode != 1) {
         const unsigned n = p.totals[1];
         for (unsigned j = gtid; j < n; j += gstride) {
             const unsigned path = (p.cflat[j] & ~kFbEye) % (unsigned)p.cap;
@@ -1946,6 +1950,24 @@ __device__ __forceinline__ void finish_pixels(const rtk::DevScene& s, const rtk:
         }
     }
     const int npix = (p.chunk_rows / p.aa) * p.width;
+    if (p.fin_mode) {
+        // the split: part 1 the pixels final after k_mix, part 2 the pixels with a kPathFb sample (the continued
+        // ones came first above); after a fallback-queue overflow (any occlusion byte may still change) part 2
+        // takes every pixel
+        const bool all = p.totals[6] != 0;
+        if (p.fin_mode == 1 && all) return;
+        for (int q = (int)gtid; q < npix; q += (int)gstride) {
+            const int rr = q / p.width, ocol = q - rr * p.width;
+            int bits = 0;
+            for (int k = 0; k < p.aa; ++k)
+                for (int l = 0; l < p.aa; ++l) bits |= p.pinfo[slab_slot(p.tiles_x, ocol * p.aa + l, rr * p.aa + k)];
+            const bool later = (bits & (kPathCont | kPathFb)) != 0;
+            if (p.fin_mode == 1 ? !later
+                                : !(p.fin_cont && (bits & kPathCont)) && (all || later))   // (fin_cont: the loop above)
+                finish_pixel<LDS, CMP>(s, e, p, rr, ocol);
+        }
+        return;
+    }
     for (int q = (int)gtid; q < npix; q += (int)gstride) {
         const int rr = q / p.width, ocol = q - rr * p.width;
         if (p.fin_cont && pixel_cont(p, rr, ocol)) continue;
@@ -2065,7 +2087,7 @@ __device__ void fallback_chain(const rtk::DevScene& s, const rtk::Eye& e, const 
     }
     for (int i = n - 1; i >= 0; --i) c = vclamp(add(Ls[i], had(c, Km[i])), 0.0f, FLT_MAX);   // :436-451
     p.tail[path] = make_float4(c.x, c.y, c.z, 0.0f);
-    p.pinfo[path] = k0 | (kEndTail << 8) | (k0 >= p.la || cont ? kPathCont : 0);
+    p.pinfo[path] = k0 | (kEndTail << 8) | (k0 >= p.la || cont ? kPathCont : 0) | (p.fin_mode ? kPathFb : 0);
 }
 
 __global__ __launch_bounds__(kBlock) void k_fallback(rtk::DevScene s, rtk::Eye e, PcParams p) {
@@ -2275,7 +2297,7 @@ unsigned chain_block_scap(int n0, int grid, int levels, int nlights) {
 }
 
 hipError_t launch_chain_chunk(const rtk::DevScene& s, const rtk::Eye& e, const PcParams& p, bool count,
-                              hipStream_t st, KTimer* kt) {
+                              hipStream_t st, KTimer* kt, const FinSplit* fs) {
     const dim3 blk(kBlock);
     auto mark = [&](int k) { if (kt) kt->mark(k, st); };
     const bool phase_b = p.kinline < s.max_depth;     // any continuation possible
@@ -2308,6 +2330,18 @@ hipError_t launch_chain_chunk(const rtk::DevScene& s, const rtk::Eye& e, const P
         if (split) hipLaunchKernelGGL((k_mix<false, false>), dim3(mgrid), blk, 0, st, s, e, q);
         else hipLaunchKernelGGL((k_mix<false, true>), dim3(mgrid), blk, 0, st, s, e, q);
     }
+    // k_finish split (fin_mode): the pixels final after k_mix shade on the side stream beside the rest
+    const bool fsplit = fs && fs->side && p.fin_mode && phase_b && !count && !split;
+    if (fsplit) {
+        hipError_t e2 = hipEventRecord(fs->fork, st);
+        if (e2 == hipSuccess) e2 = hipStreamWaitEvent(fs->side, fs->fork, 0);
+        if (e2 != hipSuccess) return e2;
+        PcParams f1 = p;
+        f1.fin_cont = p.aa == 1;
+        f1.fin_mode = 1;
+        launch_finish(s, e, f1, fs->side);
+        if ((e2 = hipEventRecord(fs->join, fs->side)) != hipSuccess) return e2;
+    }
     if (p.tail_live > 0 && phase_b && !count) {   // phase B's tail chains, one wave each
         mark(kKTail);
         hipLaunchKernelGGL(k_tail, dim3(p.tail_grid), dim3(64), 0, st, s, p);
@@ -2331,8 +2365,13 @@ hipError_t launch_chain_chunk(const rtk::DevScene& s, const rtk::Eye& e, const P
     hipLaunchKernelGGL(k_fallback, dim3(p.fb_grid), blk, 0, st, s, e, p);
     PcParams f = p;
     f.fin_cont = phase_b && p.aa == 1;
+    f.fin_mode = fsplit ? 2 : 0;
     mark(kKFinish);
     launch_finish(s, e, f, st);
+    if (fsplit) {
+        const hipError_t e2 = hipStreamWaitEvent(st, fs->join, 0);
+        if (e2 != hipSuccess) return e2;
+    }
     mark(kKEnd);
     return hipGetLastError();
 }

@@ -58,6 +58,9 @@ constexpr unsigned kFbEye = 0x80000000u;
 constexpr uint8_t kOccDeferred = 2;
 // pinfo bit of a path continued in phase B (set by phase A's hand-off, kept by phase B's end)
 constexpr int kPathCont = 1 << 16;
+// pinfo bit of a path whose phase-A shadow ray went to k_fallback's queue (its occlusion byte is written there):
+// k_finish's split (PcParams::fin_mode) leaves its pixel to the part after k_fallback
+constexpr int kPathFb = 1 << 17;
 
 // Device counter block (u64 slots, RT_RENDER_COUNT launches).  0-6 are rt_stats' (primary, shadow,
 // reflection, node visits, triangle tests, sphere tests, skipped shadow rays); the per-role slots
@@ -195,6 +198,10 @@ struct PcParams {
                       // regions (workgroup w: regions w, w + G, ...); k_pack_a packs only the continuations
     int fin_grid;     // k_finish workgroups at most (0: a lane per output pixel), a grid-stride loop beyond
     int fin_cont;     // k_finish: the continued paths' pixels first (chain path: cflat, totals[1], kPathCont)
+    int fin_mode;     // k_finish split over two streams (lone frames with k_tail): 0 every pixel; 1 (beside k_tail,
+                      // right after k_mix) the pixels final then -- no sample continued (kPathCont) or with a phase-A
+                      // shadow ray in k_fallback's queue (kPathFb), none after a fallback-queue overflow; 2 (after
+                      // k_fallback) the others
     int refill;       // a wave refills once <= refill of its lanes are still walking
     int orefill;      // the same for the shadow (any-hit) walks
     int brefill;      // the same for phase-B chains
@@ -279,7 +286,13 @@ struct KTimer {
     }
 };
 
+// side/fork/join (lone frames with k_tail, PcParams::fin_mode): k_finish's part for the pixels final after k_mix
+// runs on `side` beside k_tail and the rest, joined back into `stream` before it returns (null: one k_finish).
+struct FinSplit {
+    hipStream_t side = nullptr;
+    hipEvent_t fork = nullptr, join = nullptr;
+};
 hipError_t launch_chain_chunk(const rtk::DevScene& s, const rtk::Eye& e, const PcParams& p, bool count,
-                              hipStream_t stream, KTimer* kt = nullptr);
+                              hipStream_t stream, KTimer* kt = nullptr, const FinSplit* fs = nullptr);
 
 }  // namespace rtc

@@ -141,6 +141,7 @@ struct rt_scene {
     int tune_tail_a = 0;        // RT_TAIL_A: a lone frame's phase-A samples go to k_tail_a once at most this many are left
     int tune_tail_a_b = 0;      // RT_TAIL_A_B: the same in frame batches
     int tune_tail_all = 0;      // RT_TAIL_ALL=1 (tests): every phase-B chain to k_tail at its first walk (where a tail is on)
+    int tune_fin_split = 1;     // RT_FIN_SPLIT: with a phase-B tail, k_finish's pixels final after k_mix on a side stream
     int tune_dchunk = 0;        // RT_DCHUNK: a lone frame's A shadow tasks dealt dynamically in chunks of this many (0: static)
     int tune_tail_grid = 0;     // RT_TAIL_GRID: k_tail's one-wave workgroups (0: 16 per CU)
     int tune_btail = 64;        // RT_BTAIL: the same once the continuations are exhausted (1: 1.24, 4: 1.18, 16: 1.15, 64: 1.14 ms)
@@ -179,6 +180,7 @@ struct rt_scene {
     // on demand, carved per frame); slot 0 serves single renders, slots
     // [0, kSlots) the concurrent frames of rt_render_cameras*.
     static constexpr int kSlots = 6;
+    struct FinSide { hipStream_t st = nullptr; hipEvent_t fork = nullptr, join = nullptr; } fin_side[kSlots];
     // An arena may be used from any caller stream: `last` is recorded after each
     // use on `last_stream`, and a use from another stream first waits on it.
     struct Arena {
@@ -218,6 +220,11 @@ struct rt_scene {
         for (auto& e : kt.ev)
             if (e) (void)hipEventDestroy(e);
         for (auto& a : arenas) (void)hipFree(a.hist);
+        for (auto& f : fin_side) {
+            if (f.st) (void)hipStreamDestroy(f.st);
+            if (f.fork) (void)hipEventDestroy(f.fork);
+            if (f.join) (void)hipEventDestroy(f.join);
+        }
         for (auto& e : cont_ev)
             if (e) (void)hipEventDestroy(e);
         if (h_cont) (void)hipHostFree(h_cont);
@@ -450,6 +457,7 @@ int upload_rest(rt_scene* s, const rt_options* opts) {
     if (const char* e = std::getenv("RT_TAIL")) s->tune_tail = std::max(0, std::atoi(e));
     if (const char* e = std::getenv("RT_TAIL_B")) s->tune_tail_b = std::max(0, std::atoi(e));
     if (const char* e = std::getenv("RT_TAIL_ALL")) s->tune_tail_all = std::atoi(e) != 0;
+    if (const char* e = std::getenv("RT_FIN_SPLIT")) s->tune_fin_split = std::atoi(e) != 0;
     if (const char* e = std::getenv("RT_TAIL_A")) s->tune_tail_a = std::max(0, std::atoi(e));
     if (const char* e = std::getenv("RT_TAIL_A_B")) s->tune_tail_a_b = std::max(0, std::atoi(e));
     if (const char* e = std::getenv("RT_TAIL_GRID")) s->tune_tail_grid = std::max(1, std::atoi(e));
@@ -930,6 +938,20 @@ int render_chain(rt_scene* s, const rtk::Eye& eye, const rtk::FrameParams& f, bo
     p.tail_live = !count && P.phase_b ? (P.split_occ ? s->tune_tail_b : s->tune_tail) : 0;
     p.tail_grid = s->tune_tail_grid > 0 ? s->tune_tail_grid : 16 * s->num_cus;
     p.tail_all = s->tune_tail_all;
+    // k_finish in two parts on two streams where a phase-B tail follows k_mix (launch_chain_chunk): part 1, the
+    // pixels final after k_mix, beside k_tail, k_occlude and k_fallback; part 2 the rest
+    const bool fin_split = s->tune_fin_split && p.tail_live > 0 && P.phase_b && !P.split_occ && !count;
+    p.fin_mode = fin_split ? 2 : 0;
+    rtc::FinSplit fsp;
+    if (fin_split) {
+        auto& fsd = s->fin_side[slot];
+        if (!fsd.st) HIP_TRY(hipStreamCreateWithFlags(&fsd.st, hipStreamNonBlocking));
+        if (!fsd.fork) HIP_TRY(hipEventCreateWithFlags(&fsd.fork, hipEventDisableTiming));
+        if (!fsd.join) HIP_TRY(hipEventCreateWithFlags(&fsd.join, hipEventDisableTiming));
+        fsp.side = fsd.st;
+        fsp.fork = fsd.fork;
+        fsp.join = fsd.join;
+    }
     p.tailqA = static_cast<uint2*>(at(P.o_tailqA));
     p.tail_a = !count ? (P.split_occ ? s->tune_tail_a_b : s->tune_tail_a) : 0;
     p.dchunk = !count && !P.split_occ && RT_LEAF_QUEUE ? s->tune_dchunk : 0;
@@ -1016,7 +1038,7 @@ int render_chain(rt_scene* s, const rtk::Eye& eye, const rtk::FrameParams& f, bo
             for (int i = 0; i < rtc::KTimer::kMax; ++i)
                 if (!s->kt.ev[i]) HIP_TRY(hipEventCreate(&s->kt.ev[i]));
             s->kt.n = 0;
-            HIP_TRY(rtc::launch_chain_chunk(s->dev, eye, p, count, st, &s->kt));
+            HIP_TRY(rtc::launch_chain_chunk(s->dev, eye, p, count, st, &s->kt, fin_split ? &fsp : nullptr));
             HIP_TRY(hipEventSynchronize(s->kt.ev[s->kt.n - 1]));
             for (int i = 0; i + 1 < s->kt.n; ++i) {
                 float ms = 0;
@@ -1025,7 +1047,7 @@ int render_chain(rt_scene* s, const rtk::Eye& eye, const rtk::FrameParams& f, bo
             }
             s->kt_launches++;
         } else {
-            HIP_TRY(rtc::launch_chain_chunk(s->dev, eye, p, count, st));
+            HIP_TRY(rtc::launch_chain_chunk(s->dev, eye, p, count, st, nullptr, fin_split ? &fsp : nullptr));
         }
     }
     // the share, read back later (a chunk of a forked frame: the parent call reads the frame's peak)

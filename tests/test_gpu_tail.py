@@ -46,6 +46,12 @@ ENVS = [
     {"RT_TAIL": "500", "RT_BQ_CAP": "0", "RT_TAIL_GRID": "7"},
     {"RT_TAIL": "1", "RT_TAIL_ALL": "1", "RT_COMPACT": "2", "RT_TAIL_B": "1"},
     {"RT_TAIL": "1000000", "RT_OCC_INPLACE": "0"},
+    # k_finish split (on with any phase-B tail in a lone frame): off; with every ray deferred to k_fallback
+    # (kPathFb pixels in part 2); with the fallback shadow queue overflowing (part 2 takes every pixel)
+    {"RT_TAIL": "2000", "RT_FIN_SPLIT": "0"},
+    {"RT_TAIL": "2000", "RT_FORCE_FALLBACK": "2"},
+    {"RT_TAIL": "2000", "RT_FORCE_FALLBACK": "3", "RT_FBS_CAP": "64"},
+    {"RT_TAIL": "1", "RT_TAIL_ALL": "1", "RT_FBS_CAP": "64", "RT_FORCE_FALLBACK": "2"},
     # phase A's stragglers to k_tail_a (levels 0..1, then phase B as usual)
     {"RT_TAIL_A": "1", "RT_TAIL_A_B": "1"},
     {"RT_TAIL_A": "5000", "RT_TAIL_A_B": "5000", "RT_TAIL": "2000", "RT_TAIL_B": "2000"},
