@@ -325,10 +325,6 @@ __device__ __forceinline__ void fb_chain(const PcParams& p, unsigned entry) {
     if (i < p.fbc_cap) p.fbc[i] = entry;       // fbc_cap = cap: a sample defers at most one ray per launch
 }
 __device__ __forceinline__ void fb_shadow(const PcParams& p, unsigned owner) {
-    if (p.fin_mode) {                          // a phase-A record's shadow ray: its pixel waits for k_fallback
-        const unsigned lvp = owner / (unsigned)p.nlights;
-        if (lvp < (unsigned)p.la * (unsigned)p.cap) atomicOr(&p.pinfo[lvp % (unsigned)p.cap], kPathFb);
-    }
     const unsigned i = atomicAdd(&p.totals[5], 1u);
     if (i < p.fbs_cap) {
         p.fbs[i] = owner;
@@ -519,22 +515,6 @@ __device__ __forceinline__ unsigned unit_order(const PcParams& p, unsigned u, un
     return p.uorder_on ? p.uorder[u] : unit_col_order(p, u, units);
 }
 
-// A chain handed to k_tail: the record id whose reflection is its next ray (PcParams::tailq; each
-// continuation at most once, so cb entries suffice).  Lanes of a wave call it together or alone.
-__device__ __forceinline__ void tail_push(const PcParams& p, unsigned entry) {
-    const unsigned i = atomicAdd(&p.totals[7], 1u);
-    if (i < p.cb) p.tailq[i] = entry;
-}
-
-// A phase-A sample handed to k_tail_a: {sample | level << 31, the k_chain workgroup whose queue regions take
-// its tasks} (PcParams::tailqA, totals[11] entries, at most one per sample).  Its unit is marked heavy for the
-// next frame's dealing (the hand-off cut its step count short).
-__device__ __forceinline__ void tail_push_a(const PcParams& p, unsigned path, int level, unsigned blk, unsigned steps) {
-    const unsigned i = atomicAdd(&p.totals[11], 1u);
-    if (i < (unsigned)p.cap) p.tailqA[i] = make_uint2(path | ((unsigned)level << 31), blk);
-    if (p.urank) atomicMax(&p.ucost[path >> 8], max(steps, kHotSteps[0]));
-}
-
 // closest-hit chains of one phase (raytracer.cpp:385-439 minus the shading):
 // record each hit, queue its shadow tasks, follow (or hand on) mirrors.
 template <bool COUNT, bool CONT, bool BQ = CONT>
@@ -564,25 +544,9 @@ __device__ void chain_body(const rtk::DevScene& s, const rtk::Eye& e, const PcPa
     Walk wk;
     unsigned t_grab = 0, tsteps = 0, twit = 0, wit = 0;   // trace: grab time, own steps, wave steps
     unsigned ssteps = 0;     // phase A (p.urank): walk steps of the lane's current sample
-    // phase B's tail (PcParams::tail_live): this wave hands its chains to k_tail (wave-uniform), once the launch's
-    // live chains -- its continuations with records less those ended or handed on, counted in 8 sharded words
-    // (kLiveShard0) -- are at most tail_live
-    // phase A likewise (PcParams::tail_a): once every unit is taken and at most tail_a started samples are
-    // still in phase A (word 2 of a shard counts the samples started, word 1 those ended), a wave hands its
-    // samples to k_tail_a
-    bool to_tail = false, tail_go = false;
-    const bool tail_on = !COUNT && (CONT ? p.tail_live > 0 : p.tail_a > 0);
-    const unsigned nconts = CONT && tail_on ? min(p.totals[1], p.cb) : 0u;
-    unsigned* const live_shard = &p.totals[kLiveShard0 + kLiveStride * (blk & 7u) + (CONT ? 0 : 1)];
-    (void)to_tail;
-    (void)tail_go;
-    (void)nconts;
-    (void)live_shard;
     StepStat stat;
     while (true) {
         // (1) epilogue of finished walks: record, queue shadow tasks, reflect or hand on
-        bool fin = false;        // this lane's chain ended here or left for k_tail(_a) / k_fallback / phase B
-        bool started = false;    // phase A: this lane took a sample here
         if (st == kDone) {
             const HitRec h = wk.best;
             const bool hit = h.prim >= 0;
@@ -655,18 +619,12 @@ __device__ void chain_body(const rtk::DevScene& s, const rtk::Eye& e, const PcPa
             }
             if (ends || handoff) {
                 st = kIdle;
-                fin = true;
                 if (!CONT && !COUNT && p.urank && ssteps >= kHotSteps[1]) atomicMax(&p.ucost[path >> 8], ssteps);
                 if (kTraceBuild && p.trace && !CONT) { p.trace[2 * path] = t_grab; p.trace[2 * path + 1] = (unsigned)wall_clock64(); }
                 if (kTraceBuild && p.trace && CONT) {       // phase B: {grab, end, last level, walk steps} after A's entries
                     unsigned* tb = p.trace + 2 * ((size_t)p.cap + p.trace_blocks) + 4 * (size_t)path;
                     tb[0] = t_grab; tb[1] = (unsigned)wall_clock64(); tb[2] = (unsigned)k | ((wit - twit) << 8); tb[3] = tsteps;
                 }
-            } else if (!COUNT && to_tail) {   // the next level in k_tail(_a): its ray is this record's reflection
-                if (CONT) tail_push(p, (unsigned)lvp);
-                else tail_push_a(p, path, k + 1, blk, ssteps);
-                st = kIdle;
-                fin = true;
             } else {
                 const V dk = r.d;
                 r = reflect_ray(s, hitp, nn, r.d);
@@ -677,7 +635,6 @@ __device__ void chain_body(const rtk::DevScene& s, const rtk::Eye& e, const PcPa
                     if (!CONT) p.pinfo[path] = kPathCont;   // (k_fallback's path)
                     fb_chain(p, (unsigned)lvp);
                     st = kIdle;
-                    fin = true;
                 } else {
                     st = walk_begin<COUNT>(s, r, wk, w) ? kTrav : kDone;
                 }
@@ -729,12 +686,8 @@ __device__ void chain_body(const rtk::DevScene& s, const rtk::Eye& e, const PcPa
                             k = (int)(lvp / (unsigned)p.cap) + 1;
                             r = reflect_from_record(s, p, lvp, path);
                             nrefl++;
-                            if (!COUNT && defer_closest(s, r)) {
-                                fb_chain(p, lvp);
-                                fin = true;
-                            } else {
-                                st = walk_begin<COUNT>(s, r, wk, w) ? kTrav : kDone;
-                            }
+                            if (!COUNT && defer_closest(s, r)) fb_chain(p, lvp);
+                            else st = walk_begin<COUNT>(s, r, wk, w) ? kTrav : kDone;
                         } else {
                             const unsigned idx = (dyn ? uid : blk + (v >> 8) * G) * 256u + (v & 255u);
                             if (slab_sample_ray(p, idx, &r)) {
@@ -743,14 +696,10 @@ __device__ void chain_body(const rtk::DevScene& s, const rtk::Eye& e, const PcPa
                                 ssteps = 0;
                                 if (kTraceBuild && p.trace) t_grab = (unsigned)wall_clock64();
                                 nprim++;
-                                started = true;
-                                if (s.max_depth < 0) {
-                                    p.pinfo[path] = 0 | (kEndZero << 8);   // depth 0 > max: black
-                                    fin = true;
-                                } else if (!COUNT && defer_closest(s, r)) {
+                                if (s.max_depth < 0) p.pinfo[path] = 0 | (kEndZero << 8);   // depth 0 > max: black
+                                else if (!COUNT && defer_closest(s, r)) {
                                     p.pinfo[path] = kPathCont;   // (k_fallback's path)
                                     fb_chain(p, kFbEye | path);
-                                    fin = true;
                                 }
                                 else st = walk_begin<COUNT>(s, r, wk, w) ? kTrav : kDone;
                             }
@@ -759,56 +708,14 @@ __device__ void chain_body(const rtk::DevScene& s, const rtk::Eye& e, const PcPa
                 }
             }
         }
-        if (tail_on) {               // the live-chain counts (ended, and phase A's started)
-            const unsigned nf = (unsigned)__popcll(__ballot(fin)), ns = (unsigned)__popcll(__ballot(started));
-            if (nf && lane_id() == 0) atomicAdd(live_shard, nf);
-            if (!CONT && ns && lane_id() == 0) atomicAdd(live_shard + 1, ns);
-        }
         if (!__any(st != kIdle)) {
             if (exhausted) break;
             continue;
         }
         // (3) walk until enough lanes need service
         const int thresh = exhausted ? 0 : (CONT ? p.brefill : p.refill);
-        unsigned poll = 0;
         while (true) {
-            const int nt = __popcll(__ballot(st == kTrav));
-            // phase B's tail starts once at most tail_live of the launch's chains are left (polled every 32
-            // iterations by an exhausted wave): then most of the GPU is idle, and the chains left walk on whole
-            // waves in k_tail instead of beside each other here
-            if (tail_on && exhausted && !tail_go && (poll++ & 31u) == 0u) {
-                const int ln = lane_id();
-                const int wd = CONT ? 0 : 1;
-                unsigned v = ln < 8 ? __hip_atomic_load(&p.totals[kLiveShard0 + kLiveStride * ln + wd], __ATOMIC_RELAXED,
-                                                        __HIP_MEMORY_SCOPE_AGENT)
-                                    : 0u;
-                unsigned u = !CONT && ln < 8 ? __hip_atomic_load(&p.totals[kLiveShard0 + kLiveStride * ln + 2],
-                                                                 __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
-                                             : 0u;
-#pragma unroll
-                for (int o = 1; o < 8; o <<= 1) {
-                    v += __shfl_xor(v, o, 64);
-                    u += __shfl_xor(u, o, 64);
-                }
-                const unsigned ended = __shfl(v, 0, 64), begun = CONT ? nconts : __shfl(u, 0, 64);
-                tail_go = ended + (unsigned)(CONT ? p.tail_live : p.tail_a) >= begun;
-            }
-            // phase B's tail: each chain hands on the walk it is on (k_tail restarts it from its ray, the reflection
-            // of the previous level's record), and the lanes whose walk just finished record it and hand on the next
-            // level (the epilogue above); (tail_all, tests: every chain's first phase-B walk, exhausted or not)
-            if (tail_on && ((exhausted && tail_go) || p.tail_all)) {
-                to_tail = true;
-                const bool tr = st == kTrav;
-                if (tr) {
-                    if (CONT) tail_push(p, (unsigned)rec_id(p, k - 1, path, cix));
-                    else tail_push_a(p, path, k, blk, ssteps);
-                    st = kIdle;
-                }
-                const unsigned nf = (unsigned)__popcll(__ballot(tr));
-                if (nf && lane_id() == 0) atomicAdd(live_shard, nf);
-                break;
-            }
-            if (nt <= thresh ||
+            if (__popcll(__ballot(st == kTrav)) <= thresh ||
                 __popcll(__ballot(st == kDone)) >= (CONT ? (exhausted ? p.btail : p.bservice) : p.service))
                 break;
             stat.step(st == kTrav, wk.cur >= 0, RT_STEP_STATS && st == kTrav && wk.tree == nullptr && leaf_postponed(s.leaf_wait, wk));
@@ -1003,19 +910,11 @@ __device__ __forceinline__ void lq_flush(const rtk::DevScene& s, const Ray& r, f
 }
 
 // The shadow tasks tasks[j] of this workgroup (as occlude_body) with the leaf queue; production only.
-// dctr (a launch-wide counter, zeroed before the launch): the tasks are dealt dynamically instead, in chunks of
-// p.dchunk consecutive tasks, the workgroup's k-th chunk taken from the counter by the wave whose grab first
-// reaches it (in order, as chain_body's dynamic units; g_uid, reset by the caller), so workgroups that start
-// late or finish early balance the work; at most kDynUnits chunks per workgroup.
-// ochunk: static chunk size (0: p.ochunk).
 __device__ void occlude_queue_body(const rtk::DevScene& s, const PcParams& p, unsigned blk, unsigned G,
-                                   const unsigned* tasks, unsigned total, unsigned* dctr = nullptr,
-                                   unsigned ochunk = 0) {
+                                   const unsigned* tasks, unsigned total) {
     const int lane = lane_id(), wave = (int)(threadIdx.x >> 6);
-    const unsigned sC = ochunk ? ochunk : (unsigned)p.ochunk;
-    const unsigned dC = (unsigned)p.dchunk, nchunks = dctr ? (total + dC - 1) / dC : 0u;
-    const unsigned n = dctr ? (unsigned)kDynUnits * dC : chunk_count(total, G, blk, sC);
-    const UDiv och(sC), nld((unsigned)s.nlights);
+    const unsigned n = chunk_count(total, G, blk, (unsigned)p.ochunk);
+    const UDiv och((unsigned)p.ochunk), nld((unsigned)s.nlights);
     // the queue count, the hit mask and the queued counts are written by other lanes of the wave:
     // every read is an atomic load (no value kept in a register across the loop)
     if (lane == 0) {
@@ -1059,36 +958,10 @@ __device__ void occlude_queue_body(const rtk::DevScene& s, const PcParams& p, un
                 prog = true;
                 const unsigned base = wave_grab_lds(&g_head, idle);
                 if (base + (unsigned)__popcll(idle) >= n) exhausted = true;
-                unsigned gid = 0;                  // dctr: the lane's chunk (kUidNone: none left)
-                if (dctr) {
-                    const unsigned jf = (base + dC - 1u) / dC;      // the first chunk starting inside this grab
-                    if (lane == 0 && jf * dC < base + (unsigned)__popcll(idle) && jf < (unsigned)kDynUnits) {
-                        bool late = false;
-                        unsigned ns = 0;
-                        if (jf > 0)
-                            while (lds_load(&g_uid[jf - 1]) == kUidUnset) {
-                                if (spin_over(s, ns)) { late = true; break; }
-                                __builtin_amdgcn_s_sleep(1);
-                            }
-                        const unsigned g = late ? nchunks : atomicAdd(dctr, 1u);
-                        lds_store(&g_uid[jf], g < nchunks ? g : kUidNone);
-                    }
-                    const unsigned idx = base + lane_rank(idle);
-                    if (!have && idx < n) {
-                        unsigned ns = 0;
-                        while ((gid = lds_load(&g_uid[idx / dC])) == kUidUnset) {
-                            if (spin_over(s, ns)) { gid = kUidNone; break; }
-                            __builtin_amdgcn_s_sleep(1);
-                        }
-                    }
-                    if (__any(!have && idx < n && gid == kUidNone)) exhausted = true;
-                }
                 if (!have) {
                     const unsigned idx = base + lane_rank(idle);
-                    const unsigned j = dctr ? (gid == kUidNone ? total : gid * dC + idx % dC)
-                                            : (idx < n ? chunk_task(idx, G, blk, och) : total);
-                    if (j < total) {
-                        owner = tasks[j];
+                    if (idx < n) {
+                        owner = tasks[chunk_task(idx, G, blk, och)];
                         r = shadow_from_record(s, p, owner, &tlim, nld);
                         if (defer_any(s, r)) {
                             fb_shadow(p, owner);
@@ -1318,375 +1191,21 @@ template <bool COUNT, bool BQ>
 __global__ __launch_bounds__(kBlock, BQ || COUNT ? RT_MIX_WAVES : RT_MIX_NOBQ_WAVES) void k_mix(rtk::DevScene s,
                                                                                                   rtk::Eye e, PcParams p) {
     const bool chain = blockIdx.x < (unsigned)p.gb;
-    const unsigned t_start = kTraceBuild && p.trace ? (unsigned)wall_clock64() : 0u;
-    unsigned t_chain = 0;
     if (threadIdx.x == 0) g_ccnt = 0;
     if (BQ && chain && kBq > 0) bq_init();
     block_init(s);
     if (chain) {
         if (p.bprio) __builtin_amdgcn_s_setprio(3);    // the deep chains are the frame's critical path
         chain_body<COUNT, true, BQ>(s, e, p, blockIdx.x, (unsigned)p.gb, phase_b(p));
-        if (kTraceBuild && p.trace) t_chain = (unsigned)wall_clock64();
-    }
-    if constexpr (!COUNT && RT_LEAF_QUEUE) {
-        // A's shadow tasks: dealt dynamically in p.dchunk chunks when dchunk > 0, and then the chain workgroups
-        // join once their chains are done or handed to k_tail; else statically to the shadow-role workgroups
-        if (p.dchunk > 0) {
-            if (chain) {
-                __syncthreads();                   // every wave is done with the chain role's LDS
-                if (threadIdx.x == 0) g_head = 0;
-            }
-            if (threadIdx.x < kDynUnits) g_uid[threadIdx.x] = kUidUnset;
-            __syncthreads();
-            occlude_queue_body(s, p, 0, 1, p.sflatA, p.totals[0], &p.totals[10]);
-        } else if (!chain) {
+    } else {
+        if constexpr (!COUNT && RT_LEAF_QUEUE)
             occlude_queue_body(s, p, blockIdx.x - p.gb, gridDim.x - p.gb, p.sflatA, p.totals[0]);
-        }
-    } else if (!chain) {
-        occlude_body<COUNT>(s, p, blockIdx.x - p.gb, gridDim.x - p.gb, p.sflatA, p.totals[0], 0);
+        else
+            occlude_body<COUNT>(s, p, blockIdx.x - p.gb, gridDim.x - p.gb, p.sflatA, p.totals[0], 0);
     }
     // a lone frame's next unit order, by the last shadow-role workgroup once its shadow rays are done:
     // beside phase B's deep chains, off the frame's critical path (in k_pack_a it cost 30 us there)
     if (!COUNT && !chain && p.urank && blockIdx.x == gridDim.x - 1) rank_units(p);
-    if (kTraceBuild && p.trace) {            // diagnostics: {start, chain role end, end, role} per workgroup
-        __syncthreads();
-        if (threadIdx.x == 0 && blockIdx.x < (unsigned)p.trace_blocks) {
-            unsigned* tm = p.trace + 2 * ((size_t)p.cap + p.trace_blocks) + 4 * (size_t)p.cap + 4 * (size_t)blockIdx.x;
-            tm[0] = t_start; tm[1] = t_chain; tm[2] = (unsigned)wall_clock64(); tm[3] = chain ? 1u : 2u;
-        }
-    }
-}
-
-// ---------------------------------------------------------------------------
-// k_tail: phase B's last chains, one WAVE per chain.
-//
-// A lone frame's time is set by its deepest mirror chains: ~150 dependent walk steps
-// after phase A, each ~250 dependent VALU instructions when a lane walks its own ray, and in k_mix a
-// lane's chain also waits for the other walks of its wave.  Once k_mix's chain waves run out of
-// continuations, the few chains left leave them at a level boundary (chain_body: PcParams::tail_live) and
-// this kernel walks each on a whole wave: the ray and the walk state are wave-uniform, lane c < 6 tests
-// slot c of a wide node (its six planes, not all 36), lane j tests primitive j of a leaf record, and the
-// traversal stack is one entry per lane (lane i holds entry i), pushed with v_writelane and popped with
-// v_readlane -- a step is ~50 instructions instead of ~250, with no LDS round trip.
-//
-// The walk is wide_closest_step's, entry for entry: the slots of a node in the reference's visiting order
-// (the node's rank word for the ray's octant), the first passing one next, the others pushed highest rank
-// deepest with their entry t, re-checked against tMax when popped; a leaf record's EXACT box tested like
-// the reference's leaf pop, then its primitives folded in stored order with the reference's update rule
-// (raytracer.cpp:210-222) -- so the hit, and every record, occlusion task and path word written here, are
-// the ones k_mix would have written.  The epilogue is chain_body's (record, shadow tasks -- into the owning
-// k_mix workgroup's phase-B region, walked by k_occlude after this kernel -- path end, or the reflection).
-// ---------------------------------------------------------------------------
-__device__ __forceinline__ int rdl(int v, int l) { return __builtin_amdgcn_readlane(v, l); }
-__device__ __forceinline__ float rdlf(float v, int l) { return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), l)); }
-
-// The reference's closest hit of a NaN-free, wide-range ray (walk_begin's wide case), walked by the whole
-// wave; every lane returns the same result.
-__device__ HitRec tail_closest(const rtk::DevScene& s, const Ray& r, int* steps_out = nullptr) {
-    constexpr int W = dl::kWideSlots;
-    const int lane = lane_id();
-    HitRec best{-1.0f, -1};
-    float tmax = FLT_MAX;
-    int stk_code = 0;                       // lane i: stack entry i {code, entry t}
-    float stk_t = 0.0f;
-    int sp = 0;
-    int cur = s.wroot;
-    const int sgn = (r.d.x > 0.0f ? 1 : 0) | (r.d.y > 0.0f ? 2 : 0) | (r.d.z > 0.0f ? 4 : 0);
-    const int ridx = (sgn & 4) ? (sgn ^ 7) : sgn;
-    // slot lane c: the plane dwords' half and pair (lanes >= 6 mirror slot 5 and are never valid)
-    const int c = lane < W ? lane : W - 1;
-    const int pr = c >> 1;
-    const uint32_t hs = (uint32_t)(c & 1) << 4;
-    const float ro[3] = {r.o.x, r.o.y, r.o.z}, ri[3] = {r.inv.x, r.inv.y, r.inv.z};
-    int steps = 0;
-    while (true) {
-        if (++steps > s.walk_cap) {                               // walk_runaway
-            __hip_atomic_fetch_or(s.err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            break;
-        }
-        cur = __builtin_amdgcn_readfirstlane(cur);
-        if (cur >= 0) {
-            const uint32_t* N = reinterpret_cast<const uint32_t*>(&s.wnodes[cur]);
-            const float4 hd = *reinterpret_cast<const float4*>(N);
-            uint32_t rw = N[28 + ridx];
-            uint32_t pl[6];
-#pragma unroll
-            for (int a = 0; a < 3; ++a) {
-                pl[a] = N[4 + a * 3 + pr] >> hs;
-                pl[3 + a] = N[13 + a * 3 + pr] >> hs;
-            }
-            const int code = (int)N[22 + c];
-            const uint32_t ex = __float_as_uint(hd.w);
-            if (sgn & 4) rw = (uint32_t)(__builtin_popcount(ex >> 24) - 1) * 0111111u - rw;
-            // slot c's box: wide_slabs' arithmetic for one slot (the same operations on the same words)
-            const float org[3] = {hd.x, hd.y, hd.z};
-            float tmn = 0.0f, tmx = 0.0f;
-#pragma unroll
-            for (int a = 0; a < 3; ++a) {
-                const float sc = __uint_as_float(((ex >> (8 * a)) & 255u) << 23);
-                const bool neg = __float_as_int(ri[a]) < 0;
-                const float si = sc * ri[a];
-                const float z = org[a] - ro[a];
-                const float oi = z * ri[a];
-                const float cc = __builtin_fmaf(sc, 0x1p-5f, __builtin_fabsf(org[a]) * 0x1p-23f);
-                const float m = __builtin_fmaf(__builtin_fabsf(z), 6.0f * 0x1p-23f, cc);
-                const float M = __builtin_fmaf(m, __builtin_fabsf(ri[a]), 0x1p-126f);
-                const uint32_t nw = neg ? pl[3 + a] : pl[a], fw = neg ? pl[a] : pl[3 + a];
-                const float tn = fma_mix_h<0>(nw, si, oi - M), tf = fma_mix_h<0>(fw, si, oi + M);
-                tmn = a == 0 ? tn : __builtin_fmaxf(tmn, tn);
-                tmx = a == 0 ? tf : __builtin_fminf(tmx, tf);
-            }
-            const bool valid = lane < W && tmx >= __builtin_fmaxf(0.0f, tmn) && tmn <= tmax;
-            const uint32_t vs = (uint32_t)__ballot(valid);        // by slot
-            if (vs) {
-                const uint32_t rws = (uint32_t)__builtin_amdgcn_readfirstlane((int)rw);
-                uint32_t vm = 0;                                   // valid slots in rank order
-#pragma unroll
-                for (int j = 0; j < W; ++j) vm |= ((vs >> j) & 1u) << ((rws >> (3 * j)) & 7u);
-                const uint32_t first = (uint32_t)__builtin_ctz(vm);
-                // slot lane c's stack position: sp + (valid slots ranked after it), the first slot (the next
-                // node) at the top, sp + np, which the pop reads back at once (the reference visits the first
-                // next, then the others in rank order); invalid slots aim at no lane
-                const int np = __builtin_popcount(vm) - 1;
-                const uint32_t rk = (rw >> (3 * c)) & 7u;
-                const int pos = valid ? sp + __builtin_popcount(vm >> (rk + 1u)) : -1;
-                // lane i takes the entry of the slot lane aiming at it (straight-line, one slot at a time)
-#pragma unroll
-                for (int j = 0; j < W; ++j) {
-                    const int pj = rdl(pos, j);
-                    const int vc = rdl(code, j);
-                    const float vt = rdlf(tmn, j);
-                    stk_code = lane == pj ? vc : stk_code;
-                    stk_t = lane == pj ? vt : stk_t;
-                }
-                (void)first;
-                sp += np;
-                cur = rdl(stk_code, sp);
-                continue;
-            }
-        } else {
-            const float4* L = s.lrec + (cur & ~dl::kLeafBit);
-            const float4 h0 = L[0], h1 = L[1];
-            float lt;
-            if (box_hit_fast(r, h0, h1, &lt) && lt <= tmax) {        // the reference leaf's exact box (:184)
-                const int cnt = __builtin_amdgcn_readfirstlane(__float_as_int(h0.w));
-                const int slot0 = __float_as_int(h1.w);
-                for (int b0 = 0; b0 < cnt; b0 += 64) {
-                    const int j = b0 + lane;
-                    bool h = false;
-                    float t = 0.0f;
-                    if (j < cnt) {
-                        const float4 p0 = L[2 + 3 * j], p1 = L[3 + 3 * j], p2 = L[4 + 3 * j];
-                        h = __float_as_int(p0.w) >= 0 ? tri_hit(r, p0, p1, p2, &t) : sphere_hit(r, p0, p1, &t);
-                    }
-                    // the hits in stored order, with the reference's update rule (:213-221)
-                    for (uint64_t hm = __ballot(h); hm; hm &= hm - 1ull) {
-                        const int jj = __builtin_ctzll(hm);
-                        const float tj = rdlf(t, jj);
-                        if (tj < best.t || best.t == -1.0f) {
-                            best.t = tj;
-                            best.prim = slot0 + b0 + jj;
-                            tmax = tj;
-                        }
-                    }
-                }
-            }
-        }
-        bool found = false;                                        // pop until an entry passes its tMax check
-        while (sp > 0) {
-            --sp;
-            const float et = rdlf(stk_t, sp);
-            if (et <= tmax) {
-                cur = rdl(stk_code, sp);
-                found = true;
-                break;
-            }
-        }
-        if (!found) break;
-    }
-    if (steps_out) *steps_out = steps;
-    return best;
-}
-
-// Chain entry e (PcParams::tailq) to its end: k_mix's chain_body epilogue per level, on one wave.
-__device__ void tail_chain(const rtk::DevScene& s, const PcParams& p, unsigned e) {
-    const unsigned cap = (unsigned)p.cap, aspace = (unsigned)p.la * cap;
-    unsigned path, c;
-    int k;
-    if (e < aspace) {                              // phase A's last record: the continuation's start
-        path = e % cap;
-        k = (int)(e / cap) + 1;
-        c = p.cid[path];
-    } else {
-        const unsigned q = e - aspace;
-        c = q % p.cb;
-        k = p.la + (int)(q / p.cb) + 1;
-        path = (p.cflat[c] & ~kFbEye) % cap;
-    }
-    // shadow tasks: a flat list (sflatB, totals[2]) where B's regions are walked in place (lone frames: k_occlude
-    // walks it after them); else the owning k_mix workgroup's region, which k_pack_b packs
-    const unsigned blk = (c / (unsigned)p.tchunk) % (unsigned)p.gb;
-    unsigned* const sq = p.occ_inplace_b ? p.sflatB : p.sqB + (size_t)blk * p.scapB;
-    unsigned* const sn = p.occ_inplace_b ? &p.totals[2] : &p.scntB[blk];
-    const int nl = s.nlights;
-    Ray r = reflect_from_record(s, p, e, path);
-    size_t prev = e;
-    const bool lead = lane_id() == 0;
-    while (true) {
-        if (defer_closest(s, r)) {                 // the rest of this path: k_fallback
-            if (lead) fb_chain(p, (unsigned)prev);
-            return;
-        }
-        const HitRec h = tail_closest(s, r);
-        const bool hit = h.prim >= 0;
-        V nn{0.0f, 0.0f, 0.0f}, hitp{0.0f, 0.0f, 0.0f};
-        int mat = 0, code = 0;
-        const size_t lvp = rec_id(p, k, path, c);
-        if (hit) {
-            hit_surface(s, r, h, &nn, &mat, &code);
-            hitp = add(r.o, mul(r.d, h.t));
-            if (lead) rec_write(p, lvp, hitp, code, r.d, mat);
-            // one shadow task per light whose ray can change the pixel (light_needed), appended to the owning
-            // workgroup's phase-B region
-            const unsigned own0 = (unsigned)(lvp * nl);
-            unsigned want = 0;
-            for (int l = 0; l < nl && l < 32; ++l) {
-                if (s.cull_shadows && !light_needed(s, hitp, nn, l)) {
-                    if (lead) p.occ[lvp * nl + l] = 1;     // shaded as occluded: the same sum (light_needed)
-                } else {
-                    want |= 1u << l;
-                }
-            }
-            for (int l = 32; l < nl; ++l) {       // (more than 32 lights: one task at a time)
-                if (s.cull_shadows && !light_needed(s, hitp, nn, l)) {
-                    if (lead) p.occ[lvp * nl + l] = 1;
-                } else if (lead) {
-                    sq[atomicAdd(sn, 1u)] = own0 + (unsigned)l;
-                }
-            }
-            if (want && lead) {
-                unsigned at = atomicAdd(sn, (unsigned)__builtin_popcount(want));
-                for (uint32_t wm = want; wm; wm &= wm - 1u) sq[at++] = own0 + (unsigned)__builtin_ctz(wm);
-            }
-        }
-        if (!hit) {                                                          // :442-449
-            if (lead) p.pinfo[path] = k | (kEndZero << 8) | kPathCont;
-            return;
-        }
-        if (!s.mats[mat - 1].is_mirror) {
-            if (lead) p.pinfo[path] = (k + 1) | (kEndLast << 8) | kPathCont;
-            return;
-        }
-        if (k >= s.max_depth) {                    // child beyond MaxRecursionDepth: 0 (:387-389)
-            if (lead) p.pinfo[path] = (k + 1) | (kEndZero << 8) | kPathCont;
-            return;
-        }
-        r = reflect_ray(s, hitp, nn, r.d);
-        ++k;
-        prev = lvp;
-    }
-}
-
-// Phase A's stragglers (PcParams::tailqA), one wave each: sample `path` from level `level` to the end of phase
-// A -- chain_body's phase-A epilogue per level (record, shadow tasks into the owning k_chain workgroup's region,
-// path end, or the continuation handed to phase B in that workgroup's continuation region), so k_pack_a and
-// phase B see exactly what k_chain would have left.
-__device__ void tail_chain_a(const rtk::DevScene& s, const PcParams& p, uint2 e) {
-    const unsigned path = e.x & 0x7fffffffu, blk = e.y;
-    int k = (int)(e.x >> 31);
-    const int nl = s.nlights;
-    const bool lead = lane_id() == 0;
-    Ray r;
-    slab_sample_ray(p, path, &r);                  // the eye ray (level 0)
-    if (k == 1) {                                  // level 1: the reflection of record 0 (reflect_from_record's values)
-        const float4 a = p.rec[path];
-        const V h0{a.x, a.y, a.z};
-        r = reflect_ray(s, h0, surface_normal(s, h0, __float_as_int(a.w)), r.d);
-    }
-    while (true) {
-        if (defer_closest(s, r)) {                 // the rest of this path: k_fallback
-            if (lead) {
-                p.pinfo[path] = kPathCont;         // (k_fallback's path)
-                if (k == 0) {
-                    fb_chain(p, kFbEye | path);
-                } else {
-                    const unsigned prev = (unsigned)rec_id(p, k - 1, path, 0);
-                    if (prev < p.dbase) {          // reflect_from_record: the direction of level k - 1
-                        Ray r0;
-                        slab_sample_ray(p, path, &r0);
-                        p.tail[path] = make_float4(r0.d.x, r0.d.y, r0.d.z, 0.0f);
-                    }
-                    fb_chain(p, prev);
-                }
-            }
-            return;
-        }
-        const HitRec h = tail_closest(s, r);
-        const bool hit = h.prim >= 0;
-        V nn{0.0f, 0.0f, 0.0f}, hitp{0.0f, 0.0f, 0.0f};
-        int mat = 0, code = 0;
-        const size_t lvp = rec_id(p, k, path, 0);
-        if (hit) {
-            hit_surface(s, r, h, &nn, &mat, &code);
-            hitp = add(r.o, mul(r.d, h.t));
-            if (lead) rec_write(p, lvp, hitp, code, r.d, mat);
-            const unsigned own0 = (unsigned)(lvp * nl);
-            unsigned* const sq = p.sqA + (size_t)blk * p.scapA;
-            for (int l = 0; l < nl; ++l) {
-                if (s.cull_shadows && !light_needed(s, hitp, nn, l)) {
-                    if (lead) p.occ[lvp * nl + l] = 1;     // shaded as occluded: the same sum (light_needed)
-                } else if (lead) {
-                    sq[atomicAdd(&p.scntA[blk], 1u)] = own0 + (unsigned)l;
-                }
-            }
-        }
-        if (!hit) {                                                          // :442-449
-            if (lead) p.pinfo[path] = k | ((k == 0 ? kEndBg : kEndZero) << 8);
-            return;
-        }
-        if (!s.mats[mat - 1].is_mirror) {
-            if (lead) p.pinfo[path] = (k + 1) | (kEndLast << 8);
-            return;
-        }
-        if (k >= s.max_depth) {                    // child beyond MaxRecursionDepth: 0 (:387-389)
-            if (lead) p.pinfo[path] = (k + 1) | (kEndZero << 8);
-            return;
-        }
-        if (k >= p.kinline) {                      // deeper levels: phase B, a continuation of this workgroup
-            if (lead) {
-                p.cq[(size_t)blk * p.ccapA + atomicAdd(&p.ccnt[blk], 1u)] = (unsigned)((size_t)k * p.cap + path);
-                p.pinfo[path] = kPathCont;
-                if (lvp < p.dbase) p.tail[path] = make_float4(r.d.x, r.d.y, r.d.z, 0.0f);   // reflect_from_record
-            }
-            return;
-        }
-        r = reflect_ray(s, hitp, nn, r.d);
-        ++k;
-    }
-}
-
-__global__ __launch_bounds__(64) void k_tail_a(rtk::DevScene s, PcParams p) {
-    const unsigned n = min(p.totals[11], (unsigned)p.cap);
-    unsigned i = blockIdx.x;
-    while (i < n) {
-        tail_chain_a(s, p, p.tailqA[i]);
-        unsigned next = 0;
-        if (lane_id() == 0) next = gridDim.x + atomicAdd(&p.totals[12], 1u);
-        i = (unsigned)__builtin_amdgcn_readfirstlane((int)next);
-    }
-}
-
-// One wave per workgroup; wave w first takes entry w, then the next entries from a launch-wide counter
-// (totals[8]), so a long chain does not hold up others behind it and the first round has no contention.
-__global__ __launch_bounds__(64) void k_tail(rtk::DevScene s, PcParams p) {
-    const unsigned n = min(p.totals[7], p.cb);
-    unsigned i = blockIdx.x;
-    while (i < n) {
-        tail_chain(s, p, p.tailq[i]);
-        unsigned next = 0;
-        if (lane_id() == 0) next = gridDim.x + atomicAdd(&p.totals[8], 1u);
-        i = (unsigned)__builtin_amdgcn_readfirstlane((int)next);
-    }
 }
 
 // Phase B's shadow tasks (which = 1), or phase A's (which = 0: p.split_occ, frame batches).
@@ -1700,13 +1219,6 @@ __global__ __launch_bounds__(kBlock, RT_OCC_WAVES_PER_EU) void k_occlude(rtk::De
         const bool inplace = which ? p.occ_inplace_b != 0 : p.occ_inplace != 0;
         if (inplace) {
             occlude_regions(s, p, which, blockIdx.x, gridDim.x);
-            if (which && p.tail_live > 0) {       // k_tail's shadow tasks (a flat list in sflatB, totals[2])
-                __syncthreads();
-                if (threadIdx.x == 0) g_head = 0;
-                __syncthreads();
-                // (one task per workgroup at a time: few rays, from the deepest chains, spread over the GPU)
-                occlude_queue_body(s, p, blockIdx.x, gridDim.x, p.sflatB, p.totals[2], nullptr, 1u);
-            }
         } else if (which) {
             occlude_queue_body(s, p, blockIdx.x, gridDim.x, p.sflatB, p.totals[2]);
         } else {
@@ -1932,7 +1444,7 @@ template <bool LDS, bool CMP>
 __device__ __forceinline__ void finish_pixels(const rtk::DevScene& s, const rtk::Eye& e, const PcParams& p) {
     const int F = p.aa;
     const unsigned gtid = blockIdx.x * kBlock + threadIdx.x, gstride = gridDim.x * kBlock;
-    if (p.fin_cont && p.fin_mode != 1) {
+    if (p.fin_cont) {
         const unsigned n = p.totals[1];
         for (unsigned j = gtid; j < n; j += gstride) {
             const unsigned path = (p.cflat[j] & ~kFbEye) % (unsigned)p.cap;
@@ -1950,24 +1462,6 @@ __device__ __forceinline__ void finish_pixels(const rtk::DevScene& s, const rtk:
         }
     }
     const int npix = (p.chunk_rows / p.aa) * p.width;
-    if (p.fin_mode) {
-        // the split: part 1 the pixels final after k_mix, part 2 the pixels with a kPathFb sample (the continued
-        // ones came first above); after a fallback-queue overflow (any occlusion byte may still change) part 2
-        // takes every pixel
-        const bool all = p.totals[6] != 0;
-        if (p.fin_mode == 1 && all) return;
-        for (int q = (int)gtid; q < npix; q += (int)gstride) {
-            const int rr = q / p.width, ocol = q - rr * p.width;
-            int bits = 0;
-            for (int k = 0; k < p.aa; ++k)
-                for (int l = 0; l < p.aa; ++l) bits |= p.pinfo[slab_slot(p.tiles_x, ocol * p.aa + l, rr * p.aa + k)];
-            const bool later = (bits & (kPathCont | kPathFb)) != 0;
-            if (p.fin_mode == 1 ? !later
-                                : !(p.fin_cont && (bits & kPathCont)) && (all || later))   // (fin_cont: the loop above)
-                finish_pixel<LDS, CMP>(s, e, p, rr, ocol);
-        }
-        return;
-    }
     for (int q = (int)gtid; q < npix; q += (int)gstride) {
         const int rr = q / p.width, ocol = q - rr * p.width;
         if (p.fin_cont && pixel_cont(p, rr, ocol)) continue;
@@ -2087,7 +1581,7 @@ __device__ void fallback_chain(const rtk::DevScene& s, const rtk::Eye& e, const 
     }
     for (int i = n - 1; i >= 0; --i) c = vclamp(add(Ls[i], had(c, Km[i])), 0.0f, FLT_MAX);   // :436-451
     p.tail[path] = make_float4(c.x, c.y, c.z, 0.0f);
-    p.pinfo[path] = k0 | (kEndTail << 8) | (k0 >= p.la || cont ? kPathCont : 0) | (p.fin_mode ? kPathFb : 0);
+    p.pinfo[path] = k0 | (kEndTail << 8) | (k0 >= p.la || cont ? kPathCont : 0);
 }
 
 __global__ __launch_bounds__(kBlock) void k_fallback(rtk::DevScene s, rtk::Eye e, PcParams p) {
@@ -2104,8 +1598,6 @@ __global__ __launch_bounds__(kBlock) void k_fallback(rtk::DevScene s, rtk::Eye e
         atomicAdd(&p.counters[kCntFbChains], (unsigned long long)p.totals[4]);
         atomicAdd(&p.counters[kCntFbShadows], (unsigned long long)p.totals[5]);
         if (p.totals[6]) atomicAdd(&p.counters[kCntFbOvfScans], 1ull);
-        atomicAdd(&p.counters[kCntFbTail], (unsigned long long)min(p.totals[7], p.cb));
-        atomicAdd(&p.counters[kCntFbTailA], (unsigned long long)min(p.totals[11], (unsigned)p.cap));
     }
     for (unsigned i = gt; i < nfc + novf; i += gs)
         fallback_chain(s, e, p, i < nfc ? p.fbc[i] : p.cflat[p.cb + (i - nfc)], stk, w, i >= nfc);
@@ -2181,8 +1673,6 @@ __global__ __launch_bounds__(kBlock) void k_walk_timing(rtk::DevScene s, const f
                     }
                     h = HitRec{0.0f, cur};
                 }
-            } else if (mode == 5) {              // k_tail's walk: the whole wave on one ray
-                if (threadIdx.x < 64) h = tail_closest(s, r, &steps);
             } else if ((int)threadIdx.x < lanes) {
                 Walk wk;
                 bool go = mode == 0 ? walk_begin<false>(s, r, wk, w) : walk_begin<true>(s, r, wk, w);
@@ -2235,7 +1725,6 @@ hipError_t launch_walk_timing(const rtk::DevScene& s, const float* rays, int n, 
                               unsigned long long* out, hipStream_t st) {
     if (mode == 0) hipLaunchKernelGGL(k_walk_timing<0>, dim3(1), dim3(kBlock), 0, st, s, rays, n, lanes, reps, out);
     else if (mode == 1) hipLaunchKernelGGL(k_walk_timing<1>, dim3(1), dim3(kBlock), 0, st, s, rays, n, lanes, reps, out);
-    else if (mode == 5) hipLaunchKernelGGL(k_walk_timing<5>, dim3(1), dim3(kBlock), 0, st, s, rays, n, lanes, reps, out);
     else if (mode == 3) hipLaunchKernelGGL(k_walk_timing<3>, dim3(1), dim3(kBlock), 0, st, s, rays, n, lanes, reps, out);
     else hipLaunchKernelGGL(k_walk_timing<4>, dim3(1), dim3(kBlock), 0, st, s, rays, n, lanes, reps, out);
     return hipGetLastError();
@@ -2297,22 +1786,17 @@ unsigned chain_block_scap(int n0, int grid, int levels, int nlights) {
 }
 
 hipError_t launch_chain_chunk(const rtk::DevScene& s, const rtk::Eye& e, const PcParams& p, bool count,
-                              hipStream_t st, KTimer* kt, const FinSplit* fs) {
+                              hipStream_t st, KTimer* kt) {
     const dim3 blk(kBlock);
     auto mark = [&](int k) { if (kt) kt->mark(k, st); };
     const bool phase_b = p.kinline < s.max_depth;     // any continuation possible
-    {   // B's packed count (k_tail's flat list where B's regions are walked in place), the dynamic unit and
-        // shadow-chunk counters, k_fallback's counts, the tail's counters
-        const hipError_t me = hipMemsetAsync(p.totals + 2, 0, (kTotalsWords - 2) * sizeof(unsigned), st);
+    {   // the dynamic unit counter and k_fallback's counts
+        const hipError_t me = hipMemsetAsync(p.totals + 3, 0, (kTotalsWords - 3) * sizeof(unsigned), st);
         if (me != hipSuccess) return me;
     }
     mark(kKChain);
     if (count) hipLaunchKernelGGL(k_chain<true>, dim3(p.grid), blk, 0, st, s, e, p);
     else hipLaunchKernelGGL(k_chain<false>, dim3(p.grid), blk, 0, st, s, e, p);
-    if (p.tail_a > 0 && !count) {                   // phase A's stragglers, one wave each
-        mark(kKTail);
-        hipLaunchKernelGGL(k_tail_a, dim3(p.tail_grid), dim3(64), 0, st, s, p);
-    }
     mark(kKPackA);
     hipLaunchKernelGGL(k_pack_a, dim3(p.grid), blk, 0, st, p);
     PcParams q = p;
@@ -2329,22 +1813,6 @@ hipError_t launch_chain_chunk(const rtk::DevScene& s, const rtk::Eye& e, const P
     } else {
         if (split) hipLaunchKernelGGL((k_mix<false, false>), dim3(mgrid), blk, 0, st, s, e, q);
         else hipLaunchKernelGGL((k_mix<false, true>), dim3(mgrid), blk, 0, st, s, e, q);
-    }
-    // k_finish split (fin_mode): the pixels final after k_mix shade on the side stream beside the rest
-    const bool fsplit = fs && fs->side && p.fin_mode && phase_b && !count && !split;
-    if (fsplit) {
-        hipError_t e2 = hipEventRecord(fs->fork, st);
-        if (e2 == hipSuccess) e2 = hipStreamWaitEvent(fs->side, fs->fork, 0);
-        if (e2 != hipSuccess) return e2;
-        PcParams f1 = p;
-        f1.fin_cont = p.aa == 1;
-        f1.fin_mode = 1;
-        launch_finish(s, e, f1, fs->side);
-        if ((e2 = hipEventRecord(fs->join, fs->side)) != hipSuccess) return e2;
-    }
-    if (p.tail_live > 0 && phase_b && !count) {   // phase B's tail chains, one wave each
-        mark(kKTail);
-        hipLaunchKernelGGL(k_tail, dim3(p.tail_grid), dim3(64), 0, st, s, p);
     }
     if (split) {
         mark(kKOccA);
@@ -2365,13 +1833,8 @@ hipError_t launch_chain_chunk(const rtk::DevScene& s, const rtk::Eye& e, const P
     hipLaunchKernelGGL(k_fallback, dim3(p.fb_grid), blk, 0, st, s, e, p);
     PcParams f = p;
     f.fin_cont = phase_b && p.aa == 1;
-    f.fin_mode = fsplit ? 2 : 0;
     mark(kKFinish);
     launch_finish(s, e, f, st);
-    if (fsplit) {
-        const hipError_t e2 = hipStreamWaitEvent(st, fs->join, 0);
-        if (e2 != hipSuccess) return e2;
-    }
     mark(kKEnd);
     return hipGetLastError();
 }

@@ -58,9 +58,6 @@ constexpr unsigned kFbEye = 0x80000000u;
 constexpr uint8_t kOccDeferred = 2;
 // pinfo bit of a path continued in phase B (set by phase A's hand-off, kept by phase B's end)
 constexpr int kPathCont = 1 << 16;
-// pinfo bit of a path whose phase-A shadow ray went to k_fallback's queue (its occlusion byte is written there):
-// k_finish's split (PcParams::fin_mode) leaves its pixel to the part after k_fallback
-constexpr int kPathFb = 1 << 17;
 
 // Device counter block (u64 slots, RT_RENDER_COUNT launches).  0-6 are rt_stats' (primary, shadow,
 // reflection, node visits, triangle tests, sphere tests, skipped shadow rays); the per-role slots
@@ -88,8 +85,6 @@ enum CounterSlot : int {
     kCntFbChains,         //   closest-hit rays deferred (not in range of the wide trees' slab test)
     kCntFbShadows,        //   shadow rays deferred
     kCntFbOvfScans,       //   launches whose fallback shadow queue overflowed (occlusion bytes scanned)
-    kCntFbTail,           //   phase-B chains handed to k_tail
-    kCntFbTailA,          //   phase-A samples handed to k_tail_a
 };
 
 // Phase-A levels whose records may leave out the direction (PcParams::dbase): k_finish rebuilds them
@@ -116,12 +111,8 @@ __host__ __device__ inline unsigned unit_col(int tiles_x, int ublk_h, int ublk_w
 }
 
 // PcParams::totals words: packed task counts (0-2), the phase-A unit counter (3), k_fallback's chain /
-// shadow counts and shadow-queue overflow (4-6), phase B's tail entries (7), k_tail's entry counter (8),
-// k_mix's dynamic shadow-chunk counter (10), phase A's tail entries (11) and k_tail_a's entry counter (12);
-// the live-chain counts in 8 shards, one 128-B line each (kLiveShard0 + kLiveStride * i: a wave adds to shard
-// blk % 8): word 0 phase B's chains ended, 1 phase A's samples ended, 2 phase A's samples started.
-constexpr int kLiveShard0 = 32, kLiveStride = 32;
-constexpr int kTotalsWords = kLiveShard0 + 8 * kLiveStride;
+// shadow counts and shadow-queue overflow (4-6), the rest spare.
+constexpr int kTotalsWords = 12;
 
 // Unit cost classes (PcParams::ucost): the most phase-A walk steps a sample of the unit took.
 constexpr unsigned kHotSteps[2] = {96, 32};
@@ -198,10 +189,6 @@ struct PcParams {
                       // regions (workgroup w: regions w, w + G, ...); k_pack_a packs only the continuations
     int fin_grid;     // k_finish workgroups at most (0: a lane per output pixel), a grid-stride loop beyond
     int fin_cont;     // k_finish: the continued paths' pixels first (chain path: cflat, totals[1], kPathCont)
-    int fin_mode;     // k_finish split over two streams (lone frames with k_tail): 0 every pixel; 1 (beside k_tail,
-                      // right after k_mix) the pixels final then -- no sample continued (kPathCont) or with a phase-A
-                      // shadow ray in k_fallback's queue (kPathFb), none after a fallback-queue overflow; 2 (after
-                      // k_fallback) the others
     int refill;       // a wave refills once <= refill of its lanes are still walking
     int orefill;      // the same for the shadow (any-hit) walks
     int brefill;      // the same for phase-B chains
@@ -229,21 +216,6 @@ struct PcParams {
     // (new fields at the end: kernel arguments are loaded in runs of neighbours, so a field inserted
     // among the walk kernels' ones changed their SGPR spills 28 -> 67)
     unsigned* cont_peak;  // frames of several chunks: the most continuations of one chunk (k_pack_a, atomicMax)
-    // Phase B's tail (pathchain.hip k_tail): once at most tail_live of the launch's phase-B chains are left (0:
-    // never), a k_mix chain wave with no continuation left to take hands its chains on, each as the record id
-    // whose reflection is its next ray, into tailq (totals[7] entries, at most cb); k_tail walks each on a
-    // whole wave, tail_grid one-wave workgroups
-    unsigned* tailq;
-    int tail_live;
-    int tail_grid;
-    int tail_all;     // tests: every chain handed on at its first phase-B walk, exhausted or not
-    // phase A's stragglers (pathchain.hip k_tail_a, between k_chain and k_pack_a): once every unit is taken and at
-    // most tail_a started samples are still in phase A (0: never), a k_chain wave hands its samples on as
-    // {sample | level << 31, workgroup} (totals[11] of them, at most cap)
-    uint2* tailqA;
-    int tail_a;
-    int dchunk;       // k_mix (lone frames): A's shadow tasks dealt dynamically in chunks of this many (totals[10]),
-                      // the chain workgroups joining once their chains are done; 0: static dealing
 };
 
 // Worst-case task-queue slots per workgroup: every sample of the workgroup
@@ -272,7 +244,7 @@ hipError_t launch_walk_timing(const rtk::DevScene& s, const float* rays, int n, 
 // Diagnostics (RT_KTIME=1 scenes, rt_kernel_times): HIP events recorded between the kernels of a
 // chain launch on its stream, so the host can split the launch's time per kernel (one slot: the
 // kernels run back to back).
-enum KernelKind : int { kKChain = 0, kKPackA, kKMix, kKOccA, kKPackB, kKOccB, kKFinish, kKFallback, kKTail, kKEnd, kKKinds };
+enum KernelKind : int { kKChain = 0, kKPackA, kKMix, kKOccA, kKPackB, kKOccB, kKFinish, kKFallback, kKEnd, kKKinds };
 struct KTimer {
     static constexpr int kMax = 16;
     hipEvent_t ev[kMax] = {};
@@ -286,13 +258,7 @@ struct KTimer {
     }
 };
 
-// side/fork/join (lone frames with k_tail, PcParams::fin_mode): k_finish's part for the pixels final after k_mix
-// runs on `side` beside k_tail and the rest, joined back into `stream` before it returns (null: one k_finish).
-struct FinSplit {
-    hipStream_t side = nullptr;
-    hipEvent_t fork = nullptr, join = nullptr;
-};
 hipError_t launch_chain_chunk(const rtk::DevScene& s, const rtk::Eye& e, const PcParams& p, bool count,
-                              hipStream_t stream, KTimer* kt = nullptr, const FinSplit* fs = nullptr);
+                              hipStream_t stream, KTimer* kt = nullptr);
 
 }  // namespace rtc

@@ -136,14 +136,6 @@ struct rt_scene {
                                 // batches, and B's LDS-queue overflow in lone frames (0: packed)
     int tune_compact = 1;       // RT_COMPACT: phase-A records without directions (16 B instead of 32): 1 frame batches,
                                 // 2 every launch, 0 none
-    int tune_tail = 0;          // RT_TAIL: a lone frame's phase-B chains go to k_tail once at most this many are left (0: off)
-    int tune_tail_b = 0;        // RT_TAIL_B: the same in frame batches
-    int tune_tail_a = 0;        // RT_TAIL_A: a lone frame's phase-A samples go to k_tail_a once at most this many are left
-    int tune_tail_a_b = 0;      // RT_TAIL_A_B: the same in frame batches
-    int tune_tail_all = 0;      // RT_TAIL_ALL=1 (tests): every phase-B chain to k_tail at its first walk (where a tail is on)
-    int tune_fin_split = 1;     // RT_FIN_SPLIT: with a phase-B tail, k_finish's pixels final after k_mix on a side stream
-    int tune_dchunk = 0;        // RT_DCHUNK: a lone frame's A shadow tasks dealt dynamically in chunks of this many (0: static)
-    int tune_tail_grid = 0;     // RT_TAIL_GRID: k_tail's one-wave workgroups (0: 16 per CU)
     int tune_btail = 64;        // RT_BTAIL: the same once the continuations are exhausted (1: 1.24, 4: 1.18, 16: 1.15, 64: 1.14 ms)
     int tune_dyn = 1;           // RT_DYN_UNITS: phase-A waves take sample units from a launch-wide counter
     int tune_ublk_h = -1, tune_ublk_w = 8;  // RT_UBLK_H / RT_UBLK_W: phase-A unit column blocks (unit_order;
@@ -180,7 +172,6 @@ struct rt_scene {
     // on demand, carved per frame); slot 0 serves single renders, slots
     // [0, kSlots) the concurrent frames of rt_render_cameras*.
     static constexpr int kSlots = 6;
-    struct FinSide { hipStream_t st = nullptr; hipEvent_t fork = nullptr, join = nullptr; } fin_side[kSlots];
     // An arena may be used from any caller stream: `last` is recorded after each
     // use on `last_stream`, and a use from another stream first waits on it.
     struct Arena {
@@ -220,11 +211,6 @@ struct rt_scene {
         for (auto& e : kt.ev)
             if (e) (void)hipEventDestroy(e);
         for (auto& a : arenas) (void)hipFree(a.hist);
-        for (auto& f : fin_side) {
-            if (f.st) (void)hipStreamDestroy(f.st);
-            if (f.fork) (void)hipEventDestroy(f.fork);
-            if (f.join) (void)hipEventDestroy(f.join);
-        }
         for (auto& e : cont_ev)
             if (e) (void)hipEventDestroy(e);
         if (h_cont) (void)hipHostFree(h_cont);
@@ -454,14 +440,6 @@ int upload_rest(rt_scene* s, const rt_options* opts) {
     if (const char* e = std::getenv("RT_FGRID")) s->tune_fgrid = std::max(0, std::atoi(e));
     if (const char* e = std::getenv("RT_BQ_CAP")) s->tune_bq_cap = std::max(0, std::atoi(e));
     if (const char* e = std::getenv("RT_BSERVICE")) s->tune_bservice = std::max(1, std::min(64, std::atoi(e)));
-    if (const char* e = std::getenv("RT_TAIL")) s->tune_tail = std::max(0, std::atoi(e));
-    if (const char* e = std::getenv("RT_TAIL_B")) s->tune_tail_b = std::max(0, std::atoi(e));
-    if (const char* e = std::getenv("RT_TAIL_ALL")) s->tune_tail_all = std::atoi(e) != 0;
-    if (const char* e = std::getenv("RT_FIN_SPLIT")) s->tune_fin_split = std::atoi(e) != 0;
-    if (const char* e = std::getenv("RT_TAIL_A")) s->tune_tail_a = std::max(0, std::atoi(e));
-    if (const char* e = std::getenv("RT_TAIL_A_B")) s->tune_tail_a_b = std::max(0, std::atoi(e));
-    if (const char* e = std::getenv("RT_TAIL_GRID")) s->tune_tail_grid = std::max(1, std::atoi(e));
-    if (const char* e = std::getenv("RT_DCHUNK")) s->tune_dchunk = std::max(0, std::atoi(e));
     if (const char* e = std::getenv("RT_BTAIL")) s->tune_btail = std::max(1, std::min(64, std::atoi(e)));
     if (const char* e = std::getenv("RT_COMPACT")) s->tune_compact = std::max(0, std::min(2, std::atoi(e)));
     if (const char* e = std::getenv("RT_OCC_INPLACE")) s->tune_occ_inplace = std::atoi(e) != 0;
@@ -638,7 +616,7 @@ struct ChainPlan {
     size_t dbase = 0;               // records below it without directions (pathchain.hpp)
     int clevels = 0;
     size_t o_rec = 0, o_recd = 0, o_pinfo = 0, o_occ = 0, o_sqA = 0, o_scntA = 0, o_sflatA = 0, o_cq = 0, o_ccnt = 0,
-           o_cflat = 0, o_sqB = 0, o_scntB = 0, o_sflatB = 0, o_totals = 0, o_cid = 0, o_tailq = 0, o_tailqA = 0, o_tail = 0,
+           o_cflat = 0, o_sqB = 0, o_scntB = 0, o_sflatB = 0, o_totals = 0, o_cid = 0, o_tail = 0,
            o_fbc = 0, o_fbs = 0, bytes = 0;
 };
 
@@ -744,8 +722,6 @@ ChainPlan chain_plan(const rt_scene* s, const ChainGeom& g, size_t nunits, bool 
         P.o_cflat = L.take<unsigned>(cap);
         P.o_sqB = L.take<unsigned>((size_t)P.gb * P.scapB); P.o_scntB = L.take<unsigned>(P.gb + 1);
         P.o_sflatB = L.take<unsigned>(P.cb * (levels - P.la) * nl);
-        P.o_tailq = L.take<unsigned>(P.phase_b ? P.cb : 0);
-        P.o_tailqA = L.take<uint2>(cap);
     }
     P.o_totals = L.take<unsigned>(rtc::kTotalsWords);
     P.bytes = L.off;
@@ -932,35 +908,6 @@ int render_chain(rt_scene* s, const rtk::Eye& eye, const rtk::FrameParams& f, bo
     p.occ_inplace = RT_LEAF_QUEUE && !count && P.split_occ && s->tune_occ_inplace ? 1 : 0;
     p.occ_inplace_b = RT_LEAF_QUEUE && !P.split_occ && !count && s->tune_occ_inplace ? 1 : 0;
     p.cont_peak = peak ? s->d_cont_peak : nullptr;
-    // phase B's last chains on one wave each (k_tail): production launches only (the counting passes walk
-    // the reference tree with the reference's counters)
-    p.tailq = static_cast<unsigned*>(at(P.o_tailq));
-    p.tail_live = !count && P.phase_b ? (P.split_occ ? s->tune_tail_b : s->tune_tail) : 0;
-    p.tail_grid = s->tune_tail_grid > 0 ? s->tune_tail_grid : 16 * s->num_cus;
-    p.tail_all = s->tune_tail_all;
-    // k_finish in two parts on two streams where a phase-B tail follows k_mix (launch_chain_chunk): part 1, the
-    // pixels final after k_mix, beside k_tail, k_occlude and k_fallback; part 2 the rest
-    const bool fin_split = s->tune_fin_split && p.tail_live > 0 && P.phase_b && !P.split_occ && !count;
-    p.fin_mode = fin_split ? 2 : 0;
-    rtc::FinSplit fsp;
-    if (fin_split) {
-        auto& fsd = s->fin_side[slot];
-        if (!fsd.st) HIP_TRY(hipStreamCreateWithFlags(&fsd.st, hipStreamNonBlocking));
-        if (!fsd.fork) HIP_TRY(hipEventCreateWithFlags(&fsd.fork, hipEventDisableTiming));
-        if (!fsd.join) HIP_TRY(hipEventCreateWithFlags(&fsd.join, hipEventDisableTiming));
-        fsp.side = fsd.st;
-        fsp.fork = fsd.fork;
-        fsp.join = fsd.join;
-    }
-    p.tailqA = static_cast<uint2*>(at(P.o_tailqA));
-    p.tail_a = !count ? (P.split_occ ? s->tune_tail_a_b : s->tune_tail_a) : 0;
-    p.dchunk = !count && !P.split_occ && RT_LEAF_QUEUE ? s->tune_dchunk : 0;
-    if (p.dchunk > 0) {   // every task reachable: k_mix's workgroups take at most kDynUnits chunks each; and at
-                          // least a wave's grab (64), which then holds at most one chunk's first task
-        const size_t worst = cap * (size_t)P.levels_a * nl, wgs = (size_t)std::max(1, s->mix_grid);
-        p.dchunk = (int)std::max<size_t>({(size_t)p.dchunk, 64,
-                                          (worst + wgs * rtc::kDynUnits - 1) / (wgs * rtc::kDynUnits)});
-    }
     p.refill = s->tune_refill >= 0 ? s->tune_refill : 0;
     p.service = s->tune_service >= 0 ? s->tune_service : 64;
     p.bservice = s->tune_bservice;
@@ -989,7 +936,7 @@ int render_chain(rt_scene* s, const rtk::Eye& eye, const rtk::FrameParams& f, bo
         p.fouts[i] = i < p.nframes && p.nframes > 1 ? f.outs[i] : f.out;
     }
     p.trace_blocks = std::max(s->mix_grid, s->occl_grid);
-    const size_t trace_n = 2 * (cap + (size_t)p.trace_blocks) + 4 * cap + 4 * (size_t)p.trace_blocks;
+    const size_t trace_n = 2 * (cap + (size_t)p.trace_blocks) + 4 * cap;
     p.trace = trace_buffer(s, trace_n);
     // lone frames in one launch (a drop-in caller's repeated frames): phase-A units heaviest-first by the
     // previous frame of the same geometry (PcParams::uorder), and this frame's costs ranked for the next
@@ -1038,7 +985,7 @@ int render_chain(rt_scene* s, const rtk::Eye& eye, const rtk::FrameParams& f, bo
             for (int i = 0; i < rtc::KTimer::kMax; ++i)
                 if (!s->kt.ev[i]) HIP_TRY(hipEventCreate(&s->kt.ev[i]));
             s->kt.n = 0;
-            HIP_TRY(rtc::launch_chain_chunk(s->dev, eye, p, count, st, &s->kt, fin_split ? &fsp : nullptr));
+            HIP_TRY(rtc::launch_chain_chunk(s->dev, eye, p, count, st, &s->kt));
             HIP_TRY(hipEventSynchronize(s->kt.ev[s->kt.n - 1]));
             for (int i = 0; i + 1 < s->kt.n; ++i) {
                 float ms = 0;
@@ -1047,7 +994,7 @@ int render_chain(rt_scene* s, const rtk::Eye& eye, const rtk::FrameParams& f, bo
             }
             s->kt_launches++;
         } else {
-            HIP_TRY(rtc::launch_chain_chunk(s->dev, eye, p, count, st, nullptr, fin_split ? &fsp : nullptr));
+            HIP_TRY(rtc::launch_chain_chunk(s->dev, eye, p, count, st));
         }
     }
     // the share, read back later (a chunk of a forked frame: the parent call reads the frame's peak)
