@@ -145,7 +145,7 @@ int rt_device_count(int* count);
  * created afterwards (rt_scene_create / rt_scene_load_xml) hold a replica on
  * each of devices 0..n-1 and one RCCL communicator over them; rt_render and
  * rt_render_cameras then split every frame into stripe_rows-row stripes dealt
- * round-robin over the devices (env RT_GROUP_STRIPE, default 8), render them
+ * round-robin over the devices (env RT_GROUP_STRIPE, default 4), render them
  * concurrently (one HIP stream per device), gather the uint8 slabs to device 0
  * with ONE ncclGather over xGMI, un-interleave them there and copy the frame
  * to the caller's buffer -- designed to give the same bytes as one GPU; the

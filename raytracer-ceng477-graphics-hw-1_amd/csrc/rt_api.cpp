@@ -1389,11 +1389,18 @@ int render_cameras(rt_scene* s, const rt_camera* cams, int n, int aa, void* cons
             if (!s->slot_done[k]) HIP_TRY(hipEventCreateWithFlags(&s->slot_done[k], hipEventDisableTiming));
             HIP_TRY(hipStreamWaitEvent(s->slot_stream[k], s->fork_ev, 0));
         }
+        static const bool log_submit = std::getenv("RT_LOG_SUBMIT") != nullptr;   // diagnostics: host time per batch
+        auto now_us = [] { return std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now().time_since_epoch()).count(); };
+        const double ts0 = log_submit ? now_us() : 0.0;
         for (int b = 0; b < nb; ++b) {
             const int k = (b + slot0) % nslot, i = starts[b];
+            const double tb = log_submit ? now_us() : 0.0;
             const int rc = render_batch(s, cams + i, starts[b + 1] - i, aa, rows_of(i), rank, nranks, outs_dev + i,
                                         s->slot_stream[k], flags, k);
             if (rc) return rc;
+            if (log_submit)
+                std::fprintf(stderr, "{\"submit\": {\"batch\": %d, \"frames\": %d, \"slot\": %d, \"start_us\": %.1f, \"us\": %.1f}}\n",
+                             b, starts[b + 1] - i, k, tb - ts0, now_us() - tb);
         }
         for (int j = 0; j < used; ++j) {
             const int k = (j + slot0) % nslot;

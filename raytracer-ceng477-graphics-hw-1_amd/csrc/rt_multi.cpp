@@ -106,7 +106,7 @@ struct rt_group {
     uint8_t* image = nullptr;            // device 0: the assembled frames
     size_t image_cap = 0;
     hipEvent_t ev0 = nullptr, ev1 = nullptr;   // device 0: kernel time of a group call
-    int stripe_rows = 8;                 // RT_GROUP_STRIPE
+    int stripe_rows = 4;                 // RT_GROUP_STRIPE (4: 5.5x at N = 8 in the rehearsal, 8: 5.0x)
 
     int dev(int d) const { return virt ? 0 : d; }
 

@@ -51,7 +51,7 @@ def _counters(c):
     return (c["primary"], c["shadow"], c["reflection"], c["node_visits"], c["tri_tests"], c["sphere_tests"])
 
 
-@pytest.mark.parametrize("stripe", ["8", "3"])
+@pytest.mark.parametrize("stripe", ["4", "8", "3"])
 @pytest.mark.parametrize("name", ["C3_hm_1080p_d6_aa1", "C3_hm_1080p_d6_aa2", "cornellbox_aa1", "C1_simple_aa3"])
 def test_group_render_equals_golden(name, stripe, group, goldens, pkg, scene_dir, monkeypatch):
     monkeypatch.setenv("RT_GROUP_STRIPE", stripe)
@@ -98,7 +98,7 @@ def virtual_group(request, pkg, torch_cuda, monkeypatch):
     pkg.set_devices(0)
 
 
-@pytest.mark.parametrize("stripe,batch", [("8", None), ("5", None), ("8", "1")])
+@pytest.mark.parametrize("stripe,batch", [("4", None), ("8", None), ("5", None), ("4", "1")])
 def test_virtual_group_frames_equal_golden(virtual_group, stripe, batch, goldens, pkg, scene_dir, monkeypatch):
     """N > 1 group path on one GPU: single frames (rt_render) and frame batches (rt_render_cameras:
     every rank renders its stripes of a run of same-size cameras in flight together, one grouped
