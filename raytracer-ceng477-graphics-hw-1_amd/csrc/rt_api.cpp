@@ -123,7 +123,8 @@ struct rt_scene {
     // 159.6, 16 M 147.4, 32 M 140.6 ms/frame.  32 M samples = 15 GB of workspace per slot (C3).
     size_t chunk_samples = size_t(32) << 20;
     int tune_batch = 32;        // RT_BATCH: frames per batched launch (rt_render_frames/cameras; 1 = off)
-    bool tune_balance = true;   // RT_BALANCE: a call's frames dealt evenly over every slot (render_cameras)
+    bool tune_balance = false;  // RT_BALANCE=1: a call's frames dealt evenly over every slot (render_cameras; 20-frame
+                                // calls, 4 same-box runs each: 0.4316 ms/frame against 0.4221 for the greedy batches)
     int tune_slots = 3;         // RT_SLOTS: frame batches in flight together (workspace slots, <= kSlots;
                                 // default GPU_MAX_HW_QUEUES - 1)
     int tune_fgrid = 0;         // RT_FGRID: k_finish workgroups at most (0: 8 per CU; its waves are dispatch-bound
@@ -1331,11 +1332,12 @@ int render_cameras(rt_scene* s, const rt_camera* cams, int n, int aa, void* cons
             if (!s->slot_done[k]) HIP_TRY(hipEventCreateWithFlags(&s->slot_done[k], hipEventDisableTiming));
         }
         poll_cont(s, false);
-        // runs of consecutive same-size frames; a run of L frames goes out as nb batches of (nearly) equal
-        // size, nb = max(min(nslot, L), ceil(L / m)) where m is the most frames one launch's plan fits in the
-        // slot's workspace share (at most bmax): every slot busy when the run allows (concurrent batches
-        // overlap each other's tails), and no slot with more frames than another (a 20-frame call on 6
-        // slots: 4,4,3,3,3,3 rather than 4,4,4,4,4 on 5; RT_BALANCE=0: the greedy m-frame batches)
+        // runs of consecutive same-size frames; a run of L frames goes out as batches of min(m, ceil(L / nslot))
+        // frames, m the most frames one launch's plan fits in the slot's workspace share (at most bmax): a
+        // 20-frame call on 6 slots runs 4,4,4,4,4 on 5.  RT_BALANCE=1: nb = max(min(nslot, L), ceil(L / m))
+        // batches of (nearly) equal size, every slot busy (4,4,3,3,3,3) -- measured slower: the sixth
+        // concurrent batch's first kernel starts ~0.65 ms after the others (RT_LOG_SUBMIT, whatever the
+        // hardware-queue count), so its end sets the call's
         const bool balance = s->tune_balance;
         for (int i = 0; i < n;) {
             const auto& c = cams[i];
@@ -1389,18 +1391,42 @@ int render_cameras(rt_scene* s, const rt_camera* cams, int n, int aa, void* cons
             if (!s->slot_done[k]) HIP_TRY(hipEventCreateWithFlags(&s->slot_done[k], hipEventDisableTiming));
             HIP_TRY(hipStreamWaitEvent(s->slot_stream[k], s->fork_ev, 0));
         }
-        static const bool log_submit = std::getenv("RT_LOG_SUBMIT") != nullptr;   // diagnostics: host time per batch
+        // RT_LOG_SUBMIT=1 (diagnostics): per batch, the host's submission time and (HIP events on the slot
+        // streams, waited for at the end of the call: this makes the call synchronous) its GPU start and end
+        static const bool log_submit = std::getenv("RT_LOG_SUBMIT") != nullptr;
         auto now_us = [] { return std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now().time_since_epoch()).count(); };
         const double ts0 = log_submit ? now_us() : 0.0;
+        std::vector<hipEvent_t> bev;
+        std::vector<double> host_us;
         for (int b = 0; b < nb; ++b) {
             const int k = (b + slot0) % nslot, i = starts[b];
             const double tb = log_submit ? now_us() : 0.0;
+            if (log_submit) {
+                bev.resize(bev.size() + 2);
+                HIP_TRY(hipEventCreate(&bev[bev.size() - 2]));
+                HIP_TRY(hipEventCreate(&bev[bev.size() - 1]));
+                HIP_TRY(hipEventRecord(bev[bev.size() - 2], s->slot_stream[k]));
+            }
             const int rc = render_batch(s, cams + i, starts[b + 1] - i, aa, rows_of(i), rank, nranks, outs_dev + i,
                                         s->slot_stream[k], flags, k);
             if (rc) return rc;
-            if (log_submit)
-                std::fprintf(stderr, "{\"submit\": {\"batch\": %d, \"frames\": %d, \"slot\": %d, \"start_us\": %.1f, \"us\": %.1f}}\n",
-                             b, starts[b + 1] - i, k, tb - ts0, now_us() - tb);
+            if (log_submit) {
+                HIP_TRY(hipEventRecord(bev.back(), s->slot_stream[k]));
+                host_us.push_back(tb - ts0);
+                host_us.push_back(now_us() - tb);
+            }
+        }
+        if (log_submit) {
+            for (auto e : bev) HIP_TRY(hipEventSynchronize(e));
+            for (int b = 0; b < nb; ++b) {
+                float g0 = 0, g1 = 0;
+                HIP_TRY(hipEventElapsedTime(&g0, bev[0], bev[2 * b]));
+                HIP_TRY(hipEventElapsedTime(&g1, bev[0], bev[2 * b + 1]));
+                std::fprintf(stderr, "{\"submit\": {\"batch\": %d, \"frames\": %d, \"slot\": %d, \"host_start_us\": %.1f, "
+                             "\"host_us\": %.1f, \"gpu_start_ms\": %.4f, \"gpu_end_ms\": %.4f}}\n",
+                             b, starts[b + 1] - starts[b], (b + slot0) % nslot, host_us[2 * b], host_us[2 * b + 1], g0, g1);
+            }
+            for (auto e : bev) (void)hipEventDestroy(e);
         }
         for (int j = 0; j < used; ++j) {
             const int k = (j + slot0) % nslot;
