@@ -132,8 +132,9 @@ def golden_sha(config: str, aa: int) -> str | None:
     gfile = ROOT / "tests" / "golden" / "goldens.json"
     if not gfile.exists():
         return None
+    name = config[:-4] if config.endswith(".xml") else config       # (MS / MB: the reference scene files)
     for g in json.loads(gfile.read_text())["goldens"]:
-        if g["name"] == f"{config}_aa{aa}" and len(g["cameras"]) >= 1:
+        if g["name"] == f"{name}_aa{aa}" and len(g["cameras"]) >= 1:
             return g["cameras"][0].get("sha256_rgb")
     return None
 

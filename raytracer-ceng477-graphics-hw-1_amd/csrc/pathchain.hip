@@ -1802,12 +1802,14 @@ hipError_t launch_chain_chunk(const rtk::DevScene& s, const rtk::Eye& e, const P
     PcParams q = p;
     if (!phase_b) q.gb = 0;
     // p.split_occ (frame batches): k_mix only walks the chains, A's shadow tasks go to k_occlude (5 waves
-    // per SIMD); otherwise k_mix's other workgroups walk them beside the chains
-    const bool split = p.split_occ && phase_b;
+    // per SIMD; in place where p.occ_inplace, k_pack_a then leaving them unpacked); otherwise k_mix's other
+    // workgroups walk them beside the chains.  Frame batches without phase B (depth 0): no k_mix at all
+    const bool split = p.split_occ != 0;
     const int mgrid = split ? q.gb : q.gb + p.ogrid;
     mark(kKMix);
     // frame batches (split): phase B's shadow tasks all through k_pack_b + k_occlude (no LDS queue)
-    if (count) {
+    if (mgrid == 0) {
+    } else if (count) {
         if (split) hipLaunchKernelGGL((k_mix<true, false>), dim3(mgrid), blk, 0, st, s, e, q);
         else hipLaunchKernelGGL((k_mix<true, true>), dim3(mgrid), blk, 0, st, s, e, q);
     } else {

@@ -304,6 +304,33 @@ def test_render_frames_device_batch(nranks, nframes, gname, path, batch, goldens
         assert _stats(cnt) == tuple(nframes * x for x in _counters(c))
 
 
+@pytest.mark.parametrize("gname", ["C1_simple_aa1", "C1_simple_aa3", "C2_cornellbox_800_d0_aa1",
+                                   "C2_cornellbox_800_d0_aa2", "hm_verbatim_aa1", "C3_hm_1080p_d6_aa1",
+                                   "C3_hm_1080p_d6_aa2", "cornellbox_aa1", "simple_reflectance_aa1",
+                                   "mirror_spheres_aa1", "marbles_aa1"])
+def test_render_frames_device_production(gname, goldens, pkg, scene_dir, torch_cuda):
+    """The bench's own call at N = 1 with the production (timed) kernels: one rank, 4-row stripes, a
+    batch of 7 frames of camera 0 (frame-batch launches: compact records, A's shadow rays through
+    k_occlude where phase B exists, and without it -- depth 0, C2 -- too); every frame equals the
+    golden.  (test_render_frames_device_batch checks the counting kernels' batches.)"""
+    torch = torch_cuda
+    g = golden_by_name(goldens, gname)
+    ref = torch.from_numpy(load_golden_image(g["cameras"][0]).copy()).to("cuda:0")
+    aa, stripe, nframes = g["aa"], 4, 7
+    with pkg.Scene.from_xml(config_path(scene_dir, g["config"]), device=0) as s:
+        cam = s.camera(g["cameras"][0]["camera"])
+        W, H = cam.image_width, cam.image_height
+        slabs = torch.zeros((nframes, H, W, 3), dtype=torch.uint8, device="cuda:0")
+        stream = torch.cuda.current_stream().cuda_stream
+        for rep in range(2):                     # the second call sized by the first's read-backs
+            slabs.zero_()
+            s.render_frames_device([cam] * nframes, aa, [slabs[f].data_ptr() for f in range(nframes)], stream,
+                                   stripe_rows=stripe, rank=0, nranks=1)
+            torch.cuda.synchronize()
+            for f in range(nframes):
+                assert torch.equal(slabs[f], ref), f"{gname} call {rep} frame {f}"
+
+
 @pytest.mark.parametrize("slots", ["3", "4", "6"])
 def test_render_frames_device_many_batches(slots, goldens, pkg, scene_dir, torch_cuda, monkeypatch):
     """70 frames of 8-rank shards: more frames than kMaxFrames (32) per batch and more batches than
