@@ -246,7 +246,7 @@ int upload_scene(rt_scene* s, const rt_options* opts);
 // and builds the trees on the host, and is joined before the upload (a drop-in caller's first frame no
 // longer pays both in sequence).  RT_NO_WARMUP=1 disables it (A/B).
 std::mutex g_warm_mu;
-std::future<void> g_warm;
+std::future<void> g_warm, g_warm2;
 bool g_warm_started = false;
 
 // Only for an explicit device (opts->device >= 0) or a device group (whose primary is device 0): -1
@@ -271,10 +271,36 @@ void start_device_warmup(const rt_options* opts) {
         (void)hipSetDevice(want);
         (void)hipFree(nullptr);
         const double t2 = log ? now() : 0.0;
-        int a = 0, b = 0, c = 0;
-        (void)rtc::chain_occupancy(&a, &b, &c);     // loads the kernels' code objects
+        // what only the first render needs goes on a second thread, joined once the scene is uploaded
+        // (join_device_warmup_full): the kernels' code objects, and a pageable read-back (a drop-in frame's
+        // first copy back otherwise paid ~9 ms of staging set-up, tools/exp_cli.py --phases)
+        g_warm2 = std::async(std::launch::async, [want, log, now] {
+            (void)hipSetDevice(want);
+            int a = 0, b = 0, c = 0;
+            (void)rtc::chain_occupancy(&a, &b, &c);
+            const double t3 = log ? now() : 0.0;
+            size_t wb = 1u << 20;
+            if (const char* e = std::getenv("RT_WARM_BYTES")) wb = (size_t)std::max(256L, std::atol(e));
+            void* d = nullptr;
+            std::vector<unsigned char> h(wb);
+            if (hipMalloc(&d, wb) == hipSuccess) {
+                (void)hipMemset(d, 0, wb);
+                (void)hipMemcpy(h.data(), d, wb, hipMemcpyDeviceToHost);
+                (void)hipFree(d);
+            }
+            if (log) std::fprintf(stderr, "{\"rt_init2\": {\"code_objects\": %.3f, \"readback\": %.3f}}\n", t3, now());
+        });
+        // the scene upload's needs: the process's first allocation, copy and fill (~20 ms on the box)
+        void* d = nullptr;
+        unsigned char h[256] = {};
+        if (hipMalloc(&d, 4096) == hipSuccess) {
+            (void)hipMemcpy(d, h, sizeof h, hipMemcpyHostToDevice);
+            (void)hipMemset(d, 0, 4096);
+            (void)hipStreamSynchronize(nullptr);
+            (void)hipFree(d);
+        }
         if (log)
-            std::fprintf(stderr, "{\"rt_init\": {\"start\": %.3f, \"device_count\": %.3f, \"context\": %.3f, \"code_objects\": %.3f}}\n",
+            std::fprintf(stderr, "{\"rt_init\": {\"start\": %.3f, \"device_count\": %.3f, \"context\": %.3f, \"first_op\": %.3f}}\n",
                          t0, t1, t2, now());
     });
 }
@@ -282,6 +308,11 @@ void start_device_warmup(const rt_options* opts) {
 void join_device_warmup() {
     std::lock_guard<std::mutex> lk(g_warm_mu);
     if (g_warm.valid()) g_warm.get();
+}
+void join_device_warmup_full() {
+    join_device_warmup();
+    std::lock_guard<std::mutex> lk(g_warm_mu);
+    if (g_warm2.valid()) g_warm2.get();
 }
 
 double ms_since(std::chrono::steady_clock::time_point t) {
@@ -326,6 +357,7 @@ int finish_scene(rt_scene* s, const rt_options* opts) {
         HIP_TRY(hipSetDevice(s->device));    // (the early upload set it on its own thread)
     }
     rc = upload_rest(s, &o);
+    join_device_warmup_full();
     if (!rc && ndev >= 1) rc = rt_internal_group_create(s, ndev, &s->group);
     s->upload_ms = ms_since(t);              // (the part after the build: the early upload overlaps it)
     return rc;
@@ -852,7 +884,9 @@ int render_chain(rt_scene* s, const rtk::Eye& eye, const rtk::FrameParams& f, bo
     // order this use after the arena's previous one (possibly on another stream)
     if (arena.last && arena.last_stream != st) HIP_TRY(hipStreamWaitEvent(st, arena.last, 0));
     if (arena.bytes < P.bytes) {
-        if (std::getenv("RT_LOG_ALLOC"))            // diagnostics: a growth inside a timed region serialises it
+        const bool log_alloc = std::getenv("RT_LOG_ALLOC") != nullptr;   // diagnostics: a growth inside a timed
+        const auto ta = std::chrono::steady_clock::now();                // region serialises it
+        if (log_alloc)
             std::fprintf(stderr, "librt_hip: slot %d workspace %.1f -> %.1f MB (frames %d, cb %zu of %zu)\n", slot,
                          arena.bytes / 1e6, P.bytes / 1e6, g.nframes, P.cb, P.cap);
         if (arena.p) HIP_TRY(hipStreamSynchronize(st));   // the previous frames on it may still use it
@@ -865,6 +899,7 @@ int render_chain(rt_scene* s, const rtk::Eye& eye, const rtk::FrameParams& f, bo
         const size_t want = std::min(P.bytes + P.bytes / 16, std::max(P.bytes, s->slot_budget()));
         HIP_TRY(hipMalloc(reinterpret_cast<void**>(&arena.p), want));
         arena.bytes = want;
+        if (log_alloc) std::fprintf(stderr, "librt_hip: slot %d workspace growth took %.2f ms\n", slot, ms_since(ta));
     }
     auto at = [&](size_t o) { return static_cast<void*>(arena.p + o); };
     rtc::PcParams p{};
@@ -1546,14 +1581,22 @@ int rt_render_cameras(rt_scene* s, const rt_camera* cams, int n, int aa, uint8_t
     for (int i = 0; i < n; ++i) dev[i] = s->batch_out + off[i];
     const bool count = stats != nullptr;
     if (count) HIP_TRY(hipMemset(s->d_counters, 0, rtc::kCounters * sizeof(unsigned long long)));
+    static const bool log = std::getenv("RT_LOG_INIT") != nullptr;   // diagnostics (tools/exp_cli.py --phases)
+    const double t_out = log ? ms_since(t0) : 0.0;
     int rc = render_cameras(s, cams, n, aa, dev.data(), nullptr, count ? RT_RENDER_COUNT : 0, 0, 0, 1, true);
+    const double t_sub = log ? ms_since(t0) : 0.0;
+    double t_gpu = 0.0;
     if (rc == RT_OK) {
         HIP_TRY(hipDeviceSynchronize());
+        if (log) t_gpu = ms_since(t0);
         for (int i = 0; i < n; ++i)
             HIP_TRY(hipMemcpy(outs[i], dev[i], (size_t)cams[i].image_width * cams[i].image_height * 3,
                               hipMemcpyDeviceToHost));
     }
     HIP_TRY(hipDeviceSynchronize());
+    if (log)
+        std::fprintf(stderr, "{\"rt_render_cameras\": {\"outputs_ms\": %.3f, \"submitted_ms\": %.3f, \"gpu_done_ms\": %.3f, "
+                     "\"copied_ms\": %.3f}}\n", t_out, t_sub, t_gpu, ms_since(t0));
     if (rc) return rc;
     if ((rc = check_device_error(s))) return rc;
     if (stats) {

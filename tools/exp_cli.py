@@ -64,7 +64,7 @@ def phases(hm, reps, extra_env=None, aa=1):
         for l in r.stderr.splitlines():
             if l.startswith("{"):
                 ev.update(json.loads(l))
-        c, i = ev["cli"], ev.get("rt_init", {})
+        c, i, i2 = ev["cli"], ev.get("rt_init", {}), ev.get("rt_init2", {})
         row = {"wall": t_end - t_spawn, "spawn_to_main": c["main"] - t_spawn,
                "load": c["loaded"] - c["main"], "render_d2h": c["rendered"] - c["loaded"],
                "write_ppm": c["written"] - c["rendered"], "after_write_to_exit": t_end - c["written"],
@@ -72,8 +72,15 @@ def phases(hm, reps, extra_env=None, aa=1):
                "stree": c["stree_ms"], "upload_after_build": c["upload_ms"]}
         if i:
             row.update({"init_start_after_main": i["start"] - c["main"], "hip_device_count": i["device_count"] - i["start"],
-                        "hip_context": i["context"] - i["device_count"], "code_objects": i["code_objects"] - i["context"],
-                        "init_end_after_main": i["code_objects"] - c["main"]})
+                        "hip_context": i["context"] - i["device_count"], "first_device_op": i["first_op"] - i["context"],
+                        "init_end_after_main": i["first_op"] - c["main"]})
+            if i2:     # the second warm-up thread (joined after the upload)
+                row.update({"code_objects": i2["code_objects"] - i["context"], "readback_warm": i2["readback"] - i2["code_objects"],
+                            "init2_end_after_main": i2["readback"] - c["main"]})
+        rc = ev.get("rt_render_cameras")
+        if rc:     # inside render_d2h: output buffers, submission, GPU done, D2H copies (ms from the call's start)
+            row.update({"rc_outputs": rc["outputs_ms"], "rc_submit": rc["submitted_ms"] - rc["outputs_ms"],
+                        "rc_gpu_wait": rc["gpu_done_ms"] - rc["submitted_ms"], "rc_d2h": rc["copied_ms"] - rc["gpu_done_ms"]})
         rows.append(row)
     keys = rows[0].keys()
     return {k: round(sorted(r[k] for r in rows)[len(rows) // 2], 2) for k in keys}
@@ -90,8 +97,11 @@ def main():
     if a.phases:
         hm = pkg.scenes.write_config("hm_verbatim", d)
         for aa in (1, 2):
-            for name, env in (("default", None), ("normal_exit", {"RT_CLI_EXIT": "normal"}),
-                              ("no_warmup", {"RT_NO_WARMUP": "1"})):
+            variants = [("default", None), ("normal_exit", {"RT_CLI_EXIT": "normal"}), ("no_warmup", {"RT_NO_WARMUP": "1"})]
+            if os.environ.get("EXP_CLI_VARIANTS"):    # "name:K=V,K2=W;name2:..." instead of the three above
+                variants = [(v.split(":")[0], dict(kv.split("=", 1) for kv in v.split(":", 1)[1].split(",") if kv))
+                            for v in os.environ["EXP_CLI_VARIANTS"].split(";")]
+            for name, env in variants:
                 print(json.dumps({"scene": "horse_and_mug.xml", "aa": aa, "variant": name,
                                   "median_ms": phases(hm, a.reps, env, aa)}), flush=True)
         return
