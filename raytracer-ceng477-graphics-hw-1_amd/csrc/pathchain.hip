@@ -619,7 +619,7 @@ __device__ void chain_body(const rtk::DevScene& s, const rtk::Eye& e, const PcPa
             }
             if (ends || handoff) {
                 st = kIdle;
-                if (!CONT && !COUNT && p.urank && ssteps >= kHotSteps[1]) atomicMax(&p.ucost[path >> 8], ssteps);
+                if (!CONT && !COUNT && p.urank && ssteps >= kHotSteps[kUnitClasses - 2]) atomicMax(&p.ucost[path >> 8], ssteps);
                 if (kTraceBuild && p.trace && !CONT) { p.trace[2 * path] = t_grab; p.trace[2 * path + 1] = (unsigned)wall_clock64(); }
                 if (kTraceBuild && p.trace && CONT) {       // phase B: {grab, end, last level, walk steps} after A's entries
                     unsigned* tb = p.trace + 2 * ((size_t)p.cap + p.trace_blocks) + 4 * (size_t)path;
@@ -1114,34 +1114,45 @@ __device__ void pack_region(const unsigned* q, unsigned cap, const unsigned* cnt
 
 // After phase A: pack its shadow tasks and continuations (one workgroup per region).
 // The next frame's phase-A unit order (PcParams::uorder, k_mix's last shadow-role workgroup in lone frames):
-// the units by cost class (kHotSteps), each class in
-// the column order (the table ucol, made on the host); ucost cleared for the next frame's marks.  One
-// workgroup: thread t takes a contiguous run of the column order; the per-class offsets come from one block-wide exclusive scan of the three
-// counts packed into a 64-bit word (21 bits each: at most 2^21 units).
-__device__ __forceinline__ int unit_class(unsigned c) { return c >= kHotSteps[0] ? 0 : c >= kHotSteps[1] ? 1 : 2; }
+// the units by cost class (kHotSteps, the heaviest class first; seven classes: 9 us less per repeated C3
+// frame than three, profiles/r05_ab_rank.txt), each class in the column order (the table ucol, made on the
+// host); ucost cleared for the next frame's marks.  One workgroup: thread t takes a contiguous run of the
+// column order; the per-class offsets come from block-wide exclusive scans of the runs' class counts.
+__device__ __forceinline__ int unit_class(unsigned c) {
+#pragma unroll
+    for (int i = 0; i < kUnitClasses - 1; ++i)
+        if (c >= kHotSteps[i]) return i;
+    return kUnitClasses - 1;
+}
 __device__ void rank_units(const PcParams& p) {
-    __shared__ unsigned long long s_wave[kBlock / 64];
+    __shared__ unsigned s_wave[kBlock / 64][kUnitClasses];
     const unsigned units = ((unsigned)p.n0 + 255u) / 256u;
     const unsigned per = (units + kBlock - 1) / kBlock, j0 = min(units, threadIdx.x * per), j1 = min(units, j0 + per);
-    unsigned long long mine = 0;               // class counts of this thread's run, 21 bits each
-    for (unsigned j = j0; j < j1; ++j) mine += 1ull << (21 * unit_class(p.ucost[p.ucol[j]]));
-    unsigned long long inc = mine;             // inclusive scan in the wave, then over the waves
+    unsigned mine[kUnitClasses] = {};          // class counts of this thread's run
+    for (unsigned j = j0; j < j1; ++j) ++mine[unit_class(p.ucost[p.ucol[j]])];
     const int lane = lane_id(), wave = (int)(threadIdx.x >> 6);
-    for (int off = 1; off < 64; off <<= 1) {
-        const unsigned long long v = __shfl_up(inc, off, 64);
-        if (lane >= off) inc += v;
+    unsigned inc[kUnitClasses];                // inclusive scans in the wave, then over the waves
+#pragma unroll
+    for (int c = 0; c < kUnitClasses; ++c) {
+        inc[c] = mine[c];
+        for (int off = 1; off < 64; off <<= 1) {
+            const unsigned v = __shfl_up(inc[c], off, 64);
+            if (lane >= off) inc[c] += v;
+        }
+        if (lane == 63) s_wave[wave][c] = inc[c];
     }
-    if (lane == 63) s_wave[wave] = inc;
     __syncthreads();
-    unsigned long long before = 0, total = 0;
-    for (int w = 0; w < kBlock / 64; ++w) {
-        if (w < wave) before += s_wave[w];
-        total += s_wave[w];
+    unsigned at[kUnitClasses], base = 0;
+#pragma unroll
+    for (int c = 0; c < kUnitClasses; ++c) {
+        unsigned before = 0, total = 0;
+        for (int w = 0; w < kBlock / 64; ++w) {
+            if (w < wave) before += s_wave[w][c];
+            total += s_wave[w][c];
+        }
+        at[c] = base + before + inc[c] - mine[c];
+        base += total;
     }
-    const unsigned long long ex = before + inc - mine;
-    const unsigned m = (1u << 21) - 1u;
-    const unsigned t0 = (unsigned)total & m, t1 = (unsigned)(total >> 21) & m;
-    unsigned at[3] = {(unsigned)ex & m, t0 + ((unsigned)(ex >> 21) & m), t0 + t1 + ((unsigned)(ex >> 42) & m)};
     for (unsigned j = j0; j < j1; ++j) {
         const unsigned u = p.ucol[j];
         p.uorder[at[unit_class(p.ucost[u])]++] = u;

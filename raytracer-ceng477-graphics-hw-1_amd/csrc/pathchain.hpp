@@ -115,7 +115,10 @@ __host__ __device__ inline unsigned unit_col(int tiles_x, int ublk_h, int ublk_w
 constexpr int kTotalsWords = 12;
 
 // Unit cost classes (PcParams::ucost): the most phase-A walk steps a sample of the unit took.
-constexpr unsigned kHotSteps[2] = {96, 32};
+// Classes 0..5: at least kHotSteps[c] steps; class kUnitClasses - 1: the rest (and units no sample of which
+// reached kHotSteps[5], which k_chain does not mark).
+constexpr int kUnitClasses = 7;
+constexpr unsigned kHotSteps[kUnitClasses - 1] = {224, 160, 128, 96, 64, 32};
 
 struct PcParams {
     int width, height, aa, stripe_rows, rank, nranks, slab_rows;
@@ -175,8 +178,8 @@ struct PcParams {
     int occ_grid;     // resident k_occlude workgroups
     // Lone frames' phase-A units, the previous frame's heaviest first (rt_api.cpp render_chain,
     // hot_units): k_chain records per unit the most walk steps a sample of it took (ucost: samples of at
-    // least kHotSteps[1] only, atomicMax), k_pack_a ranks the units into uorder by that cost's class
-    // (>= kHotSteps[0], >= kHotSteps[1], the rest; each class in the column order) and clears ucost; the
+    // least kHotSteps[5] only, atomicMax), k_mix's last shadow-role workgroup ranks the units into uorder by
+    // that cost's class (kHotSteps, heaviest first; each class in the column order) and clears ucost; the
     // next frame of the same geometry deals its units in that order (uorder_on).  Where the work goes,
     // never what it computes.
     unsigned* ucost;
