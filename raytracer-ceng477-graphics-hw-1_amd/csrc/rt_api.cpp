@@ -129,7 +129,8 @@ struct rt_scene {
                                 // default GPU_MAX_HW_QUEUES - 1)
     int tune_fgrid = 0;         // RT_FGRID: k_finish workgroups at most (0: 8 per CU; its waves are dispatch-bound
                                 // at a lane per pixel: 0.515 -> 0.49 ms per batched frame)
-    int tune_gb = 0;            // RT_GB: phase-B chain workgroups in k_mix (0: 1.875 per CU for a lone frame, 1 for batches)
+    int tune_gb = 0;            // RT_GB: phase-B chain workgroups in k_mix (0: 1.875 per CU for a lone frame, 1.5 for batches)
+    int tune_gb_b = 0;          // RT_GB_B: the same for frame batches only (0: 1.5 per CU)
     int tune_bq_cap = 1 << 30;  // RT_BQ_CAP: phase-B shadow queue slots (tests force the k_occlude spill path)
     int tune_bservice = 64;     // RT_BSERVICE: phase-B waves service finished walks once this many lanes are done
     int tune_hot_units = 1;     // RT_HOT_UNITS: lone frames deal phase-A units heaviest-first by the previous frame's steps
@@ -470,6 +471,7 @@ int upload_rest(rt_scene* s, const rt_options* opts) {
         s->chunk_samples = std::max<size_t>(4096, std::min<size_t>(size_t(1) << 26, std::strtoull(e, nullptr, 10)));
     if (const char* e = std::getenv("RT_KINLINE")) s->tune_kinline = std::max(0, std::atoi(e));
     if (const char* e = std::getenv("RT_GB")) s->tune_gb = std::max(0, std::atoi(e));
+    if (const char* e = std::getenv("RT_GB_B")) s->tune_gb_b = std::max(0, std::atoi(e));
     if (const char* e = std::getenv("RT_FGRID")) s->tune_fgrid = std::max(0, std::atoi(e));
     if (const char* e = std::getenv("RT_BQ_CAP")) s->tune_bq_cap = std::max(0, std::atoi(e));
     if (const char* e = std::getenv("RT_BSERVICE")) s->tune_bservice = std::max(1, std::min(64, std::atoi(e)));
@@ -706,7 +708,10 @@ ChainPlan chain_plan(const rt_scene* s, const ChainGeom& g, size_t nunits, bool 
     // frame batches: A's shadow rays in their own 5-wave k_occlude launch (split_occ) and 1 phase-B
     // workgroup per CU (6 slots in flight: 0.504-0.512 -> 0.495 ms/frame; 0.5 per CU 0.500, 2 0.4995)
     P.split_occ = g.nframes > 1 && (!std::getenv("RT_SPLIT_OCC") || std::atoi(std::getenv("RT_SPLIT_OCC")));
-    const int gb_default = g.nframes > 1 ? (P.split_occ ? s->num_cus : s->num_cus / 2) : 30 * s->num_cus / 16;
+    // (round 5, the driver's 20-frame call on 5 slots: 1.5 per CU 0.4175 against 1 per CU 0.4282 ms/frame, three
+    // interleaved same-box rounds, 96-frame calls +-0; profiles/r05_ab_gb.txt)
+    const int gb_default = g.nframes > 1 ? (s->tune_gb_b > 0 ? s->tune_gb_b : P.split_occ ? 3 * s->num_cus / 2 : s->num_cus / 2)
+                                         : 30 * s->num_cus / 16;
     P.gb = P.phase_b ? std::max(1, std::min(s->mix_grid - 1, s->tune_gb > 0 ? s->tune_gb : gb_default)) : 0;
     P.levels_a = std::min(P.kinline, std::max(s->dev.max_depth, 0)) + 1;
     // dynamic phase-A units: a workgroup may take up to twice its static share (at most
