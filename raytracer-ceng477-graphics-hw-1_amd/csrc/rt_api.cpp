@@ -705,7 +705,7 @@ ChainPlan chain_plan(const rt_scene* s, const ChainGeom& g, size_t nunits, bool 
     // 2.03 0.956 ms);
     // in frame batches other frames hide them and the shadow role wants the CUs (C3: 0.5 per CU
     // 0.550 ms/frame, 0.75 0.552, 1 0.554, 1.25 0.557, 1.5625 0.568)
-    // frame batches: A's shadow rays in their own 5-wave k_occlude launch (split_occ) and 1 phase-B
+    // frame batches: A's shadow rays in their own 5-wave k_occlude launch (split_occ) and (round 3) 1 phase-B
     // workgroup per CU (6 slots in flight: 0.504-0.512 -> 0.495 ms/frame; 0.5 per CU 0.500, 2 0.4995)
     P.split_occ = g.nframes > 1 && (!std::getenv("RT_SPLIT_OCC") || std::atoi(std::getenv("RT_SPLIT_OCC")));
     // (round 5, the driver's 20-frame call on 5 slots: 1.5 per CU 0.4175 against 1 per CU 0.4282 ms/frame, three
