@@ -116,7 +116,8 @@ struct rt_scene {
     // gain from chunks only when other frames hide the tail: 128 gives batches 0.685 -> 0.650 ms/frame
     // but a lone frame 1.15 -> 1.36 ms, so a lone frame keeps fine interleaving.
     int tune_tchunk = 0;        // RT_TCHUNK (0: 128 for frame batches, 1 for one frame)
-    int tune_ochunk = 256;      // RT_OCHUNK
+    int tune_ochunk = 0;        // RT_OCHUNK (0: 256 in frame batches, 128 in lone frames -- 41-frame medians
+                                // 0.8776 against 0.8826 ms, three interleaved rounds, profiles/r05_lone_knobs.txt)
     int tune_kinline = 1;       // RT_KINLINE: deepest level of phase A
     // RT_CHUNK_SAMPLES: samples per chain-path launch (chunk / frame batch).  Bigger launches leave
     // fewer tails per sample: C3 batches 4 M 0.72, 8 M 0.66, 16 M 0.63, 32 M 0.59 ms/frame; C5 8 M
@@ -452,7 +453,7 @@ int upload_rest(rt_scene* s, const rt_options* opts) {
     if (const char* e = std::getenv("RT_REFILL")) s->tune_refill = std::max(0, std::min(63, std::atoi(e)));
     if (const char* e = std::getenv("RT_SERVICE")) s->tune_service = std::max(1, std::min(64, std::atoi(e)));
     if (const char* e = std::getenv("RT_TCHUNK")) s->tune_tchunk = std::max(1, std::min(4096, std::atoi(e)));
-    if (const char* e = std::getenv("RT_OCHUNK")) s->tune_ochunk = std::max(1, std::min(4096, std::atoi(e)));
+    if (const char* e = std::getenv("RT_OCHUNK")) s->tune_ochunk = std::max(0, std::min(4096, std::atoi(e)));
     if (const char* e = std::getenv("RT_BPRIO")) s->tune_bprio = std::atoi(e) != 0;
     if (const char* e = std::getenv("RT_BREFILL")) s->tune_brefill = std::max(0, std::min(63, std::atoi(e)));
     if (const char* e = std::getenv("RT_OREFILL")) s->tune_orefill = std::max(0, std::min(63, std::atoi(e)));
@@ -960,7 +961,7 @@ int render_chain(rt_scene* s, const rtk::Eye& eye, const rtk::FrameParams& f, bo
     // continuations dealt one at a time round-robin for a lone frame (its deep chains spread over
     // the phase-B workgroups: 1.12 -> 1.10 ms; 2: 1.11-1.14, 4: 1.12-1.13), in chunks of 128 in batches
     p.tchunk = P.tchunk;
-    p.ochunk = s->tune_ochunk;
+    p.ochunk = s->tune_ochunk > 0 ? s->tune_ochunk : P.split_occ ? 256 : 128;
     p.lq_wait = std::getenv("RT_LQ_WAIT") ? std::max(1, std::min(64, std::atoi(std::getenv("RT_LQ_WAIT")))) : 32;
     p.dyn_units = (int)P.dyn_units;
     p.ublk_h = s->tune_ublk_h;
