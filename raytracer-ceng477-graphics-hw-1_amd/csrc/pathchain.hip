@@ -1129,7 +1129,11 @@ __device__ void rank_units(const PcParams& p) {
     const unsigned units = ((unsigned)p.n0 + 255u) / 256u;
     const unsigned per = (units + kBlock - 1) / kBlock, j0 = min(units, threadIdx.x * per), j1 = min(units, j0 + per);
     unsigned mine[kUnitClasses] = {};          // class counts of this thread's run
-    for (unsigned j = j0; j < j1; ++j) ++mine[unit_class(p.ucost[p.ucol[j]])];
+    for (unsigned j = j0; j < j1; ++j) {
+        const int cls = unit_class(p.ucost[p.ucol[j]]);
+#pragma unroll
+        for (int c = 0; c < kUnitClasses; ++c) mine[c] += c == cls ? 1u : 0u;
+    }
     const int lane = lane_id(), wave = (int)(threadIdx.x >> 6);
     unsigned inc[kUnitClasses];                // inclusive scans in the wave, then over the waves
 #pragma unroll
@@ -1155,7 +1159,12 @@ __device__ void rank_units(const PcParams& p) {
     }
     for (unsigned j = j0; j < j1; ++j) {
         const unsigned u = p.ucol[j];
-        p.uorder[at[unit_class(p.ucost[u])]++] = u;
+        const int cls = unit_class(p.ucost[u]);
+        unsigned pos = 0;
+#pragma unroll
+        for (int c = 0; c < kUnitClasses; ++c)     // (no dynamic index into at[]: it would live in scratch)
+            if (c == cls) pos = at[c]++;
+        p.uorder[pos] = u;
         p.ucost[u] = 0;
     }
 }
