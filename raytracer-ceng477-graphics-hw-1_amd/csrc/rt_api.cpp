@@ -137,8 +137,9 @@ struct rt_scene {
     int tune_hot_units = 1;     // RT_HOT_UNITS: lone frames deal phase-A units heaviest-first by the previous frame's steps
     int tune_occ_inplace = 1;   // RT_OCC_INPLACE: A's shadow tasks read in their regions by k_occlude in frame
                                 // batches, and B's LDS-queue overflow in lone frames (0: packed)
-    int tune_compact = 1;       // RT_COMPACT: phase-A records without directions (16 B instead of 32): 1 frame batches,
-                                // 2 every launch, 0 none
+    int tune_compact = 0;       // RT_COMPACT: phase-A records without directions (16 B instead of 32): 1 frame batches,
+                                // 2 every launch, 0 none (round 5: 0 -- 20-frame calls 0.4151 -> 0.4040 ms/frame, 96-frame
+                                // calls -0.4 %, for 0.06 GB more HBM traffic per frame; profiles/r05_ab_compact.txt)
     int tune_btail = 64;        // RT_BTAIL: the same once the continuations are exhausted (1: 1.24, 4: 1.18, 16: 1.15, 64: 1.14 ms)
     int tune_dyn = 1;           // RT_DYN_UNITS: phase-A waves take sample units from a launch-wide counter
     int tune_ublk_h = -1, tune_ublk_w = 8;  // RT_UBLK_H / RT_UBLK_W: phase-A unit column blocks (unit_order;
@@ -741,8 +742,8 @@ ChainPlan chain_plan(const rt_scene* s, const ChainGeom& g, size_t nunits, bool 
     const size_t nrec = cap * P.la + P.cb * (levels - P.la);
     ArenaLayout L;
     // phase A's records without their directions where k_finish can rebuild them (pathchain.hpp dbase)
-    // (frame batches by default: a lone frame's k_finish is on its critical path and the rebuilt
-    // directions cost it more than the saved bytes; RT_COMPACT=2 everywhere, 0 nowhere)
+    // (RT_COMPACT=1 frame batches, 2 everywhere; off by default since round 5: the rebuilt directions cost
+    // k_finish more than the saved bytes gain k_chain and k_occlude)
     const bool cmp = s->tune_compact == 2 || (s->tune_compact == 1 && g.nframes > 1);
     P.clevels = cmp ? std::min(P.la, rtc::kCompactLevels) : 0;
     P.dbase = cap * (size_t)P.clevels;
