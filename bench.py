@@ -60,26 +60,25 @@ HBM_SPEC_GBPS = 8000.0     # MI355X spec (MI355X_MICROARCH.md §HBM); the line p
 B_NODE, B_TRI, B_SPH, B_PIX = 32, 36, 16, 3
 
 
-def kernel_bytes(r: dict, c: dict, out_pixels: int, batched: bool, nlights: int) -> dict:
+def kernel_bytes(r: dict, c: dict, out_pixels: int, batched: bool, nlights: int, compact: bool = False) -> dict:
     """Algorithmic bytes of one frame per kernel of the chain path (pathchain.hip), from a
     production-fetch counting pass: `r` = its per-role counter slots (Scene.counters_raw: the bytes
     each role's walks fetch -- wide-node lines, leaf records, primitives -- and its ray / hit counts),
-    `c` = the reference's counters.  Workspace traffic per item: a hit writes its record -- 16 B in
-    phase A (compact records, pathchain.hpp dbase: hit point and surface code), 32 B in phase B (with
-    the direction and material) -- and reads its 16-B face normal (TriShade); a traced shadow task id
+    `c` = the reference's counters.  Workspace traffic per item: a hit writes its record -- 32 B (hit
+    point, surface code, direction and material), or 16 B in phase A with compact records (RT_COMPACT,
+    pathchain.hpp dbase) -- and reads its 16-B face normal (TriShade); a traced shadow task id
     is written (4 B), read by its walker with the record's first 16 B and the normal, and its 1-B
     result written; a skipped one (light_needed) writes its 1-B result; a continuation id and its
     direction word (16 B, tail) are written in phase A and read in phase B with its record and normal;
     packing reads and writes each task id (in frame batches only the continuations'); k_finish reads every sample's path word (4 B) and every
     hit's record, normal and occlusion dword(s) (4 B when the record's bytes sit in one dword: 1, 2 or
     4 lights; else 8), and writes 3 B per pixel.
-    One frame alone, A's shadow rays run in k_mix's shadow role; in frame batches in k_occlude.  One
-    frame alone keeps 32-B phase-A records (rt_api.cpp chain_plan: compact records in frame batches
-    only, RT_COMPACT=2 everywhere)."""
+    One frame alone, A's shadow rays run in k_mix's shadow role; in frame batches in k_occlude.  Phase-A
+    records are 32 B, or 16 B where `compact` (the launches' own report: counter slot compact_launches;
+    rt_api.cpp full_records_fit decides by the frames a launch fits)."""
     NRM, TASK, OCC = 16, 4, 1
     REC_B = 32
-    compact = os.environ.get("RT_COMPACT", "1")
-    REC_A = 16 if compact == "2" or (compact == "1" and batched) else 32
+    REC_A = 16 if compact else 32
     DIRW = 16 if REC_A == 16 else 0
     inplace = batched and os.environ.get("RT_OCC_INPLACE", "1") != "0"   # A's tasks walked where k_chain left them
     samples, skipped = c["primary_rays"], c["shadow_rays_skipped"]
@@ -386,8 +385,15 @@ def main() -> int:
     # what the timed kernels left to k_fallback, per frame (warmup + timed frames since the reset)
     fbr = scene.counters_raw()
     fb_frames = max(a.warmup, F) + a.steps
-    fallback = {k[3:]: round(fbr[k] / fb_frames, 2) for k in scene.FALLBACK_SLOTS if k != "fb_launches"}
+    fallback = {k[3:]: round(fbr[k] / fb_frames, 2) for k in scene.FALLBACK_SLOTS if k.startswith("fb_") and k != "fb_launches"}
     fallback["launches_per_frame"] = round(fbr["fb_launches"] / fb_frames, 4)
+    # the timed launches' phase-A record size (compact 16-B records where a launch's frames needed them,
+    # rt_api.cpp full_records_fit): the per-kernel byte model follows the majority
+    compact_frac = fbr["compact_launches"] / max(1, fbr["fb_launches"])
+    fallback["compact_record_launches_frac"] = round(compact_frac, 3)
+    kbytes = kernel_bytes(roles, cnt, rows * W, batched=F > 1, nlights=nlights, compact=compact_frac >= 0.5)
+    alg_bytes = sum(kbytes.values())
+    ws_bytes = alg_bytes - trav_bytes
     fallback["note"] = ("per frame, timed kernels: continuations A->B, those beyond the phase-B record space "
                         "(walked whole by k_fallback), deferred closest-hit / shadow rays (outside the wide "
                         "trees' slab-test range), fallback shadow-queue overflows")

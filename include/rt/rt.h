@@ -293,7 +293,8 @@ int rt_counters_read(rt_scene* scene, rt_stats* stats);   /* synchronises the de
  * RT_COUNT_PROD=1 (the production walks' fetched bytes).  24..29 (every launch,
  * timed or counting; round 4): chain launches, continuations, continuations
  * beyond the phase-B record space (walked by k_fallback), deferred closest-hit
- * rays, deferred shadow rays, launches whose fallback shadow queue overflowed. */
+ * rays, deferred shadow rays, launches whose fallback shadow queue overflowed.
+ * 30 (round 5): launches with compact 16-B phase-A records (RT_COMPACT). */
 int rt_counters_read_raw(rt_scene* scene, uint64_t* out, int n);
 /* Diagnostics (ABI 7): per-kernel device time of the chain path's launches
  * since the last reset, for a scene created with env RT_KTIME=1 (events between

@@ -434,7 +434,7 @@ class Scene:
 
     # slots 24.. (pathchain.hpp kCntFb*): per chain launch, what the timed walks left to k_fallback
     FALLBACK_SLOTS = ("fb_launches", "fb_continuations", "fb_continuations_beyond_cb", "fb_deferred_closest",
-                      "fb_deferred_shadow", "fb_shadow_queue_overflows")
+                      "fb_deferred_shadow", "fb_shadow_queue_overflows", "compact_launches")
 
     KERNEL_KINDS = ("k_chain", "k_pack_a", "k_mix", "k_occlude_a", "k_pack_b", "k_occlude_b", "k_finish", "k_fallback")
 

@@ -1618,6 +1618,7 @@ __global__ __launch_bounds__(kBlock) void k_fallback(rtk::DevScene s, rtk::Eye e
         atomicAdd(&p.counters[kCntFbChains], (unsigned long long)p.totals[4]);
         atomicAdd(&p.counters[kCntFbShadows], (unsigned long long)p.totals[5]);
         if (p.totals[6]) atomicAdd(&p.counters[kCntFbOvfScans], 1ull);
+        if (p.clevels) atomicAdd(&p.counters[kCntCompactLaunches], 1ull);
     }
     for (unsigned i = gt; i < nfc + novf; i += gs)
         fallback_chain(s, e, p, i < nfc ? p.fbc[i] : p.cflat[p.cb + (i - nfc)], stk, w, i >= nfc);

@@ -85,6 +85,7 @@ enum CounterSlot : int {
     kCntFbChains,         //   closest-hit rays deferred (not in range of the wide trees' slab test)
     kCntFbShadows,        //   shadow rays deferred
     kCntFbOvfScans,       //   launches whose fallback shadow queue overflowed (occlusion bytes scanned)
+    kCntCompactLaunches,  // chain launches with compact (16-B) phase-A records (PcParams::clevels > 0)
 };
 
 // Phase-A levels whose records may leave out the direction (PcParams::dbase): k_finish rebuilds them

@@ -137,9 +137,10 @@ struct rt_scene {
     int tune_hot_units = 1;     // RT_HOT_UNITS: lone frames deal phase-A units heaviest-first by the previous frame's steps
     int tune_occ_inplace = 1;   // RT_OCC_INPLACE: A's shadow tasks read in their regions by k_occlude in frame
                                 // batches, and B's LDS-queue overflow in lone frames (0: packed)
-    int tune_compact = 0;       // RT_COMPACT: phase-A records without directions (16 B instead of 32): 1 frame batches,
-                                // 2 every launch, 0 none (round 5: 0 -- 20-frame calls 0.4151 -> 0.4040 ms/frame, 96-frame
-                                // calls -0.4 %, for 0.06 GB more HBM traffic per frame; profiles/r05_ab_compact.txt)
+    int tune_compact = 3;       // RT_COMPACT: phase-A records without directions (16 B instead of 32): 1 frame batches,
+                                // 2 every launch, 0 none, 3 (round 5) frame batches only where full records would leave
+                                // fewer than 4 frames per launch (full_records_fit; C3 AA1 20-frame calls 0.4151 -> 0.4040
+                                // ms/frame with full records, 96-frame calls -0.4 %; profiles/r05_ab_compact.txt)
     int tune_btail = 64;        // RT_BTAIL: the same once the continuations are exhausted (1: 1.24, 4: 1.18, 16: 1.15, 64: 1.14 ms)
     int tune_dyn = 1;           // RT_DYN_UNITS: phase-A waves take sample units from a launch-wide counter
     int tune_ublk_h = -1, tune_ublk_w = 8;  // RT_UBLK_H / RT_UBLK_W: phase-A unit column blocks (unit_order;
@@ -478,7 +479,7 @@ int upload_rest(rt_scene* s, const rt_options* opts) {
     if (const char* e = std::getenv("RT_BQ_CAP")) s->tune_bq_cap = std::max(0, std::atoi(e));
     if (const char* e = std::getenv("RT_BSERVICE")) s->tune_bservice = std::max(1, std::min(64, std::atoi(e)));
     if (const char* e = std::getenv("RT_BTAIL")) s->tune_btail = std::max(1, std::min(64, std::atoi(e)));
-    if (const char* e = std::getenv("RT_COMPACT")) s->tune_compact = std::max(0, std::min(2, std::atoi(e)));
+    if (const char* e = std::getenv("RT_COMPACT")) s->tune_compact = std::max(0, std::min(3, std::atoi(e)));
     if (const char* e = std::getenv("RT_OCC_INPLACE")) s->tune_occ_inplace = std::atoi(e) != 0;
     if (const char* e = std::getenv("RT_HOT_UNITS")) s->tune_hot_units = std::atoi(e) != 0;
     if (const char* e = std::getenv("RT_SPLIT")) s->tune_split = std::max(1, std::atoi(e));
@@ -692,7 +693,20 @@ int ensure_chain_grids(rt_scene* s) {
 
 // Every size of a launch of `nunits` row units, and its arena layout: worst-case queue sizing (every
 // sample recording every level), so no queue can overflow.  (ensure_chain_grids first.)
-ChainPlan chain_plan(const rt_scene* s, const ChainGeom& g, size_t nunits, bool count, size_t cb_want = 0) {
+ChainPlan chain_plan(const rt_scene* s, const ChainGeom& g, size_t nunits, bool count, size_t cb_want = 0,
+                     int cmp_mode = -1);
+
+// RT_COMPACT=3 (the default): frame batches keep full 32-B phase-A records where a 4-frame launch of this
+// frame size fits the slot's workspace share with them (C3 AA1: faster, §7 round 5), and compact 16-B ones
+// where it does not (C3 AA2: 1.83 -> 1.53 ms/frame with compact records: more frames per launch).
+bool full_records_fit(const rt_scene* s, const ChainGeom& g) {
+    ChainGeom g4 = g;
+    g4.nframes = 4;
+    const size_t per_frame = (g.units_total + (size_t)g.nframes - 1) / (size_t)g.nframes;
+    return chain_plan(s, g4, 4 * per_frame, false, 0, 0).bytes <= s->slot_budget();
+}
+
+ChainPlan chain_plan(const rt_scene* s, const ChainGeom& g, size_t nunits, bool count, size_t cb_want, int cmp_mode) {
     const int levels = g.levels, nl = g.nl;
     const int max_grid = s->chain_grid;
     ChainPlan P;
@@ -742,9 +756,12 @@ ChainPlan chain_plan(const rt_scene* s, const ChainGeom& g, size_t nunits, bool 
     const size_t nrec = cap * P.la + P.cb * (levels - P.la);
     ArenaLayout L;
     // phase A's records without their directions where k_finish can rebuild them (pathchain.hpp dbase)
-    // (RT_COMPACT=1 frame batches, 2 everywhere; off by default since round 5: the rebuilt directions cost
-    // k_finish more than the saved bytes gain k_chain and k_occlude)
-    const bool cmp = s->tune_compact == 2 || (s->tune_compact == 1 && g.nframes > 1);
+    // (RT_COMPACT=1 frame batches, 2 everywhere, 0 nowhere, 3 frame batches whose 4-frame launches would not fit
+    // with full records (full_records_fit): the rebuilt directions cost k_finish more than the saved bytes gain
+    // k_chain and k_occlude, unless the bytes buy frames per launch)
+    const bool cmp = cmp_mode >= 0 ? cmp_mode != 0
+                                   : s->tune_compact == 2 || (s->tune_compact == 1 && g.nframes > 1) ||
+                                         (s->tune_compact == 3 && g.nframes > 1 && !full_records_fit(s, g));
     P.clevels = cmp ? std::min(P.la, rtc::kCompactLevels) : 0;
     P.dbase = cap * (size_t)P.clevels;
     P.o_rec = L.take<float4>(nrec);

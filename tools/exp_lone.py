@@ -43,7 +43,7 @@ def child():
             ms, n = s.kernel_times(reset=True)
             kt = {k: round(v / (reps + 3), 4) for k, v in ms.items()}
         fbr = s.counters_raw()           # what the timed kernels left to k_fallback, per frame
-        fb = {k[3:]: round(fbr[k] / reps, 1) for k in s.FALLBACK_SLOTS if k != "fb_launches" and fbr[k]}
+        fb = {(k[3:] if k.startswith("fb_") else k): round(fbr[k] / reps, 1) for k in s.FALLBACK_SLOTS if k != "fb_launches" and fbr[k]}
         print(json.dumps({"median_ms": round(ts[len(ts) // 2], 4), "min_ms": round(ts[0], 4), "fallback": fb,
                           "sha_prefix": __import__("hashlib").sha256(out.cpu().numpy().tobytes()).hexdigest()[:12],
                           "kernel_times": kt}))
