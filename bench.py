@@ -546,7 +546,8 @@ def main() -> int:
     tfile = ROOT / "profiles" / f"traffic_{mode}.json"
     if tfile.exists():
         t = json.loads(tfile.read_text())
-        if t.get("config") == config and t.get("path") == a.path and t.get("hbm_bytes_per_frame"):
+        if (t.get("config") == config and t.get("aa", 1) == aa and t.get("path") == a.path
+                and t.get("hbm_bytes_per_frame")):
             traffic = int(t["hbm_bytes_per_frame"] / world)
             traffic_src = (f"profiles/{t.get('tag')}_traffic.json ({mode}; rocprofv3 2*FETCH_SIZE+WRITE_SIZE, "
                            f"N=1 frame / N)")

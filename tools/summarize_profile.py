@@ -100,7 +100,8 @@ for k, b in kb.items():
                               "frac_of_l2_line_peak": round(gbps / peak, 4) if gbps and peak else None,
                               "hbm_bytes_per_frame": per_kernel_bytes.get(k)}
 mode = "batched" if (trace.get("config", {}).get("frames_in_flight") or 1) > 1 else "one_frame"
-res = {"tag": tag, "mode": mode, "config": trace.get("config", {}).get("workload"), "path": trace.get("roofline", {}).get("path"),
+res = {"tag": tag, "mode": mode, "config": trace.get("config", {}).get("workload"), "aa": trace.get("config", {}).get("aa", 1),
+       "path": trace.get("roofline", {}).get("path"),
        "frames": frames, "workspace_slots": trace.get("config", {}).get("workspace_slots"),
        "frames_in_flight": trace.get("config", {}).get("frames_in_flight"),
        "kernel_ms_per_frame_rocprof": kernel_ms_sum, "per_kernel_ms_per_frame": per_kernel_ms,
