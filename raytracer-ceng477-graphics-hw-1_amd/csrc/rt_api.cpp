@@ -124,6 +124,8 @@ struct rt_scene {
     // 159.6, 16 M 147.4, 32 M 140.6 ms/frame.  32 M samples = 15 GB of workspace per slot (C3).
     size_t chunk_samples = size_t(32) << 20;
     int tune_batch = 32;        // RT_BATCH: frames per batched launch (rt_render_frames/cameras; 1 = off)
+    long long tune_batch_samples = 1ll << 21;   // RT_BATCH_SAMPLES: a multi-frame call's batches hold at least ~this
+                                                // many samples each (fewer batches than slots for small frames)
     bool tune_balance = false;  // RT_BALANCE=1: a call's frames dealt evenly over every slot (render_cameras; 20-frame
                                 // calls, 4 same-box runs each: 0.4316 ms/frame against 0.4221 for the greedy batches)
     int tune_slots = 3;         // RT_SLOTS: frame batches in flight together (workspace slots, <= kSlots;
@@ -461,6 +463,7 @@ int upload_rest(rt_scene* s, const rt_options* opts) {
     if (const char* e = std::getenv("RT_OREFILL")) s->tune_orefill = std::max(0, std::min(63, std::atoi(e)));
     if (const char* e = std::getenv("RT_BATCH")) s->tune_batch = std::max(1, std::atoi(e));
     if (const char* e = std::getenv("RT_BALANCE")) s->tune_balance = std::atoi(e) != 0;
+    if (const char* e = std::getenv("RT_BATCH_SAMPLES")) s->tune_batch_samples = std::max(1ll, std::atoll(e));
     // frame batches in flight: one HIP stream each beside the caller's; HIP multiplexes streams beyond
     // GPU_MAX_HW_QUEUES hardware queues (4 by default) onto the same queues, which serialises them
     // (C3: 4 slots on 4 queues 0.60 ms/frame, on 8 queues 0.51)
@@ -1419,7 +1422,14 @@ int render_cameras(rt_scene* s, const rt_camera* cams, int n, int aa, void* cons
                 const int nbr = std::max(std::min(nslot, L), (L + m - 1) / m);
                 for (int b = 0; b < nbr; ++b) starts.push_back(i + (int)((long long)L * b / nbr));
             } else {                               // round 4: batches of min(m, ceil(L / nslot)) frames
-                const int ch = std::min(m, (L + nslot - 1) / nslot);
+                // as many batches as slots, but at least ~batch_samples samples each: a run of small frames
+                // (a rank's 1/8 share of 20 C3 frames) goes out in 3 batches of 7 rather than 5 of 4 -- each batch
+                // ends with its own phase-B tail, which few samples do not hide (the one-GPU rehearsal of 8 ranks:
+                // 0.105 -> 0.094 ms per frame, profiles/r05_shard20.txt)
+                const double run_samples = (double)L * rt_slab_rows(c.image_height, rows_of(i), nranks) * c.image_width *
+                                           aa * aa;
+                const int nbat = std::max(1, std::min(nslot, (int)std::ceil(run_samples / (double)s->tune_batch_samples)));
+                const int ch = std::min(m, (L + nbat - 1) / nbat);
                 for (int b = 0; b < L; b += ch) starts.push_back(i + b);
             }
             i += L;
