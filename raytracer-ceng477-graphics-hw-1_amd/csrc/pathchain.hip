@@ -1014,7 +1014,7 @@ __device__ void occlude_queue_body(const rtk::DevScene& s, const PcParams& p, un
                 wide_slabs(nd, r, tmn, tmx);
                 uint32_t vs = 0;                  // empty slots: +inf / -inf planes, never hit
 #pragma unroll
-                for (int c = 0; c < W; ++c) vs |= (uint32_t)(tmx[c] >= __builtin_fmaxf(0.0f, tmn[c])) << c;
+                for (int c = 0; c < W; ++c) vs |= (uint32_t)any_slot_valid(tmn[c], tmx[c]) << c;
                 if (vs) {
                     if (__all(!(trav && cur >= 0) || sp + W <= kOStk)) {
                         // every hit slot written unconditionally (misses to the sink entry), the

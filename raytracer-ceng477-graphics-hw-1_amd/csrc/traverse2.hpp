@@ -467,6 +467,17 @@ __device__ __forceinline__ void wide_slabs(const WideNode& n, const Ray& r, floa
 }
 __device__ __forceinline__ int wide_code(const WideNode& n, int c) { return (int)wide_dw(n, 22 + c); }
 
+// Any-hit slot validity, tmx >= max(0, tmn), with the max as one v_max_f32 on the slab values.  Written
+// as fmaxf, the compiler regroups max(0, max(x, y, z)) as max3(max(x, y), z, 0) and quiets both inputs
+// of the two-input max first (v_max_f32 v, v, v: fma_mix_h's results come from asm, so it cannot prove
+// them canonical) -- 12 extra instructions per wide any-hit step.  Same result: arithmetic never
+// yields a signalling NaN, which is all the quieting would change.
+__device__ __forceinline__ bool any_slot_valid(float tmn, float tmx) {
+    float m;
+    asm("v_max_f32 %0, 0, %1" : "=v"(m) : "v"(tmn));
+    return tmx >= m;
+}
+
 // Primitives of a leaf record (header at L[0..1], prims from L[2]); the first
 // one is passed in already loaded, the next one is in flight while the
 // current one is tested.  f(slot, p0, p1, p2) with slot = its Prim[] index;
@@ -761,7 +772,7 @@ __device__ __forceinline__ int wide_any_step(const rtk::DevScene& s, const Ray& 
         wide_slabs(n, r, tmn, tmx);
         uint32_t vs = 0;                  // empty slots: +inf / -inf planes, never valid (quantize_wide)
 #pragma unroll
-        for (int c = 0; c < W; ++c) vs |= (uint32_t)(tmx[c] >= __builtin_fmaxf(0.0f, tmn[c])) << c;
+        for (int c = 0; c < W; ++c) vs |= (uint32_t)any_slot_valid(tmn[c], tmx[c]) << c;
         if (vs) {
             if (__all(k.sp + W <= STK::kLds)) {
                 // the whole wave has LDS room: every hit slot written unconditionally, the first one
