@@ -33,7 +33,7 @@
 extern "C" {
 #endif
 
-#define RT_ABI_VERSION 11
+#define RT_ABI_VERSION 12
 
 typedef enum rt_status {
     RT_OK = 0,
@@ -321,6 +321,14 @@ int rt_scene_check(rt_scene* scene);
  * (raytracer.cpp:177-225). */
 int rt_primary_hits(rt_scene* scene, const rt_camera* cam, int aa_factor,
                     float* t_out, int32_t* material_out);
+/* The same dump from the TIMED walk (ABI 12): one whole frame through the
+ * production kernels (k_chain's reference-order wide-tree walk, k_fallback
+ * for the rays it defers), with each sample's level-0 tSmall and material
+ * stored where the production kernel records its hit.  Unset entries (a
+ * sample no kernel recorded) read back as NaN / -1.  Parity surface for
+ * Ray::getFirstIntersection (raytracer.cpp:177-225) on the product path. */
+int rt_primary_hits_production(rt_scene* scene, const rt_camera* cam, int aa_factor,
+                               float* t_out, int32_t* material_out);
 
 /* ---- host utilities ---- */
 /* ImageProcessor::downSample (raytracer.cpp:459-484) on host buffers. */

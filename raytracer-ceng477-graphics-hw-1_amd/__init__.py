@@ -175,6 +175,7 @@ _SIGS = [
     ("rt_kernel_times", ctypes.c_int, [_P, _P, ctypes.c_int, ctypes.c_int]),
     ("rt_scene_check", ctypes.c_int, [_P]),
     ("rt_primary_hits", ctypes.c_int, [_P, ctypes.POINTER(Camera), ctypes.c_int, _P, _P]),
+    ("rt_primary_hits_production", ctypes.c_int, [_P, ctypes.POINTER(Camera), ctypes.c_int, _P, _P]),
     ("rt_downsample_host", ctypes.c_int, [_P, ctypes.c_int, ctypes.c_int, ctypes.c_int, _P]),
     ("rt_write_ppm", ctypes.c_int, [ctypes.c_char_p, _P, ctypes.c_int, ctypes.c_int]),
 ]
@@ -454,12 +455,16 @@ class Scene:
         last check (rt_scene_check)."""
         _check(lib().rt_scene_check(self._h))
 
-    def primary_hits(self, cam: Camera, aa: int = 1) -> tuple[np.ndarray, np.ndarray]:
+    def primary_hits(self, cam: Camera, aa: int = 1, walk: str = "reference") -> tuple[np.ndarray, np.ndarray]:
+        """Level-0 closest hit per internal pixel: tSmall (-1 on a miss) and material id (0 on a miss).
+        walk="production": the timed kernels' own walk (rt_primary_hits_production: k_chain with the two
+        stores added, k_fallback for deferred rays); "reference": the side kernel's binary-tree walk
+        (rt_primary_hits)."""
         H, W = cam.image_height * aa, cam.image_width * aa
         t = np.empty((H, W), dtype=np.float32)
         m = np.empty((H, W), dtype=np.int32)
-        _check(lib().rt_primary_hits(self._h, ctypes.byref(cam), aa, t.ctypes.data_as(ctypes.c_void_p),
-                                     m.ctypes.data_as(ctypes.c_void_p)))
+        fn = {"reference": lib().rt_primary_hits, "production": lib().rt_primary_hits_production}[walk]
+        _check(fn(self._h, ctypes.byref(cam), aa, t.ctypes.data_as(ctypes.c_void_p), m.ctypes.data_as(ctypes.c_void_p)))
         return t, m
 
 

@@ -21,6 +21,7 @@
 // queued light-major within each wave, so a wave of k_occlude walks rays
 // toward one light from neighbouring surface points.
 #include <hip/hip_runtime.h>
+#include <hip/hip_ext.h>
 
 #include "pathchain.hpp"
 #include "traverse2.hpp"
@@ -314,8 +315,9 @@ __device__ __forceinline__ Ray shadow_from_record(const rtk::DevScene& s, const 
 // Rays the timed walks leave to k_fallback: not NaN-free, or beyond the range of the wide trees' fused
 // slab test (wide_ray_ok; in practice a direction component of exactly 0, whose 1/d is infinite).
 // The production kernels then carry only the wide-tree walks (fewer registers: no VGPR spills).
-__device__ __forceinline__ bool defer_closest(const rtk::DevScene& s, const Ray& r) {
-    return s.nnodes > 0 && ((s.force_fb & 1) || !(s.use_wide && ray_nan_free(r) && wide_ray_ok(r)));
+// (tests: force_fb bit 0 defers every closest-hit ray, bit 2 only reflected ones -- refl)
+__device__ __forceinline__ bool defer_closest(const rtk::DevScene& s, const Ray& r, bool refl) {
+    return s.nnodes > 0 && ((s.force_fb & (refl ? 5 : 1)) || !(s.use_wide && ray_nan_free(r) && wide_ray_ok(r)));
 }
 __device__ __forceinline__ bool defer_any(const rtk::DevScene& s, const Ray& r) {
     return s.nnodes > 0 && ((s.force_fb & 2) || !(s.use_stree == 2 && ray_nan_free(r) && wide_ray_ok(r)));
@@ -517,7 +519,9 @@ __device__ __forceinline__ unsigned unit_order(const PcParams& p, unsigned u, un
 
 // closest-hit chains of one phase (raytracer.cpp:385-439 minus the shading):
 // record each hit, queue its shadow tasks, follow (or hand on) mirrors.
-template <bool COUNT, bool CONT, bool BQ = CONT>
+// DBG (k_chain<false, true>, rt_primary_hits_production): also store each sample's level-0 hit (PcParams::dbg_t,
+// dbg_m) -- the same walk, two stores added.
+template <bool COUNT, bool CONT, bool BQ = CONT, bool DBG = false>
 __device__ void chain_body(const rtk::DevScene& s, const rtk::Eye& e, const PcParams& p, unsigned blk, unsigned G,
                            const PhaseOut& o) {
     WalkStack stk;
@@ -558,6 +562,13 @@ __device__ void chain_body(const rtk::DevScene& s, const rtk::Eye& e, const PcPa
                 hitp = add(r.o, mul(r.d, h.t));
                 rec_write(p, lvp, hitp, code, r.d, mat);
                 if (COUNT) nhit++;
+            }
+            if (DBG && !CONT && k == 0) {
+                int row, col;
+                if (slab_sample_pixel(p, path, &row, &col)) {
+                    p.dbg_t[(size_t)row * p.wi + col] = h.t;
+                    p.dbg_m[(size_t)row * p.wi + col] = hit ? mat : 0;
+                }
             }
             // one shadow task per light (:399-404) whose ray can change the pixel (light_needed; the
             // counting passes trace every one, as the reference does); light-major within the wave
@@ -630,9 +641,11 @@ __device__ void chain_body(const rtk::DevScene& s, const rtk::Eye& e, const PcPa
                 r = reflect_ray(s, hitp, nn, r.d);
                 ++k;
                 nrefl++;
-                if (!COUNT && defer_closest(s, r)) {     // the rest of this path: k_fallback
+                if (!COUNT && defer_closest(s, r, true)) {     // the rest of this path: k_fallback
                     if (lvp < p.dbase) p.tail[path] = make_float4(dk.x, dk.y, dk.z, 0.0f);   // reflect_from_record
-                    if (!CONT) p.pinfo[path] = kPathCont;   // (k_fallback's path)
+                    // (k_fallback's path; fallback_chain's pinfo write clears the bit again for a phase-A path,
+                    // so fin_cont's second loop still finishes its pixel)
+                    if (!CONT) p.pinfo[path] = kPathCont;
                     fb_chain(p, (unsigned)lvp);
                     st = kIdle;
                 } else {
@@ -686,7 +699,7 @@ __device__ void chain_body(const rtk::DevScene& s, const rtk::Eye& e, const PcPa
                             k = (int)(lvp / (unsigned)p.cap) + 1;
                             r = reflect_from_record(s, p, lvp, path);
                             nrefl++;
-                            if (!COUNT && defer_closest(s, r)) fb_chain(p, lvp);
+                            if (!COUNT && defer_closest(s, r, true)) fb_chain(p, lvp);
                             else st = walk_begin<COUNT>(s, r, wk, w) ? kTrav : kDone;
                         } else {
                             const unsigned idx = (dyn ? uid : blk + (v >> 8) * G) * 256u + (v & 255u);
@@ -697,8 +710,9 @@ __device__ void chain_body(const rtk::DevScene& s, const rtk::Eye& e, const PcPa
                                 if (kTraceBuild && p.trace) t_grab = (unsigned)wall_clock64();
                                 nprim++;
                                 if (s.max_depth < 0) p.pinfo[path] = 0 | (kEndZero << 8);   // depth 0 > max: black
-                                else if (!COUNT && defer_closest(s, r)) {
-                                    p.pinfo[path] = kPathCont;   // (k_fallback's path)
+                                else if (!COUNT && defer_closest(s, r, false)) {
+                                    // (k_fallback's path; fallback_chain's pinfo write clears the bit again)
+                                    p.pinfo[path] = kPathCont;
                                     fb_chain(p, kFbEye | path);
                                 }
                                 else st = walk_begin<COUNT>(s, r, wk, w) ? kTrav : kDone;
@@ -1065,12 +1079,12 @@ __device__ __forceinline__ PhaseOut phase_b(const PcParams& p) {
 }
 
 // Phase A: every sample, levels [0, kinline].
-template <bool COUNT>
+template <bool COUNT, bool DBG = false>
 __global__ __launch_bounds__(kBlock, COUNT ? 4 : RT_WAVES_PER_EU) void k_chain(rtk::DevScene s, rtk::Eye e, PcParams p) {
     if (threadIdx.x == 0) g_ccnt = 0;
     if (threadIdx.x < kDynUnits) g_uid[threadIdx.x] = kUidUnset;
     block_init(s);
-    chain_body<COUNT, false>(s, e, p, blockIdx.x, gridDim.x, phase_a(p));
+    chain_body<COUNT, false, false, DBG>(s, e, p, blockIdx.x, gridDim.x, phase_a(p));
 }
 
 // Region b of a per-workgroup queue (q[b*cap ..], cnt[b] entries) copied to
@@ -1572,6 +1586,18 @@ __device__ void fallback_chain(const rtk::DevScene& s, const rtk::Eye& e, const 
             }
         }
         const HitRec h = wk.best;
+        if (p.dbg_t && k == 0) {                   // diagnostics: a deferred eye ray's hit (PcParams::dbg_t)
+            int row, col, mat = 0;
+            if (h.prim >= 0) {
+                V nn;
+                int code;
+                hit_surface(s, r, h, &nn, &mat, &code);
+            }
+            if (slab_sample_pixel(p, path, &row, &col)) {
+                p.dbg_t[(size_t)row * p.wi + col] = h.t;
+                p.dbg_m[(size_t)row * p.wi + col] = mat;
+            }
+        }
         if (h.prim < 0) {                          // miss: background at depth 0, else 0 (:442-449)
             if (k == 0) c = V{s.bgx, s.bgy, s.bgz};
             break;
@@ -1720,17 +1746,27 @@ __global__ __launch_bounds__(kBlock) void k_walk_timing(rtk::DevScene s, const f
 
 }  // namespace
 
+// A kernel launch; with a KTimer, through hipExtLaunchKernel with the timer's next start / stop events.
+#define RT_LAUNCH(KT, KIND, KERN, GRID, BLK, ST, ...)                                                       \
+    do {                                                                                                 \
+        hipEvent_t e0_ = nullptr, e1_ = nullptr;                                                         \
+        if (KT) (KT)->take(KIND, &e0_, &e1_);                                                            \
+        if (e0_) hipExtLaunchKernelGGL(KERN, GRID, BLK, 0, ST, e0_, e1_, 0, __VA_ARGS__);                \
+        else hipLaunchKernelGGL(KERN, GRID, BLK, 0, ST, __VA_ARGS__);                                    \
+    } while (0)
+
 // Shading + fold + SSAA: k_finish (a lane per pixel; materials and lights in LDS), or k_finish_any for
 // larger scenes.
-void launch_finish(const rtk::DevScene& s, const rtk::Eye& e, const PcParams& p, hipStream_t st) {
+void launch_finish(const rtk::DevScene& s, const rtk::Eye& e, const PcParams& p, hipStream_t st, KTimer* kt) {
     const int npix = (p.chunk_rows / p.aa) * p.width;
     const dim3 pgrid(std::max(1, std::min((npix + kBlock - 1) / kBlock, p.fin_grid > 0 ? p.fin_grid : INT32_MAX)));
+    const dim3 blk(kBlock);
     if (s.nmats <= kFinishMats && s.nlights <= kFinishLights) {
-        if (p.clevels) hipLaunchKernelGGL((k_finish<true>), pgrid, dim3(kBlock), 0, st, s, e, p);
-        else hipLaunchKernelGGL((k_finish<false>), pgrid, dim3(kBlock), 0, st, s, e, p);
+        if (p.clevels) RT_LAUNCH(kt, kKFinish, (k_finish<true>), pgrid, blk, st, s, e, p);
+        else RT_LAUNCH(kt, kKFinish, (k_finish<false>), pgrid, blk, st, s, e, p);
     } else {
-        if (p.clevels) hipLaunchKernelGGL((k_finish_any<true>), pgrid, dim3(kBlock), 0, st, s, e, p);
-        else hipLaunchKernelGGL((k_finish_any<false>), pgrid, dim3(kBlock), 0, st, s, e, p);
+        if (p.clevels) RT_LAUNCH(kt, kKFinish, (k_finish_any<true>), pgrid, blk, st, s, e, p);
+        else RT_LAUNCH(kt, kKFinish, (k_finish_any<false>), pgrid, blk, st, s, e, p);
     }
 }
 
@@ -1809,17 +1845,15 @@ unsigned chain_block_scap(int n0, int grid, int levels, int nlights) {
 hipError_t launch_chain_chunk(const rtk::DevScene& s, const rtk::Eye& e, const PcParams& p, bool count,
                               hipStream_t st, KTimer* kt) {
     const dim3 blk(kBlock);
-    auto mark = [&](int k) { if (kt) kt->mark(k, st); };
     const bool phase_b = p.kinline < s.max_depth;     // any continuation possible
     {   // the dynamic unit counter and k_fallback's counts
         const hipError_t me = hipMemsetAsync(p.totals + 3, 0, (kTotalsWords - 3) * sizeof(unsigned), st);
         if (me != hipSuccess) return me;
     }
-    mark(kKChain);
-    if (count) hipLaunchKernelGGL(k_chain<true>, dim3(p.grid), blk, 0, st, s, e, p);
-    else hipLaunchKernelGGL(k_chain<false>, dim3(p.grid), blk, 0, st, s, e, p);
-    mark(kKPackA);
-    hipLaunchKernelGGL(k_pack_a, dim3(p.grid), blk, 0, st, p);
+    if (count) RT_LAUNCH(kt, kKChain, k_chain<true>, dim3(p.grid), blk, st, s, e, p);
+    else if (p.dbg_t) RT_LAUNCH(kt, kKChain, (k_chain<false, true>), dim3(p.grid), blk, st, s, e, p);
+    else RT_LAUNCH(kt, kKChain, k_chain<false>, dim3(p.grid), blk, st, s, e, p);
+    RT_LAUNCH(kt, kKPackA, k_pack_a, dim3(p.grid), blk, st, p);
     PcParams q = p;
     if (!phase_b) q.gb = 0;
     // p.split_occ (frame batches): k_mix only walks the chains, A's shadow tasks go to k_occlude (5 waves
@@ -1827,38 +1861,31 @@ hipError_t launch_chain_chunk(const rtk::DevScene& s, const rtk::Eye& e, const P
     // workgroups walk them beside the chains.  Frame batches without phase B (depth 0): no k_mix at all
     const bool split = p.split_occ != 0;
     const int mgrid = split ? q.gb : q.gb + p.ogrid;
-    mark(kKMix);
     // frame batches (split): phase B's shadow tasks all through k_pack_b + k_occlude (no LDS queue)
     if (mgrid == 0) {
     } else if (count) {
-        if (split) hipLaunchKernelGGL((k_mix<true, false>), dim3(mgrid), blk, 0, st, s, e, q);
-        else hipLaunchKernelGGL((k_mix<true, true>), dim3(mgrid), blk, 0, st, s, e, q);
+        if (split) RT_LAUNCH(kt, kKMix, (k_mix<true, false>), dim3(mgrid), blk, st, s, e, q);
+        else RT_LAUNCH(kt, kKMix, (k_mix<true, true>), dim3(mgrid), blk, st, s, e, q);
     } else {
-        if (split) hipLaunchKernelGGL((k_mix<false, false>), dim3(mgrid), blk, 0, st, s, e, q);
-        else hipLaunchKernelGGL((k_mix<false, true>), dim3(mgrid), blk, 0, st, s, e, q);
+        if (split) RT_LAUNCH(kt, kKMix, (k_mix<false, false>), dim3(mgrid), blk, st, s, e, q);
+        else RT_LAUNCH(kt, kKMix, (k_mix<false, true>), dim3(mgrid), blk, st, s, e, q);
     }
     if (split) {
-        mark(kKOccA);
-        if (count) hipLaunchKernelGGL(k_occlude<true>, dim3(p.occ_grid), blk, 0, st, s, p, 0);
-        else hipLaunchKernelGGL(k_occlude<false>, dim3(p.occ_grid), blk, 0, st, s, p, 0);
+        if (count) RT_LAUNCH(kt, kKOccA, k_occlude<true>, dim3(p.occ_grid), blk, st, s, p, 0);
+        else RT_LAUNCH(kt, kKOccA, k_occlude<false>, dim3(p.occ_grid), blk, st, s, p, 0);
     }
     if (phase_b) {
-        mark(kKPackB);
-        if (count || !p.occ_inplace_b) hipLaunchKernelGGL(k_pack_b, dim3(p.gb), blk, 0, st, p);
+        if (count || !p.occ_inplace_b) RT_LAUNCH(kt, kKPackB, k_pack_b, dim3(p.gb), blk, st, p);
         const int og = split ? p.occ_grid : p.ogrid;
-        mark(kKOccB);
-        if (count) hipLaunchKernelGGL(k_occlude<true>, dim3(og), blk, 0, st, s, p, 1);
-        else hipLaunchKernelGGL(k_occlude<false>, dim3(og), blk, 0, st, s, p, 1);
+        if (count) RT_LAUNCH(kt, kKOccB, k_occlude<true>, dim3(og), blk, st, s, p, 1);
+        else RT_LAUNCH(kt, kKOccB, k_occlude<false>, dim3(og), blk, st, s, p, 1);
     }
+    RT_LAUNCH(kt, kKFallback, k_fallback, dim3(p.fb_grid), blk, st, s, e, p);
     // continued pixels first only where they are few and deep (one sample per pixel): with 16 samples
     // a pixel (C5: 130 vs 106 ms) and without phase B (C2: +5 %) the extra pinfo reads cost more
-    mark(kKFallback);
-    hipLaunchKernelGGL(k_fallback, dim3(p.fb_grid), blk, 0, st, s, e, p);
     PcParams f = p;
     f.fin_cont = phase_b && p.aa == 1;
-    mark(kKFinish);
-    launch_finish(s, e, f, st);
-    mark(kKEnd);
+    launch_finish(s, e, f, st, kt);
     return hipGetLastError();
 }
 

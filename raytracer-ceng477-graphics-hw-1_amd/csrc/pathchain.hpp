@@ -30,7 +30,7 @@ constexpr int kMaxFrames = 32;        // frames of one batched launch (PcParams 
 #ifndef RT_BQ
 #define RT_BQ 1536
 #endif
-constexpr int kMaxBq = RT_BQ;
+constexpr int kMaxBq = RT_BQ;   // phase-B workgroup shadow queue (LDS slots, pathchain.hip)
 // Diagnostics build (RT_TRACE_BUILD=1, tools/trace_report.py): the chain kernels record wall-clock
 // timings per sample, continuation and shadow workgroup into PcParams::trace (env RT_TRACE names the
 // dump).  Off in the product build: its counters cost the walk kernels registers.
@@ -43,7 +43,7 @@ constexpr bool kTraceBuild = RT_TRACE_BUILD != 0;
 // built.
 #ifndef RT_LEAF_QUEUE
 #define RT_LEAF_QUEUE 1
-#endif          // phase-B workgroup shadow queue (LDS slots, pathchain.hip)
+#endif
 
 enum PathKind : int {
     kEndBg = 0,     // deepest ray missed at depth 0: background
@@ -220,6 +220,12 @@ struct PcParams {
     // (new fields at the end: kernel arguments are loaded in runs of neighbours, so a field inserted
     // among the walk kernels' ones changed their SGPR spills 28 -> 67)
     unsigned* cont_peak;  // frames of several chunks: the most continuations of one chunk (k_pack_a, atomicMax)
+    // Diagnostics (rt_primary_hits_production): each sample's level-0 closest hit as the TIMED walk found it
+    // -- tSmall (-1 on a miss) and material id (0 on a miss) at internal pixel row * wi + col -- written by
+    // k_chain<false, true> (the production kernel with these two stores added) and, for an eye ray the
+    // timed walks defer, by k_fallback.  Null in every other launch.
+    float* dbg_t;
+    int* dbg_m;
 };
 
 // Worst-case task-queue slots per workgroup: every sample of the workgroup
@@ -245,19 +251,22 @@ hipError_t launch_udiv(const unsigned* v, int nv, const unsigned* d, int nd, uns
 hipError_t launch_walk_timing(const rtk::DevScene& s, const float* rays, int n, int lanes, int reps, int mode,
                               unsigned long long* out, hipStream_t st);
 
-// Diagnostics (RT_KTIME=1 scenes, rt_kernel_times): HIP events recorded between the kernels of a
-// chain launch on its stream, so the host can split the launch's time per kernel (one slot: the
-// kernels run back to back).
-enum KernelKind : int { kKChain = 0, kKPackA, kKMix, kKOccA, kKPackB, kKOccB, kKFinish, kKFallback, kKEnd, kKKinds };
+// Diagnostics (RT_KTIME=1 scenes, rt_kernel_times): each kernel of a chain launch is launched with
+// hipExtLaunchKernel's start / stop events, which take the dispatch's own begin and end timestamps
+// (what rocprofv3 --kernel-trace reports), so the host can split the launch's time per kernel without
+// markers between the kernels (round 5's inter-kernel events read 23 % above rocprof's kernel sums).
+enum KernelKind : int { kKChain = 0, kKPackA, kKMix, kKOccA, kKPackB, kKOccB, kKFinish, kKFallback, kKKinds };
 struct KTimer {
     static constexpr int kMax = 16;
-    hipEvent_t ev[kMax] = {};
+    hipEvent_t ev0[kMax] = {}, ev1[kMax] = {};
     int kind[kMax] = {};
     int n = 0;
-    void mark(int k, hipStream_t st) {
-        if (n < kMax && ev[n]) {
+    // the next kernel's start / stop events (both null once full or not created)
+    void take(int k, hipEvent_t* a, hipEvent_t* b) {
+        if (n < kMax && ev0[n] && ev1[n]) {
             kind[n] = k;
-            (void)hipEventRecord(ev[n++], st);
+            *a = ev0[n];
+            *b = ev1[n++];
         }
     }
 };

@@ -52,9 +52,9 @@ struct DevScene {
     int leaf_wait;        // 4-wide walks: a lane at a leaf record waits while fewer than leaf_wait/64 of the
                           // wave's walking lanes are at one (0: never waits; RT_LEAF_WAIT)
     int cull_shadows;     // chain path: shadow rays that cannot change the pixel are not traced
-    int force_fb;         // tests (RT_FORCE_FALLBACK): the timed chain kernels defer every closest-hit (bit 0)
-                          // and/or any-hit (bit 1) ray to k_fallback
                           // (pathchain.hip light_needed; every material's kd finite; RT_CULL=0 disables)
+    int force_fb;         // tests (RT_FORCE_FALLBACK): the timed chain kernels defer every closest-hit (bit 0),
+                          // any-hit (bit 1) and/or reflected closest-hit (bit 2) ray to k_fallback
 
     // Sphere prims carry ~sphere_index in p0.w (negative), triangles their id.
     __device__ __forceinline__ bool prim_is_sphere(int, const float4 p0) const {

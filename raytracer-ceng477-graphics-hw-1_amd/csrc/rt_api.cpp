@@ -166,7 +166,9 @@ struct rt_scene {
     rtc::KTimer kt;
     static constexpr size_t kStagingReserve = size_t(64) << 20;
     size_t slot_budget() const {
-        const size_t fixed = scene_bytes + kStagingReserve;
+        // the scene, and the host-output staging (rt_render's frame, rt_render_cameras' frames) at its live
+        // size or the reserve, whichever is larger; fit_arenas drops an arena a staging growth leaves over
+        const size_t fixed = scene_bytes + std::max(kStagingReserve, out_cap + batch_out_cap);
         const size_t arenas = ws_budget > 2 * fixed ? ws_budget - fixed : ws_budget / 2;
         return arenas / (size_t)std::max(1, std::min(tune_slots, kSlots));
     }
@@ -205,6 +207,8 @@ struct rt_scene {
     hipEvent_t fork_ev = nullptr;
     uint8_t* batch_out = nullptr;              // device frames of rt_render_cameras (host outputs)
     size_t batch_out_cap = 0;
+    float* dbg_t = nullptr;                    // rt_primary_hits_production: the level-0 hit dump (PcParams::dbg_t)
+    int* dbg_m = nullptr;
 
     ~rt_scene() {
         if (group) rt_internal_group_destroy(group);
@@ -215,8 +219,10 @@ struct rt_scene {
             if (slot_done[i]) (void)hipEventDestroy(slot_done[i]);
         }
         if (fork_ev) (void)hipEventDestroy(fork_ev);
-        for (auto& e : kt.ev)
-            if (e) (void)hipEventDestroy(e);
+        for (int i = 0; i < rtc::KTimer::kMax; ++i) {
+            if (kt.ev0[i]) (void)hipEventDestroy(kt.ev0[i]);
+            if (kt.ev1[i]) (void)hipEventDestroy(kt.ev1[i]);
+        }
         for (auto& a : arenas) (void)hipFree(a.hist);
         for (auto& e : cont_ev)
             if (e) (void)hipEventDestroy(e);
@@ -697,19 +703,23 @@ int ensure_chain_grids(rt_scene* s) {
 // Every size of a launch of `nunits` row units, and its arena layout: worst-case queue sizing (every
 // sample recording every level), so no queue can overflow.  (ensure_chain_grids first.)
 ChainPlan chain_plan(const rt_scene* s, const ChainGeom& g, size_t nunits, bool count, size_t cb_want = 0,
-                     int cmp_mode = -1);
+                     int cmp_mode = -1, bool use_share = true);
 
 // RT_COMPACT=3 (the default): frame batches keep full 32-B phase-A records where a 4-frame launch of this
 // frame size fits the slot's workspace share with them (C3 AA1: faster, §7 round 5), and compact 16-B ones
-// where it does not (C3 AA2: 1.83 -> 1.53 ms/frame with compact records: more frames per launch).
+// where it does not (C3 AA2: 1.83 -> 1.53 ms/frame with compact records: more frames per launch).  Decided
+// with the default phase-B record space (not the measured continuation share, which moves as read-backs
+// arrive): one frame geometry always gets the same record size, so a timed call never switches it and
+// reallocates a workspace.
 bool full_records_fit(const rt_scene* s, const ChainGeom& g) {
     ChainGeom g4 = g;
     g4.nframes = 4;
     const size_t per_frame = (g.units_total + (size_t)g.nframes - 1) / (size_t)g.nframes;
-    return chain_plan(s, g4, 4 * per_frame, false, 0, 0).bytes <= s->slot_budget();
+    return chain_plan(s, g4, 4 * per_frame, false, 0, 0, false).bytes <= s->slot_budget();
 }
 
-ChainPlan chain_plan(const rt_scene* s, const ChainGeom& g, size_t nunits, bool count, size_t cb_want, int cmp_mode) {
+ChainPlan chain_plan(const rt_scene* s, const ChainGeom& g, size_t nunits, bool count, size_t cb_want, int cmp_mode,
+                     bool use_share) {
     const int levels = g.levels, nl = g.nl;
     const int max_grid = s->chain_grid;
     ChainPlan P;
@@ -746,7 +756,7 @@ ChainPlan chain_plan(const rt_scene* s, const ChainGeom& g, size_t nunits, bool 
     // (at least cap / RT_CONT_DEN, more once frame batches report a larger continuation share: that share
     // + 10 %)
     const size_t cb_guess = std::max(cap / (size_t)std::max(1, s->tune_cont_den),
-                                     (size_t)((double)cap * std::min(1.0, s->cont_frac * 1.1 + 0.005)));
+                                     use_share ? (size_t)((double)cap * std::min(1.0, s->cont_frac * 1.1 + 0.005)) : 0);
     P.cb = P.la >= levels ? 0 : (count ? cap : std::min(cap, std::max(cb_guess, std::min<size_t>(cap, 65536))));
     if (cb_want > 0 && !count && P.la < levels) P.cb = std::min(cap, std::max(P.cb, cb_want));
     if (s->tune_cont_cb > 0 && !count && P.la < levels) P.cb = std::min(cap, (size_t)s->tune_cont_cb);
@@ -971,6 +981,8 @@ int render_chain(rt_scene* s, const rtk::Eye& eye, const rtk::FrameParams& f, bo
     p.occ_inplace = RT_LEAF_QUEUE && !count && P.split_occ && s->tune_occ_inplace ? 1 : 0;
     p.occ_inplace_b = RT_LEAF_QUEUE && !P.split_occ && !count && s->tune_occ_inplace ? 1 : 0;
     p.cont_peak = peak ? s->d_cont_peak : nullptr;
+    p.dbg_t = count ? nullptr : s->dbg_t;
+    p.dbg_m = count ? nullptr : s->dbg_m;
     p.refill = s->tune_refill >= 0 ? s->tune_refill : 0;
     p.service = s->tune_service >= 0 ? s->tune_service : 64;
     p.bservice = s->tune_bservice;
@@ -1044,15 +1056,18 @@ int render_chain(rt_scene* s, const rtk::Eye& eye, const rtk::FrameParams& f, bo
         }
         if (p.grid > P.G) return fail(RT_ERR_LIMIT, "internal: chain grid exceeds the workspace");
         if (s->ktime) {
-            // diagnostics: events between the kernels, then the launch's per-kernel split (synchronous)
-            for (int i = 0; i < rtc::KTimer::kMax; ++i)
-                if (!s->kt.ev[i]) HIP_TRY(hipEventCreate(&s->kt.ev[i]));
+            // diagnostics: each kernel's own start / stop timestamps (KTimer), then the launch's per-kernel split
+            // (synchronous)
+            for (int i = 0; i < rtc::KTimer::kMax; ++i) {
+                if (!s->kt.ev0[i]) HIP_TRY(hipEventCreate(&s->kt.ev0[i]));
+                if (!s->kt.ev1[i]) HIP_TRY(hipEventCreate(&s->kt.ev1[i]));
+            }
             s->kt.n = 0;
             HIP_TRY(rtc::launch_chain_chunk(s->dev, eye, p, count, st, &s->kt));
-            HIP_TRY(hipEventSynchronize(s->kt.ev[s->kt.n - 1]));
-            for (int i = 0; i + 1 < s->kt.n; ++i) {
+            HIP_TRY(hipStreamSynchronize(st));
+            for (int i = 0; i < s->kt.n; ++i) {
                 float ms = 0;
-                HIP_TRY(hipEventElapsedTime(&ms, s->kt.ev[i], s->kt.ev[i + 1]));
+                HIP_TRY(hipEventElapsedTime(&ms, s->kt.ev0[i], s->kt.ev1[i]));
                 s->kt_ms[s->kt.kind[i]] += ms;
             }
             s->kt_launches++;
@@ -1088,6 +1103,18 @@ int check_device_error(rt_scene* s) {
     if (e == 0) return RT_OK;
     HIP_TRY(hipMemset(s->d_err, 0, sizeof(unsigned)));
     return device_error(e);
+}
+
+// After a host-output staging buffer grew (slot_budget takes it off the budget): free the arenas now over
+// their slot's share (the device is idle: the growth synchronised); each is re-made within it at its next use.
+void fit_arenas(rt_scene* s) {
+    const size_t share = s->slot_budget();
+    for (auto& a : s->arenas)
+        if (a.bytes > share) {
+            (void)hipFree(a.p);
+            a.p = nullptr;
+            a.bytes = 0;
+        }
 }
 
 }  // namespace
@@ -1610,6 +1637,7 @@ int rt_render_cameras(rt_scene* s, const rt_camera* cams, int n, int aa, uint8_t
         s->batch_out_cap = 0;
         HIP_TRY(hipMalloc(reinterpret_cast<void**>(&s->batch_out), off[n]));
         s->batch_out_cap = off[n];
+        fit_arenas(s);
     }
     std::vector<void*> dev(n);
     for (int i = 0; i < n; ++i) dev[i] = s->batch_out + off[i];
@@ -1799,6 +1827,8 @@ int rt_render(rt_scene* s, const rt_camera* cam, int aa, uint8_t* out_rgb, rt_st
         s->out_cap = 0;
         HIP_TRY(hipMalloc(reinterpret_cast<void**>(&s->d_out), bytes));
         s->out_cap = bytes;
+        HIP_TRY(hipDeviceSynchronize());
+        fit_arenas(s);
     }
     const bool count = stats != nullptr;
     if (count) HIP_TRY(hipMemset(s->d_counters, 0, rtc::kCounters * sizeof(unsigned long long)));
@@ -1851,6 +1881,38 @@ int rt_primary_hits(rt_scene* s, const rt_camera* cam, int aa, float* t_out, int
     (void)hipFree(dm);
     if (e != hipSuccess) return fail(RT_ERR_HIP, std::string("primary hits: ") + hipGetErrorName(e));
     return RT_OK;
+}
+
+int rt_primary_hits_production(rt_scene* s, const rt_camera* cam, int aa, float* t_out, int32_t* m_out) {
+    if (!s) return fail(RT_ERR_ARG, "scene is NULL");
+    if (s->host_only) return fail(RT_ERR_NO_DEVICE, "scene was created with RT_OPT_HOST_ONLY");
+    int rc = check_camera(cam, aa);
+    if (rc) return rc;
+    HIP_TRY(hipSetDevice(s->device));
+    const int W = cam->image_width * aa, H = cam->image_height * aa;
+    const size_t n = (size_t)W * H, out_bytes = (size_t)cam->image_width * cam->image_height * 3;
+    char* d = nullptr;             // t, material, then the frame itself
+    HIP_TRY(hipMalloc(reinterpret_cast<void**>(&d), 8 * n + out_bytes));
+    float* dt = reinterpret_cast<float*>(d);
+    int* dm = reinterpret_cast<int*>(d + 4 * n);
+    // unset entries read back as NaN / -1: a sample the production kernels never recorded shows up
+    hipError_t e = hipMemset(d, 0xff, 8 * n);
+    if (e == hipSuccess) {
+        s->dbg_t = dt;
+        s->dbg_m = dm;
+        // the production kernels of one whole frame on this device (rt_render_device's launch sequence; no
+        // sub-frame split, whose virtual ranks would index their own slabs)
+        rc = render_frame(s, cam, aa, cam->image_height, 0, 1, d + 8 * n, nullptr, 0, 0, false);
+        s->dbg_t = nullptr;
+        s->dbg_m = nullptr;
+        e = hipDeviceSynchronize();
+    }
+    if (!rc && e == hipSuccess && t_out) e = hipMemcpy(t_out, dt, n * 4, hipMemcpyDeviceToHost);
+    if (!rc && e == hipSuccess && m_out) e = hipMemcpy(m_out, dm, n * 4, hipMemcpyDeviceToHost);
+    (void)hipFree(d);
+    if (rc) return rc;
+    if (e != hipSuccess) return fail(RT_ERR_HIP, std::string("primary hits (production): ") + hipGetErrorName(e));
+    return check_device_error(s);
 }
 
 int rt_downsample_host(const uint8_t* in, int width, int height, int factor, uint8_t* out) {

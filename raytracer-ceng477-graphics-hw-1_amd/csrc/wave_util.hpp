@@ -70,6 +70,27 @@ __device__ __forceinline__ bool slab_sample_ray(const P& p, unsigned s, Ray* r) 
     return true;
 }
 
+// The internal pixel (frame row, column) whose eye ray slab_sample_ray gives slot s (diagnostics).
+template <class P>
+__device__ __forceinline__ bool slab_sample_pixel(const P& p, unsigned s, int* row, int* col) {
+    const unsigned tile = s >> 6, lane = s & 63;
+    const int tx = (int)(tile % (unsigned)p.tiles_x), ty = (int)(tile / (unsigned)p.tiles_x);
+    const int ix = tx * 8 + (int)(lane & 7);
+    const int iyc = ty * 8 + (int)(lane >> 3);
+    if (ix >= p.wi || iyc >= p.chunk_rows) return false;
+    const int iy = p.chunk_row0 + iyc;
+    int lr = iy / p.aa;
+    const int sub = iy - lr * p.aa;
+    if (lr >= p.slab_rows) return false;
+    batch_frame(p, &lr);
+    const int stripe = lr / p.stripe_rows;
+    const int g = (stripe * p.nranks + p.rank) * p.stripe_rows + (lr - stripe * p.stripe_rows);
+    if (g >= p.height) return false;
+    *row = g * p.aa + sub;
+    *col = ix;
+    return true;
+}
+
 // Does slot s of the chunk hold a sample of this rank's slab (slab_sample_ray's checks)?
 template <class P>
 __device__ __forceinline__ bool slab_slot_valid(const P& p, unsigned s) {

@@ -1,11 +1,15 @@
 """GPU: the bench's own timed configuration, and the workspace budget.
 
 bench.py times C3 (horse_and_mug 1920x1080, depth 6, AA1) as one rank with 4-row
-stripes, 8 hardware queues (6 workspace slots), frame batches with 16-B phase-A
-records, after two 96-frame warm-up calls; the driver runs it with --steps 20, one
-20-frame rt_render_frames_device call that render_cameras deals over the six slots
-(4,4,3,3,3,3 frames; RT_BALANCE=0: round 4's 4,4,4,4,4).  Every frame of that call
-must be the reference's image (raytracer.cpp:505-519 renders each camera once).
+stripes, 8 hardware queues (6 workspace slots), after two 96-frame warm-up calls;
+the driver runs it with --steps 20: one 20-frame rt_render_frames_device call.
+With the defaults its frames go out as greedy frame batches (RT_BALANCE=0:
+min(m, ceil(20 / 6)) = 4 frames each, 4,4,4,4,4 on 5 slots) with full 32-B
+phase-A records (RT_COMPACT=3: a 4-frame C3 AA1 launch fits its slot's share
+with them; compact 16-B records are for frame sizes that do not, such as AA2).
+RT_BALANCE=1 (4,4,3,3,3,3 on 6 slots) is the measured-slower alternative, kept
+under test.  Every frame of that call must be the reference's image
+(raytracer.cpp:505-519 renders each camera once).
 
 RT_WS_BUDGET_MB (rt.h rt_scene_memory) bounds the scene's HBM: the uploaded scene,
 its output staging and every slot's arena; a lone frame's arena follows the frame.
@@ -43,8 +47,10 @@ def test_bench_timed_call_equals_golden(balance, goldens, pkg, scene_dir, torch_
             s.render_frames_device([cam] * 96, 1, [b.data_ptr() for b in bufs], st, stripe_rows=4)
         torch.cuda.synchronize()
         bufs.zero_()
+        before = s.counters_raw()["compact_launches"]
         s.render_frames_device([cam] * 20, 1, [bufs[i].data_ptr() for i in range(20)], st, stripe_rows=4)
         s.check()
+        assert s.counters_raw()["compact_launches"] == before, "the timed call's launches must use full records"
         for i in range(20):
             assert torch.equal(bufs[i], ref), f"frame {i} of the timed call"
         # and the lone frame after it (bench's single_frame)
@@ -72,6 +78,13 @@ def test_workspace_within_budget(goldens, pkg, scene_dir, torch_cuda, monkeypatc
             assert torch.equal(bufs[i], ref), f"frame {i}"
         img, _ = s.render(cam, aa=1)
         assert torch.equal(torch.from_numpy(img).to("cuda:0"), ref)
+        m = s.memory()
+        assert m["scene_bytes"] + m["workspace_bytes"] <= 1024 << 20, m
+        # host-output staging beyond the 64 MB reserve (rt_render_cameras: 16 C3 frames, 100 MB) comes off
+        # the arenas' budget too
+        imgs, _ = s.render_cameras([cam] * 16, aa=1)
+        for i, im in enumerate(imgs):
+            assert torch.equal(torch.from_numpy(im).to("cuda:0"), ref), f"camera frame {i}"
         m = s.memory()
         assert m["scene_bytes"] + m["workspace_bytes"] <= 1024 << 20, m
 

@@ -9,6 +9,10 @@ branch of it and compare with the reference goldens (raytracer.cpp:385-452):
     shaded and folded in k_fallback: tail colours, kEndTail);
   * =2: every shadow ray deferred (the fallback shadow queue);
   * =3: both;
+  * =4: every reflected ray deferred (phase A records level 0, k_fallback
+    walks the rest of each mirror path from level 1; its pinfo write clears
+    the kPathCont bit k_chain set, so k_finish's second loop finishes the
+    pixel -- ADVICE r5);
   * RT_CONT_CB=1000: continuations beyond 1,000 finish in k_fallback;
   * RT_FBS_CAP=64 with =2: the shadow queue overflows (marked occlusion bytes
     scanned by k_fallback);
@@ -38,6 +42,7 @@ ENVS = [
     {"RT_FORCE_FALLBACK": "1"},
     {"RT_FORCE_FALLBACK": "2"},
     {"RT_FORCE_FALLBACK": "3"},
+    {"RT_FORCE_FALLBACK": "4"},
     {"RT_CONT_CB": "1000"},
     # phase-A records with their directions (RT_COMPACT=0, pathchain.hpp dbase = 0): the continuations
     # and k_fallback read the stored direction words instead of the chain's tail copies

@@ -60,14 +60,25 @@ def test_render_bit_exact(name, path, goldens, pkg, scene_dir, torch_cuda):
 
 @pytest.mark.parametrize("name", ["C1_simple_aa1", "C2_cornellbox_800_d0_aa1", "hm_verbatim_aa1",
                                   "C3_hm_1080p_d6_aa1"])
-def test_primary_hit_t(name, goldens, pkg, scene_dir, torch_cuda):
+@pytest.mark.parametrize("walk", ["production", "reference"])
+def test_primary_hit_t(name, walk, goldens, pkg, scene_dir, torch_cuda):
+    """north_star's hit-t bar against the compiled reference's dump (Ray::getFirstIntersection,
+    raytracer.cpp:177-225).  walk="production": the TIMED walk -- one frame through the production kernels,
+    k_chain storing each sample's level-0 tSmall and material where it records its hit (k_fallback for the
+    rays the timed walks defer); "reference": the side kernel's binary-tree walk, a second check."""
     g = golden_by_name(goldens, name)
     z = np.load(GOLDEN_DIR / g["primary_hits"]["file"], allow_pickle=False)
     with pkg.Scene.from_xml(config_path(scene_dir, g["config"]), device=0) as s:
-        t, m = s.primary_hits(s.camera(0), aa=g["aa"])
+        t, m = s.primary_hits(s.camera(0), aa=g["aa"], walk=walk)
+        if walk == "production":       # the dump's frame went through the production kernels' whole sequence
+            s.check()
     ft, fm = t.reshape(-1), m.reshape(-1)
+    assert not np.isnan(ft).any() and (fm >= 0).all(), "a sample's level-0 hit was never recorded"
     assert np.array_equal(fm[z["idx"]], z["material"])
-    assert np.max(np.abs(ft[z["idx"]] - z["t"])) <= T_TOL
+    d = np.abs(ft[z["idx"]] - z["t"])
+    assert np.max(d) <= T_TOL
+    exact = float(np.mean(ft[z["idx"]].view(np.uint32) == z["t"].astype(np.float32).view(np.uint32)))
+    print(f"{name} {walk}: max |dt| {float(np.max(d)):.3g}, bit-exact fraction {exact:.6f} of {len(z['idx'])}")
     # stronger than the bar: the full-frame t array is bit-identical
     assert hashlib.sha256(ft.tobytes()).hexdigest() == g["primary_hits"]["sha256_t"]
     assert hashlib.sha256(fm.tobytes()).hexdigest() == g["primary_hits"]["sha256_material"]

@@ -32,7 +32,7 @@ def test_library_exports_every_declared_symbol(pkg):
         assert hasattr(L, n), n
     bound = {s[0] for s in pkg._SIGS}
     assert set(names) == bound, "ctypes bindings out of sync with rt.h"
-    assert L.rt_abi_version() == 11
+    assert L.rt_abi_version() == 12
 
 
 def test_cli_binary_built(pkg):

@@ -113,7 +113,7 @@ res = {"tag": tag, "mode": mode, "config": trace.get("config", {}).get("workload
                "HBM bytes = 2*FETCH_SIZE + WRITE_SIZE; alg bytes = the traced line's roofline.alg_bytes_per_kernel "
                "(k_occlude = A's + B's shadow walks); achieved = alg bytes / rocprof ms"}
 (prof / f"{tag}_traffic.json").write_text(json.dumps(res, indent=1))
-(prof / f"traffic_{mode}.json").write_text(json.dumps(res, indent=1))
+(prof / (f"traffic_{mode}.json" if res["aa"] == 1 else f"traffic_{mode}_aa{res['aa']}.json")).write_text(json.dumps(res, indent=1))
 with open(prof / f"{tag}_bench.jsonl", "w") as f:
     for l in (trace, full):
         if l:
