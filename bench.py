@@ -21,7 +21,7 @@ Roofline: the walks fetch a small, cache-resident scene, so
 the memory roofline that bounds them is the L2's (MI355X_MICROARCH.md §L2,
 ~34.5 TB/s aggregate), not HBM's.  `achieved` = the bytes the TIMED kernels
 fetch and move per frame -- traversal bytes counted by a production-fetch
-counting pass (RT_COUNT_PROD: the same walks as the timed kernels, counting
+counting pass (RT_DEBUG 0x20: the same walks as the timed kernels, counting
 their node, leaf-record and primitive loads) plus the workspace bytes of the
 chain path (records, task ids, occlusion bytes, output; a per-ray model of
 pathchain.hip) -- divided by the frame's kernel time.  The HBM bytes actually
@@ -80,7 +80,7 @@ def kernel_bytes(r: dict, c: dict, out_pixels: int, batched: bool, nlights: int,
     REC_B = 32
     REC_A = 16 if compact else 32
     DIRW = 16 if REC_A == 16 else 0
-    inplace = batched and os.environ.get("RT_OCC_INPLACE", "1") != "0"   # A's tasks walked where k_chain left them
+    inplace = batched                     # A's tasks walked where k_chain left them (PcParams::occ_inplace)
     samples, skipped = c["primary_rays"], c["shadow_rays_skipped"]
     a_sh, bq, bo, conts = r["a_shadow_rays"], r["bq_shadow_rays"], r["bo_shadow_rays"], r["continuations"]
     shadow_ws = TASK + 16 + NRM + OCC
@@ -153,6 +153,10 @@ def parse():
     ap.add_argument("--trace", action="store_true",
                     help="profiling runs (tools/profile_round.sh): only the counting passes, warmup and timed frames "
                          "run, so per-frame kernel sums from rocprofv3 can be checked against kernel_ms")
+    ap.add_argument("--one-slot", action="store_true",
+                    help="profiling runs: ONE workspace slot with the share of the budget one of the default slots gets "
+                         "(the configuration of the line's kernel_ms_one_slot), so rocprofv3's per-kernel times of "
+                         "this run check the line's per-kernel ones")
     ap.add_argument("--inflight", type=int, default=None,
                     help="frames submitted together (rt_render_frames_device frame batches; 1 = one frame at a "
                          "time; default 96, C5 1: its frames are already 250x larger than one launch's chunk)")
@@ -261,6 +265,18 @@ def main() -> int:
     tmpdir = tempfile.mkdtemp(prefix=f"rtbench{rank}_")
     xml = pkg.scenes.write_config(config, tmpdir)
 
+    def one_slot_env():
+        """RT_SLOTS=1 and the RT_WS_BUDGET_MB that gives that slot the share one of the default slots gets: the
+        scene and the 64 MB staging reserve off the budget, the rest over the slots (rt_api.cpp slot_budget)."""
+        nslots = int(os.environ.get("RT_SLOTS", max(1, min(6, int(os.environ["GPU_MAX_HW_QUEUES"]) - 1))))
+        budget_mb = int(os.environ.get("RT_WS_BUDGET_MB", "16384"))
+        probe = pkg.Scene.from_xml(xml, device=local, render_path=a.path)
+        fixed_mb = (probe.memory()["scene_bytes"] >> 20) + 1 + 64
+        probe.close()
+        return {"RT_SLOTS": "1", "RT_WS_BUDGET_MB": str(max(64, (budget_mb - fixed_mb) // nslots + fixed_mb))}
+
+    if a.one_slot:
+        os.environ.update(one_slot_env())
     t0 = time.perf_counter()
     scene = pkg.Scene.from_xml(xml, device=local, render_path=a.path)
     load_s = time.perf_counter() - t0
@@ -296,17 +312,21 @@ def main() -> int:
     note(f"peaks {({k: round(v) for k, v in peaks.items()})}")
     # Counting passes (not timed).  (1) the reference's exact work (rays, node visits, tests): the
     # metric's ray counts, equal to the reference's counters (parity tests); (2) the production walks'
-    # own fetched bytes (RT_COUNT_PROD: a scene whose counting kernels walk the timed kernels' trees).
+    # own fetched bytes (RT_DEBUG 0x20: a scene whose counting kernels walk the timed kernels' trees).
     scene.counters_reset(sp)
     scene.render_device(cam, aa, slab.data_ptr(), sp, S, rank, world, count=True)
     cnt = scene.counters_read()
     ref_alg_bytes = (cnt["node_visits"] * B_NODE + cnt["tri_tests"] * B_TRI + cnt["sphere_tests"] * B_SPH
                      + rows * W * aa * aa * B_PIX)
-    os.environ["RT_COUNT_PROD"] = "1"
+    dbg0 = os.environ.get("RT_DEBUG")
+    os.environ["RT_DEBUG"] = str(int(dbg0 or "0", 0) | 0x20)
     try:
         pscene = pkg.Scene.from_xml(xml, device=local, render_path=a.path)
     finally:
-        del os.environ["RT_COUNT_PROD"]
+        if dbg0 is None:
+            os.environ.pop("RT_DEBUG", None)
+        else:
+            os.environ["RT_DEBUG"] = dbg0
     pscene.counters_reset(sp)
     pscene.render_device(cam, aa, slab.data_ptr(), sp, S, rank, world, count=True)
     pcnt = pscene.counters_read()
@@ -504,7 +524,7 @@ def main() -> int:
     footprint = scene.memory()
     footprint["total_bytes"] = footprint["scene_bytes"] + footprint["workspace_bytes"]
 
-    # per-kernel device time (rank 0): a scene with RT_KTIME=1 launches each kernel of a chain launch with
+    # per-kernel device time (rank 0): a scene with RT_DEBUG 0x10 launches each kernel of a chain launch with
     # its own start / stop timestamps (hipExtLaunchKernel events: the dispatch's begin and end, as rocprofv3
     # --kernel-trace reports them) on ONE workspace slot (kernels back to back) -- the frame batches of the
     # timed configuration and one frame alone.  The slot's workspace share is the timed run's (the scene
@@ -512,12 +532,9 @@ def main() -> int:
     # frames as the timed run's do
     ktimes = None
     if rank == 0 and a.path == "chain" and not a.trace:
-        nslots = int(os.environ.get("RT_SLOTS", max(1, min(6, int(os.environ["GPU_MAX_HW_QUEUES"]) - 1))))
-        budget_mb = int(os.environ.get("RT_WS_BUDGET_MB", "16384"))
-        fixed_mb = (footprint["scene_bytes"] >> 20) + 1 + 64
-        share_mb = max(64, (budget_mb - fixed_mb) // nslots + fixed_mb)
-        saved = {k: os.environ.get(k) for k in ("RT_KTIME", "RT_SLOTS", "RT_WS_BUDGET_MB")}
-        os.environ.update(RT_KTIME="1", RT_SLOTS="1", RT_WS_BUDGET_MB=str(share_mb))
+        saved = {k: os.environ.get(k) for k in ("RT_DEBUG", "RT_SLOTS", "RT_WS_BUDGET_MB")}
+        os.environ.update(RT_DEBUG=str(int(saved["RT_DEBUG"] or "0", 0) | 0x10),
+                          **(one_slot_env() if not a.one_slot else {}))
         try:
             kscene = pkg.Scene.from_xml(xml, device=local, render_path=a.path)
         finally:
@@ -563,7 +580,7 @@ def main() -> int:
         value = ps_frame * a.steps / elapsed / 1e6
         # priced against the driver-timed wall time per frame (ms_per_step), as the headline is
         achieved = alg_bytes / (ms / 1e3) / 1e9
-        # each kernel's own fraction: its alg bytes per frame / its one-slot time per frame (RT_KTIME),
+        # each kernel's own fraction: its alg bytes per frame / its one-slot time per frame (RT_DEBUG 0x10),
         # against the measured L2 full-line peak (and the divergent-gather ceiling of its fetch shape)
         per_kernel, per_kernel_one, dominant = None, None, None
 

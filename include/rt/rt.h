@@ -290,15 +290,16 @@ int rt_counters_read(rt_scene* scene, rt_stats* stats);   /* synchronises the de
  * CounterSlot): phase-A / phase-B closest-hit walk bytes (or node visits), walks
  * and hits, continuations, and the shadow rays of A, of B's workgroup queue and
  * of B's overflow -- bytes and rays each.  Bytes when the scene was created with
- * RT_COUNT_PROD=1 (the production walks' fetched bytes).  24..29 (every launch,
+ * RT_DEBUG=0x20 (the production walks' fetched bytes).  24..29 (every launch,
  * timed or counting; round 4): chain launches, continuations, continuations
  * beyond the phase-B record space (walked by k_fallback), deferred closest-hit
  * rays, deferred shadow rays, launches whose fallback shadow queue overflowed.
  * 30 (round 5): launches with compact 16-B phase-A records (RT_COMPACT). */
 int rt_counters_read_raw(rt_scene* scene, uint64_t* out, int n);
 /* Diagnostics (ABI 7): per-kernel device time of the chain path's launches
- * since the last reset, for a scene created with env RT_KTIME=1 (events between
- * the kernels of each launch; each launch then synchronises).  ms[k] for k =
+ * since the last reset, for a scene created with env RT_DEBUG=0x10 (each kernel's
+ * own dispatch start / end timestamps, as rocprofv3 reports them -- ABI 12; each
+ * launch then synchronises).  ms[k] for k =
  * k_chain, k_pack_a, k_mix, k_occlude (A's shadows, frame batches), k_pack_b,
  * k_occlude (B's overflow), k_finish, k_fallback.  Returns the launches timed. */
 int rt_kernel_times(rt_scene* scene, double* ms, int n, int reset);

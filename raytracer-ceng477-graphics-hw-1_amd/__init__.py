@@ -440,7 +440,7 @@ class Scene:
     KERNEL_KINDS = ("k_chain", "k_pack_a", "k_mix", "k_occlude_a", "k_pack_b", "k_occlude_b", "k_finish", "k_fallback")
 
     def kernel_times(self, reset: bool = True) -> tuple[dict, int]:
-        """rt_kernel_times (RT_KTIME=1 scenes): ms per kernel of the chain launches, and the launch count."""
+        """rt_kernel_times (scenes created with RT_DEBUG 0x10): ms per kernel of the chain launches, and the launch count."""
         ms = np.zeros(16, dtype=np.float64)
         n = lib().rt_kernel_times(self._h, ms.ctypes.data_as(ctypes.c_void_p), 16, int(reset))
         if n < 0:

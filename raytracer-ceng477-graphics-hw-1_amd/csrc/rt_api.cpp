@@ -27,6 +27,17 @@ namespace {
 thread_local std::string g_err;
 std::atomic<int> g_devices{0};          // rt_set_devices: device group of scenes created afterwards (0: none)
 
+// RT_DEBUG: diagnostics and measurement modes, one bit mask (read when used, so a caller may change it between
+// scenes): 0x01 log the start-up phases (tools/exp_cli.py --phases), 0x02 log workspace growths, 0x04 log each
+// frame batch's submission and GPU span (makes batched calls synchronous), 0x08 no device warm-up thread,
+// 0x10 per-kernel times of chain launches (scenes created with it: rt_kernel_times), 0x20 production-fetch
+// counting passes (scenes created with it count the bytes the timed walks fetch: bench.py roofline).
+enum : int { kDbgLogInit = 1, kDbgLogAlloc = 2, kDbgLogSubmit = 4, kDbgNoWarmup = 8, kDbgKtime = 16, kDbgCountProd = 32 };
+int debug_flags() {
+    const char* e = std::getenv("RT_DEBUG");
+    return e ? (int)std::strtol(e, nullptr, 0) : 0;
+}
+
 int fail(int code, const std::string& msg) {
     g_err = msg;
     return code;
@@ -105,62 +116,38 @@ struct rt_scene {
     dl::LeafBig* d_leafbig = nullptr;
     int num_cus = 256;
     int chain_grid = 0, occl_grid = 0, mix_grid = 0;   // resident-sized persistent grids (lazily queried)
-    int tune_refill = -1;       // RT_REFILL (-1: path default)
-    int tune_service = -1;      // RT_SERVICE (-1: path default)
-    int tune_orefill = 32;      // RT_OREFILL
-    int tune_brefill = 32;      // RT_BREFILL
-    int tune_bprio = 1;         // RT_BPRIO
-    // Task chunks: tasks c*ch .. c*ch+ch-1 go to workgroup c mod G.  Shadow tasks (uniform cost,
-    // neighbouring rays toward one light) gain from coherent chunks: C3 batched 0.80 -> 0.685 ms/frame
-    // at 128, single-frame 1.18 -> 1.11-1.15 ms.  Continuations (the mug's clustered mirror chains)
-    // gain from chunks only when other frames hide the tail: 128 gives batches 0.685 -> 0.650 ms/frame
-    // but a lone frame 1.15 -> 1.36 ms, so a lone frame keeps fine interleaving.
-    int tune_tchunk = 0;        // RT_TCHUNK (0: 128 for frame batches, 1 for one frame)
-    int tune_ochunk = 0;        // RT_OCHUNK (0: 256 in frame batches, 128 in lone frames -- 41-frame medians
-                                // 0.8776 against 0.8826 ms, three interleaved rounds, profiles/r05_lone_knobs.txt)
-    int tune_kinline = 1;       // RT_KINLINE: deepest level of phase A
-    // RT_CHUNK_SAMPLES: samples per chain-path launch (chunk / frame batch).  Bigger launches leave
-    // fewer tails per sample: C3 batches 4 M 0.72, 8 M 0.66, 16 M 0.63, 32 M 0.59 ms/frame; C5 8 M
-    // 159.6, 16 M 147.4, 32 M 140.6 ms/frame.  32 M samples = 15 GB of workspace per slot (C3).
-    size_t chunk_samples = size_t(32) << 20;
-    int tune_batch = 32;        // RT_BATCH: frames per batched launch (rt_render_frames/cameras; 1 = off)
+    // Scheduling constants (the measured defaults of DESIGN.md §7; the knobs that varied them were removed in
+    // round 6 with the settings measured slower).  Task chunks: tasks c*ch .. c*ch+ch-1 go to workgroup c mod G
+    // -- continuations in chunks of 128 in frame batches, one at a time in a lone frame (its clustered mirror
+    // chains spread over every workgroup: a lone frame 1.36 -> 1.15 ms), shadow tasks in chunks of 256 in
+    // frame batches and 128 in lone frames (0.8826 -> 0.8776 ms, profiles/r05_lone_knobs.txt).
+    static constexpr int kKinline = 1;           // deepest level of phase A
+    // samples per chain-path launch at most (bigger launches leave fewer tails per sample: C3 batches 4 M 0.72,
+    // 8 M 0.66, 16 M 0.63, 32 M 0.59 ms/frame); the workspace budget usually binds first
+    static constexpr size_t kChunkSamples = size_t(32) << 20;
+    static constexpr int kContDen = 6;           // phase-B records for at least cap / 6 continuations (C3: ~9 %)
+    int tune_orefill = 32;      // RT_OREFILL (tests: the leaf-queue walker's refill threshold)
+    int tune_lq_wait = 32;      // RT_LQ_WAIT (tests: the leaf-queue flush threshold)
     long long tune_batch_samples = 1ll << 21;   // RT_BATCH_SAMPLES: a multi-frame call's batches hold at least ~this
                                                 // many samples each (fewer batches than slots for small frames)
-    bool tune_balance = false;  // RT_BALANCE=1: a call's frames dealt evenly over every slot (render_cameras; 20-frame
-                                // calls, 4 same-box runs each: 0.4316 ms/frame against 0.4221 for the greedy batches)
     int tune_slots = 3;         // RT_SLOTS: frame batches in flight together (workspace slots, <= kSlots;
                                 // default GPU_MAX_HW_QUEUES - 1)
-    int tune_fgrid = 0;         // RT_FGRID: k_finish workgroups at most (0: 8 per CU; its waves are dispatch-bound
-                                // at a lane per pixel: 0.515 -> 0.49 ms per batched frame)
-    int tune_gb = 0;            // RT_GB: phase-B chain workgroups in k_mix (0: 1.875 per CU for a lone frame, 1.5 for batches)
-    int tune_gb_b = 0;          // RT_GB_B: the same for frame batches only (0: 1.5 per CU)
     int tune_bq_cap = 1 << 30;  // RT_BQ_CAP: phase-B shadow queue slots (tests force the k_occlude spill path)
-    int tune_bservice = 64;     // RT_BSERVICE: phase-B waves service finished walks once this many lanes are done
     int tune_hot_units = 1;     // RT_HOT_UNITS: lone frames deal phase-A units heaviest-first by the previous frame's steps
-    int tune_occ_inplace = 1;   // RT_OCC_INPLACE: A's shadow tasks read in their regions by k_occlude in frame
-                                // batches, and B's LDS-queue overflow in lone frames (0: packed)
     int tune_compact = 3;       // RT_COMPACT: phase-A records without directions (16 B instead of 32): 1 frame batches,
                                 // 2 every launch, 0 none, 3 (round 5) frame batches only where full records would leave
                                 // fewer than 4 frames per launch (full_records_fit; C3 AA1 20-frame calls 0.4151 -> 0.4040
                                 // ms/frame with full records, 96-frame calls -0.4 %; profiles/r05_ab_compact.txt)
-    int tune_btail = 64;        // RT_BTAIL: the same once the continuations are exhausted (1: 1.24, 4: 1.18, 16: 1.15, 64: 1.14 ms)
-    int tune_dyn = 1;           // RT_DYN_UNITS: phase-A waves take sample units from a launch-wide counter
-    int tune_ublk_h = -1, tune_ublk_w = 8;  // RT_UBLK_H / RT_UBLK_W: phase-A unit column blocks (unit_order;
-                                            // H -1: a frame high, 0: row-major units)
-    int tune_split = 1;         // RT_SPLIT: a frame runs as this many concurrent interleaved sub-frames (2: +8%, 3: +18% on C3)
     // RT_WS_BUDGET_MB: HBM for the scene on its device -- the uploaded scene, a 64 MB reserve for output
     // staging, and the chain-path workspace arenas of all slots together, each slot's arena (headroom
     // included) within an even share of the rest.  A launch's arena is sized for the worst case (every
     // sample recording every level), so the budget bounds the samples per launch (and the frames per frame
     // batch).  A lone frame's arena follows the frame (chain_launch_units), not the share.
     size_t ws_budget = size_t(16) << 30;
-    // RT_CONT_DEN: phase-B records for cap / den continuations per launch (C3: ~9 % of the samples
-    // continue; the rest, if any, finish in k_fallback); 1 = every sample
-    int tune_cont_den = 6;
     int tune_cont_cb = 0;       // RT_CONT_CB (tests): exactly this many (k_fallback finishes the rest)
     int tune_fbs_cap = 0;       // RT_FBS_CAP (tests): k_fallback shadow-queue slots (0: one per sample)
     size_t scene_bytes = 0;     // device bytes of the uploaded scene (trees, primitives, tables)
-    bool ktime = false;         // RT_KTIME: per-kernel times of chain launches (rt_kernel_times; syncs each launch)
+    bool ktime = false;         // RT_DEBUG 0x10: per-kernel times of chain launches (rt_kernel_times; syncs each launch)
     double kt_ms[rtc::kKKinds] = {};
     long long kt_launches = 0;
     rtc::KTimer kt;
@@ -196,7 +183,7 @@ struct rt_scene {
     // continuation share of frame batches (phase B's record space, cb): each batched launch copies its
     // continuation count (k_pack_a's total) to pinned memory behind it; once that copy is done the share
     // is folded into cont_frac, which sizes the next launches' cb (and so their frames per launch)
-    double cont_frac = 0;                      // 0: none seen yet (cap / tune_cont_den)
+    double cont_frac = 0;                      // 0: none seen yet (cap / kContDen)
     unsigned* h_cont = nullptr;                // pinned, per slot
     unsigned* d_cont_peak = nullptr;           // a frame of several chunks: its chunks' most continuations
     hipEvent_t cont_ev[kSlots] = {};
@@ -256,7 +243,7 @@ int upload_scene(rt_scene* s, const rt_options* opts);
 // The process's first scene: HIP's runtime and device initialisation (~0.25 s on the GPU box: runtime,
 // device context, the kernels' code objects) runs on a helper thread while this thread reads the XML
 // and builds the trees on the host, and is joined before the upload (a drop-in caller's first frame no
-// longer pays both in sequence).  RT_NO_WARMUP=1 disables it (A/B).
+// longer pays both in sequence).  RT_DEBUG 0x08 disables it (A/B).
 std::mutex g_warm_mu;
 std::future<void> g_warm, g_warm2;
 bool g_warm_started = false;
@@ -266,15 +253,15 @@ bool g_warm_started = false;
 // on the caller's thread first (a one-process-per-GPU caller passing -1 got an extra context
 // and code-object load on GPU 0 in every rank).
 void start_device_warmup(const rt_options* opts) {
-    if ((opts && (opts->flags & RT_OPT_HOST_ONLY)) || std::getenv("RT_NO_WARMUP")) return;
+    if ((opts && (opts->flags & RT_OPT_HOST_ONLY)) || (debug_flags() & kDbgNoWarmup)) return;
     const int want = g_devices.load() >= 1 ? 0 : (opts ? opts->device : -1);
     if (want < 0) return;
     std::lock_guard<std::mutex> lk(g_warm_mu);
     if (g_warm_started) return;
     g_warm_started = true;
     g_warm = std::async(std::launch::async, [want] {
-        // RT_LOG_INIT=1 (diagnostics, tools/exp_cli.py --phases): the warm-up's steps on the steady clock, ms
-        const bool log = std::getenv("RT_LOG_INIT") != nullptr;
+        // RT_DEBUG 0x01 (tools/exp_cli.py --phases): the warm-up's steps on the steady clock, ms
+        const bool log = (debug_flags() & kDbgLogInit) != 0;
         auto now = [] { return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now().time_since_epoch()).count(); };
         const double t0 = log ? now() : 0.0;
         int n = 0;
@@ -291,8 +278,7 @@ void start_device_warmup(const rt_options* opts) {
             int a = 0, b = 0, c = 0;
             (void)rtc::chain_occupancy(&a, &b, &c);
             const double t3 = log ? now() : 0.0;
-            size_t wb = 1u << 20;
-            if (const char* e = std::getenv("RT_WARM_BYTES")) wb = (size_t)std::max(256L, std::atol(e));
+            const size_t wb = 1u << 20;
             void* d = nullptr;
             std::vector<unsigned char> h(wb);
             if (hipMalloc(&d, wb) == hipSuccess) {
@@ -460,15 +446,8 @@ int upload_rest(rt_scene* s, const rt_options* opts) {
         HIP_TRY(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, s->device));
         s->num_cus = std::max(1, cus);
     }
-    if (const char* e = std::getenv("RT_REFILL")) s->tune_refill = std::max(0, std::min(63, std::atoi(e)));
-    if (const char* e = std::getenv("RT_SERVICE")) s->tune_service = std::max(1, std::min(64, std::atoi(e)));
-    if (const char* e = std::getenv("RT_TCHUNK")) s->tune_tchunk = std::max(1, std::min(4096, std::atoi(e)));
-    if (const char* e = std::getenv("RT_OCHUNK")) s->tune_ochunk = std::max(0, std::min(4096, std::atoi(e)));
-    if (const char* e = std::getenv("RT_BPRIO")) s->tune_bprio = std::atoi(e) != 0;
-    if (const char* e = std::getenv("RT_BREFILL")) s->tune_brefill = std::max(0, std::min(63, std::atoi(e)));
     if (const char* e = std::getenv("RT_OREFILL")) s->tune_orefill = std::max(0, std::min(63, std::atoi(e)));
-    if (const char* e = std::getenv("RT_BATCH")) s->tune_batch = std::max(1, std::atoi(e));
-    if (const char* e = std::getenv("RT_BALANCE")) s->tune_balance = std::atoi(e) != 0;
+    if (const char* e = std::getenv("RT_LQ_WAIT")) s->tune_lq_wait = std::max(1, std::min(64, std::atoi(e)));
     if (const char* e = std::getenv("RT_BATCH_SAMPLES")) s->tune_batch_samples = std::max(1ll, std::atoll(e));
     // frame batches in flight: one HIP stream each beside the caller's; HIP multiplexes streams beyond
     // GPU_MAX_HW_QUEUES hardware queues (4 by default) onto the same queues, which serialises them
@@ -479,25 +458,12 @@ int upload_rest(rt_scene* s, const rt_options* opts) {
         s->tune_slots = std::max(1, std::min(rt_scene::kSlots, (hwq > 0 ? hwq : 4) - 1));
     }
     if (const char* e = std::getenv("RT_SLOTS")) s->tune_slots = std::max(1, std::atoi(e));
-    if (const char* e = std::getenv("RT_CHUNK_SAMPLES"))
-        s->chunk_samples = std::max<size_t>(4096, std::min<size_t>(size_t(1) << 26, std::strtoull(e, nullptr, 10)));
-    if (const char* e = std::getenv("RT_KINLINE")) s->tune_kinline = std::max(0, std::atoi(e));
-    if (const char* e = std::getenv("RT_GB")) s->tune_gb = std::max(0, std::atoi(e));
-    if (const char* e = std::getenv("RT_GB_B")) s->tune_gb_b = std::max(0, std::atoi(e));
-    if (const char* e = std::getenv("RT_FGRID")) s->tune_fgrid = std::max(0, std::atoi(e));
     if (const char* e = std::getenv("RT_BQ_CAP")) s->tune_bq_cap = std::max(0, std::atoi(e));
-    if (const char* e = std::getenv("RT_BSERVICE")) s->tune_bservice = std::max(1, std::min(64, std::atoi(e)));
-    if (const char* e = std::getenv("RT_BTAIL")) s->tune_btail = std::max(1, std::min(64, std::atoi(e)));
     if (const char* e = std::getenv("RT_COMPACT")) s->tune_compact = std::max(0, std::min(3, std::atoi(e)));
-    if (const char* e = std::getenv("RT_OCC_INPLACE")) s->tune_occ_inplace = std::atoi(e) != 0;
     if (const char* e = std::getenv("RT_HOT_UNITS")) s->tune_hot_units = std::atoi(e) != 0;
-    if (const char* e = std::getenv("RT_SPLIT")) s->tune_split = std::max(1, std::atoi(e));
-    if (const char* e = std::getenv("RT_DYN_UNITS")) s->tune_dyn = std::atoi(e) != 0;
-    if (const char* e = std::getenv("RT_UBLK_H")) s->tune_ublk_h = std::max(-1, std::atoi(e));
-    if (const char* e = std::getenv("RT_UBLK_W")) s->tune_ublk_w = std::max(1, std::atoi(e));
     if (const char* e = std::getenv("RT_TRACE")) s->trace_file = e;
-    s->ktime = std::getenv("RT_KTIME") && std::atoi(std::getenv("RT_KTIME")) != 0;
-    if (const char* e = std::getenv("RT_CONT_DEN")) s->tune_cont_den = std::max(1, std::atoi(e));
+    const int dbg = debug_flags();
+    s->ktime = (dbg & kDbgKtime) != 0;
     if (const char* e = std::getenv("RT_CONT_CB")) s->tune_cont_cb = std::max(0, std::atoi(e));
     if (const char* e = std::getenv("RT_FBS_CAP")) s->tune_fbs_cap = std::max(0, std::atoi(e));
     if (const char* e = std::getenv("RT_WS_BUDGET_MB"))
@@ -531,17 +497,16 @@ int upload_rest(rt_scene* s, const rt_options* opts) {
     d.swroot = s->bvh.swroot;
     // occlusion tree for NaN-free shadow rays: 2 = 4-wide quantized form, 1 = binary, 0 = off (RT_STREE)
     d.use_stree = !s->bvh.swnodes.empty() ? 2 : (s->bvh.spairs.empty() ? 0 : 1);
-    if (const char* e = std::getenv("RT_STREE")) {
-        const int v = std::atoi(e);
-        d.use_stree = v <= 0 ? 0 : (v >= 2 && !s->bvh.swnodes.empty() ? 2 : (s->bvh.spairs.empty() ? 0 : 1));
-    }
-    // closest-hit walks of NaN-free rays: the reference tree's wide form, reference order (RT_WIDE_WALK=0: the
-    // binary form)
+    // closest-hit walks of NaN-free rays: the reference tree's wide form, reference order (tests, RT_WIDE_WALK=0:
+    // the binary forms of both trees, every walk in k_fallback)
     d.wnodes = s->d_wnodes;
     d.wroot = s->bvh.wroot;
     d.use_wide = !s->bvh.nodes.empty() && !s->bvh.lrec.empty() &&
                  (!s->bvh.wnodes.empty() || (s->bvh.root_info < 0 && s->bvh.root_lrec >= 0));
-    if (const char* e = std::getenv("RT_WIDE_WALK")) d.use_wide = d.use_wide && std::atoi(e) != 0;
+    if (const char* e = std::getenv("RT_WIDE_WALK"); e && std::atoi(e) == 0) {
+        d.use_wide = 0;
+        d.use_stree = s->bvh.spairs.empty() ? 0 : 1;
+    }
     d.err = s->d_err;
     {   // walk_runaway: 64 x (every node of the largest tree + leaves); RT_WALK_CAP overrides (tests)
         const long long nodes = (long long)s->bvh.pairs.size() + s->bvh.leaves + 64;   // the largest tree
@@ -552,18 +517,16 @@ int upload_rest(rt_scene* s, const rt_options* opts) {
     // longest legitimate wait: one walk of at most nodes + leaves steps); RT_SPIN_CAP overrides (tests)
     d.spin_cap = 1 << 24;
     if (const char* e = std::getenv("RT_SPIN_CAP")) d.spin_cap = std::max(0, std::atoi(e));   // 0: every wait gives up
-    d.leaf_wait = 24;   // measured: 0 1.20, 8 1.19, 16-32 1.166, 48 1.22, 64 1.46 ms (C3)
-    if (const char* e = std::getenv("RT_LEAF_WAIT")) d.leaf_wait = std::max(0, std::min(64, std::atoi(e)));
+    d.leaf_wait = 24;   // measured: 0 1.20, 8 1.19, 16-32 1.166, 48 1.22, 64 1.46 ms (C3; round 6 at HEAD: 0 / 16 +4 / +3 %)
     d.leaf_wait_any = d.leaf_wait;
-    if (const char* e = std::getenv("RT_LEAF_WAIT_ANY")) d.leaf_wait_any = std::max(0, std::min(64, std::atoi(e)));
     // shadow rays of lights behind the surface add +-0 when kd is finite (pathchain.hip light_needed)
     d.cull_shadows = 1;
     for (const auto& m : s->host.materials)
         if (!std::isfinite(m.diffuse.x) || !std::isfinite(m.diffuse.y) || !std::isfinite(m.diffuse.z)) d.cull_shadows = 0;
     if (const char* e = std::getenv("RT_CULL")) d.cull_shadows = d.cull_shadows && std::atoi(e) != 0;
-    d.force_fb = std::getenv("RT_FORCE_FALLBACK") ? std::atoi(std::getenv("RT_FORCE_FALLBACK")) : 0;
-    // measurement: counting passes walk the production trees and count fetched bytes (bench.py)
-    d.count_prod = std::getenv("RT_COUNT_PROD") ? 1 : 0;
+    if (const char* e = std::getenv("RT_FORCE_FALLBACK")) d.force_fb = std::atoi(e);
+    // measurement (RT_DEBUG 0x20): counting passes walk the production trees and count fetched bytes (bench.py)
+    d.count_prod = (dbg & kDbgCountProd) ? 1 : 0;
     return RT_OK;
 }
 
@@ -599,7 +562,6 @@ int check_camera(const rt_camera* cam, int aa) {
     return RT_OK;
 }
 
-constexpr long long kSplitMinSamples = 1 << 19;      // smaller frames are not split into sub-frames
 
 // RT_TRACE diagnostics: a device buffer of n u32 and, after the frame, a raw
 // dump {magic, path, a, b, n, payload...} (see tools/trace_report.py).
@@ -694,9 +656,6 @@ int ensure_chain_grids(rt_scene* s) {
     s->chain_grid = std::min(rtc::kMaxChainGrid, std::max(1, cb) * s->num_cus);
     s->mix_grid = std::max(1, mb) * s->num_cus;
     s->occl_grid = std::max(1, ob) * s->num_cus;
-    if (const char* e = std::getenv("RT_CGRID")) s->chain_grid = std::max(1, std::min(rtc::kMaxChainGrid, std::atoi(e)));
-    if (const char* e = std::getenv("RT_OGRID")) s->occl_grid = std::max(1, std::atoi(e));
-    if (const char* e = std::getenv("RT_MGRID")) s->mix_grid = std::max(2, std::atoi(e));
     return RT_OK;
 }
 
@@ -727,7 +686,7 @@ ChainPlan chain_plan(const rt_scene* s, const ChainGeom& g, size_t nunits, bool 
     const size_t cap = P.cap;
     P.G = std::max(1, std::min(max_grid, (int)((std::min<size_t>(cap, INT32_MAX) + 255) / 256)));
     // phase split: A walks levels [0, kinline], B the rest (k_mix chain role, gb workgroups)
-    P.kinline = std::max(0, s->tune_kinline);
+    P.kinline = rt_scene::kKinline;
     P.phase_b = P.kinline < s->dev.max_depth;
     // phase-B workgroups: a lone frame's deep chains are its critical path (1.875 per CU best since
     // round 3: C3 one frame, 61-frame medians, 1.5625 0.946-0.948, 1.72 0.940, 1.875 0.925-0.935,
@@ -736,31 +695,29 @@ ChainPlan chain_plan(const rt_scene* s, const ChainGeom& g, size_t nunits, bool 
     // 0.550 ms/frame, 0.75 0.552, 1 0.554, 1.25 0.557, 1.5625 0.568)
     // frame batches: A's shadow rays in their own 5-wave k_occlude launch (split_occ) and (round 3) 1 phase-B
     // workgroup per CU (6 slots in flight: 0.504-0.512 -> 0.495 ms/frame; 0.5 per CU 0.500, 2 0.4995)
-    P.split_occ = g.nframes > 1 && (!std::getenv("RT_SPLIT_OCC") || std::atoi(std::getenv("RT_SPLIT_OCC")));
+    P.split_occ = g.nframes > 1;
     // (round 5, the driver's 20-frame call on 5 slots: 1.5 per CU 0.4175 against 1 per CU 0.4282 ms/frame, three
     // interleaved same-box rounds, 96-frame calls +-0; profiles/r05_ab_gb.txt)
-    const int gb_default = g.nframes > 1 ? (s->tune_gb_b > 0 ? s->tune_gb_b : P.split_occ ? 3 * s->num_cus / 2 : s->num_cus / 2)
-                                         : 30 * s->num_cus / 16;
-    P.gb = P.phase_b ? std::max(1, std::min(s->mix_grid - 1, s->tune_gb > 0 ? s->tune_gb : gb_default)) : 0;
+    const int gb_default = g.nframes > 1 ? 3 * s->num_cus / 2 : 30 * s->num_cus / 16;
+    P.gb = P.phase_b ? std::max(1, std::min(s->mix_grid - 1, gb_default)) : 0;
     P.levels_a = std::min(P.kinline, std::max(s->dev.max_depth, 0)) + 1;
     // dynamic phase-A units: a workgroup may take up to twice its static share (at most
     // rtc::kDynUnits), and its queues are sized for that
     const unsigned share = rtc::chain_block_units((int)std::min<size_t>(cap, INT32_MAX), P.G);
-    P.dyn_units = s->tune_dyn && share <= (unsigned)rtc::kDynUnits ? std::min(2u * share, (unsigned)rtc::kDynUnits) : 0u;
+    P.dyn_units = share <= (unsigned)rtc::kDynUnits ? std::min(2u * share, (unsigned)rtc::kDynUnits) : 0u;
     const unsigned units_a = P.dyn_units ? P.dyn_units : share;
     P.scapA = units_a * 256u * (unsigned)(P.levels_a * nl);
     P.ccapA = units_a * 256u;
     // records: levels [0, la) for every sample; deeper ones (phase B) for the first cb continuations
     // (the rest finish in k_fallback; counting passes keep every one: cb = cap)
     P.la = !P.phase_b ? levels : P.levels_a;
-    // (at least cap / RT_CONT_DEN, more once frame batches report a larger continuation share: that share
-    // + 10 %)
-    const size_t cb_guess = std::max(cap / (size_t)std::max(1, s->tune_cont_den),
+    // (at least cap / kContDen, more once frame batches report a larger continuation share: that share + 10 %)
+    const size_t cb_guess = std::max(cap / (size_t)rt_scene::kContDen,
                                      use_share ? (size_t)((double)cap * std::min(1.0, s->cont_frac * 1.1 + 0.005)) : 0);
     P.cb = P.la >= levels ? 0 : (count ? cap : std::min(cap, std::max(cb_guess, std::min<size_t>(cap, 65536))));
     if (cb_want > 0 && !count && P.la < levels) P.cb = std::min(cap, std::max(P.cb, cb_want));
     if (s->tune_cont_cb > 0 && !count && P.la < levels) P.cb = std::min(cap, (size_t)s->tune_cont_cb);
-    P.tchunk = s->tune_tchunk > 0 ? s->tune_tchunk : (g.nframes > 1 ? 128 : 1);
+    P.tchunk = g.nframes > 1 ? 128 : 1;
     {   // a phase-B workgroup's continuations: at most ceil(chunks / gb) chunks of tchunk (chunk_count)
         const size_t ch = (size_t)P.tchunk, nch = (P.cb + ch - 1) / ch;
         const size_t per_wg = P.gb > 0 ? (nch + P.gb - 1) / P.gb * ch : 0;
@@ -798,12 +755,12 @@ ChainPlan chain_plan(const rt_scene* s, const ChainGeom& g, size_t nunits, bool 
     return P;
 }
 
-// Row units of one launch: as many as the chunk target (RT_CHUNK_SAMPLES), the u32 task ids and the
+// Row units of one launch: as many as the chunk target (kChunkSamples), the u32 task ids and the
 // slot's share of the workspace budget (RT_WS_BUDGET_MB over the slots) allow -- the largest count
 // whose chain_plan arena fits the budget (at least one unit, whatever its size).
 size_t chain_launch_units(rt_scene* s, const ChainGeom& g, bool count, size_t* cb_out = nullptr) {
     const size_t id_limit = (size_t)(INT32_MAX - 1) / ((size_t)g.levels * g.nl);   // u32 task owner ids (pathchain.hpp)
-    size_t units = std::min(g.units_total, std::max<size_t>(1, std::min(s->chunk_samples, id_limit) / g.unit_samples));
+    size_t units = std::min(g.units_total, std::max<size_t>(1, std::min(rt_scene::kChunkSamples, id_limit) / g.unit_samples));
     const size_t budget = s->slot_budget();
     if (chain_plan(s, g, units, count).bytes > budget) {
         size_t lo = 1, hi = units;                 // largest units in [1, units] whose arena fits the budget
@@ -921,7 +878,7 @@ int render_chain(rt_scene* s, const rtk::Eye& eye, const rtk::FrameParams& f, bo
     // order this use after the arena's previous one (possibly on another stream)
     if (arena.last && arena.last_stream != st) HIP_TRY(hipStreamWaitEvent(st, arena.last, 0));
     if (arena.bytes < P.bytes) {
-        const bool log_alloc = std::getenv("RT_LOG_ALLOC") != nullptr;   // diagnostics: a growth inside a timed
+        const bool log_alloc = (debug_flags() & kDbgLogAlloc) != 0;   // diagnostics: a growth inside a timed
         const auto ta = std::chrono::steady_clock::now();                // region serialises it
         if (log_alloc)
             std::fprintf(stderr, "librt_hip: slot %d workspace %.1f -> %.1f MB (frames %d, cb %zu of %zu)\n", slot,
@@ -972,33 +929,36 @@ int render_chain(rt_scene* s, const rtk::Eye& eye, const rtk::FrameParams& f, bo
     p.gb = P.gb;
     p.ogrid = P.phase_b ? std::max(1, s->mix_grid - P.gb) : s->mix_grid;
     p.occ_grid = s->occl_grid;
-    p.fin_grid = s->tune_fgrid > 0 ? s->tune_fgrid : 8 * s->num_cus;
+    p.fin_grid = 8 * s->num_cus;        // k_finish: at most 8 workgroups per CU (dispatch-bound at a lane per pixel)
     p.split_occ = P.split_occ ? 1 : 0;
     // A's shadow tasks walked where k_chain left them by k_occlude in frame batches (a lone frame's k_mix
     // shadow role deals them packed: in place, its uneven regions cost k_mix +60 us, k_pack_a -10); B's
     // LDS-queue overflow likewise in a lone frame.  The in-place walks are the leaf-queue walker's
     // (RT_LEAF_QUEUE builds), the only device code that reads task regions unpacked.
-    p.occ_inplace = RT_LEAF_QUEUE && !count && P.split_occ && s->tune_occ_inplace ? 1 : 0;
-    p.occ_inplace_b = RT_LEAF_QUEUE && !P.split_occ && !count && s->tune_occ_inplace ? 1 : 0;
+    p.occ_inplace = RT_LEAF_QUEUE && !count && P.split_occ ? 1 : 0;
+    p.occ_inplace_b = RT_LEAF_QUEUE && !P.split_occ && !count ? 1 : 0;
     p.cont_peak = peak ? s->d_cont_peak : nullptr;
     p.dbg_t = count ? nullptr : s->dbg_t;
     p.dbg_m = count ? nullptr : s->dbg_m;
-    p.refill = s->tune_refill >= 0 ? s->tune_refill : 0;
-    p.service = s->tune_service >= 0 ? s->tune_service : 64;
-    p.bservice = s->tune_bservice;
-    p.btail = s->tune_btail;
+    // wave service policy (pathchain.hpp PcParams; round 6 re-sweep at HEAD, every other setting +-0.5 % or slower:
+    // profiles/r06_lone_knob_resweep.jsonl): phase A refills a wave once all its lanes are idle and services it once
+    // all are done; phase B refills once <= 32 lanes walk and services once all 64 are done, at top priority
+    p.refill = 0;
+    p.service = 64;
+    p.bservice = 64;
+    p.btail = 64;
     p.bq_cap = std::min(s->tune_bq_cap, rtc::kMaxBq);
     p.orefill = s->tune_orefill;
-    p.brefill = s->tune_brefill;
-    p.bprio = s->tune_bprio;
+    p.brefill = 32;
+    p.bprio = 1;
     // continuations dealt one at a time round-robin for a lone frame (its deep chains spread over
     // the phase-B workgroups: 1.12 -> 1.10 ms; 2: 1.11-1.14, 4: 1.12-1.13), in chunks of 128 in batches
     p.tchunk = P.tchunk;
-    p.ochunk = s->tune_ochunk > 0 ? s->tune_ochunk : P.split_occ ? 256 : 128;
-    p.lq_wait = std::getenv("RT_LQ_WAIT") ? std::max(1, std::min(64, std::atoi(std::getenv("RT_LQ_WAIT")))) : 32;
+    p.ochunk = P.split_occ ? 256 : 128;
+    p.lq_wait = s->tune_lq_wait;
     p.dyn_units = (int)P.dyn_units;
-    p.ublk_h = s->tune_ublk_h;
-    p.ublk_w = std::max(1, s->tune_ublk_w);
+    p.ublk_h = -1;                      // phase-A units in column blocks a frame high and 8 units (2,048 px) wide
+    p.ublk_w = 8;
     p.out = f.out; p.counters = f.counters;
     p.out_k = f.out_k; p.out_j = f.out_j;
     p.nframes = std::max(1, f.nframes);
@@ -1016,7 +976,7 @@ int render_chain(rt_scene* s, const rtk::Eye& eye, const rtk::FrameParams& f, bo
     // lone frames in one launch (a drop-in caller's repeated frames): phase-A units heaviest-first by the
     // previous frame of the same geometry (PcParams::uorder), and this frame's costs ranked for the next
     const bool hot = s->tune_hot_units && !count && p.nframes == 1 && P.dyn_units > 0 &&
-                     units == g.units_total && !p.trace;
+                     units == g.units_total;
     p.urank = p.uorder_on = 0;
     for (int r0 = f.chunk_j * chunk_rows; r0 < li; r0 += f.chunk_k * chunk_rows) {
         p.chunk_row0 = r0;
@@ -1290,41 +1250,12 @@ int rt_slab_rows(int height, int stripe_rows, int nranks) {
 }  // extern "C"
 
 namespace {
-// A frame split into K interleaved sub-frames rendered concurrently, sub-frame
-// j on slot j (its own stream and workspace), forked from and joined back into
-// `stream`.  Sub-frame j is virtual rank rank + j*N of N*K (stripe g of rank r
-// is stripe g*K + j... of the rank's slab, pathchain.hip out_row), so it writes
-// its pixels straight into the caller's slab.  One sub-frame's tail (its few
-// long mirror chains) overlaps the others' bulk.
-int render_split(rt_scene* s, const rtk::Eye& eye, const rtk::FrameParams& f, bool count, hipStream_t stream, int K) {
-    if (!s->fork_ev) HIP_TRY(hipEventCreateWithFlags(&s->fork_ev, hipEventDisableTiming));
-    HIP_TRY(hipEventRecord(s->fork_ev, stream));
-    for (int j = 0; j < K; ++j) {
-        if (!s->slot_stream[j]) HIP_TRY(hipStreamCreateWithFlags(&s->slot_stream[j], hipStreamNonBlocking));
-        if (!s->slot_done[j]) HIP_TRY(hipEventCreateWithFlags(&s->slot_done[j], hipEventDisableTiming));
-        HIP_TRY(hipStreamWaitEvent(s->slot_stream[j], s->fork_ev, 0));
-    }
-    for (int j = 0; j < K; ++j) {
-        rtk::FrameParams q = f;
-        q.rank = f.rank + j * f.nranks;
-        q.nranks = f.nranks * K;
-        q.slab_rows = rt_slab_rows(f.height, f.stripe_rows, q.nranks);
-        q.out_k = K;
-        q.out_j = j;
-        const int rc = render_chain(s, eye, q, count, s->slot_stream[j], j);
-        if (rc) return rc;
-    }
-    for (int j = 0; j < K; ++j) {
-        HIP_TRY(hipEventRecord(s->slot_done[j], s->slot_stream[j]));
-        HIP_TRY(hipStreamWaitEvent(stream, s->slot_done[j], 0));
-    }
-    return RT_OK;
-}
+constexpr long long kMergeFrameSamples = 1 << 19;   // render_cameras: frames below this are merged into larger batches
 
-// One frame (rank `rank`'s stripes) on `stream`, chain-path workspace `slot`;
-// split_ok: the frame may be split into concurrent sub-frames (render_split).
+// One frame (rank `rank`'s stripes) on `stream`, chain-path workspace `slot`.  (Splitting a frame into
+// concurrent interleaved sub-frames measured slower, +8 % / +18 % for 2 / 3, and was removed in round 6.)
 int render_frame(rt_scene* s, const rt_camera* cam, int aa, int stripe_rows, int rank, int nranks, void* out_dev,
-                 hipStream_t stream, int flags, int slot, bool split_ok = false) {
+                 hipStream_t stream, int flags, int slot) {
     if (!s || !out_dev) return fail(RT_ERR_ARG, "scene/out is NULL");
     if (s->host_only) return fail(RT_ERR_NO_DEVICE, "scene was created with RT_OPT_HOST_ONLY");
     int rc = check_camera(cam, aa);
@@ -1343,10 +1274,6 @@ int render_frame(rt_scene* s, const rt_camera* cam, int aa, int stripe_rows, int
     p.out = static_cast<uint8_t*>(out_dev);
     p.counters = s->d_counters;
     const bool count = (flags & RT_RENDER_COUNT) != 0;
-    const int K = std::min(rt_scene::kSlots, std::max(1, s->tune_split));
-    const long long samples = (long long)p.slab_rows * p.width * aa * aa;
-    if (split_ok && K > 1 && samples >= kSplitMinSamples)
-        return render_split(s, eye, p, count, stream, K);
     return render_chain(s, eye, p, count, stream, slot);
 }
 }  // namespace
@@ -1356,8 +1283,7 @@ extern "C" {
 
 int rt_render_device(rt_scene* s, const rt_camera* cam, int aa, int stripe_rows, int rank, int nranks,
                      void* out_dev, void* stream, int flags) {
-    return render_frame(s, cam, aa, stripe_rows, rank, nranks, out_dev, static_cast<hipStream_t>(stream), flags, 0,
-                        true);
+    return render_frame(s, cam, aa, stripe_rows, rank, nranks, out_dev, static_cast<hipStream_t>(stream), flags, 0);
 }
 
 // raytracer.cpp:505-519 (one render per camera), batched: the cameras' frames
@@ -1403,13 +1329,12 @@ int render_cameras(rt_scene* s, const rt_camera* cams, int n, int aa, void* cons
                    int flags, int stripe_rows = 0, int rank = 0, int nranks = 1, bool may_wait = false,
                    int batch_max = 0, int slot0 = 0) {
     auto rows_of = [&](int i) { return stripe_rows > 0 ? stripe_rows : cams[i].image_height; };
-    const bool batching = n > 1 && s->tune_batch > 1;
-    if (batching) {
+    if (n > 1) {
         // consecutive same-size frames, up to kMaxFrames and one chain chunk of samples per batch
         const int nslot = std::max(1, std::min(s->tune_slots, rt_scene::kSlots));
         // (batch_max, slot0: the rest of a call after its first batch, on the next slots -- batches of the
         // same size as the calls that follow, on every slot, so no workspace grows inside those)
-        const int bmax = std::min({s->tune_batch, rtc::kMaxFrames, batch_max > 0 ? batch_max : rtc::kMaxFrames});
+        const int bmax = std::min(rtc::kMaxFrames, batch_max > 0 ? batch_max : rtc::kMaxFrames);
         std::vector<int> starts;
         HIP_TRY(hipSetDevice(s->device));
         if (const int rc = ensure_chain_grids(s)) return rc;
@@ -1422,12 +1347,10 @@ int render_cameras(rt_scene* s, const rt_camera* cams, int n, int aa, void* cons
         }
         poll_cont(s, false);
         // runs of consecutive same-size frames; a run of L frames goes out as batches of min(m, ceil(L / nslot))
-        // frames, m the most frames one launch's plan fits in the slot's workspace share (at most bmax): a
-        // 20-frame call on 6 slots runs 4,4,4,4,4 on 5.  RT_BALANCE=1: nb = max(min(nslot, L), ceil(L / m))
-        // batches of (nearly) equal size, every slot busy (4,4,3,3,3,3) -- measured slower: the sixth
-        // concurrent batch's first kernel starts ~0.65 ms after the others (RT_LOG_SUBMIT, whatever the
-        // hardware-queue count), so its end sets the call's
-        const bool balance = s->tune_balance;
+        // frames, m the most frames one launch's plan fits in the slot's workspace share: a 20-frame call on 6
+        // slots runs 4,4,4,4,4 on 5.  (Round 5's balanced deal, 4,4,3,3,3,3 with every slot busy, measured
+        // slower -- the sixth concurrent batch's first kernel starts ~0.65 ms after the others whatever the
+        // hardware-queue count -- and was removed in round 6.)
         for (int i = 0; i < n;) {
             const auto& c = cams[i];
             // a batch of k frames: one launch (render_chain's own plan fits the slot's workspace share)
@@ -1445,27 +1368,25 @@ int render_cameras(rt_scene* s, const rt_camera* cams, int n, int aa, void* cons
                 ++L;
             int m = 1;
             while (m < std::min(bmax, L) && fits(m + 1)) ++m;
-            if (balance) {
-                const int nbr = std::max(std::min(nslot, L), (L + m - 1) / m);
-                for (int b = 0; b < nbr; ++b) starts.push_back(i + (int)((long long)L * b / nbr));
-            } else {                               // round 4: batches of min(m, ceil(L / nslot)) frames
-                // as many batches as slots, but at least ~batch_samples samples each: a run of small frames
-                // (a rank's 1/8 share of 20 C3 frames) goes out in 3 batches of 7 rather than 5 of 4 -- each batch
-                // ends with its own phase-B tail, which few samples do not hide (the one-GPU rehearsal of 8 ranks:
-                // 0.105 -> 0.094 ms per frame, profiles/r05_shard20.txt)
-                const double run_samples = (double)L * rt_slab_rows(c.image_height, rows_of(i), nranks) * c.image_width *
-                                           aa * aa;
-                const int nbat = std::max(1, std::min(nslot, (int)std::ceil(run_samples / (double)s->tune_batch_samples)));
-                const int ch = std::min(m, (L + nbat - 1) / nbat);
-                for (int b = 0; b < L; b += ch) starts.push_back(i + b);
-            }
+            // as many batches as slots, but, for small frames (< kMergeFrameSamples each, such as a rank's 1/8 share
+            // of a C3 frame), at least ~batch_samples samples each: 20 such frames go out in 3 batches of 7 rather
+            // than 5 of 4 -- each batch ends with its own phase-B tail, which few samples do not hide (the one-GPU
+            // rehearsal of 8 ranks: 0.105 -> 0.094 ms per frame, profiles/r05_shard20.txt).  Frames of
+            // kMergeFrameSamples or more are never merged beyond that: round 5's rule, applied to every frame size,
+            // put a 2-frame marbles call in one batch, 1.27 -> 1.68 ms per frame (the round-6 call-size sweep,
+            // profiles/r06_sweep_callsize_*.jsonl)
+            const double frame_samples = (double)rt_slab_rows(c.image_height, rows_of(i), nranks) * c.image_width * aa * aa;
+            const double need = frame_samples < (double)kMergeFrameSamples ? (double)s->tune_batch_samples : 1.0;
+            const int nbat = std::max(1, std::min(nslot, (int)std::ceil((double)L * frame_samples / need)));
+            const int ch = std::min(m, (L + nbat - 1) / nbat);
+            for (int b = 0; b < L; b += ch) starts.push_back(i + b);
             i += L;
         }
         starts.push_back(n);
         const int nb = (int)starts.size() - 1;
         if (nb == 1) return render_batch(s, cams, n, aa, rows_of(0), rank, nranks, outs_dev, stream, flags, 0);
         if (may_wait && s->cont_frac == 0 && !(flags & RT_RENDER_COUNT) && s->tune_cont_cb == 0 &&
-            s->dev.max_depth > s->tune_kinline) {
+            s->dev.max_depth > rt_scene::kKinline) {
             // the scene's continuation share is not known yet: one batch first, waited for, so the rest
             // are sized by it (once per scene; a mirror-heavy scene otherwise sends most of its deep
             // chains to k_fallback until the first read-backs arrive).  Synchronous callers only (ADVICE
@@ -1487,9 +1408,9 @@ int render_cameras(rt_scene* s, const rt_camera* cams, int n, int aa, void* cons
             if (!s->slot_done[k]) HIP_TRY(hipEventCreateWithFlags(&s->slot_done[k], hipEventDisableTiming));
             HIP_TRY(hipStreamWaitEvent(s->slot_stream[k], s->fork_ev, 0));
         }
-        // RT_LOG_SUBMIT=1 (diagnostics): per batch, the host's submission time and (HIP events on the slot
+        // RT_DEBUG 0x04 (diagnostics): per batch, the host's submission time and (HIP events on the slot
         // streams, waited for at the end of the call: this makes the call synchronous) its GPU start and end
-        static const bool log_submit = std::getenv("RT_LOG_SUBMIT") != nullptr;
+        const bool log_submit = (debug_flags() & kDbgLogSubmit) != 0;
         auto now_us = [] { return std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now().time_since_epoch()).count(); };
         const double ts0 = log_submit ? now_us() : 0.0;
         std::vector<hipEvent_t> bev;
@@ -1531,33 +1452,7 @@ int render_cameras(rt_scene* s, const rt_camera* cams, int n, int aa, void* cons
         }
         return RT_OK;
     }
-    if (n == 1) {
-        for (int i = 0; i < n; ++i) {
-            const int rc = render_frame(s, &cams[i], aa, rows_of(i), rank, nranks, outs_dev[i], stream, flags, 0);
-            if (rc) return rc;
-        }
-        return RT_OK;
-    }
-    if (!s->fork_ev) HIP_TRY(hipEventCreateWithFlags(&s->fork_ev, hipEventDisableTiming));
-    HIP_TRY(hipEventRecord(s->fork_ev, stream));
-    const int nslot = std::max(1, std::min(s->tune_slots, rt_scene::kSlots));
-    const int used = std::min(n, nslot);
-    for (int k = 0; k < used; ++k) {
-        if (!s->slot_stream[k]) HIP_TRY(hipStreamCreateWithFlags(&s->slot_stream[k], hipStreamNonBlocking));
-        if (!s->slot_done[k]) HIP_TRY(hipEventCreateWithFlags(&s->slot_done[k], hipEventDisableTiming));
-        HIP_TRY(hipStreamWaitEvent(s->slot_stream[k], s->fork_ev, 0));
-    }
-    for (int i = 0; i < n; ++i) {
-        const int k = i % nslot;
-        const int rc = render_frame(s, &cams[i], aa, rows_of(i), rank, nranks, outs_dev[i], s->slot_stream[k],
-                                    flags, k);
-        if (rc) return rc;
-    }
-    for (int k = 0; k < used; ++k) {
-        HIP_TRY(hipEventRecord(s->slot_done[k], s->slot_stream[k]));
-        HIP_TRY(hipStreamWaitEvent(stream, s->slot_done[k], 0));
-    }
-    return RT_OK;
+    return render_frame(s, &cams[0], aa, rows_of(0), rank, nranks, outs_dev[0], stream, flags, 0);
 }
 
 int rt_render_cameras_device(rt_scene* s, const rt_camera* cams, int n, int aa, void* const* outs_dev, void* stream,
@@ -1643,7 +1538,7 @@ int rt_render_cameras(rt_scene* s, const rt_camera* cams, int n, int aa, uint8_t
     for (int i = 0; i < n; ++i) dev[i] = s->batch_out + off[i];
     const bool count = stats != nullptr;
     if (count) HIP_TRY(hipMemset(s->d_counters, 0, rtc::kCounters * sizeof(unsigned long long)));
-    static const bool log = std::getenv("RT_LOG_INIT") != nullptr;   // diagnostics (tools/exp_cli.py --phases)
+    const bool log = (debug_flags() & kDbgLogInit) != 0;   // diagnostics (tools/exp_cli.py --phases)
     const double t_out = log ? ms_since(t0) : 0.0;
     int rc = render_cameras(s, cams, n, aa, dev.data(), nullptr, count ? RT_RENDER_COUNT : 0, 0, 0, 1, true);
     const double t_sub = log ? ms_since(t0) : 0.0;
@@ -1902,7 +1797,7 @@ int rt_primary_hits_production(rt_scene* s, const rt_camera* cam, int aa, float*
         s->dbg_m = dm;
         // the production kernels of one whole frame on this device (rt_render_device's launch sequence; no
         // sub-frame split, whose virtual ranks would index their own slabs)
-        rc = render_frame(s, cam, aa, cam->image_height, 0, 1, d + 8 * n, nullptr, 0, 0, false);
+        rc = render_frame(s, cam, aa, cam->image_height, 0, 1, d + 8 * n, nullptr, 0, 0);
         s->dbg_t = nullptr;
         s->dbg_m = nullptr;
         e = hipDeviceSynchronize();

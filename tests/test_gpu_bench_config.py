@@ -3,13 +3,11 @@
 bench.py times C3 (horse_and_mug 1920x1080, depth 6, AA1) as one rank with 4-row
 stripes, 8 hardware queues (6 workspace slots), after two 96-frame warm-up calls;
 the driver runs it with --steps 20: one 20-frame rt_render_frames_device call.
-With the defaults its frames go out as greedy frame batches (RT_BALANCE=0:
-min(m, ceil(20 / 6)) = 4 frames each, 4,4,4,4,4 on 5 slots) with full 32-B
-phase-A records (RT_COMPACT=3: a 4-frame C3 AA1 launch fits its slot's share
-with them; compact 16-B records are for frame sizes that do not, such as AA2).
-RT_BALANCE=1 (4,4,3,3,3,3 on 6 slots) is the measured-slower alternative, kept
-under test.  Every frame of that call must be the reference's image
-(raytracer.cpp:505-519 renders each camera once).
+Its frames go out as greedy frame batches (min(m, ceil(20 / 6)) = 4 frames
+each, 4,4,4,4,4 on 5 slots) with full 32-B phase-A records (RT_COMPACT=3: a
+4-frame C3 AA1 launch fits its slot's share with them; compact 16-B records
+are for frame sizes that do not, such as AA2).  Every frame of that call must
+be the reference's image (raytracer.cpp:505-519 renders each camera once).
 
 RT_WS_BUDGET_MB (rt.h rt_scene_memory) bounds the scene's HBM: the uploaded scene,
 its output staging and every slot's arena; a lone frame's arena follows the frame.
@@ -32,10 +30,8 @@ def torch_cuda():
     return torch
 
 
-@pytest.mark.parametrize("balance", ["1", "0"])
-def test_bench_timed_call_equals_golden(balance, goldens, pkg, scene_dir, torch_cuda, monkeypatch):
+def test_bench_timed_call_equals_golden(goldens, pkg, scene_dir, torch_cuda):
     torch = torch_cuda
-    monkeypatch.setenv("RT_BALANCE", balance)
     g = golden_by_name(goldens, "C3_hm_1080p_d6_aa1")
     ref = torch.from_numpy(load_golden_image(g["cameras"][0]).copy()).to("cuda:0")
     with pkg.Scene.from_xml(config_path(scene_dir, g["config"]), device=0) as s:

@@ -134,7 +134,7 @@ def test_skipped_shadow_rays(gname, goldens, pkg, scene_dir, torch_cuda, monkeyp
     """Shadow rays whose light is behind the surface are not traced by the chain path
     (pathchain.hip light_needed): the image is the golden with and without the skip (RT_CULL=0), the
     counting pass still reports the reference's shadow rays, and a production counting pass
-    (RT_COUNT_PROD, which skips them) reports the same totals and the same number skipped."""
+    (RT_DEBUG 0x20, which skips them) reports the same totals and the same number skipped."""
     g = golden_by_name(goldens, gname)
     cam_g = g["cameras"][0]
     ref = load_golden_image(cam_g)
@@ -143,13 +143,13 @@ def test_skipped_shadow_rays(gname, goldens, pkg, scene_dir, torch_cuda, monkeyp
         for prod in ("0", "1"):
             monkeypatch.setenv("RT_CULL", cull)
             if prod == "1":
-                monkeypatch.setenv("RT_COUNT_PROD", "1")
+                monkeypatch.setenv("RT_DEBUG", "0x20")      # production-fetch counting passes
             else:
-                monkeypatch.delenv("RT_COUNT_PROD", raising=False)
+                monkeypatch.delenv("RT_DEBUG", raising=False)
             with pkg.Scene.from_xml(config_path(scene_dir, g["config"]), device=0, render_path="chain") as s:
                 c, _ = s.cameras()[cam_g["camera"]]
                 img, st[cull, prod] = s.render(c, aa=g["aa"], stats=True)
-                assert np.array_equal(img, ref), f"RT_CULL={cull} RT_COUNT_PROD={prod} (counting pass)"
+                assert np.array_equal(img, ref), f"RT_CULL={cull} production counting={prod}"
                 img2, _ = s.render(c, aa=g["aa"], stats=False)
                 assert np.array_equal(img2, ref), f"RT_CULL={cull} (timed kernels)"
     ref_counts = _counters(cam_g["counters"])
@@ -279,19 +279,16 @@ def test_render_cameras_batched(name, path, goldens, pkg, scene_dir, torch_cuda)
             assert np.array_equal(img, load_golden_image(g["cameras"][i % len(sel)]))
 
 
-@pytest.mark.parametrize("batch", ["16", "1"])
 @pytest.mark.parametrize("path", PATHS)
 @pytest.mark.parametrize("nranks,nframes,gname", [(1, 2, "C3_hm_1080p_d6_aa1"), (8, 8, "C3_hm_1080p_d6_aa1"),
                                                   (3, 5, "C3_hm_1080p_d6_aa1"), (8, 3, "C3_hm_1080p_d6_aa2"),
                                                   (2, 17, "C3_hm_1080p_d6_aa1")])
-def test_render_frames_device_batch(nranks, nframes, gname, path, batch, goldens, pkg, scene_dir, torch_cuda,
-                                    monkeypatch):
+def test_render_frames_device_batch(nranks, nframes, gname, path, goldens, pkg, scene_dir, torch_cuda):
     """Frame batches (rt_render_frames_device, the bench's in-flight frames): every rank's stripes
     of every frame of one batched launch equal the golden, and the work counters are exactly
     nframes times the frame's (no frame's work is shared or skipped).  nframes 17 > kMaxFrames
-    (two batches on two slots); RT_BATCH=1: frames concurrent on slots instead of batched."""
+    (two batches on two slots)."""
     torch = torch_cuda
-    monkeypatch.setenv("RT_BATCH", batch)
     g = golden_by_name(goldens, gname)
     ref = load_golden_image(g["cameras"][0])
     aa, stripe = g["aa"], 8

@@ -48,12 +48,12 @@ def shas(d):
 
 
 def phases(hm, reps, extra_env=None, aa=1):
-    """One CLI process per rep with --timing and RT_LOG_INIT=1: the steady-clock (CLOCK_MONOTONIC) stamps the
+    """One CLI process per rep with --timing and RT_DEBUG=1: the steady-clock (CLOCK_MONOTONIC) stamps the
     CLI and the library's warm-up thread print, against the parent's own stamps around the process."""
     rows = []
     for _ in range(reps):
         wd = tempfile.mkdtemp()
-        env = dict(os.environ, RT_LOG_INIT="1", **(extra_env or {}))
+        env = dict(os.environ, RT_DEBUG=str(int(os.environ.get("RT_DEBUG", "0"), 0) | 1), **(extra_env or {}))
         t_spawn = time.monotonic() * 1e3
         r = subprocess.run([str(CLI), hm, "--aa", str(aa), "--timing"], cwd=wd, capture_output=True, text=True,
                            timeout=120, env=env)
@@ -97,7 +97,7 @@ def main():
     if a.phases:
         hm = pkg.scenes.write_config("hm_verbatim", d)
         for aa in (1, 2):
-            variants = [("default", None), ("normal_exit", {"RT_CLI_EXIT": "normal"}), ("no_warmup", {"RT_NO_WARMUP": "1"})]
+            variants = [("default", None), ("normal_exit", {"RT_CLI_EXIT": "normal"}), ("no_warmup", {"RT_DEBUG": "9"})]
             if os.environ.get("EXP_CLI_VARIANTS"):    # "name:K=V,K2=W;name2:..." instead of the three above
                 variants = [(v.split(":")[0], dict(kv.split("=", 1) for kv in v.split(":", 1)[1].split(",") if kv))
                             for v in os.environ["EXP_CLI_VARIANTS"].split(";")]

@@ -83,6 +83,22 @@ def main():
             cap, og = a, b
             smp = tr[:2 * cap]
             r = summarise(path + "/k_chain", smp[0::2], smp[1::2])
+            # per 8x8 tile (the 64 samples a wave grabs together): grab, last end, span -- the phase-A tail
+            g0, g1 = smp[0::2].astype(np.int64), smp[1::2].astype(np.int64)
+            ntile = cap // 64
+            okt = (g1[:ntile * 64] != 0).reshape(ntile, 64)
+            t00 = g0[g1 != 0].min()
+            gs = np.where(okt, ((g0[:ntile * 64] - t00) & 0xffffffff).reshape(ntile, 64), 1 << 40).min(axis=1) * TICK_US
+            ge = np.where(okt, ((g1[:ntile * 64] - t00) & 0xffffffff).reshape(ntile, 64), -1).max(axis=1) * TICK_US
+            ge_med = np.array([np.median(((g1[t * 64:(t + 1) * 64][okt[t]] - t00) & 0xffffffff) * TICK_US)
+                               if okt[t].any() else -1 for t in range(ntile)])
+            live = okt.any(axis=1)
+            order = np.argsort(-(ge - gs) * live)[:10]
+            r["tiles"] = {"n": int(live.sum()),
+                          "span_pct_us": {p: round(float(np.percentile((ge - gs)[live], p)), 1) for p in (50, 90, 99, 100)},
+                          "longest": [{"tile": int(t), "grab": round(float(gs[t]), 1), "end": round(float(ge[t]), 1),
+                                       "median_end": round(float(ge_med[t]), 1), "live": int(okt[t].sum())}
+                                      for t in order]}
             ob = tr[2 * cap:2 * (cap + og)]
             okb = ob[1::2] != 0
             t0 = smp[0::2][smp[1::2] != 0].min()
