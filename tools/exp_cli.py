@@ -53,7 +53,8 @@ def phases(hm, reps, extra_env=None, aa=1):
     rows = []
     for _ in range(reps):
         wd = tempfile.mkdtemp()
-        env = dict(os.environ, RT_DEBUG=str(int(os.environ.get("RT_DEBUG", "0"), 0) | 1), **(extra_env or {}))
+        env = dict(os.environ, **(extra_env or {}))
+        env["RT_DEBUG"] = str(int(env.get("RT_DEBUG", "0"), 0) | 1)
         t_spawn = time.monotonic() * 1e3
         r = subprocess.run([str(CLI), hm, "--aa", str(aa), "--timing"], cwd=wd, capture_output=True, text=True,
                            timeout=120, env=env)
