@@ -1,5 +1,6 @@
 #!/bin/bash
-# The round's evidence in one GPU call (bash tools/round6.sh TAG), each step under its own time limit:
+# The round's evidence (bash tools/round6.sh TAG [PART]; PART 1: steps 1-2, 2: step 3, default both), each
+# step under its own time limit:
 #  1. the GPU suite;
 #  2. one-slot profiles of C3 (rocprofv3 --kernel-trace --stats, then FETCH_SIZE and WRITE_SIZE passes, each
 #     its own run) of bench.py --trace --one-slot: 96-frame calls (the configuration of the line's
@@ -11,6 +12,8 @@ export TMPDIR=/tmp
 TAG=${1:-r06}
 OUT=gpurun_out/r6_$TAG
 mkdir -p "$OUT"
+PART=${2:-all}
+if [ "$PART" != 2 ]; then
 timeout -k 10 600 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread > "$OUT/tests.log" 2>&1
 rc=$?; echo "tests rc=$rc"; tail -2 "$OUT/tests.log"; [ $rc -ne 0 ] && exit $rc
 prof() {   # prof NAME bench-args...
@@ -25,6 +28,8 @@ prof() {   # prof NAME bench-args...
 }
 prof b96 --steps 96 --warmup 5 --one-slot && prof aa2 --aa 2 --steps 96 --warmup 5 --one-slot \
   && prof f1 --inflight 1 --steps 32 --warmup 3 || exit 1
+fi
+[ "$PART" = 1 ] && exit 0
 run() { local name=$1; shift; timeout -k 10 300 python3 bench.py "$@" > "$OUT/$name.jsonl" 2> "$OUT/$name.err"; local rc=$?; echo "line $name rc=$rc"; return $rc; }
 run c3_20 --steps 20 --warmup 5 && run c3 --no-cpu-baseline && run c3_aa2 --aa 2 --steps 20 --warmup 5 --no-cpu-baseline \
   && run c3_f1 --inflight 1 --steps 32 --warmup 3 --no-cpu-baseline && run c2 --config C2 --steps 192 --no-cpu-baseline \
