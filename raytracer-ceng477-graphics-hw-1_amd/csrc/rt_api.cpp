@@ -22,6 +22,11 @@
 #include "pathchain.hpp"
 #include "rt_internal.hpp"
 
+// phase-B workgroups per CU x 4 in frame batches (a compile-time setting for same-box A/B builds)
+#ifndef RT_GB_BATCH_Q4
+#define RT_GB_BATCH_Q4 6
+#endif
+
 namespace {
 
 thread_local std::string g_err;
@@ -698,7 +703,7 @@ ChainPlan chain_plan(const rt_scene* s, const ChainGeom& g, size_t nunits, bool 
     P.split_occ = g.nframes > 1;
     // (round 5, the driver's 20-frame call on 5 slots: 1.5 per CU 0.4175 against 1 per CU 0.4282 ms/frame, three
     // interleaved same-box rounds, 96-frame calls +-0; profiles/r05_ab_gb.txt)
-    const int gb_default = g.nframes > 1 ? 3 * s->num_cus / 2 : 30 * s->num_cus / 16;
+    const int gb_default = g.nframes > 1 ? RT_GB_BATCH_Q4 * s->num_cus / 4 : 30 * s->num_cus / 16;
     P.gb = P.phase_b ? std::max(1, std::min(s->mix_grid - 1, gb_default)) : 0;
     P.levels_a = std::min(P.kinline, std::max(s->dev.max_depth, 0)) + 1;
     // dynamic phase-A units: a workgroup may take up to twice its static share (at most
