@@ -476,7 +476,7 @@ __device__ uint32_t bq_consume(const rtk::DevScene& s, const PcParams& p, WalkSt
                     r = shadow_from_record_l2(s, p, owner, &tlim);
                     ++n;
                     if (!COUNT && defer_any(s, r)) fb_shadow(p, owner);
-                    else if (walk_begin<COUNT>(s, r, wk, w, true)) active = true;
+                    else if (COUNT ? walk_begin<COUNT>(s, r, wk, w, true) : walk_begin_wide(s, r, wk, true)) active = true;
                     else p.occ[owner] = 0;
                 }
             }
@@ -649,7 +649,7 @@ __device__ void chain_body(const rtk::DevScene& s, const rtk::Eye& e, const PcPa
                     fb_chain(p, (unsigned)lvp);
                     st = kIdle;
                 } else {
-                    st = walk_begin<COUNT>(s, r, wk, w) ? kTrav : kDone;
+                    st = (COUNT ? walk_begin<COUNT>(s, r, wk, w) : walk_begin_wide(s, r, wk)) ? kTrav : kDone;
                 }
             }
         }
@@ -700,7 +700,7 @@ __device__ void chain_body(const rtk::DevScene& s, const rtk::Eye& e, const PcPa
                             r = reflect_from_record(s, p, lvp, path);
                             nrefl++;
                             if (!COUNT && defer_closest(s, r, true)) fb_chain(p, lvp);
-                            else st = walk_begin<COUNT>(s, r, wk, w) ? kTrav : kDone;
+                            else st = (COUNT ? walk_begin<COUNT>(s, r, wk, w) : walk_begin_wide(s, r, wk)) ? kTrav : kDone;
                         } else {
                             const unsigned idx = (dyn ? uid : blk + (v >> 8) * G) * 256u + (v & 255u);
                             if (slab_sample_ray(p, idx, &r)) {
@@ -715,7 +715,7 @@ __device__ void chain_body(const rtk::DevScene& s, const rtk::Eye& e, const PcPa
                                     p.pinfo[path] = kPathCont;
                                     fb_chain(p, kFbEye | path);
                                 }
-                                else st = walk_begin<COUNT>(s, r, wk, w) ? kTrav : kDone;
+                                else st = (COUNT ? walk_begin<COUNT>(s, r, wk, w) : walk_begin_wide(s, r, wk)) ? kTrav : kDone;
                             }
                         }
                     }
@@ -806,7 +806,7 @@ __device__ void occlude_body(const rtk::DevScene& s, const PcParams& p, unsigned
                         r = shadow_from_record(s, p, owner, &tlim);
                         nrays++;
                         if (!COUNT && defer_any(s, r)) fb_shadow(p, owner);
-                        else if (walk_begin<COUNT>(s, r, wk, w, true)) active = true;
+                        else if (COUNT ? walk_begin<COUNT>(s, r, wk, w, true) : walk_begin_wide(s, r, wk, true)) active = true;
                         else p.occ[owner] = 0;
                     }
                 }

@@ -352,6 +352,22 @@ __device__ __forceinline__ bool walk_begin(const rtk::DevScene& s, const Ray& r,
     return box_hit(r, lo, hi, &bt) && (any || bt <= k.tmax);
 }
 
+// walk_begin for the timed kernels, whose rays have already passed defer_closest / defer_any (NaN-free, in
+// range of the wide trees' slab test, the wide trees built): the wide-tree branch only, so the production
+// walkers carry no root box, pair pointers or binary-tree set-up (their kernel arguments otherwise stayed
+// live in SGPRs across the walk loops).  false: nothing to traverse.
+__device__ __forceinline__ bool walk_begin_wide(const rtk::DevScene& s, const Ray& r, Walk& k, bool any = false) {
+    k.best = HitRec{-1.0f, -1};
+    k.tmax = FLT_MAX;
+    k.sp = 0;
+    k.steps = 0;
+    k.fast = true;
+    k.tree = nullptr;
+    k.cur = any ? s.swroot : s.wroot;
+    k.sgn = (r.d.x > 0.0f ? 1 : 0) | (r.d.y > 0.0f ? 2 : 0) | (r.d.z > 0.0f ? 4 : 0);
+    return s.nnodes > 0;
+}
+
 // Child boxes of a wide node (dl::Wide), slab-tested against a NaN-free ray.
 typedef float f2v __attribute__((ext_vector_type(2)));
 

@@ -39,71 +39,63 @@ __device__ __forceinline__ void wave_add_counter(unsigned long long* c, unsigned
 template <class P>
 __device__ __forceinline__ int batch_frame(const P& p, int* lr) {
     if (p.nframes <= 1) return 0;
-    const int f = *lr / p.frame_rows;
-    *lr -= f * p.frame_rows;
-    return f;
+    const unsigned f = (unsigned)*lr / (unsigned)p.frame_rows;
+    *lr -= (int)(f * (unsigned)p.frame_rows);
+    return (int)f;
 }
 
-// Slab-local sample slot -> eye ray.  Slots are ordered by 8x8 internal-pixel
-// tiles (one tile per wave) for ray coherence; slab rows map to global rows
-// through the stripe round-robin.  P needs: wi tiles_x chunk_row0 chunk_rows
-// aa slab_rows stripe_rows nranks rank height nframes frame_rows eyes, with
-// eyes[0] the camera of a lone frame too (read per lane from the kernel
-// arguments: a kernel that also kept a separate Eye argument live held its
-// 13 words in scalar registers, which the walk loops then spilled).
+// Slab-local sample slot -> (frame, internal row, column) of its eye ray.  Slots are ordered by 8x8
+// internal-pixel tiles (one tile per wave) for ray coherence; slab rows map to global rows through the
+// stripe round-robin.  Every quantity is non-negative, so the divisions by the launch's (wave-uniform)
+// sizes are unsigned: no sign set-up per divisor, which the walk kernels otherwise kept in SGPRs across
+// their loops (and spilled).  P needs: wi tiles_x chunk_row0 chunk_rows aa slab_rows stripe_rows nranks
+// rank height nframes frame_rows.
+template <class P>
+__device__ __forceinline__ bool slab_sample_pos(const P& p, unsigned s, int* frame, int* row, int* col) {
+    const unsigned tile = s >> 6, lane = s & 63;
+    const unsigned ty = tile / (unsigned)p.tiles_x, tx = tile - ty * (unsigned)p.tiles_x;
+    const unsigned ix = tx * 8u + (lane & 7u);
+    const unsigned iyc = ty * 8u + (lane >> 3);
+    if (ix >= (unsigned)p.wi || iyc >= (unsigned)p.chunk_rows) return false;
+    const unsigned iy = (unsigned)p.chunk_row0 + iyc;
+    const unsigned lr0 = iy / (unsigned)p.aa;
+    const unsigned sub = iy - lr0 * (unsigned)p.aa;
+    if (lr0 >= (unsigned)p.slab_rows) return false;
+    int lri = (int)lr0;
+    *frame = batch_frame(p, &lri);
+    const unsigned lr = (unsigned)lri;
+    const unsigned stripe = lr / (unsigned)p.stripe_rows;
+    const unsigned g = (stripe * (unsigned)p.nranks + (unsigned)p.rank) * (unsigned)p.stripe_rows +
+                       (lr - stripe * (unsigned)p.stripe_rows);
+    if (g >= (unsigned)p.height) return false;
+    *row = (int)(g * (unsigned)p.aa + sub);
+    *col = (int)ix;
+    return true;
+}
+
+// Slab-local sample slot -> eye ray (eyes[0] is the camera of a lone frame too; read per lane from the
+// kernel arguments: a kernel that also kept a separate Eye argument live held its 13 words in scalar
+// registers, which the walk loops then spilled).
 template <class P>
 __device__ __forceinline__ bool slab_sample_ray(const P& p, unsigned s, Ray* r) {
-    const unsigned tile = s >> 6, lane = s & 63;
-    const int tx = (int)(tile % (unsigned)p.tiles_x), ty = (int)(tile / (unsigned)p.tiles_x);
-    const int ix = tx * 8 + (int)(lane & 7);
-    const int iyc = ty * 8 + (int)(lane >> 3);
-    if (ix >= p.wi || iyc >= p.chunk_rows) return false;
-    const int iy = p.chunk_row0 + iyc;
-    int lr = iy / p.aa;
-    const int sub = iy - lr * p.aa;
-    if (lr >= p.slab_rows) return false;
-    const int f = batch_frame(p, &lr);
-    const int stripe = lr / p.stripe_rows;
-    const int g = (stripe * p.nranks + p.rank) * p.stripe_rows + (lr - stripe * p.stripe_rows);
-    if (g >= p.height) return false;
-    *r = eye_ray(p.eyes[f], g * p.aa + sub, ix);
+    int f, row, col;
+    if (!slab_sample_pos(p, s, &f, &row, &col)) return false;
+    *r = eye_ray(p.eyes[f], row, col);
     return true;
 }
 
 // The internal pixel (frame row, column) whose eye ray slab_sample_ray gives slot s (diagnostics).
 template <class P>
 __device__ __forceinline__ bool slab_sample_pixel(const P& p, unsigned s, int* row, int* col) {
-    const unsigned tile = s >> 6, lane = s & 63;
-    const int tx = (int)(tile % (unsigned)p.tiles_x), ty = (int)(tile / (unsigned)p.tiles_x);
-    const int ix = tx * 8 + (int)(lane & 7);
-    const int iyc = ty * 8 + (int)(lane >> 3);
-    if (ix >= p.wi || iyc >= p.chunk_rows) return false;
-    const int iy = p.chunk_row0 + iyc;
-    int lr = iy / p.aa;
-    const int sub = iy - lr * p.aa;
-    if (lr >= p.slab_rows) return false;
-    batch_frame(p, &lr);
-    const int stripe = lr / p.stripe_rows;
-    const int g = (stripe * p.nranks + p.rank) * p.stripe_rows + (lr - stripe * p.stripe_rows);
-    if (g >= p.height) return false;
-    *row = g * p.aa + sub;
-    *col = ix;
-    return true;
+    int f;
+    return slab_sample_pos(p, s, &f, row, col);
 }
 
 // Does slot s of the chunk hold a sample of this rank's slab (slab_sample_ray's checks)?
 template <class P>
 __device__ __forceinline__ bool slab_slot_valid(const P& p, unsigned s) {
-    const unsigned tile = s >> 6, lane = s & 63;
-    const int tx = (int)(tile % (unsigned)p.tiles_x), ty = (int)(tile / (unsigned)p.tiles_x);
-    const int ix = tx * 8 + (int)(lane & 7);
-    const int iyc = ty * 8 + (int)(lane >> 3);
-    if (ix >= p.wi || iyc >= p.chunk_rows) return false;
-    int lr = (p.chunk_row0 + iyc) / p.aa;
-    if (lr >= p.slab_rows) return false;
-    batch_frame(p, &lr);
-    const int stripe = lr / p.stripe_rows;
-    return (stripe * p.nranks + p.rank) * p.stripe_rows + (lr - stripe * p.stripe_rows) < p.height;
+    int f, row, col;
+    return slab_sample_pos(p, s, &f, &row, &col);
 }
 
 // Inverse of the tile ordering: chunk-relative internal pixel -> slot.
