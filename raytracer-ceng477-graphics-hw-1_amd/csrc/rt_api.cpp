@@ -143,9 +143,9 @@ struct rt_scene {
                                 // 2 every launch, 0 none, 3 (round 5) frame batches only where full records would leave
                                 // fewer than 4 frames per launch (full_records_fit; C3 AA1 20-frame calls 0.4151 -> 0.4040
                                 // ms/frame with full records, 96-frame calls -0.4 %; profiles/r05_ab_compact.txt)
-    // RT_WS_BUDGET_MB: HBM for the scene on its device -- the uploaded scene, a 64 MB reserve for output
-    // staging, and the chain-path workspace arenas of all slots together, each slot's arena (headroom
-    // included) within an even share of the rest.  A launch's arena is sized for the worst case (every
+    // RT_WS_BUDGET_MB: HBM for the scene on its device -- the uploaded scene, the host-output staging (its
+    // live size, at least a 64 MB reserve), and the chain-path workspace arenas of all slots together, each
+    // slot's arena (headroom included) within an even share of the rest.  A launch's arena is sized for the worst case (every
     // sample recording every level), so the budget bounds the samples per launch (and the frames per frame
     // batch).  A lone frame's arena follows the frame (chain_launch_units), not the share.
     size_t ws_budget = size_t(16) << 30;
