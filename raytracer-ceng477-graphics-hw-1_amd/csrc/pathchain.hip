@@ -206,6 +206,8 @@ __device__ __forceinline__ unsigned wave_grab_lds(unsigned* ctr, unsigned long l
 __shared__ unsigned g_ccnt;    // block-local continuation count
 __shared__ unsigned g_uid[kDynUnits];   // dynamic phase-A units: the workgroup's k-th unit (kUidUnset: not yet taken)
 constexpr unsigned kUidUnset = ~0u, kUidNone = ~0u - 1u;
+// A mixed-deal virtual unit (PcParams::ugrp): kUidMix | log2 G << 28 | sub-unit << 24 | group.
+constexpr unsigned kUidMix = 0x80000000u;
 
 struct PhaseOut {              // where a chain phase writes its tasks
     unsigned* sq;              // shadow tasks, region blk at sq + blk * scap
@@ -516,6 +518,17 @@ __device__ __forceinline__ unsigned unit_col_order(const PcParams& p, unsigned u
 __device__ __forceinline__ unsigned unit_order(const PcParams& p, unsigned u, unsigned units) {
     return p.uorder_on ? p.uorder[u] : unit_col_order(p, u, units);
 }
+// Sample slot of position o (0..255) of a mixed-deal virtual unit (kUidMix code; PcParams::ugrp): the
+// group's G virtual units are G * 4 wave chunks of 64 positions; in chunk w, positions l < h = 64 / G hold
+// samples w * h + l of the hot unit (h / 8 whole rows of one of its 8x8 tiles), the others the group's light
+// units' samples in order.
+__device__ __forceinline__ unsigned mix_sample(const PcParams& p, unsigned code, unsigned o) {
+    const unsigned lg = (code >> 28) & 3u, sub = (code >> 24) & 7u, g = code & 0xFFFFFFu;
+    const unsigned h = 64u >> lg, vv = (sub << 8) | o, w = vv >> 6, l = vv & 63u;
+    const unsigned c = w * (64u - h) + (l - h);
+    const unsigned slot = l < h ? 0u : 1u + (c >> 8), off = l < h ? w * h + l : (c & 255u);
+    return p.ugrp[(g << lg) + slot] * 256u + off;
+}
 
 // closest-hit chains of one phase (raytracer.cpp:385-439 minus the shading):
 // record each hit, queue its shadow tasks, follow (or hand on) mirrors.
@@ -702,7 +715,8 @@ __device__ void chain_body(const rtk::DevScene& s, const rtk::Eye& e, const PcPa
                             if (!COUNT && defer_closest(s, r, true)) fb_chain(p, lvp);
                             else st = (COUNT ? walk_begin<COUNT>(s, r, wk, w) : walk_begin_wide(s, r, wk)) ? kTrav : kDone;
                         } else {
-                            const unsigned idx = (dyn ? uid : blk + (v >> 8) * G) * 256u + (v & 255u);
+                            const unsigned idx = dyn && (uid & kUidMix) ? mix_sample(p, uid, v & 255u)
+                                                 : (dyn ? uid : blk + (v >> 8) * G) * 256u + (v & 255u);
                             if (slab_sample_ray(p, idx, &r)) {
                                 path = idx;
                                 k = 0;
@@ -1138,6 +1152,10 @@ __device__ __forceinline__ int unit_class(unsigned c) {
         if (c >= kHotSteps[i]) return i;
     return kUnitClasses - 1;
 }
+// The mixed deal pays where the heavy units' lockstep waves are phase A's tail, not where the launch's bulk
+// outlasts them: C3 (6.3 units per k_chain workgroup) one frame -4 %, C3 at SSAA 2 (25 per workgroup) +1 %,
+// 1024^2 scenes (3.2) +-1.5 % (profiles/r06_mix_*.jsonl).
+constexpr unsigned kMixRounds = 12;
 __device__ void rank_units(const PcParams& p) {
     __shared__ unsigned s_wave[kBlock / 64][kUnitClasses];
     const unsigned units = ((unsigned)p.n0 + 255u) / 256u;
@@ -1160,7 +1178,8 @@ __device__ void rank_units(const PcParams& p) {
         if (lane == 63) s_wave[wave][c] = inc[c];
     }
     __syncthreads();
-    unsigned at[kUnitClasses], base = 0;
+    unsigned at[kUnitClasses], base = 0, nhot = 0;
+    const int mcls = p.mix_cls & 0xff;
 #pragma unroll
     for (int c = 0; c < kUnitClasses; ++c) {
         unsigned before = 0, total = 0;
@@ -1170,7 +1189,19 @@ __device__ void rank_units(const PcParams& p) {
         }
         at[c] = base + before + inc[c] - mine[c];
         base += total;
+        if (c < mcls) nhot += total;
     }
+    // the mixed deal (PcParams::ugrp): groups of G = 2^lg units, all in the resident workgroups' first units
+    // (so every hot unit starts at once; with more hot units than that, the heaviest grid / G), and only in
+    // launches of at most kMixRounds units per workgroup
+    unsigned lg = (unsigned)(p.mix_cls >> 8) & 3u;
+    if (lg == 0) {
+        lg = 3;
+        while (lg > 1 && (nhot << lg) > (unsigned)p.grid) --lg;
+    }
+    nhot = min(nhot, (unsigned)p.grid >> lg);
+    if (nhot == 0 || (nhot << lg) > units || units > kMixRounds * (unsigned)p.grid) lg = 0, nhot = 0;
+    const unsigned nlight = nhot * ((1u << lg) - 1u);
     for (unsigned j = j0; j < j1; ++j) {
         const unsigned u = p.ucol[j];
         const int cls = unit_class(p.ucost[u]);
@@ -1178,9 +1209,20 @@ __device__ void rank_units(const PcParams& p) {
 #pragma unroll
         for (int c = 0; c < kUnitClasses; ++c)     // (no dynamic index into at[]: it would live in scratch)
             if (c == cls) pos = at[c]++;
-        p.uorder[pos] = u;
+        // heaviest-first position pos -> a group's hot unit, a group's light unit (the lightest nlight),
+        // or a plain unit after the groups' virtual units
+        if (pos < nhot) {
+            p.ugrp[pos << lg] = u;
+        } else if (pos >= units - nlight) {
+            const unsigned q = units - 1u - pos, g = q / ((1u << lg) - 1u);
+            p.ugrp[(g << lg) + 1u + (q - g * ((1u << lg) - 1u))] = u;
+        } else {
+            p.uorder[pos + nlight] = u;
+        }
         p.ucost[u] = 0;
     }
+    for (unsigned v = threadIdx.x; v < (nhot << lg); v += kBlock)
+        p.uorder[v] = kUidMix | lg << 28 | (v & ((1u << lg) - 1u)) << 24 | v >> lg;
 }
 
 __global__ __launch_bounds__(kBlock) void k_pack_a(PcParams p) {

@@ -119,7 +119,10 @@ constexpr int kTotalsWords = 12;
 // Classes 0..5: at least kHotSteps[c] steps; class kUnitClasses - 1: the rest (and units no sample of which
 // reached kHotSteps[5], which k_chain does not mark).
 constexpr int kUnitClasses = 7;
-constexpr unsigned kHotSteps[kUnitClasses - 1] = {224, 160, 128, 96, 64, 32};
+#ifndef RT_HOT_MIN
+#define RT_HOT_MIN 32     // (48 with the mixed deal: one frame +0.6 %, profiles/r06_mix_ab.jsonl)
+#endif
+constexpr unsigned kHotSteps[kUnitClasses - 1] = {224, 160, 128, 96, 64, RT_HOT_MIN};
 
 struct PcParams {
     int width, height, aa, stripe_rows, rank, nranks, slab_rows;
@@ -226,6 +229,14 @@ struct PcParams {
     // timed walks defer, by k_fallback.  Null in every other launch.
     float* dbg_t;
     int* dbg_m;
+    // Lone frames' mixed deal (rank_units, unit_order): the units of the mix_cls heaviest cost classes ("hot")
+    // are dealt first, each in a group with G - 1 of the lightest units, the group's 64-sample wave chunks
+    // holding 64 / G samples (whole 8-pixel rows) of the hot unit and the rest of the light ones, so that no
+    // wave starts with more than 64 / G heavy walks.  ugrp[g * G + 0] = group g's hot unit, [g * G + 1 + j] its
+    // light ones; uorder holds kUidMix codes for the groups' virtual units.  mix_cls: bits 0-7 the classes
+    // (0: off), bits 8-9 log2 G (0: from the hot-unit count and the grid, at most 8 hot rows per wave).
+    unsigned* ugrp;
+    int mix_cls;
 };
 
 // Worst-case task-queue slots per workgroup: every sample of the workgroup

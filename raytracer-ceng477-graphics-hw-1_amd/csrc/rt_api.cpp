@@ -139,6 +139,9 @@ struct rt_scene {
                                 // default GPU_MAX_HW_QUEUES - 1)
     int tune_bq_cap = 1 << 30;  // RT_BQ_CAP: phase-B shadow queue slots (tests force the k_occlude spill path)
     int tune_hot_units = 1;     // RT_HOT_UNITS: lone frames deal phase-A units heaviest-first by the previous frame's steps
+    int tune_mix = 5 | 1 << 8;  // RT_MIX: PcParams::mix_cls: lone frames deal the units of >= 64 steps (classes
+                                // 0-4) in pairs with light ones, half of each wave's first lanes (C3 one frame
+                                // 0.876 -> 0.837 ms; 16 of 64 lanes the same, 8 of 64 +-0; profiles/r06_mix_*.jsonl)
     int tune_compact = 3;       // RT_COMPACT: phase-A records without directions (16 B instead of 32): 1 frame batches,
                                 // 2 every launch, 0 none, 3 (round 5) frame batches only where full records would leave
                                 // fewer than 4 frames per launch (full_records_fit; C3 AA1 20-frame calls 0.4151 -> 0.4040
@@ -180,7 +183,7 @@ struct rt_scene {
         size_t bytes = 0;
         hipEvent_t last = nullptr;
         hipStream_t last_stream = nullptr;
-        // lone frames' phase-A unit order (PcParams::ucost / uorder): ucost then uorder, hist_units each
+        // lone frames' phase-A unit order (PcParams::ucost / uorder): ucost, uorder, ucol, ugrp, hist_units each
         unsigned* hist = nullptr;
         unsigned hist_units = 0;
         uint64_t hist_key = 0;               // the launch geometry uorder was ranked for (0: none yet)
@@ -466,6 +469,7 @@ int upload_rest(rt_scene* s, const rt_options* opts) {
     if (const char* e = std::getenv("RT_BQ_CAP")) s->tune_bq_cap = std::max(0, std::atoi(e));
     if (const char* e = std::getenv("RT_COMPACT")) s->tune_compact = std::max(0, std::min(3, std::atoi(e)));
     if (const char* e = std::getenv("RT_HOT_UNITS")) s->tune_hot_units = std::atoi(e) != 0;
+    if (const char* e = std::getenv("RT_MIX")) s->tune_mix = std::atoi(e);
     if (const char* e = std::getenv("RT_TRACE")) s->trace_file = e;
     const int dbg = debug_flags();
     s->ktime = (dbg & kDbgKtime) != 0;
@@ -983,6 +987,8 @@ int render_chain(rt_scene* s, const rtk::Eye& eye, const rtk::FrameParams& f, bo
     const bool hot = s->tune_hot_units && !count && p.nframes == 1 && P.dyn_units > 0 &&
                      units == g.units_total;
     p.urank = p.uorder_on = 0;
+    p.ugrp = nullptr;
+    p.mix_cls = 0;
     for (int r0 = f.chunk_j * chunk_rows; r0 < li; r0 += f.chunk_k * chunk_rows) {
         p.chunk_row0 = r0;
         p.chunk_rows = std::min(chunk_rows, li - r0);
@@ -996,7 +1002,7 @@ int render_chain(rt_scene* s, const rtk::Eye& eye, const rtk::FrameParams& f, bo
                 arena.hist = nullptr;
                 arena.hist_units = 0;
                 arena.hist_key = 0;
-                HIP_TRY(hipMalloc(reinterpret_cast<void**>(&arena.hist), 3 * (size_t)nu * sizeof(unsigned)));
+                HIP_TRY(hipMalloc(reinterpret_cast<void**>(&arena.hist), 4 * (size_t)nu * sizeof(unsigned)));
                 HIP_TRY(hipMemsetAsync(arena.hist, 0, 2 * (size_t)nu * sizeof(unsigned), st));
                 arena.hist_units = nu;
             }
@@ -1008,6 +1014,8 @@ int render_chain(rt_scene* s, const rtk::Eye& eye, const rtk::FrameParams& f, bo
             p.ucost = arena.hist;
             p.uorder = arena.hist + nu;
             p.ucol = arena.hist + 2 * (size_t)nu;
+            p.ugrp = arena.hist + 3 * (size_t)nu;
+            p.mix_cls = s->tune_mix;
             if (arena.hist_key != key) {           // this geometry's column order (unit_col), once
                 std::vector<unsigned> col(nu);
                 for (unsigned u = 0; u < nu; ++u) col[u] = rtc::unit_col(p.tiles_x, p.ublk_h, p.ublk_w, p.nframes, u, nu);

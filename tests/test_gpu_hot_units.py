@@ -1,7 +1,7 @@
 """GPU: a lone frame's phase-A units dealt by the previous frame's costs (pathchain.hip rank_units: seven
 cost classes, heaviest first).  Only where work runs changes: every repeated frame must equal the
-reference's image -- ranked or not, with the phase-B record space cut, with the LDS shadow queue off and
-with every shadow ray deferred to k_fallback.
+reference's image -- ranked or not, with the mixed deal of the heaviest units (PcParams::ugrp), with the
+phase-B record space cut, with the LDS shadow queue off and with every shadow ray deferred to k_fallback.
 """
 from __future__ import annotations
 
@@ -27,6 +27,10 @@ ENVS = [
     {"RT_HOT_UNITS": "1", "RT_CONT_CB": "2000"},             # most continuations beyond the record space
     {"RT_HOT_UNITS": "1", "RT_BQ_CAP": "0"},
     {"RT_HOT_UNITS": "1", "RT_FORCE_FALLBACK": "2"},
+    {"RT_HOT_UNITS": "1", "RT_MIX": "0"},                    # heaviest first, no mixed deal
+    {"RT_HOT_UNITS": "1", "RT_MIX": "5"},                    # mixed deal, G from the hot-unit count and the grid
+    {"RT_HOT_UNITS": "1", "RT_MIX": str(6 | 1 << 8)},        # every marked class, G = 2
+    {"RT_HOT_UNITS": "1", "RT_MIX": str(1 | 3 << 8), "RT_CONT_CB": "2000"},   # G = 8, record space cut
 ]
 
 

@@ -97,7 +97,11 @@ def main():
             r["tiles"] = {"n": int(live.sum()),
                           "span_pct_us": {p: round(float(np.percentile((ge - gs)[live], p)), 1) for p in (50, 90, 99, 100)},
                           "longest": [{"tile": int(t), "grab": round(float(gs[t]), 1), "end": round(float(ge[t]), 1),
-                                       "median_end": round(float(ge_med[t]), 1), "live": int(okt[t].sum())}
+                                       "median_end": round(float(ge_med[t]), 1), "live": int(okt[t].sum()),
+                                       # the tile's distinct (start, end) pairs: lanes of one wave end together
+                                       "spans": sorted({(round(float(((g0[t * 64 + i] - t00) & 0xffffffff) * TICK_US), 1),
+                                                         round(float(((g1[t * 64 + i] - t00) & 0xffffffff) * TICK_US), 1))
+                                                        for i in range(64) if okt[t, i]})[:16]}
                                       for t in order]}
             ob = tr[2 * cap:2 * (cap + og)]
             okb = ob[1::2] != 0
