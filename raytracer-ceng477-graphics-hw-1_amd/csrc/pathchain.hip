@@ -402,6 +402,73 @@ __device__ __forceinline__ unsigned chunk_task(unsigned v, unsigned G, unsigned 
     const unsigned q = ch.div(v);
     return (blk + q * G) * ch.d + (v - q * ch.d);
 }
+// Phase A's per-workgroup task regions (shadow tasks sqA / scntA, continuations cq / ccnt) read as ONE list
+// in region order -- the order k_pack_a's packing gives them, without the copy: each consumer workgroup holds
+// the regions' exclusive count prefix in LDS (region_prefix) and maps list index j to its region by binary
+// search (region_task).  A lone frame's k_mix reads both lists so (no packing kernel between its phase A
+// and phase B: -10 us per C3 frame); frame batches keep k_pack_a's packed continuations (cflat), which their
+// k_mix reads 2 % faster (profiles/r06_nopack_ab.jsonl); k_fallback reads the continuations so in both.
+__shared__ unsigned g_pref[kMaxChainGrid + 1];
+// g_pref[0, nreg] = the exclusive prefix of cnt[0, nreg) (g_pref[nreg] = the total, returned).  Every thread
+// of the workgroup; nreg <= kMaxChainGrid.  A call, not inlined: inlined at the kernels' start it still cost
+// k_mix 7 VGPRs and 31-37 more SGPR spills in its walk loops.
+__device__ __noinline__ unsigned region_prefix(const unsigned* cnt, unsigned nreg) {
+    __shared__ unsigned s_psum[kBlock / 64];
+    const int lane = lane_id(), wave = (int)(threadIdx.x >> 6);
+    const unsigned per = (nreg + kBlock - 1u) / kBlock;
+    const unsigned r0 = min(nreg, threadIdx.x * per), r1 = min(nreg, r0 + per);
+    unsigned sum = 0;
+    for (unsigned r = r0; r < r1; ++r) sum += cnt[r];
+    unsigned inc = sum;
+    for (int off = 1; off < 64; off <<= 1) {
+        const unsigned v = __shfl_up(inc, off, 64);
+        if (lane >= off) inc += v;
+    }
+    if (lane == 63) s_psum[wave] = inc;
+    __syncthreads();
+    unsigned at = inc - sum, total = 0;
+    for (int w = 0; w < kBlock / 64; ++w) {
+        if (w < wave) at += s_psum[w];
+        total += s_psum[w];
+    }
+    for (unsigned r = r0; r < r1; ++r) {
+        g_pref[r] = at;
+        at += cnt[r];
+    }
+    if (threadIdx.x == 0) g_pref[nreg] = total;
+    __syncthreads();
+    return total;
+}
+// Entry j (< g_pref[nreg]) of the region list: region r with g_pref[r] <= j < g_pref[r + 1] (the last r with
+// g_pref[r] <= j: empty regions are skipped), its entry j - g_pref[r].
+__device__ __forceinline__ unsigned region_task(const unsigned* q, unsigned cap, unsigned nreg, unsigned j) {
+    unsigned lo = 0, hi = nreg;
+    while (hi - lo > 1u) {
+        const unsigned mid = (lo + hi) >> 1;
+        if (g_pref[mid] <= j) lo = mid;
+        else hi = mid;
+    }
+    return q[(size_t)lo * cap + (j - g_pref[lo])];
+}
+// A shadow-task list: a packed array (REG false) or the phase-A regions through g_pref (REG true).
+template <bool REG>
+struct TaskList {
+    const unsigned* q;
+    unsigned cap, nreg;
+    __device__ __forceinline__ unsigned operator[](unsigned j) const {
+        if constexpr (REG) return region_task(q, cap, nreg, j);
+        else return q[j];
+    }
+};
+__device__ __forceinline__ TaskList<false> flat_list(const unsigned* q) { return TaskList<false>{q, 0u, 0u}; }
+__device__ __forceinline__ TaskList<true> shadow_regions_a(const PcParams& p) {
+    return TaskList<true>{p.sqA, p.scapA, (unsigned)p.grid};
+}
+__device__ __forceinline__ unsigned cont_entry(const PcParams& p, unsigned j) {   // continuation j (region order)
+    return region_task(p.cq, p.ccapA, (unsigned)p.grid, j);
+}
+
+
 __device__ __forceinline__ Ray shadow_from_record(const rtk::DevScene& s, const PcParams& p, unsigned owner,
                                                   float* tlim, const UDiv& nl) {
     const unsigned lvp = nl.div(owner);
@@ -534,15 +601,16 @@ __device__ __forceinline__ unsigned mix_sample(const PcParams& p, unsigned code,
 // record each hit, queue its shadow tasks, follow (or hand on) mirrors.
 // DBG (k_chain<false, true>, rt_primary_hits_production): also store each sample's level-0 hit (PcParams::dbg_t,
 // dbg_m) -- the same walk, two stores added.
+// nconts (phase B): the continuations (BQ: region_prefix of ccnt in g_pref).
 template <bool COUNT, bool CONT, bool BQ = CONT, bool DBG = false>
 __device__ void chain_body(const rtk::DevScene& s, const rtk::Eye& e, const PcParams& p, unsigned blk, unsigned G,
-                           const PhaseOut& o) {
+                           const PhaseOut& o, unsigned nconts = 0) {
     WalkStack stk;
     Work w;
     uint32_t nprim = 0, nrefl = 0, nskip = 0, nhit = 0, ncont = 0;
     const int nl = s.nlights;
     unsigned nb;
-    if (CONT) nb = chunk_count(min(p.totals[1], p.cb), G, blk, (unsigned)p.tchunk);   // the rest: k_fallback
+    if (CONT) nb = chunk_count(min(nconts, p.cb), G, blk, (unsigned)p.tchunk);   // the rest: k_fallback
     else nb = group_samples((unsigned)p.n0, G, blk);
     // dynamic units (phase A, p.dyn_units > 0): the workgroup's k-th 256-sample unit is not
     // blk + k*G but the next one of a launch-wide counter (p.totals[3], zeroed before the launch),
@@ -705,7 +773,10 @@ __device__ void chain_body(const rtk::DevScene& s, const rtk::Eye& e, const PcPa
                     if (v < nb && uid != kUidNone) {
                         if (CONT) {
                             const unsigned j = chunk_task(v, G, blk, (unsigned)p.tchunk);
-                            const unsigned lvp = p.cflat[j];
+                            // a lone frame (BQ): the region-order list, and its phase-B records' index for
+                            // k_finish (cid); frame batches: k_pack_a's packed list, which stored cid
+                            const unsigned lvp = BQ ? cont_entry(p, j) : p.cflat[j];
+                            if (BQ) p.cid[lvp % (unsigned)p.cap] = j;
                             cix = j;
                             if (kTraceBuild && p.trace) { t_grab = (unsigned)wall_clock64(); tsteps = 0; twit = wit; }
                             path = lvp % (unsigned)p.cap;
@@ -791,9 +862,9 @@ __device__ void chain_body(const rtk::DevScene& s, const rtk::Eye& e, const PcPa
 
 // any-hit of the packed shadow tasks j = blk, blk+G, ... < total
 // (raytracer.cpp:227-280).
-template <bool COUNT>
+template <bool COUNT, class TL>
 __device__ void occlude_body(const rtk::DevScene& s, const PcParams& p, unsigned blk, unsigned G,
-                             const unsigned* tasks, unsigned total, int role) {   // role 0: A's tasks, 1: B's overflow
+                             const TL tasks, unsigned total, int role) {   // role 0: A's tasks, 1: B's overflow
     WalkStack stk;
     Work w;
     uint32_t nrays = 0;
@@ -938,8 +1009,9 @@ __device__ __forceinline__ void lq_flush(const rtk::DevScene& s, const Ray& r, f
 }
 
 // The shadow tasks tasks[j] of this workgroup (as occlude_body) with the leaf queue; production only.
+template <class TL>
 __device__ void occlude_queue_body(const rtk::DevScene& s, const PcParams& p, unsigned blk, unsigned G,
-                                   const unsigned* tasks, unsigned total) {
+                                   const TL tasks, unsigned total) {
     const int lane = lane_id(), wave = (int)(threadIdx.x >> 6);
     const unsigned n = chunk_count(total, G, blk, (unsigned)p.ochunk);
     const UDiv och((unsigned)p.ochunk), nld((unsigned)s.nlights);
@@ -1103,8 +1175,8 @@ __global__ __launch_bounds__(kBlock, COUNT ? 4 : RT_WAVES_PER_EU) void k_chain(r
 
 // Region b of a per-workgroup queue (q[b*cap ..], cnt[b] entries) copied to
 // its place in the packed array: the consumers then index tasks directly.
-// Workgroup 0 stores the total.
-// cid (continuations): cid[sample] = the packed index of its continuation (its phase-B records).
+// Workgroup 0 stores the total.  cid (continuations): cid[sample] = the packed index of its continuation
+// (its phase-B records).
 __device__ void pack_region(const unsigned* q, unsigned cap, const unsigned* cnt, int nreg, unsigned* flat,
                             unsigned* total, unsigned b, unsigned* cid = nullptr, unsigned ncap = 1) {
     __shared__ unsigned s_before, s_all;
@@ -1140,7 +1212,6 @@ __device__ void pack_region(const unsigned* q, unsigned cap, const unsigned* cnt
     __syncthreads();
 }
 
-// After phase A: pack its shadow tasks and continuations (one workgroup per region).
 // The next frame's phase-A unit order (PcParams::uorder, k_mix's last shadow-role workgroup in lone frames):
 // the units by cost class (kHotSteps, the heaviest class first; seven classes: 9 us less per repeated C3
 // frame than three, profiles/r05_ab_rank.txt), each class in the column order (the table ucol, made on the
@@ -1225,8 +1296,8 @@ __device__ void rank_units(const PcParams& p) {
         p.uorder[v] = kUidMix | lg << 28 | (v & ((1u << lg) - 1u)) << 24 | v >> lg;
 }
 
+// Frame batches after phase A: their continuations packed (A's shadow tasks stay in their regions).
 __global__ __launch_bounds__(kBlock) void k_pack_a(PcParams p) {
-    if (!p.occ_inplace) pack_region(p.sqA, p.scapA, p.scntA, p.grid, p.sflatA, &p.totals[0], blockIdx.x);
     pack_region(p.cq, p.ccapA, p.ccnt, p.grid, p.cflat, &p.totals[1], blockIdx.x, p.cid, (unsigned)p.cap);
     if (p.cont_peak && blockIdx.x == 0 && threadIdx.x == 0) atomicMax(p.cont_peak, p.totals[1]);   // (its own write)
 }
@@ -1259,7 +1330,7 @@ __device__ __forceinline__ void occlude_regions(const rtk::DevScene& s, const Pc
             if (threadIdx.x == 0) g_head = 0;
             __syncthreads();
         }
-        occlude_queue_body(s, p, 0, 1, q + (size_t)r * qcap, cnt[r]);
+        occlude_queue_body(s, p, 0, 1, flat_list(q + (size_t)r * qcap), cnt[r]);
     }
 }
 
@@ -1270,17 +1341,26 @@ __global__ __launch_bounds__(kBlock, BQ || COUNT ? RT_MIX_WAVES : RT_MIX_NOBQ_WA
     if (threadIdx.x == 0) g_ccnt = 0;
     if (BQ && chain && kBq > 0) bq_init();
     block_init(s);
+    // the role's phase-A list: a lone frame's (BQ) continuations or A's shadow tasks in region order (g_pref);
+    // frame batches' continuations packed by k_pack_a (which also stored their count)
+    unsigned total;
+    if constexpr (BQ) total = region_prefix(chain ? p.ccnt : p.scntA, (unsigned)p.grid);
+    else total = p.totals[1];
     if (chain) {
+        if (BQ && blockIdx.x == 0 && threadIdx.x == 0) {
+            p.totals[1] = total;                       // the launch's continuations (k_fallback, the host)
+            if (p.cont_peak) atomicMax(p.cont_peak, total);
+        }
         if (p.bprio) __builtin_amdgcn_s_setprio(3);    // the deep chains are the frame's critical path
-        chain_body<COUNT, true, BQ>(s, e, p, blockIdx.x, (unsigned)p.gb, phase_b(p));
-    } else {
+        chain_body<COUNT, true, BQ>(s, e, p, blockIdx.x, (unsigned)p.gb, phase_b(p), total);
+    } else if constexpr (BQ) {                          // (the shadow role: lone frames only)
         if constexpr (!COUNT && RT_LEAF_QUEUE)
-            occlude_queue_body(s, p, blockIdx.x - p.gb, gridDim.x - p.gb, p.sflatA, p.totals[0]);
+            occlude_queue_body(s, p, blockIdx.x - p.gb, gridDim.x - p.gb, shadow_regions_a(p), total);
         else
-            occlude_body<COUNT>(s, p, blockIdx.x - p.gb, gridDim.x - p.gb, p.sflatA, p.totals[0], 0);
+            occlude_body<COUNT>(s, p, blockIdx.x - p.gb, gridDim.x - p.gb, shadow_regions_a(p), total, 0);
     }
     // a lone frame's next unit order, by the last shadow-role workgroup once its shadow rays are done:
-    // beside phase B's deep chains, off the frame's critical path (in k_pack_a it cost 30 us there)
+    // beside phase B's deep chains, off the frame's critical path (in a packing pass it cost 30 us there)
     if (!COUNT && !chain && p.urank && blockIdx.x == gridDim.x - 1) rank_units(p);
 }
 
@@ -1293,16 +1373,13 @@ __global__ __launch_bounds__(kBlock, RT_OCC_WAVES_PER_EU) void k_occlude(rtk::De
         // one region at a time (no packed copy of 4 B in and out per task): A's in frame batches, B's
         // LDS-queue overflow in lone frames (few tasks; no k_pack_b launch on the frame's critical path)
         const bool inplace = which ? p.occ_inplace_b != 0 : p.occ_inplace != 0;
-        if (inplace) {
-            occlude_regions(s, p, which, blockIdx.x, gridDim.x);
-        } else if (which) {
-            occlude_queue_body(s, p, blockIdx.x, gridDim.x, p.sflatB, p.totals[2]);
-        } else {
-            occlude_queue_body(s, p, blockIdx.x, gridDim.x, p.sflatA, p.totals[0]);
-        }
+        // (production A's tasks here are always in place: p.occ_inplace with p.split_occ; no g_pref in this
+        // kernel, whose 6 waves per SIMD need its LDS)
+        if (inplace || !which) occlude_regions(s, p, which, blockIdx.x, gridDim.x);
+        else occlude_queue_body(s, p, blockIdx.x, gridDim.x, flat_list(p.sflatB), p.totals[2]);
     } else {
-        if (which) occlude_body<COUNT>(s, p, blockIdx.x, gridDim.x, p.sflatB, p.totals[2], 1);
-        else occlude_body<COUNT>(s, p, blockIdx.x, gridDim.x, p.sflatA, p.totals[0], 0);
+        if (which) occlude_body<COUNT>(s, p, blockIdx.x, gridDim.x, flat_list(p.sflatB), p.totals[2], 1);
+        else occlude_body<COUNT>(s, p, blockIdx.x, gridDim.x, shadow_regions_a(p), region_prefix(p.scntA, (unsigned)p.grid), 0);
     }
 }
 
@@ -1513,17 +1590,17 @@ __device__ __forceinline__ bool pixel_cont(const PcParams& p, int rr, int ocol) 
     return cont;
 }
 
-// p.fin_cont (chain path): the pixels of the paths continued in phase B first (cflat, totals[1] of
-// them; each pixel once, by the lane holding its first continued sample), so their long folds
+// p.fin_cont (chain path): the pixels of the paths continued in phase B first (phase A's continuation
+// regions; each pixel once, by the lane holding its first continued sample), so their long folds
 // overlap the rest; then every pixel without a continued sample (pinfo's kPathCont bit).
 template <bool LDS, bool CMP>
 __device__ __forceinline__ void finish_pixels(const rtk::DevScene& s, const rtk::Eye& e, const PcParams& p) {
     const int F = p.aa;
     const unsigned gtid = blockIdx.x * kBlock + threadIdx.x, gstride = gridDim.x * kBlock;
-    if (p.fin_cont) {
-        const unsigned n = p.totals[1];
-        for (unsigned j = gtid; j < n; j += gstride) {
-            const unsigned path = (p.cflat[j] & ~kFbEye) % (unsigned)p.cap;
+    if (p.fin_cont) {        // the continuations where phase A left them: region r to workgroup r mod G
+        for (unsigned r = blockIdx.x; r < (unsigned)p.grid; r += gridDim.x)
+        for (unsigned j = threadIdx.x, n = p.ccnt[r]; j < n; j += kBlock) {
+            const unsigned path = p.cq[(size_t)r * p.ccapA + j] % (unsigned)p.cap;
             const unsigned tile = path >> 6, lane = path & 63u;
             const int ix = (int)(tile % (unsigned)p.tiles_x) * 8 + (int)(lane & 7u);
             const int iyc = (int)(tile / (unsigned)p.tiles_x) * 8 + (int)(lane >> 3);
@@ -1593,7 +1670,7 @@ __device__ __forceinline__ bool fallback_any(const rtk::DevScene& s, const Ray& 
 }
 
 __device__ void fallback_chain(const rtk::DevScene& s, const rtk::Eye& e, const PcParams& p, unsigned entry,
-                               WalkStack& stk, Work& w, bool cont = false) {   // cont: a continuation (cflat)
+                               WalkStack& stk, Work& w, bool cont = false) {   // cont: a continuation (cont_entry)
     const unsigned cap = (unsigned)p.cap;
     unsigned path;
     int k;
@@ -1611,7 +1688,7 @@ __device__ void fallback_chain(const rtk::DevScene& s, const rtk::Eye& e, const 
         } else {
             const size_t q = entry - aspace;
             kprev = p.la + (int)(q / p.cb);
-            path = (p.cflat[q % p.cb] & ~kFbEye) % cap;
+            path = cont_entry(p, (unsigned)(q % p.cb)) % cap;   // (k_fallback: g_pref holds the continuations)
         }
         k = kprev + 1;
         r = reflect_from_record(s, p, entry, path);
@@ -1674,11 +1751,12 @@ __device__ void fallback_chain(const rtk::DevScene& s, const rtk::Eye& e, const 
 
 __global__ __launch_bounds__(kBlock) void k_fallback(rtk::DevScene s, rtk::Eye e, PcParams p) {
     block_init(s);
+    const unsigned ncont = region_prefix(p.ccnt, (unsigned)p.grid);   // the continuation list (cont_entry)
     WalkStack stk;
     Work w;
     const unsigned gt = blockIdx.x * kBlock + threadIdx.x, gs = gridDim.x * kBlock;
     const unsigned nfc = min(p.totals[4], p.fbc_cap);
-    const unsigned ncont = p.totals[1], novf = ncont > p.cb ? ncont - p.cb : 0u;
+    const unsigned novf = ncont > p.cb ? ncont - p.cb : 0u;
     if (gt == 0 && p.counters) {                   // what this launch left to k_fallback (rt_counters_read_raw)
         atomicAdd(&p.counters[kCntFbLaunches], 1ull);
         atomicAdd(&p.counters[kCntFbConts], (unsigned long long)ncont);
@@ -1689,7 +1767,7 @@ __global__ __launch_bounds__(kBlock) void k_fallback(rtk::DevScene s, rtk::Eye e
         if (p.clevels) atomicAdd(&p.counters[kCntCompactLaunches], 1ull);
     }
     for (unsigned i = gt; i < nfc + novf; i += gs)
-        fallback_chain(s, e, p, i < nfc ? p.fbc[i] : p.cflat[p.cb + (i - nfc)], stk, w, i >= nfc);
+        fallback_chain(s, e, p, i < nfc ? p.fbc[i] : cont_entry(p, p.cb + (i - nfc)), stk, w, i >= nfc);
     const unsigned nfs = min(p.totals[5], p.fbs_cap);
     for (unsigned i = gt; i < nfs; i += gs) {
         const unsigned owner = p.fbs[i];
@@ -1888,18 +1966,19 @@ hipError_t launch_chain_chunk(const rtk::DevScene& s, const rtk::Eye& e, const P
                               hipStream_t st, KTimer* kt) {
     const dim3 blk(kBlock);
     const bool phase_b = p.kinline < s.max_depth;     // any continuation possible
-    {   // the dynamic unit counter and k_fallback's counts
-        const hipError_t me = hipMemsetAsync(p.totals + 3, 0, (kTotalsWords - 3) * sizeof(unsigned), st);
+    {   // the task counts (k_mix stores the continuations'), the dynamic unit counter, k_fallback's counts
+        const hipError_t me = hipMemsetAsync(p.totals, 0, kTotalsWords * sizeof(unsigned), st);
         if (me != hipSuccess) return me;
     }
     if (count) RT_LAUNCH(kt, kKChain, k_chain<true>, dim3(p.grid), blk, st, s, e, p);
     else if (p.dbg_t) RT_LAUNCH(kt, kKChain, (k_chain<false, true>), dim3(p.grid), blk, st, s, e, p);
     else RT_LAUNCH(kt, kKChain, k_chain<false>, dim3(p.grid), blk, st, s, e, p);
-    RT_LAUNCH(kt, kKPackA, k_pack_a, dim3(p.grid), blk, st, p);
+    // frame batches: their continuations packed; a lone frame's k_mix reads phase A's regions (region_prefix)
+    if (p.split_occ) RT_LAUNCH(kt, kKPackA, k_pack_a, dim3(p.grid), blk, st, p);
     PcParams q = p;
     if (!phase_b) q.gb = 0;
     // p.split_occ (frame batches): k_mix only walks the chains, A's shadow tasks go to k_occlude (5 waves
-    // per SIMD; in place where p.occ_inplace, k_pack_a then leaving them unpacked); otherwise k_mix's other
+    // per SIMD; in place, p.occ_inplace); otherwise k_mix's other
     // workgroups walk them beside the chains.  Frame batches without phase B (depth 0): no k_mix at all
     const bool split = p.split_occ != 0;
     const int mgrid = split ? q.gb : q.gb + p.ogrid;

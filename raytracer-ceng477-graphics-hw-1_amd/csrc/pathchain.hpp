@@ -25,7 +25,8 @@
 
 namespace rtc {
 
-constexpr int kMaxChainGrid = 2048;   // k_chain workgroups (= task-queue regions)
+constexpr int kMaxChainGrid = 1280;   // k_chain workgroups (= task-queue regions; 5 per CU on 256 CUs): the
+                                      // consumers' LDS region prefix (pathchain.hip g_pref) holds this many
 constexpr int kMaxFrames = 32;        // frames of one batched launch (PcParams kernarg: 64 B each) (rt_render_frames_device)
 #ifndef RT_BQ
 #define RT_BQ 1536
@@ -111,7 +112,7 @@ __host__ __device__ inline unsigned unit_col(int tiles_x, int ublk_h, int ublk_w
     return (r0 + l / w) * upr + c0 + l % w;
 }
 
-// PcParams::totals words: packed task counts (0-2), the phase-A unit counter (3), k_fallback's chain /
+// PcParams::totals words: task counts (1-2), the phase-A unit counter (3), k_fallback's chain /
 // shadow counts and shadow-queue overflow (4-6), the rest spare.
 constexpr int kTotalsWords = 12;
 
@@ -144,7 +145,7 @@ struct PcParams {
     uint8_t* occ;
     int la;           // levels stored for every sample (phase A's; all levels on the fused path)
     unsigned cb;      // continuations with records (the rest finish in k_fallback)
-    unsigned* cid;    // [cap]: continuation index of a continued sample (k_pack_a)
+    unsigned* cid;    // [cap]: continuation index of a continued sample (k_pack_a; a lone frame's k_mix at its grab)
     float4* tail;     // [cap]: folded colour of the levels k_fallback finished (kEndTail)
     // k_fallback's work: rays the timed walks do not take (NaN-free and in range for the wide trees'
     // fused slab test, wide_walk_ok) and continuations beyond cb.  fbc: chain entries (kFbEye | sample
@@ -156,20 +157,23 @@ struct PcParams {
     unsigned fbs_cap;
     int fb_grid;      // k_fallback workgroups
     // phase A (k_chain: levels [0, kinline]) and phase B (k_mix chain role: deeper levels).
-    // Task queues hold u32 owner ids; per-workgroup regions, counts, exclusive prefixes.
+    // Task queues hold u32 owner ids in per-workgroup regions with their counts; phase A's are read in place
+    // as one list in region order (pathchain.hip region_prefix) or region by region, except frame batches'
+    // continuations (k_pack_a); phase B's overflow packed (k_pack_b) in frame batches.
     unsigned* sqA;    // shadow tasks of A: [grid][scapA], owner = (level*cap + sample)*nl + light
     unsigned scapA;
     unsigned* scntA;  // [grid]
-    unsigned* sflatA; // A's shadow tasks packed in region order (k_pack_a), totals[0] of them
+    unsigned* spare0; // (unused: the walk kernels' SGPR allocation follows the argument layout)
     unsigned* cq;     // continuations of A: [grid][ccapA], owner = level*cap + sample of the last record
     unsigned ccapA;
     unsigned* ccnt;   // [grid]
-    unsigned* cflat;  // continuations packed (k_pack_a), totals[1] of them
+    unsigned* cflat;  // frame batches: continuations packed in region order (k_pack_a), totals[1] of them
     unsigned* sqB;    // shadow tasks of B: [gb][scapB]
     unsigned scapB;
     unsigned* scntB;  // [gb]
     unsigned* sflatB; // B's shadow tasks packed (k_pack_b), totals[2] of them
-    unsigned* totals; // [kTotalsWords]: packed task counts (3), phase-A unit counter, k_fallback chains / shadows /
+    unsigned* totals; // [kTotalsWords]: task counts (1: A's continuations, k_pack_a / k_mix; 2: B's packed overflow), the
+                      // phase-A unit counter, k_fallback chains / shadows /
                       // overflow
     int kinline;      // deepest level phase A walks (>= max_depth: no phase B)
     int gb;           // k_mix workgroups in the chain role (the other p.ogrid ones occlude A's tasks)
@@ -195,7 +199,7 @@ struct PcParams {
     int occ_inplace;  // 1 (split_occ production launches): k_occlude walks A's shadow tasks in their phase-A
                       // regions (workgroup w: regions w, w + G, ...); k_pack_a packs only the continuations
     int fin_grid;     // k_finish workgroups at most (0: a lane per output pixel), a grid-stride loop beyond
-    int fin_cont;     // k_finish: the continued paths' pixels first (chain path: cflat, totals[1], kPathCont)
+    int fin_cont;     // k_finish: the continued paths' pixels first (chain path: the continuation list, kPathCont)
     int refill;       // a wave refills once <= refill of its lanes are still walking
     int orefill;      // the same for the shadow (any-hit) walks
     int brefill;      // the same for phase-B chains
@@ -222,7 +226,7 @@ struct PcParams {
     int trace_blocks;
     // (new fields at the end: kernel arguments are loaded in runs of neighbours, so a field inserted
     // among the walk kernels' ones changed their SGPR spills 28 -> 67)
-    unsigned* cont_peak;  // frames of several chunks: the most continuations of one chunk (k_pack_a, atomicMax)
+    unsigned* cont_peak;  // frames of several chunks: the most continuations of one chunk (k_mix / k_pack_a, atomicMax)
     // Diagnostics (rt_primary_hits_production): each sample's level-0 closest hit as the TIMED walk found it
     // -- tSmall (-1 on a miss) and material id (0 on a miss) at internal pixel row * wi + col -- written by
     // k_chain<false, true> (the production kernel with these two stores added) and, for an eye ray the

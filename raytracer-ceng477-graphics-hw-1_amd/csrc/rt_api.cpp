@@ -189,7 +189,7 @@ struct rt_scene {
         uint64_t hist_key = 0;               // the launch geometry uorder was ranked for (0: none yet)
     } arenas[kSlots];
     // continuation share of frame batches (phase B's record space, cb): each batched launch copies its
-    // continuation count (k_pack_a's total) to pinned memory behind it; once that copy is done the share
+    // continuation count (k_pack_a's or k_mix's total) to pinned memory behind it; once that copy is done the share
     // is folded into cont_frac, which sizes the next launches' cb (and so their frames per launch)
     double cont_frac = 0;                      // 0: none seen yet (cap / kContDen)
     unsigned* h_cont = nullptr;                // pinned, per slot
@@ -633,7 +633,7 @@ struct ChainPlan {
     // arena offsets
     size_t dbase = 0;               // records below it without directions (pathchain.hpp)
     int clevels = 0;
-    size_t o_rec = 0, o_recd = 0, o_pinfo = 0, o_occ = 0, o_sqA = 0, o_scntA = 0, o_sflatA = 0, o_cq = 0, o_ccnt = 0,
+    size_t o_rec = 0, o_recd = 0, o_pinfo = 0, o_occ = 0, o_sqA = 0, o_scntA = 0, o_cq = 0, o_ccnt = 0,
            o_cflat = 0, o_sqB = 0, o_scntB = 0, o_sflatB = 0, o_totals = 0, o_cid = 0, o_tail = 0,
            o_fbc = 0, o_fbs = 0, bytes = 0;
 };
@@ -753,9 +753,8 @@ ChainPlan chain_plan(const rt_scene* s, const ChainGeom& g, size_t nunits, bool 
     P.o_fbs = L.take<unsigned>(cap);
     {
         P.o_sqA = L.take<unsigned>((size_t)P.G * P.scapA); P.o_scntA = L.take<unsigned>(P.G);
-        P.o_sflatA = L.take<unsigned>(cap * P.levels_a * nl);
         P.o_cq = L.take<unsigned>((size_t)P.G * P.ccapA); P.o_ccnt = L.take<unsigned>(P.G);
-        P.o_cflat = L.take<unsigned>(cap);
+        if (P.split_occ) P.o_cflat = L.take<unsigned>(cap);   // frame batches' packed continuations (k_pack_a)
         P.o_sqB = L.take<unsigned>((size_t)P.gb * P.scapB); P.o_scntB = L.take<unsigned>(P.gb + 1);
         P.o_sflatB = L.take<unsigned>(P.cb * (levels - P.la) * nl);
     }
@@ -821,7 +820,7 @@ void poll_cont(rt_scene* s, bool wait) {
     }
 }
 
-// A launch's continuation count (k_pack_a's total, or a frame's chunk peak) copied to pinned memory behind
+// A launch's continuation count (k_pack_a's or k_mix's total, or a frame's chunk peak) copied to pinned memory behind
 // it on `st`; poll_cont folds it into the scene's continuation share once the copy is done.
 int read_back_cont(rt_scene* s, hipStream_t st, int slot, const unsigned* src, size_t cap) {
     if (!s->h_cont) HIP_TRY(hipHostMalloc(reinterpret_cast<void**>(&s->h_cont), rt_scene::kSlots * sizeof(unsigned)));
@@ -857,7 +856,7 @@ int render_chain(rt_scene* s, const rtk::Eye& eye, const rtk::FrameParams& f, bo
     const int nchunks = (li + chunk_rows - 1) / chunk_rows;
     const int K = std::min({nchunks, s->tune_slots, rt_scene::kSlots});
     // a frame of several chunks reports its chunks' largest continuation share (the record space must
-    // hold the mirror-heavy chunks', not the last chunk's): k_pack_a's atomicMax into one word, cleared
+    // hold the mirror-heavy chunks', not the last chunk's): k_mix's / k_pack_a's atomicMax into one word, cleared
     // here, on the caller's stream before the chunks fork
     const bool peak = nchunks > 1 && !count && P.phase_b && s->tune_cont_cb == 0;
     if (peak && f.chunk_k == 1) {
@@ -916,9 +915,10 @@ int render_chain(rt_scene* s, const rtk::Eye& eye, const rtk::FrameParams& f, bo
     p.pinfo = static_cast<int*>(at(P.o_pinfo));
     p.occ = static_cast<uint8_t*>(at(P.o_occ));
     p.sqA = static_cast<unsigned*>(at(P.o_sqA)); p.scapA = P.scapA;
-    p.scntA = static_cast<unsigned*>(at(P.o_scntA)); p.sflatA = static_cast<unsigned*>(at(P.o_sflatA));
+    p.scntA = static_cast<unsigned*>(at(P.o_scntA));
     p.cq = static_cast<unsigned*>(at(P.o_cq)); p.ccapA = P.ccapA;
-    p.ccnt = static_cast<unsigned*>(at(P.o_ccnt)); p.cflat = static_cast<unsigned*>(at(P.o_cflat));
+    p.ccnt = static_cast<unsigned*>(at(P.o_ccnt));
+    p.cflat = P.split_occ ? static_cast<unsigned*>(at(P.o_cflat)) : nullptr;
     p.sqB = static_cast<unsigned*>(at(P.o_sqB)); p.scapB = P.scapB;
     p.scntB = static_cast<unsigned*>(at(P.o_scntB)); p.sflatB = static_cast<unsigned*>(at(P.o_sflatB));
     p.totals = static_cast<unsigned*>(at(P.o_totals));
@@ -940,10 +940,10 @@ int render_chain(rt_scene* s, const rtk::Eye& eye, const rtk::FrameParams& f, bo
     p.occ_grid = s->occl_grid;
     p.fin_grid = 8 * s->num_cus;        // k_finish: at most 8 workgroups per CU (dispatch-bound at a lane per pixel)
     p.split_occ = P.split_occ ? 1 : 0;
-    // A's shadow tasks walked where k_chain left them by k_occlude in frame batches (a lone frame's k_mix
-    // shadow role deals them packed: in place, its uneven regions cost k_mix +60 us, k_pack_a -10); B's
-    // LDS-queue overflow likewise in a lone frame.  The in-place walks are the leaf-queue walker's
-    // (RT_LEAF_QUEUE builds), the only device code that reads task regions unpacked.
+    // A's shadow tasks walked where k_chain left them, region by region, by k_occlude in frame batches (a
+    // lone frame's k_mix shadow role deals them in chunks of the region-order list instead, region_prefix:
+    // region by region, their uneven sizes cost k_mix +60 us); B's LDS-queue overflow region by region in a
+    // lone frame.  The region-by-region walks are the leaf-queue walker's (RT_LEAF_QUEUE builds).
     p.occ_inplace = RT_LEAF_QUEUE && !count && P.split_occ ? 1 : 0;
     p.occ_inplace_b = RT_LEAF_QUEUE && !P.split_occ && !count ? 1 : 0;
     p.cont_peak = peak ? s->d_cont_peak : nullptr;
@@ -1025,7 +1025,7 @@ int render_chain(rt_scene* s, const rtk::Eye& eye, const rtk::FrameParams& f, bo
             }
             p.urank = 1;
             p.uorder_on = arena.hist_key == key ? 1 : 0;   // ranked by the previous frame of this geometry
-            arena.hist_key = key;                          // (its k_pack_a ran before this k_chain: stream order)
+            arena.hist_key = key;                          // (its k_mix ran before this k_chain: stream order)
         }
         if (p.grid > P.G) return fail(RT_ERR_LIMIT, "internal: chain grid exceeds the workspace");
         if (s->ktime) {
