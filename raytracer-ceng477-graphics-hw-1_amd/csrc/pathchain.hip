@@ -773,10 +773,13 @@ __device__ void chain_body(const rtk::DevScene& s, const rtk::Eye& e, const PcPa
                     if (v < nb && uid != kUidNone) {
                         if (CONT) {
                             const unsigned j = chunk_task(v, G, blk, (unsigned)p.tchunk);
-                            // a lone frame (BQ): the region-order list, and its phase-B records' index for
-                            // k_finish (cid); frame batches: k_pack_a's packed list, which stored cid
+                            // a lone frame (BQ): the region-order list, and for k_finish its phase-B records'
+                            // index (cid) and the packed entry; frame batches: k_pack_a's packed list and cid
                             const unsigned lvp = BQ ? cont_entry(p, j) : p.cflat[j];
-                            if (BQ) p.cid[lvp % (unsigned)p.cap] = j;
+                            if (BQ) {
+                                p.cid[lvp % (unsigned)p.cap] = j;
+                                p.cflat[j] = lvp;
+                            }
                             cix = j;
                             if (kTraceBuild && p.trace) { t_grab = (unsigned)wall_clock64(); tsteps = 0; twit = wit; }
                             path = lvp % (unsigned)p.cap;
@@ -1590,17 +1593,18 @@ __device__ __forceinline__ bool pixel_cont(const PcParams& p, int rr, int ocol) 
     return cont;
 }
 
-// p.fin_cont (chain path): the pixels of the paths continued in phase B first (phase A's continuation
-// regions; each pixel once, by the lane holding its first continued sample), so their long folds
+// p.fin_cont (chain path): the pixels of the paths continued in phase B first (the packed continuations,
+// cflat: k_pack_a's, or a lone frame's k_mix / k_fallback stored them at their grab; each pixel once, by the
+// lane holding its first continued sample), so their long folds
 // overlap the rest; then every pixel without a continued sample (pinfo's kPathCont bit).
 template <bool LDS, bool CMP>
 __device__ __forceinline__ void finish_pixels(const rtk::DevScene& s, const rtk::Eye& e, const PcParams& p) {
     const int F = p.aa;
     const unsigned gtid = blockIdx.x * kBlock + threadIdx.x, gstride = gridDim.x * kBlock;
-    if (p.fin_cont) {        // the continuations where phase A left them: region r to workgroup r mod G
-        for (unsigned r = blockIdx.x; r < (unsigned)p.grid; r += gridDim.x)
-        for (unsigned j = threadIdx.x, n = p.ccnt[r]; j < n; j += kBlock) {
-            const unsigned path = p.cq[(size_t)r * p.ccapA + j] % (unsigned)p.cap;
+    if (p.fin_cont) {
+        const unsigned n = p.totals[1];
+        for (unsigned j = gtid; j < n; j += gstride) {
+            const unsigned path = (p.cflat[j] & ~kFbEye) % (unsigned)p.cap;
             const unsigned tile = path >> 6, lane = path & 63u;
             const int ix = (int)(tile % (unsigned)p.tiles_x) * 8 + (int)(lane & 7u);
             const int iyc = (int)(tile / (unsigned)p.tiles_x) * 8 + (int)(lane >> 3);
@@ -1766,8 +1770,16 @@ __global__ __launch_bounds__(kBlock) void k_fallback(rtk::DevScene s, rtk::Eye e
         if (p.totals[6]) atomicAdd(&p.counters[kCntFbOvfScans], 1ull);
         if (p.clevels) atomicAdd(&p.counters[kCntCompactLaunches], 1ull);
     }
-    for (unsigned i = gt; i < nfc + novf; i += gs)
-        fallback_chain(s, e, p, i < nfc ? p.fbc[i] : cont_entry(p, p.cb + (i - nfc)), stk, w, i >= nfc);
+    for (unsigned i = gt; i < nfc + novf; i += gs) {
+        unsigned entry;
+        if (i < nfc) {
+            entry = p.fbc[i];
+        } else {                                   // a continuation beyond cb (packed for k_finish: a lone frame)
+            entry = cont_entry(p, p.cb + (i - nfc));
+            p.cflat[p.cb + (i - nfc)] = entry;
+        }
+        fallback_chain(s, e, p, entry, stk, w, i >= nfc);
+    }
     const unsigned nfs = min(p.totals[5], p.fbs_cap);
     for (unsigned i = gt; i < nfs; i += gs) {
         const unsigned owner = p.fbs[i];

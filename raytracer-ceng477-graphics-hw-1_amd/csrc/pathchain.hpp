@@ -167,7 +167,8 @@ struct PcParams {
     unsigned* cq;     // continuations of A: [grid][ccapA], owner = level*cap + sample of the last record
     unsigned ccapA;
     unsigned* ccnt;   // [grid]
-    unsigned* cflat;  // frame batches: continuations packed in region order (k_pack_a), totals[1] of them
+    unsigned* cflat;  // continuations packed in region order (k_pack_a; a lone frame's k_mix / k_fallback at their
+                      // grab), totals[1] of them
     unsigned* sqB;    // shadow tasks of B: [gb][scapB]
     unsigned scapB;
     unsigned* scntB;  // [gb]

@@ -754,7 +754,7 @@ ChainPlan chain_plan(const rt_scene* s, const ChainGeom& g, size_t nunits, bool 
     {
         P.o_sqA = L.take<unsigned>((size_t)P.G * P.scapA); P.o_scntA = L.take<unsigned>(P.G);
         P.o_cq = L.take<unsigned>((size_t)P.G * P.ccapA); P.o_ccnt = L.take<unsigned>(P.G);
-        if (P.split_occ) P.o_cflat = L.take<unsigned>(cap);   // frame batches' packed continuations (k_pack_a)
+        P.o_cflat = L.take<unsigned>(cap);   // packed continuations (k_pack_a; a lone frame's k_mix / k_fallback)
         P.o_sqB = L.take<unsigned>((size_t)P.gb * P.scapB); P.o_scntB = L.take<unsigned>(P.gb + 1);
         P.o_sflatB = L.take<unsigned>(P.cb * (levels - P.la) * nl);
     }
@@ -918,7 +918,7 @@ int render_chain(rt_scene* s, const rtk::Eye& eye, const rtk::FrameParams& f, bo
     p.scntA = static_cast<unsigned*>(at(P.o_scntA));
     p.cq = static_cast<unsigned*>(at(P.o_cq)); p.ccapA = P.ccapA;
     p.ccnt = static_cast<unsigned*>(at(P.o_ccnt));
-    p.cflat = P.split_occ ? static_cast<unsigned*>(at(P.o_cflat)) : nullptr;
+    p.cflat = static_cast<unsigned*>(at(P.o_cflat));
     p.sqB = static_cast<unsigned*>(at(P.o_sqB)); p.scapB = P.scapB;
     p.scntB = static_cast<unsigned*>(at(P.o_scntB)); p.sflatB = static_cast<unsigned*>(at(P.o_sflatB));
     p.totals = static_cast<unsigned*>(at(P.o_totals));
