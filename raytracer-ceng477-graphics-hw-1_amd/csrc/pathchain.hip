@@ -441,29 +441,41 @@ __device__ __noinline__ unsigned region_prefix(const unsigned* cnt, unsigned nre
 }
 // Entry j (< g_pref[nreg]) of the region list: region r with g_pref[r] <= j < g_pref[r + 1] (the last r with
 // g_pref[r] <= j: empty regions are skipped), its entry j - g_pref[r].
-__device__ __forceinline__ unsigned region_task(const unsigned* q, unsigned cap, unsigned nreg, unsigned j) {
+__device__ __forceinline__ unsigned region_of(unsigned nreg, unsigned j) {
     unsigned lo = 0, hi = nreg;
     while (hi - lo > 1u) {
         const unsigned mid = (lo + hi) >> 1;
         if (g_pref[mid] <= j) lo = mid;
         else hi = mid;
     }
-    return q[(size_t)lo * cap + (j - g_pref[lo])];
+    return lo;
 }
-// A shadow-task list: a packed array (REG false) or the phase-A regions through g_pref (REG true).
+__device__ __forceinline__ unsigned region_task(const unsigned* q, unsigned cap, unsigned nreg, unsigned j) {
+    const unsigned r = region_of(nreg, j);
+    return q[(size_t)r * cap + (j - g_pref[r])];
+}
+// A shadow-task list: a packed array (REG false) or the phase-A regions through g_pref (REG true).  The shadow
+// walkers take tasks in chunks of consecutive indices, so a lane's next task is nearly always in its previous
+// one's region (hint): two LDS reads instead of the search's eleven.
 template <bool REG>
 struct TaskList {
     const unsigned* q;
-    unsigned cap, nreg;
-    __device__ __forceinline__ unsigned operator[](unsigned j) const {
-        if constexpr (REG) return region_task(q, cap, nreg, j);
-        else return q[j];
+    unsigned cap, nreg, hint;
+    __device__ __forceinline__ unsigned operator[](unsigned j) {
+        if constexpr (REG) {
+            unsigned r = hint;
+            if (!(g_pref[r] <= j && j < g_pref[r + 1])) hint = r = region_of(nreg, j);
+            return q[(size_t)r * cap + (j - g_pref[r])];
+        } else {
+            return q[j];
+        }
     }
 };
-__device__ __forceinline__ TaskList<false> flat_list(const unsigned* q) { return TaskList<false>{q, 0u, 0u}; }
+__device__ __forceinline__ TaskList<false> flat_list(const unsigned* q) { return TaskList<false>{q, 0u, 0u, 0u}; }
 __device__ __forceinline__ TaskList<true> shadow_regions_a(const PcParams& p) {
-    return TaskList<true>{p.sqA, p.scapA, (unsigned)p.grid};
+    return TaskList<true>{p.sqA, p.scapA, (unsigned)p.grid, 0u};
 }
+
 __device__ __forceinline__ unsigned cont_entry(const PcParams& p, unsigned j) {   // continuation j (region order)
     return region_task(p.cq, p.ccapA, (unsigned)p.grid, j);
 }
@@ -601,8 +613,9 @@ __device__ __forceinline__ unsigned mix_sample(const PcParams& p, unsigned code,
 // record each hit, queue its shadow tasks, follow (or hand on) mirrors.
 // DBG (k_chain<false, true>, rt_primary_hits_production): also store each sample's level-0 hit (PcParams::dbg_t,
 // dbg_m) -- the same walk, two stores added.
-// nconts (phase B): the continuations (BQ: region_prefix of ccnt in g_pref).
-template <bool COUNT, bool CONT, bool BQ = CONT, bool DBG = false>
+// nconts (phase B): the continuations.  RL (a whole lone frame, PcParams::rlists): read in region order through
+// g_pref (region_prefix); otherwise k_pack_a's packed list.
+template <bool COUNT, bool CONT, bool BQ = CONT, bool DBG = false, bool RL = false>
 __device__ void chain_body(const rtk::DevScene& s, const rtk::Eye& e, const PcParams& p, unsigned blk, unsigned G,
                            const PhaseOut& o, unsigned nconts = 0) {
     WalkStack stk;
@@ -773,10 +786,10 @@ __device__ void chain_body(const rtk::DevScene& s, const rtk::Eye& e, const PcPa
                     if (v < nb && uid != kUidNone) {
                         if (CONT) {
                             const unsigned j = chunk_task(v, G, blk, (unsigned)p.tchunk);
-                            // a lone frame (BQ): the region-order list, and for k_finish its phase-B records'
-                            // index (cid) and the packed entry; frame batches: k_pack_a's packed list and cid
-                            const unsigned lvp = BQ ? cont_entry(p, j) : p.cflat[j];
-                            if (BQ) {
+                            // RL: the region-order list, and for k_finish its phase-B records' index (cid) and
+                            // the packed entry; otherwise k_pack_a's list and cid
+                            const unsigned lvp = RL ? cont_entry(p, j) : p.cflat[j];
+                            if (RL) {
                                 p.cid[lvp % (unsigned)p.cap] = j;
                                 p.cflat[j] = lvp;
                             }
@@ -867,7 +880,7 @@ __device__ void chain_body(const rtk::DevScene& s, const rtk::Eye& e, const PcPa
 // (raytracer.cpp:227-280).
 template <bool COUNT, class TL>
 __device__ void occlude_body(const rtk::DevScene& s, const PcParams& p, unsigned blk, unsigned G,
-                             const TL tasks, unsigned total, int role) {   // role 0: A's tasks, 1: B's overflow
+                             TL tasks, unsigned total, int role) {   // role 0: A's tasks, 1: B's overflow
     WalkStack stk;
     Work w;
     uint32_t nrays = 0;
@@ -1014,7 +1027,7 @@ __device__ __forceinline__ void lq_flush(const rtk::DevScene& s, const Ray& r, f
 // The shadow tasks tasks[j] of this workgroup (as occlude_body) with the leaf queue; production only.
 template <class TL>
 __device__ void occlude_queue_body(const rtk::DevScene& s, const PcParams& p, unsigned blk, unsigned G,
-                                   const TL tasks, unsigned total) {
+                                   TL tasks, unsigned total) {
     const int lane = lane_id(), wave = (int)(threadIdx.x >> 6);
     const unsigned n = chunk_count(total, G, blk, (unsigned)p.ochunk);
     const UDiv och((unsigned)p.ochunk), nld((unsigned)s.nlights);
@@ -1299,8 +1312,10 @@ __device__ void rank_units(const PcParams& p) {
         p.uorder[v] = kUidMix | lg << 28 | (v & ((1u << lg) - 1u)) << 24 | v >> lg;
 }
 
-// Frame batches after phase A: their continuations packed (A's shadow tasks stay in their regions).
+// After phase A (frame batches, the chunks of a larger lone frame): the continuations packed, and A's shadow
+// tasks where they are not walked in place (p.sflatA: a lone frame's chunks).
 __global__ __launch_bounds__(kBlock) void k_pack_a(PcParams p) {
+    if (p.sflatA) pack_region(p.sqA, p.scapA, p.scntA, p.grid, p.sflatA, &p.totals[0], blockIdx.x);
     pack_region(p.cq, p.ccapA, p.ccnt, p.grid, p.cflat, &p.totals[1], blockIdx.x, p.cid, (unsigned)p.cap);
     if (p.cont_peak && blockIdx.x == 0 && threadIdx.x == 0) atomicMax(p.cont_peak, p.totals[1]);   // (its own write)
 }
@@ -1337,30 +1352,34 @@ __device__ __forceinline__ void occlude_regions(const rtk::DevScene& s, const Pc
     }
 }
 
-template <bool COUNT, bool BQ>
+// RL (a whole lone frame, PcParams::rlists): phase A's lists read in their regions (g_pref) -- a separate
+// instantiation, since the region code alone, never run, cost the packed variant 5 % in C5's big launches.
+template <bool COUNT, bool BQ, bool RL = false>
 __global__ __launch_bounds__(kBlock, BQ || COUNT ? RT_MIX_WAVES : RT_MIX_NOBQ_WAVES) void k_mix(rtk::DevScene s,
                                                                                                   rtk::Eye e, PcParams p) {
     const bool chain = blockIdx.x < (unsigned)p.gb;
     if (threadIdx.x == 0) g_ccnt = 0;
     if (BQ && chain && kBq > 0) bq_init();
     block_init(s);
-    // the role's phase-A list: a lone frame's (BQ) continuations or A's shadow tasks in region order (g_pref);
-    // frame batches' continuations packed by k_pack_a (which also stored their count)
+    // the role's phase-A list: a whole lone frame's (p.rlists) continuations or A's shadow tasks in region order
+    // (g_pref); otherwise packed by k_pack_a (which also stored their counts)
     unsigned total;
-    if constexpr (BQ) total = region_prefix(chain ? p.ccnt : p.scntA, (unsigned)p.grid);
-    else total = p.totals[1];
+    if constexpr (RL) total = region_prefix(chain ? p.ccnt : p.scntA, (unsigned)p.grid);
+    else total = chain ? p.totals[1] : p.totals[0];
     if (chain) {
-        if (BQ && blockIdx.x == 0 && threadIdx.x == 0) {
+        if (RL && blockIdx.x == 0 && threadIdx.x == 0) {
             p.totals[1] = total;                       // the launch's continuations (k_fallback, the host)
             if (p.cont_peak) atomicMax(p.cont_peak, total);
         }
         if (p.bprio) __builtin_amdgcn_s_setprio(3);    // the deep chains are the frame's critical path
-        chain_body<COUNT, true, BQ>(s, e, p, blockIdx.x, (unsigned)p.gb, phase_b(p), total);
+        chain_body<COUNT, true, BQ, false, RL>(s, e, p, blockIdx.x, (unsigned)p.gb, phase_b(p), total);
     } else if constexpr (BQ) {                          // (the shadow role: lone frames only)
-        if constexpr (!COUNT && RT_LEAF_QUEUE)
-            occlude_queue_body(s, p, blockIdx.x - p.gb, gridDim.x - p.gb, shadow_regions_a(p), total);
-        else
-            occlude_body<COUNT>(s, p, blockIdx.x - p.gb, gridDim.x - p.gb, shadow_regions_a(p), total, 0);
+        const auto tl = [&] {
+            if constexpr (RL) return shadow_regions_a(p);
+            else return flat_list(p.sflatA);
+        }();
+        if constexpr (!COUNT && RT_LEAF_QUEUE) occlude_queue_body(s, p, blockIdx.x - p.gb, gridDim.x - p.gb, tl, total);
+        else occlude_body<COUNT>(s, p, blockIdx.x - p.gb, gridDim.x - p.gb, tl, total, 0);
     }
     // a lone frame's next unit order, by the last shadow-role workgroup once its shadow rays are done:
     // beside phase B's deep chains, off the frame's critical path (in a packing pass it cost 30 us there)
@@ -1904,7 +1923,7 @@ void launch_finish(const rtk::DevScene& s, const rtk::Eye& e, const PcParams& p,
 
 hipError_t chain_occupancy(int* chain_blocks_per_cu, int* mix_blocks_per_cu, int* occlude_blocks_per_cu) {
     hipError_t e = hipOccupancyMaxActiveBlocksPerMultiprocessor(chain_blocks_per_cu, k_chain<false>, kBlock, 0);
-    if (e == hipSuccess) e = hipOccupancyMaxActiveBlocksPerMultiprocessor(mix_blocks_per_cu, k_mix<false, true>, kBlock, 0);
+    if (e == hipSuccess) e = hipOccupancyMaxActiveBlocksPerMultiprocessor(mix_blocks_per_cu, k_mix<false, true, true>, kBlock, 0);
     if (e == hipSuccess)
         e = hipOccupancyMaxActiveBlocksPerMultiprocessor(occlude_blocks_per_cu, k_occlude<false>, kBlock, 0);
     return e;
@@ -1985,8 +2004,8 @@ hipError_t launch_chain_chunk(const rtk::DevScene& s, const rtk::Eye& e, const P
     if (count) RT_LAUNCH(kt, kKChain, k_chain<true>, dim3(p.grid), blk, st, s, e, p);
     else if (p.dbg_t) RT_LAUNCH(kt, kKChain, (k_chain<false, true>), dim3(p.grid), blk, st, s, e, p);
     else RT_LAUNCH(kt, kKChain, k_chain<false>, dim3(p.grid), blk, st, s, e, p);
-    // frame batches: their continuations packed; a lone frame's k_mix reads phase A's regions (region_prefix)
-    if (p.split_occ) RT_LAUNCH(kt, kKPackA, k_pack_a, dim3(p.grid), blk, st, p);
+    // phase A's lists packed, except a whole lone frame's: its k_mix reads them in their regions (region_prefix)
+    if (!p.rlists) RT_LAUNCH(kt, kKPackA, k_pack_a, dim3(p.grid), blk, st, p);
     PcParams q = p;
     if (!phase_b) q.gb = 0;
     // p.split_occ (frame batches): k_mix only walks the chains, A's shadow tasks go to k_occlude (5 waves
@@ -1998,9 +2017,11 @@ hipError_t launch_chain_chunk(const rtk::DevScene& s, const rtk::Eye& e, const P
     if (mgrid == 0) {
     } else if (count) {
         if (split) RT_LAUNCH(kt, kKMix, (k_mix<true, false>), dim3(mgrid), blk, st, s, e, q);
+        else if (p.rlists) RT_LAUNCH(kt, kKMix, (k_mix<true, true, true>), dim3(mgrid), blk, st, s, e, q);
         else RT_LAUNCH(kt, kKMix, (k_mix<true, true>), dim3(mgrid), blk, st, s, e, q);
     } else {
         if (split) RT_LAUNCH(kt, kKMix, (k_mix<false, false>), dim3(mgrid), blk, st, s, e, q);
+        else if (p.rlists) RT_LAUNCH(kt, kKMix, (k_mix<false, true, true>), dim3(mgrid), blk, st, s, e, q);
         else RT_LAUNCH(kt, kKMix, (k_mix<false, true>), dim3(mgrid), blk, st, s, e, q);
     }
     if (split) {

@@ -163,7 +163,7 @@ struct PcParams {
     unsigned* sqA;    // shadow tasks of A: [grid][scapA], owner = (level*cap + sample)*nl + light
     unsigned scapA;
     unsigned* scntA;  // [grid]
-    unsigned* spare0; // (unused: the walk kernels' SGPR allocation follows the argument layout)
+    unsigned* sflatA; // the chunks of a lone frame: A's shadow tasks packed in region order (k_pack_a), totals[0]
     unsigned* cq;     // continuations of A: [grid][ccapA], owner = level*cap + sample of the last record
     unsigned ccapA;
     unsigned* ccnt;   // [grid]
@@ -242,6 +242,9 @@ struct PcParams {
     // (0: off), bits 8-9 log2 G (0: from the hot-unit count and the grid, at most 8 hot rows per wave).
     unsigned* ugrp;
     int mix_cls;
+    int rlists;       // 1: a whole lone frame -- k_mix reads phase A's lists in their regions (pathchain.hip
+                      // region_prefix) and stores cflat / cid itself; 0: k_pack_a packs them (cflat, and sflatA
+                      // where A's shadow tasks are not walked in place)
 };
 
 // Worst-case task-queue slots per workgroup: every sample of the workgroup

@@ -627,13 +627,14 @@ struct ChainPlan {
     size_t cap = 0;                 // samples of the launch
     int G = 1, gb = 0, levels_a = 1, kinline = 0;
     bool phase_b = false, split_occ = false;
+    bool rlists = false;   // a whole lone frame in one launch: phase A's lists read in their regions (no k_pack_a)
     unsigned dyn_units = 0, scapA = 0, ccapA = 0, scapB = 0;
     int la = 1, tchunk = 1;         // levels stored per sample; phase-B continuation chunk
     size_t cb = 0;                  // continuations with phase-B records
     // arena offsets
     size_t dbase = 0;               // records below it without directions (pathchain.hpp)
     int clevels = 0;
-    size_t o_rec = 0, o_recd = 0, o_pinfo = 0, o_occ = 0, o_sqA = 0, o_scntA = 0, o_cq = 0, o_ccnt = 0,
+    size_t o_rec = 0, o_recd = 0, o_pinfo = 0, o_occ = 0, o_sqA = 0, o_scntA = 0, o_sflatA = 0, o_cq = 0, o_ccnt = 0,
            o_cflat = 0, o_sqB = 0, o_scntB = 0, o_sflatB = 0, o_totals = 0, o_cid = 0, o_tail = 0,
            o_fbc = 0, o_fbs = 0, bytes = 0;
 };
@@ -705,6 +706,10 @@ ChainPlan chain_plan(const rt_scene* s, const ChainGeom& g, size_t nunits, bool 
     // frame batches: A's shadow rays in their own 5-wave k_occlude launch (split_occ) and (round 3) 1 phase-B
     // workgroup per CU (6 slots in flight: 0.504-0.512 -> 0.495 ms/frame; 0.5 per CU 0.500, 2 0.4995)
     P.split_occ = g.nframes > 1;
+    // a whole lone frame in one launch reads phase A's lists where k_chain left them (no packing kernel between
+    // its phases: C3 -10 us); the chunks of a larger frame keep k_pack_a (C5: region lists +2.5-4 % per frame,
+    // profiles/r06_nopack_ab.jsonl)
+    P.rlists = g.nframes <= 1 && nunits >= g.units_total;
     // (round 5, the driver's 20-frame call on 5 slots: 1.5 per CU 0.4175 against 1 per CU 0.4282 ms/frame, three
     // interleaved same-box rounds, 96-frame calls +-0; profiles/r05_ab_gb.txt)
     const int gb_default = g.nframes > 1 ? RT_GB_BATCH_Q4 * s->num_cus / 4 : 30 * s->num_cus / 16;
@@ -753,6 +758,7 @@ ChainPlan chain_plan(const rt_scene* s, const ChainGeom& g, size_t nunits, bool 
     P.o_fbs = L.take<unsigned>(cap);
     {
         P.o_sqA = L.take<unsigned>((size_t)P.G * P.scapA); P.o_scntA = L.take<unsigned>(P.G);
+        if (!P.split_occ && !P.rlists) P.o_sflatA = L.take<unsigned>(cap * P.levels_a * nl);   // packed (k_pack_a)
         P.o_cq = L.take<unsigned>((size_t)P.G * P.ccapA); P.o_ccnt = L.take<unsigned>(P.G);
         P.o_cflat = L.take<unsigned>(cap);   // packed continuations (k_pack_a; a lone frame's k_mix / k_fallback)
         P.o_sqB = L.take<unsigned>((size_t)P.gb * P.scapB); P.o_scntB = L.take<unsigned>(P.gb + 1);
@@ -916,6 +922,8 @@ int render_chain(rt_scene* s, const rtk::Eye& eye, const rtk::FrameParams& f, bo
     p.occ = static_cast<uint8_t*>(at(P.o_occ));
     p.sqA = static_cast<unsigned*>(at(P.o_sqA)); p.scapA = P.scapA;
     p.scntA = static_cast<unsigned*>(at(P.o_scntA));
+    p.sflatA = !P.split_occ && !P.rlists ? static_cast<unsigned*>(at(P.o_sflatA)) : nullptr;
+    p.rlists = P.rlists ? 1 : 0;
     p.cq = static_cast<unsigned*>(at(P.o_cq)); p.ccapA = P.ccapA;
     p.ccnt = static_cast<unsigned*>(at(P.o_ccnt));
     p.cflat = static_cast<unsigned*>(at(P.o_cflat));
