@@ -112,7 +112,7 @@ __host__ __device__ inline unsigned unit_col(int tiles_x, int ublk_h, int ublk_w
     return (r0 + l / w) * upr + c0 + l % w;
 }
 
-// PcParams::totals words: task counts (1-2), the phase-A unit counter (3), k_fallback's chain /
+// PcParams::totals words: task counts (0-2), the phase-A unit counter (3), k_fallback's chain /
 // shadow counts and shadow-queue overflow (4-6), the rest spare.
 constexpr int kTotalsWords = 12;
 
@@ -157,9 +157,10 @@ struct PcParams {
     unsigned fbs_cap;
     int fb_grid;      // k_fallback workgroups
     // phase A (k_chain: levels [0, kinline]) and phase B (k_mix chain role: deeper levels).
-    // Task queues hold u32 owner ids in per-workgroup regions with their counts; phase A's are read in place
-    // as one list in region order (pathchain.hip region_prefix) or region by region, except frame batches'
-    // continuations (k_pack_a); phase B's overflow packed (k_pack_b) in frame batches.
+    // Task queues hold u32 owner ids in per-workgroup regions with their counts.  Phase A's are packed by
+    // k_pack_a (continuations: cflat; a lone frame's chunks' shadow tasks: sflatA), walked region by region
+    // (frame batches' shadow tasks), or read as one list in region order (a whole lone frame, PcParams::rlists,
+    // pathchain.hip region_prefix); phase B's overflow is packed by k_pack_b in frame batches.
     unsigned* sqA;    // shadow tasks of A: [grid][scapA], owner = (level*cap + sample)*nl + light
     unsigned scapA;
     unsigned* scntA;  // [grid]
@@ -173,8 +174,8 @@ struct PcParams {
     unsigned scapB;
     unsigned* scntB;  // [gb]
     unsigned* sflatB; // B's shadow tasks packed (k_pack_b), totals[2] of them
-    unsigned* totals; // [kTotalsWords]: task counts (1: A's continuations, k_pack_a / k_mix; 2: B's packed overflow), the
-                      // phase-A unit counter, k_fallback chains / shadows /
+    unsigned* totals; // [kTotalsWords]: task counts (0: A's packed shadow tasks; 1: A's continuations, k_pack_a /
+                      // k_mix; 2: B's packed overflow), the phase-A unit counter, k_fallback chains / shadows /
                       // overflow
     int kinline;      // deepest level phase A walks (>= max_depth: no phase B)
     int gb;           // k_mix workgroups in the chain role (the other p.ogrid ones occlude A's tasks)
