@@ -1399,6 +1399,8 @@ __global__ __launch_bounds__(kBlock, RT_OCC_WAVES_PER_EU) void k_occlude(rtk::De
         // kernel, whose 6 waves per SIMD need its LDS)
         if (inplace || !which) occlude_regions(s, p, which, blockIdx.x, gridDim.x);
         else occlude_queue_body(s, p, blockIdx.x, gridDim.x, flat_list(p.sflatB), p.totals[2]);
+        // a lone frame without phase B walks A's shadow tasks here (no k_mix): the next frame's unit order
+        if (!which && p.urank && blockIdx.x == gridDim.x - 1) rank_units(p);
     } else {
         if (which) occlude_body<COUNT>(s, p, blockIdx.x, gridDim.x, flat_list(p.sflatB), p.totals[2], 1);
         else occlude_body<COUNT>(s, p, blockIdx.x, gridDim.x, shadow_regions_a(p), region_prefix(p.scntA, (unsigned)p.grid), 0);
@@ -2010,9 +2012,13 @@ hipError_t launch_chain_chunk(const rtk::DevScene& s, const rtk::Eye& e, const P
     if (!phase_b) q.gb = 0;
     // p.split_occ (frame batches): k_mix only walks the chains, A's shadow tasks go to k_occlude (5 waves
     // per SIMD; in place, p.occ_inplace); otherwise k_mix's other
-    // workgroups walk them beside the chains.  Frame batches without phase B (depth 0): no k_mix at all
+    // workgroups walk them beside the chains.  Without phase B (depth 0): no k_mix at all, A's shadow tasks
+    // in k_occlude, a lone frame's too
     const bool split = p.split_occ != 0;
-    const int mgrid = split ? q.gb : q.gb + p.ogrid;
+    // a lone frame without phase B (depth 0): A's shadow tasks in place by the 6-wave k_occlude instead of
+    // k_mix's 4-wave shadow role (C2 one frame 0.146 -> 0.140 ms, profiles/r06_d0_ab.jsonl)
+    const bool occ_a = split || (!phase_b && !count);
+    const int mgrid = occ_a ? (split ? q.gb : 0) : q.gb + p.ogrid;
     // frame batches (split): phase B's shadow tasks all through k_pack_b + k_occlude (no LDS queue)
     if (mgrid == 0) {
     } else if (count) {
@@ -2024,7 +2030,7 @@ hipError_t launch_chain_chunk(const rtk::DevScene& s, const rtk::Eye& e, const P
         else if (p.rlists) RT_LAUNCH(kt, kKMix, (k_mix<false, true, true>), dim3(mgrid), blk, st, s, e, q);
         else RT_LAUNCH(kt, kKMix, (k_mix<false, true>), dim3(mgrid), blk, st, s, e, q);
     }
-    if (split) {
+    if (occ_a) {
         if (count) RT_LAUNCH(kt, kKOccA, k_occlude<true>, dim3(p.occ_grid), blk, st, s, p, 0);
         else RT_LAUNCH(kt, kKOccA, k_occlude<false>, dim3(p.occ_grid), blk, st, s, p, 0);
     }
