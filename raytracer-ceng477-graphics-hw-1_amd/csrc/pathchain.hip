@@ -204,6 +204,7 @@ __device__ __forceinline__ unsigned wave_grab_lds(unsigned* ctr, unsigned long l
 // 256-sample units, continuation and shadow tasks by index j -> j mod G.
 // ---------------------------------------------------------------------------
 __shared__ unsigned g_ccnt;    // block-local continuation count
+__shared__ unsigned g_dcnt;    // ... of those queued at the region's end (PcParams::pdepth: deep last frame)
 __shared__ unsigned g_uid[kDynUnits];   // dynamic phase-A units: the workgroup's k-th unit (kUidUnset: not yet taken)
 constexpr unsigned kUidUnset = ~0u, kUidNone = ~0u - 1u;
 // A mixed-deal virtual unit (PcParams::ugrp): kUidMix | log2 G << 28 | sub-unit << 24 | group.
@@ -713,12 +714,22 @@ __device__ void chain_body(const rtk::DevScene& s, const rtk::Eye& e, const PcPa
             } else {
                 ends = false;
             }
+            if (CONT && !COUNT && ends && p.pdepth) p.pdepth[path % p.frame_slots] = (uint8_t)min(k + 1, 255);
             const bool handoff = !ends && k >= o.kinline;                      // deeper levels: next phase
             const unsigned long long cm = __ballot(handoff);
             if (handoff) {
                 if (COUNT) ncont++;
-                const unsigned base = wave_grab_lds(&g_ccnt, cm);
-                o.cq[(size_t)blk * o.ccap + base + lane_rank(cm)] = (unsigned)((size_t)k * p.cap + path);
+                // a continuation the previous frame saw go deep (PcParams::pdepth): from the region's end, packed first
+                const bool deep = !CONT && !COUNT && p.pdepth && p.pdepth[path % p.frame_slots] >= (uint8_t)p.deep_min;
+                const unsigned long long dm = __ballot(deep);
+                unsigned slot;
+                if (deep) {
+                    slot = o.ccap - 1u - (wave_grab_lds(&g_dcnt, dm) + lane_rank(dm));
+                } else {
+                    const unsigned long long sm = cm & ~dm;
+                    slot = wave_grab_lds(&g_ccnt, sm) + lane_rank(sm);
+                }
+                o.cq[(size_t)blk * o.ccap + slot] = (unsigned)((size_t)k * p.cap + path);
                 p.pinfo[path] = kPathCont;        // continued in phase B (finish_pixels' order)
                 if (lvp < p.dbase) p.tail[path] = make_float4(r.d.x, r.d.y, r.d.z, 0.0f);   // reflect_from_record
             }
@@ -861,7 +872,10 @@ __device__ void chain_body(const rtk::DevScene& s, const rtk::Eye& e, const PcPa
     __syncthreads();
     if (threadIdx.x == 0) {
         o.scount[blk] = g_scnt;
-        if (!CONT) o.ccount[blk] = g_ccnt;
+        if (!CONT) {
+            o.ccount[blk] = g_ccnt;
+            if (p.ccntd) p.ccntd[blk] = g_dcnt;
+        }
     }
     if (COUNT) {
         // shadow rays not traced (light_needed): counter 6; a production counting pass (count_prod)
@@ -1183,7 +1197,7 @@ __device__ __forceinline__ PhaseOut phase_b(const PcParams& p) {
 // Phase A: every sample, levels [0, kinline].
 template <bool COUNT, bool DBG = false>
 __global__ __launch_bounds__(kBlock, COUNT ? 4 : RT_WAVES_PER_EU) void k_chain(rtk::DevScene s, rtk::Eye e, PcParams p) {
-    if (threadIdx.x == 0) g_ccnt = 0;
+    if (threadIdx.x == 0) g_ccnt = g_dcnt = 0;
     if (threadIdx.x < kDynUnits) g_uid[threadIdx.x] = kUidUnset;
     block_init(s);
     chain_body<COUNT, false, false, DBG>(s, e, p, blockIdx.x, gridDim.x, phase_a(p));
@@ -1193,8 +1207,10 @@ __global__ __launch_bounds__(kBlock, COUNT ? 4 : RT_WAVES_PER_EU) void k_chain(r
 // its place in the packed array: the consumers then index tasks directly.
 // Workgroup 0 stores the total.  cid (continuations): cid[sample] = the packed index of its continuation
 // (its phase-B records).
-__device__ void pack_region(const unsigned* q, unsigned cap, const unsigned* cnt, int nreg, unsigned* flat,
-                            unsigned* total, unsigned b, unsigned* cid = nullptr, unsigned ncap = 1) {
+__device__ unsigned pack_region(const unsigned* q, unsigned cap, const unsigned* cnt, int nreg, unsigned* flat,
+                                unsigned* total, unsigned b, unsigned* cid = nullptr, unsigned ncap = 1,
+                                bool top = false, unsigned base = 0) {
+    // (top: the region's entries are at its end, q[b * cap + cap - 1 - k]; base: the packed array's offset)
     __shared__ unsigned s_before, s_all;
     if (threadIdx.x == 0) { s_before = 0; s_all = 0; }
     __syncthreads();
@@ -1208,11 +1224,12 @@ __device__ void pack_region(const unsigned* q, unsigned cap, const unsigned* cnt
     if (all) atomicAdd(&s_all, all);
     if (before) atomicAdd(&s_before, before);
     __syncthreads();
-    const unsigned off = s_before, n = cnt[b];
+    const unsigned off = base + s_before, n = cnt[b];
     const unsigned* src = q + (size_t)b * cap;
+    auto at = [&](unsigned k) { return top ? src[cap - 1u - k] : src[k]; };
     unsigned k = threadIdx.x;
     for (; k + 3 * kBlock < n; k += 4 * kBlock) {          // four loads in flight per lane
-        const unsigned v0 = src[k], v1 = src[k + kBlock], v2 = src[k + 2 * kBlock], v3 = src[k + 3 * kBlock];
+        const unsigned v0 = at(k), v1 = at(k + kBlock), v2 = at(k + 2 * kBlock), v3 = at(k + 3 * kBlock);
         flat[off + k] = v0; flat[off + k + kBlock] = v1; flat[off + k + 2 * kBlock] = v2; flat[off + k + 3 * kBlock] = v3;
         if (cid) {
             cid[(v0 & ~kFbEye) % ncap] = off + k; cid[(v1 & ~kFbEye) % ncap] = off + k + kBlock;
@@ -1220,12 +1237,14 @@ __device__ void pack_region(const unsigned* q, unsigned cap, const unsigned* cnt
         }
     }
     for (; k < n; k += kBlock) {
-        const unsigned v = src[k];
+        const unsigned v = at(k);
         flat[off + k] = v;
         if (cid) cid[(v & ~kFbEye) % ncap] = off + k;
     }
-    if (b == 0 && threadIdx.x == 0) *total = s_all;
+    const unsigned tot = s_all;
+    if (total && b == 0 && threadIdx.x == 0) *total = tot;
     __syncthreads();
+    return tot;
 }
 
 // The next frame's phase-A unit order (PcParams::uorder, k_mix's last shadow-role workgroup in lone frames):
@@ -1316,7 +1335,14 @@ __device__ void rank_units(const PcParams& p) {
 // tasks where they are not walked in place (p.sflatA: a lone frame's chunks).
 __global__ __launch_bounds__(kBlock) void k_pack_a(PcParams p) {
     if (p.sflatA) pack_region(p.sqA, p.scapA, p.scntA, p.grid, p.sflatA, &p.totals[0], blockIdx.x);
-    pack_region(p.cq, p.ccapA, p.ccnt, p.grid, p.cflat, &p.totals[1], blockIdx.x, p.cid, (unsigned)p.cap);
+    // the continuations the previous frame saw go deep first (PcParams::pdepth; k_chain queued them at their
+    // regions' ends), then the rest
+    unsigned nd = 0;
+    if (p.ccntd) nd = pack_region(p.cq, p.ccapA, p.ccntd, p.grid, p.cflat, nullptr, blockIdx.x, p.cid, (unsigned)p.cap,
+                                  true);
+    const unsigned ns = pack_region(p.cq, p.ccapA, p.ccnt, p.grid, p.cflat, nullptr, blockIdx.x, p.cid,
+                                    (unsigned)p.cap, false, nd);
+    if (blockIdx.x == 0 && threadIdx.x == 0) p.totals[1] = nd + ns;
     if (p.cont_peak && blockIdx.x == 0 && threadIdx.x == 0) atomicMax(p.cont_peak, p.totals[1]);   // (its own write)
 }
 __global__ __launch_bounds__(kBlock) void k_pack_b(PcParams p) {

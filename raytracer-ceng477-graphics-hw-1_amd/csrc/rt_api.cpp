@@ -139,6 +139,7 @@ struct rt_scene {
                                 // default GPU_MAX_HW_QUEUES - 1)
     int tune_bq_cap = 1 << 30;  // RT_BQ_CAP: phase-B shadow queue slots (tests force the k_occlude spill path)
     int tune_hot_units = 1;     // RT_HOT_UNITS: lone frames deal phase-A units heaviest-first by the previous frame's steps
+    int tune_deep = 5;          // RT_DEEP: PcParams::deep_min (frame batches' deep-first deal; 0: off)
     int tune_mix = 5 | 1 << 8;  // RT_MIX: PcParams::mix_cls: lone frames deal the units of >= 64 steps (classes
                                 // 0-4) in pairs with light ones, half of each wave's first lanes (C3 one frame
                                 // 0.876 -> 0.837 ms; 16 of 64 lanes the same, 8 of 64 +-0; profiles/r06_mix_*.jsonl)
@@ -187,6 +188,10 @@ struct rt_scene {
         unsigned* hist = nullptr;
         unsigned hist_units = 0;
         uint64_t hist_key = 0;               // the launch geometry uorder was ranked for (0: none yet)
+        // frame batches' deep-first deal (PcParams::pdepth): the levels of the previous frame's chains per frame slot
+        uint8_t* pdepth = nullptr;
+        size_t pdepth_n = 0;
+        uint64_t pdepth_key = 0;
     } arenas[kSlots];
     // continuation share of frame batches (phase B's record space, cb): each batched launch copies its
     // continuation count (k_pack_a's or k_mix's total) to pinned memory behind it; once that copy is done the share
@@ -219,6 +224,7 @@ struct rt_scene {
             if (kt.ev1[i]) (void)hipEventDestroy(kt.ev1[i]);
         }
         for (auto& a : arenas) (void)hipFree(a.hist);
+        for (auto& a : arenas) (void)hipFree(a.pdepth);
         for (auto& e : cont_ev)
             if (e) (void)hipEventDestroy(e);
         if (h_cont) (void)hipHostFree(h_cont);
@@ -470,6 +476,7 @@ int upload_rest(rt_scene* s, const rt_options* opts) {
     if (const char* e = std::getenv("RT_COMPACT")) s->tune_compact = std::max(0, std::min(3, std::atoi(e)));
     if (const char* e = std::getenv("RT_HOT_UNITS")) s->tune_hot_units = std::atoi(e) != 0;
     if (const char* e = std::getenv("RT_MIX")) s->tune_mix = std::atoi(e);
+    if (const char* e = std::getenv("RT_DEEP")) s->tune_deep = std::max(0, std::atoi(e));
     if (const char* e = std::getenv("RT_TRACE")) s->trace_file = e;
     const int dbg = debug_flags();
     s->ktime = (dbg & kDbgKtime) != 0;
@@ -635,7 +642,7 @@ struct ChainPlan {
     size_t dbase = 0;               // records below it without directions (pathchain.hpp)
     int clevels = 0;
     size_t o_rec = 0, o_recd = 0, o_pinfo = 0, o_occ = 0, o_sqA = 0, o_scntA = 0, o_sflatA = 0, o_cq = 0, o_ccnt = 0,
-           o_cflat = 0, o_sqB = 0, o_scntB = 0, o_sflatB = 0, o_totals = 0, o_cid = 0, o_tail = 0,
+           o_cflat = 0, o_ccntd = 0, o_sqB = 0, o_scntB = 0, o_sflatB = 0, o_totals = 0, o_cid = 0, o_tail = 0,
            o_fbc = 0, o_fbs = 0, bytes = 0;
 };
 
@@ -760,6 +767,7 @@ ChainPlan chain_plan(const rt_scene* s, const ChainGeom& g, size_t nunits, bool 
         P.o_sqA = L.take<unsigned>((size_t)P.G * P.scapA); P.o_scntA = L.take<unsigned>(P.G);
         if (!P.split_occ && !P.rlists) P.o_sflatA = L.take<unsigned>(cap * P.levels_a * nl);   // packed (k_pack_a)
         P.o_cq = L.take<unsigned>((size_t)P.G * P.ccapA); P.o_ccnt = L.take<unsigned>(P.G);
+        if (P.split_occ) P.o_ccntd = L.take<unsigned>(P.G);   // deep-first continuations (PcParams::ccntd)
         P.o_cflat = L.take<unsigned>(cap);   // packed continuations (k_pack_a; a lone frame's k_mix / k_fallback)
         P.o_sqB = L.take<unsigned>((size_t)P.gb * P.scapB); P.o_scntB = L.take<unsigned>(P.gb + 1);
         P.o_sflatB = L.take<unsigned>(P.cb * (levels - P.la) * nl);
@@ -994,6 +1002,37 @@ int render_chain(rt_scene* s, const rtk::Eye& eye, const rtk::FrameParams& f, bo
     // previous frame of the same geometry (PcParams::uorder), and this frame's costs ranked for the next
     const bool hot = s->tune_hot_units && !count && p.nframes == 1 && P.dyn_units > 0 &&
                      units == g.units_total;
+    // frame batches' deep-first deal (PcParams::pdepth): one launch of whole frames whose internal rows are whole
+    // tile rows; the depths of the slot's previous launch of the same frame geometry (zero, all shallow, else)
+    p.pdepth = nullptr;
+    p.ccntd = nullptr;
+    p.frame_slots = 0;
+    p.deep_min = 0;
+    if (s->tune_deep > 0 && !count && P.split_occ && P.phase_b && !P.rlists && units == g.units_total &&
+        (p.frame_rows * p.aa) % 8 == 0) {
+        const size_t fs = (size_t)p.tiles_x * (size_t)(p.frame_rows * p.aa / 8) * 64;
+        uint64_t key = 1469598103934665603ull;
+        for (long long v : {(long long)p.width, (long long)p.height, (long long)p.aa, (long long)p.stripe_rows,
+                            (long long)p.rank, (long long)p.nranks, (long long)p.frame_rows, (long long)fs})
+            key = (key ^ (uint64_t)v) * 1099511628211ull;
+        if (arena.pdepth_n < fs) {
+            if (arena.pdepth) HIP_TRY(hipStreamSynchronize(st));   // earlier launches may still use it
+            (void)hipFree(arena.pdepth);
+            arena.pdepth = nullptr;
+            arena.pdepth_n = 0;
+            HIP_TRY(hipMalloc(reinterpret_cast<void**>(&arena.pdepth), fs));
+            arena.pdepth_n = fs;
+            arena.pdepth_key = 0;
+        }
+        if (arena.pdepth_key != key) {
+            HIP_TRY(hipMemsetAsync(arena.pdepth, 0, fs, st));
+            arena.pdepth_key = key;
+        }
+        p.pdepth = arena.pdepth;
+        p.ccntd = static_cast<unsigned*>(at(P.o_ccntd));
+        p.frame_slots = (unsigned)fs;
+        p.deep_min = s->tune_deep;
+    }
     p.urank = p.uorder_on = 0;
     p.ugrp = nullptr;
     p.mix_cls = 0;

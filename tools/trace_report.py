@@ -4,7 +4,7 @@ summarise the per-sample wall-clock trace (100 MHz counter, 10 ns ticks):
 when samples start / finish, how many are in flight over time, the slowest
 ones.  Answers "is the frame bound by bulk throughput or by its tail?".
 
-  python tools/trace_report.py [chain|megakernel ...]
+  python tools/trace_report.py [chain|megakernel ...]     (env TRACE_FRAMES=n: one n-frame batch instead)
 """
 import json
 import os
@@ -72,9 +72,13 @@ def main():
         os.environ["RT_TRACE"] = tf
         sc = pkg.Scene.from_xml(xml, device=0, render_path=path)
         cam = sc.camera(0)
-        out = torch.empty((cam.image_height, cam.image_width, 3), dtype=torch.uint8, device=dev)
+        nf = int(os.environ.get("TRACE_FRAMES", "1"))   # > 1: one frame batch of nf frames (one launch if it fits)
+        out = torch.empty((nf, cam.image_height, cam.image_width, 3), dtype=torch.uint8, device=dev)
         for _ in range(3):
-            sc.render_device(cam, 1, out.data_ptr(), st.cuda_stream)
+            if nf == 1:
+                sc.render_device(cam, 1, out[0].data_ptr(), st.cuda_stream)
+            else:
+                sc.render_frames_device([cam] * nf, 1, [out[i].data_ptr() for i in range(nf)], st.cuda_stream)
         torch.cuda.synchronize()
         kind, a, b, tr = load(tf)
         if kind == 2:     # megakernel: per output pixel
