@@ -714,13 +714,13 @@ __device__ void chain_body(const rtk::DevScene& s, const rtk::Eye& e, const PcPa
             } else {
                 ends = false;
             }
-            if (CONT && !COUNT && ends && p.pdepth) p.pdepth[path % p.frame_slots] = (uint8_t)min(k + 1, 255);
+            if (CONT && !COUNT && ends && p.pdepth) p.pdepth[path] = (uint8_t)min(k + 1, 255);
             const bool handoff = !ends && k >= o.kinline;                      // deeper levels: next phase
             const unsigned long long cm = __ballot(handoff);
             if (handoff) {
                 if (COUNT) ncont++;
                 // a continuation the previous frame saw go deep (PcParams::pdepth): from the region's end, packed first
-                const bool deep = !CONT && !COUNT && p.pdepth && p.pdepth[path % p.frame_slots] >= (uint8_t)p.deep_min;
+                const bool deep = !CONT && !COUNT && p.pdepth && p.pdepth[path] >= (uint8_t)p.deep_min;
                 const unsigned long long dm = __ballot(deep);
                 unsigned slot;
                 if (deep) {

@@ -246,13 +246,12 @@ struct PcParams {
     int rlists;       // 1: a whole lone frame -- k_mix reads phase A's lists in their regions (pathchain.hip
                       // region_prefix) and stores cflat / cid itself; 0: k_pack_a packs them (cflat, and sflatA
                       // where A's shadow tasks are not walked in place)
-    // Frame batches' deep-first deal: pdepth[frame slot] = the levels the previous frame of this geometry's chain
-    // recorded there (k_mix, at its chain's end); k_chain queues a continuation whose pdepth >= deep_min at its
-    // region's end (ccntd counts them) and k_pack_a packs those first, so k_mix starts the deep chains first.
+    // Frame batches' deep-first deal: pdepth[sample slot] = the levels its chain reached in the slot's previous
+    // launch of this geometry (k_mix, at the chain's end); k_chain queues a continuation whose pdepth >= deep_min
+    // at its region's end (ccntd counts them) and k_pack_a packs those first, so k_mix starts the deep chains first.
     // Null: off.  Where work runs, never what it computes.
     uint8_t* pdepth;
     unsigned* ccntd;
-    unsigned frame_slots;   // sample slots per frame (a frame's internal rows are whole 8-row tile rows)
     int deep_min;
 };
 

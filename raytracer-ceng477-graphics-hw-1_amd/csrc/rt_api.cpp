@@ -1002,18 +1002,18 @@ int render_chain(rt_scene* s, const rtk::Eye& eye, const rtk::FrameParams& f, bo
     // previous frame of the same geometry (PcParams::uorder), and this frame's costs ranked for the next
     const bool hot = s->tune_hot_units && !count && p.nframes == 1 && P.dyn_units > 0 &&
                      units == g.units_total;
-    // frame batches' deep-first deal (PcParams::pdepth): one launch of whole frames whose internal rows are whole
-    // tile rows; the depths of the slot's previous launch of the same frame geometry (zero, all shallow, else)
+    // frame batches' deep-first deal (PcParams::pdepth): one launch of whole frames; the depths of the slot's
+    // previous launch of the same geometry (frame size and frames per launch) per sample slot (zero, all
+    // shallow, else)
     p.pdepth = nullptr;
     p.ccntd = nullptr;
-    p.frame_slots = 0;
     p.deep_min = 0;
-    if (s->tune_deep > 0 && !count && P.split_occ && P.phase_b && !P.rlists && units == g.units_total &&
-        (p.frame_rows * p.aa) % 8 == 0) {
-        const size_t fs = (size_t)p.tiles_x * (size_t)(p.frame_rows * p.aa / 8) * 64;
+    if (s->tune_deep > 0 && !count && P.split_occ && P.phase_b && !P.rlists && units == g.units_total) {
+        const size_t fs = cap;
         uint64_t key = 1469598103934665603ull;
         for (long long v : {(long long)p.width, (long long)p.height, (long long)p.aa, (long long)p.stripe_rows,
-                            (long long)p.rank, (long long)p.nranks, (long long)p.frame_rows, (long long)fs})
+                            (long long)p.rank, (long long)p.nranks, (long long)p.frame_rows, (long long)p.nframes,
+                            (long long)p.n0, (long long)fs})
             key = (key ^ (uint64_t)v) * 1099511628211ull;
         if (arena.pdepth_n < fs) {
             if (arena.pdepth) HIP_TRY(hipStreamSynchronize(st));   // earlier launches may still use it
@@ -1030,7 +1030,6 @@ int render_chain(rt_scene* s, const rtk::Eye& eye, const rtk::FrameParams& f, bo
         }
         p.pdepth = arena.pdepth;
         p.ccntd = static_cast<unsigned*>(at(P.o_ccntd));
-        p.frame_slots = (unsigned)fs;
         p.deep_min = s->tune_deep;
     }
     p.urank = p.uorder_on = 0;
