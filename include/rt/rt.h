@@ -255,7 +255,7 @@ int rt_cramer_div(const float* den, const float* num, float* out, int n);
 int rt_udiv(const uint32_t* v, int nv, const uint32_t* d, int nd, uint32_t* q);
 /* HBM held by a scene on its (first) device (ABI 7): the uploaded scene (trees,
  * primitives, tables) and the render workspaces allocated so far (chain-path
- * arenas of every slot, output staging).  The workspaces grow on demand up to
+ * arenas of every slot and their side tables, output staging).  The workspaces grow on demand up to
  * the scene's budget, env RT_WS_BUDGET_MB at scene creation (default 16384 MB
  * for all slots together); a frame batch or chunk is sized to fit it. */
 int rt_scene_memory(const rt_scene* scene, uint64_t* scene_bytes, uint64_t* workspace_bytes);

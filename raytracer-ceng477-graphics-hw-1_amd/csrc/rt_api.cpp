@@ -166,7 +166,10 @@ struct rt_scene {
         // size or the reserve, whichever is larger; fit_arenas drops an arena a staging growth leaves over
         const size_t fixed = scene_bytes + std::max(kStagingReserve, out_cap + batch_out_cap);
         const size_t arenas = ws_budget > 2 * fixed ? ws_budget - fixed : ws_budget / 2;
-        return arenas / (size_t)std::max(1, std::min(tune_slots, kSlots));
+        // (1 % of each share for the slot's side tables beside its arena: the deep-first deal's depth table,
+        // 1 B per sample of a launch, and the lone frame's unit tables, 16 B per 256 samples -- an arena
+        // holds well over 100 B per sample)
+        return arenas / (size_t)std::max(1, std::min(tune_slots, kSlots)) / 101 * 100;
     }
     double xml_ms = 0, prep_ms = 0, upload_ms = 0;   // scene creation phases (rt_scene_bvh_info)
     bool warned_budget = false;    // one row unit alone exceeds the slot budget (chain_launch_units): told once
@@ -1294,7 +1297,7 @@ int rt_scene_export_nodes(const rt_scene* s, void* out, int capacity) {
 int rt_scene_memory(const rt_scene* s, uint64_t* scene_bytes, uint64_t* workspace_bytes) {
     if (!s) return fail(RT_ERR_ARG, "scene is NULL");
     size_t ws = s->out_cap + s->batch_out_cap + s->trace_cap * sizeof(unsigned);
-    for (const auto& a : s->arenas) ws += a.bytes;
+    for (const auto& a : s->arenas) ws += a.bytes + a.pdepth_n + 4 * (size_t)a.hist_units * sizeof(unsigned);
     if (scene_bytes) *scene_bytes = s->host_only ? 0 : s->scene_bytes;
     if (workspace_bytes) *workspace_bytes = ws;
     return RT_OK;
