@@ -1665,6 +1665,24 @@ __device__ __forceinline__ void finish_pixels(const rtk::DevScene& s, const rtk:
             if (first == path) finish_pixel<LDS, CMP>(s, e, p, rr, ocol);
         }
     }
+    if (F == 1) {   // one sample a pixel: a wave per 8x8 tile, the records' own order (C3 -0.5 to -1 %)
+        for (unsigned q = gtid; q < (unsigned)p.n0; q += gstride) {
+            const unsigned tile = q >> 6, lane = q & 63u;
+            const unsigned ty = tile / (unsigned)p.tiles_x, tx = tile - ty * (unsigned)p.tiles_x;
+            const int ocol = (int)(tx * 8u + (lane & 7u)), rr = (int)(ty * 8u + (lane >> 3));
+            if (ocol >= p.width || rr >= p.chunk_rows) continue;
+            if (p.fin_cont && (p.pinfo[q] & kPathCont)) continue;
+            int lf = p.chunk_row0 + rr;                         // finish_pixel at F = 1: sample q is the pixel
+            if (lf >= p.slab_rows) continue;
+            const int fr = batch_frame(p, &lf);
+            const int stripe = lf / p.stripe_rows;
+            if ((stripe * p.nranks + p.rank) * p.stripe_rows + (lf - stripe * p.stripe_rows) >= p.height) continue;
+            const V c = path_shade_fold<LDS, CMP>(s, e, p, q);
+            uint8_t* o = (p.nframes > 1 ? p.fouts[fr] : p.out) + ((size_t)out_row(p, lf) * p.width + ocol) * 3;
+            o[0] = (uint8_t)quantise(c.x); o[1] = (uint8_t)quantise(c.y); o[2] = (uint8_t)quantise(c.z);
+        }
+        return;
+    }
     const int npix = (p.chunk_rows / p.aa) * p.width;
     for (int q = (int)gtid; q < npix; q += (int)gstride) {
         const int rr = q / p.width, ocol = q - rr * p.width;
